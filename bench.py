@@ -1,0 +1,173 @@
+"""Benchmark: co-visitation build over synthetic OTTO-shaped sessions on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--events E]
+
+One step = one full co-visitation build of BASELINE.json configs[1]: all five rules over
+~220M events (100k-session files) -> per-(rule, aid, aid_next) count and count_ge2 tables
+resident in HBM (model/count_co_events.py:80-100 + the cross-file groupby of :168).
+Inputs are resident in HBM before the timed region. Prints one JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def cpu_baseline(ev_sessions: int, n_files: int, seed: int = 0) -> dict:
+    """The CPU restatement (oracle/covis_oracle.c, single thread) timed on a bounded sample:
+    the first n_files 100k-session files of the same synthetic stream."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import covis as oracle  # checker / baseline only
+    import otto_recommender_amd.synth as synth
+    n = min(ev_sessions, n_files * synth.SESSIONS_PER_FILE)
+    ev = synth.generate(n, 0, seed)
+    fb = synth.file_session_bounds(n)
+    t0 = time.perf_counter()
+    per_file = oracle.count_co_events_files(ev.session_offsets, ev.aid, ev.ts, ev.type, fb)
+    dt = time.perf_counter() - t0
+    pairs = sum(int(p[k][2].sum()) for p in per_file for k in p)
+    return {"value": pairs / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "sample": f"first {len(fb) - 1} files ({n} sessions, {ev.n_events} events, {pairs} pairs) "
+                      f"of the same stream, oracle/covis_oracle.c per-file count, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--events", type=int, default=220_000_000)
+    ap.add_argument("--cpu-files", type=int, default=5)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import otto_recommender_amd.synth as synth
+    from otto_recommender_amd import covis as gc
+    from otto_recommender_amd import _lib
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+
+    # ---- workload: sessions until E events, 100k-session files, files dealt to ranks
+    n_sess, n_ev = synth.sessions_for_events(args.events, 0, args.seed)
+    fb_all = synth.file_session_bounds(n_sess)
+    n_files = len(fb_all) - 1
+    my_files = list(range(rank, n_files, world))
+    t0 = time.perf_counter()
+    parts = [synth.generate(int(fb_all[f + 1] - fb_all[f]), int(fb_all[f]), args.seed) for f in my_files]
+    sizes = [p.n_sessions for p in parts]
+    fb = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    off = np.zeros(int(fb[-1]) + 1, np.int64)
+    base = 0
+    for i, p in enumerate(parts):
+        off[fb[i]:fb[i + 1] + 1] = p.session_offsets + base
+        base += p.n_events
+    ev = synth.Events(off, np.concatenate([p.session for p in parts]), np.concatenate([p.aid for p in parts]),
+                      np.concatenate([p.ts for p in parts]), np.concatenate([p.type for p in parts]))
+    del parts
+    gen_s = time.perf_counter() - t0
+    dev = gc.DeviceEvents.from_host(ev, fb)
+    ctx = _lib.context()
+    torch.cuda.synchronize()
+
+    def step():
+        tab = gc.count_co_events_fused(dev, ctx=ctx)
+        return tab
+
+    for _ in range(args.warmup):
+        step().free()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tabs = []
+    for _ in range(args.steps):
+        tabs.append(step())
+        if len(tabs) > 1:
+            tabs.pop(0).free()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    tab = tabs[-1]
+    stats = {n: tab.stats(n) for n in tab.names}
+    pairs = sum(s["n_pairs"] for s in stats.values())
+    rows = sum(s["n_rows"] for s in stats.values())
+
+    # phase timing of one extra (untimed) step with HIP events on the launch stream
+    ctx.set_timing(True)
+    tab.free()
+    tab = step()
+    phases = ctx.timings()
+    ctx.set_timing(False)
+    tab.free()
+
+    t_step = dt / args.steps
+    if world > 1:
+        tt = torch.tensor([t_step, float(pairs), float(rows), float(ev.n_events)], dtype=torch.float64, device="cuda")
+        t_max = tt[:1].clone(); dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        tot = tt[1:].clone(); dist.all_reduce(tot)
+        t_step = float(t_max.item()); pairs, rows, n_events = (float(x) for x in tot.tolist())
+    else:
+        n_events = ev.n_events
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    # byte model of SURVEY.md §8(d): B = 9E + 8(S+1) + 16P + 12U
+    b_model = 9.0 * n_events + 8.0 * (n_sess + 1) + 16.0 * pairs + 12.0 * rows
+    dom = max(phases, key=lambda p: p[1]) if phases else ("step", t_step * 1e3, b_model)
+    dom_bytes = dom[2] if dom[2] > 0 else b_model
+    achieved = dom_bytes / (dom[1] / 1e3) / 1e9
+    out = {
+        "metric": "co-visit pairs/sec + candidates/sec at 220M events, 1/2/4/8 MI355X",
+        "value": pairs / t_step,
+        "unit": "pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": t_step * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (otto-synth seed 0, SURVEY.md §8(d)); inputs resident in HBM",
+        "config": {"workload": "configs[1]: all 5 co-visitation rules, 220M events, 100k-session files",
+                   "events": int(n_events), "sessions": int(n_sess), "files": n_files,
+                   "parallelism": f"files dealt over {world} GPU(s)"},
+        "pairs": int(pairs), "rows": int(rows),
+        "events_per_s": n_events / t_step,
+        "step_roofline": {"bound": "hbm", "model_bytes": b_model, "achieved": b_model / t_step / 1e9,
+                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": b_model / t_step / 1e9 / HBM_PEAK_GBS},
+        "roofline": {"bound": "hbm", "kernel": dom[0], "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None},
+        "phases_ms": {p[0]: round(p[1], 3) for p in phases},
+        "gen_s": round(gen_s, 1),
+    }
+    if not args.no_cpu and world == 1:
+        out["cpu_baseline"] = cpu_baseline(n_sess, args.cpu_files, args.seed)
+    print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

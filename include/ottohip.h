@@ -1,0 +1,127 @@
+/* ottohip.h -- C-ABI of libottohip.so, the MI355X (gfx950) co-visitation engine.
+ *
+ * This is the drop-in boundary for the hot path of nicolaivicol/otto-recommender. The
+ * reference has no FFI: its boundary is a set of Python functions on polars DataFrames
+ * (SURVEY.md §8b). Each entry point below names the reference function it replaces; the
+ * Python host layer (otto-recommender_amd/covis.py) binds them with ctypes and keeps the
+ * reference's names, arguments and file contracts. See INTEGRATION.md for the bindings.
+ *
+ * Conventions
+ *   - Buffers are DEVICE pointers unless a field says "host". The caller owns inputs;
+ *     the library owns results (ottohip_table) and its workspace (ottohip_ctx).
+ *   - Every int-returning call returns 0 on success and a negative OTTOHIP_E* code on
+ *     failure; ottohip_last_error() gives a thread-local message.
+ *   - One host thread per context; calls are ordered on the given stream (hipStream_t
+ *     passed as void*, NULL = default stream). A context is bound to one device.
+ */
+#ifndef OTTOHIP_H
+#define OTTOHIP_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  OTTOHIP_OK = 0,
+  OTTOHIP_EINVAL = -1,    /* bad argument / shape */
+  OTTOHIP_ERANGE = -2,    /* aid, type or ts outside the supported range */
+  OTTOHIP_ENOMEM = -3,    /* device allocation failed */
+  OTTOHIP_EHIP = -4,      /* HIP runtime error */
+  OTTOHIP_ELIMIT = -5,    /* input exceeds an engine limit (documented in DESIGN.md) */
+};
+
+typedef struct ottohip_ctx ottohip_ctx;
+typedef struct ottohip_table ottohip_table;
+
+/* One co-visitation rule: pairs (i, j) of one session with type_i == this_type,
+ * type_j in next_type_mask (bit t = type t) and |ts_j - ts_i| <= max_abs_dt.
+ * Mirrors config.MAP_NAME_COUNT_TYPE / MAP_MAX_TIME_TO_NEXT (config.py:43-49, 81-88). */
+typedef struct {
+  int32_t this_type;
+  uint32_t next_type_mask;
+  int32_t max_abs_dt;
+} ottohip_rule;
+
+/* Session-sorted CSR events: session s owns rows [session_offsets[s], session_offsets[s+1])
+ * of aid/ts/type; session_offsets[0] == 0. Schema of etl/jsonl_to_parquet.py:23-29.
+ * file_session_bounds (HOST, n_files+1 entries) partitions sessions into the reference's
+ * parquet files; per-file counts drive the merge rule of count_co_events.py:131-132. */
+typedef struct {
+  const int64_t* session_offsets;
+  int64_t n_sessions;
+  const int32_t* aid;
+  const int32_t* ts;
+  const int8_t* type;
+  int64_t n_events;
+  const int64_t* file_session_bounds; /* host */
+  int32_t n_files;
+} ottohip_events;
+
+typedef struct {
+  int32_t min_dt;   /* config.MIN_TIME_TO_NEXT (-86400), count_co_events.py:33-36 */
+  int32_t max_dt;   /* config.MAX_TIME_TO_NEXT (+86400) */
+  int32_t n_items;  /* aid range [0, n_items); OTTO: 1855603 */
+  int32_t dedup;    /* 1 = df.unique() first (count_co_events.py:92) */
+} ottohip_covis_params;
+
+/* per-rule statistics of a count table */
+typedef struct {
+  int64_t n_rows;          /* distinct (aid, aid_next) over all files */
+  int64_t n_pairs;         /* qualifying ordered pairs = sum of counts */
+  int64_t file_rows;       /* sum over files of per-file distinct rows (N of :117) */
+  int64_t file_rows_ge2;   /* same, per-file rows with count >= 2 (after :131-132) */
+} ottohip_rule_stats;
+
+int ottohip_ctx_create(int device, ottohip_ctx** out);
+void ottohip_ctx_destroy(ottohip_ctx* ctx);
+const char* ottohip_last_error(void);
+/* phase timing (HIP events on the call's stream): enable, then read after a call */
+int ottohip_ctx_set_timing(ottohip_ctx* ctx, int enable);
+int ottohip_ctx_timing(ottohip_ctx* ctx, int idx, const char** name, float* ms, double* bytes);
+
+/* Co-visitation counts for all rules over all files in one pass.
+ * Replaces the per-file stage of count_co_events_all_files (model/count_co_events.py:80-100:
+ * unique :92 + self_merge_big_df :41-57 + count_co_events :60-77) and the cross-file
+ * groupby of concat_files_w_stats (:168). For every (rule, aid, aid_next) the table holds
+ *   count     = sum over files of the per-file count          (all rows)
+ *   count_ge2 = sum over files of per-file counts that are >= 2 (MIN_COUNT_IN_PART rule)
+ * With n_files == 1 the table IS the reference's per-file output of :94. */
+int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip_rule* rules,
+                        int n_rules, const ottohip_covis_params* params, ottohip_table** out,
+                        void* stream);
+int ottohip_table_stats(const ottohip_table* t, int rule, ottohip_rule_stats* st);
+/* copy one rule's rows (unordered) into caller device buffers of n_rows entries;
+ * any output pointer may be NULL */
+int ottohip_table_copy(const ottohip_table* t, int rule, int32_t* aid, int32_t* aid_next,
+                       uint32_t* count, uint32_t* count_ge2, void* stream);
+void ottohip_table_free(ottohip_table* t);
+
+/* Final merge of concat_files_w_stats (model/count_co_events.py:103-181) for one rule:
+ * pick count or count_ge2 (the per-file filter applies iff click_rule && file_rows > 1e8),
+ * keep count >= min_count (MIN_COUNT_TO_SAVE, config.py:56-62), order by count desc with
+ * the deterministic tie-break (aid asc, aid_next asc), keep the first max_rows rows
+ * (MAX_CO_EVENT_PAIRS_TO_SAVE_DISK). Writes up to max_rows rows; *n_out = rows written.
+ * Returns OTTOHIP_ELIMIT if the reference would take its part-wise branch (:135-166),
+ * which is not implemented on the device yet. */
+typedef struct {
+  int32_t click_rule;        /* 'click_to' in name */
+  int32_t min_count_in_part; /* MIN_COUNT_IN_PART (2) */
+  int32_t min_count;         /* MIN_COUNT_TO_SAVE[name] */
+  int64_t max_rows;          /* MAX_CO_EVENT_PAIRS_TO_SAVE_DISK */
+  int64_t filter_rows;       /* 100_000_000 threshold of :131 */
+  int64_t max_rows_groupby;  /* MAX_ROWS_POLARS_GROUPBY (3e8) of :135 */
+} ottohip_merge_params;
+int ottohip_table_finalize(ottohip_ctx* ctx, const ottohip_table* t, int rule,
+                           const ottohip_merge_params* mp, int32_t* aid, int32_t* aid_next,
+                           int32_t* count, int64_t* n_out, void* stream);
+
+/* Test hooks for the device primitives the engine is built from (parity tests only). */
+int ottohip_test_exclusive_scan_u32(ottohip_ctx* ctx, const uint32_t* in, uint64_t* out, int64_t n,
+                                    uint64_t* total_host, void* stream);
+int ottohip_test_radix_sort_pairs(ottohip_ctx* ctx, uint32_t* keys, uint32_t* vals, int64_t n,
+                                  int bits, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,228 @@
+"""Co-visitation counting on MI355X behind the reference's function signatures.
+
+Mirrors model/count_co_events.py:
+  count_co_events(df)                         :60-77  (here: raw events in, fused GPU path)
+  count_co_events_all_files(dir_sessions, dir_stats, skip_if_exists=True)   :80-100
+  concat_files_w_stats(name, dir_stats, files_stats=None)                   :103-181
+plus the fused build used by the benchmark:
+  count_co_events_fused(events, file_bounds) -> CovisTable   (count + cross-file merge in one pass)
+
+All compute goes through libottohip.so (include/ottohip.h); there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+import glob
+import os
+from pathlib import Path
+from typing import Dict
+
+import numpy as np
+
+from . import _lib
+from . import config
+from .synth import Events, events_from_columns, read_parquet_events
+
+
+def reference_rules(names=None):
+    """config.MAP_NAME_COUNT_TYPE + MAP_MAX_TIME_TO_NEXT as C-ABI rules (config.py:43-49,81-88)."""
+    names = list(names or config.CO_EVENTS_TO_COUNT)
+    arr = (_lib.Rule * len(names))()
+    for i, n in enumerate(names):
+        this, nxt = config.MAP_NAME_COUNT_TYPE[n]
+        arr[i].this_type = this
+        arr[i].next_type_mask = sum(1 << t for t in nxt)
+        arr[i].max_abs_dt = config.MAP_MAX_TIME_TO_NEXT[n]
+    return names, arr
+
+
+class DeviceEvents:
+    """Events resident in HBM (torch tensors as device buffers) + host file bounds."""
+
+    def __init__(self, offsets, aid, ts, type_, file_bounds, n_sessions, n_events):
+        self.offsets, self.aid, self.ts, self.type = offsets, aid, ts, type_
+        self.file_bounds = np.ascontiguousarray(file_bounds, dtype=np.int64)
+        self.n_sessions, self.n_events = int(n_sessions), int(n_events)
+
+    @staticmethod
+    def from_host(ev: Events, file_bounds=None, device=None) -> "DeviceEvents":
+        import torch
+        _lib.require_gpu()
+        dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        off = np.ascontiguousarray(ev.session_offsets - ev.session_offsets[0], np.int64)
+        if file_bounds is None:
+            file_bounds = np.array([0, ev.n_sessions], np.int64)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=False)
+        return DeviceEvents(t(off), t(ev.aid), t(ev.ts), t(ev.type), file_bounds, ev.n_sessions, ev.n_events)
+
+    def abi(self) -> _lib.Events:
+        e = _lib.Events()
+        e.session_offsets = _lib.ptr(self.offsets)
+        e.n_sessions = self.n_sessions
+        e.aid, e.ts, e.type = _lib.ptr(self.aid), _lib.ptr(self.ts), _lib.ptr(self.type)
+        e.n_events = self.n_events
+        e.file_session_bounds = self.file_bounds.ctypes.data
+        e.n_files = len(self.file_bounds) - 1
+        return e
+
+
+class CovisTable:
+    """Device-resident result of ottohip_covis_count: per rule (aid, aid_next, count, count_ge2)."""
+
+    def __init__(self, handle, names, ctx):
+        self.h = handle
+        self.names = list(names)
+        self.ctx = ctx
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def free(self):
+        if self.h:
+            _lib.load().ottohip_table_free(self.h)
+            self.h = ctypes.c_void_p()
+
+    def _rule(self, name) -> int:
+        return self.names.index(name) if isinstance(name, str) else int(name)
+
+    def stats(self, name) -> dict:
+        st = _lib.RuleStats()
+        _lib.check(_lib.load().ottohip_table_stats(self.h, self._rule(name), ctypes.byref(st)))
+        return {"n_rows": st.n_rows, "n_pairs": st.n_pairs, "file_rows": st.file_rows,
+                "file_rows_ge2": st.file_rows_ge2}
+
+    def to_torch(self, name, stream=None):
+        import torch
+        n = self.stats(name)["n_rows"]
+        dev = torch.device("cuda", self.ctx.device)
+        a = torch.empty(n, dtype=torch.int32, device=dev)
+        b = torch.empty(n, dtype=torch.int32, device=dev)
+        c = torch.empty(n, dtype=torch.int32, device=dev)   # u32 bits
+        c2 = torch.empty(n, dtype=torch.int32, device=dev)
+        _lib.check(_lib.load().ottohip_table_copy(self.h, self._rule(name), _lib.ptr(a), _lib.ptr(b), _lib.ptr(c),
+                                                  _lib.ptr(c2), _lib.stream_handle(stream)))
+        return a, b, c, c2
+
+    def to_numpy(self, name, sort=True):
+        """(aid:int32, aid_next:int32, count:uint32, count_ge2:uint32), sorted by (aid, aid_next)."""
+        a, b, c, c2 = (x.cpu().numpy() for x in self.to_torch(name))
+        c, c2 = c.view(np.uint32), c2.view(np.uint32)
+        if sort:
+            o = np.lexsort((b, a))
+            a, b, c, c2 = a[o], b[o], c[o], c2[o]
+        return a, b, c, c2
+
+    def finalize(self, name, stream=None, max_rows=None):
+        """concat_files_w_stats' final step (:131-175) on the device for one rule:
+        returns torch (aid, aid_next, count:int32) in (count desc, aid, aid_next) order."""
+        import torch
+        rname = self.names[self._rule(name)]
+        mp = _lib.MergeParams()
+        mp.click_rule = 1 if "click_to" in rname else 0
+        mp.min_count_in_part = config.MIN_COUNT_IN_PART.get(rname, 1)
+        mp.min_count = config.MIN_COUNT_TO_SAVE.get(rname, 1)
+        mp.max_rows = config.MAX_CO_EVENT_PAIRS_TO_SAVE_DISK if max_rows is None else int(max_rows)
+        mp.filter_rows = config.CLICK_FILTER_ROWS
+        mp.max_rows_groupby = config.MAX_ROWS_POLARS_GROUPBY
+        n = min(self.stats(name)["n_rows"], mp.max_rows)
+        dev = torch.device("cuda", self.ctx.device)
+        a = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        b = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        c = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        n_out = ctypes.c_int64(0)
+        _lib.check(_lib.load().ottohip_table_finalize(self.ctx.h, self.h, self._rule(name), ctypes.byref(mp),
+                                                      _lib.ptr(a), _lib.ptr(b), _lib.ptr(c), ctypes.byref(n_out),
+                                                      _lib.stream_handle(stream)))
+        k = int(n_out.value)
+        return a[:k], b[:k], c[:k]
+
+
+def count_co_events_fused(events: DeviceEvents, names=None, n_items: int = config.N_ITEMS_OTTO, dedup: bool = True,
+                          stream=None, ctx=None) -> CovisTable:
+    """All rules over all files of `events` in one device pass (per-file counts folded into
+    count / count_ge2): count_co_events_all_files + the groupby of concat_files_w_stats."""
+    ctx = ctx or _lib.context()
+    names, rules = reference_rules(names)
+    p = _lib.CovisParams()
+    p.min_dt, p.max_dt, p.n_items, p.dedup = config.MIN_TIME_TO_NEXT, config.MAX_TIME_TO_NEXT, int(n_items), int(dedup)
+    ev = events.abi()
+    h = ctypes.c_void_p()
+    _lib.check(_lib.load().ottohip_covis_count(ctx.h, ctypes.byref(ev), rules, len(names), ctypes.byref(p),
+                                               ctypes.byref(h), _lib.stream_handle(stream)))
+    return CovisTable(h, names, ctx)
+
+
+def _n_items_for(aid: np.ndarray) -> int:
+    return max(config.N_ITEMS_OTTO, int(aid.max()) + 1 if len(aid) else 1)
+
+
+def count_co_events(df, names=None) -> Dict[str, "object"]:
+    """model/count_co_events.py:60 on RAW events (session, aid, ts, type): unique + self-join +
+    time filter + per-rule groupby count, fused on the GPU without materialising the join.
+    Returns {name: pandas.DataFrame[aid:int32, aid_next:int32, count:uint32]} (row order unspecified,
+    as in the reference). A pre-joined frame (with 'aid_next') is rejected: the device path
+    never builds the Cartesian product."""
+    import pandas as pd
+    if "aid_next" in df.columns:
+        raise ValueError("count_co_events() takes raw events; the joined frame of self_merge() is not materialised "
+                         "on the device path")
+    ev = events_from_columns(df["session"].to_numpy(), df["aid"].to_numpy(), df["ts"].to_numpy(),
+                             df["type"].to_numpy())
+    dev = DeviceEvents.from_host(ev)
+    tab = count_co_events_fused(dev, names, n_items=_n_items_for(ev.aid))
+    out = {}
+    for n in tab.names:
+        a, b, c, _ = tab.to_numpy(n, sort=False)
+        out[n] = pd.DataFrame({"aid": a, "aid_next": b, "count": c.astype(np.uint32)})
+    return out
+
+
+def _write_table(path, aid, aid_next, count, count_dtype):
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    pq.write_table(pa.table({"aid": np.asarray(aid, np.int32), "aid_next": np.asarray(aid_next, np.int32),
+                             "count": np.asarray(count).astype(count_dtype)}), path)
+
+
+def count_co_events_all_files(dir_sessions, dir_stats, skip_if_exists=True):
+    """model/count_co_events.py:80-100: per parquet file of sessions, the 5 count tables
+    written to {dir_stats}/{name}/{stem}.parquet as (aid:int32, aid_next:int32, count:uint32)."""
+    files = sorted(glob.glob(f"{dir_sessions}/*.parquet"))
+    for f in files:
+        stem = Path(f).stem
+        outs = {n: f"{dir_stats}/{n}/{stem}.parquet" for n in config.CO_EVENTS_TO_COUNT}
+        if skip_if_exists and all(os.path.exists(p) for p in outs.values()):
+            continue
+        ev = read_parquet_events(f)
+        tab = count_co_events_fused(DeviceEvents.from_host(ev), n_items=_n_items_for(ev.aid))
+        for n, p in outs.items():
+            a, b, c, _ = tab.to_numpy(n, sort=False)
+            _write_table(p, a, b, c, np.uint32)
+        tab.free()
+
+
+def count_co_events_build(dir_sessions, dir_stats, names=None):
+    """Fused equivalent of `count_co_events_all_files` + `concat_files_w_stats` for one folder:
+    reads every session file once, counts all files in one device pass and writes the merged
+    tables {dir_stats}/{name}.parquet (aid:int32, aid_next:int32, count:int32), count desc."""
+    files = sorted(glob.glob(f"{dir_sessions}/*.parquet"))
+    parts = [read_parquet_events(f) for f in files]
+    bounds = np.zeros(len(parts) + 1, np.int64)
+    for i, p in enumerate(parts):
+        bounds[i + 1] = bounds[i] + p.n_sessions
+    off = np.zeros(int(bounds[-1]) + 1, np.int64)
+    cols = [np.concatenate([getattr(p, k) for p in parts]) for k in ("session", "aid", "ts", "type")]
+    pos = 0
+    for i, p in enumerate(parts):
+        off[bounds[i]:bounds[i + 1] + 1] = p.session_offsets - p.session_offsets[0] + pos
+        pos += p.n_events
+    ev = Events(off, *cols)
+    tab = count_co_events_fused(DeviceEvents.from_host(ev, bounds), names, n_items=_n_items_for(ev.aid))
+    for n in tab.names:
+        a, b, c = (x.cpu().numpy() for x in tab.finalize(n))
+        _write_table(f"{dir_stats}/{n}.parquet", a, b, c, np.int32)
+    tab.free()

@@ -1,0 +1,501 @@
+// Host orchestration of the co-visitation engine and the C-ABI of include/ottohip.h.
+#include <cstdarg>
+#include <algorithm>
+#include "prims.h"
+#include "covis_kernels.h"
+
+using namespace ottohip;
+
+namespace ottohip {
+static thread_local char g_err[1024] = "";
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+}
+}  // namespace ottohip
+
+// device buffers of one count table (reused across calls through the context's spare slot)
+struct TableBufs {
+  uint64_t cap = 0;
+  uint8_t* rule = nullptr;
+  int32_t* aid = nullptr;
+  int32_t* aid_next = nullptr;
+  uint32_t* count = nullptr;
+  uint32_t* count_ge2 = nullptr;
+  void release() {
+    if (rule) (void)hipFree(rule);
+    if (aid) (void)hipFree(aid);
+    if (aid_next) (void)hipFree(aid_next);
+    if (count) (void)hipFree(count);
+    if (count_ge2) (void)hipFree(count_ge2);
+    *this = TableBufs();
+  }
+  int alloc(uint64_t n) {
+    if (hipMalloc(&rule, n) || hipMalloc(&aid, n * 4) || hipMalloc(&aid_next, n * 4) || hipMalloc(&count, n * 4) ||
+        hipMalloc(&count_ge2, n * 4)) {
+      (void)hipGetLastError();
+      release();
+      set_error("table allocation for %llu rows failed", (unsigned long long)n);
+      return OTTOHIP_ENOMEM;
+    }
+    cap = n;
+    return 0;
+  }
+};
+
+struct ottohip_ctx : public Ctx {
+  TableBufs spare;  // buffers of the last freed table, reused by the next count
+};
+
+struct ottohip_table {
+  int device = 0;
+  int n_rules = 0;
+  int64_t n_rows = 0;
+  TableBufs b;
+  ottohip_rule_stats stats[MAX_RULES];
+  ottohip_ctx* ctx = nullptr;
+};
+
+static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+template <class T>
+static int d2h(T* host, const T* dev, size_t n, hipStream_t s) {
+  OH_HIP(hipMemcpyAsync(host, dev, n * sizeof(T), hipMemcpyDeviceToHost, s));
+  OH_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+static unsigned grid_for(int64_t n, int t = 256) { return (unsigned)std::max<int64_t>(1, ceil_div(n, t)); }
+
+extern "C" {
+
+const char* ottohip_last_error(void) { return ottohip::g_err; }
+
+int ottohip_ctx_create(int device, ottohip_ctx** out) {
+  if (!out) { set_error("ottohip_ctx_create: out is NULL"); return OTTOHIP_EINVAL; }
+  OH_HIP(hipSetDevice(device));
+  ottohip_ctx* c = new ottohip_ctx();
+  c->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
+  if (hipHostMalloc(reinterpret_cast<void**>(&c->pinned), 64 * sizeof(uint64_t)) != hipSuccess) c->pinned = nullptr;
+  *out = c;
+  return 0;
+}
+
+void ottohip_ctx_destroy(ottohip_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  hipDeviceSynchronize();
+  ctx->ws.release();
+  ctx->spare.release();
+  for (auto e : ctx->event_pool) hipEventDestroy(e);
+  if (ctx->pinned) hipHostFree(ctx->pinned);
+  delete ctx;
+}
+
+int ottohip_ctx_set_timing(ottohip_ctx* ctx, int enable) {
+  if (!ctx) return OTTOHIP_EINVAL;
+  ctx->timing = enable != 0;
+  return 0;
+}
+
+int ottohip_ctx_timing(ottohip_ctx* ctx, int idx, const char** name, float* ms, double* bytes) {
+  if (!ctx) return OTTOHIP_EINVAL;
+  if (idx < 0) return (int)ctx->phases.size();
+  if (idx >= (int)ctx->phases.size()) return OTTOHIP_EINVAL;
+  Phase& p = ctx->phases[idx];
+  OH_HIP(hipEventSynchronize(p.b));
+  float t = 0;
+  OH_HIP(hipEventElapsedTime(&t, p.a, p.b));
+  if (name) *name = p.name.c_str();
+  if (ms) *ms = t;
+  if (bytes) *bytes = p.bytes;
+  return 0;
+}
+
+int ottohip_test_exclusive_scan_u32(ottohip_ctx* ctx, const uint32_t* in, uint64_t* out, int64_t n,
+                                    uint64_t* total_host, void* stream) {
+  if (!ctx) return OTTOHIP_EINVAL;
+  uint64_t* tot;
+  OH_TRY(ctx->ws.get("test_total", 1, &tot));
+  OH_TRY(exclusive_scan_u32(ctx, in, out, n, tot, S(stream)));
+  if (total_host) OH_TRY(d2h(total_host, tot, 1, S(stream)));
+  return 0;
+}
+
+int ottohip_test_radix_sort_pairs(ottohip_ctx* ctx, uint32_t* keys, uint32_t* vals, int64_t n, int bits,
+                                  void* stream) {
+  if (!ctx || bits < 0 || bits > 32) return OTTOHIP_EINVAL;
+  uint32_t *ka, *va;
+  OH_TRY(ctx->ws.get("test_ka", (size_t)std::max<int64_t>(n, 1), &ka));
+  OH_TRY(ctx->ws.get("test_va", (size_t)std::max<int64_t>(n, 1), &va));
+  uint32_t *k = keys, *v = vals;
+  OH_TRY(radix_sort_pairs(ctx, k, v, ka, va, n, bits, S(stream)));
+  if (k != keys) {
+    OH_HIP(hipMemcpyAsync(keys, k, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, S(stream)));
+    OH_HIP(hipMemcpyAsync(vals, v, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, S(stream)));
+  }
+  return 0;
+}
+
+int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip_rule* rules, int n_rules,
+                        const ottohip_covis_params* params, ottohip_table** out, void* stream) {
+  if (!ctx || !ev || !rules || !params || !out) { set_error("ottohip_covis_count: NULL argument"); return OTTOHIP_EINVAL; }
+  *out = nullptr;
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  ctx->reset_timing();
+  const int64_t E = ev->n_events, Sn = ev->n_sessions;
+  if (n_rules < 1 || n_rules > MAX_RULES) { set_error("n_rules=%d outside [1, %d]", n_rules, MAX_RULES); return OTTOHIP_EINVAL; }
+  if (E < 0 || Sn < 0 || (E > 0 && (!ev->session_offsets || !ev->aid || !ev->ts || !ev->type))) {
+    set_error("bad event table"); return OTTOHIP_EINVAL;
+  }
+  if (E >= ((int64_t)1 << 32)) { set_error("n_events=%lld >= 2^32 (split into shards)", (long long)E); return OTTOHIP_ELIMIT; }
+  if (params->n_items < 1 || params->n_items > (1 << 30)) { set_error("n_items=%d outside [1, 2^30]", params->n_items); return OTTOHIP_ERANGE; }
+  if (ev->n_files < 1 || !ev->file_session_bounds) { set_error("need >= 1 file"); return OTTOHIP_EINVAL; }
+  if (ev->file_session_bounds[0] != 0 || ev->file_session_bounds[ev->n_files] != Sn) {
+    set_error("file_session_bounds must start at 0 and end at n_sessions"); return OTTOHIP_EINVAL;
+  }
+  for (int f = 0; f < ev->n_files; ++f)
+    if (ev->file_session_bounds[f + 1] < ev->file_session_bounds[f]) { set_error("file bounds not monotone"); return OTTOHIP_EINVAL; }
+  if (ev->n_files > 65535) { set_error("n_files > 65535"); return OTTOHIP_ELIMIT; }
+
+  RulesDev R;
+  memset(&R, 0, sizeof R);
+  int max_per_type = 1;
+  for (int r = 0; r < n_rules; ++r) {
+    const ottohip_rule& q = rules[r];
+    if (q.this_type < 0 || q.this_type > 2 || (q.next_type_mask & ~7u) || q.max_abs_dt < 0) {
+      set_error("rule %d invalid", r); return OTTOHIP_EINVAL;
+    }
+    R.lo[r] = std::max(params->min_dt, -q.max_abs_dt);
+    R.hi[r] = std::min(params->max_dt, q.max_abs_dt);
+    R.mask[r] = q.next_type_mask;
+    int t = q.this_type;
+    R.rule_of_type[t][R.n_of_type[t]++] = r;
+    max_per_type = std::max(max_per_type, R.n_of_type[t]);
+  }
+  for (int r = 0; r < n_rules; ++r)
+    if (R.lo[r] > R.hi[r]) R.mask[r] = 0;  // empty window: never matches (count stays 0)
+  Layout Lt;
+  Lt.A = std::max(1, bits_for((uint64_t)params->n_items));
+  Lt.F = bits_for((uint64_t)ev->n_files);
+  Lt.BR = bits_for((uint64_t)max_per_type);
+  Lt.WB = Lt.BR + Lt.A + Lt.F;
+  Lt.amask = (1u << Lt.A) - 1u;
+  if (Lt.WB > 32) {
+    set_error("word layout %d rule + %d aid + %d file bits > 32: reduce files per call", Lt.BR, Lt.A, Lt.F);
+    return OTTOHIP_ELIMIT;
+  }
+
+  ottohip_table* T = new ottohip_table();
+  T->device = ctx->device;
+  T->n_rules = n_rules;
+  T->ctx = ctx;
+  memset(T->stats, 0, sizeof T->stats);
+  auto fail = [&](int rc) { ottohip_table_free(T); return rc; };
+  if (E == 0 || Sn == 0) { *out = T; return 0; }
+
+  Workspace& ws = ctx->ws;
+  const int64_t NB = ceil_div(E, EV_BLOCK);
+  int64_t *first, *fb;
+  int32_t *long_list, *n_long;
+  int* err;
+  const int64_t long_cap = E / (LCAP + 1) + 1;
+  int rc;
+  if ((rc = ws.get("first", (size_t)NB + 1, &first)) || (rc = ws.get("fb", (size_t)ev->n_files + 1, &fb)) ||
+      (rc = ws.get("long_list", (size_t)long_cap, &long_list)) || (rc = ws.get("n_long", 4, &n_long)) ||
+      (rc = ws.get("err", 4, &err)))
+    return fail(rc);
+  if (hipMemcpyAsync(fb, ev->file_session_bounds, (ev->n_files + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s) ||
+      hipMemsetAsync(n_long, 0, 4 * sizeof(int32_t), s) || hipMemsetAsync(err, 0, sizeof(int), s)) {
+    set_error("hip memcpy/memset failed"); return fail(OTTOHIP_EHIP);
+  }
+  const int64_t* off = ev->session_offsets;
+
+  // ---- S1 prep
+  uint64_t* evp;
+  if ((rc = ws.get("ev", (size_t)E, &evp))) return fail(rc);
+  int ph = ctx->begin("prep", s, 9.0 * E + 8.0 * (Sn + 1) + 8.0 * E);
+  k_block_first<<<grid_for(Sn + 1), 256, 0, s>>>(off, Sn, NB, first, long_list, n_long);
+  k_prep<<<grid_for(NB, 4), 256, 0, s>>>(off, first, NB, ev->aid, ev->ts, ev->type, evp, params->n_items,
+                                          params->dedup, err);
+  if (hipGetLastError() != hipSuccess) { set_error("k_prep launch failed"); return fail(OTTOHIP_EHIP); }
+  int32_t nl = 0;
+  if ((rc = d2h(&nl, n_long, 1, s))) return fail(rc);
+  std::vector<int64_t> loff;
+  uint64_t *lscr = nullptr;
+  uint32_t *lpscr = nullptr;
+  int64_t* d_loff = nullptr;
+  if (nl > 0) {
+    std::vector<int32_t> ll(nl);
+    if ((rc = d2h(ll.data(), long_list, (size_t)nl, s))) return fail(rc);
+    std::sort(ll.begin(), ll.end());
+    if (hipMemcpy(long_list, ll.data(), nl * sizeof(int32_t), hipMemcpyHostToDevice)) return fail(OTTOHIP_EHIP);
+    loff.resize(nl + 1);
+    loff[0] = 0;
+    for (int i = 0; i < nl; ++i) {
+      int64_t ab[2];
+      if (hipMemcpy(ab, off + ll[i], 2 * sizeof(int64_t), hipMemcpyDeviceToHost)) return fail(OTTOHIP_EHIP);
+      loff[i + 1] = loff[i] + (ab[1] - ab[0]);
+    }
+    if ((rc = ws.get("long_scr", (size_t)(2 * loff[nl]), &lscr)) ||
+        (rc = ws.get("long_pscr", (size_t)(3 * (loff[nl] + nl)), &lpscr)) ||
+        (rc = ws.get("long_off", (size_t)(nl + 1), &d_loff)))
+      return fail(rc);
+    if (hipMemcpy(d_loff, loff.data(), (nl + 1) * sizeof(int64_t), hipMemcpyHostToDevice)) return fail(OTTOHIP_EHIP);
+    k_prep_long<<<nl, 64, 0, s>>>(off, long_list, d_loff, lscr, ev->aid, ev->ts, ev->type, evp, params->n_items,
+                                  params->dedup, err);
+  }
+  ctx->end(ph, s);
+
+  // ---- S2 count
+  uint32_t *cnt, *rk, *pos, *rk2, *pos2;
+  if ((rc = ws.get("cnt", (size_t)E, &cnt)) || (rc = ws.get("rk", (size_t)E, &rk)) || (rc = ws.get("pos", (size_t)E, &pos)) ||
+      (rc = ws.get("rk2", (size_t)E, &rk2)) || (rc = ws.get("pos2", (size_t)E, &pos2)))
+    return fail(rc);
+  ph = ctx->begin("count", s, 8.0 * E + 12.0 * E);
+  k_count<<<grid_for(NB, 4), 256, 0, s>>>(off, first, NB, evp, R, Lt.A, cnt, rk, pos);
+  if (nl > 0) k_count_long<<<nl, 64, 0, s>>>(off, long_list, d_loff, lscr, lpscr, evp, R, Lt.A, cnt, rk, pos);
+  if (hipGetLastError() != hipSuccess) { set_error("k_count launch failed"); return fail(OTTOHIP_EHIP); }
+  ctx->end(ph, s);
+
+  // ---- S3 rows (aid-major transpose)
+  ph = ctx->begin("rows", s, 0);
+  uint32_t *rks = rk, *poss = pos;
+  if ((rc = radix_sort_pairs(ctx, rks, poss, rk2, pos2, E, Lt.A + 2, s))) return fail(rc);
+  uint32_t *c_sorted = (rks == rk) ? rk2 : rk, *row_flag = (poss == pos) ? pos2 : pos;  // reuse the idle pair
+  const uint32_t INV = 3u << Lt.A;
+  k_gather_counts<<<grid_for(E), 256, 0, s>>>(rks, poss, cnt, E, INV, c_sorted, row_flag);
+  uint64_t *woff, *row_idx, *tot;
+  if ((rc = ws.get("woff", (size_t)E, &woff)) || (rc = ws.get("row_idx", (size_t)E, &row_idx)) ||
+      (rc = ws.get("tot", 4, &tot)))
+    return fail(rc);
+  if ((rc = exclusive_scan_u32(ctx, c_sorted, woff, E, tot, s))) return fail(rc);
+  if ((rc = exclusive_scan_u32(ctx, row_flag, row_idx, E, tot + 1, s))) return fail(rc);
+  uint64_t PR[2];
+  if ((rc = d2h(PR, tot, 2, s))) return fail(rc);
+  int herr = 0;
+  if ((rc = d2h(&herr, err, 1, s))) return fail(rc);
+  if (herr) { set_error("input out of range: aid outside [0, n_items) or type outside {0,1,2}"); return fail(OTTOHIP_ERANGE); }
+  const uint64_t P = PR[0];
+  const int64_t Rn = (int64_t)PR[1];
+  uint64_t *poff, *row_begin;
+  uint32_t* row_key;
+  if ((rc = ws.get("poff", (size_t)E, &poff)) || (rc = ws.get("row_key", (size_t)std::max<int64_t>(Rn, 1), &row_key)) ||
+      (rc = ws.get("row_begin", (size_t)std::max<int64_t>(Rn, 1), &row_begin)))
+    return fail(rc);
+  k_rows<<<grid_for(E), 256, 0, s>>>(rks, poss, E, INV, woff, row_flag, row_idx, poff, row_key, row_begin);
+  ctx->end(ph, s);
+  if (P == 0) { *out = T; return 0; }
+
+  // ---- S4 emit
+  uint32_t *w0, *w1;
+  if ((rc = ws.get("words0", (size_t)P, &w0)) || (rc = ws.get("words1", (size_t)P, &w1))) return fail(rc);
+  ph = ctx->begin("emit", s, 8.0 * E + 12.0 * E + 4.0 * (double)P);
+  k_emit<<<grid_for(NB, 4), 256, 0, s>>>(off, first, NB, evp, R, Lt, fb, ev->n_files, cnt, poff, w0);
+  if (nl > 0)
+    k_emit_long<<<nl, 64, 0, s>>>(off, long_list, d_loff, lscr, lpscr, evp, R, Lt, fb, ev->n_files, cnt, poff, w0);
+  if (hipGetLastError() != hipSuccess) { set_error("k_emit launch failed"); return fail(OTTOHIP_EHIP); }
+  ctx->end(ph, s);
+
+  // ---- S5 reduce
+  if (ctx->spare.cap >= P) {
+    T->b = ctx->spare;
+    ctx->spare = TableBufs();
+  } else {
+    (void)hipDeviceSynchronize();
+    ctx->spare.release();
+    if ((rc = T->b.alloc(P))) return fail(rc);
+  }
+  unsigned long long *cursor, *stats, *lcount;
+  if ((rc = ws.get("cursor", 1, &cursor)) || (rc = ws.get("stats", MAX_RULES * 4, &stats)) ||
+      (rc = ws.get("lcount", 4, &lcount)))
+    return fail(rc);
+  hipMemsetAsync(cursor, 0, 8, s);
+  hipMemsetAsync(stats, 0, MAX_RULES * 4 * 8, s);
+  OutRows O;
+  O.rule = T->b.rule; O.aid = T->b.aid; O.aid_next = T->b.aid_next; O.count = T->b.count; O.count_ge2 = T->b.count_ge2;
+  O.cursor = cursor; O.cap = P; O.stats = stats;
+
+  ph = ctx->begin("reduce", s, 4.0 * (double)P);
+  // level 0 task lists come from the rows
+  Task *tiny, *hash, *splitA;
+  uint64_t cap0 = (uint64_t)std::max<int64_t>(Rn, 1);
+  if ((rc = ws.get("t_tiny", cap0 * sizeof(Task), reinterpret_cast<void**>(&tiny))) ||
+      (rc = ws.get("t_hash", cap0 * sizeof(Task), reinterpret_cast<void**>(&hash))) ||
+      (rc = ws.get("t_splitA", cap0 * sizeof(Task), reinterpret_cast<void**>(&splitA))))
+    return fail(rc);
+  TaskLists TL;
+  TL.tiny = tiny; TL.hash = hash; TL.split = splitA; TL.n = lcount;
+  TL.cap_tiny = TL.cap_hash = TL.cap_split = cap0;
+  hipMemsetAsync(lcount, 0, 4 * 8, s);
+  k_classify_rows<<<grid_for(Rn), 256, 0, s>>>(row_begin, Rn, P, Lt.WB, TL, err);
+  const int agg_grid = ctx->n_cu * 8;
+  bool srcA = true;
+  for (int level = 0; level < 8; ++level) {
+    unsigned long long nlist[3];
+    if ((rc = d2h(nlist, lcount, 3, s))) return fail(rc);
+    if ((rc = d2h(&herr, err, 1, s))) return fail(rc);
+    if (herr) { set_error("task list overflow / row too large (err=%d)", herr); return fail(OTTOHIP_ELIMIT); }
+    if (nlist[0]) k_agg_tiny<<<(unsigned)std::min<uint64_t>(ceil_div((int64_t)nlist[0], 4), (uint64_t)ctx->n_cu * 32), 256, 0, s>>>(
+        TL.tiny, (int64_t)nlist[0], w0, w1, row_key, R, Lt, O);
+    if (nlist[1]) k_agg_hash<<<(unsigned)std::min<uint64_t>(nlist[1], (uint64_t)agg_grid), AGG_T, 0, s>>>(
+        TL.hash, (int64_t)nlist[1], w0, w1, row_key, R, Lt, O);
+    const int64_t ns = (int64_t)nlist[2];
+    if (ns == 0) break;
+    Task* cur_split = TL.split;
+    // chunk / digit bases
+    uint32_t *nch, *ndg;
+    uint64_t *chb, *dgb, *tot2;
+    if ((rc = ws.get("sp_nch", (size_t)ns, &nch)) || (rc = ws.get("sp_ndg", (size_t)ns, &ndg)) ||
+        (rc = ws.get("sp_chb", (size_t)ns + 1, &chb)) || (rc = ws.get("sp_dgb", (size_t)ns + 1, &dgb)) ||
+        (rc = ws.get("sp_tot", 2, &tot2)))
+      return fail(rc);
+    k_split_prepare<<<grid_for(ns), 256, 0, s>>>(cur_split, ns, nch, ndg);
+    if ((rc = exclusive_scan_u32(ctx, nch, chb, ns, tot2, s)) || (rc = exclusive_scan_u32(ctx, ndg, dgb, ns, tot2 + 1, s)))
+      return fail(rc);
+    uint64_t tt[2];
+    if ((rc = d2h(tt, tot2, 2, s))) return fail(rc);
+    const int64_t nchunks = (int64_t)tt[0], ndig = (int64_t)tt[1];
+    uint32_t* dcount;
+    uint64_t* doff;
+    unsigned long long* dcur;
+    if ((rc = ws.get("sp_dcount", (size_t)ndig, &dcount)) || (rc = ws.get("sp_doff", (size_t)ndig, &doff)) ||
+        (rc = ws.get("sp_dcur", (size_t)ndig, &dcur)))
+      return fail(rc);
+    hipMemsetAsync(dcount, 0, ndig * 4, s);
+    k_split_hist<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, dgb, w0, w1, dcount);
+    if ((rc = exclusive_scan_u32(ctx, dcount, doff, ndig, nullptr, s))) return fail(rc);
+    k_split_cursor<<<grid_for(ndig), 256, 0, s>>>(cur_split, ns, dgb, doff, dcur, ndig);
+    k_split_scatter<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, dgb, w0, w1, dcur);
+    // next lists
+    const uint64_t capn = (uint64_t)ndig;
+    Task *ntiny, *nhash, *nsplit;
+    if ((rc = ws.get("t_tiny", std::max(cap0, capn) * sizeof(Task), reinterpret_cast<void**>(&ntiny))) ||
+        (rc = ws.get("t_hash", std::max(cap0, capn) * sizeof(Task), reinterpret_cast<void**>(&nhash))) ||
+        (rc = ws.get(srcA ? "t_splitB" : "t_splitA", capn * sizeof(Task), reinterpret_cast<void**>(&nsplit))))
+      return fail(rc);
+    TL.tiny = ntiny; TL.hash = nhash; TL.split = nsplit;
+    TL.cap_tiny = TL.cap_hash = std::max(cap0, capn); TL.cap_split = capn;
+    hipMemsetAsync(lcount, 0, 4 * 8, s);
+    k_split_classify<<<grid_for(ndig), 256, 0, s>>>(cur_split, ns, dgb, dcount, doff, ndig, TL, err);
+    srcA = !srcA;
+    if (hipGetLastError() != hipSuccess) { set_error("split launch failed"); return fail(OTTOHIP_EHIP); }
+  }
+  ctx->end(ph, s);
+  unsigned long long U = 0;
+  if ((rc = d2h(&U, cursor, 1, s))) return fail(rc);
+  unsigned long long st[MAX_RULES * 4];
+  if ((rc = d2h(st, stats, MAX_RULES * 4, s))) return fail(rc);
+  if (hipGetLastError() != hipSuccess) { set_error("reduce failed"); return fail(OTTOHIP_EHIP); }
+  T->n_rows = (int64_t)U;
+  for (int r = 0; r < n_rules; ++r) {
+    T->stats[r].n_rows = (int64_t)st[r * 4 + 0];
+    T->stats[r].n_pairs = (int64_t)st[r * 4 + 1];
+    T->stats[r].file_rows = (int64_t)st[r * 4 + 2];
+    T->stats[r].file_rows_ge2 = (int64_t)st[r * 4 + 3];
+  }
+  *out = T;
+  return 0;
+}
+
+int ottohip_table_stats(const ottohip_table* t, int rule, ottohip_rule_stats* st) {
+  if (!t || !st || rule < 0 || rule >= t->n_rules) { set_error("table_stats: bad args"); return OTTOHIP_EINVAL; }
+  *st = t->stats[rule];
+  return 0;
+}
+
+int ottohip_table_copy(const ottohip_table* t, int rule, int32_t* aid, int32_t* aid_next, uint32_t* count,
+                       uint32_t* count_ge2, void* stream) {
+  if (!t || rule < 0 || rule >= t->n_rules) { set_error("table_copy: bad args"); return OTTOHIP_EINVAL; }
+  if (t->n_rows == 0 || t->stats[rule].n_rows == 0) return 0;
+  hipStream_t s = S(stream);
+  Ctx* ctx = t->ctx;
+  uint32_t* flag;
+  uint64_t* idx;
+  OH_TRY(ctx->ws.get("copy_flag", (size_t)t->n_rows, &flag));
+  OH_TRY(ctx->ws.get("copy_idx", (size_t)t->n_rows, &idx));
+  k_select_rule<<<grid_for(t->n_rows), 256, 0, s>>>(t->b.rule, t->n_rows, rule, flag);
+  OH_TRY(exclusive_scan_u32(ctx, flag, idx, t->n_rows, nullptr, s));
+  k_compact_rule<<<grid_for(t->n_rows), 256, 0, s>>>(t->b.rule, t->n_rows, rule, idx, t->b.aid, t->b.aid_next,
+                                                     t->b.count, t->b.count_ge2, aid, aid_next, count, count_ge2);
+  OH_HIP(hipGetLastError());
+  return 0;
+}
+
+void ottohip_table_free(ottohip_table* t) {
+  if (!t) return;
+  (void)hipSetDevice(t->device);
+  (void)hipDeviceSynchronize();
+  if (t->ctx && t->b.cap > t->ctx->spare.cap) {  // keep the larger buffer set for the next call
+    t->ctx->spare.release();
+    t->ctx->spare = t->b;
+  } else {
+    t->b.release();
+  }
+  delete t;
+}
+
+}  // extern "C"
+
+extern "C" int ottohip_table_finalize(ottohip_ctx* ctx, const ottohip_table* t, int rule,
+                                      const ottohip_merge_params* mp, int32_t* aid, int32_t* aid_next,
+                                      int32_t* count, int64_t* n_out, void* stream) {
+  if (!ctx || !t || !mp || !n_out || rule < 0 || rule >= t->n_rules) { set_error("finalize: bad args"); return OTTOHIP_EINVAL; }
+  *n_out = 0;
+  hipStream_t s = S(stream);
+  const ottohip_rule_stats& st = t->stats[rule];
+  const bool use_ge2 = mp->click_rule && st.file_rows > mp->filter_rows;
+  const int64_t n_after = use_ge2 ? st.file_rows_ge2 : st.file_rows;
+  if (n_after > mp->max_rows_groupby) {
+    set_error("rule %d: %lld per-file rows > %lld: the reference's part-wise branch (count_co_events.py:135-166) "
+              "is not implemented on the device", rule, (long long)n_after, (long long)mp->max_rows_groupby);
+    return OTTOHIP_ELIMIT;
+  }
+  if (t->n_rows == 0) return 0;
+  const uint32_t thr = (uint32_t)std::max<int32_t>(mp->min_count, 1);
+  Workspace& ws = ctx->ws;
+  const int64_t n = t->n_rows;
+  uint32_t* flag;
+  uint64_t *idx, *tot;
+  OH_TRY(ws.get("fin_flag", (size_t)n, &flag));
+  OH_TRY(ws.get("fin_idx", (size_t)n, &idx));
+  OH_TRY(ws.get("fin_tot", 1, &tot));
+  k_fin_select<<<grid_for(n), 256, 0, s>>>(t->b.rule, t->b.count, t->b.count_ge2, n, rule, use_ge2 ? 1 : 0, thr, flag);
+  OH_TRY(exclusive_scan_u32(ctx, flag, idx, n, tot, s));
+  uint64_t m = 0;
+  OH_TRY(d2h(&m, tot, 1, s));
+  if (m == 0) return 0;
+  uint32_t *sa, *sb, *sc, *k0, *v0, *k1, *v1;
+  OH_TRY(ws.get("fin_sa", (size_t)m, &sa));
+  OH_TRY(ws.get("fin_sb", (size_t)m, &sb));
+  OH_TRY(ws.get("fin_sc", (size_t)m, &sc));
+  OH_TRY(ws.get("fin_k0", (size_t)m, &k0));
+  OH_TRY(ws.get("fin_v0", (size_t)m, &v0));
+  OH_TRY(ws.get("fin_k1", (size_t)m, &k1));
+  OH_TRY(ws.get("fin_v1", (size_t)m, &v1));
+  k_fin_compact<<<grid_for(n), 256, 0, s>>>(flag, idx, n, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2,
+                                            use_ge2 ? 1 : 0, sa, sb, sc);
+  // LSD: aid_next asc, then aid asc, then count desc (stable) -> (count desc, aid, aid_next)
+  const int abits = 31;
+  uint32_t *k = k0, *v = v0;
+  k_iota_key<<<grid_for((int64_t)m), 256, 0, s>>>(sb, (int64_t)m, k, v);
+  OH_TRY(radix_sort_pairs(ctx, k, v, k == k0 ? k1 : k0, v == v0 ? v1 : v0, (int64_t)m, abits, s));
+  uint32_t* kn = (k == k0) ? k1 : k0;
+  k_gather_key<<<grid_for((int64_t)m), 256, 0, s>>>(sa, v, (int64_t)m, 0, kn);
+  k = kn;
+  OH_TRY(radix_sort_pairs(ctx, k, v, k == k0 ? k1 : k0, v == v0 ? v1 : v0, (int64_t)m, abits, s));
+  kn = (k == k0) ? k1 : k0;
+  k_gather_key<<<grid_for((int64_t)m), 256, 0, s>>>(sc, v, (int64_t)m, 1, kn);
+  k = kn;
+  OH_TRY(radix_sort_pairs(ctx, k, v, k == k0 ? k1 : k0, v == v0 ? v1 : v0, (int64_t)m, 32, s));
+  const int64_t keep = std::min<int64_t>((int64_t)m, mp->max_rows);
+  k_fin_out<<<grid_for(keep), 256, 0, s>>>(v, keep, sa, sb, sc, aid, aid_next, count);
+  OH_HIP(hipGetLastError());
+  *n_out = keep;
+  return 0;
+}

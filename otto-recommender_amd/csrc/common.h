@@ -1,0 +1,142 @@
+// Shared host/device helpers for libottohip.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+#include <map>
+
+#include "ottohip.h"
+
+namespace ottohip {
+
+void set_error(const char* fmt, ...);
+
+#define OH_HIP(expr)                                                              \
+  do {                                                                            \
+    hipError_t e_ = (expr);                                                       \
+    if (e_ != hipSuccess) {                                                       \
+      ::ottohip::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #expr,           \
+                           hipGetErrorString(e_));                                \
+      return e_ == hipErrorOutOfMemory ? OTTOHIP_ENOMEM : OTTOHIP_EHIP;           \
+    }                                                                             \
+  } while (0)
+
+#define OH_TRY(expr)                 \
+  do {                               \
+    int rc_ = (expr);                \
+    if (rc_ != 0) return rc_;        \
+  } while (0)
+
+// Named, grow-only device buffers owned by a context (no allocation inside launches).
+struct Workspace {
+  struct Buf { void* p = nullptr; size_t bytes = 0; };
+  std::map<std::string, Buf> bufs;
+  int get(const char* name, size_t bytes, void** out) {
+    Buf& b = bufs[name];
+    if (b.bytes < bytes) {
+      if (b.p) { (void)hipDeviceSynchronize(); (void)hipFree(b.p); b.p = nullptr; b.bytes = 0; }
+      size_t want = bytes < 256 ? 256 : bytes;
+      hipError_t e = hipMalloc(&b.p, want);
+      if (e != hipSuccess) {
+        set_error("workspace '%s': hipMalloc(%zu) failed: %s", name, want, hipGetErrorString(e));
+        return OTTOHIP_ENOMEM;
+      }
+      b.bytes = want;
+    }
+    *out = b.p;
+    return 0;
+  }
+  template <class T> int get(const char* name, size_t n, T** out) {
+    return get(name, n * sizeof(T), reinterpret_cast<void**>(out));
+  }
+  void release() {
+    for (auto& kv : bufs) if (kv.second.p) hipFree(kv.second.p);
+    bufs.clear();
+  }
+};
+
+struct Phase { std::string name; hipEvent_t a, b; double bytes; };
+
+struct Ctx {
+  int device = 0;
+  int n_cu = 256;
+  Workspace ws;
+  uint64_t* pinned = nullptr;   // small host staging for D2H scalars
+  bool timing = false;
+  std::vector<Phase> phases;
+  std::vector<hipEvent_t> event_pool;
+  size_t event_used = 0;
+  hipEvent_t take_event() {
+    if (event_used == event_pool.size()) {
+      hipEvent_t e; hipEventCreate(&e); event_pool.push_back(e);
+    }
+    return event_pool[event_used++];
+  }
+  void reset_timing() { phases.clear(); event_used = 0; }
+  // open a named phase on the stream (no-op unless timing is enabled)
+  int begin(const char* name, hipStream_t s, double bytes = 0) {
+    if (!timing) return -1;
+    Phase p; p.name = name; p.a = take_event(); p.b = take_event(); p.bytes = bytes;
+    hipEventRecord(p.a, s);
+    phases.push_back(p);
+    return (int)phases.size() - 1;
+  }
+  void end(int id, hipStream_t s) { if (id >= 0) hipEventRecord(phases[id].b, s); }
+};
+
+inline int bits_for(uint64_t n_values) {  // bits needed to store values in [0, n_values)
+  int b = 0;
+  while (b < 64 && (uint64_t(1) << b) < n_values) ++b;
+  return b;
+}
+__host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ---------------------------------------------------------------- device helpers
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {  // popcount of m below this lane
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+  uint32_t lo = __shfl((uint32_t)v, src), hi = __shfl((uint32_t)(v >> 32), src);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  const uint32_t l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t t = __shfl_up(v, d);
+    if (l >= (uint32_t)d) v += t;
+  }
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v) {
+  const uint32_t l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t lo = __shfl_up((uint32_t)v, d), hi = __shfl_up((uint32_t)(v >> 32), d);
+    uint64_t t = ((uint64_t)hi << 32) | lo;
+    if (l >= (uint32_t)d) v += t;
+  }
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+  return v;
+}
+
+// Packed event: high 32 = ts ^ 0x80000000 (orders like signed ts), low 32 = aid << 2 | type.
+// Sorting packed events ascending orders a session by (ts, aid, type); equal words are the
+// exact duplicates removed by df.unique() (model/count_co_events.py:92).
+constexpr uint64_t EV_INVALID = ~uint64_t(0);
+__device__ __forceinline__ uint64_t ev_pack(int32_t aid, int32_t ts, int32_t type) {
+  return ((uint64_t)((uint32_t)ts ^ 0x80000000u) << 32) | ((uint32_t)aid << 2) | (uint32_t)type;
+}
+__device__ __forceinline__ int32_t ev_ts(uint64_t e) { return (int32_t)((uint32_t)(e >> 32) ^ 0x80000000u); }
+__device__ __forceinline__ int32_t ev_aid(uint64_t e) { return (int32_t)(((uint32_t)e) >> 2); }
+__device__ __forceinline__ int32_t ev_type(uint64_t e) { return (int32_t)(e & 3u); }
+
+}  // namespace ottohip

@@ -1,0 +1,807 @@
+// Co-visitation counting kernels for gfx950 (included once, by abi.hip) (model/count_co_events.py:17-100, :168).
+//
+// Pipeline (DESIGN.md §3 has the data layout and byte model):
+//   S1 prep     wave per block of sessions: pack (ts, aid, type) into u64, sort each session
+//               in LDS, drop exact duplicates (df.unique(), :92)
+//   S2 count    wave per block of sessions: per event i and rule r, the number of partners j
+//               in the session window (binary search on ts + per-type prefix counts in LDS);
+//               row key = (type_i, aid_i)
+//   S3 rows     stable LSD radix sort of events by row key; exclusive scan of counts gives
+//               each event its run of output words: rows (aid-major) are contiguous
+//   S4 emit     wave per block of sessions, 16-lane subgroups per event: write one u32 word
+//               (rule | aid_next | file) per qualifying pair at its row position
+//   S5 reduce   rows <= 64 words: one wave; <= 2048 words: one workgroup, two-phase LDS hash
+//               (per-file counts, then folded over files); larger rows: MSD split by the
+//               word's top bits (256-way) until buckets fit
+// Output: per (rule, aid, aid_next): count (sum over files), count_ge2 (sum of per-file
+// counts >= 2) and per-rule file-row statistics for the merge rule of :131-135.
+#pragma once
+#include "prims.h"
+
+namespace ottohip {
+
+constexpr int MAX_RULES = 8;
+constexpr int EV_BLOCK = 256;     // events per wave block (sessions starting in it)
+constexpr int LCAP = 512;         // sessions up to LCAP events run from LDS
+constexpr int TINY = 64;          // rows/buckets up to TINY words: one wave
+constexpr int SMALL = 2048;       // up to SMALL words: one workgroup hash
+constexpr int HASH_REM = 11;      // buckets whose remaining key bits <= 11 hash directly
+constexpr uint32_t W_EMPTY = 0xFFFFFFFFu;
+
+struct RulesDev {
+  int32_t lo[MAX_RULES], hi[MAX_RULES];    // window on dt = ts_j - ts_i, inclusive
+  uint32_t mask[MAX_RULES];                // allowed next types
+  int32_t n_of_type[4];                    // rules whose this_type == t
+  int32_t rule_of_type[4][MAX_RULES];      // global rule id per (t, local index)
+};
+
+struct Layout {
+  int A;      // aid bits
+  int F;      // file bits
+  int BR;     // local rule bits
+  int WB;     // word bits = BR + A + F
+  uint32_t amask;
+};
+
+struct Task {
+  uint64_t begin;
+  uint32_t len;
+  uint32_t row;
+  uint32_t rem;   // key bits not yet used for splitting (from the top)
+  uint32_t buf;   // which word buffer holds it
+};
+
+struct OutRows {
+  uint8_t* rule;
+  int32_t* aid;
+  int32_t* aid_next;
+  uint32_t* count;
+  uint32_t* count_ge2;
+  unsigned long long* cursor;
+  uint64_t cap;
+  unsigned long long* stats;  // [MAX_RULES][4]: rows, pairs, file_rows, file_rows_ge2
+};
+
+// ------------------------------------------------------------------ block maps
+__global__ void k_block_first(const int64_t* __restrict__ off, int64_t S, int64_t NB,
+                              int64_t* __restrict__ first, int32_t* __restrict__ long_list,
+                              int32_t* __restrict__ n_long) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > S) return;
+  const int64_t lo = s == 0 ? 0 : off[s - 1] / EV_BLOCK + 1;
+  const int64_t hi = s == S ? NB : off[s] / EV_BLOCK;
+  for (int64_t b = lo; b <= hi && b <= NB; ++b) first[b] = s;
+  if (s < S && off[s + 1] - off[s] > LCAP) {
+    int k = atomicAdd(n_long, 1);
+    long_list[k] = (int32_t)s;
+  }
+}
+
+__device__ __forceinline__ int file_of(const int64_t* fb, int nf, int64_t s) {
+  int lo = 0, hi = nf;  // largest f with fb[f] <= s
+  while (hi - lo > 1) {
+    int m = (lo + hi) >> 1;
+    if (fb[m] <= s) lo = m; else hi = m;
+  }
+  return lo;
+}
+
+// ------------------------------------------------------------------ S1 prep
+// Sort one session (n events) by packed key and compact distinct keys into out[0..);
+// the tail [n_kept, n) is set to EV_INVALID. Executed by one wave.
+__device__ __forceinline__ void prep_session(const int32_t* __restrict__ aid, const int32_t* __restrict__ ts,
+                                             const int8_t* __restrict__ ty, int64_t e0, int n,
+                                             uint64_t* keys, uint64_t* sorted, uint64_t* __restrict__ out,
+                                             int n_items, int dedup, int* err) {
+  const int l = lane_id();
+  for (int k = l; k < n; k += 64) {
+    const int32_t a = aid[e0 + k], t = ts[e0 + k], y = ty[e0 + k];
+    if (a < 0 || a >= n_items || y < 0 || y > 2) atomicOr(err, 1);
+    keys[k] = ev_pack(a < 0 ? 0 : a, t, y & 3);
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  for (int k = l; k < n; k += 64) {
+    const uint64_t v = keys[k];
+    int r = 0;
+    for (int j = 0; j < n; ++j) {
+      const uint64_t u = keys[j];
+      r += (u < v) | ((u == v) & (j < k));
+    }
+    sorted[r] = v;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  int base = 0;
+  for (int k0 = 0; k0 < n; k0 += 64) {
+    const int k = k0 + l;
+    const uint64_t v = k < n ? sorted[k] : EV_INVALID;
+    const bool keep = k < n && (!dedup || k == 0 || sorted[k - 1] != v);
+    const uint64_t m = __ballot(keep);
+    if (keep) out[base + (int)mbcnt(m)] = v;
+    base += (int)__popcll(m);
+  }
+  for (int k = base + l; k < n; k += 64) out[k] = EV_INVALID;
+}
+
+__global__ __launch_bounds__(256) void k_prep(const int64_t* __restrict__ off, const int64_t* __restrict__ first,
+                                              int64_t NB, const int32_t* __restrict__ aid,
+                                              const int32_t* __restrict__ ts, const int8_t* __restrict__ ty,
+                                              uint64_t* __restrict__ ev, int n_items, int dedup, int* err) {
+  __shared__ uint64_t sh[4][2][LCAP];
+  const int w = threadIdx.x >> 6;
+  const int64_t g = (int64_t)blockIdx.x * 4 + w;
+  if (g >= NB) return;
+  const int64_t s0 = first[g], s1 = first[g + 1];
+  for (int64_t s = s0; s < s1; ++s) {
+    const int64_t e0 = off[s];
+    const int n = (int)(off[s + 1] - e0);
+    if (n > LCAP || n == 0) continue;
+    prep_session(aid, ts, ty, e0, n, sh[w][0], sh[w][1], ev + e0, n_items, dedup, err);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+__global__ __launch_bounds__(64) void k_prep_long(const int64_t* __restrict__ off, const int32_t* __restrict__ list,
+                                                  const int64_t* __restrict__ scratch_off,
+                                                  uint64_t* __restrict__ scratch, const int32_t* __restrict__ aid,
+                                                  const int32_t* __restrict__ ts, const int8_t* __restrict__ ty,
+                                                  uint64_t* __restrict__ ev, int n_items, int dedup, int* err) {
+  const int64_t s = list[blockIdx.x];
+  const int64_t e0 = off[s];
+  const int n = (int)(off[s + 1] - e0);
+  uint64_t* keys = scratch + 2 * scratch_off[blockIdx.x];
+  prep_session(aid, ts, ty, e0, n, keys, keys + n, ev + e0, n_items, dedup, err);
+}
+
+// ------------------------------------------------------------------ S2 count
+struct SessView {
+  const uint64_t* ev;   // sorted valid events [0, nv)
+  int nv;
+  const uint32_t* pref; // pref[t * (cap+1) + k]: events of type t among [0, k)
+  int pstride;
+};
+
+// load a session into LDS/global scratch and build per-type exclusive prefix counts
+__device__ __forceinline__ int load_session(const uint64_t* __restrict__ src, int n, uint64_t* evs,
+                                            uint32_t* pref, int pstride) {
+  const int l = lane_id();
+  int nv = 0;
+  uint32_t base0 = 0, base1 = 0, base2 = 0;
+  for (int k0 = 0; k0 < n; k0 += 64) {
+    const int k = k0 + l;
+    const uint64_t v = k < n ? src[k] : EV_INVALID;
+    if (k < n) evs[k] = v;
+    const bool valid = v != EV_INVALID;
+    const int t = (int)(v & 3u);
+    const uint64_t m0 = __ballot(valid && t == 0), m1 = __ballot(valid && t == 1), m2 = __ballot(valid && t == 2);
+    if (k < n) {
+      pref[0 * pstride + k] = base0 + mbcnt(m0);
+      pref[1 * pstride + k] = base1 + mbcnt(m1);
+      pref[2 * pstride + k] = base2 + mbcnt(m2);
+    }
+    base0 += (uint32_t)__popcll(m0); base1 += (uint32_t)__popcll(m1); base2 += (uint32_t)__popcll(m2);
+    nv += (int)__popcll(__ballot(valid));
+  }
+  if (l == 0) {  // pref[t][nv] = totals (invalid slots carry no types, so totals at n == at nv)
+    pref[0 * pstride + nv] = base0; pref[1 * pstride + nv] = base1; pref[2 * pstride + nv] = base2;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  return nv;
+}
+
+__device__ __forceinline__ int lower_ts(const uint64_t* evs, int nv, int64_t x) {  // first k: ts_k >= x
+  int lo = 0, hi = nv;
+  while (lo < hi) {
+    const int m = (lo + hi) >> 1;
+    if ((int64_t)ev_ts(evs[m]) < x) lo = m + 1; else hi = m;
+  }
+  return lo;
+}
+__device__ __forceinline__ int upper_ts(const uint64_t* evs, int nv, int64_t x) {  // first k: ts_k > x
+  int lo = 0, hi = nv;
+  while (lo < hi) {
+    const int m = (lo + hi) >> 1;
+    if ((int64_t)ev_ts(evs[m]) <= x) lo = m + 1; else hi = m;
+  }
+  return lo;
+}
+
+// number of events identical to evs[i] (adjacent in sorted order); 1 after dedup
+__device__ __forceinline__ int equal_run(const uint64_t* evs, int nv, int i) {
+  const uint64_t v = evs[i];
+  int a = i, b = i + 1;
+  while (a > 0 && evs[a - 1] == v) --a;
+  while (b < nv && evs[b] == v) ++b;
+  return b - a;
+}
+
+__device__ __forceinline__ uint32_t count_event(const SessView& S, int i, const RulesDev& R) {
+  const uint64_t e = S.ev[i];
+  const int t = ev_type(e);
+  const int64_t tsi = ev_ts(e);
+  uint32_t c = 0;
+  int run = -1;
+  for (int q = 0; q < R.n_of_type[t]; ++q) {
+    const int r = R.rule_of_type[t][q];
+    const int jb = lower_ts(S.ev, S.nv, tsi + R.lo[r]);
+    const int je = upper_ts(S.ev, S.nv, tsi + R.hi[r]);
+    if (je <= jb) continue;
+    uint32_t m = 0;
+    for (int tt = 0; tt < 3; ++tt)
+      if ((R.mask[r] >> tt) & 1u) m += S.pref[tt * S.pstride + je] - S.pref[tt * S.pstride + jb];
+    if (((R.mask[r] >> t) & 1u) && R.lo[r] <= 0 && R.hi[r] >= 0) {
+      if (run < 0) run = equal_run(S.ev, S.nv, i);
+      m -= (uint32_t)run;  // the identity row of :23-27 (and exact twins when dedup is off)
+    }
+    c += m;
+  }
+  return c;
+}
+
+__device__ __forceinline__ void count_session(const SessView& S, int64_t e0, int n, const RulesDev& R, int A,
+                                              uint32_t* __restrict__ cnt, uint32_t* __restrict__ rk,
+                                              uint32_t* __restrict__ pos) {
+  const uint32_t INV = 3u << A;
+  for (int k = lane_id(); k < n; k += 64) {
+    uint32_t c = 0, key = INV;
+    if (k < S.nv) {
+      c = count_event(S, k, R);
+      if (c) { const uint64_t e = S.ev[k]; key = ((uint32_t)ev_type(e) << A) | (uint32_t)ev_aid(e); }
+    }
+    cnt[e0 + k] = c;
+    rk[e0 + k] = key;
+    pos[e0 + k] = (uint32_t)(e0 + k);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_count(const int64_t* __restrict__ off, const int64_t* __restrict__ first,
+                                               int64_t NB, const uint64_t* __restrict__ ev, RulesDev R, int A,
+                                               uint32_t* __restrict__ cnt, uint32_t* __restrict__ rk,
+                                               uint32_t* __restrict__ pos) {
+  __shared__ uint64_t sev[4][LCAP];
+  __shared__ uint32_t spref[4][3 * (LCAP + 1)];
+  const int w = threadIdx.x >> 6;
+  const int64_t g = (int64_t)blockIdx.x * 4 + w;
+  if (g >= NB) return;
+  for (int64_t s = first[g]; s < first[g + 1]; ++s) {
+    const int64_t e0 = off[s];
+    const int n = (int)(off[s + 1] - e0);
+    if (n > LCAP || n == 0) continue;
+    SessView S;
+    S.ev = sev[w]; S.pref = spref[w]; S.pstride = LCAP + 1;
+    S.nv = load_session(ev + e0, n, sev[w], spref[w], LCAP + 1);
+    count_session(S, e0, n, R, A, cnt, rk, pos);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+__global__ __launch_bounds__(64) void k_count_long(const int64_t* __restrict__ off, const int32_t* __restrict__ list,
+                                                   const int64_t* __restrict__ scratch_off,
+                                                   uint64_t* __restrict__ scratch, uint32_t* __restrict__ pscratch,
+                                                   const uint64_t* __restrict__ ev, RulesDev R, int A,
+                                                   uint32_t* __restrict__ cnt, uint32_t* __restrict__ rk,
+                                                   uint32_t* __restrict__ pos) {
+  const int64_t s = list[blockIdx.x];
+  const int64_t e0 = off[s];
+  const int n = (int)(off[s + 1] - e0);
+  const int64_t so = scratch_off[blockIdx.x];
+  SessView S;
+  uint64_t* evs = scratch + 2 * so;
+  uint32_t* pref = pscratch + 3 * (so + blockIdx.x);
+  S.ev = evs; S.pref = pref; S.pstride = n + 1;
+  S.nv = load_session(ev + e0, n, evs, pref, n + 1);
+  count_session(S, e0, n, R, A, cnt, rk, pos);
+}
+
+// ------------------------------------------------------------------ S3 rows
+__global__ void k_gather_counts(const uint32_t* __restrict__ rk, const uint32_t* __restrict__ pos,
+                                const uint32_t* __restrict__ cnt, int64_t n, uint32_t INV,
+                                uint32_t* __restrict__ c_sorted, uint32_t* __restrict__ row_flag) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t key = rk[k];
+  const bool valid = key != INV;
+  c_sorted[k] = valid ? cnt[pos[k]] : 0u;
+  row_flag[k] = valid && (k == 0 || rk[k - 1] != key);
+}
+
+__global__ void k_rows(const uint32_t* __restrict__ rk, const uint32_t* __restrict__ pos, int64_t n, uint32_t INV,
+                       const uint64_t* __restrict__ woff, const uint32_t* __restrict__ row_flag,
+                       const uint64_t* __restrict__ row_idx, uint64_t* __restrict__ poff,
+                       uint32_t* __restrict__ row_key, uint64_t* __restrict__ row_begin) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t key = rk[k];
+  if (key == INV) return;
+  poff[pos[k]] = woff[k];
+  if (row_flag[k]) {
+    const uint64_t r = row_idx[k];
+    row_key[r] = key;
+    row_begin[r] = woff[k];
+  }
+}
+
+// ------------------------------------------------------------------ S4 emit
+__device__ __forceinline__ void emit_session(const SessView& S, int64_t e0, const RulesDev& R, const Layout& L,
+                                             uint32_t file, const uint32_t* __restrict__ cnt,
+                                             const uint64_t* __restrict__ poff, uint32_t* __restrict__ words) {
+  const int l = lane_id();
+  const int sg = l >> 4, sl = l & 15;
+  const int shiftR = L.A + L.F;
+  for (int i0 = 0; i0 < S.nv; i0 += 4) {
+    const int i = i0 + sg;
+    bool active = i < S.nv && cnt[e0 + i] != 0u;
+    uint64_t out = active ? poff[e0 + i] : 0;
+    const uint64_t e = active ? S.ev[i] : 0;
+    const int t = ev_type(e);
+    const int64_t tsi = ev_ts(e);
+    const int nr = active ? R.n_of_type[t] : 0;
+    for (int q = 0; q < nr; ++q) {
+      const int r = R.rule_of_type[t][q];
+      const int jb = lower_ts(S.ev, S.nv, tsi + R.lo[r]);
+      const int je = upper_ts(S.ev, S.nv, tsi + R.hi[r]);
+      const uint32_t hi = ((uint32_t)q << shiftR) | file;
+      for (int j0 = jb; j0 < je; j0 += 16) {
+        const int j = j0 + sl;
+        bool match = false;
+        uint32_t word = 0;
+        if (j < je) {
+          const uint64_t ej = S.ev[j];
+          match = ej != e && ((R.mask[r] >> ev_type(ej)) & 1u);
+          word = hi | ((uint32_t)ev_aid(ej) << L.F);
+        }
+        const uint32_t bal = (uint32_t)(__ballot(match) >> (sg * 16)) & 0xFFFFu;
+        if (match) words[out + (uint64_t)__popc(bal & ((1u << sl) - 1u))] = word;
+        out += (uint64_t)__popc(bal);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_emit(const int64_t* __restrict__ off, const int64_t* __restrict__ first,
+                                              int64_t NB, const uint64_t* __restrict__ ev, RulesDev R, Layout L,
+                                              const int64_t* __restrict__ fb, int nf,
+                                              const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ poff,
+                                              uint32_t* __restrict__ words) {
+  __shared__ uint64_t sev[4][LCAP];
+  __shared__ uint32_t spref[4][3 * (LCAP + 1)];
+  const int w = threadIdx.x >> 6;
+  const int64_t g = (int64_t)blockIdx.x * 4 + w;
+  if (g >= NB) return;
+  const int64_t s0 = first[g], s1 = first[g + 1];
+  if (s0 >= s1) return;
+  int f = file_of(fb, nf, s0);
+  for (int64_t s = s0; s < s1; ++s) {
+    while (f + 1 < nf && fb[f + 1] <= s) ++f;
+    const int64_t e0 = off[s];
+    const int n = (int)(off[s + 1] - e0);
+    if (n > LCAP || n == 0) continue;
+    SessView S;
+    S.ev = sev[w]; S.pref = spref[w]; S.pstride = LCAP + 1;
+    S.nv = load_session(ev + e0, n, sev[w], spref[w], LCAP + 1);
+    emit_session(S, e0, R, L, (uint32_t)f, cnt, poff, words);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+__global__ __launch_bounds__(64) void k_emit_long(const int64_t* __restrict__ off, const int32_t* __restrict__ list,
+                                                  const int64_t* __restrict__ scratch_off,
+                                                  uint64_t* __restrict__ scratch, uint32_t* __restrict__ pscratch,
+                                                  const uint64_t* __restrict__ ev, RulesDev R, Layout L,
+                                                  const int64_t* __restrict__ fb, int nf,
+                                                  const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ poff,
+                                                  uint32_t* __restrict__ words) {
+  const int64_t s = list[blockIdx.x];
+  const int64_t e0 = off[s];
+  const int n = (int)(off[s + 1] - e0);
+  const int64_t so = scratch_off[blockIdx.x];
+  SessView S;
+  uint64_t* evs = scratch + 2 * so;
+  uint32_t* pref = pscratch + 3 * (so + blockIdx.x);
+  S.ev = evs; S.pref = pref; S.pstride = n + 1;
+  S.nv = load_session(ev + e0, n, evs, pref, n + 1);
+  emit_session(S, e0, R, L, (uint32_t)file_of(fb, nf, s), cnt, poff, words);
+}
+
+// ------------------------------------------------------------------ S5 reduce
+__device__ __forceinline__ uint32_t hslot(uint32_t w, uint32_t mask) { return (w * 0x9E3779B1u >> 7) & mask; }
+
+// row (type, aid) -> global rule id and output fields
+struct RowInfo { int type; int32_t aid; };
+__device__ __forceinline__ RowInfo row_info(const uint32_t* row_key, uint32_t row, int A) {
+  const uint32_t k = row_key[row];
+  RowInfo ri; ri.type = (int)(k >> A); ri.aid = (int32_t)(k & ((1u << A) - 1u));
+  return ri;
+}
+
+__device__ __forceinline__ void put_row(const OutRows& O, uint64_t p, int rule, int32_t aid, int32_t next,
+                                        uint32_t c, uint32_t c2) {
+  if (p < O.cap) {
+    O.rule[p] = (uint8_t)rule; O.aid[p] = aid; O.aid_next[p] = next; O.count[p] = c; O.count_ge2[p] = c2;
+  }
+}
+
+// one wave per task with len <= 64
+__global__ __launch_bounds__(256) void k_agg_tiny(const Task* __restrict__ tasks, int64_t n_tasks,
+                                                  const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
+                                                  const uint32_t* __restrict__ row_key, RulesDev R, Layout L,
+                                                  OutRows O) {
+  const int l = lane_id();
+  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  unsigned long long st[MAX_RULES][4];
+  for (int r = 0; r < MAX_RULES; ++r) for (int k = 0; k < 4; ++k) st[r][k] = 0;
+  const uint32_t fmask = (1u << L.F) - 1u;
+  for (int64_t ti = gw; ti < n_tasks; ti += nw) {
+    const Task T = tasks[ti];
+    const uint32_t* W = T.buf ? w1 : w0;
+    const uint32_t w = l < (int)T.len ? W[T.begin + l] : W_EMPTY;
+    // per-file count of this word and first-occurrence flag
+    uint32_t cf = 0; bool first = true;
+    for (int j = 0; j < (int)T.len; ++j) {
+      const uint32_t u = __shfl(w, j);
+      cf += u == w;
+      first &= !(u == w && j < l);
+    }
+    const uint32_t k2 = w >> L.F;
+    uint32_t call = 0, c2 = 0, nf1 = 0, nf2 = 0; bool firstk = true;
+    for (int j = 0; j < (int)T.len; ++j) {
+      const uint32_t u = __shfl(w, j);
+      const bool fj = __shfl((int)first, j);
+      const uint32_t cj = __shfl(cf, j);
+      if (fj && (u >> L.F) == k2) {
+        call += cj; c2 += cj >= 2 ? cj : 0; nf1 += 1; nf2 += cj >= 2;
+        firstk &= !(j < l);
+      }
+    }
+    const bool emit = l < (int)T.len && first && firstk;
+    const uint64_t m = __ballot(emit);
+    unsigned long long base = 0;
+    if (l == 0) base = atomicAdd(O.cursor, (unsigned long long)__popcll(m));
+    base = __shfl(base, 0);
+    const RowInfo ri = row_info(row_key, T.row, L.A);
+    const int ql = (int)(k2 >> L.A);
+    if (emit) {
+      const int rule = R.rule_of_type[ri.type][ql];
+      put_row(O, base + mbcnt(m), rule, ri.aid, (int32_t)(k2 & L.amask), call, c2);
+      (void)fmask;
+    }
+    for (int q = 0; q < R.n_of_type[ri.type]; ++q) {
+      const bool mine = emit && ql == q;
+      const uint32_t a0 = wave_sum(mine ? 1u : 0u), a1 = wave_sum(mine ? call : 0u);
+      const uint32_t a2 = wave_sum(mine ? nf1 : 0u), a3 = wave_sum(mine ? nf2 : 0u);
+      const int rule = R.rule_of_type[ri.type][q];
+      st[rule][0] += a0; st[rule][1] += a1; st[rule][2] += a2; st[rule][3] += a3;
+    }
+  }
+  if (l == 0)
+    for (int r = 0; r < MAX_RULES; ++r)
+      for (int k = 0; k < 4; ++k)
+        if (st[r][k]) atomicAdd(&O.stats[r * 4 + k], st[r][k]);
+}
+
+// one workgroup per task: LDS hash of (rule|aid_next|file) counts, then folded over files
+constexpr int AGG_T = 256;
+constexpr int HCAP = 4096;
+__global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tasks, int64_t n_tasks,
+                                                    const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
+                                                    const uint32_t* __restrict__ row_key, RulesDev R, Layout L,
+                                                    OutRows O) {
+  __shared__ uint32_t lds[4 * HCAP];  // 64 KiB: phase A uses [0, 2cap), phase B [0, 4cap)
+  __shared__ unsigned long long sstat[MAX_RULES][4];
+  __shared__ uint32_t sbase[2];
+  __shared__ uint32_t wtot[AGG_T / 64];
+  const int tid = threadIdx.x;
+  for (int64_t ti = blockIdx.x; ti < n_tasks; ti += gridDim.x) {
+    const Task T = tasks[ti];
+    const uint32_t* W = (T.buf ? w1 : w0) + T.begin;
+    uint32_t dbound = T.len;
+    if (T.rem < 31 && (1u << T.rem) < dbound) dbound = 1u << T.rem;
+    uint32_t cap = 64;
+    while (cap < 2 * dbound) cap <<= 1;
+    const uint32_t cm = cap - 1;
+    uint32_t* keyA = lds;
+    uint32_t* cntA = lds + cap;
+    for (uint32_t i = tid; i < cap; i += AGG_T) { keyA[i] = W_EMPTY; cntA[i] = 0; }
+    if (tid < MAX_RULES * 4) (&sstat[0][0])[tid] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < T.len; i += AGG_T) {
+      const uint32_t w = W[i];
+      uint32_t h = hslot(w, cm);
+      while (true) {
+        const uint32_t prev = atomicCAS(&keyA[h], W_EMPTY, w);
+        if (prev == W_EMPTY || prev == w) { atomicAdd(&cntA[h], 1u); break; }
+        h = (h + 1) & cm;
+      }
+    }
+    __syncthreads();
+    constexpr int SL = HCAP / AGG_T;  // 16 slots per thread at most
+    uint32_t kw[SL], kc[SL];
+#pragma unroll
+    for (int s = 0; s < SL; ++s) {
+      const uint32_t slot = tid + s * AGG_T;
+      kw[s] = slot < cap ? keyA[slot] : W_EMPTY;
+      kc[s] = slot < cap ? cntA[slot] : 0;
+    }
+    __syncthreads();
+    uint32_t* keyB = lds;
+    uint32_t* cB = lds + cap;
+    uint32_t* c2B = lds + 2 * cap;
+    uint32_t* nfB = lds + 3 * cap;
+    for (uint32_t i = tid; i < cap; i += AGG_T) { keyB[i] = W_EMPTY; cB[i] = 0; c2B[i] = 0; nfB[i] = 0; }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < SL; ++s) {
+      if (kw[s] == W_EMPTY) continue;
+      const uint32_t k2 = kw[s] >> L.F;
+      const uint32_t c = kc[s];
+      uint32_t h = hslot(k2, cm);
+      while (true) {
+        const uint32_t prev = atomicCAS(&keyB[h], W_EMPTY, k2);
+        if (prev == W_EMPTY || prev == k2) break;
+        h = (h + 1) & cm;
+      }
+      atomicAdd(&cB[h], c);
+      if (c >= 2) atomicAdd(&c2B[h], c);
+      atomicAdd(&nfB[h], 1u | ((c >= 2 ? 1u : 0u) << 16));
+    }
+    __syncthreads();
+    // compact and write
+    const RowInfo ri = row_info(row_key, T.row, L.A);
+    uint32_t mine = 0;
+    for (uint32_t i = tid; i < cap; i += AGG_T) mine += keyB[i] != W_EMPTY;
+    const uint32_t incl = wave_incl_scan(mine);
+    if ((tid & 63) == 63) wtot[tid >> 6] = incl;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+    for (int k = 0; k < AGG_T / 64; ++k) { if (k < (tid >> 6)) pre += wtot[k]; tot += wtot[k]; }
+    if (tid == 0) {
+      const unsigned long long b = atomicAdd(O.cursor, (unsigned long long)tot);
+      sbase[0] = (uint32_t)b; sbase[1] = (uint32_t)(b >> 32);
+    }
+    __syncthreads();
+    uint64_t p = (((uint64_t)sbase[1] << 32) | sbase[0]) + pre + incl - mine;
+    for (uint32_t i = tid; i < cap; i += AGG_T) {
+      const uint32_t k2 = keyB[i];
+      if (k2 == W_EMPTY) continue;
+      const int q = (int)(k2 >> L.A);
+      const int rule = R.rule_of_type[ri.type][q];
+      const uint32_t nf = nfB[i];
+      put_row(O, p++, rule, ri.aid, (int32_t)(k2 & L.amask), cB[i], c2B[i]);
+      atomicAdd(&sstat[rule][0], 1ull);
+      atomicAdd(&sstat[rule][1], (unsigned long long)cB[i]);
+      atomicAdd(&sstat[rule][2], (unsigned long long)(nf & 0xFFFFu));
+      atomicAdd(&sstat[rule][3], (unsigned long long)(nf >> 16));
+    }
+    __syncthreads();
+    if (tid < MAX_RULES * 4) {
+      const unsigned long long v = (&sstat[0][0])[tid];
+      if (v) atomicAdd(&O.stats[tid], v);
+    }
+    __syncthreads();
+  }
+}
+
+// ---- classification of rows and split buckets into task lists
+struct TaskLists {
+  Task* tiny; Task* hash; Task* split;
+  unsigned long long* n;  // [3]
+  uint64_t cap_tiny, cap_hash, cap_split;
+};
+
+__device__ __forceinline__ void push_task(const TaskLists& TL, uint64_t begin, uint64_t len, uint32_t row,
+                                          uint32_t rem, uint32_t buf, int* err) {
+  if (len == 0) return;
+  Task t; t.begin = begin; t.len = (uint32_t)len; t.row = row; t.rem = rem; t.buf = buf;
+  if (len > 0xFFFFFFFFull) { atomicOr(err, 2); return; }
+  if (len <= (uint64_t)TINY) {
+    const unsigned long long k = atomicAdd(&TL.n[0], 1ull);
+    if (k < TL.cap_tiny) TL.tiny[k] = t; else atomicOr(err, 4);
+  } else if (len <= (uint64_t)SMALL || rem <= (uint32_t)HASH_REM) {
+    const unsigned long long k = atomicAdd(&TL.n[1], 1ull);
+    if (k < TL.cap_hash) TL.hash[k] = t; else atomicOr(err, 4);
+  } else {
+    const unsigned long long k = atomicAdd(&TL.n[2], 1ull);
+    if (k < TL.cap_split) TL.split[k] = t; else atomicOr(err, 4);
+  }
+}
+
+__global__ void k_classify_rows(const uint64_t* __restrict__ row_begin, int64_t R, uint64_t P, int WB,
+                                TaskLists TL, int* err) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const uint64_t b = row_begin[r];
+  const uint64_t e = r + 1 < R ? row_begin[r + 1] : P;
+  push_task(TL, b, e - b, (uint32_t)r, (uint32_t)WB, 0u, err);
+}
+
+// split: per task k digit bits, chunks of SPLIT_CH words
+constexpr int SPLIT_CH = 16384;
+constexpr int SPLIT_T = 256;
+
+__device__ __forceinline__ int split_bits(const Task& t) {
+  int k = 1;
+  while (k < 8 && ((uint64_t)t.len >> k) > 1024) ++k;
+  if ((uint32_t)k > t.rem) k = (int)t.rem;
+  return k;
+}
+
+__global__ void k_split_prepare(const Task* __restrict__ tasks, int64_t n, uint32_t* __restrict__ nchunks,
+                                uint32_t* __restrict__ ndigits) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  nchunks[i] = (uint32_t)ceil_div((int64_t)tasks[i].len, SPLIT_CH);
+  ndigits[i] = 1u << split_bits(tasks[i]);
+}
+
+__device__ __forceinline__ int64_t find_task(const uint64_t* chunk_base, int64_t n, uint64_t c) {
+  int64_t lo = 0, hi = n;  // largest t with chunk_base[t] <= c
+  while (hi - lo > 1) {
+    const int64_t m = (lo + hi) >> 1;
+    if (chunk_base[m] <= c) lo = m; else hi = m;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(SPLIT_T) void k_split_hist(const Task* __restrict__ tasks, int64_t n,
+                                                        const uint64_t* __restrict__ chunk_base,
+                                                        const uint64_t* __restrict__ digit_base,
+                                                        const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
+                                                        uint32_t* __restrict__ dcount) {
+  __shared__ uint32_t h[256];
+  const int64_t t = find_task(chunk_base, n, blockIdx.x);
+  const Task T = tasks[t];
+  const int k = split_bits(T);
+  const int sh = (int)T.rem - k;
+  const uint32_t dm = (1u << k) - 1u;
+  const uint64_t c0 = (uint64_t)(blockIdx.x - chunk_base[t]) * SPLIT_CH;
+  const uint64_t c1 = c0 + SPLIT_CH < T.len ? c0 + SPLIT_CH : T.len;
+  const uint32_t* W = (T.buf ? w1 : w0) + T.begin;
+  for (int i = threadIdx.x; i < 256; i += SPLIT_T) h[i] = 0;
+  __syncthreads();
+  for (uint64_t i = c0 + threadIdx.x; i < c1; i += SPLIT_T) atomicAdd(&h[(W[i] >> sh) & dm], 1u);
+  __syncthreads();
+  for (int d = threadIdx.x; d <= (int)dm; d += SPLIT_T)
+    if (h[d]) atomicAdd(&dcount[digit_base[t] + d], h[d]);
+}
+
+__global__ void k_split_cursor(const Task* __restrict__ tasks, int64_t n, const uint64_t* __restrict__ digit_base,
+                               const uint64_t* __restrict__ doff, unsigned long long* __restrict__ cur,
+                               int64_t n_digits_total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_digits_total) return;
+  const int64_t t = find_task(digit_base, n, (uint64_t)i);
+  cur[i] = tasks[t].begin + (doff[i] - doff[digit_base[t]]);
+}
+
+constexpr int SUB = 4096;  // scatter sub-tile (staged in LDS in digit order)
+__global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restrict__ tasks, int64_t n,
+                                                           const uint64_t* __restrict__ chunk_base,
+                                                           const uint64_t* __restrict__ digit_base,
+                                                           uint32_t* __restrict__ w0, uint32_t* __restrict__ w1,
+                                                           unsigned long long* __restrict__ cur) {
+  __shared__ uint32_t h[256], st[256], fill[256];
+  __shared__ unsigned long long gb[256];
+  __shared__ uint32_t stage[SUB];
+  __shared__ uint32_t wsum[SPLIT_T / 64];
+  const int64_t t = find_task(chunk_base, n, blockIdx.x);
+  const Task T = tasks[t];
+  const int k = split_bits(T);
+  const int sh = (int)T.rem - k;
+  const uint32_t dm = (1u << k) - 1u;
+  const uint64_t c0 = (uint64_t)(blockIdx.x - chunk_base[t]) * SPLIT_CH;
+  const uint64_t c1 = c0 + SPLIT_CH < T.len ? c0 + SPLIT_CH : T.len;
+  const uint32_t* Win = (T.buf ? w1 : w0) + T.begin;
+  uint32_t* Wout = T.buf ? w0 : w1;
+  const int tid = threadIdx.x;
+  for (uint64_t s0 = c0; s0 < c1; s0 += SUB) {
+    const int m = (int)((c1 - s0) < (uint64_t)SUB ? (c1 - s0) : (uint64_t)SUB);
+    h[tid] = 0; fill[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < m; i += SPLIT_T) atomicAdd(&h[(Win[s0 + i] >> sh) & dm], 1u);
+    __syncthreads();
+    {  // exclusive scan of h over 256 digits -> st; reserve global ranges
+      const uint32_t v = h[tid];
+      const uint32_t incl = wave_incl_scan(v);
+      if ((tid & 63) == 63) wsum[tid >> 6] = incl;
+      __syncthreads();
+      uint32_t pre = 0;
+      for (int q = 0; q < (tid >> 6); ++q) pre += wsum[q];
+      st[tid] = pre + incl - v;
+      if (v) gb[tid] = atomicAdd(&cur[digit_base[t] + tid], (unsigned long long)v);
+    }
+    __syncthreads();
+    for (int i = tid; i < m; i += SPLIT_T) {
+      const uint32_t w = Win[s0 + i];
+      const uint32_t d = (w >> sh) & dm;
+      stage[st[d] + atomicAdd(&fill[d], 1u)] = w;
+    }
+    __syncthreads();
+    for (int p = tid; p < m; p += SPLIT_T) {
+      const uint32_t w = stage[p];
+      const uint32_t d = (w >> sh) & dm;
+      Wout[gb[d] + (p - st[d])] = w;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void k_split_classify(const Task* __restrict__ tasks, int64_t n, const uint64_t* __restrict__ digit_base,
+                                 const uint32_t* __restrict__ dcount, const uint64_t* __restrict__ doff,
+                                 int64_t n_digits_total, TaskLists TL, int* err) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_digits_total) return;
+  const uint32_t c = dcount[i];
+  if (!c) return;
+  const int64_t t = find_task(digit_base, n, (uint64_t)i);
+  const Task T = tasks[t];
+  const int k = split_bits(T);
+  push_task(TL, T.begin + (doff[i] - doff[digit_base[t]]), c, T.row, T.rem - (uint32_t)k, T.buf ^ 1u, err);
+}
+
+// ------------------------------------------------------------------ per-rule compaction
+__global__ void k_select_rule(const uint8_t* __restrict__ rule, int64_t n, int r, uint32_t* __restrict__ flag) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) flag[i] = rule[i] == (uint8_t)r;
+}
+__global__ void k_compact_rule(const uint8_t* __restrict__ rule, int64_t n, int r, const uint64_t* __restrict__ idx,
+                               const int32_t* __restrict__ a, const int32_t* __restrict__ b,
+                               const uint32_t* __restrict__ c, const uint32_t* __restrict__ c2,
+                               int32_t* __restrict__ oa, int32_t* __restrict__ ob, uint32_t* __restrict__ oc,
+                               uint32_t* __restrict__ oc2) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || rule[i] != (uint8_t)r) return;
+  const uint64_t p = idx[i];
+  if (oa) oa[p] = a[i];
+  if (ob) ob[p] = b[i];
+  if (oc) oc[p] = c[i];
+  if (oc2) oc2[p] = c2[i];
+}
+
+// ------------------------------------------------------------------ finalize (merge A6)
+// flag rows of rule r whose selected count passes the threshold
+__global__ void k_fin_select(const uint8_t* __restrict__ rule, const uint32_t* __restrict__ c,
+                             const uint32_t* __restrict__ c2, int64_t n, int r, int use_ge2, uint32_t thr,
+                             uint32_t* __restrict__ flag) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t v = use_ge2 ? c2[i] : c[i];
+  flag[i] = rule[i] == (uint8_t)r && v >= thr;
+}
+__global__ void k_fin_compact(const uint32_t* __restrict__ flag, const uint64_t* __restrict__ idx, int64_t n,
+                              const int32_t* __restrict__ a, const int32_t* __restrict__ b,
+                              const uint32_t* __restrict__ c, const uint32_t* __restrict__ c2, int use_ge2,
+                              uint32_t* __restrict__ sa, uint32_t* __restrict__ sb, uint32_t* __restrict__ sc) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !flag[i]) return;
+  const uint64_t p = idx[i];
+  sa[p] = (uint32_t)a[i]; sb[p] = (uint32_t)b[i]; sc[p] = use_ge2 ? c2[i] : c[i];
+}
+__global__ void k_iota_key(const uint32_t* __restrict__ src, int64_t n, uint32_t* __restrict__ key,
+                           uint32_t* __restrict__ val) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  key[i] = src[i]; val[i] = (uint32_t)i;
+}
+// key[i] = src[val[i]] (optionally inverted for a descending sort)
+__global__ void k_gather_key(const uint32_t* __restrict__ src, const uint32_t* __restrict__ val, int64_t n,
+                             int invert, uint32_t* __restrict__ key) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t v = src[val[i]];
+  key[i] = invert ? ~v : v;
+}
+__global__ void k_fin_out(const uint32_t* __restrict__ val, int64_t n, const uint32_t* __restrict__ sa,
+                          const uint32_t* __restrict__ sb, const uint32_t* __restrict__ sc,
+                          int32_t* __restrict__ oa, int32_t* __restrict__ ob, int32_t* __restrict__ oc) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t j = val[i];
+  if (oa) oa[i] = (int32_t)sa[j];
+  if (ob) ob[i] = (int32_t)sb[j];
+  if (oc) oc[i] = (int32_t)sc[j];
+}
+
+}  // namespace ottohip

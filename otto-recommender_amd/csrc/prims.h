@@ -1,0 +1,14 @@
+#pragma once
+#include "common.h"
+
+namespace ottohip {
+// out[i] = sum(in[0..i)), 64-bit; optional device total
+int exclusive_scan_u32(Ctx* ctx, const uint32_t* in, uint64_t* out, int64_t n, uint64_t* total,
+                       hipStream_t s);
+int exclusive_scan_u64(Ctx* ctx, const uint64_t* in, uint64_t* out, int64_t n, uint64_t* total,
+                       hipStream_t s);
+// stable LSD sort of (key, val) by key bits [0, bits); ping-pongs with the *_alt buffers and
+// returns the buffers holding the result in keys/vals
+int radix_sort_pairs(Ctx* ctx, uint32_t*& keys, uint32_t*& vals, uint32_t* keys_alt, uint32_t* vals_alt,
+                     int64_t n, int bits, hipStream_t s);
+}  // namespace ottohip

@@ -1,0 +1,214 @@
+// Device primitives used by the co-visitation engine: exclusive scans and a stable LSD
+// radix sort of (u32 key, u32 value) pairs. Written for wave64 / gfx950:
+//   * scans: 256-thread blocks, 8 consecutive items per thread (32-B vector loads), wave
+//     shuffle scan + one LDS hop across the 4 waves, recursive over block sums;
+//   * radix sort: 8-bit digits, 4096-key tiles, stable wave-level multisplit by 8 ballots,
+//     per-wave digit counters in LDS, keys staged in LDS in digit order so the global
+//     scatter writes one contiguous run per (tile, digit).
+#include "prims.h"
+
+namespace ottohip {
+
+constexpr int SCAN_T = 256, SCAN_I = 8, SCAN_TILE = SCAN_T * SCAN_I;
+
+template <class T>
+__global__ __launch_bounds__(SCAN_T) void k_block_sums(const T* __restrict__ in, int64_t n,
+                                                       uint64_t* __restrict__ sums) {
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_I;
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_I; ++i)
+    if (base + i < n) s += (uint64_t)in[base + i];
+  __shared__ uint64_t ws[SCAN_T / 64];
+  s = wave_incl_scan64(s);
+  if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int w = 0; w < SCAN_T / 64; ++w) t += ws[w];
+    sums[blockIdx.x] = t;
+  }
+}
+
+// exclusive scan of one tile, plus the tile's offset from `offs` (or 0); total to *total
+template <class T>
+__global__ __launch_bounds__(SCAN_T) void k_scan_tile(const T* __restrict__ in, int64_t n,
+                                                      uint64_t* __restrict__ out,
+                                                      const uint64_t* __restrict__ offs,
+                                                      uint64_t* __restrict__ total) {
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_I;
+  uint64_t v[SCAN_I];
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_I; ++i) {
+    v[i] = (base + i < n) ? (uint64_t)in[base + i] : 0;
+    s += v[i];
+  }
+  __shared__ uint64_t ws[SCAN_T / 64];
+  const uint64_t incl = wave_incl_scan64(s);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) ws[w] = incl;
+  __syncthreads();
+  uint64_t pre = offs ? offs[blockIdx.x] : 0;
+  for (int k = 0; k < w; ++k) pre += ws[k];
+  uint64_t run = pre + incl - s;
+#pragma unroll
+  for (int i = 0; i < SCAN_I; ++i) {
+    if (base + i < n) out[base + i] = run;
+    run += v[i];
+  }
+  if (total && threadIdx.x == SCAN_T - 1 && blockIdx.x == gridDim.x - 1) *total = run;
+}
+
+template <class T>
+static int scan_rec(Ctx* ctx, const T* in, uint64_t* out, int64_t n, uint64_t* total, hipStream_t s,
+                    int depth) {
+  if (n <= 0) {
+    if (total) OH_HIP(hipMemsetAsync(total, 0, sizeof(uint64_t), s));
+    return 0;
+  }
+  const int64_t nb = ceil_div(n, SCAN_TILE);
+  if (nb == 1) {
+    k_scan_tile<T><<<1, SCAN_T, 0, s>>>(in, n, out, nullptr, total);
+    OH_HIP(hipGetLastError());
+    return 0;
+  }
+  char name[32];
+  snprintf(name, sizeof name, "scan_sums%d", depth);
+  uint64_t* sums;
+  OH_TRY(ctx->ws.get(name, (size_t)nb, &sums));
+  k_block_sums<T><<<(unsigned)nb, SCAN_T, 0, s>>>(in, n, sums);
+  OH_HIP(hipGetLastError());
+  OH_TRY(scan_rec<uint64_t>(ctx, sums, sums, nb, nullptr, s, depth + 1));  // in place is safe per tile
+  k_scan_tile<T><<<(unsigned)nb, SCAN_T, 0, s>>>(in, n, out, sums, total);
+  OH_HIP(hipGetLastError());
+  return 0;
+}
+
+int exclusive_scan_u32(Ctx* ctx, const uint32_t* in, uint64_t* out, int64_t n, uint64_t* total,
+                       hipStream_t s) {
+  return scan_rec<uint32_t>(ctx, in, out, n, total, s, 0);
+}
+int exclusive_scan_u64(Ctx* ctx, const uint64_t* in, uint64_t* out, int64_t n, uint64_t* total,
+                       hipStream_t s) {
+  return scan_rec<uint64_t>(ctx, in, out, n, total, s, 0);
+}
+
+// ------------------------------------------------------------------ radix sort
+constexpr int RS_T = 256, RS_WAVES = RS_T / 64, RS_R = 16, RS_TILE = RS_T * RS_R;  // 4096
+
+__global__ __launch_bounds__(RS_T) void k_rs_hist(const uint32_t* __restrict__ keys, int64_t n, int shift,
+                                                  uint32_t* __restrict__ hist, int nb) {
+  __shared__ uint32_t h[RS_WAVES][256];
+  for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_T) (&h[0][0])[i] = 0;
+  __syncthreads();
+  const int w = threadIdx.x >> 6;
+  const int64_t t0 = (int64_t)blockIdx.x * RS_TILE;
+#pragma unroll 4
+  for (int r = 0; r < RS_R; ++r) {
+    const int64_t idx = t0 + r * RS_T + threadIdx.x;
+    if (idx < n) atomicAdd(&h[w][(keys[idx] >> shift) & 255u], 1u);
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < 256; d += RS_T) {
+    uint32_t c = 0;
+    for (int k = 0; k < RS_WAVES; ++k) c += h[k][d];
+    hist[(int64_t)d * nb + blockIdx.x] = c;
+  }
+}
+
+__global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict__ kin,
+                                                     const uint32_t* __restrict__ vin,
+                                                     uint32_t* __restrict__ kout,
+                                                     uint32_t* __restrict__ vout, int64_t n, int shift,
+                                                     const uint64_t* __restrict__ gofs, int nb) {
+  __shared__ uint32_t wcnt[RS_WAVES][256];
+  __shared__ uint32_t bstart[256];
+  __shared__ uint32_t wsum[RS_WAVES];
+  __shared__ uint32_t stage_k[RS_TILE];
+  __shared__ uint32_t stage_v[RS_TILE];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int64_t t0 = (int64_t)blockIdx.x * RS_TILE;
+  for (int i = tid; i < RS_WAVES * 256; i += RS_T) (&wcnt[0][0])[i] = 0;
+  __syncthreads();
+  uint32_t key[RS_R], val[RS_R], rnk[RS_R];
+  // wave w owns the contiguous quarter [t0 + w*1024, t0 + (w+1)*1024): stable order
+#pragma unroll
+  for (int r = 0; r < RS_R; ++r) {
+    const int64_t idx = t0 + w * (RS_R * 64) + r * 64 + l;
+    const bool valid = idx < n;
+    key[r] = valid ? kin[idx] : 0u;
+    val[r] = valid ? vin[idx] : 0u;
+    const uint32_t d = (key[r] >> shift) & 255u;
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bb = __ballot(bit);
+      m &= bit ? bb : ~bb;
+    }
+    const uint32_t below = mbcnt(m);
+    const uint32_t old = wcnt[w][d];
+    __builtin_amdgcn_wave_barrier();
+    if (valid && below == 0) wcnt[w][d] = old + (uint32_t)__popcll(m);
+    __builtin_amdgcn_wave_barrier();
+    rnk[r] = old + below;
+  }
+  __syncthreads();
+  // per digit: wave offsets (exclusive over waves) and the tile-local digit start
+  {
+    const int d = tid;  // RS_T == 256 digits
+    uint32_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < RS_WAVES; ++k) { uint32_t c = wcnt[k][d]; wcnt[k][d] = tot; tot += c; }
+    const uint32_t incl = wave_incl_scan(tot);
+    if (l == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (int k = 0; k < w; ++k) pre += wsum[k];
+    bstart[d] = pre + incl - tot;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < RS_R; ++r) {
+    const int64_t idx = t0 + w * (RS_R * 64) + r * 64 + l;
+    if (idx < n) {
+      const uint32_t d = (key[r] >> shift) & 255u;
+      const uint32_t p = bstart[d] + wcnt[w][d] + rnk[r];
+      stage_k[p] = key[r];
+      stage_v[p] = val[r];
+    }
+  }
+  __syncthreads();
+  const int64_t tn = n - t0 < RS_TILE ? n - t0 : RS_TILE;
+  for (int p = tid; p < tn; p += RS_T) {
+    const uint32_t k = stage_k[p];
+    const uint32_t d = (k >> shift) & 255u;
+    const uint64_t dst = gofs[(int64_t)d * nb + blockIdx.x] + (uint64_t)(p - bstart[d]);
+    kout[dst] = k;
+    vout[dst] = stage_v[p];
+  }
+}
+
+int radix_sort_pairs(Ctx* ctx, uint32_t*& keys, uint32_t*& vals, uint32_t* keys_alt, uint32_t* vals_alt,
+                     int64_t n, int bits, hipStream_t s) {
+  if (n <= 1 || bits <= 0) return 0;
+  if (n >= ((int64_t)1 << 32)) { set_error("radix_sort_pairs: n=%lld too large", (long long)n); return OTTOHIP_ELIMIT; }
+  const int nb = (int)ceil_div(n, RS_TILE);
+  uint32_t* hist; uint64_t* gofs;
+  OH_TRY(ctx->ws.get("rs_hist", (size_t)nb * 256, &hist));
+  OH_TRY(ctx->ws.get("rs_gofs", (size_t)nb * 256, &gofs));
+  uint32_t *ka = keys, *va = vals, *kb = keys_alt, *vb = vals_alt;
+  for (int shift = 0; shift < bits; shift += 8) {
+    k_rs_hist<<<nb, RS_T, 0, s>>>(ka, n, shift, hist, nb);
+    OH_HIP(hipGetLastError());
+    OH_TRY(exclusive_scan_u32(ctx, hist, gofs, (int64_t)nb * 256, nullptr, s));
+    k_rs_scatter<<<nb, RS_T, 0, s>>>(ka, va, kb, vb, n, shift, gofs, nb);
+    OH_HIP(hipGetLastError());
+    std::swap(ka, kb); std::swap(va, vb);
+  }
+  keys = ka; vals = va;  // result buffers (may be the alternates)
+  return 0;
+}
+
+}  // namespace ottohip
