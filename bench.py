@@ -99,16 +99,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    tabs = []
+    tab = None
     for _ in range(args.steps):
-        tabs.append(step())
-        if len(tabs) > 1:
-            tabs.pop(0).free()
+        if tab is not None:
+            tab.free()  # returns its buffers to the context for the next build
+        tab = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    tab = tabs[-1]
     stats = {n: tab.stats(n) for n in tab.names}
     pairs = sum(s["n_pairs"] for s in stats.values())
     rows = sum(s["n_rows"] for s in stats.values())

@@ -336,17 +336,18 @@ int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohi
   k_classify_rows<<<grid_for(Rn), 256, 0, s>>>(row_begin, Rn, P, Lt.WB, TL, err);
   const int agg_grid = ctx->n_cu * 8;
   bool srcA = true;
-  for (int level = 0; level < 8; ++level) {
+  bool drained = false;
+  for (int level = 0; level < 40; ++level) {
     unsigned long long nlist[3];
     if ((rc = d2h(nlist, lcount, 3, s))) return fail(rc);
     if ((rc = d2h(&herr, err, 1, s))) return fail(rc);
     if (herr) { set_error("task list overflow / row too large (err=%d)", herr); return fail(OTTOHIP_ELIMIT); }
     if (nlist[0]) k_agg_tiny<<<(unsigned)std::min<uint64_t>(ceil_div((int64_t)nlist[0], 4), (uint64_t)ctx->n_cu * 32), 256, 0, s>>>(
-        TL.tiny, (int64_t)nlist[0], w0, w1, row_key, R, Lt, O);
+        TL.tiny, (int64_t)nlist[0], w0, w1, row_key, R, Lt, n_rules, O);
     if (nlist[1]) k_agg_hash<<<(unsigned)std::min<uint64_t>(nlist[1], (uint64_t)agg_grid), AGG_T, 0, s>>>(
-        TL.hash, (int64_t)nlist[1], w0, w1, row_key, R, Lt, O);
+        TL.hash, (int64_t)nlist[1], w0, w1, row_key, R, Lt, n_rules, O);
     const int64_t ns = (int64_t)nlist[2];
-    if (ns == 0) break;
+    if (ns == 0) { drained = true; break; }
     Task* cur_split = TL.split;
     // chunk / digit bases
     uint32_t *nch, *ndg;
@@ -355,7 +356,7 @@ int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohi
         (rc = ws.get("sp_chb", (size_t)ns + 1, &chb)) || (rc = ws.get("sp_dgb", (size_t)ns + 1, &dgb)) ||
         (rc = ws.get("sp_tot", 2, &tot2)))
       return fail(rc);
-    k_split_prepare<<<grid_for(ns), 256, 0, s>>>(cur_split, ns, nch, ndg);
+    k_split_prepare<<<grid_for(ns), 256, 0, s>>>(cur_split, ns, Lt.WB, nch, ndg);
     if ((rc = exclusive_scan_u32(ctx, nch, chb, ns, tot2, s)) || (rc = exclusive_scan_u32(ctx, ndg, dgb, ns, tot2 + 1, s)))
       return fail(rc);
     uint64_t tt[2];
@@ -368,10 +369,10 @@ int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohi
         (rc = ws.get("sp_dcur", (size_t)ndig, &dcur)))
       return fail(rc);
     hipMemsetAsync(dcount, 0, ndig * 4, s);
-    k_split_hist<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, dgb, w0, w1, dcount);
+    k_split_hist<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, dgb, w0, w1, Lt.WB, dcount);
     if ((rc = exclusive_scan_u32(ctx, dcount, doff, ndig, nullptr, s))) return fail(rc);
     k_split_cursor<<<grid_for(ndig), 256, 0, s>>>(cur_split, ns, dgb, doff, dcur, ndig);
-    k_split_scatter<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, dgb, w0, w1, dcur);
+    k_split_scatter<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, dgb, w0, w1, Lt.WB, dcur);
     // next lists
     const uint64_t capn = (uint64_t)ndig;
     Task *ntiny, *nhash, *nsplit;
@@ -382,17 +383,24 @@ int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohi
     TL.tiny = ntiny; TL.hash = nhash; TL.split = nsplit;
     TL.cap_tiny = TL.cap_hash = std::max(cap0, capn); TL.cap_split = capn;
     hipMemsetAsync(lcount, 0, 4 * 8, s);
-    k_split_classify<<<grid_for(ndig), 256, 0, s>>>(cur_split, ns, dgb, dcount, doff, ndig, TL, err);
+    k_split_classify<<<grid_for(ndig), 256, 0, s>>>(cur_split, ns, dgb, dcount, doff, ndig, Lt.WB, TL, err);
     srcA = !srcA;
     if (hipGetLastError() != hipSuccess) { set_error("split launch failed"); return fail(OTTOHIP_EHIP); }
   }
   ctx->end(ph, s);
+  if (!drained) { set_error("reduce: split levels did not converge"); return fail(OTTOHIP_ELIMIT); }
   unsigned long long U = 0;
   if ((rc = d2h(&U, cursor, 1, s))) return fail(rc);
   unsigned long long st[MAX_RULES * 4];
   if ((rc = d2h(st, stats, MAX_RULES * 4, s))) return fail(rc);
   if (hipGetLastError() != hipSuccess) { set_error("reduce failed"); return fail(OTTOHIP_EHIP); }
   T->n_rows = (int64_t)U;
+  unsigned long long sum_pairs = 0;
+  for (int r = 0; r < n_rules; ++r) sum_pairs += st[r * 4 + 1];
+  if (sum_pairs != P || U > P) {  // conservation: every emitted pair is counted exactly once
+    set_error("reduce: %llu pairs counted of %llu emitted (rows %llu)", sum_pairs, (unsigned long long)P, U);
+    return fail(OTTOHIP_EHIP);
+  }
   for (int r = 0; r < n_rules; ++r) {
     T->stats[r].n_rows = (int64_t)st[r * 4 + 0];
     T->stats[r].n_pairs = (int64_t)st[r * 4 + 1];

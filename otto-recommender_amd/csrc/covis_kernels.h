@@ -423,77 +423,120 @@ __device__ __forceinline__ void put_row(const OutRows& O, uint64_t p, int rule, 
   }
 }
 
+// per-thread statistics per global rule, indexed statically (no scratch)
+struct RuleAcc {
+  uint32_t rows[MAX_RULES], nf1[MAX_RULES], nf2[MAX_RULES];
+  unsigned long long pairs[MAX_RULES];
+  __device__ void zero() {
+#pragma unroll
+    for (int r = 0; r < MAX_RULES; ++r) { rows[r] = nf1[r] = nf2[r] = 0; pairs[r] = 0; }
+  }
+  __device__ void add(int rule, uint32_t c, uint32_t nf) {
+#pragma unroll
+    for (int r = 0; r < MAX_RULES; ++r)
+      if (r == rule) { rows[r] += 1; pairs[r] += c; nf1[r] += nf & 0xFFFFu; nf2[r] += nf >> 16; }
+  }
+  // wave reduction, then one device atomic per nonzero statistic
+  __device__ void flush(unsigned long long* stats, int n_rules) {
+    for (int r = 0; r < n_rules; ++r) {
+      unsigned long long v[4] = {rows[0], pairs[0], nf1[0], nf2[0]};
+#pragma unroll
+      for (int q = 0; q < MAX_RULES; ++q)
+        if (q == r) { v[0] = rows[q]; v[1] = pairs[q]; v[2] = nf1[q]; v[3] = nf2[q]; }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        unsigned long long x = v[k];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+          const uint32_t lo = __shfl_xor((uint32_t)x, d), hi = __shfl_xor((uint32_t)(x >> 32), d);
+          x += ((unsigned long long)hi << 32) | lo;
+        }
+        if (lane_id() == 0 && x) atomicAdd(&stats[r * 4 + k], x);
+      }
+    }
+  }
+};
+
 // one wave per task with len <= 64
 __global__ __launch_bounds__(256) void k_agg_tiny(const Task* __restrict__ tasks, int64_t n_tasks,
                                                   const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
                                                   const uint32_t* __restrict__ row_key, RulesDev R, Layout L,
-                                                  OutRows O) {
+                                                  int n_rules, OutRows O) {
   const int l = lane_id();
   const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  unsigned long long st[MAX_RULES][4];
-  for (int r = 0; r < MAX_RULES; ++r) for (int k = 0; k < 4; ++k) st[r][k] = 0;
-  const uint32_t fmask = (1u << L.F) - 1u;
+  RuleAcc acc;
+  acc.zero();
   for (int64_t ti = gw; ti < n_tasks; ti += nw) {
     const Task T = tasks[ti];
+    const int len = (int)T.len;
     const uint32_t* W = T.buf ? w1 : w0;
-    const uint32_t w = l < (int)T.len ? W[T.begin + l] : W_EMPTY;
+    const uint32_t w = l < len ? W[T.begin + l] : W_EMPTY;
     // per-file count of this word and first-occurrence flag
-    uint32_t cf = 0; bool first = true;
-    for (int j = 0; j < (int)T.len; ++j) {
+    uint32_t cf = 0; bool first = l < len;
+    for (int j = 0; j < len; ++j) {
       const uint32_t u = __shfl(w, j);
       cf += u == w;
       first &= !(u == w && j < l);
     }
     const uint32_t k2 = w >> L.F;
-    uint32_t call = 0, c2 = 0, nf1 = 0, nf2 = 0; bool firstk = true;
-    for (int j = 0; j < (int)T.len; ++j) {
+    uint32_t call = 0, c2 = 0, nf = 0; bool firstk = true;
+    const uint64_t fm = __ballot(first);
+    for (int j = 0; j < len; ++j) {
+      if (!((fm >> j) & 1ull)) continue;  // wave-uniform skip
       const uint32_t u = __shfl(w, j);
-      const bool fj = __shfl((int)first, j);
       const uint32_t cj = __shfl(cf, j);
-      if (fj && (u >> L.F) == k2) {
-        call += cj; c2 += cj >= 2 ? cj : 0; nf1 += 1; nf2 += cj >= 2;
+      if ((u >> L.F) == k2) {
+        call += cj; c2 += cj >= 2 ? cj : 0; nf += 1u + ((cj >= 2 ? 1u : 0u) << 16);
         firstk &= !(j < l);
       }
     }
-    const bool emit = l < (int)T.len && first && firstk;
+    const bool emit = first && firstk;
     const uint64_t m = __ballot(emit);
     unsigned long long base = 0;
     if (l == 0) base = atomicAdd(O.cursor, (unsigned long long)__popcll(m));
     base = __shfl(base, 0);
     const RowInfo ri = row_info(row_key, T.row, L.A);
-    const int ql = (int)(k2 >> L.A);
     if (emit) {
-      const int rule = R.rule_of_type[ri.type][ql];
+      const int rule = R.rule_of_type[ri.type][k2 >> L.A];
       put_row(O, base + mbcnt(m), rule, ri.aid, (int32_t)(k2 & L.amask), call, c2);
-      (void)fmask;
-    }
-    for (int q = 0; q < R.n_of_type[ri.type]; ++q) {
-      const bool mine = emit && ql == q;
-      const uint32_t a0 = wave_sum(mine ? 1u : 0u), a1 = wave_sum(mine ? call : 0u);
-      const uint32_t a2 = wave_sum(mine ? nf1 : 0u), a3 = wave_sum(mine ? nf2 : 0u);
-      const int rule = R.rule_of_type[ri.type][q];
-      st[rule][0] += a0; st[rule][1] += a1; st[rule][2] += a2; st[rule][3] += a3;
+      acc.add(rule, call, nf);
     }
   }
-  if (l == 0)
-    for (int r = 0; r < MAX_RULES; ++r)
-      for (int k = 0; k < 4; ++k)
-        if (st[r][k]) atomicAdd(&O.stats[r * 4 + k], st[r][k]);
+  acc.flush(O.stats, n_rules);
 }
 
-// one workgroup per task: LDS hash of (rule|aid_next|file) counts, then folded over files
+// one workgroup per task: LDS hash of (rule|aid_next|file) counts, then folded over files.
+// Phase A slots: u64 (word << 32 | count); phase B: u64 (key2 << 32 | count) + u64 (count_ge2 << 32 | nf2 << 16 | nf1)
 constexpr int AGG_T = 256;
 constexpr int HCAP = 4096;
+constexpr unsigned long long SLOT_EMPTY = 0xFFFFFFFF00000000ull;
+
+__device__ __forceinline__ uint32_t hash_insert(unsigned long long* slots, uint32_t key, uint32_t inc, uint32_t cm) {
+  uint32_t h = hslot(key, cm);
+  while (true) {
+    const unsigned long long v = slots[h];
+    const uint32_t k = (uint32_t)(v >> 32);
+    if (k == key) { atomicAdd(&slots[h], (unsigned long long)inc); return h; }
+    if (k == W_EMPTY) {
+      const unsigned long long old = atomicCAS(&slots[h], v, ((unsigned long long)key << 32) | inc);
+      if (old == v) return h;
+      continue;  // lost the race: re-read this slot
+    }
+    h = (h + 1) & cm;
+  }
+}
+
 __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tasks, int64_t n_tasks,
                                                     const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
                                                     const uint32_t* __restrict__ row_key, RulesDev R, Layout L,
-                                                    OutRows O) {
-  __shared__ uint32_t lds[4 * HCAP];  // 64 KiB: phase A uses [0, 2cap), phase B [0, 4cap)
-  __shared__ unsigned long long sstat[MAX_RULES][4];
+                                                    int n_rules, OutRows O) {
+  __shared__ unsigned long long lds[2 * HCAP];  // 64 KiB: phase A [0, cap), phase B [0, 2cap)
   __shared__ uint32_t sbase[2];
   __shared__ uint32_t wtot[AGG_T / 64];
   const int tid = threadIdx.x;
+  RuleAcc acc;
+  acc.zero();
   for (int64_t ti = blockIdx.x; ti < n_tasks; ti += gridDim.x) {
     const Task T = tasks[ti];
     const uint32_t* W = (T.buf ? w1 : w0) + T.begin;
@@ -502,18 +545,20 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
     uint32_t cap = 64;
     while (cap < 2 * dbound) cap <<= 1;
     const uint32_t cm = cap - 1;
-    uint32_t* keyA = lds;
-    uint32_t* cntA = lds + cap;
-    for (uint32_t i = tid; i < cap; i += AGG_T) { keyA[i] = W_EMPTY; cntA[i] = 0; }
-    if (tid < MAX_RULES * 4) (&sstat[0][0])[tid] = 0;
+    unsigned long long* A = lds;
+    for (uint32_t i = tid; i < cap; i += AGG_T) A[i] = SLOT_EMPTY;
     __syncthreads();
-    for (uint32_t i = tid; i < T.len; i += AGG_T) {
-      const uint32_t w = W[i];
-      uint32_t h = hslot(w, cm);
-      while (true) {
-        const uint32_t prev = atomicCAS(&keyA[h], W_EMPTY, w);
-        if (prev == W_EMPTY || prev == w) { atomicAdd(&cntA[h], 1u); break; }
-        h = (h + 1) & cm;
+    for (uint32_t i0 = 0; i0 < T.len; i0 += AGG_T) {
+      const uint32_t i = i0 + tid;
+      const bool act = i < T.len;
+      const uint32_t w = act ? W[i] : W_EMPTY;
+      // wave-uniform word (heavy buckets): one add for the whole wave
+      const uint32_t wu = __builtin_amdgcn_readfirstlane(w);
+      const uint64_t am = __ballot(act);
+      if (am && __ballot(act && w == wu) == am) {
+        if ((tid & 63) == 0) hash_insert(A, wu, (uint32_t)__popcll(am), cm);
+      } else if (act) {
+        hash_insert(A, w, 1u, cm);
       }
     }
     __syncthreads();
@@ -522,36 +567,27 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
 #pragma unroll
     for (int s = 0; s < SL; ++s) {
       const uint32_t slot = tid + s * AGG_T;
-      kw[s] = slot < cap ? keyA[slot] : W_EMPTY;
-      kc[s] = slot < cap ? cntA[slot] : 0;
+      const unsigned long long v = slot < cap ? A[slot] : SLOT_EMPTY;
+      kw[s] = (uint32_t)(v >> 32);
+      kc[s] = (uint32_t)v;
     }
     __syncthreads();
-    uint32_t* keyB = lds;
-    uint32_t* cB = lds + cap;
-    uint32_t* c2B = lds + 2 * cap;
-    uint32_t* nfB = lds + 3 * cap;
-    for (uint32_t i = tid; i < cap; i += AGG_T) { keyB[i] = W_EMPTY; cB[i] = 0; c2B[i] = 0; nfB[i] = 0; }
+    unsigned long long* B = lds;            // key2 << 32 | count
+    unsigned long long* B2 = lds + cap;     // count_ge2 << 32 | nf2 << 16 | nf1
+    for (uint32_t i = tid; i < cap; i += AGG_T) { B[i] = SLOT_EMPTY; B2[i] = 0; }
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < SL; ++s) {
       if (kw[s] == W_EMPTY) continue;
-      const uint32_t k2 = kw[s] >> L.F;
       const uint32_t c = kc[s];
-      uint32_t h = hslot(k2, cm);
-      while (true) {
-        const uint32_t prev = atomicCAS(&keyB[h], W_EMPTY, k2);
-        if (prev == W_EMPTY || prev == k2) break;
-        h = (h + 1) & cm;
-      }
-      atomicAdd(&cB[h], c);
-      if (c >= 2) atomicAdd(&c2B[h], c);
-      atomicAdd(&nfB[h], 1u | ((c >= 2 ? 1u : 0u) << 16));
+      const uint32_t h = hash_insert(B, kw[s] >> L.F, c, cm);
+      atomicAdd(&B2[h], ((unsigned long long)(c >= 2 ? c : 0u) << 32) | 1ull | ((c >= 2 ? 1ull : 0ull) << 16));
     }
     __syncthreads();
     // compact and write
     const RowInfo ri = row_info(row_key, T.row, L.A);
     uint32_t mine = 0;
-    for (uint32_t i = tid; i < cap; i += AGG_T) mine += keyB[i] != W_EMPTY;
+    for (uint32_t i = tid; i < cap; i += AGG_T) mine += (uint32_t)(B[i] >> 32) != W_EMPTY;
     const uint32_t incl = wave_incl_scan(mine);
     if ((tid & 63) == 63) wtot[tid >> 6] = incl;
     __syncthreads();
@@ -564,24 +600,18 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
     __syncthreads();
     uint64_t p = (((uint64_t)sbase[1] << 32) | sbase[0]) + pre + incl - mine;
     for (uint32_t i = tid; i < cap; i += AGG_T) {
-      const uint32_t k2 = keyB[i];
+      const unsigned long long v = B[i];
+      const uint32_t k2 = (uint32_t)(v >> 32);
       if (k2 == W_EMPTY) continue;
-      const int q = (int)(k2 >> L.A);
-      const int rule = R.rule_of_type[ri.type][q];
-      const uint32_t nf = nfB[i];
-      put_row(O, p++, rule, ri.aid, (int32_t)(k2 & L.amask), cB[i], c2B[i]);
-      atomicAdd(&sstat[rule][0], 1ull);
-      atomicAdd(&sstat[rule][1], (unsigned long long)cB[i]);
-      atomicAdd(&sstat[rule][2], (unsigned long long)(nf & 0xFFFFu));
-      atomicAdd(&sstat[rule][3], (unsigned long long)(nf >> 16));
-    }
-    __syncthreads();
-    if (tid < MAX_RULES * 4) {
-      const unsigned long long v = (&sstat[0][0])[tid];
-      if (v) atomicAdd(&O.stats[tid], v);
+      const unsigned long long v2 = B2[i];
+      const int rule = R.rule_of_type[ri.type][k2 >> L.A];
+      const uint32_t c = (uint32_t)v, c2 = (uint32_t)(v2 >> 32), nf = (uint32_t)v2;
+      put_row(O, p++, rule, ri.aid, (int32_t)(k2 & L.amask), c, c2);
+      acc.add(rule, c, nf);
     }
     __syncthreads();
   }
+  acc.flush(O.stats, n_rules);
 }
 
 // ---- classification of rows and split buckets into task lists
@@ -621,19 +651,24 @@ __global__ void k_classify_rows(const uint64_t* __restrict__ row_begin, int64_t 
 constexpr int SPLIT_CH = 16384;
 constexpr int SPLIT_T = 256;
 
-__device__ __forceinline__ int split_bits(const Task& t) {
-  int k = 1;
-  while (k < 8 && ((uint64_t)t.len >> k) > 1024) ++k;
-  if ((uint32_t)k > t.rem) k = (int)t.rem;
-  return k;
+// First split of a row: enough bits for ~1024-word buckets. A bucket that is still large
+// after a split is dominated by a few keys: take the bits down to HASH_REM (at most 8) at once.
+__device__ __forceinline__ int split_bits(const Task& t, int WB) {
+  int k = 8;
+  if ((int)t.rem == WB) {
+    k = 1;
+    while (k < 8 && ((uint64_t)t.len >> k) > 1024) ++k;
+  }
+  const int maxk = (int)t.rem - HASH_REM;
+  if (k > maxk) k = maxk;
+  return k < 1 ? 1 : k;
 }
-
-__global__ void k_split_prepare(const Task* __restrict__ tasks, int64_t n, uint32_t* __restrict__ nchunks,
+__global__ void k_split_prepare(const Task* __restrict__ tasks, int64_t n, int WB, uint32_t* __restrict__ nchunks,
                                 uint32_t* __restrict__ ndigits) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   nchunks[i] = (uint32_t)ceil_div((int64_t)tasks[i].len, SPLIT_CH);
-  ndigits[i] = 1u << split_bits(tasks[i]);
+  ndigits[i] = 1u << split_bits(tasks[i], WB);
 }
 
 __device__ __forceinline__ int64_t find_task(const uint64_t* chunk_base, int64_t n, uint64_t c) {
@@ -649,11 +684,11 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_hist(const Task* __restrict__
                                                         const uint64_t* __restrict__ chunk_base,
                                                         const uint64_t* __restrict__ digit_base,
                                                         const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
-                                                        uint32_t* __restrict__ dcount) {
+                                                        int WB, uint32_t* __restrict__ dcount) {
   __shared__ uint32_t h[256];
   const int64_t t = find_task(chunk_base, n, blockIdx.x);
   const Task T = tasks[t];
-  const int k = split_bits(T);
+  const int k = split_bits(T, WB);
   const int sh = (int)T.rem - k;
   const uint32_t dm = (1u << k) - 1u;
   const uint64_t c0 = (uint64_t)(blockIdx.x - chunk_base[t]) * SPLIT_CH;
@@ -681,14 +716,14 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
                                                            const uint64_t* __restrict__ chunk_base,
                                                            const uint64_t* __restrict__ digit_base,
                                                            uint32_t* __restrict__ w0, uint32_t* __restrict__ w1,
-                                                           unsigned long long* __restrict__ cur) {
+                                                           int WB, unsigned long long* __restrict__ cur) {
   __shared__ uint32_t h[256], st[256], fill[256];
   __shared__ unsigned long long gb[256];
   __shared__ uint32_t stage[SUB];
   __shared__ uint32_t wsum[SPLIT_T / 64];
   const int64_t t = find_task(chunk_base, n, blockIdx.x);
   const Task T = tasks[t];
-  const int k = split_bits(T);
+  const int k = split_bits(T, WB);
   const int sh = (int)T.rem - k;
   const uint32_t dm = (1u << k) - 1u;
   const uint64_t c0 = (uint64_t)(blockIdx.x - chunk_base[t]) * SPLIT_CH;
@@ -730,14 +765,14 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
 
 __global__ void k_split_classify(const Task* __restrict__ tasks, int64_t n, const uint64_t* __restrict__ digit_base,
                                  const uint32_t* __restrict__ dcount, const uint64_t* __restrict__ doff,
-                                 int64_t n_digits_total, TaskLists TL, int* err) {
+                                 int64_t n_digits_total, int WB, TaskLists TL, int* err) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_digits_total) return;
   const uint32_t c = dcount[i];
   if (!c) return;
   const int64_t t = find_task(digit_base, n, (uint64_t)i);
   const Task T = tasks[t];
-  const int k = split_bits(T);
+  const int k = split_bits(T, WB);
   push_task(TL, T.begin + (doff[i] - doff[digit_base[t]]), c, T.row, T.rem - (uint32_t)k, T.buf ^ 1u, err);
 }
 
