@@ -52,7 +52,8 @@ struct ottohip_ctx : public Ctx {
 struct ottohip_table {
   int device = 0;
   int n_rules = 0;
-  int64_t n_rows = 0;
+  int64_t n_rows = 0;   // valid rows (sum over rules)
+  int64_t n_slots = 0;  // entries of the row arrays; holes carry rule = 0xFF
   TableBufs b;
   ottohip_rule_stats stats[MAX_RULES];
   ottohip_ctx* ctx = nullptr;
@@ -311,15 +312,13 @@ int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohi
     ctx->spare.release();
     if ((rc = T->b.alloc(P))) return fail(rc);
   }
-  unsigned long long *cursor, *stats, *lcount;
-  if ((rc = ws.get("cursor", 1, &cursor)) || (rc = ws.get("stats", MAX_RULES * 4, &stats)) ||
-      (rc = ws.get("lcount", 4, &lcount)))
-    return fail(rc);
-  hipMemsetAsync(cursor, 0, 8, s);
+  unsigned long long *stats, *lcount;
+  if ((rc = ws.get("stats", MAX_RULES * 4, &stats)) || (rc = ws.get("lcount", 4, &lcount))) return fail(rc);
   hipMemsetAsync(stats, 0, MAX_RULES * 4 * 8, s);
+  hipMemsetAsync(T->b.rule, 0xFF, P, s);  // rows are written at their task's word offsets: holes stay 0xFF
   OutRows O;
   O.rule = T->b.rule; O.aid = T->b.aid; O.aid_next = T->b.aid_next; O.count = T->b.count; O.count_ge2 = T->b.count_ge2;
-  O.cursor = cursor; O.cap = P; O.stats = stats;
+  O.cap = P; O.stats = stats;
 
   ph = ctx->begin("reduce", s, 4.0 * (double)P);
   // level 0 task lists come from the rows
@@ -342,12 +341,17 @@ int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohi
     if ((rc = d2h(nlist, lcount, 3, s))) return fail(rc);
     if ((rc = d2h(&herr, err, 1, s))) return fail(rc);
     if (herr) { set_error("task list overflow / row too large (err=%d)", herr); return fail(OTTOHIP_ELIMIT); }
-    if (nlist[0]) k_agg_tiny<<<(unsigned)std::min<uint64_t>(ceil_div((int64_t)nlist[0], 4), (uint64_t)ctx->n_cu * 32), 256, 0, s>>>(
-        TL.tiny, (int64_t)nlist[0], w0, w1, row_key, R, Lt, n_rules, O);
-    if (nlist[1]) k_agg_hash<<<(unsigned)std::min<uint64_t>(nlist[1], (uint64_t)agg_grid), AGG_T, 0, s>>>(
-        TL.hash, (int64_t)nlist[1], w0, w1, row_key, R, Lt, n_rules, O);
+    if (nlist[0])
+      k_agg_tiny<<<(unsigned)std::min<uint64_t>(ceil_div((int64_t)nlist[0], 4), (uint64_t)ctx->n_cu * 32), 256, 0, s>>>(
+          TL.tiny, (int64_t)nlist[0], w0, w1, row_key, R, Lt, n_rules, O);
+    if (nlist[1]) {  // tasks that overflow the LDS table are appended to the split list
+      k_agg_hash<<<(unsigned)std::min<uint64_t>(nlist[1], (uint64_t)agg_grid), AGG_T, 0, s>>>(
+          TL.hash, (int64_t)nlist[1], w0, w1, row_key, R, Lt, n_rules, O, TL.split, lcount + 2);
+      if ((rc = d2h(nlist, lcount, 3, s))) return fail(rc);
+    }
     const int64_t ns = (int64_t)nlist[2];
     if (ns == 0) { drained = true; break; }
+    if ((uint64_t)ns > TL.cap_split) { set_error("split list overflow"); return fail(OTTOHIP_ELIMIT); }
     Task* cur_split = TL.split;
     // chunk / digit bases
     uint32_t *nch, *ndg;
@@ -373,15 +377,15 @@ int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohi
     if ((rc = exclusive_scan_u32(ctx, dcount, doff, ndig, nullptr, s))) return fail(rc);
     k_split_cursor<<<grid_for(ndig), 256, 0, s>>>(cur_split, ns, dgb, doff, dcur, ndig);
     k_split_scatter<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, dgb, w0, w1, Lt.WB, dcur);
-    // next lists
+    // next lists (a sub-bucket is one task in exactly one list: ndig bounds every list)
     const uint64_t capn = (uint64_t)ndig;
     Task *ntiny, *nhash, *nsplit;
     if ((rc = ws.get("t_tiny", std::max(cap0, capn) * sizeof(Task), reinterpret_cast<void**>(&ntiny))) ||
         (rc = ws.get("t_hash", std::max(cap0, capn) * sizeof(Task), reinterpret_cast<void**>(&nhash))) ||
-        (rc = ws.get(srcA ? "t_splitB" : "t_splitA", capn * sizeof(Task), reinterpret_cast<void**>(&nsplit))))
+        (rc = ws.get(srcA ? "t_splitB" : "t_splitA", std::max(cap0, capn) * sizeof(Task), reinterpret_cast<void**>(&nsplit))))
       return fail(rc);
     TL.tiny = ntiny; TL.hash = nhash; TL.split = nsplit;
-    TL.cap_tiny = TL.cap_hash = std::max(cap0, capn); TL.cap_split = capn;
+    TL.cap_tiny = TL.cap_hash = TL.cap_split = std::max(cap0, capn);
     hipMemsetAsync(lcount, 0, 4 * 8, s);
     k_split_classify<<<grid_for(ndig), 256, 0, s>>>(cur_split, ns, dgb, dcount, doff, ndig, Lt.WB, TL, err);
     srcA = !srcA;
@@ -389,14 +393,13 @@ int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohi
   }
   ctx->end(ph, s);
   if (!drained) { set_error("reduce: split levels did not converge"); return fail(OTTOHIP_ELIMIT); }
-  unsigned long long U = 0;
-  if ((rc = d2h(&U, cursor, 1, s))) return fail(rc);
   unsigned long long st[MAX_RULES * 4];
   if ((rc = d2h(st, stats, MAX_RULES * 4, s))) return fail(rc);
   if (hipGetLastError() != hipSuccess) { set_error("reduce failed"); return fail(OTTOHIP_EHIP); }
+  unsigned long long sum_pairs = 0, U = 0;
+  for (int r = 0; r < n_rules; ++r) { sum_pairs += st[r * 4 + 1]; U += st[r * 4 + 0]; }
   T->n_rows = (int64_t)U;
-  unsigned long long sum_pairs = 0;
-  for (int r = 0; r < n_rules; ++r) sum_pairs += st[r * 4 + 1];
+  T->n_slots = (int64_t)P;
   if (sum_pairs != P || U > P) {  // conservation: every emitted pair is counted exactly once
     set_error("reduce: %llu pairs counted of %llu emitted (rows %llu)", sum_pairs, (unsigned long long)P, U);
     return fail(OTTOHIP_EHIP);
@@ -423,13 +426,14 @@ int ottohip_table_copy(const ottohip_table* t, int rule, int32_t* aid, int32_t* 
   if (t->n_rows == 0 || t->stats[rule].n_rows == 0) return 0;
   hipStream_t s = S(stream);
   Ctx* ctx = t->ctx;
+  const int64_t n = t->n_slots;
   uint32_t* flag;
   uint64_t* idx;
-  OH_TRY(ctx->ws.get("copy_flag", (size_t)t->n_rows, &flag));
-  OH_TRY(ctx->ws.get("copy_idx", (size_t)t->n_rows, &idx));
-  k_select_rule<<<grid_for(t->n_rows), 256, 0, s>>>(t->b.rule, t->n_rows, rule, flag);
-  OH_TRY(exclusive_scan_u32(ctx, flag, idx, t->n_rows, nullptr, s));
-  k_compact_rule<<<grid_for(t->n_rows), 256, 0, s>>>(t->b.rule, t->n_rows, rule, idx, t->b.aid, t->b.aid_next,
+  OH_TRY(ctx->ws.get("copy_flag", (size_t)n, &flag));
+  OH_TRY(ctx->ws.get("copy_idx", (size_t)n, &idx));
+  k_select_rule<<<grid_for(n), 256, 0, s>>>(t->b.rule, n, rule, flag);
+  OH_TRY(exclusive_scan_u32(ctx, flag, idx, n, nullptr, s));
+  k_compact_rule<<<grid_for(n), 256, 0, s>>>(t->b.rule, n, rule, idx, t->b.aid, t->b.aid_next,
                                                      t->b.count, t->b.count_ge2, aid, aid_next, count, count_ge2);
   OH_HIP(hipGetLastError());
   return 0;
@@ -467,7 +471,7 @@ extern "C" int ottohip_table_finalize(ottohip_ctx* ctx, const ottohip_table* t, 
   if (t->n_rows == 0) return 0;
   const uint32_t thr = (uint32_t)std::max<int32_t>(mp->min_count, 1);
   Workspace& ws = ctx->ws;
-  const int64_t n = t->n_rows;
+  const int64_t n = t->n_slots;
   uint32_t* flag;
   uint64_t *idx, *tot;
   OH_TRY(ws.get("fin_flag", (size_t)n, &flag));

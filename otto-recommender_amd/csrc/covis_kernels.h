@@ -57,7 +57,6 @@ struct OutRows {
   int32_t* aid_next;
   uint32_t* count;
   uint32_t* count_ge2;
-  unsigned long long* cursor;
   uint64_t cap;
   unsigned long long* stats;  // [MAX_RULES][4]: rows, pairs, file_rows, file_rows_ge2
 };
@@ -493,13 +492,10 @@ __global__ __launch_bounds__(256) void k_agg_tiny(const Task* __restrict__ tasks
     }
     const bool emit = first && firstk;
     const uint64_t m = __ballot(emit);
-    unsigned long long base = 0;
-    if (l == 0) base = atomicAdd(O.cursor, (unsigned long long)__popcll(m));
-    base = __shfl(base, 0);
     const RowInfo ri = row_info(row_key, T.row, L.A);
-    if (emit) {
+    if (emit) {  // a task's outputs (<= its words) go to its own word range: no cursor
       const int rule = R.rule_of_type[ri.type][k2 >> L.A];
-      put_row(O, base + mbcnt(m), rule, ri.aid, (int32_t)(k2 & L.amask), call, c2);
+      put_row(O, T.begin + mbcnt(m), rule, ri.aid, (int32_t)(k2 & L.amask), call, c2);
       acc.add(rule, call, nf);
     }
   }
@@ -512,7 +508,8 @@ constexpr int AGG_T = 256;
 constexpr int HCAP = 4096;
 constexpr unsigned long long SLOT_EMPTY = 0xFFFFFFFF00000000ull;
 
-__device__ __forceinline__ uint32_t hash_insert(unsigned long long* slots, uint32_t key, uint32_t inc, uint32_t cm) {
+__device__ __forceinline__ uint32_t hash_insert(unsigned long long* slots, uint32_t key, uint32_t inc, uint32_t cm,
+                                                bool* created = nullptr) {
   uint32_t h = hslot(key, cm);
   while (true) {
     const unsigned long long v = slots[h];
@@ -520,20 +517,28 @@ __device__ __forceinline__ uint32_t hash_insert(unsigned long long* slots, uint3
     if (k == key) { atomicAdd(&slots[h], (unsigned long long)inc); return h; }
     if (k == W_EMPTY) {
       const unsigned long long old = atomicCAS(&slots[h], v, ((unsigned long long)key << 32) | inc);
-      if (old == v) return h;
+      if (old == v) { if (created) *created = true; return h; }
       continue;  // lost the race: re-read this slot
     }
     h = (h + 1) & cm;
   }
 }
 
+// Task lists filled by classification kernels (wave-aggregated pushes)
+struct TaskLists {
+  Task* tiny; Task* hash; Task* split;
+  unsigned long long* n;  // [3]
+  uint64_t cap_tiny, cap_hash, cap_split;
+};
+
 __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tasks, int64_t n_tasks,
                                                     const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
                                                     const uint32_t* __restrict__ row_key, RulesDev R, Layout L,
-                                                    int n_rules, OutRows O) {
+                                                    int n_rules, OutRows O, Task* __restrict__ overflow,
+                                                    unsigned long long* __restrict__ n_overflow) {
   __shared__ unsigned long long lds[2 * HCAP];  // 64 KiB: phase A [0, cap), phase B [0, 2cap)
-  __shared__ uint32_t sbase[2];
   __shared__ uint32_t wtot[AGG_T / 64];
+  __shared__ uint32_t nocc;
   const int tid = threadIdx.x;
   RuleAcc acc;
   acc.zero();
@@ -542,26 +547,44 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
     const uint32_t* W = (T.buf ? w1 : w0) + T.begin;
     uint32_t dbound = T.len;
     if (T.rem < 31 && (1u << T.rem) < dbound) dbound = 1u << T.rem;
+    // optimistic: more keys possible than fit; give up at 3/4 fill and send the task to a split
+    const bool optimistic = 2 * dbound > (uint32_t)HCAP;
     uint32_t cap = 64;
-    while (cap < 2 * dbound) cap <<= 1;
-    const uint32_t cm = cap - 1;
+    while (cap < 2 * dbound && cap < (uint32_t)HCAP) cap <<= 1;
+    const uint32_t cm = cap - 1, limit = (uint32_t)HCAP * 3 / 4;
     unsigned long long* A = lds;
     for (uint32_t i = tid; i < cap; i += AGG_T) A[i] = SLOT_EMPTY;
+    if (tid == 0) nocc = 0;
     __syncthreads();
+    bool full = false;
     for (uint32_t i0 = 0; i0 < T.len; i0 += AGG_T) {
+      // each thread adds at most one key after this check: the table never fills up
+      if (optimistic && nocc > limit) { full = true; break; }
       const uint32_t i = i0 + tid;
       const bool act = i < T.len;
       const uint32_t w = act ? W[i] : W_EMPTY;
-      // wave-uniform word (heavy buckets): one add for the whole wave
       const uint32_t wu = __builtin_amdgcn_readfirstlane(w);
       const uint64_t am = __ballot(act);
-      if (am && __ballot(act && w == wu) == am) {
-        if ((tid & 63) == 0) hash_insert(A, wu, (uint32_t)__popcll(am), cm);
+      bool created = false;
+      if (am && __ballot(act && w == wu) == am) {  // wave-uniform word: one add for the wave
+        if ((tid & 63) == 0) hash_insert(A, wu, (uint32_t)__popcll(am), cm, &created);
       } else if (act) {
-        hash_insert(A, w, 1u, cm);
+        hash_insert(A, w, 1u, cm, &created);
+      }
+      if (optimistic) {
+        const uint32_t nc = (uint32_t)__popcll(__ballot(created));
+        if (nc && (tid & 63) == 0) atomicAdd(&nocc, nc);
       }
     }
-    __syncthreads();
+    full = __syncthreads_or(full);
+    if (full) {
+      if (tid == 0) {
+        const unsigned long long k = atomicAdd(n_overflow, 1ull);
+        overflow[k] = T;  // capacity = number of hash tasks
+      }
+      __syncthreads();
+      continue;
+    }
     constexpr int SL = HCAP / AGG_T;  // 16 slots per thread at most
     uint32_t kw[SL], kc[SL];
 #pragma unroll
@@ -584,21 +607,16 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
       atomicAdd(&B2[h], ((unsigned long long)(c >= 2 ? c : 0u) << 32) | 1ull | ((c >= 2 ? 1ull : 0ull) << 16));
     }
     __syncthreads();
-    // compact and write
+    // compact into the task's own word range (outputs <= words)
     const RowInfo ri = row_info(row_key, T.row, L.A);
     uint32_t mine = 0;
     for (uint32_t i = tid; i < cap; i += AGG_T) mine += (uint32_t)(B[i] >> 32) != W_EMPTY;
     const uint32_t incl = wave_incl_scan(mine);
     if ((tid & 63) == 63) wtot[tid >> 6] = incl;
     __syncthreads();
-    uint32_t pre = 0, tot = 0;
-    for (int k = 0; k < AGG_T / 64; ++k) { if (k < (tid >> 6)) pre += wtot[k]; tot += wtot[k]; }
-    if (tid == 0) {
-      const unsigned long long b = atomicAdd(O.cursor, (unsigned long long)tot);
-      sbase[0] = (uint32_t)b; sbase[1] = (uint32_t)(b >> 32);
-    }
-    __syncthreads();
-    uint64_t p = (((uint64_t)sbase[1] << 32) | sbase[0]) + pre + incl - mine;
+    uint32_t pre = 0;
+    for (int k = 0; k < (tid >> 6); ++k) pre += wtot[k];
+    uint64_t p = T.begin + pre + incl - mine;
     for (uint32_t i = tid; i < cap; i += AGG_T) {
       const unsigned long long v = B[i];
       const uint32_t k2 = (uint32_t)(v >> 32);
@@ -615,50 +633,55 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
 }
 
 // ---- classification of rows and split buckets into task lists
-struct TaskLists {
-  Task* tiny; Task* hash; Task* split;
-  unsigned long long* n;  // [3]
-  uint64_t cap_tiny, cap_hash, cap_split;
-};
 
-__device__ __forceinline__ void push_task(const TaskLists& TL, uint64_t begin, uint64_t len, uint32_t row,
-                                          uint32_t rem, uint32_t buf, int* err) {
-  if (len == 0) return;
+// class of a task: 0 tiny, 1 hash, 2 split (level-0 rows only; sub-buckets hash optimistically)
+__device__ __forceinline__ int task_class(uint64_t len, uint32_t rem, bool is_row) {
+  if (len <= (uint64_t)TINY) return 0;
+  if (len <= (uint64_t)SMALL || rem <= (uint32_t)HASH_REM || !is_row) return 1;
+  return 2;
+}
+// wave-aggregated push: every lane of the wave must call it (valid = has a task)
+__device__ __forceinline__ void push_task_wave(const TaskLists& TL, bool valid, uint64_t begin, uint64_t len,
+                                               uint32_t row, uint32_t rem, uint32_t buf, bool is_row, int* err) {
+  if (valid && len > 0xFFFFFFFFull) { atomicOr(err, 2); valid = false; }
+  const int c = valid ? task_class(len, rem, is_row) : -1;
   Task t; t.begin = begin; t.len = (uint32_t)len; t.row = row; t.rem = rem; t.buf = buf;
-  if (len > 0xFFFFFFFFull) { atomicOr(err, 2); return; }
-  if (len <= (uint64_t)TINY) {
-    const unsigned long long k = atomicAdd(&TL.n[0], 1ull);
-    if (k < TL.cap_tiny) TL.tiny[k] = t; else atomicOr(err, 4);
-  } else if (len <= (uint64_t)SMALL || rem <= (uint32_t)HASH_REM) {
-    const unsigned long long k = atomicAdd(&TL.n[1], 1ull);
-    if (k < TL.cap_hash) TL.hash[k] = t; else atomicOr(err, 4);
-  } else {
-    const unsigned long long k = atomicAdd(&TL.n[2], 1ull);
-    if (k < TL.cap_split) TL.split[k] = t; else atomicOr(err, 4);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const uint64_t m = __ballot(c == q);
+    if (!m) continue;
+    unsigned long long base = 0;
+    if (mbcnt(m) == 0 && c == q) base = atomicAdd(&TL.n[q], (unsigned long long)__popcll(m));
+    const int leader = __ffsll((long long)m) - 1;
+    base = ((unsigned long long)__shfl((uint32_t)(base >> 32), leader) << 32) | __shfl((uint32_t)base, leader);
+    if (c == q) {
+      const unsigned long long k = base + mbcnt(m);
+      Task* list = q == 0 ? TL.tiny : (q == 1 ? TL.hash : TL.split);
+      const uint64_t capq = q == 0 ? TL.cap_tiny : (q == 1 ? TL.cap_hash : TL.cap_split);
+      if (k < capq) list[k] = t; else atomicOr(err, 4);
+    }
   }
 }
 
 __global__ void k_classify_rows(const uint64_t* __restrict__ row_begin, int64_t R, uint64_t P, int WB,
                                 TaskLists TL, int* err) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R) return;
-  const uint64_t b = row_begin[r];
-  const uint64_t e = r + 1 < R ? row_begin[r + 1] : P;
-  push_task(TL, b, e - b, (uint32_t)r, (uint32_t)WB, 0u, err);
+  const bool valid = r < R;
+  uint64_t b = 0, e = 0;
+  if (valid) { b = row_begin[r]; e = r + 1 < R ? row_begin[r + 1] : P; }
+  push_task_wave(TL, valid && e > b, b, e - b, (uint32_t)r, (uint32_t)WB, 0u, true, err);
 }
 
 // split: per task k digit bits, chunks of SPLIT_CH words
 constexpr int SPLIT_CH = 16384;
 constexpr int SPLIT_T = 256;
 
-// First split of a row: enough bits for ~1024-word buckets. A bucket that is still large
-// after a split is dominated by a few keys: take the bits down to HASH_REM (at most 8) at once.
+// Bits for one split: enough for ~1024-word buckets, at most 8 and never below HASH_REM
+// remaining bits (such buckets hash with a guaranteed fit).
 __device__ __forceinline__ int split_bits(const Task& t, int WB) {
-  int k = 8;
-  if ((int)t.rem == WB) {
-    k = 1;
-    while (k < 8 && ((uint64_t)t.len >> k) > 1024) ++k;
-  }
+  (void)WB;
+  int k = 1;
+  while (k < 8 && ((uint64_t)t.len >> k) > 1024) ++k;
   const int maxk = (int)t.rem - HASH_REM;
   if (k > maxk) k = maxk;
   return k < 1 ? 1 : k;
@@ -767,13 +790,18 @@ __global__ void k_split_classify(const Task* __restrict__ tasks, int64_t n, cons
                                  const uint32_t* __restrict__ dcount, const uint64_t* __restrict__ doff,
                                  int64_t n_digits_total, int WB, TaskLists TL, int* err) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_digits_total) return;
-  const uint32_t c = dcount[i];
-  if (!c) return;
-  const int64_t t = find_task(digit_base, n, (uint64_t)i);
-  const Task T = tasks[t];
-  const int k = split_bits(T, WB);
-  push_task(TL, T.begin + (doff[i] - doff[digit_base[t]]), c, T.row, T.rem - (uint32_t)k, T.buf ^ 1u, err);
+  const uint32_t c = i < n_digits_total ? dcount[i] : 0u;
+  Task T;
+  T.begin = 0; T.rem = 0; T.row = 0; T.buf = 0; T.len = 0;
+  uint64_t b = 0;
+  int k = 0;
+  if (c) {
+    const int64_t t = find_task(digit_base, n, (uint64_t)i);
+    T = tasks[t];
+    k = split_bits(T, WB);
+    b = T.begin + (doff[i] - doff[digit_base[t]]);
+  }
+  push_task_wave(TL, c != 0, b, c, T.row, T.rem - (uint32_t)k, T.buf ^ 1u, false, err);
 }
 
 // ------------------------------------------------------------------ per-rule compaction
