@@ -508,20 +508,30 @@ constexpr int AGG_T = 256;
 constexpr int HCAP = 4096;
 constexpr unsigned long long SLOT_EMPTY = 0xFFFFFFFF00000000ull;
 
+__device__ __forceinline__ unsigned long long lds_load(unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Open addressing with linear probing over u64 slots (key << 32 | count). Returns the slot, or
+// HASH_FULL after probing every slot (the caller sends the task to a split: never spins).
+constexpr uint32_t HASH_FULL = 0xFFFFFFFFu;
 __device__ __forceinline__ uint32_t hash_insert(unsigned long long* slots, uint32_t key, uint32_t inc, uint32_t cm,
                                                 bool* created = nullptr) {
   uint32_t h = hslot(key, cm);
-  while (true) {
-    const unsigned long long v = slots[h];
+  unsigned long long v = lds_load(&slots[h]);
+  for (uint32_t probes = 0; probes <= cm;) {
     const uint32_t k = (uint32_t)(v >> 32);
     if (k == key) { atomicAdd(&slots[h], (unsigned long long)inc); return h; }
     if (k == W_EMPTY) {
       const unsigned long long old = atomicCAS(&slots[h], v, ((unsigned long long)key << 32) | inc);
       if (old == v) { if (created) *created = true; return h; }
-      continue;  // lost the race: re-read this slot
+      v = old;  // lost the race: look at what the winner wrote
+      continue;
     }
     h = (h + 1) & cm;
+    ++probes;
+    v = lds_load(&slots[h]);
   }
+  return HASH_FULL;
 }
 
 // Task lists filled by classification kernels (wave-aggregated pushes)
@@ -559,18 +569,23 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
     bool full = false;
     for (uint32_t i0 = 0; i0 < T.len; i0 += AGG_T) {
       // each thread adds at most one key after this check: the table never fills up
-      if (optimistic && nocc > limit) { full = true; break; }
+      if (optimistic && __hip_atomic_load(&nocc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > limit) {
+        full = true;
+        break;
+      }
       const uint32_t i = i0 + tid;
       const bool act = i < T.len;
       const uint32_t w = act ? W[i] : W_EMPTY;
       const uint32_t wu = __builtin_amdgcn_readfirstlane(w);
       const uint64_t am = __ballot(act);
       bool created = false;
+      uint32_t hs = 0;
       if (am && __ballot(act && w == wu) == am) {  // wave-uniform word: one add for the wave
-        if ((tid & 63) == 0) hash_insert(A, wu, (uint32_t)__popcll(am), cm, &created);
+        if ((tid & 63) == 0) hs = hash_insert(A, wu, (uint32_t)__popcll(am), cm, &created);
       } else if (act) {
-        hash_insert(A, w, 1u, cm, &created);
+        hs = hash_insert(A, w, 1u, cm, &created);
       }
+      if (hs == HASH_FULL) { full = true; break; }
       if (optimistic) {
         const uint32_t nc = (uint32_t)__popcll(__ballot(created));
         if (nc && (tid & 63) == 0) atomicAdd(&nocc, nc);
@@ -603,7 +618,8 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
     for (int s = 0; s < SL; ++s) {
       if (kw[s] == W_EMPTY) continue;
       const uint32_t c = kc[s];
-      const uint32_t h = hash_insert(B, kw[s] >> L.F, c, cm);
+      const uint32_t h = hash_insert(B, kw[s] >> L.F, c, cm);  // <= distinct words: always fits
+      if (h == HASH_FULL) continue;
       atomicAdd(&B2[h], ((unsigned long long)(c >= 2 ? c : 0u) << 32) | 1ull | ((c >= 2 ? 1ull : 0ull) << 16));
     }
     __syncthreads();

@@ -164,6 +164,20 @@ def test_heavy_rows_split_and_hash_paths(gpu):
     _assert_single_file(ev, n_items=200_000)
 
 
+def test_hot_row_overflow_resplit(gpu):
+    # a hot aid next to ~1M distinct partners: split buckets overflow the LDS table and are re-split
+    rng = np.random.default_rng(9)
+    n_s, n = 3000, 40
+    rows = []
+    for s in range(n_s):
+        ts = np.sort(rng.integers(0, 3600, n))
+        aid = np.where(np.arange(n) % 2 == 0, 7, rng.integers(0, 1_800_000, n))
+        rows.append(np.stack([np.full(n, s), aid, ts, np.zeros(n, np.int64)], 1))
+    a = np.concatenate(rows)
+    ev = synth.events_from_columns(a[:, 0], a[:, 1], a[:, 2], a[:, 3])
+    _assert_single_file(ev, names=["click_to_click"])
+
+
 def test_dedup_off_matches_pandas_without_unique(gpu):
     df = synth.generate(300, first_session=99).to_pandas()
     df = df._append(df.sample(frac=0.1, random_state=4)).sort_values(["session", "ts"], kind="stable")
