@@ -23,8 +23,10 @@ namespace ottohip {
 constexpr int MAX_RULES = 8;
 constexpr int EV_BLOCK = 256;     // events per wave block (sessions starting in it)
 constexpr int LCAP = 512;         // sessions up to LCAP events run from LDS
-constexpr int TINY = 64;          // rows/buckets up to TINY words: one wave
-constexpr int SMALL = 2048;       // up to SMALL words: one workgroup hash
+constexpr int TINY = 64;          // rows/buckets up to TINY words: one wave, in registers
+constexpr int WAVE_MAX = 512;     // up to WAVE_MAX words: one wave, LDS hash (16 KiB per wave)
+constexpr int SMALL = 2048;       // up to SMALL words: one workgroup, LDS hash
+constexpr int SPLIT_TARGET = 512; // split buckets aim at this many words
 constexpr int HASH_REM = 11;      // buckets whose remaining key bits <= 11 hash directly
 constexpr uint32_t W_EMPTY = 0xFFFFFFFFu;
 
@@ -535,10 +537,105 @@ __device__ __forceinline__ uint32_t hash_insert(unsigned long long* slots, uint3
 }
 
 // Task lists filled by classification kernels (wave-aggregated pushes)
+// one wave per task with TINY < len <= WAVE_MAX: words prefetched to registers, private LDS
+// region per wave (no workgroup barriers), two-phase hash as k_agg_hash
+constexpr int WCAP = 1024;  // phase-A slots per wave (phase B uses 2 * WCAP u64)
+__global__ __launch_bounds__(256) void k_agg_wave(const Task* __restrict__ tasks, int64_t n_tasks,
+                                                  const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
+                                                  const uint32_t* __restrict__ row_key, RulesDev R, Layout L,
+                                                  int n_rules, OutRows O) {
+  __shared__ unsigned long long lds[4][2 * WCAP];  // 64 KiB: 16 KiB per wave
+  const int l = lane_id();
+  const int wv = threadIdx.x >> 6;
+  unsigned long long* A = lds[wv];
+  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  RuleAcc acc;
+  acc.zero();
+  constexpr int NW = WAVE_MAX / 64;  // words per lane
+  for (int64_t ti = gw; ti < n_tasks; ti += nw) {
+    const Task T = tasks[ti];
+    const uint32_t* W = (T.buf ? w1 : w0) + T.begin;
+    uint32_t w[NW];
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+      const uint32_t i = (uint32_t)(l + 64 * j);
+      w[j] = i < T.len ? W[i] : W_EMPTY;
+    }
+    uint32_t dbound = T.len;
+    if (T.rem < 31 && (1u << T.rem) < dbound) dbound = 1u << T.rem;
+    uint32_t cap = 64;
+    while (cap < 2 * dbound) cap <<= 1;
+    const uint32_t cm = cap - 1;
+    for (uint32_t i = l; i < cap; i += 64) A[i] = SLOT_EMPTY;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+      if (64u * j >= T.len) break;
+      const bool act = w[j] != W_EMPTY;
+      const uint32_t wu = __builtin_amdgcn_readfirstlane(w[j]);
+      const uint64_t am = __ballot(act);
+      if (__ballot(act && w[j] == wu) == am) {
+        if (l == 0) hash_insert(A, wu, (uint32_t)__popcll(am), cm);
+      } else if (act) {
+        hash_insert(A, w[j], 1u, cm);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    constexpr int SL = WCAP / 64;  // 16
+    uint32_t kw[SL], kc[SL];
+#pragma unroll
+    for (int q = 0; q < SL; ++q) {
+      const uint32_t slot = (uint32_t)(l + 64 * q);
+      const unsigned long long v = slot < cap ? lds_load(&A[slot]) : SLOT_EMPTY;
+      kw[q] = (uint32_t)(v >> 32);
+      kc[q] = (uint32_t)v;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    unsigned long long* B = A;
+    unsigned long long* B2 = A + cap;
+    for (uint32_t i = l; i < cap; i += 64) { B[i] = SLOT_EMPTY; B2[i] = 0; }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+    for (int q = 0; q < SL; ++q) {
+      if (kw[q] == W_EMPTY) continue;
+      const uint32_t c = kc[q];
+      const uint32_t h = hash_insert(B, kw[q] >> L.F, c, cm);
+      if (h == HASH_FULL) continue;
+      atomicAdd(&B2[h], ((unsigned long long)(c >= 2 ? c : 0u) << 32) | 1ull | ((c >= 2 ? 1ull : 0ull) << 16));
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const RowInfo ri = row_info(row_key, T.row, L.A);
+    uint64_t p = T.begin;
+    for (uint32_t i0 = 0; i0 < cap; i0 += 64) {
+      const uint32_t i = i0 + l;
+      const unsigned long long v = lds_load(&B[i]);
+      const uint32_t k2 = (uint32_t)(v >> 32);
+      const bool valid = k2 != W_EMPTY;
+      const uint64_t m = __ballot(valid);
+      if (valid) {
+        const unsigned long long v2 = lds_load(&B2[i]);
+        const int rule = R.rule_of_type[ri.type][k2 >> L.A];
+        const uint32_t c = (uint32_t)v, c2 = (uint32_t)(v2 >> 32), nf = (uint32_t)v2;
+        put_row(O, p + mbcnt(m), rule, ri.aid, (int32_t)(k2 & L.amask), c, c2);
+        acc.add(rule, c, nf);
+      }
+      p += (uint64_t)__popcll(m);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  acc.flush(O.stats, n_rules);
+}
+
 struct TaskLists {
-  Task* tiny; Task* hash; Task* split;
-  unsigned long long* n;  // [3]
-  uint64_t cap_tiny, cap_hash, cap_split;
+  Task* tiny; Task* hash; Task* split; Task* wave;
+  unsigned long long* n;  // [4]: tiny, hash, split, wave
+  uint64_t cap;           // capacity of every list
 };
 
 __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tasks, int64_t n_tasks,
@@ -567,15 +664,24 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
     if (tid == 0) nocc = 0;
     __syncthreads();
     bool full = false;
-    for (uint32_t i0 = 0; i0 < T.len; i0 += AGG_T) {
+    constexpr int PF = 8;  // words per thread loaded ahead of their inserts
+    uint32_t wbuf[PF];
+    for (uint32_t i0 = 0; i0 < T.len && !full; i0 += AGG_T * PF) {
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        const uint32_t i = i0 + j * AGG_T + tid;
+        wbuf[j] = i < T.len ? W[i] : W_EMPTY;
+      }
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+      if (i0 + j * AGG_T >= T.len) break;
       // each thread adds at most one key after this check: the table never fills up
       if (optimistic && __hip_atomic_load(&nocc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > limit) {
         full = true;
         break;
       }
-      const uint32_t i = i0 + tid;
-      const bool act = i < T.len;
-      const uint32_t w = act ? W[i] : W_EMPTY;
+      const uint32_t w = wbuf[j];
+      const bool act = w != W_EMPTY;
       const uint32_t wu = __builtin_amdgcn_readfirstlane(w);
       const uint64_t am = __ballot(act);
       bool created = false;
@@ -589,6 +695,7 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
       if (optimistic) {
         const uint32_t nc = (uint32_t)__popcll(__ballot(created));
         if (nc && (tid & 63) == 0) atomicAdd(&nocc, nc);
+      }
       }
     }
     full = __syncthreads_or(full);
@@ -650,9 +757,11 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
 
 // ---- classification of rows and split buckets into task lists
 
-// class of a task: 0 tiny, 1 hash, 2 split (level-0 rows only; sub-buckets hash optimistically)
+// class of a task: 0 tiny, 3 wave hash, 1 workgroup hash, 2 split (level-0 rows only; split
+// buckets larger than SMALL hash optimistically and come back as split tasks on overflow)
 __device__ __forceinline__ int task_class(uint64_t len, uint32_t rem, bool is_row) {
   if (len <= (uint64_t)TINY) return 0;
+  if (len <= (uint64_t)WAVE_MAX) return 3;
   if (len <= (uint64_t)SMALL || rem <= (uint32_t)HASH_REM || !is_row) return 1;
   return 2;
 }
@@ -663,7 +772,7 @@ __device__ __forceinline__ void push_task_wave(const TaskLists& TL, bool valid, 
   const int c = valid ? task_class(len, rem, is_row) : -1;
   Task t; t.begin = begin; t.len = (uint32_t)len; t.row = row; t.rem = rem; t.buf = buf;
 #pragma unroll
-  for (int q = 0; q < 3; ++q) {
+  for (int q = 0; q < 4; ++q) {
     const uint64_t m = __ballot(c == q);
     if (!m) continue;
     unsigned long long base = 0;
@@ -672,9 +781,8 @@ __device__ __forceinline__ void push_task_wave(const TaskLists& TL, bool valid, 
     base = ((unsigned long long)__shfl((uint32_t)(base >> 32), leader) << 32) | __shfl((uint32_t)base, leader);
     if (c == q) {
       const unsigned long long k = base + mbcnt(m);
-      Task* list = q == 0 ? TL.tiny : (q == 1 ? TL.hash : TL.split);
-      const uint64_t capq = q == 0 ? TL.cap_tiny : (q == 1 ? TL.cap_hash : TL.cap_split);
-      if (k < capq) list[k] = t; else atomicOr(err, 4);
+      Task* list = q == 0 ? TL.tiny : (q == 1 ? TL.hash : (q == 2 ? TL.split : TL.wave));
+      if (k < TL.cap) list[k] = t; else atomicOr(err, 4);
     }
   }
 }
@@ -697,7 +805,7 @@ constexpr int SPLIT_T = 256;
 __device__ __forceinline__ int split_bits(const Task& t, int WB) {
   (void)WB;
   int k = 1;
-  while (k < 8 && ((uint64_t)t.len >> k) > 1024) ++k;
+  while (k < 8 && ((uint64_t)t.len >> k) > (uint64_t)SPLIT_TARGET) ++k;
   const int maxk = (int)t.rem - HASH_REM;
   if (k > maxk) k = maxk;
   return k < 1 ? 1 : k;
