@@ -26,7 +26,7 @@ constexpr int LCAP = 512;         // sessions up to LCAP events run from LDS
 constexpr int TINY = 64;          // rows/buckets up to TINY words: one wave, in registers
 constexpr int WAVE_MAX = 512;     // up to WAVE_MAX words: one wave, LDS hash (16 KiB per wave)
 constexpr int SMALL = 2048;       // up to SMALL words: one workgroup, LDS hash
-constexpr int SPLIT_TARGET = 512; // split buckets aim at this many words
+constexpr int SPLIT_TARGET = 256; // split buckets aim at this many words
 constexpr int HASH_REM = 11;      // buckets whose remaining key bits <= 11 hash directly
 constexpr uint32_t W_EMPTY = 0xFFFFFFFFu;
 
@@ -537,6 +537,52 @@ __device__ __forceinline__ uint32_t hash_insert(unsigned long long* slots, uint3
 }
 
 // Task lists filled by classification kernels (wave-aggregated pushes)
+// Batched insert of N keys per lane (W_EMPTY = none): the N probe reads are issued together so
+// their LDS latency overlaps; returns the number of slots this lane created; slot[j] gets the
+// slot index (HASH_FULL if the table was full).
+template <int N>
+__device__ __forceinline__ uint32_t hash_insert_batch(unsigned long long* slots, const uint32_t (&key)[N],
+                                                      const uint32_t (&inc)[N], uint32_t cm, uint32_t (&slot)[N]) {
+  uint32_t h[N];
+  bool pend[N];
+  uint32_t probes[N];
+  uint32_t created = 0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    pend[j] = key[j] != W_EMPTY;
+    h[j] = hslot(key[j], cm);
+    probes[j] = 0;
+    slot[j] = HASH_FULL;
+  }
+  while (true) {
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < N; ++j) any |= pend[j];
+    if (!any) break;
+    unsigned long long v[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) v[j] = pend[j] ? lds_load(&slots[h[j]]) : 0ull;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      if (!pend[j]) continue;
+      const uint32_t k = (uint32_t)(v[j] >> 32);
+      if (k == key[j]) {
+        atomicAdd(&slots[h[j]], (unsigned long long)inc[j]);
+        slot[j] = h[j];
+        pend[j] = false;
+      } else if (k == W_EMPTY) {
+        const unsigned long long nv = ((unsigned long long)key[j] << 32) | inc[j];
+        if (atomicCAS(&slots[h[j]], v[j], nv) == v[j]) { slot[j] = h[j]; pend[j] = false; ++created; }
+        // else: retry the same slot with a fresh read
+      } else {
+        h[j] = (h[j] + 1) & cm;
+        if (++probes[j] > cm) pend[j] = false;  // full: slot stays HASH_FULL
+      }
+    }
+  }
+  return created;
+}
+
 // one wave per task with TINY < len <= WAVE_MAX: words prefetched to registers, private LDS
 // region per wave (no workgroup barriers), two-phase hash as k_agg_hash
 constexpr int WCAP = 1024;  // phase-A slots per wave (phase B uses 2 * WCAP u64)
@@ -570,17 +616,20 @@ __global__ __launch_bounds__(256) void k_agg_wave(const Task* __restrict__ tasks
     for (uint32_t i = l; i < cap; i += 64) A[i] = SLOT_EMPTY;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    {
+      uint32_t inc[NW], slot[NW];
 #pragma unroll
-    for (int j = 0; j < NW; ++j) {
-      if (64u * j >= T.len) break;
-      const bool act = w[j] != W_EMPTY;
-      const uint32_t wu = __builtin_amdgcn_readfirstlane(w[j]);
-      const uint64_t am = __ballot(act);
-      if (__ballot(act && w[j] == wu) == am) {
-        if (l == 0) hash_insert(A, wu, (uint32_t)__popcll(am), cm);
-      } else if (act) {
-        hash_insert(A, w[j], 1u, cm);
+      for (int j = 0; j < NW; ++j) {  // a wave-uniform word becomes one add of the wave's count
+        const bool act = w[j] != W_EMPTY;
+        const uint32_t wu = __builtin_amdgcn_readfirstlane(w[j]);
+        const uint64_t am = __ballot(act);
+        inc[j] = 1u;
+        if (am && __ballot(act && w[j] == wu) == am) {
+          inc[j] = (uint32_t)__popcll(am);
+          if (l != 0) w[j] = W_EMPTY;
+        }
       }
+      hash_insert_batch<NW>(A, w, inc, cm, slot);
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -601,12 +650,21 @@ __global__ __launch_bounds__(256) void k_agg_wave(const Task* __restrict__ tasks
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 #pragma unroll
-    for (int q = 0; q < SL; ++q) {
-      if (kw[q] == W_EMPTY) continue;
-      const uint32_t c = kc[q];
-      const uint32_t h = hash_insert(B, kw[q] >> L.F, c, cm);
-      if (h == HASH_FULL) continue;
-      atomicAdd(&B2[h], ((unsigned long long)(c >= 2 ? c : 0u) << 32) | 1ull | ((c >= 2 ? 1ull : 0ull) << 16));
+    for (int q0 = 0; q0 < SL; q0 += 8) {
+      uint32_t k2[8], c8[8], slot[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        k2[j] = kw[q0 + j] == W_EMPTY ? W_EMPTY : kw[q0 + j] >> L.F;
+        c8[j] = kc[q0 + j];
+      }
+      if (64u * q0 >= cap) break;
+      hash_insert_batch<8>(B, k2, c8, cm, slot);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (slot[j] == HASH_FULL) continue;
+        const uint32_t c = c8[j];
+        atomicAdd(&B2[slot[j]], ((unsigned long long)(c >= 2 ? c : 0u) << 32) | 1ull | ((c >= 2 ? 1ull : 0ull) << 16));
+      }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -658,7 +716,7 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
     const bool optimistic = 2 * dbound > (uint32_t)HCAP;
     uint32_t cap = 64;
     while (cap < 2 * dbound && cap < (uint32_t)HCAP) cap <<= 1;
-    const uint32_t cm = cap - 1, limit = (uint32_t)HCAP * 3 / 4;
+    const uint32_t cm = cap - 1, limit = (uint32_t)HCAP / 4;  // + 256 threads x 8 keys stays < HCAP
     unsigned long long* A = lds;
     for (uint32_t i = tid; i < cap; i += AGG_T) A[i] = SLOT_EMPTY;
     if (tid == 0) nocc = 0;
@@ -672,30 +730,29 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
         const uint32_t i = i0 + j * AGG_T + tid;
         wbuf[j] = i < T.len ? W[i] : W_EMPTY;
       }
-#pragma unroll
-      for (int j = 0; j < PF; ++j) {
-      if (i0 + j * AGG_T >= T.len) break;
-      // each thread adds at most one key after this check: the table never fills up
+      // each thread adds at most PF keys after this check: 256 * 8 < HCAP / 4 keeps the table from filling
       if (optimistic && __hip_atomic_load(&nocc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > limit) {
         full = true;
         break;
       }
-      const uint32_t w = wbuf[j];
-      const bool act = w != W_EMPTY;
-      const uint32_t wu = __builtin_amdgcn_readfirstlane(w);
-      const uint64_t am = __ballot(act);
-      bool created = false;
-      uint32_t hs = 0;
-      if (am && __ballot(act && w == wu) == am) {  // wave-uniform word: one add for the wave
-        if ((tid & 63) == 0) hs = hash_insert(A, wu, (uint32_t)__popcll(am), cm, &created);
-      } else if (act) {
-        hs = hash_insert(A, w, 1u, cm, &created);
+      uint32_t inc[PF], slot[PF];
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {  // a wave-uniform word becomes one add of the wave's count
+        const bool act = wbuf[j] != W_EMPTY;
+        const uint32_t wu = __builtin_amdgcn_readfirstlane(wbuf[j]);
+        const uint64_t am = __ballot(act);
+        inc[j] = 1u;
+        if (am && __ballot(act && wbuf[j] == wu) == am) {
+          inc[j] = (uint32_t)__popcll(am);
+          if ((tid & 63) != 0) wbuf[j] = W_EMPTY;
+        }
       }
-      if (hs == HASH_FULL) { full = true; break; }
+      const uint32_t created = hash_insert_batch<PF>(A, wbuf, inc, cm, slot);
+#pragma unroll
+      for (int j = 0; j < PF; ++j) full |= wbuf[j] != W_EMPTY && slot[j] == HASH_FULL;
       if (optimistic) {
-        const uint32_t nc = (uint32_t)__popcll(__ballot(created));
+        const uint32_t nc = wave_sum(created);
         if (nc && (tid & 63) == 0) atomicAdd(&nocc, nc);
-      }
       }
     }
     full = __syncthreads_or(full);
@@ -722,12 +779,21 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
     for (uint32_t i = tid; i < cap; i += AGG_T) { B[i] = SLOT_EMPTY; B2[i] = 0; }
     __syncthreads();
 #pragma unroll
-    for (int s = 0; s < SL; ++s) {
-      if (kw[s] == W_EMPTY) continue;
-      const uint32_t c = kc[s];
-      const uint32_t h = hash_insert(B, kw[s] >> L.F, c, cm);  // <= distinct words: always fits
-      if (h == HASH_FULL) continue;
-      atomicAdd(&B2[h], ((unsigned long long)(c >= 2 ? c : 0u) << 32) | 1ull | ((c >= 2 ? 1ull : 0ull) << 16));
+    for (int s0 = 0; s0 < SL; s0 += 8) {  // <= distinct words: always fits
+      if ((uint32_t)(s0 * AGG_T) >= cap) break;
+      uint32_t k2[8], c8[8], slot[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        k2[j] = kw[s0 + j] == W_EMPTY ? W_EMPTY : kw[s0 + j] >> L.F;
+        c8[j] = kc[s0 + j];
+      }
+      hash_insert_batch<8>(B, k2, c8, cm, slot);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (slot[j] == HASH_FULL) continue;
+        const uint32_t c = c8[j];
+        atomicAdd(&B2[slot[j]], ((unsigned long long)(c >= 2 ? c : 0u) << 32) | 1ull | ((c >= 2 ? 1ull : 0ull) << 16));
+      }
     }
     __syncthreads();
     // compact into the task's own word range (outputs <= words)
