@@ -314,7 +314,7 @@ int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohi
     if ((rc = T->b.alloc(P))) return fail(rc);
   }
   unsigned long long *stats, *lcount;
-  if ((rc = ws.get("stats", MAX_RULES * 4, &stats)) || (rc = ws.get("lcount", 4, &lcount))) return fail(rc);
+  if ((rc = ws.get("stats", MAX_RULES * 4, &stats)) || (rc = ws.get("lcount", 8, &lcount))) return fail(rc);
   hipMemsetAsync(stats, 0, MAX_RULES * 4 * 8, s);
   hipMemsetAsync(T->b.rule, 0xFF, P, s);  // rows are written at their task's word offsets: holes stay 0xFF
   OutRows O;
@@ -323,17 +323,20 @@ int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohi
 
   ph = ctx->begin("reduce", s, 4.0 * (double)P);
   // level 0 task lists come from the rows
-  Task *tiny, *hash, *splitA, *wave;
   uint64_t cap0 = (uint64_t)std::max<int64_t>(Rn, 1);
-  if ((rc = ws.get("t_tiny", cap0 * sizeof(Task), reinterpret_cast<void**>(&tiny))) ||
-      (rc = ws.get("t_hash", cap0 * sizeof(Task), reinterpret_cast<void**>(&hash))) ||
-      (rc = ws.get("t_wave", cap0 * sizeof(Task), reinterpret_cast<void**>(&wave))) ||
-      (rc = ws.get("t_splitA", cap0 * sizeof(Task), reinterpret_cast<void**>(&splitA))))
-    return fail(rc);
   TaskLists TL;
-  TL.tiny = tiny; TL.hash = hash; TL.split = splitA; TL.wave = wave; TL.n = lcount;
-  TL.cap = cap0;
-  hipMemsetAsync(lcount, 0, 4 * 8, s);
+  TL.n = lcount;
+  auto get_lists = [&](uint64_t capl, const char* split_name) -> int {
+    static const char* names[N_SORT] = {"t_sort0", "t_sort1", "t_sort2", "t_sort3", "t_sort4"};
+    for (int c = 0; c < N_SORT; ++c)
+      if (int r = ws.get(names[c], capl * sizeof(Task), reinterpret_cast<void**>(&TL.sort[c]))) return r;
+    if (int r = ws.get("t_hash", capl * sizeof(Task), reinterpret_cast<void**>(&TL.hash))) return r;
+    if (int r = ws.get(split_name, capl * sizeof(Task), reinterpret_cast<void**>(&TL.split))) return r;
+    TL.cap = capl;
+    return 0;
+  };
+  if ((rc = get_lists(cap0, "t_splitA"))) return fail(rc);
+  hipMemsetAsync(lcount, 0, 8 * 8, s);
   k_classify_rows<<<grid_for(Rn), 256, 0, s>>>(row_begin, Rn, P, Lt.WB, TL, err);
   const int agg_grid = ctx->n_cu * 8;
   bool srcA = true;
@@ -341,25 +344,26 @@ int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohi
   const bool dbg = getenv("OTTOHIP_DEBUG") != nullptr;
   if (dbg) fprintf(stderr, "[ottohip] E=%lld P=%llu rows=%lld nlong=%d\n", (long long)E, (unsigned long long)P, (long long)Rn, nl);
   for (int level = 0; level < 40; ++level) {
-    unsigned long long nlist[4];
-    if ((rc = d2h(nlist, lcount, 4, s))) return fail(rc);
-    if (dbg)
-      fprintf(stderr, "[ottohip] level %d: tiny %llu wave %llu hash %llu split %llu\n", level, nlist[0], nlist[3], nlist[1],
-              nlist[2]);
+    unsigned long long nlist[N_SORT + 2];
+    if ((rc = d2h(nlist, lcount, N_SORT + 2, s))) return fail(rc);
     if ((rc = d2h(&herr, err, 1, s))) return fail(rc);
     if (herr) { set_error("task list overflow / row too large (err=%d)", herr); return fail(OTTOHIP_ELIMIT); }
-    if (nlist[0])
-      k_agg_tiny<<<(unsigned)std::min<uint64_t>(ceil_div((int64_t)nlist[0], 4), (uint64_t)ctx->n_cu * 32), 256, 0, s>>>(
-          TL.tiny, (int64_t)nlist[0], w0, w1, row_key, R, Lt, n_rules, O);
-    if (nlist[3])
-      k_agg_wave<<<(unsigned)std::min<uint64_t>(ceil_div((int64_t)nlist[3], 4), (uint64_t)ctx->n_cu * 16), 256, 0, s>>>(
-          TL.wave, (int64_t)nlist[3], w0, w1, row_key, R, Lt, n_rules, O);
-    if (nlist[1]) {  // tasks that overflow the LDS table are appended to the split list
-      k_agg_hash<<<(unsigned)std::min<uint64_t>(nlist[1], (uint64_t)agg_grid), AGG_T, 0, s>>>(
-          TL.hash, (int64_t)nlist[1], w0, w1, row_key, R, Lt, n_rules, O, TL.split, lcount + 2);
-      if ((rc = d2h(nlist, lcount, 4, s))) return fail(rc);
+    if (dbg)
+      fprintf(stderr, "[ottohip] level %d: sort %llu/%llu/%llu/%llu/%llu hash %llu split %llu\n", level, nlist[0],
+              nlist[1], nlist[2], nlist[3], nlist[4], nlist[N_SORT], nlist[N_SORT + 1]);
+    const unsigned sgrid = (unsigned)ctx->n_cu * 32;
+#define OH_SORT(c, M)                                                                                      \
+    if (nlist[c])                                                                                          \
+      k_agg_sort<M><<<(unsigned)std::min<uint64_t>(ceil_div((int64_t)nlist[c], 4), sgrid), 256, 0, s>>>(   \
+          TL.sort[c], (int64_t)nlist[c], w0, w1, row_key, R, Lt, n_rules, O);
+    OH_SORT(0, 1) OH_SORT(1, 2) OH_SORT(2, 4) OH_SORT(3, 8) OH_SORT(4, 16)
+#undef OH_SORT
+    if (nlist[N_SORT]) {  // tasks that overflow the LDS table are appended to the split list
+      k_agg_hash<<<(unsigned)std::min<uint64_t>(nlist[N_SORT], (uint64_t)agg_grid), AGG_T, 0, s>>>(
+          TL.hash, (int64_t)nlist[N_SORT], w0, w1, row_key, R, Lt, n_rules, O, TL.split, lcount + N_SORT + 1);
+      if ((rc = d2h(nlist, lcount, N_SORT + 2, s))) return fail(rc);
     }
-    const int64_t ns = (int64_t)nlist[2];
+    const int64_t ns = (int64_t)nlist[N_SORT + 1];
     if (dbg) fprintf(stderr, "[ottohip] level %d: split after hash overflow %lld\n", level, (long long)ns);
     if (ns == 0) { drained = true; break; }
     if ((uint64_t)ns > TL.cap) { set_error("split list overflow"); return fail(OTTOHIP_ELIMIT); }
@@ -390,16 +394,8 @@ int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohi
     k_split_scatter<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, dgb, w0, w1, Lt.WB, dcur);
     // next lists (a sub-bucket is one task in exactly one list: ndig bounds every list)
     const uint64_t capn = (uint64_t)ndig;
-    Task *ntiny, *nhash, *nsplit, *nwave;
-    const uint64_t capl = std::max(cap0, capn);
-    if ((rc = ws.get("t_tiny", capl * sizeof(Task), reinterpret_cast<void**>(&ntiny))) ||
-        (rc = ws.get("t_hash", capl * sizeof(Task), reinterpret_cast<void**>(&nhash))) ||
-        (rc = ws.get("t_wave", capl * sizeof(Task), reinterpret_cast<void**>(&nwave))) ||
-        (rc = ws.get(srcA ? "t_splitB" : "t_splitA", capl * sizeof(Task), reinterpret_cast<void**>(&nsplit))))
-      return fail(rc);
-    TL.tiny = ntiny; TL.hash = nhash; TL.split = nsplit; TL.wave = nwave;
-    TL.cap = capl;
-    hipMemsetAsync(lcount, 0, 4 * 8, s);
+    if ((rc = get_lists(std::max(cap0, capn), srcA ? "t_splitB" : "t_splitA"))) return fail(rc);
+    hipMemsetAsync(lcount, 0, 8 * 8, s);
     k_split_classify<<<grid_for(ndig), 256, 0, s>>>(cur_split, ns, dgb, dcount, doff, ndig, Lt.WB, TL, err);
     srcA = !srcA;
     if (hipGetLastError() != hipSuccess) { set_error("split launch failed"); return fail(OTTOHIP_EHIP); }

@@ -536,6 +536,150 @@ __device__ __forceinline__ uint32_t hash_insert(unsigned long long* slots, uint3
   return HASH_FULL;
 }
 
+// ---- register sort path: one wave per task of <= 64*M words, no LDS, no atomics
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+  const uint32_t l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = __shfl_up(v, d);
+    if (l >= (uint32_t)d) v = v > t ? v : t;
+  }
+  return v;
+}
+
+// Bitonic sort of 64*M keys held as v[m] = element (lane*M + m), ascending.
+template <int M>
+__device__ __forceinline__ void wave_bitonic_sort(uint32_t (&v)[M]) {
+  constexpr int N = 64 * M;
+  const uint32_t l = lane_id();
+#pragma unroll
+  for (int k = 2; k <= N; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j >= M) {  // partner in lane l ^ (j / M), same register
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          const uint32_t e = l * M + m;
+          const uint32_t o = __shfl_xor(v[m], j / M);
+          const bool up = (e & k) == 0, lower = (e & j) == 0;
+          v[m] = (lower == up) ? (v[m] < o ? v[m] : o) : (v[m] > o ? v[m] : o);
+        }
+      } else {  // partner in this lane
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          if (m & j) continue;
+          const uint32_t e = l * M + m;
+          const bool up = (e & k) == 0;
+          const uint32_t a = v[m], b = v[m ^ j];
+          const bool sw = up ? (a > b) : (a < b);
+          v[m] = sw ? b : a;
+          v[m ^ j] = sw ? a : b;
+        }
+      }
+    }
+  }
+}
+
+// inclusive scan over elements e = lane*M + m (sum or max)
+template <int M, bool MAX>
+__device__ __forceinline__ void wave_scan_elems(uint32_t (&x)[M]) {
+#pragma unroll
+  for (int m = 1; m < M; ++m) x[m] = MAX ? (x[m] > x[m - 1] ? x[m] : x[m - 1]) : x[m] + x[m - 1];
+  const uint32_t tot = x[M - 1];
+  uint32_t incl = MAX ? wave_incl_max(tot) : wave_incl_scan(tot);
+  uint32_t excl = __shfl_up(incl, 1);
+  if (lane_id() == 0) excl = 0;
+#pragma unroll
+  for (int m = 0; m < M; ++m) x[m] = MAX ? (x[m] > excl ? x[m] : excl) : x[m] + excl;
+}
+
+template <int M>
+__global__ __launch_bounds__(256) void k_agg_sort(const Task* __restrict__ tasks, int64_t n_tasks,
+                                                  const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
+                                                  const uint32_t* __restrict__ row_key, RulesDev R, Layout L,
+                                                  int n_rules, OutRows O) {
+  const uint32_t l = lane_id();
+  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  RuleAcc acc;
+  acc.zero();
+  for (int64_t ti = gw; ti < n_tasks; ti += nw) {
+    const Task T = tasks[ti];
+    const uint32_t* W = (T.buf ? w1 : w0) + T.begin;
+    uint32_t v[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {  // coalesced load (element m*64 + l), then sorted anyway
+      const uint32_t i = (uint32_t)(m * 64) + l;
+      v[m] = i < T.len ? W[i] : W_EMPTY;
+    }
+    wave_bitonic_sort<M>(v);
+    // neighbours: previous element (e-1) and next element (e+1)
+    uint32_t prv[M], nxt[M];
+    {
+      const uint32_t pl = __shfl_up(v[M - 1], 1), nl = __shfl_down(v[0], 1);
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        prv[m] = m > 0 ? v[m - 1] : (l == 0 ? W_EMPTY : pl);
+        nxt[m] = m < M - 1 ? v[m + 1] : (l == 63 ? W_EMPTY : nl);
+      }
+    }
+    // w-runs: start index scan; count at each run end
+    uint32_t st[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const uint32_t e = l * M + m;
+      const bool start = v[m] != W_EMPTY && (e == 0 || prv[m] != v[m]);
+      st[m] = start ? e + 1 : 0;  // +1 so that 0 means "none"
+    }
+    wave_scan_elems<M, true>(st);
+    uint32_t X[M], Y[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const uint32_t e = l * M + m;
+      const bool wend = v[m] != W_EMPTY && nxt[m] != v[m];
+      const uint32_t cf = e + 2 - st[m];  // e - start + 1
+      X[m] = wend ? (cf | ((cf >= 2 ? cf : 0u) << 16)) : 0u;
+      Y[m] = wend ? (1u | ((cf >= 2 ? 1u : 0u) << 16)) : 0u;
+    }
+    // fold per-file counts over (rule, aid_next) runs: prefix sums minus the value before the run
+    uint32_t PX[M], PY[M], BX[M], BY[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) { PX[m] = X[m]; PY[m] = Y[m]; }
+    wave_scan_elems<M, false>(PX);
+    wave_scan_elems<M, false>(PY);
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const uint32_t e = l * M + m;
+      const bool kstart = v[m] != W_EMPTY && (e == 0 || (prv[m] >> L.F) != (v[m] >> L.F));
+      BX[m] = kstart ? PX[m] - X[m] : 0u;
+      BY[m] = kstart ? PY[m] - Y[m] : 0u;
+    }
+    wave_scan_elems<M, true>(BX);
+    wave_scan_elems<M, true>(BY);
+    const RowInfo ri = row_info(row_key, T.row, L.A);
+    uint32_t nmine = 0;
+    bool kend[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      kend[m] = v[m] != W_EMPTY && (nxt[m] == W_EMPTY || (nxt[m] >> L.F) != (v[m] >> L.F));
+      nmine += kend[m];
+    }
+    const uint32_t incl = wave_incl_scan(nmine);
+    uint64_t p = T.begin + incl - nmine;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      if (!kend[m]) continue;
+      const uint32_t sx = PX[m] - BX[m], sy = PY[m] - BY[m];
+      const uint32_t k2 = v[m] >> L.F;
+      const int rule = R.rule_of_type[ri.type][k2 >> L.A];
+      const uint32_t c = sx & 0xFFFFu, c2 = sx >> 16;
+      put_row(O, p++, rule, ri.aid, (int32_t)(k2 & L.amask), c, c2);
+      acc.add(rule, c, sy);
+    }
+  }
+  acc.flush(O.stats, n_rules);
+}
+
 // Task lists filled by classification kernels (wave-aggregated pushes)
 // Batched insert of N keys per lane (W_EMPTY = none): the N probe reads are issued together so
 // their LDS latency overlaps; returns the number of slots this lane created; slot[j] gets the
@@ -690,9 +834,13 @@ __global__ __launch_bounds__(256) void k_agg_wave(const Task* __restrict__ tasks
   acc.flush(O.stats, n_rules);
 }
 
+constexpr int N_SORT = 5;  // register-sort classes: 64, 128, 256, 512, 1024 words
+constexpr int SORT_MAX = 64 << (N_SORT - 1);
 struct TaskLists {
-  Task* tiny; Task* hash; Task* split; Task* wave;
-  unsigned long long* n;  // [4]: tiny, hash, split, wave
+  Task* sort[N_SORT];     // register sort by size class
+  Task* hash;             // workgroup LDS hash (heavy buckets)
+  Task* split;            // MSD split
+  unsigned long long* n;  // [N_SORT + 2]: sort classes..., hash, split
   uint64_t cap;           // capacity of every list
 };
 
@@ -823,13 +971,14 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
 
 // ---- classification of rows and split buckets into task lists
 
-// class of a task: 0 tiny, 3 wave hash, 1 workgroup hash, 2 split (level-0 rows only; split
-// buckets larger than SMALL hash optimistically and come back as split tasks on overflow)
+// class of a task: [0, N_SORT) register sort of <= 64 << c words; N_SORT workgroup hash
+// (bounded key range, or a split bucket that stayed large: skewed, hashed optimistically and
+// sent back to a split on overflow); N_SORT + 1 split (rows)
 __device__ __forceinline__ int task_class(uint64_t len, uint32_t rem, bool is_row) {
-  if (len <= (uint64_t)TINY) return 0;
-  if (len <= (uint64_t)WAVE_MAX) return 3;
-  if (len <= (uint64_t)SMALL || rem <= (uint32_t)HASH_REM || !is_row) return 1;
-  return 2;
+  for (int c = 0; c < N_SORT; ++c)
+    if (len <= (uint64_t)(64 << c)) return c;
+  if (rem <= (uint32_t)HASH_REM || !is_row) return N_SORT;
+  return N_SORT + 1;
 }
 // wave-aggregated push: every lane of the wave must call it (valid = has a task)
 __device__ __forceinline__ void push_task_wave(const TaskLists& TL, bool valid, uint64_t begin, uint64_t len,
@@ -838,7 +987,7 @@ __device__ __forceinline__ void push_task_wave(const TaskLists& TL, bool valid, 
   const int c = valid ? task_class(len, rem, is_row) : -1;
   Task t; t.begin = begin; t.len = (uint32_t)len; t.row = row; t.rem = rem; t.buf = buf;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < N_SORT + 2; ++q) {
     const uint64_t m = __ballot(c == q);
     if (!m) continue;
     unsigned long long base = 0;
@@ -847,7 +996,7 @@ __device__ __forceinline__ void push_task_wave(const TaskLists& TL, bool valid, 
     base = ((unsigned long long)__shfl((uint32_t)(base >> 32), leader) << 32) | __shfl((uint32_t)base, leader);
     if (c == q) {
       const unsigned long long k = base + mbcnt(m);
-      Task* list = q == 0 ? TL.tiny : (q == 1 ? TL.hash : (q == 2 ? TL.split : TL.wave));
+      Task* list = q < N_SORT ? TL.sort[q] : (q == N_SORT ? TL.hash : TL.split);
       if (k < TL.cap) list[k] = t; else atomicOr(err, 4);
     }
   }
