@@ -390,13 +390,13 @@ int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohi
     hipMemsetAsync(dcount, 0, ndig * 4, s);
     k_split_hist<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, dgb, w0, w1, Lt.WB, dcount);
     if ((rc = exclusive_scan_u32(ctx, dcount, doff, ndig, nullptr, s))) return fail(rc);
-    k_split_cursor<<<grid_for(ndig), 256, 0, s>>>(cur_split, ns, dgb, doff, dcur, ndig);
+    k_split_cursor<<<grid_for(ns * 64), 256, 0, s>>>(cur_split, ns, dgb, doff, dcur, Lt.WB);
     k_split_scatter<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, dgb, w0, w1, Lt.WB, dcur);
     // next lists (a sub-bucket is one task in exactly one list: ndig bounds every list)
     const uint64_t capn = (uint64_t)ndig;
     if ((rc = get_lists(std::max(cap0, capn), srcA ? "t_splitB" : "t_splitA"))) return fail(rc);
     hipMemsetAsync(lcount, 0, 8 * 8, s);
-    k_split_classify<<<grid_for(ndig), 256, 0, s>>>(cur_split, ns, dgb, dcount, doff, ndig, Lt.WB, TL, err);
+    k_split_classify<<<grid_for(ns * 64), 256, 0, s>>>(cur_split, ns, dgb, dcount, doff, Lt.WB, TL, err);
     srcA = !srcA;
     if (hipGetLastError() != hipSuccess) { set_error("split launch failed"); return fail(OTTOHIP_EHIP); }
   }

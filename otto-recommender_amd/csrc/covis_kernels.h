@@ -1064,13 +1064,16 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_hist(const Task* __restrict__
     if (h[d]) atomicAdd(&dcount[digit_base[t] + d], h[d]);
 }
 
+// one wave per split task: sub-bucket starts of its 2^k digits (cursor for the scatter)
 __global__ void k_split_cursor(const Task* __restrict__ tasks, int64_t n, const uint64_t* __restrict__ digit_base,
-                               const uint64_t* __restrict__ doff, unsigned long long* __restrict__ cur,
-                               int64_t n_digits_total) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_digits_total) return;
-  const int64_t t = find_task(digit_base, n, (uint64_t)i);
-  cur[i] = tasks[t].begin + (doff[i] - doff[digit_base[t]]);
+                               const uint64_t* __restrict__ doff, unsigned long long* __restrict__ cur, int WB) {
+  const int64_t t = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (t >= n) return;
+  const Task T = tasks[t];
+  const uint64_t db = digit_base[t];
+  const int nd = 1 << split_bits(T, WB);
+  const uint64_t d0 = doff[db];
+  for (int d = lane_id(); d < nd; d += 64) cur[db + d] = T.begin + (doff[db + d] - d0);
 }
 
 constexpr int SUB = 4096;  // scatter sub-tile (staged in LDS in digit order)
@@ -1125,22 +1128,23 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
   }
 }
 
+// one wave per split task: push its non-empty sub-buckets as tasks of the next level
 __global__ void k_split_classify(const Task* __restrict__ tasks, int64_t n, const uint64_t* __restrict__ digit_base,
-                                 const uint32_t* __restrict__ dcount, const uint64_t* __restrict__ doff,
-                                 int64_t n_digits_total, int WB, TaskLists TL, int* err) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t c = i < n_digits_total ? dcount[i] : 0u;
-  Task T;
-  T.begin = 0; T.rem = 0; T.row = 0; T.buf = 0; T.len = 0;
-  uint64_t b = 0;
-  int k = 0;
-  if (c) {
-    const int64_t t = find_task(digit_base, n, (uint64_t)i);
-    T = tasks[t];
-    k = split_bits(T, WB);
-    b = T.begin + (doff[i] - doff[digit_base[t]]);
+                                 const uint32_t* __restrict__ dcount, const uint64_t* __restrict__ doff, int WB,
+                                 TaskLists TL, int* err) {
+  const int64_t t = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (t >= n) return;  // wave-uniform
+  const Task T = tasks[t];
+  const uint64_t db = digit_base[t];
+  const int k = split_bits(T, WB);
+  const int nd = 1 << k;
+  const uint64_t d0 = doff[db];
+  for (int d0l = 0; d0l < nd; d0l += 64) {
+    const int d = d0l + (int)lane_id();
+    const uint32_t c = d < nd ? dcount[db + d] : 0u;
+    const uint64_t b = c ? T.begin + (doff[db + d] - d0) : 0;
+    push_task_wave(TL, c != 0, b, c, T.row, T.rem - (uint32_t)k, T.buf ^ 1u, false, err);
   }
-  push_task_wave(TL, c != 0, b, c, T.row, T.rem - (uint32_t)k, T.buf ^ 1u, false, err);
 }
 
 // ------------------------------------------------------------------ per-rule compaction
