@@ -396,7 +396,7 @@ int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohi
     const uint64_t capn = (uint64_t)ndig;
     if ((rc = get_lists(std::max(cap0, capn), srcA ? "t_splitB" : "t_splitA"))) return fail(rc);
     hipMemsetAsync(lcount, 0, 8 * 8, s);
-    k_split_classify<<<grid_for(ns * 64), 256, 0, s>>>(cur_split, ns, dgb, dcount, doff, Lt.WB, TL, err);
+    k_split_classify<<<grid_for(ndig), 256, 0, s>>>(cur_split, ns, dgb, dcount, doff, ndig, Lt.WB, TL, err);
     srcA = !srcA;
     if (hipGetLastError() != hipSuccess) { set_error("split launch failed"); return fail(OTTOHIP_EHIP); }
   }

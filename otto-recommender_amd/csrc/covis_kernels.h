@@ -980,25 +980,36 @@ __device__ __forceinline__ int task_class(uint64_t len, uint32_t rem, bool is_ro
   if (rem <= (uint32_t)HASH_REM || !is_row) return N_SORT;
   return N_SORT + 1;
 }
-// wave-aggregated push: every lane of the wave must call it (valid = has a task)
-__device__ __forceinline__ void push_task_wave(const TaskLists& TL, bool valid, uint64_t begin, uint64_t len,
-                                               uint32_t row, uint32_t rem, uint32_t buf, bool is_row, int* err) {
+// Block-aggregated push: every thread of the (256-thread) block must call it once. Per list:
+// LDS counter per block, then one device atomic per list per block.
+constexpr int N_LISTS = N_SORT + 2;
+__device__ __forceinline__ void push_task_block(const TaskLists& TL, bool valid, uint64_t begin, uint64_t len,
+                                                uint32_t row, uint32_t rem, uint32_t buf, bool is_row, int* err) {
+  __shared__ uint32_t bcnt[N_LISTS];
+  __shared__ unsigned long long bbase[N_LISTS];
   if (valid && len > 0xFFFFFFFFull) { atomicOr(err, 2); valid = false; }
   const int c = valid ? task_class(len, rem, is_row) : -1;
-  Task t; t.begin = begin; t.len = (uint32_t)len; t.row = row; t.rem = rem; t.buf = buf;
+  if (threadIdx.x < N_LISTS) bcnt[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t my = 0;
 #pragma unroll
-  for (int q = 0; q < N_SORT + 2; ++q) {
+  for (int q = 0; q < N_LISTS; ++q) {
     const uint64_t m = __ballot(c == q);
     if (!m) continue;
-    unsigned long long base = 0;
-    if (mbcnt(m) == 0 && c == q) base = atomicAdd(&TL.n[q], (unsigned long long)__popcll(m));
-    const int leader = __ffsll((long long)m) - 1;
-    base = ((unsigned long long)__shfl((uint32_t)(base >> 32), leader) << 32) | __shfl((uint32_t)base, leader);
-    if (c == q) {
-      const unsigned long long k = base + mbcnt(m);
-      Task* list = q < N_SORT ? TL.sort[q] : (q == N_SORT ? TL.hash : TL.split);
-      if (k < TL.cap) list[k] = t; else atomicOr(err, 4);
-    }
+    uint32_t wb = 0;
+    if (mbcnt(m) == 0 && c == q) wb = atomicAdd(&bcnt[q], (uint32_t)__popcll(m));
+    wb = __shfl(wb, __ffsll((long long)m) - 1);
+    if (c == q) my = wb + mbcnt(m);
+  }
+  __syncthreads();
+  if (threadIdx.x < N_LISTS && bcnt[threadIdx.x])
+    bbase[threadIdx.x] = atomicAdd(&TL.n[threadIdx.x], (unsigned long long)bcnt[threadIdx.x]);
+  __syncthreads();
+  if (c >= 0) {
+    const unsigned long long k = bbase[c] + my;
+    Task t; t.begin = begin; t.len = (uint32_t)len; t.row = row; t.rem = rem; t.buf = buf;
+    Task* list = c < N_SORT ? TL.sort[c] : (c == N_SORT ? TL.hash : TL.split);
+    if (k < TL.cap) list[k] = t; else atomicOr(err, 4);
   }
 }
 
@@ -1008,7 +1019,7 @@ __global__ void k_classify_rows(const uint64_t* __restrict__ row_begin, int64_t 
   const bool valid = r < R;
   uint64_t b = 0, e = 0;
   if (valid) { b = row_begin[r]; e = r + 1 < R ? row_begin[r + 1] : P; }
-  push_task_wave(TL, valid && e > b, b, e - b, (uint32_t)r, (uint32_t)WB, 0u, true, err);
+  push_task_block(TL, valid && e > b, b, e - b, (uint32_t)r, (uint32_t)WB, 0u, true, err);
 }
 
 // split: per task k digit bits, chunks of SPLIT_CH words
@@ -1128,23 +1139,23 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
   }
 }
 
-// one wave per split task: push its non-empty sub-buckets as tasks of the next level
+// one thread per (split task, digit): push the non-empty sub-buckets as next-level tasks
 __global__ void k_split_classify(const Task* __restrict__ tasks, int64_t n, const uint64_t* __restrict__ digit_base,
-                                 const uint32_t* __restrict__ dcount, const uint64_t* __restrict__ doff, int WB,
-                                 TaskLists TL, int* err) {
-  const int64_t t = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (t >= n) return;  // wave-uniform
-  const Task T = tasks[t];
-  const uint64_t db = digit_base[t];
-  const int k = split_bits(T, WB);
-  const int nd = 1 << k;
-  const uint64_t d0 = doff[db];
-  for (int d0l = 0; d0l < nd; d0l += 64) {
-    const int d = d0l + (int)lane_id();
-    const uint32_t c = d < nd ? dcount[db + d] : 0u;
-    const uint64_t b = c ? T.begin + (doff[db + d] - d0) : 0;
-    push_task_wave(TL, c != 0, b, c, T.row, T.rem - (uint32_t)k, T.buf ^ 1u, false, err);
+                                 const uint32_t* __restrict__ dcount, const uint64_t* __restrict__ doff,
+                                 int64_t n_digits_total, int WB, TaskLists TL, int* err) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t c = i < n_digits_total ? dcount[i] : 0u;
+  Task T;
+  T.begin = 0; T.rem = 0; T.row = 0; T.buf = 0; T.len = 0;
+  uint64_t b = 0;
+  int k = 0;
+  if (c) {
+    const int64_t t = find_task(digit_base, n, (uint64_t)i);
+    T = tasks[t];
+    k = split_bits(T, WB);
+    b = T.begin + (doff[i] - doff[digit_base[t]]);
   }
+  push_task_block(TL, c != 0, b, c, T.row, T.rem - (uint32_t)k, T.buf ^ 1u, false, err);
 }
 
 // ------------------------------------------------------------------ per-rule compaction
