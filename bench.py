@@ -41,6 +41,61 @@ def cpu_baseline(ev_sessions: int, n_files: int, seed: int = 0) -> dict:
                       f"of the same stream, oracle/covis_oracle.c per-file count, {dt:.1f} s"}
 
 
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def bench_knn(steps: int, warmup: int, n_items: int, n_q: int, with_cpu: bool) -> dict:
+    """BASELINE configs[2]: W2V top-20 kNN, 1.8M x 100 items, first 600k vocabulary rows as
+    queries (config.py:125; model/w2vec_aids.py:203), one model per step."""
+    import torch
+    import otto_recommender_amd.synth as synth
+    from otto_recommender_amd import _lib
+    from otto_recommender_amd.w2vec import KnnIndex
+    ctx = _lib.context()
+    emb = synth.embeddings(n_items)
+    index = KnnIndex(emb, ctx)
+    for _ in range(warmup):
+        index.search(None, n_q=n_q, k=20)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        idx, d2 = index.search(None, n_q=n_q, k=20)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    ctx.set_timing(True)
+    index.search(None, n_q=n_q, k=20)
+    ph = {n: ms for n, ms, _ in ctx.timings()}
+    ctx.set_timing(False)
+    flops = 2.0 * n_q * n_items * emb.shape[1]
+    main_ms = ph.get("knn_main", dt * 1e3)
+    out = {"metric": "W2V top-20 kNN queries/s (exact, bf16 MFMA + fp32 rerank)", "value": n_q / dt,
+           "unit": "queries/s", "ms_per_step": dt * 1e3, "steps": steps,
+           "config": {"workload": "configs[2]: 1.86M items x 100-d, 600k queries, k=20", "items": n_items,
+                      "queries": n_q, "k": 20},
+           "dtype": "bf16 (fp32 accumulate, fp32 rerank)",
+           "roofline": {"bound": "mfma", "kernel": "k_knn_main", "achieved": flops / (main_ms / 1e3) / 1e12,
+                        "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": flops / (main_ms / 1e3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, "traffic": None,
+                        "flops_model": "2*Q*V*100 (K padding to 128 and the top-k epilogue not counted)"},
+           "phases_ms": {k: round(v, 3) for k, v in ph.items()},
+           "reference_faiss_ivf_queries_per_s": 705}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import knn as oracle_knn  # checker / baseline only
+        nq_cpu = 2000
+        t0 = time.perf_counter()
+        ri, _ = oracle_knn.topk_exact(emb, np.arange(nq_cpu), 20)
+        tc = time.perf_counter() - t0
+        gi = idx[:nq_cpu].cpu().numpy()
+        out["sample_exact_match"] = float(np.mean([set(a) == set(b) for a, b in zip(gi, ri)]))
+        out["cpu_baseline"] = {"value": nq_cpu / tc, "unit": "queries/s", "cores": torch.get_num_threads(),
+                               "kind": "port",
+                               "sample": f"{nq_cpu} queries, exact brute force (oracle/knn.py: torch-CPU fp32 "
+                                         f"preselect + fp64 rerank), {tc:.1f} s"}
+    index.free()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -50,6 +105,9 @@ def main():
     ap.add_argument("--cpu-files", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--knn-steps", type=int, default=2, help="0 disables the configs[2] kNN measurement")
+    ap.add_argument("--knn-items", type=int, default=1_855_603)
+    ap.add_argument("--knn-queries", type=int, default=600_000)
     args = ap.parse_args()
 
     import torch
@@ -163,6 +221,10 @@ def main():
     }
     if not args.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(n_sess, args.cpu_files, args.seed)
+    if args.knn_steps > 0 and world == 1:
+        del dev
+        torch.cuda.empty_cache()
+        out["knn"] = bench_knn(args.knn_steps, 1, args.knn_items, args.knn_queries, not args.no_cpu)
     print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

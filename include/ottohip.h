@@ -115,6 +115,21 @@ int ottohip_table_finalize(ottohip_ctx* ctx, const ottohip_table* t, int rule,
                            const ottohip_merge_params* mp, int32_t* aid, int32_t* aid_next,
                            int32_t* count, int64_t* n_out, void* stream);
 
+/* ---- Word2Vec top-K similarity (model/w2vec_aids.py:98-173) ------------------------------
+ * Replaces load_index_faiss_ivff (:98-110) + get_top_k_similar_faiss (:125-173): exact L2
+ * search (the reference's IVFFlat nlist 100 / nprobe 3 is approximate). The index packs the
+ * caller's fp32 embeddings [n_items x dim] (device, kept referenced) into a bf16 MFMA operand;
+ * ottohip_knn_topk returns, per query row, the k nearest rows in ascending squared L2
+ * distance (ties by row index), distances exact in fp32 (candidates from bf16 MFMA scores,
+ * reranked). dim <= 126, k <= 64. query_rows (device, n_q) index the embedding rows
+ * (get_top_k_similar_faiss queries words_q, a subset of words); NULL = rows 0..n_q-1. */
+typedef struct ottohip_knn_index ottohip_knn_index;
+int ottohip_knn_index_create(ottohip_ctx* ctx, const float* emb, int64_t n_items, int dim,
+                             ottohip_knn_index** out, void* stream);
+int ottohip_knn_topk(ottohip_ctx* ctx, const ottohip_knn_index* index, const int32_t* query_rows,
+                     int64_t n_q, int k, int32_t* out_idx, float* out_d2, void* stream);
+void ottohip_knn_index_free(ottohip_knn_index* index);
+
 /* Test hooks for the device primitives the engine is built from (parity tests only). */
 int ottohip_test_exclusive_scan_u32(ottohip_ctx* ctx, const uint32_t* in, uint64_t* out, int64_t n,
                                     uint64_t* total_host, void* stream);

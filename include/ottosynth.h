@@ -36,6 +36,8 @@ int64_t otto_synth_sessions_for_events(const otto_synth_params* p, int64_t s0, i
  * output index 0); session may be NULL */
 int otto_synth_fill(const otto_synth_params* p, int64_t s0, int64_t n, const int64_t* offsets,
                     int32_t* session, int32_t* aid, int32_t* ts, int8_t* type);
+/* item embeddings [n x dim] fp32, row i = frequency rank i (config 3 of SURVEY.md §8(d)) */
+int otto_synth_embeddings(uint64_t seed, int64_t n, int dim, int n_clusters, float* out);
 /* aid -> popularity rank (inverse of the generator's rank -> aid permutation) */
 int otto_synth_item_rank(const otto_synth_params* p, int32_t* rank_of_aid);
 

@@ -63,6 +63,9 @@ SIGNATURES = {
     "ottohip_table_free": (None, [_VP]),
     "ottohip_table_finalize": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.POINTER(MergeParams), _VP, _VP, _VP,
                                               ctypes.POINTER(_I64), _VP]),
+    "ottohip_knn_index_create": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, ctypes.POINTER(_VP), _VP]),
+    "ottohip_knn_topk": (ctypes.c_int, [_VP, _VP, _VP, _I64, ctypes.c_int, _VP, _VP, _VP]),
+    "ottohip_knn_index_free": (None, [_VP]),
     "ottohip_test_exclusive_scan_u32": (ctypes.c_int, [_VP, _VP, _VP, _I64, ctypes.POINTER(ctypes.c_uint64), _VP]),
     "ottohip_test_radix_sort_pairs": (ctypes.c_int, [_VP, _VP, _VP, _I64, ctypes.c_int, _VP]),
 }

@@ -49,6 +49,9 @@ struct TableBufs {
 struct ottohip_ctx : public Ctx {
   TableBufs spare;  // buffers of the last freed table, reused by the next count
 };
+namespace ottohip {
+Ctx* ctx_base(ottohip_ctx* c) { return c; }
+}
 
 struct ottohip_table {
   int device = 0;

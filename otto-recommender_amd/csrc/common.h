@@ -13,6 +13,8 @@
 namespace ottohip {
 
 void set_error(const char* fmt, ...);
+struct Ctx;
+Ctx* ctx_base(ottohip_ctx* c);  // abi.hip
 
 #define OH_HIP(expr)                                                              \
   do {                                                                            \

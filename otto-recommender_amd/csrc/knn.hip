@@ -1,0 +1,252 @@
+// Word2Vec top-K neighbour search on gfx950 MFMA (model/w2vec_aids.py:125-173).
+//
+// The reference searches a faiss IVFFlat index (nlist 100, nprobe 3, METRIC_L2) for the first
+// 600k vocabulary rows, k = 20 (w2vec_aids.py:98-110,164). This engine is exact:
+//   1. k_knn_pack: items -> bf16 [V x 128]; columns [0, dim) = v, columns dim, dim+1 = hi/lo
+//      bf16 split of -|v|^2 / 2, rest 0. Queries -> bf16 [Q x 128] with 1, 1 in those columns.
+//      One MFMA product then gives s = q.v - |v|^2/2, and |q - v|^2 = |q|^2 - 2 s ranks like -s.
+//   2. k_knn_main: v_mfma_f32_32x32x16_bf16 with items as A (64-item tiles staged through LDS,
+//      XOR-swizzled 16-B chunks, double-buffered) and 32 queries per wave held in registers
+//      as B; accumulator lane = query, 16 item scores per lane. Each lane keeps the best 32
+//      scores it saw (threshold test, rare register insert): 64 candidates per query.
+//   3. k_knn_rerank: one wave per query recomputes |q - v|^2 exactly in fp32 for the 64
+//      candidates and sorts by (d2, index): the top-k rows and their exact squared distances.
+#include <cmath>
+#include "common.h"
+
+namespace ottohip {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int KN_KD = 128;               // padded K (bf16 per row)
+constexpr int KN_CH = KN_KD * 2 / 16;    // 16-B chunks per row (16)
+constexpr int KN_QW = 32;                // queries per wave
+constexpr int KN_WAVES = 8;
+constexpr int KN_T = 64 * KN_WAVES;      // 512 threads
+constexpr int KN_QB = KN_QW * KN_WAVES;  // 256 queries per workgroup
+constexpr int KN_IT = 64;                // items per LDS tile
+constexpr int KN_C = 32;                 // candidates per lane (64 per query)
+constexpr int KN_CAND = 2 * KN_C;
+
+__device__ __forceinline__ uint16_t f2bf(float f) {  // round to nearest even
+  uint32_t u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+__device__ __forceinline__ float bf2f(uint16_t b) { return __uint_as_float((uint32_t)b << 16); }
+
+// items (rows of emb) -> packed bf16 with the -|v|^2/2 columns; or queries (rows[q]) with 1, 1
+__global__ void k_knn_pack(const float* __restrict__ emb, int64_t n, int dim, const int32_t* __restrict__ rows,
+                           int is_query, uint16_t* __restrict__ out) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (i >= n) return;
+  const int l = threadIdx.x & 63;
+  const int64_t src = rows ? rows[i] : i;
+  const float* v = emb + src * dim;
+  float ss = 0.f;
+  for (int d = l; d < KN_KD; d += 64) {
+    float x = d < dim ? v[d] : 0.f;
+    ss += x * x;
+    out[i * KN_KD + d] = d < dim ? f2bf(x) : 0;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
+  if (l == 0) {
+    if (is_query) {
+      out[i * KN_KD + dim] = f2bf(1.f);
+      out[i * KN_KD + dim + 1] = f2bf(1.f);
+    } else {
+      const float nh = -0.5f * ss;
+      const uint16_t hi = f2bf(nh);
+      out[i * KN_KD + dim] = hi;
+      out[i * KN_KD + dim + 1] = f2bf(nh - bf2f(hi));
+    }
+  }
+}
+
+__global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ items, int64_t V,
+                                                  const uint4* __restrict__ queries, int64_t nq,
+                                                  uint32_t* __restrict__ cand) {
+  __shared__ uint4 tile[2][KN_IT * KN_CH];  // 2 x 16 KiB
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, r = l & 31, h = l >> 5;
+  const int64_t q = (int64_t)blockIdx.x * KN_QB + w * KN_QW + r;
+  bf16x8 bq[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    uint4 u = make_uint4(0, 0, 0, 0);
+    if (q < nq) u = queries[q * KN_CH + 2 * s + h];
+    bq[s] = __builtin_bit_cast(bf16x8, u);
+  }
+  float sc[KN_C];
+  uint32_t ix[KN_C];
+#pragma unroll
+  for (int j = 0; j < KN_C; ++j) { sc[j] = -INFINITY; ix[j] = 0xFFFFFFFFu; }
+  float thr = -INFINITY;
+  int tpos = 0;
+  const int64_t nT = ceil_div(V, KN_IT);
+  uint4 st[2];
+  auto load = [&](int64_t t) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int p = tid + KN_T * u, row = p >> 4, c = p & 15;
+      const int64_t item = t * KN_IT + row;
+      st[u] = item < V ? items[item * KN_CH + (c ^ (row & 15))] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store = [&](int b) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) tile[b][tid + KN_T * u] = st[u];
+  };
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int64_t t = 0; t < nT; ++t) {
+    if (t + 1 < nT) load(t + 1);
+    const uint4* T = tile[t & 1];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      f32x16 acc = {};
+      const int row = rb * 32 + r;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const uint4 a = T[row * KN_CH + ((2 * s + h) ^ (row & 15))];
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), bq[s], acc, 0, 0, 0);
+      }
+      const int64_t ib = t * KN_IT + rb * 32 + 4 * h;
+      bool any = false;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) any |= acc[i] > thr;
+      if (any) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float s_ = acc[i];
+          const int64_t item = ib + (i & 3) + 8 * (i >> 2);
+          if (s_ > thr && item < V) {
+#pragma unroll
+            for (int j = 0; j < KN_C; ++j)
+              if (j == tpos) { sc[j] = s_; ix[j] = (uint32_t)item; }
+            thr = sc[0]; tpos = 0;
+#pragma unroll
+            for (int j = 1; j < KN_C; ++j)
+              if (sc[j] < thr) { thr = sc[j]; tpos = j; }
+          }
+        }
+      }
+    }
+    if (t + 1 < nT) store((int)((t + 1) & 1));
+    __syncthreads();
+  }
+  if (q < nq) {
+#pragma unroll
+    for (int j = 0; j < KN_C; ++j) cand[q * KN_CAND + h * KN_C + j] = ix[j];
+  }
+}
+
+// one wave per query: exact fp32 |q - v|^2 of the 64 candidates, sorted by (d2, index)
+__global__ __launch_bounds__(256) void k_knn_rerank(const float* __restrict__ emb, int64_t V, int dim,
+                                                    const int32_t* __restrict__ qrows, int64_t nq,
+                                                    const uint32_t* __restrict__ cand, int k,
+                                                    int32_t* __restrict__ out_idx, float* __restrict__ out_d2) {
+  const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (q >= nq) return;
+  const uint32_t l = lane_id();
+  const uint32_t c = cand[q * KN_CAND + l];
+  const float* qv = emb + (int64_t)(qrows ? qrows[q] : q) * dim;
+  float d2 = INFINITY;
+  if (c < (uint32_t)V) {
+    const float* v = emb + (int64_t)c * dim;
+    float acc = 0.f;
+    for (int d = 0; d < dim; ++d) {
+      const float t = qv[d] - v[d];
+      acc = fmaf(t, t, acc);
+    }
+    d2 = acc;
+  }
+  // bitonic sort of 64 (d2 bits, index) keys; d2 >= 0 so its bits order like the float
+  uint64_t key = ((uint64_t)__float_as_uint(d2) << 32) | c;
+#pragma unroll
+  for (int kk = 2; kk <= 64; kk <<= 1) {
+#pragma unroll
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      const uint64_t o = shfl64(key, (int)(l ^ (uint32_t)j));
+      const bool up = (l & kk) == 0, lower = (l & j) == 0;
+      key = (lower == up) ? (key < o ? key : o) : (key > o ? key : o);
+    }
+  }
+  if ((int)l < k) {
+    const uint32_t idx = (uint32_t)key;
+    out_idx[q * k + l] = idx < (uint32_t)V ? (int32_t)idx : -1;
+    out_d2[q * k + l] = __uint_as_float((uint32_t)(key >> 32));
+  }
+}
+
+}  // namespace ottohip
+
+using namespace ottohip;
+
+extern "C" {
+
+struct ottohip_knn_index {
+  int device;
+  int64_t n_items;
+  int dim;
+  const float* emb;      // caller-owned fp32 [n_items x dim]
+  uint16_t* packed;      // bf16 [n_items x 128]
+};
+
+int ottohip_knn_index_create(ottohip_ctx* c, const float* emb, int64_t n_items, int dim,
+                             ottohip_knn_index** out, void* stream) {
+  if (!c || !emb || !out || n_items < 1 || dim < 1 || dim > KN_KD - 2 || n_items >= (int64_t)0xFFFFFFFFu) {
+    set_error("knn_index_create: bad arguments (dim must be <= %d)", KN_KD - 2);
+    return OTTOHIP_EINVAL;
+  }
+  Ctx* ctx = ctx_base(c);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  ottohip_knn_index* ix = new ottohip_knn_index();
+  ix->device = ctx->device; ix->n_items = n_items; ix->dim = dim; ix->emb = emb;
+  if (hipMalloc(&ix->packed, (size_t)n_items * KN_KD * 2) != hipSuccess) {
+    delete ix; set_error("knn_index_create: allocation failed"); return OTTOHIP_ENOMEM;
+  }
+  k_knn_pack<<<(unsigned)ceil_div(n_items * 64, 256), 256, 0, s>>>(emb, n_items, dim, nullptr, 0, ix->packed);
+  OH_HIP(hipGetLastError());
+  *out = ix;
+  return 0;
+}
+
+void ottohip_knn_index_free(ottohip_knn_index* ix) {
+  if (!ix) return;
+  (void)hipSetDevice(ix->device);
+  (void)hipDeviceSynchronize();
+  (void)hipFree(ix->packed);
+  delete ix;
+}
+
+int ottohip_knn_topk(ottohip_ctx* c, const ottohip_knn_index* ix, const int32_t* query_rows, int64_t n_q, int k,
+                     int32_t* out_idx, float* out_d2, void* stream) {
+  if (!c || !ix || n_q < 0 || k < 1 || k > KN_CAND || !out_idx || !out_d2) {
+    set_error("knn_topk: bad arguments (1 <= k <= %d)", KN_CAND);
+    return OTTOHIP_EINVAL;
+  }
+  if (n_q == 0) return 0;
+  Ctx* ctx = ctx_base(c);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  uint16_t* qp;
+  uint32_t* cand;
+  OH_TRY(ctx->ws.get("knn_q", (size_t)n_q * KN_KD * 2, reinterpret_cast<void**>(&qp)));
+  OH_TRY(ctx->ws.get("knn_cand", (size_t)n_q * KN_CAND, &cand));
+  int ph = ctx->begin("knn_pack", s, 0);
+  k_knn_pack<<<(unsigned)ceil_div(n_q * 64, 256), 256, 0, s>>>(ix->emb, n_q, ix->dim, query_rows, 1, qp);
+  ctx->end(ph, s);
+  ph = ctx->begin("knn_main", s, 2.0 * (double)n_q * (double)ix->n_items * ix->dim);
+  k_knn_main<<<(unsigned)ceil_div(n_q, KN_QB), KN_T, 0, s>>>(reinterpret_cast<const uint4*>(ix->packed), ix->n_items,
+                                                             reinterpret_cast<const uint4*>(qp), n_q, cand);
+  ctx->end(ph, s);
+  ph = ctx->begin("knn_rerank", s, 0);
+  k_knn_rerank<<<(unsigned)ceil_div(n_q * 64, 256), 256, 0, s>>>(ix->emb, ix->n_items, ix->dim, query_rows, n_q, cand,
+                                                                 k, out_idx, out_d2);
+  ctx->end(ph, s);
+  OH_HIP(hipGetLastError());
+  return 0;
+}
+}  // extern "C"

@@ -48,7 +48,7 @@ inline double normal(uint64_t h1, uint64_t h2) {
 }
 
 enum : uint64_t { ST_LEN = 1, ST_START, ST_GAP_KIND, ST_GAP_A, ST_GAP_B, ST_TYPE, ST_REVISIT,
-                  ST_REVISIT_PICK, ST_ITEM, ST_DUP, ST_PERM };
+                  ST_REVISIT_PICK, ST_ITEM, ST_DUP, ST_PERM, ST_CENTER, ST_CLUSTER, ST_NOISE };
 
 struct ItemTable {
   uint64_t seed = 0; int64_t n = 0; double off = 0, ex = 0;
@@ -174,6 +174,36 @@ int otto_synth_fill(const otto_synth_params* p, int64_t s0, int64_t n, const int
         aid[e] = perm[r];
       }
     }
+  }
+  return 0;
+}
+
+int otto_synth_embeddings(uint64_t seed, int64_t n, int dim, int n_clusters, float* out) {
+  // Item embeddings for config 3: row i = vocabulary rank i (gensim's
+  // index_to_key is frequency-sorted, model/w2vec_aids.py:198-199). A mixture of n_clusters
+  // Gaussian clusters; the vector norm is 0.5 + 3 (1 - i/n)^2, so rarer items sit closer to
+  // the origin (model/w2vec_aids.py:144-148).
+  if (!out || n < 1 || dim < 1 || n_clusters < 1) return -1;
+  std::vector<float> cen((size_t)n_clusters * dim);
+  for (int j = 0; j < n_clusters; ++j)
+    for (int d = 0; d < dim; ++d)
+      cen[(size_t)j * dim + d] = (float)normal(draw(seed, ST_CENTER, (uint64_t)j, 2 * (uint64_t)d),
+                                               draw(seed, ST_CENTER, (uint64_t)j, 2 * (uint64_t)d + 1));
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; ++i) {
+    const int c = (int)(draw(seed, ST_CLUSTER, (uint64_t)i, 0) % (uint64_t)n_clusters);
+    float* v = out + i * dim;
+    double ss = 0;
+    for (int d = 0; d < dim; ++d) {
+      const double z = normal(draw(seed, ST_NOISE, (uint64_t)i, 2 * (uint64_t)d),
+                              draw(seed, ST_NOISE, (uint64_t)i, 2 * (uint64_t)d + 1));
+      const double x = cen[(size_t)c * dim + d] + 0.7 * z;
+      v[d] = (float)x;
+      ss += x * x;
+    }
+    const double f = 1.0 - (double)i / (double)n;
+    const double scale = (0.5 + 3.0 * f * f) / std::sqrt(ss > 0 ? ss : 1.0);
+    for (int d = 0; d < dim; ++d) v[d] = (float)(v[d] * scale);
   }
   return 0;
 }

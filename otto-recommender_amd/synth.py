@@ -51,6 +51,8 @@ def _lib():
         lib.otto_synth_sessions_for_events.restype = ctypes.c_int64
         lib.otto_synth_fill.argtypes = [P, ctypes.c_int64, ctypes.c_int64] + [ctypes.c_void_p] * 5
         lib.otto_synth_item_rank.argtypes = [P, ctypes.c_void_p]
+        lib.otto_synth_embeddings.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_void_p]
         _LIB = lib
     return _LIB
 
@@ -137,6 +139,22 @@ def item_rank(seed: int = 0, n_items: int = 1855603) -> np.ndarray:
     r = np.empty(n_items, np.int32)
     _lib().otto_synth_item_rank(ctypes.byref(p), r.ctypes.data)
     return r
+
+
+def item_words(seed: int = 0, n_items: int = 1855603) -> np.ndarray:
+    """Synthetic vocabulary in gensim index_to_key order (frequency-sorted): words[rank] = aid."""
+    r = item_rank(seed, n_items)
+    words = np.empty(n_items, np.int32)
+    words[r] = np.arange(n_items, dtype=np.int32)
+    return words
+
+
+def embeddings(n: int = 1855603, dim: int = 100, seed: int = 1, n_clusters: int = 1000) -> np.ndarray:
+    """Config-3 item embeddings (float32 [n, dim]), row i = vocabulary rank i."""
+    out = np.empty((n, dim), np.float32)
+    if _lib().otto_synth_embeddings(seed, n, dim, n_clusters, out.ctypes.data) != 0:
+        raise RuntimeError("otto_synth_embeddings failed")
+    return out
 
 
 SESSIONS_PER_FILE = 100_000  # etl/jsonl_to_parquet.py:59 (chunksize)

@@ -1,0 +1,67 @@
+"""W2V kNN (model/w2vec_aids.py:125-173): MFMA path vs the exact brute-force oracle.
+
+Tolerance (floating point): neighbour sets equal to the exact fp32/fp64 search on >= 99.5 %
+of queries (SURVEY.md §8c asks >= 0.99 overlap; the reference's own IVF reached 0.973/0.980),
+squared distances within 1e-5 relative (+1e-6 absolute), dist_w2vec = trunc(d2) within 1,
+rank_w2vec = position 1..k, the query itself first with distance 0."""
+import numpy as np
+import pytest
+
+import knn as oracle
+import otto_recommender_amd.synth as synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(emb, rows, k, gi, gd, min_exact=0.995):
+    ri, rd = oracle.topk_exact(emb, rows, k)
+    same = np.mean([set(a) == set(b) for a, b in zip(gi, ri)])
+    assert same >= min_exact, same
+    ok = np.all(gi == ri, axis=1)
+    np.testing.assert_allclose(gd[ok], rd[ok], rtol=1e-5, atol=1e-6)
+    assert np.all(np.diff(gd, axis=1) >= 0)
+
+
+def test_knn_small_exact(gpu):
+    from otto_recommender_amd.w2vec import KnnIndex
+    emb = synth.embeddings(30_000, seed=3)
+    ix = KnnIndex(emb)
+    rows = np.arange(2000)
+    i, d = ix.search(rows, k=20)
+    gi, gd = i.cpu().numpy(), d.cpu().numpy()
+    assert np.all(gi[:, 0] == rows) and np.all(gd[:, 0] == 0)
+    _check(emb, rows, 20, gi, gd)
+
+
+def test_knn_arbitrary_rows_tiny_index_and_ties(gpu):
+    from otto_recommender_amd.w2vec import KnnIndex
+    rng = np.random.default_rng(1)
+    emb = rng.normal(size=(40, 100)).astype(np.float32)
+    emb[7] = emb[3]  # exact duplicate: tie broken by row index
+    ix = KnnIndex(emb)
+    rows = np.array([3, 7, 39, 0, 11])
+    i, d = ix.search(rows, k=20)
+    gi, gd = i.cpu().numpy(), d.cpu().numpy()
+    assert list(gi[0][:2]) == [3, 7] and list(gi[1][:2]) == [3, 7]
+    _check(emb, rows, 20, gi, gd, min_exact=1.0)
+    # fewer items than k
+    ix2 = KnnIndex(emb[:5])
+    i2, d2 = ix2.search(np.array([0, 4]), k=8)
+    assert list(i2.cpu().numpy()[0][5:]) == [-1, -1, -1] and np.all(np.isinf(d2.cpu().numpy()[:, 5:]))
+
+
+def test_get_top_k_similar_faiss_frame(gpu):
+    from otto_recommender_amd import w2vec
+    emb = synth.embeddings(5000, seed=2)
+    words = np.random.default_rng(0).permutation(10_000)[:5000].astype(np.int32)
+    ix = w2vec.load_index_faiss_ivff(emb)
+    wq = list(words[:50]) + [10_000_000]  # a word without an embedding is dropped (:156-163)
+    df = w2vec.get_top_k_similar_faiss(wq, words, None, ix, k=20)
+    assert list(df.columns) == ["aid", "aid_next", "dist_w2vec", "rank_w2vec"]
+    assert len(df) == 50 * 20
+    assert str(df["dist_w2vec"].dtype) == "int32" and str(df["rank_w2vec"].dtype) == "int8"
+    ri, rd = oracle.topk_exact(emb, np.arange(50), 20)
+    assert np.array_equal(df["aid_next"].to_numpy().reshape(50, 20), words[ri])
+    assert np.all(np.abs(df["dist_w2vec"].to_numpy().reshape(50, 20) - np.trunc(rd)) <= 1)
+    assert np.array_equal(df["rank_w2vec"].to_numpy().reshape(50, 20), np.tile(np.arange(1, 21), (50, 1)))
+    assert np.array_equal(df["aid"].to_numpy().reshape(50, 20)[:, 0], words[:50])
