@@ -53,6 +53,7 @@ def bench_knn(steps: int, warmup: int, n_items: int, n_q: int, with_cpu: bool) -
     from otto_recommender_amd.w2vec import KnnIndex
     ctx = _lib.context()
     emb = synth.embeddings(n_items)
+    n_q = min(n_q, n_items)
     index = KnnIndex(emb, ctx)
     for _ in range(warmup):
         index.search(None, n_q=n_q, k=20)
@@ -106,6 +107,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--knn-steps", type=int, default=2, help="0 disables the configs[2] kNN measurement")
+    ap.add_argument("--workload", choices=["covis", "knn"], default="covis",
+                    help="covis: configs[1] line (+ the kNN sub-object); knn: only configs[2]")
     ap.add_argument("--knn-items", type=int, default=1_855_603)
     ap.add_argument("--knn-queries", type=int, default=600_000)
     args = ap.parse_args()
@@ -116,6 +119,10 @@ def main():
     from otto_recommender_amd import covis as gc
     from otto_recommender_amd import _lib
 
+    if args.workload == "knn":
+        torch.cuda.set_device(0)
+        print(json.dumps(bench_knn(max(args.knn_steps, 1), 1, args.knn_items, args.knn_queries, not args.no_cpu)))
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

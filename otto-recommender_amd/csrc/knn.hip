@@ -25,9 +25,9 @@ constexpr int KN_QW = 32;                // queries per wave
 constexpr int KN_WAVES = 8;
 constexpr int KN_T = 64 * KN_WAVES;      // 512 threads
 constexpr int KN_QB = KN_QW * KN_WAVES;  // 256 queries per workgroup
-constexpr int KN_IT = 64;                // items per LDS tile
-constexpr int KN_C = 32;                 // candidates per lane (64 per query)
-constexpr int KN_CAND = 2 * KN_C;
+constexpr int KN_IT = 128;               // items per LDS tile (4 row-blocks of 32)
+constexpr int KN_C = 20;                 // candidates per lane-half (>= k: exact top-20 in score order)
+constexpr int KN_CAND = 64;              // rerank width (2 * KN_C candidates, padded)
 
 __device__ __forceinline__ uint16_t f2bf(float f) {  // round to nearest even
   uint32_t u = __float_as_uint(f);
@@ -38,11 +38,15 @@ __device__ __forceinline__ float bf2f(uint16_t b) { return __uint_as_float((uint
 
 // items (rows of emb) -> packed bf16 with the -|v|^2/2 columns; or queries (rows[q]) with 1, 1
 __global__ void k_knn_pack(const float* __restrict__ emb, int64_t n, int dim, const int32_t* __restrict__ rows,
-                           int is_query, uint16_t* __restrict__ out) {
+                           int64_t n_items, int is_query, uint16_t* __restrict__ out, int* __restrict__ err) {
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (i >= n) return;
   const int l = threadIdx.x & 63;
-  const int64_t src = rows ? rows[i] : i;
+  int64_t src = rows ? rows[i] : i;
+  if (src < 0 || src >= n_items) {  // never read outside the embedding table
+    if (l == 0 && err) atomicOr(err, 1);
+    src = 0;
+  }
   const float* v = emb + src * dim;
   float ss = 0.f;
   for (int d = l; d < KN_KD; d += 64) {
@@ -68,7 +72,8 @@ __global__ void k_knn_pack(const float* __restrict__ emb, int64_t n, int dim, co
 __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ items, int64_t V,
                                                   const uint4* __restrict__ queries, int64_t nq,
                                                   uint32_t* __restrict__ cand) {
-  __shared__ uint4 tile[2][KN_IT * KN_CH];  // 2 x 16 KiB
+  __shared__ uint4 tile[2][KN_IT * KN_CH];  // 2 x 32 KiB
+  constexpr int PER = KN_IT * KN_CH / KN_T;   // uint4 per thread per tile (4)
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, r = l & 31, h = l >> 5;
   const int64_t q = (int64_t)blockIdx.x * KN_QB + w * KN_QW + r;
   bf16x8 bq[8];
@@ -85,61 +90,81 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
   float thr = -INFINITY;
   int tpos = 0;
   const int64_t nT = ceil_div(V, KN_IT);
-  uint4 st[2];
-  auto load = [&](int64_t t) {
+  // register staging two tiles ahead: loads for tile t+2 are issued while tile t computes
+  uint4 stA[PER], stB[PER];
+  auto load = [&](int64_t t, uint4 (&st)[PER]) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < PER; ++u) {
       const int p = tid + KN_T * u, row = p >> 4, c = p & 15;
       const int64_t item = t * KN_IT + row;
       st[u] = item < V ? items[item * KN_CH + (c ^ (row & 15))] : make_uint4(0, 0, 0, 0);
     }
   };
-  auto store = [&](int b) {
+  auto store = [&](int b, const uint4 (&st)[PER]) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) tile[b][tid + KN_T * u] = st[u];
+    for (int u = 0; u < PER; ++u) tile[b][tid + KN_T * u] = st[u];
   };
-  load(0);
-  store(0);
-  __syncthreads();
-  for (int64_t t = 0; t < nT; ++t) {
-    if (t + 1 < nT) load(t + 1);
+  auto insert = [&](float s_, uint32_t item) {
+#pragma unroll
+    for (int j = 0; j < KN_C; ++j)
+      if (j == tpos) { sc[j] = s_; ix[j] = item; }
+    thr = sc[0]; tpos = 0;
+#pragma unroll
+    for (int j = 1; j < KN_C; ++j)
+      if (sc[j] < thr) { thr = sc[j]; tpos = j; }
+  };
+  auto compute = [&](int64_t t) {
     const uint4* T = tile[t & 1];
+    constexpr int RB = KN_IT / 32;
+    f32x16 acc[RB];
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb) {
-      f32x16 acc = {};
-      const int row = rb * 32 + r;
+    for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x16{};
+    // RB independent accumulation chains, issued back to back
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
+    for (int s = 0; s < 8; ++s) {
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) {
+        const int row = rb * 32 + r;
         const uint4 a = T[row * KN_CH + ((2 * s + h) ^ (row & 15))];
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), bq[s], acc, 0, 0, 0);
+        acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), bq[s], acc[rb], 0, 0, 0);
       }
-      const int64_t ib = t * KN_IT + rb * 32 + 4 * h;
-      bool any = false;
+    }
 #pragma unroll
-      for (int i = 0; i < 16; ++i) any |= acc[i] > thr;
-      if (any) {
+    for (int rb = 0; rb < RB; ++rb) {
+      float m = acc[rb][0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) m = fmaxf(m, acc[rb][i]);
+      if (m > thr) {
+        const int64_t ib = t * KN_IT + rb * 32 + 4 * h;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const float s_ = acc[i];
           const int64_t item = ib + (i & 3) + 8 * (i >> 2);
-          if (s_ > thr && item < V) {
-#pragma unroll
-            for (int j = 0; j < KN_C; ++j)
-              if (j == tpos) { sc[j] = s_; ix[j] = (uint32_t)item; }
-            thr = sc[0]; tpos = 0;
-#pragma unroll
-            for (int j = 1; j < KN_C; ++j)
-              if (sc[j] < thr) { thr = sc[j]; tpos = j; }
-          }
+          if (acc[rb][i] > thr && item < V) insert(acc[rb][i], (uint32_t)item);
         }
       }
     }
-    if (t + 1 < nT) store((int)((t + 1) & 1));
+  };
+  load(0, stA);
+  if (nT > 1) load(1, stB);
+  store(0, stA);
+  __syncthreads();
+  // iteration t: regs hold tile t+1 (B) ; issue tile t+2 into A; compute t; store t+1 into LDS
+  for (int64_t t = 0; t < nT; t += 2) {
+    if (t + 2 < nT) load(t + 2, stA);
+    compute(t);
+    if (t + 1 < nT) store((int)((t + 1) & 1), stB);
+    __syncthreads();
+    if (t + 1 >= nT) break;
+    if (t + 3 < nT) load(t + 3, stB);
+    compute(t + 1);
+    if (t + 2 < nT) store((int)(t & 1), stA);
     __syncthreads();
   }
   if (q < nq) {
 #pragma unroll
-    for (int j = 0; j < KN_C; ++j) cand[q * KN_CAND + h * KN_C + j] = ix[j];
+    for (int j = 0; j < KN_C; ++j) cand[q * KN_CAND + h * (KN_CAND / 2) + j] = ix[j];
+#pragma unroll
+    for (int j = KN_C; j < KN_CAND / 2; ++j) cand[q * KN_CAND + h * (KN_CAND / 2) + j] = 0xFFFFFFFFu;
   }
 }
 
@@ -152,14 +177,28 @@ __global__ __launch_bounds__(256) void k_knn_rerank(const float* __restrict__ em
   if (q >= nq) return;
   const uint32_t l = lane_id();
   const uint32_t c = cand[q * KN_CAND + l];
-  const float* qv = emb + (int64_t)(qrows ? qrows[q] : q) * dim;
+  int64_t qr = qrows ? qrows[q] : q;
+  if (qr < 0 || qr >= V) qr = 0;  // flagged by k_knn_pack; the call returns an error
+  const float* qv = emb + qr * dim;
   float d2 = INFINITY;
   if (c < (uint32_t)V) {
     const float* v = emb + (int64_t)c * dim;
     float acc = 0.f;
-    for (int d = 0; d < dim; ++d) {
-      const float t = qv[d] - v[d];
-      acc = fmaf(t, t, acc);
+    if ((dim & 3) == 0) {  // rows are 16-B aligned: vector loads
+      const float4* q4 = reinterpret_cast<const float4*>(qv);
+      const float4* v4 = reinterpret_cast<const float4*>(v);
+      for (int d = 0; d < dim / 4; ++d) {
+        const float4 a = q4[d], b = v4[d];
+        float t = a.x - b.x; acc = fmaf(t, t, acc);
+        t = a.y - b.y; acc = fmaf(t, t, acc);
+        t = a.z - b.z; acc = fmaf(t, t, acc);
+        t = a.w - b.w; acc = fmaf(t, t, acc);
+      }
+    } else {
+      for (int d = 0; d < dim; ++d) {
+        const float t = qv[d] - v[d];
+        acc = fmaf(t, t, acc);
+      }
     }
     d2 = acc;
   }
@@ -208,7 +247,8 @@ int ottohip_knn_index_create(ottohip_ctx* c, const float* emb, int64_t n_items, 
   if (hipMalloc(&ix->packed, (size_t)n_items * KN_KD * 2) != hipSuccess) {
     delete ix; set_error("knn_index_create: allocation failed"); return OTTOHIP_ENOMEM;
   }
-  k_knn_pack<<<(unsigned)ceil_div(n_items * 64, 256), 256, 0, s>>>(emb, n_items, dim, nullptr, 0, ix->packed);
+  k_knn_pack<<<(unsigned)ceil_div(n_items * 64, 256), 256, 0, s>>>(emb, n_items, dim, nullptr, n_items, 0, ix->packed,
+                                                                   nullptr);
   OH_HIP(hipGetLastError());
   *out = ix;
   return 0;
@@ -229,14 +269,23 @@ int ottohip_knn_topk(ottohip_ctx* c, const ottohip_knn_index* ix, const int32_t*
     return OTTOHIP_EINVAL;
   }
   if (n_q == 0) return 0;
+  if (!query_rows && n_q > ix->n_items) {
+    set_error("knn_topk: n_q=%lld query rows 0..n_q-1 exceed the index (%lld rows)", (long long)n_q,
+              (long long)ix->n_items);
+    return OTTOHIP_EINVAL;
+  }
   Ctx* ctx = ctx_base(c);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  ctx->reset_timing();
   uint16_t* qp;
   uint32_t* cand;
+  int* err;
   OH_TRY(ctx->ws.get("knn_q", (size_t)n_q * KN_KD * 2, reinterpret_cast<void**>(&qp)));
   OH_TRY(ctx->ws.get("knn_cand", (size_t)n_q * KN_CAND, &cand));
+  OH_TRY(ctx->ws.get("knn_err", 1, &err));
+  OH_HIP(hipMemsetAsync(err, 0, sizeof(int), s));
   int ph = ctx->begin("knn_pack", s, 0);
-  k_knn_pack<<<(unsigned)ceil_div(n_q * 64, 256), 256, 0, s>>>(ix->emb, n_q, ix->dim, query_rows, 1, qp);
+  k_knn_pack<<<(unsigned)ceil_div(n_q * 64, 256), 256, 0, s>>>(ix->emb, n_q, ix->dim, query_rows, ix->n_items, 1, qp, err);
   ctx->end(ph, s);
   ph = ctx->begin("knn_main", s, 2.0 * (double)n_q * (double)ix->n_items * ix->dim);
   k_knn_main<<<(unsigned)ceil_div(n_q, KN_QB), KN_T, 0, s>>>(reinterpret_cast<const uint4*>(ix->packed), ix->n_items,
@@ -247,6 +296,12 @@ int ottohip_knn_topk(ottohip_ctx* c, const ottohip_knn_index* ix, const int32_t*
                                                                  k, out_idx, out_d2);
   ctx->end(ph, s);
   OH_HIP(hipGetLastError());
+  if (query_rows) {  // explicit rows were range-checked on the device
+    int herr = 0;
+    OH_HIP(hipMemcpyAsync(&herr, err, sizeof(int), hipMemcpyDeviceToHost, s));
+    OH_HIP(hipStreamSynchronize(s));
+    if (herr) { set_error("knn_topk: a query row is outside [0, n_items)"); return OTTOHIP_ERANGE; }
+  }
   return 0;
 }
 }  // extern "C"

@@ -65,3 +65,13 @@ def test_get_top_k_similar_faiss_frame(gpu):
     assert np.all(np.abs(df["dist_w2vec"].to_numpy().reshape(50, 20) - np.trunc(rd)) <= 1)
     assert np.array_equal(df["rank_w2vec"].to_numpy().reshape(50, 20), np.tile(np.arange(1, 21), (50, 1)))
     assert np.array_equal(df["aid"].to_numpy().reshape(50, 20)[:, 0], words[:50])
+
+
+def test_knn_rejects_out_of_range_rows(gpu):
+    from otto_recommender_amd import _lib as L
+    from otto_recommender_amd.w2vec import KnnIndex
+    ix = KnnIndex(synth.embeddings(100, seed=4))
+    with pytest.raises(L.OttoHipError):
+        ix.search(np.array([0, 100]), k=5)
+    with pytest.raises(L.OttoHipError):
+        ix.search(None, n_q=101, k=5)
