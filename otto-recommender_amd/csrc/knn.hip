@@ -12,6 +12,7 @@
 //   3. k_knn_rerank: one wave per query recomputes |q - v|^2 exactly in fp32 for the 64
 //      candidates and sorts by (d2, index): the top-k rows and their exact squared distances.
 #include <cmath>
+#include <cstdlib>
 #include "common.h"
 
 namespace ottohip {
@@ -21,12 +22,12 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int KN_KD = 128;               // padded K (bf16 per row)
 constexpr int KN_CH = KN_KD * 2 / 16;    // 16-B chunks per row (16)
-constexpr int KN_QW = 32;                // queries per wave
+constexpr int KN_QW = 64;                // queries per wave (two 32-column MFMA blocks)
 constexpr int KN_WAVES = 8;
 constexpr int KN_T = 64 * KN_WAVES;      // 512 threads
 constexpr int KN_QB = KN_QW * KN_WAVES;  // 256 queries per workgroup
 constexpr int KN_IT = 128;               // items per LDS tile (4 row-blocks of 32)
-constexpr int KN_C = 20;                 // candidates per lane-half (>= k: exact top-20 in score order)
+constexpr int KN_C = 24;                 // candidates per query (k = 20 plus a rerank margin)
 constexpr int KN_CAND = 64;              // rerank width (2 * KN_C candidates, padded)
 
 __device__ __forceinline__ uint16_t f2bf(float f) {  // round to nearest even
@@ -69,19 +70,34 @@ __global__ void k_knn_pack(const float* __restrict__ emb, int64_t n, int dim, co
   }
 }
 
+// 64 queries per wave: two 32x32 output blocks (queries qbase + [0, 32) and qbase + [32, 64))
+// share every item fragment; v_permlane32_swap then gives each lane ONE query with all 32 item
+// scores of a row-block, so each query keeps a single register list of KN_C candidates.
+// Item tiles stream into a 3-slot LDS ring by LDS-DMA (global_load_lds_dwordx4, 4 per thread
+// per tile, one tile in flight behind the one being computed): counted vmcnt + raw s_barrier.
+constexpr int KN_RING = 3;
+constexpr int KN_GL = KN_IT * KN_CH / KN_T;  // glds per thread per tile (4)
+
+template <int ABL>
 __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ items, int64_t V,
                                                   const uint4* __restrict__ queries, int64_t nq,
                                                   uint32_t* __restrict__ cand) {
-  __shared__ uint4 tile[2][KN_IT * KN_CH];  // 2 x 32 KiB
-  constexpr int PER = KN_IT * KN_CH / KN_T;   // uint4 per thread per tile (4)
+  __shared__ uint4 ring[KN_RING * KN_IT * KN_CH];  // 3 x 32 KiB, the only LDS object
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, r = l & 31, h = l >> 5;
-  const int64_t q = (int64_t)blockIdx.x * KN_QB + w * KN_QW + r;
-  bf16x8 bq[8];
+  const int64_t qbase = (int64_t)blockIdx.x * KN_QB + w * 64;
+  const auto probe = __builtin_amdgcn_permlane32_swap((unsigned)l, (unsigned)(l + 64), false, false);
+  const bool semA = __builtin_amdgcn_readfirstlane(probe[1]) == 32u;  // vsrc lane 0 received vdst lane 32
+  const int64_t q = semA ? qbase + l : qbase + ((l + 32) & 63);
+  const int offx = semA ? 0 : 4, offy = 4 - offx;
+  bf16x8 bqa[8], bqb[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
-    uint4 u = make_uint4(0, 0, 0, 0);
-    if (q < nq) u = queries[q * KN_CH + 2 * s + h];
-    bq[s] = __builtin_bit_cast(bf16x8, u);
+    const int64_t qa = qbase + r, qb = qbase + 32 + r;
+    uint4 ua = make_uint4(0, 0, 0, 0), ub = make_uint4(0, 0, 0, 0);
+    if (qa < nq) ua = queries[qa * KN_CH + 2 * s + h];
+    if (qb < nq) ub = queries[qb * KN_CH + 2 * s + h];
+    bqa[s] = __builtin_bit_cast(bf16x8, ua);
+    bqb[s] = __builtin_bit_cast(bf16x8, ub);
   }
   float sc[KN_C];
   uint32_t ix[KN_C];
@@ -90,19 +106,17 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
   float thr = -INFINITY;
   int tpos = 0;
   const int64_t nT = ceil_div(V, KN_IT);
-  // register staging two tiles ahead: loads for tile t+2 are issued while tile t computes
-  uint4 stA[PER], stB[PER];
-  auto load = [&](int64_t t, uint4 (&st)[PER]) {
+  // LDS chunk p = u*512 + tid holds item row p>>4, source chunk (p & 15) ^ (row & 15);
+  // rows past V read row V-1 (valid memory; their scores are masked below)
+  auto issue = [&](int64_t t) {
+    uint4* dst = ring + (int)(t % KN_RING) * (KN_IT * KN_CH);
 #pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int p = tid + KN_T * u, row = p >> 4, c = p & 15;
-      const int64_t item = t * KN_IT + row;
-      st[u] = item < V ? items[item * KN_CH + (c ^ (row & 15))] : make_uint4(0, 0, 0, 0);
+    for (int u = 0; u < KN_GL; ++u) {
+      const int p = u * KN_T + tid, row = p >> 4, c = p & 15;
+      int64_t item = t * KN_IT + row;
+      if (item >= V) item = V - 1;
+      __builtin_amdgcn_global_load_lds(items + item * KN_CH + (c ^ (row & 15)), dst + u * KN_T + w * 64, 16, 0, 0);
     }
-  };
-  auto store = [&](int b, const uint4 (&st)[PER]) {
-#pragma unroll
-    for (int u = 0; u < PER; ++u) tile[b][tid + KN_T * u] = st[u];
   };
   auto insert = [&](float s_, uint32_t item) {
 #pragma unroll
@@ -113,58 +127,63 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
     for (int j = 1; j < KN_C; ++j)
       if (sc[j] < thr) { thr = sc[j]; tpos = j; }
   };
-  auto compute = [&](int64_t t) {
-    const uint4* T = tile[t & 1];
-    constexpr int RB = KN_IT / 32;
-    f32x16 acc[RB];
+  issue(0);
+  if (nT > 1) issue(1);
+  for (int64_t t = 0; t < nT; ++t) {
+    if (t + 1 < nT) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // == KN_GL: tile t+1 may fly
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // tile t visible to all waves; slot (t+2)%3 = (t-1)%3 is free
+    if (t + 2 < nT) issue(t + 2);
+    const uint4* T = ring + (int)(t % KN_RING) * (KN_IT * KN_CH);
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x16{};
-    // RB independent accumulation chains, issued back to back
+    for (int rp = 0; rp < KN_IT / 64; ++rp) {  // two row-blocks of 32 items at a time
+      f32x16 accA[2] = {}, accB[2] = {};
+      const int row0 = (2 * rp) * 32 + r, row1 = row0 + 32;
+      bf16x8 cur0 = __builtin_bit_cast(bf16x8, T[row0 * KN_CH + ((0 + h) ^ (row0 & 15))]);
+      bf16x8 cur1 = __builtin_bit_cast(bf16x8, T[row1 * KN_CH + ((0 + h) ^ (row1 & 15))]);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb) {
-        const int row = rb * 32 + r;
-        const uint4 a = T[row * KN_CH + ((2 * s + h) ^ (row & 15))];
-        acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), bq[s], acc[rb], 0, 0, 0);
+      for (int s = 0; s < 8; ++s) {
+        bf16x8 nx0 = cur0, nx1 = cur1;
+        if (s < 7) {  // next k-step's fragments are read while this step's MFMAs run
+          nx0 = __builtin_bit_cast(bf16x8, T[row0 * KN_CH + ((2 * s + 2 + h) ^ (row0 & 15))]);
+          nx1 = __builtin_bit_cast(bf16x8, T[row1 * KN_CH + ((2 * s + 2 + h) ^ (row1 & 15))]);
+        }
+        accA[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur0, bqa[s], accA[0], 0, 0, 0);
+        accB[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur0, bqb[s], accB[0], 0, 0, 0);
+        accA[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur1, bqa[s], accA[1], 0, 0, 0);
+        accB[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur1, bqb[s], accB[1], 0, 0, 0);
+        cur0 = nx0;
+        cur1 = nx1;
       }
-    }
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) {
-      float m = acc[rb][0];
+      for (int u = 0; u < 2; ++u) {
 #pragma unroll
-      for (int i = 1; i < 16; ++i) m = fmaxf(m, acc[rb][i]);
-      if (m > thr) {
-        const int64_t ib = t * KN_IT + rb * 32 + 4 * h;
+        for (int i = 0; i < 16; ++i) {  // accA -> rows + offx, accB -> rows + offy of this lane's query
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(accA[u][i]), __float_as_uint(accB[u][i]),
+                                                           false, false);
+          accA[u][i] = __uint_as_float(sw[0]);
+          accB[u][i] = __uint_as_float(sw[1]);
+        }
+        float m = fmaxf(accA[u][0], accB[u][0]);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int64_t item = ib + (i & 3) + 8 * (i >> 2);
-          if (acc[rb][i] > thr && item < V) insert(acc[rb][i], (uint32_t)item);
+        for (int i = 1; i < 16; ++i) m = fmaxf(m, fmaxf(accA[u][i], accB[u][i]));
+        if (ABL) { thr = fmaxf(thr, m * 1e-30f); continue; }  // ablation build: no candidate handling
+        if (m > thr) {
+          const int64_t ib = t * KN_IT + (2 * rp + u) * 32;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int64_t base = ib + (i & 3) + 8 * (i >> 2);
+            if (accA[u][i] > thr && base + offx < V) insert(accA[u][i], (uint32_t)(base + offx));
+            if (accB[u][i] > thr && base + offy < V) insert(accB[u][i], (uint32_t)(base + offy));
+          }
         }
       }
     }
-  };
-  load(0, stA);
-  if (nT > 1) load(1, stB);
-  store(0, stA);
-  __syncthreads();
-  // iteration t: regs hold tile t+1 (B) ; issue tile t+2 into A; compute t; store t+1 into LDS
-  for (int64_t t = 0; t < nT; t += 2) {
-    if (t + 2 < nT) load(t + 2, stA);
-    compute(t);
-    if (t + 1 < nT) store((int)((t + 1) & 1), stB);
-    __syncthreads();
-    if (t + 1 >= nT) break;
-    if (t + 3 < nT) load(t + 3, stB);
-    compute(t + 1);
-    if (t + 2 < nT) store((int)(t & 1), stA);
-    __syncthreads();
   }
+  if (ABL && thr == 12345.f) ix[0] = 0;  // keep the ablated scores live
   if (q < nq) {
 #pragma unroll
-    for (int j = 0; j < KN_C; ++j) cand[q * KN_CAND + h * (KN_CAND / 2) + j] = ix[j];
-#pragma unroll
-    for (int j = KN_C; j < KN_CAND / 2; ++j) cand[q * KN_CAND + h * (KN_CAND / 2) + j] = 0xFFFFFFFFu;
+    for (int j = 0; j < KN_CAND; ++j) cand[q * KN_CAND + j] = j < KN_C ? ix[j] : 0xFFFFFFFFu;
   }
 }
 
@@ -288,7 +307,9 @@ int ottohip_knn_topk(ottohip_ctx* c, const ottohip_knn_index* ix, const int32_t*
   k_knn_pack<<<(unsigned)ceil_div(n_q * 64, 256), 256, 0, s>>>(ix->emb, n_q, ix->dim, query_rows, ix->n_items, 1, qp, err);
   ctx->end(ph, s);
   ph = ctx->begin("knn_main", s, 2.0 * (double)n_q * (double)ix->n_items * ix->dim);
-  k_knn_main<<<(unsigned)ceil_div(n_q, KN_QB), KN_T, 0, s>>>(reinterpret_cast<const uint4*>(ix->packed), ix->n_items,
+  static const int abl = getenv("OTTOHIP_KNN_ABLATE") ? atoi(getenv("OTTOHIP_KNN_ABLATE")) : 0;
+  auto kmain = abl ? k_knn_main<1> : k_knn_main<0>;
+  kmain<<<(unsigned)ceil_div(n_q, KN_QB), KN_T, 0, s>>>(reinterpret_cast<const uint4*>(ix->packed), ix->n_items,
                                                              reinterpret_cast<const uint4*>(qp), n_q, cand);
   ctx->end(ph, s);
   ph = ctx->begin("knn_rerank", s, 0);
