@@ -111,6 +111,8 @@ def main():
                     help="covis: configs[1] line (+ the kNN sub-object); knn: only configs[2]")
     ap.add_argument("--knn-items", type=int, default=1_855_603)
     ap.add_argument("--knn-queries", type=int, default=600_000)
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl = RCCL over xGMI (the product); gloo = host-staged rehearsal on fewer GPUs")
     args = ap.parse_args()
 
     import torch
@@ -127,16 +129,26 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        local = local % max(torch.cuda.device_count(), 1)  # gloo rehearsals may share a GPU
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
+    from otto_recommender_amd import dist as gd
 
     # ---- workload: sessions until E events, 100k-session files, files dealt to ranks
     n_sess, n_ev = synth.sessions_for_events(args.events, 0, args.seed)
     fb_all = synth.file_session_bounds(n_sess)
     n_files = len(fb_all) - 1
-    my_files = list(range(rank, n_files, world))
+    if world > 1:  # whole files per rank, balanced by sum of n_s^2 (work ∝ pairs)
+        lens = synth.session_lengths(n_sess, 0, args.seed).astype(np.float64)
+        weights = [float((lens[fb_all[f]:fb_all[f + 1]] ** 2).sum()) for f in range(n_files)]
+        my_files = gd.deal_files(n_files, rank, world, weights)
+    else:
+        my_files = list(range(n_files))
     t0 = time.perf_counter()
     parts = [synth.generate(int(fb_all[f + 1] - fb_all[f]), int(fb_all[f]), args.seed) for f in my_files]
     sizes = [p.n_sessions for p in parts]
@@ -155,8 +167,9 @@ def main():
     torch.cuda.synchronize()
 
     def step():
-        tab = gc.count_co_events_fused(dev, ctx=ctx)
-        return tab
+        if world > 1:  # local count -> pack by owner -> all-to-all-v (RCCL) -> merge-sum
+            return gd.count_co_events_sharded(dev, ctx=ctx)
+        return gc.count_co_events_fused(dev, ctx=ctx)
 
     for _ in range(args.warmup):
         step().free()
@@ -187,7 +200,8 @@ def main():
 
     t_step = dt / args.steps
     if world > 1:
-        tt = torch.tensor([t_step, float(pairs), float(rows), float(ev.n_events)], dtype=torch.float64, device="cuda")
+        cdev = "cuda" if args.dist_backend == "nccl" else "cpu"
+        tt = torch.tensor([t_step, float(pairs), float(rows), float(ev.n_events)], dtype=torch.float64, device=cdev)
         t_max = tt[:1].clone(); dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
         tot = tt[1:].clone(); dist.all_reduce(tot)
         t_step = float(t_max.item()); pairs, rows, n_events = (float(x) for x in tot.tolist())
@@ -216,7 +230,8 @@ def main():
         "data": "synthetic (otto-synth seed 0, SURVEY.md §8(d)); inputs resident in HBM",
         "config": {"workload": "configs[1]: all 5 co-visitation rules, 220M events, 100k-session files",
                    "events": int(n_events), "sessions": int(n_sess), "files": n_files,
-                   "parallelism": f"files dealt over {world} GPU(s)"},
+                   "parallelism": f"files dealt over {world} GPU(s)" + (
+                       f", owner(aid) all-to-all-v merge over {args.dist_backend}" if world > 1 else "")},
         "pairs": int(pairs), "rows": int(rows),
         "events_per_s": n_events / t_step,
         "step_roofline": {"bound": "hbm", "model_bytes": b_model, "achieved": b_model / t_step / 1e9,

@@ -115,6 +115,24 @@ int ottohip_table_finalize(ottohip_ctx* ctx, const ottohip_table* t, int rule,
                            const ottohip_merge_params* mp, int32_t* aid, int32_t* aid_next,
                            int32_t* count, int64_t* n_out, void* stream);
 
+/* ---- Multi-GPU exchange -------------------------------------------------
+ * The reference is single-process; these calls replace the cross-file groupby of
+ * concat_files_w_stats (model/count_co_events.py:168) when files are dealt over G ranks.
+ * Each rank counts its own whole files (ottohip_covis_count), packs its rows by owner and
+ * exchanges them (all-to-all-v issued by the host layer over RCCL); the owner rebuilds a
+ * table that equals the single-GPU table restricted to {aid : owner(aid) == rank}.
+ * Record = 4 x u32 {rule << 29 | aid, aid_next, count, count_ge2} (requires aid < 2^29). */
+int ottohip_owner_of(int32_t aid, int n_parts); /* owner rank of an aid: multiplicative hash, range-reduced */
+/* out_records: device, >= n_rows records; part_counts: HOST [n_parts] rows per owner, records
+ * of owner p follow those of owners < p. */
+int ottohip_table_pack_by_owner(ottohip_ctx* ctx, const ottohip_table* t, int n_parts, void* out_records,
+                                int64_t* part_counts, void* stream);
+/* merge-sum received records (duplicates of a (rule, aid, aid_next) key are summed) into a new
+ * table; file_stats (HOST, n_rules entries, may be NULL) supplies the GLOBAL file_rows /
+ * file_rows_ge2 (all-reduced by the caller) that ottohip_table_finalize needs. */
+int ottohip_table_from_records(ottohip_ctx* ctx, const void* records, int64_t n, int n_rules, int32_t n_items,
+                               const ottohip_rule_stats* file_stats, ottohip_table** out, void* stream);
+
 /* ---- Word2Vec top-K similarity (model/w2vec_aids.py:98-173) ------------------------------
  * Replaces load_index_faiss_ivff (:98-110) + get_top_k_similar_faiss (:125-173): exact L2
  * search (the reference's IVFFlat nlist 100 / nprobe 3 is approximate). The index packs the

@@ -63,6 +63,10 @@ SIGNATURES = {
     "ottohip_table_free": (None, [_VP]),
     "ottohip_table_finalize": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.POINTER(MergeParams), _VP, _VP, _VP,
                                               ctypes.POINTER(_I64), _VP]),
+    "ottohip_owner_of": (ctypes.c_int, [_I32, ctypes.c_int]),
+    "ottohip_table_pack_by_owner": (ctypes.c_int, [_VP, _VP, ctypes.c_int, _VP, ctypes.POINTER(_I64), _VP]),
+    "ottohip_table_from_records": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _I32, ctypes.POINTER(RuleStats),
+                                                  ctypes.POINTER(_VP), _VP]),
     "ottohip_knn_index_create": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, ctypes.POINTER(_VP), _VP]),
     "ottohip_knn_topk": (ctypes.c_int, [_VP, _VP, _VP, _I64, ctypes.c_int, _VP, _VP, _VP]),
     "ottohip_knn_index_free": (None, [_VP]),

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include "prims.h"
 #include "covis_kernels.h"
+#include "table.h"
 
 using namespace ottohip;
 
@@ -17,62 +18,10 @@ void set_error(const char* fmt, ...) {
 }
 }  // namespace ottohip
 
-// device buffers of one count table (reused across calls through the context's spare slot)
-struct TableBufs {
-  uint64_t cap = 0;
-  uint8_t* rule = nullptr;
-  int32_t* aid = nullptr;
-  int32_t* aid_next = nullptr;
-  uint32_t* count = nullptr;
-  uint32_t* count_ge2 = nullptr;
-  void release() {
-    if (rule) (void)hipFree(rule);
-    if (aid) (void)hipFree(aid);
-    if (aid_next) (void)hipFree(aid_next);
-    if (count) (void)hipFree(count);
-    if (count_ge2) (void)hipFree(count_ge2);
-    *this = TableBufs();
-  }
-  int alloc(uint64_t n) {
-    if (hipMalloc(&rule, n) || hipMalloc(&aid, n * 4) || hipMalloc(&aid_next, n * 4) || hipMalloc(&count, n * 4) ||
-        hipMalloc(&count_ge2, n * 4)) {
-      (void)hipGetLastError();
-      release();
-      set_error("table allocation for %llu rows failed", (unsigned long long)n);
-      return OTTOHIP_ENOMEM;
-    }
-    cap = n;
-    return 0;
-  }
-};
-
-struct ottohip_ctx : public Ctx {
-  TableBufs spare;  // buffers of the last freed table, reused by the next count
-};
 namespace ottohip {
 Ctx* ctx_base(ottohip_ctx* c) { return c; }
 }
 
-struct ottohip_table {
-  int device = 0;
-  int n_rules = 0;
-  int64_t n_rows = 0;   // valid rows (sum over rules)
-  int64_t n_slots = 0;  // entries of the row arrays; holes carry rule = 0xFF
-  TableBufs b;
-  ottohip_rule_stats stats[MAX_RULES];
-  ottohip_ctx* ctx = nullptr;
-};
-
-static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
-
-template <class T>
-static int d2h(T* host, const T* dev, size_t n, hipStream_t s) {
-  OH_HIP(hipMemcpyAsync(host, dev, n * sizeof(T), hipMemcpyDeviceToHost, s));
-  OH_HIP(hipStreamSynchronize(s));
-  return 0;
-}
-
-static unsigned grid_for(int64_t n, int t = 256) { return (unsigned)std::max<int64_t>(1, ceil_div(n, t)); }
 
 extern "C" {
 
@@ -199,6 +148,7 @@ int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohi
   ottohip_table* T = new ottohip_table();
   T->device = ctx->device;
   T->n_rules = n_rules;
+  T->n_items = params->n_items;
   T->ctx = ctx;
   memset(T->stats, 0, sizeof T->stats);
   auto fail = [&](int rc) { ottohip_table_free(T); return rc; };

@@ -12,6 +12,8 @@
 
 namespace ottohip {
 
+constexpr int MAX_RULES = 8;  // rules per count call (5 in the reference)
+
 void set_error(const char* fmt, ...);
 struct Ctx;
 Ctx* ctx_base(ottohip_ctx* c);  // abi.hip
@@ -127,6 +129,14 @@ __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v) {
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint32_t lo = __shfl_xor((uint32_t)v, d), hi = __shfl_xor((uint32_t)(v >> 32), d);
+    v += ((uint64_t)hi << 32) | lo;
+  }
   return v;
 }
 

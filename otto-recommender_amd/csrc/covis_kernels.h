@@ -20,7 +20,6 @@
 
 namespace ottohip {
 
-constexpr int MAX_RULES = 8;
 constexpr int EV_BLOCK = 256;     // events per wave block (sessions starting in it)
 constexpr int LCAP = 512;         // sessions up to LCAP events run from LDS
 constexpr int TINY = 64;          // rows/buckets up to TINY words: one wave, in registers

@@ -1,0 +1,61 @@
+// Count-table and context objects shared by the C-ABI translation units (abi.hip, shard.hip).
+#pragma once
+#include <algorithm>
+#include "common.h"
+
+using namespace ottohip;
+
+// device buffers of one count table (reused across calls through the context's spare slot)
+struct TableBufs {
+  uint64_t cap = 0;
+  uint8_t* rule = nullptr;
+  int32_t* aid = nullptr;
+  int32_t* aid_next = nullptr;
+  uint32_t* count = nullptr;
+  uint32_t* count_ge2 = nullptr;
+  void release() {
+    if (rule) (void)hipFree(rule);
+    if (aid) (void)hipFree(aid);
+    if (aid_next) (void)hipFree(aid_next);
+    if (count) (void)hipFree(count);
+    if (count_ge2) (void)hipFree(count_ge2);
+    *this = TableBufs();
+  }
+  int alloc(uint64_t n) {
+    if (hipMalloc(&rule, n) || hipMalloc(&aid, n * 4) || hipMalloc(&aid_next, n * 4) || hipMalloc(&count, n * 4) ||
+        hipMalloc(&count_ge2, n * 4)) {
+      (void)hipGetLastError();
+      release();
+      set_error("table allocation for %llu rows failed", (unsigned long long)n);
+      return OTTOHIP_ENOMEM;
+    }
+    cap = n;
+    return 0;
+  }
+};
+
+struct ottohip_ctx : public Ctx {
+  TableBufs spare;  // buffers of the last freed table, reused by the next count
+};
+
+struct ottohip_table {
+  int device = 0;
+  int n_rules = 0;
+  int32_t n_items = 0;  // aid range [0, n_items) of the rows
+  int64_t n_rows = 0;   // valid rows (sum over rules)
+  int64_t n_slots = 0;  // entries of the row arrays; holes carry rule = 0xFF
+  TableBufs b;
+  ottohip_rule_stats stats[MAX_RULES];
+  ottohip_ctx* ctx = nullptr;
+};
+
+static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+template <class T>
+static int d2h(T* host, const T* dev, size_t n, hipStream_t s) {
+  OH_HIP(hipMemcpyAsync(host, dev, n * sizeof(T), hipMemcpyDeviceToHost, s));
+  OH_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+static inline unsigned grid_for(int64_t n, int t = 256) { return (unsigned)std::max<int64_t>(1, ceil_div(n, t)); }

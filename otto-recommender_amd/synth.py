@@ -99,6 +99,15 @@ class Events:
         return pd.DataFrame({"session": self.session, "aid": self.aid, "ts": self.ts, "type": self.type})
 
 
+def session_lengths(n_sessions: int, first_session: int = 0, seed: int = 0, params: _Params | None = None) -> np.ndarray:
+    """Event counts of sessions [first_session, first_session + n_sessions) without generating them."""
+    p = params if params is not None else default_params(seed)
+    lens = np.empty(n_sessions, dtype=np.int32)
+    if _lib().otto_synth_lengths(ctypes.byref(p), first_session, n_sessions, lens.ctypes.data) != 0:
+        raise RuntimeError("otto_synth_lengths failed")
+    return lens
+
+
 def generate(n_sessions: int, first_session: int = 0, seed: int = 0, params: _Params | None = None) -> Events:
     p = params if params is not None else default_params(seed)
     lib = _lib()

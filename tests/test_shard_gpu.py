@@ -1,0 +1,162 @@
+"""GPU parity of the multi-GPU exchange kernels (csrc/shard.hip), emulated on one GPU.
+
+Ranks are emulated by counting disjoint file subsets separately, packing each by owner and
+feeding owner p's records from every "rank" to ottohip_table_from_records. The shards must
+equal the oracle's cross-file merge (model/count_co_events.py:168: groupby-sum over all
+per-file tables, with count_ge2 the sum of per-file counts >= 2, :131-132) restricted to
+owner(aid) == p. Integer work: bit-exact."""
+import numpy as np
+import pytest
+
+import covis as oracle
+import otto_recommender_amd.synth as synth
+
+pytestmark = pytest.mark.gpu
+NAMES = list(oracle.REFERENCE_RULES)
+
+
+def _expected(per_file):
+    out = {}
+    for n in NAMES:
+        a = np.concatenate([p[n][0] for p in per_file])
+        b = np.concatenate([p[n][1] for p in per_file])
+        c = np.concatenate([p[n][2] for p in per_file]).astype(np.int64)
+        ra, rb, rc = oracle._groupby_sum(a, b, c)
+        _, _, rg = oracle._groupby_sum(a, b, np.where(c >= 2, c, 0))
+        out[n] = (ra, rb, rc, rg)
+    return out
+
+
+def _subset_events(ev, fb, files):
+    parts = [ev.slice_sessions(int(fb[f]), int(fb[f + 1])) for f in files]
+    sizes = [p.n_sessions for p in parts]
+    bounds = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    off = np.zeros(int(bounds[-1]) + 1, np.int64)
+    pos = 0
+    for i, p in enumerate(parts):
+        off[bounds[i]:bounds[i + 1] + 1] = p.session_offsets - p.session_offsets[0] + pos
+        pos += p.n_events
+    cat = lambda k: np.concatenate([getattr(p, k) for p in parts])
+    return synth.Events(off, cat("session"), cat("aid"), cat("ts"), cat("type")), bounds
+
+
+@pytest.fixture(scope="module")
+def three_files():
+    ev = synth.generate(60_000, first_session=123_456)
+    fb = synth.file_session_bounds(ev.n_sessions, per_file=20_000)
+    per_file = oracle.count_co_events_files(ev.session_offsets, ev.aid, ev.ts, ev.type, fb)
+    return ev, fb, per_file, _expected(per_file)
+
+
+def test_owner_hash_matches_host(gpu):
+    import otto_recommender_amd._lib as L
+    from otto_recommender_amd import dist as gd
+    aids = np.array([0, 1, 2, 12345, 1855602, (1 << 29) - 1], np.int64)
+    for p in (1, 2, 3, 8, 64):
+        host = gd.owner_of(aids, p)
+        assert all(0 <= h < p for h in host)
+        assert [L.load().ottohip_owner_of(int(a), p) for a in aids] == host.tolist()
+
+
+def test_pack_by_owner_partitions_rows(gpu, three_files):
+    from otto_recommender_amd import covis as gc, dist as gd
+    ev, fb, _, exp = three_files
+    tab = gc.count_co_events_fused(gc.DeviceEvents.from_host(ev, fb))
+    recs, counts = gd.pack_by_owner(tab, 3)
+    r = recs.cpu().numpy().view(np.uint32)
+    assert sum(counts) == len(r) == sum(len(exp[n][0]) for n in NAMES)
+    start = 0
+    for p, c in enumerate(counts):
+        seg = r[start:start + c]
+        assert np.all(gd.owner_of(seg[:, 0] & ((1 << 29) - 1), 3) == p)
+        start += c
+    # the packed multiset equals the table
+    for i, n in enumerate(NAMES):
+        seg = r[(r[:, 0] >> 29) == i]
+        o = np.lexsort((seg[:, 1], seg[:, 0] & ((1 << 29) - 1)))
+        seg = seg[o]
+        ra, rb, rc, rg = exp[n]
+        np.testing.assert_array_equal(seg[:, 0] & ((1 << 29) - 1), ra)
+        np.testing.assert_array_equal(seg[:, 1], rb)
+        np.testing.assert_array_equal(seg[:, 2], rc)
+        np.testing.assert_array_equal(seg[:, 3], rg)
+    tab.free()
+
+
+@pytest.mark.parametrize("ranks", [[[0, 2], [1]], [[0], [1], [2]], [[2, 1, 0]]])
+def test_emulated_exchange_equals_global_merge(gpu, three_files, ranks):
+    import torch
+    from otto_recommender_amd import covis as gc, dist as gd
+    ev, fb, per_file, exp = three_files
+    G = len(ranks)
+    packs, fstats = [], np.zeros((len(NAMES), 2), np.int64)
+    for files in ranks:
+        sub, bounds = _subset_events(ev, fb, files)
+        t = gc.count_co_events_fused(gc.DeviceEvents.from_host(sub, bounds))
+        for i, n in enumerate(NAMES):
+            st = t.stats(n)
+            fstats[i] += (st["file_rows"], st["file_rows_ge2"])
+        recs, counts = gd.pack_by_owner(t, G)
+        packs.append((recs.clone(), counts))
+        t.free()
+    for p in range(G):
+        chunks = []
+        for recs, counts in packs:
+            s0 = sum(counts[:p])
+            chunks.append(recs[s0:s0 + counts[p]])
+        shard = gd.table_from_records(torch.cat(chunks), NAMES, 1855603, fstats.tolist())
+        for i, n in enumerate(NAMES):
+            a, b, c, c2 = shard.to_numpy(n)
+            ra, rb, rc, rg = exp[n]
+            k = gd.owner_of(ra, G) == p
+            np.testing.assert_array_equal(a, ra[k], err_msg=n)
+            np.testing.assert_array_equal(b, rb[k], err_msg=n)
+            np.testing.assert_array_equal(c, rc[k], err_msg=n)
+            np.testing.assert_array_equal(c2, rg[k], err_msg=n)
+            st = shard.stats(n)
+            assert st["n_rows"] == int(k.sum()) and st["n_pairs"] == int(rc[k].sum())
+            assert st["file_rows"] == sum(len(pf[n][0]) for pf in per_file)
+            assert st["file_rows_ge2"] == sum(int((pf[n][2] >= 2).sum()) for pf in per_file)
+        shard.free()
+
+
+def test_sharded_finalize_matches_merge_restatement(gpu, three_files):
+    """Each owner's finalize (threshold + count-desc order) equals the restatement of
+    concat_files_w_stats restricted to its aids (no global cut is active at this size)."""
+    import torch
+    from otto_recommender_amd import covis as gc, dist as gd
+    ev, fb, per_file, _ = three_files
+    tab = gc.count_co_events_fused(gc.DeviceEvents.from_host(ev, fb))
+    fstats = [(tab.stats(n)["file_rows"], tab.stats(n)["file_rows_ge2"]) for n in NAMES]
+    recs, counts = gd.pack_by_owner(tab, 2)
+    tab.free()
+    for p in range(2):
+        s0 = sum(counts[:p])
+        shard = gd.table_from_records(recs[s0:s0 + counts[p]].clone(), NAMES, 1855603, fstats)
+        for n in NAMES:
+            ra, rb, rc = oracle.concat_files_w_stats(n, [pf[n] for pf in per_file])
+            k = gd.owner_of(ra, 2) == p
+            a, b, c = (x.cpu().numpy() for x in shard.finalize(n))
+            np.testing.assert_array_equal(a, ra[k], err_msg=n)
+            np.testing.assert_array_equal(b, rb[k], err_msg=n)
+            np.testing.assert_array_equal(c, rc[k], err_msg=n)
+        shard.free()
+
+
+def test_from_records_edges(gpu):
+    import torch
+    import otto_recommender_amd._lib as L
+    from otto_recommender_amd import dist as gd
+    empty = gd.table_from_records(torch.zeros((0, 4), dtype=torch.int32, device="cuda"), NAMES, 100)
+    assert all(empty.stats(n)["n_rows"] == 0 for n in NAMES)
+    rec = lambda rows: torch.from_numpy(np.array(rows, np.uint32).view(np.int32)).cuda()
+    bad = rec([[(1 << 29) | 5, 7, 1, 0], [6 << 29 | 1, 2, 1, 0]])
+    with pytest.raises(L.OttoHipError) as e:
+        gd.table_from_records(bad, NAMES, 100)
+    assert e.value.rc == -2
+    dup = rec([[5, 7, 1, 0], [5, 7, 2, 2], [(4 << 29) | 5, 7, 3, 3], [5, 7, 4, 4]])
+    t = gd.table_from_records(dup, NAMES, 100)
+    a, b, c, c2 = t.to_numpy(NAMES[0])
+    assert a.tolist() == [5] and b.tolist() == [7] and c.tolist() == [7] and c2.tolist() == [6]
+    a, b, c, c2 = t.to_numpy(NAMES[4])
+    assert c.tolist() == [3] and c2.tolist() == [3]
