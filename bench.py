@@ -168,7 +168,7 @@ def main():
 
     def step():
         if world > 1:  # local count -> pack by owner -> all-to-all-v (RCCL) -> merge-sum
-            return gd.count_co_events_sharded(dev, ctx=ctx)
+            return gd.count_co_events_sharded(dev, my_files, n_files, ctx=ctx)
         return gc.count_co_events_fused(dev, ctx=ctx)
 
     for _ in range(args.warmup):

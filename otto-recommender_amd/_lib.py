@@ -63,10 +63,18 @@ SIGNATURES = {
     "ottohip_table_free": (None, [_VP]),
     "ottohip_table_finalize": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.POINTER(MergeParams), _VP, _VP, _VP,
                                               ctypes.POINTER(_I64), _VP]),
+    "ottohip_table_set_file_stats": (ctypes.c_int, [_VP, ctypes.c_int, _I64, _I64]),
     "ottohip_owner_of": (ctypes.c_int, [_I32, ctypes.c_int]),
     "ottohip_table_pack_by_owner": (ctypes.c_int, [_VP, _VP, ctypes.c_int, _VP, ctypes.POINTER(_I64), _VP]),
     "ottohip_table_from_records": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _I32, ctypes.POINTER(RuleStats),
                                                   ctypes.POINTER(_VP), _VP]),
+    "ottohip_covis_emit": (ctypes.c_int, [_VP, ctypes.POINTER(Events), ctypes.POINTER(Rule), ctypes.c_int,
+                                          ctypes.POINTER(CovisParams), _VP, _I32, ctypes.c_int, ctypes.POINTER(_VP),
+                                          ctypes.POINTER(_I64), ctypes.POINTER(_I64), _VP]),
+    "ottohip_emit_write": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
+    "ottohip_emit_free": (None, [_VP]),
+    "ottohip_covis_reduce_received": (ctypes.c_int, [_VP, ctypes.POINTER(Rule), ctypes.c_int, ctypes.POINTER(CovisParams),
+                                                     _I32, _VP, _I64, _VP, _I64, ctypes.POINTER(_VP), _VP]),
     "ottohip_knn_index_create": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, ctypes.POINTER(_VP), _VP]),
     "ottohip_knn_topk": (ctypes.c_int, [_VP, _VP, _VP, _I64, ctypes.c_int, _VP, _VP, _VP]),
     "ottohip_knn_index_free": (None, [_VP]),

@@ -23,6 +23,351 @@ Ctx* ctx_base(ottohip_ctx* c) { return c; }
 }
 
 
+// ---------------------------------------------------------------- count stages
+// S1-S3 state of one count call (device pointers live in the context workspace)
+struct Front {
+  RulesDev R;
+  Layout Lt;
+  int64_t E = 0, Sn = 0, NB = 0;
+  int nl = 0;
+  const int64_t* off = nullptr;
+  int64_t *first = nullptr, *fb = nullptr, *d_loff = nullptr;
+  int32_t* long_list = nullptr;
+  uint32_t* fid = nullptr;
+  uint64_t* evp = nullptr;
+  uint64_t* lscr = nullptr;
+  uint32_t* lpscr = nullptr;
+  uint32_t* cnt = nullptr;
+  uint64_t* poff = nullptr;
+  uint64_t P = 0;
+  int64_t Rn = 0;
+  uint32_t* row_key = nullptr;
+  uint64_t* row_begin = nullptr;
+};
+
+struct ottohip_emit {
+  Front F;
+  ottohip_events ev;
+  int n_parts = 1;
+  uint64_t gen = 0;
+  ottohip_ctx* ctx = nullptr;
+  std::vector<uint64_t> first_row, first_word;
+};
+
+static int check_events(const ottohip_events* ev) {
+  const int64_t E = ev->n_events, Sn = ev->n_sessions;
+  if (E < 0 || Sn < 0 || (E > 0 && (!ev->session_offsets || !ev->aid || !ev->ts || !ev->type))) {
+    set_error("bad event table"); return OTTOHIP_EINVAL;
+  }
+  if (E >= ((int64_t)1 << 32)) { set_error("n_events=%lld >= 2^32 (split into shards)", (long long)E); return OTTOHIP_ELIMIT; }
+  if (ev->n_files < 1 || !ev->file_session_bounds) { set_error("need >= 1 file"); return OTTOHIP_EINVAL; }
+  if (ev->file_session_bounds[0] != 0 || ev->file_session_bounds[ev->n_files] != Sn) {
+    set_error("file_session_bounds must start at 0 and end at n_sessions"); return OTTOHIP_EINVAL;
+  }
+  for (int f = 0; f < ev->n_files; ++f)
+    if (ev->file_session_bounds[f + 1] < ev->file_session_bounds[f]) { set_error("file bounds not monotone"); return OTTOHIP_EINVAL; }
+  if (ev->n_files > 65535) { set_error("n_files > 65535"); return OTTOHIP_ELIMIT; }
+  return 0;
+}
+
+static int setup_rules(const ottohip_rule* rules, int n_rules, const ottohip_covis_params* params, int n_files_total,
+                       RulesDev& R, Layout& Lt) {
+  if (n_rules < 1 || n_rules > MAX_RULES) { set_error("n_rules=%d outside [1, %d]", n_rules, MAX_RULES); return OTTOHIP_EINVAL; }
+  if (params->n_items < 1 || params->n_items > (1 << 30)) { set_error("n_items=%d outside [1, 2^30]", params->n_items); return OTTOHIP_ERANGE; }
+  if (n_files_total > 65535) { set_error("n_files > 65535"); return OTTOHIP_ELIMIT; }
+  memset(&R, 0, sizeof R);
+  int max_per_type = 1;
+  for (int r = 0; r < n_rules; ++r) {
+    const ottohip_rule& q = rules[r];
+    if (q.this_type < 0 || q.this_type > 2 || (q.next_type_mask & ~7u) || q.max_abs_dt < 0) {
+      set_error("rule %d invalid", r); return OTTOHIP_EINVAL;
+    }
+    R.lo[r] = std::max(params->min_dt, -q.max_abs_dt);
+    R.hi[r] = std::min(params->max_dt, q.max_abs_dt);
+    R.mask[r] = q.next_type_mask;
+    int t = q.this_type;
+    R.rule_of_type[t][R.n_of_type[t]++] = r;
+    max_per_type = std::max(max_per_type, R.n_of_type[t]);
+  }
+  for (int r = 0; r < n_rules; ++r)
+    if (R.lo[r] > R.hi[r]) R.mask[r] = 0;  // empty window: never matches (count stays 0)
+  Lt.A = std::max(1, bits_for((uint64_t)params->n_items));
+  Lt.F = bits_for((uint64_t)n_files_total);
+  Lt.BR = bits_for((uint64_t)max_per_type);
+  Lt.WB = Lt.BR + Lt.A + Lt.F;
+  Lt.amask = (1u << Lt.A) - 1u;
+  if (Lt.WB > 32) {
+    set_error("word layout %d rule + %d aid + %d file bits > 32: reduce files per call", Lt.BR, Lt.A, Lt.F);
+    return OTTOHIP_ELIMIT;
+  }
+  return 0;
+}
+
+static ottohip_table* new_table(ottohip_ctx* ctx, int n_rules, int32_t n_items) {
+  ottohip_table* T = new ottohip_table();
+  T->device = ctx->device;
+  T->n_rules = n_rules;
+  T->n_items = n_items;
+  T->ctx = ctx;
+  memset(T->stats, 0, sizeof T->stats);
+  return T;
+}
+
+// S1 prep, S2 count, S3 rows. n_parts > 1: owner-major rows, and (emit handle) owner bounds.
+static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip_covis_params* params,
+                       const int32_t* file_ids, int n_parts, Front& F, hipStream_t s, ottohip_emit* EM = nullptr) {
+  ++ctx->gen;
+  const int64_t E = ev->n_events, Sn = ev->n_sessions;
+  F.E = E; F.Sn = Sn;
+  F.P = 0; F.Rn = 0;
+  if (E == 0 || Sn == 0) return 0;
+  Workspace& ws = ctx->ws;
+  const Layout& Lt = F.Lt;
+  const RulesDev& R = F.R;
+  const int64_t NB = ceil_div(E, EV_BLOCK);
+  F.NB = NB;
+  int32_t* n_long;
+  int* err;
+  const int64_t long_cap = E / (LCAP + 1) + 1;
+  OH_TRY(ws.get("first", (size_t)NB + 1, &F.first));
+  OH_TRY(ws.get("fb", (size_t)ev->n_files + 1, &F.fb));
+  OH_TRY(ws.get("fid", (size_t)ev->n_files, &F.fid));
+  OH_TRY(ws.get("long_list", (size_t)long_cap, &F.long_list));
+  OH_TRY(ws.get("n_long", 4, &n_long));
+  OH_TRY(ws.get("err", 4, &err));
+  std::vector<uint32_t> fid(ev->n_files);
+  for (int f = 0; f < ev->n_files; ++f) fid[f] = file_ids ? (uint32_t)file_ids[f] : (uint32_t)f;
+  OH_HIP(hipMemcpyAsync(F.fb, ev->file_session_bounds, (ev->n_files + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  OH_HIP(hipMemcpyAsync(F.fid, fid.data(), ev->n_files * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  OH_HIP(hipMemsetAsync(n_long, 0, 4 * sizeof(int32_t), s));
+  OH_HIP(hipMemsetAsync(err, 0, sizeof(int), s));
+  OH_HIP(hipStreamSynchronize(s));  // fid is a stack vector
+  const int64_t* off = ev->session_offsets;
+  F.off = off;
+
+  // ---- S1 prep
+  OH_TRY(ws.get("ev", (size_t)E, &F.evp));
+  int ph = ctx->begin("prep", s, 9.0 * E + 8.0 * (Sn + 1) + 8.0 * E);
+  k_block_first<<<grid_for(Sn + 1), 256, 0, s>>>(off, Sn, NB, F.first, F.long_list, n_long);
+  k_prep<<<grid_for(NB, 4), 256, 0, s>>>(off, F.first, NB, ev->aid, ev->ts, ev->type, F.evp, params->n_items,
+                                          params->dedup, err);
+  if (hipGetLastError() != hipSuccess) { set_error("k_prep launch failed"); return OTTOHIP_EHIP; }
+  int32_t nl = 0;
+  OH_TRY(d2h(&nl, n_long, 1, s));
+  F.nl = nl;
+  if (nl > 0) {
+    std::vector<int32_t> ll(nl);
+    OH_TRY(d2h(ll.data(), F.long_list, (size_t)nl, s));
+    std::sort(ll.begin(), ll.end());
+    OH_HIP(hipMemcpy(F.long_list, ll.data(), nl * sizeof(int32_t), hipMemcpyHostToDevice));
+    std::vector<int64_t> loff(nl + 1);
+    loff[0] = 0;
+    for (int i = 0; i < nl; ++i) {
+      int64_t ab[2];
+      OH_HIP(hipMemcpy(ab, off + ll[i], 2 * sizeof(int64_t), hipMemcpyDeviceToHost));
+      loff[i + 1] = loff[i] + (ab[1] - ab[0]);
+    }
+    OH_TRY(ws.get("long_scr", (size_t)(2 * loff[nl]), &F.lscr));
+    OH_TRY(ws.get("long_pscr", (size_t)(3 * (loff[nl] + nl)), &F.lpscr));
+    OH_TRY(ws.get("long_off", (size_t)(nl + 1), &F.d_loff));
+    OH_HIP(hipMemcpy(F.d_loff, loff.data(), (nl + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+    k_prep_long<<<nl, 64, 0, s>>>(off, F.long_list, F.d_loff, F.lscr, ev->aid, ev->ts, ev->type, F.evp,
+                                  params->n_items, params->dedup, err);
+  }
+  ctx->end(ph, s);
+
+  // ---- S2 count
+  uint32_t *rk, *pos, *rk2, *pos2;
+  OH_TRY(ws.get("cnt", (size_t)E, &F.cnt));
+  OH_TRY(ws.get("rk", (size_t)E, &rk));
+  OH_TRY(ws.get("pos", (size_t)E, &pos));
+  OH_TRY(ws.get("rk2", (size_t)E, &rk2));
+  OH_TRY(ws.get("pos2", (size_t)E, &pos2));
+  ph = ctx->begin("count", s, 8.0 * E + 12.0 * E);
+  k_count<<<grid_for(NB, 4), 256, 0, s>>>(off, F.first, NB, F.evp, R, Lt.A, F.cnt, rk, pos);
+  if (nl > 0)
+    k_count_long<<<nl, 64, 0, s>>>(off, F.long_list, F.d_loff, F.lscr, F.lpscr, F.evp, R, Lt.A, F.cnt, rk, pos);
+  if (hipGetLastError() != hipSuccess) { set_error("k_count launch failed"); return OTTOHIP_EHIP; }
+  ctx->end(ph, s);
+
+  // ---- S3 rows (aid-major transpose; owner-major first when n_parts > 1)
+  ph = ctx->begin("rows", s, 0);
+  uint32_t INV = 3u << Lt.A;
+  int kbits = Lt.A + 2;
+  if (n_parts > 1) {
+    const uint32_t INV2 = (uint32_t)n_parts << (Lt.A + 2);
+    k_owner_key<<<grid_for(E), 256, 0, s>>>(rk, E, INV, Lt.A, (uint32_t)n_parts, INV2);
+    INV = INV2;
+    kbits = Lt.A + 2 + bits_for((uint64_t)n_parts + 1);
+    if (kbits > 32) { set_error("row key with owner bits > 32 bits"); return OTTOHIP_ELIMIT; }
+  }
+  uint32_t *rks = rk, *poss = pos;
+  OH_TRY(radix_sort_pairs(ctx, rks, poss, rk2, pos2, E, kbits, s));
+  uint32_t *c_sorted = (rks == rk) ? rk2 : rk, *row_flag = (poss == pos) ? pos2 : pos;  // reuse the idle pair
+  k_gather_counts<<<grid_for(E), 256, 0, s>>>(rks, poss, F.cnt, E, INV, c_sorted, row_flag);
+  uint64_t *woff, *row_idx, *tot;
+  OH_TRY(ws.get("woff", (size_t)E, &woff));
+  OH_TRY(ws.get("row_idx", (size_t)E, &row_idx));
+  OH_TRY(ws.get("tot", 4, &tot));
+  OH_TRY(exclusive_scan_u32(ctx, c_sorted, woff, E, tot, s));
+  OH_TRY(exclusive_scan_u32(ctx, row_flag, row_idx, E, tot + 1, s));
+  uint64_t PR[2];
+  OH_TRY(d2h(PR, tot, 2, s));
+  int herr = 0;
+  OH_TRY(d2h(&herr, err, 1, s));
+  if (herr) { set_error("input out of range: aid outside [0, n_items) or type outside {0,1,2}"); return OTTOHIP_ERANGE; }
+  F.P = PR[0];
+  F.Rn = (int64_t)PR[1];
+  OH_TRY(ws.get("poff", (size_t)E, &F.poff));
+  OH_TRY(ws.get("row_key", (size_t)std::max<int64_t>(F.Rn, 1), &F.row_key));
+  OH_TRY(ws.get("row_begin", (size_t)std::max<int64_t>(F.Rn, 1), &F.row_begin));
+  k_rows<<<grid_for(E), 256, 0, s>>>(rks, poss, E, INV, Lt.A + 2 >= 32 ? ~0u : (1u << (Lt.A + 2)) - 1u, woff, row_flag, row_idx, F.poff,
+                                     F.row_key, F.row_begin);
+  ctx->end(ph, s);
+  return 0;
+}
+
+// S4: words of every qualifying pair at its row's offsets
+static int covis_emit_words(ottohip_ctx* ctx, const Front& F, const ottohip_events* ev, uint32_t* w0, hipStream_t s) {
+  int ph = ctx->begin("emit", s, 8.0 * F.E + 12.0 * F.E + 4.0 * (double)F.P);
+  k_emit<<<grid_for(F.NB, 4), 256, 0, s>>>(F.off, F.first, F.NB, F.evp, F.R, F.Lt, F.fb, ev->n_files, F.fid, F.cnt,
+                                            F.poff, w0);
+  if (F.nl > 0)
+    k_emit_long<<<F.nl, 64, 0, s>>>(F.off, F.long_list, F.d_loff, F.lscr, F.lpscr, F.evp, F.R, F.Lt, F.fb,
+                                     ev->n_files, F.fid, F.cnt, F.poff, w0);
+  if (hipGetLastError() != hipSuccess) { set_error("k_emit launch failed"); return OTTOHIP_EHIP; }
+  ctx->end(ph, s);
+  return 0;
+}
+
+// S5: words grouped by row -> table rows (count, count_ge2) and per-rule statistics
+static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P, const uint64_t* row_begin,
+                        const uint32_t* row_key, int64_t Rn, const RulesDev& R, const Layout& Lt, int n_rules,
+                        ottohip_table* T, hipStream_t s) {
+  Workspace& ws = ctx->ws;
+  int rc;
+  int* err;
+  OH_TRY(ws.get("err", 4, &err));
+  if (ctx->spare.cap >= P) {
+    T->b = ctx->spare;
+    ctx->spare = TableBufs();
+  } else {
+    (void)hipDeviceSynchronize();
+    ctx->spare.release();
+    OH_TRY(T->b.alloc(P));
+  }
+  unsigned long long *stats, *lcount;
+  OH_TRY(ws.get("stats", MAX_RULES * 4, &stats));
+  OH_TRY(ws.get("lcount", 8, &lcount));
+  hipMemsetAsync(stats, 0, MAX_RULES * 4 * 8, s);
+  hipMemsetAsync(err, 0, sizeof(int), s);
+  hipMemsetAsync(T->b.rule, 0xFF, P, s);  // rows are written at their task's word offsets: holes stay 0xFF
+  OutRows O;
+  O.rule = T->b.rule; O.aid = T->b.aid; O.aid_next = T->b.aid_next; O.count = T->b.count; O.count_ge2 = T->b.count_ge2;
+  O.cap = P; O.stats = stats;
+  int herr = 0;
+
+  int ph = ctx->begin("reduce", s, 4.0 * (double)P);
+  // level 0 task lists come from the rows
+  uint64_t cap0 = (uint64_t)std::max<int64_t>(Rn, 1);
+  TaskLists TL;
+  TL.n = lcount;
+  auto get_lists = [&](uint64_t capl, const char* split_name) -> int {
+    static const char* names[N_SORT] = {"t_sort0", "t_sort1", "t_sort2", "t_sort3", "t_sort4"};
+    for (int c = 0; c < N_SORT; ++c)
+      if (int r = ws.get(names[c], capl * sizeof(Task), reinterpret_cast<void**>(&TL.sort[c]))) return r;
+    if (int r = ws.get("t_hash", capl * sizeof(Task), reinterpret_cast<void**>(&TL.hash))) return r;
+    if (int r = ws.get(split_name, capl * sizeof(Task), reinterpret_cast<void**>(&TL.split))) return r;
+    TL.cap = capl;
+    return 0;
+  };
+  if ((rc = get_lists(cap0, "t_splitA"))) return rc;
+  hipMemsetAsync(lcount, 0, 8 * 8, s);
+  k_classify_rows<<<grid_for(Rn), 256, 0, s>>>(row_begin, Rn, P, Lt.WB, TL, err);
+  const int agg_grid = ctx->n_cu * 8;
+  bool srcA = true;
+  bool drained = false;
+  const bool dbg = getenv("OTTOHIP_DEBUG") != nullptr;
+  if (dbg) fprintf(stderr, "[ottohip] P=%llu rows=%lld\n", (unsigned long long)P, (long long)Rn);
+  for (int level = 0; level < 40; ++level) {
+    unsigned long long nlist[N_SORT + 2];
+    if ((rc = d2h(nlist, lcount, N_SORT + 2, s))) return rc;
+    if ((rc = d2h(&herr, err, 1, s))) return rc;
+    if (herr) { set_error("task list overflow / row too large (err=%d)", herr); return OTTOHIP_ELIMIT; }
+    if (dbg)
+      fprintf(stderr, "[ottohip] level %d: sort %llu/%llu/%llu/%llu/%llu hash %llu split %llu\n", level, nlist[0],
+              nlist[1], nlist[2], nlist[3], nlist[4], nlist[N_SORT], nlist[N_SORT + 1]);
+    const unsigned sgrid = (unsigned)ctx->n_cu * 32;
+#define OH_SORT(c, M)                                                                                      \
+    if (nlist[c])                                                                                          \
+      k_agg_sort<M><<<(unsigned)std::min<uint64_t>(ceil_div((int64_t)nlist[c], 4), sgrid), 256, 0, s>>>(   \
+          TL.sort[c], (int64_t)nlist[c], w0, w1, row_key, R, Lt, n_rules, O);
+    OH_SORT(0, 1) OH_SORT(1, 2) OH_SORT(2, 4) OH_SORT(3, 8) OH_SORT(4, 16)
+#undef OH_SORT
+    if (nlist[N_SORT]) {  // tasks that overflow the LDS table are appended to the split list
+      k_agg_hash<<<(unsigned)std::min<uint64_t>(nlist[N_SORT], (uint64_t)agg_grid), AGG_T, 0, s>>>(
+          TL.hash, (int64_t)nlist[N_SORT], w0, w1, row_key, R, Lt, n_rules, O, TL.split, lcount + N_SORT + 1);
+      if ((rc = d2h(nlist, lcount, N_SORT + 2, s))) return rc;
+    }
+    const int64_t ns = (int64_t)nlist[N_SORT + 1];
+    if (dbg) fprintf(stderr, "[ottohip] level %d: split after hash overflow %lld\n", level, (long long)ns);
+    if (ns == 0) { drained = true; break; }
+    if ((uint64_t)ns > TL.cap) { set_error("split list overflow"); return OTTOHIP_ELIMIT; }
+    Task* cur_split = TL.split;
+    // chunk / digit bases
+    uint32_t *nch, *ndg;
+    uint64_t *chb, *dgb, *tot2;
+    if ((rc = ws.get("sp_nch", (size_t)ns, &nch)) || (rc = ws.get("sp_ndg", (size_t)ns, &ndg)) ||
+        (rc = ws.get("sp_chb", (size_t)ns + 1, &chb)) || (rc = ws.get("sp_dgb", (size_t)ns + 1, &dgb)) ||
+        (rc = ws.get("sp_tot", 2, &tot2)))
+      return rc;
+    k_split_prepare<<<grid_for(ns), 256, 0, s>>>(cur_split, ns, Lt.WB, nch, ndg);
+    if ((rc = exclusive_scan_u32(ctx, nch, chb, ns, tot2, s)) || (rc = exclusive_scan_u32(ctx, ndg, dgb, ns, tot2 + 1, s)))
+      return rc;
+    uint64_t tt[2];
+    if ((rc = d2h(tt, tot2, 2, s))) return rc;
+    const int64_t nchunks = (int64_t)tt[0], ndig = (int64_t)tt[1];
+    uint32_t* dcount;
+    uint64_t* doff;
+    unsigned long long* dcur;
+    if ((rc = ws.get("sp_dcount", (size_t)ndig, &dcount)) || (rc = ws.get("sp_doff", (size_t)ndig, &doff)) ||
+        (rc = ws.get("sp_dcur", (size_t)ndig, &dcur)))
+      return rc;
+    hipMemsetAsync(dcount, 0, ndig * 4, s);
+    k_split_hist<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, dgb, w0, w1, Lt.WB, dcount);
+    if ((rc = exclusive_scan_u32(ctx, dcount, doff, ndig, nullptr, s))) return rc;
+    k_split_cursor<<<grid_for(ns * 64), 256, 0, s>>>(cur_split, ns, dgb, doff, dcur, Lt.WB);
+    k_split_scatter<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, dgb, w0, w1, Lt.WB, dcur);
+    // next lists (a sub-bucket is one task in exactly one list: ndig bounds every list)
+    const uint64_t capn = (uint64_t)ndig;
+    if ((rc = get_lists(std::max(cap0, capn), srcA ? "t_splitB" : "t_splitA"))) return rc;
+    hipMemsetAsync(lcount, 0, 8 * 8, s);
+    k_split_classify<<<grid_for(ndig), 256, 0, s>>>(cur_split, ns, dgb, dcount, doff, ndig, Lt.WB, TL, err);
+    srcA = !srcA;
+    if (hipGetLastError() != hipSuccess) { set_error("split launch failed"); return OTTOHIP_EHIP; }
+  }
+  ctx->end(ph, s);
+  if (!drained) { set_error("reduce: split levels did not converge"); return OTTOHIP_ELIMIT; }
+  unsigned long long st[MAX_RULES * 4];
+  if ((rc = d2h(st, stats, MAX_RULES * 4, s))) return rc;
+  if (hipGetLastError() != hipSuccess) { set_error("reduce failed"); return OTTOHIP_EHIP; }
+  unsigned long long sum_pairs = 0, U = 0;
+  for (int r = 0; r < n_rules; ++r) { sum_pairs += st[r * 4 + 1]; U += st[r * 4 + 0]; }
+  T->n_rows = (int64_t)U;
+  T->n_slots = (int64_t)P;
+  if (sum_pairs != P || U > P) {  // conservation: every emitted pair is counted exactly once
+    set_error("reduce: %llu pairs counted of %llu emitted (rows %llu)", sum_pairs, (unsigned long long)P, U);
+    return OTTOHIP_EHIP;
+  }
+  for (int r = 0; r < n_rules; ++r) {
+    T->stats[r].n_rows = (int64_t)st[r * 4 + 0];
+    T->stats[r].n_pairs = (int64_t)st[r * 4 + 1];
+    T->stats[r].file_rows = (int64_t)st[r * 4 + 2];
+    T->stats[r].file_rows_ge2 = (int64_t)st[r * 4 + 3];
+  }
+  return 0;
+}
+
 extern "C" {
 
 const char* ottohip_last_error(void) { return ottohip::g_err; }
@@ -102,277 +447,155 @@ int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohi
   hipStream_t s = S(stream);
   OH_HIP(hipSetDevice(ctx->device));
   ctx->reset_timing();
-  const int64_t E = ev->n_events, Sn = ev->n_sessions;
-  if (n_rules < 1 || n_rules > MAX_RULES) { set_error("n_rules=%d outside [1, %d]", n_rules, MAX_RULES); return OTTOHIP_EINVAL; }
-  if (E < 0 || Sn < 0 || (E > 0 && (!ev->session_offsets || !ev->aid || !ev->ts || !ev->type))) {
-    set_error("bad event table"); return OTTOHIP_EINVAL;
-  }
-  if (E >= ((int64_t)1 << 32)) { set_error("n_events=%lld >= 2^32 (split into shards)", (long long)E); return OTTOHIP_ELIMIT; }
-  if (params->n_items < 1 || params->n_items > (1 << 30)) { set_error("n_items=%d outside [1, 2^30]", params->n_items); return OTTOHIP_ERANGE; }
-  if (ev->n_files < 1 || !ev->file_session_bounds) { set_error("need >= 1 file"); return OTTOHIP_EINVAL; }
-  if (ev->file_session_bounds[0] != 0 || ev->file_session_bounds[ev->n_files] != Sn) {
-    set_error("file_session_bounds must start at 0 and end at n_sessions"); return OTTOHIP_EINVAL;
-  }
-  for (int f = 0; f < ev->n_files; ++f)
-    if (ev->file_session_bounds[f + 1] < ev->file_session_bounds[f]) { set_error("file bounds not monotone"); return OTTOHIP_EINVAL; }
-  if (ev->n_files > 65535) { set_error("n_files > 65535"); return OTTOHIP_ELIMIT; }
-
-  RulesDev R;
-  memset(&R, 0, sizeof R);
-  int max_per_type = 1;
-  for (int r = 0; r < n_rules; ++r) {
-    const ottohip_rule& q = rules[r];
-    if (q.this_type < 0 || q.this_type > 2 || (q.next_type_mask & ~7u) || q.max_abs_dt < 0) {
-      set_error("rule %d invalid", r); return OTTOHIP_EINVAL;
-    }
-    R.lo[r] = std::max(params->min_dt, -q.max_abs_dt);
-    R.hi[r] = std::min(params->max_dt, q.max_abs_dt);
-    R.mask[r] = q.next_type_mask;
-    int t = q.this_type;
-    R.rule_of_type[t][R.n_of_type[t]++] = r;
-    max_per_type = std::max(max_per_type, R.n_of_type[t]);
-  }
-  for (int r = 0; r < n_rules; ++r)
-    if (R.lo[r] > R.hi[r]) R.mask[r] = 0;  // empty window: never matches (count stays 0)
-  Layout Lt;
-  Lt.A = std::max(1, bits_for((uint64_t)params->n_items));
-  Lt.F = bits_for((uint64_t)ev->n_files);
-  Lt.BR = bits_for((uint64_t)max_per_type);
-  Lt.WB = Lt.BR + Lt.A + Lt.F;
-  Lt.amask = (1u << Lt.A) - 1u;
-  if (Lt.WB > 32) {
-    set_error("word layout %d rule + %d aid + %d file bits > 32: reduce files per call", Lt.BR, Lt.A, Lt.F);
-    return OTTOHIP_ELIMIT;
-  }
-
-  ottohip_table* T = new ottohip_table();
-  T->device = ctx->device;
-  T->n_rules = n_rules;
-  T->n_items = params->n_items;
-  T->ctx = ctx;
-  memset(T->stats, 0, sizeof T->stats);
+  Front F;
+  OH_TRY(check_events(ev));
+  OH_TRY(setup_rules(rules, n_rules, params, ev->n_files, F.R, F.Lt));
+  ottohip_table* T = new_table(ctx, n_rules, params->n_items);
   auto fail = [&](int rc) { ottohip_table_free(T); return rc; };
-  if (E == 0 || Sn == 0) { *out = T; return 0; }
-
-  Workspace& ws = ctx->ws;
-  const int64_t NB = ceil_div(E, EV_BLOCK);
-  int64_t *first, *fb;
-  int32_t *long_list, *n_long;
-  int* err;
-  const int64_t long_cap = E / (LCAP + 1) + 1;
   int rc;
-  if ((rc = ws.get("first", (size_t)NB + 1, &first)) || (rc = ws.get("fb", (size_t)ev->n_files + 1, &fb)) ||
-      (rc = ws.get("long_list", (size_t)long_cap, &long_list)) || (rc = ws.get("n_long", 4, &n_long)) ||
-      (rc = ws.get("err", 4, &err)))
-    return fail(rc);
-  if (hipMemcpyAsync(fb, ev->file_session_bounds, (ev->n_files + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s) ||
-      hipMemsetAsync(n_long, 0, 4 * sizeof(int32_t), s) || hipMemsetAsync(err, 0, sizeof(int), s)) {
-    set_error("hip memcpy/memset failed"); return fail(OTTOHIP_EHIP);
+  if ((rc = covis_front(ctx, ev, params, nullptr, 1, F, s))) return fail(rc);
+  if (F.P == 0) { *out = T; return 0; }
+  uint32_t *w0, *w1;
+  if ((rc = ctx->ws.get("words0", (size_t)F.P, &w0)) || (rc = ctx->ws.get("words1", (size_t)F.P, &w1))) return fail(rc);
+  if ((rc = covis_emit_words(ctx, F, ev, w0, s))) return fail(rc);
+  if ((rc = covis_reduce(ctx, w0, w1, F.P, F.row_begin, F.row_key, F.Rn, F.R, F.Lt, n_rules, T, s))) return fail(rc);
+  *out = T;
+  return 0;
+}
+
+int ottohip_covis_emit(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip_rule* rules, int n_rules,
+                       const ottohip_covis_params* params, const int32_t* file_ids, int32_t n_files_total,
+                       int n_parts, ottohip_emit** out, int64_t* words_per_part, int64_t* rows_per_part,
+                       void* stream) {
+  if (!ctx || !ev || !rules || !params || !out || !words_per_part || !rows_per_part || n_parts < 1 ||
+      n_parts > 256) {
+    set_error("ottohip_covis_emit: bad arguments (n_parts in [1, 256])"); return OTTOHIP_EINVAL;
   }
-  const int64_t* off = ev->session_offsets;
-
-  // ---- S1 prep
-  uint64_t* evp;
-  if ((rc = ws.get("ev", (size_t)E, &evp))) return fail(rc);
-  int ph = ctx->begin("prep", s, 9.0 * E + 8.0 * (Sn + 1) + 8.0 * E);
-  k_block_first<<<grid_for(Sn + 1), 256, 0, s>>>(off, Sn, NB, first, long_list, n_long);
-  k_prep<<<grid_for(NB, 4), 256, 0, s>>>(off, first, NB, ev->aid, ev->ts, ev->type, evp, params->n_items,
-                                          params->dedup, err);
-  if (hipGetLastError() != hipSuccess) { set_error("k_prep launch failed"); return fail(OTTOHIP_EHIP); }
-  int32_t nl = 0;
-  if ((rc = d2h(&nl, n_long, 1, s))) return fail(rc);
-  std::vector<int64_t> loff;
-  uint64_t *lscr = nullptr;
-  uint32_t *lpscr = nullptr;
-  int64_t* d_loff = nullptr;
-  if (nl > 0) {
-    std::vector<int32_t> ll(nl);
-    if ((rc = d2h(ll.data(), long_list, (size_t)nl, s))) return fail(rc);
-    std::sort(ll.begin(), ll.end());
-    if (hipMemcpy(long_list, ll.data(), nl * sizeof(int32_t), hipMemcpyHostToDevice)) return fail(OTTOHIP_EHIP);
-    loff.resize(nl + 1);
-    loff[0] = 0;
-    for (int i = 0; i < nl; ++i) {
-      int64_t ab[2];
-      if (hipMemcpy(ab, off + ll[i], 2 * sizeof(int64_t), hipMemcpyDeviceToHost)) return fail(OTTOHIP_EHIP);
-      loff[i + 1] = loff[i] + (ab[1] - ab[0]);
-    }
-    if ((rc = ws.get("long_scr", (size_t)(2 * loff[nl]), &lscr)) ||
-        (rc = ws.get("long_pscr", (size_t)(3 * (loff[nl] + nl)), &lpscr)) ||
-        (rc = ws.get("long_off", (size_t)(nl + 1), &d_loff)))
-      return fail(rc);
-    if (hipMemcpy(d_loff, loff.data(), (nl + 1) * sizeof(int64_t), hipMemcpyHostToDevice)) return fail(OTTOHIP_EHIP);
-    k_prep_long<<<nl, 64, 0, s>>>(off, long_list, d_loff, lscr, ev->aid, ev->ts, ev->type, evp, params->n_items,
-                                  params->dedup, err);
+  *out = nullptr;
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  ctx->reset_timing();
+  OH_TRY(check_events(ev));
+  if (n_files_total < ev->n_files) { set_error("n_files_total < n_files"); return OTTOHIP_EINVAL; }
+  for (int f = 0; f < ev->n_files && file_ids; ++f)
+    if (file_ids[f] < 0 || file_ids[f] >= n_files_total) { set_error("file_ids[%d] outside [0, n_files_total)", f); return OTTOHIP_EINVAL; }
+  ottohip_emit* E = new ottohip_emit();
+  E->n_parts = n_parts;
+  E->ev = *ev;
+  int rc;
+  if ((rc = setup_rules(rules, n_rules, params, n_files_total, E->F.R, E->F.Lt))) { delete E; return rc; }
+  if ((rc = covis_front(ctx, ev, params, file_ids, n_parts, E->F, s))) { delete E; return rc; }
+  E->gen = ctx->gen;
+  E->ctx = ctx;
+  E->first_row.assign(n_parts + 1, 0);
+  E->first_word.assign(n_parts + 1, 0);
+  if (E->F.Rn > 0) {
+    uint64_t *d_fr, *d_fw;
+    if ((rc = ctx->ws.get("part_first_row", (size_t)n_parts + 1, &d_fr)) ||
+        (rc = ctx->ws.get("part_first_word", (size_t)n_parts + 1, &d_fw))) { delete E; return rc; }
+    k_part_bounds<<<grid_for(E->F.Rn + 1), 256, 0, s>>>(E->F.row_key, E->F.Rn, E->F.Lt.A, (uint32_t)n_parts, d_fr);
+    k_part_words<<<grid_for(n_parts + 1), 256, 0, s>>>(d_fr, E->F.row_begin, E->F.Rn, E->F.P, (uint32_t)n_parts, d_fw);
+    if ((rc = d2h(E->first_row.data(), d_fr, (size_t)n_parts + 1, s)) ||
+        (rc = d2h(E->first_word.data(), d_fw, (size_t)n_parts + 1, s))) { delete E; return rc; }
   }
-  ctx->end(ph, s);
+  for (int p = 0; p < n_parts; ++p) {
+    rows_per_part[p] = (int64_t)(E->first_row[p + 1] - E->first_row[p]);
+    words_per_part[p] = (int64_t)(E->first_word[p + 1] - E->first_word[p]);
+  }
+  *out = E;
+  return 0;
+}
 
-  // ---- S2 count
-  uint32_t *cnt, *rk, *pos, *rk2, *pos2;
-  if ((rc = ws.get("cnt", (size_t)E, &cnt)) || (rc = ws.get("rk", (size_t)E, &rk)) || (rc = ws.get("pos", (size_t)E, &pos)) ||
-      (rc = ws.get("rk2", (size_t)E, &rk2)) || (rc = ws.get("pos2", (size_t)E, &pos2)))
-    return fail(rc);
-  ph = ctx->begin("count", s, 8.0 * E + 12.0 * E);
-  k_count<<<grid_for(NB, 4), 256, 0, s>>>(off, first, NB, evp, R, Lt.A, cnt, rk, pos);
-  if (nl > 0) k_count_long<<<nl, 64, 0, s>>>(off, long_list, d_loff, lscr, lpscr, evp, R, Lt.A, cnt, rk, pos);
-  if (hipGetLastError() != hipSuccess) { set_error("k_count launch failed"); return fail(OTTOHIP_EHIP); }
-  ctx->end(ph, s);
+int ottohip_emit_write(ottohip_emit* E, uint32_t* words, uint64_t* pieces, void* stream) {
+  if (!E || (E->F.P > 0 && !words) || (E->F.Rn > 0 && !pieces)) { set_error("emit_write: bad arguments"); return OTTOHIP_EINVAL; }
+  if (E->gen != E->ctx->gen) {
+    set_error("emit_write: the context ran another count after ottohip_covis_emit"); return OTTOHIP_EINVAL;
+  }
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(E->ctx->device));
+  if (E->F.P > 0) OH_TRY(covis_emit_words(E->ctx, E->F, &E->ev, words, s));
+  if (E->F.Rn > 0) {
+    k_piece_pack<<<grid_for(E->F.Rn), 256, 0, s>>>(E->F.row_key, E->F.row_begin, E->F.Rn, E->F.P, pieces);
+    OH_HIP(hipGetLastError());
+  }
+  return 0;
+}
 
-  // ---- S3 rows (aid-major transpose)
-  ph = ctx->begin("rows", s, 0);
-  uint32_t *rks = rk, *poss = pos;
-  if ((rc = radix_sort_pairs(ctx, rks, poss, rk2, pos2, E, Lt.A + 2, s))) return fail(rc);
-  uint32_t *c_sorted = (rks == rk) ? rk2 : rk, *row_flag = (poss == pos) ? pos2 : pos;  // reuse the idle pair
-  const uint32_t INV = 3u << Lt.A;
-  k_gather_counts<<<grid_for(E), 256, 0, s>>>(rks, poss, cnt, E, INV, c_sorted, row_flag);
-  uint64_t *woff, *row_idx, *tot;
-  if ((rc = ws.get("woff", (size_t)E, &woff)) || (rc = ws.get("row_idx", (size_t)E, &row_idx)) ||
-      (rc = ws.get("tot", 4, &tot)))
-    return fail(rc);
-  if ((rc = exclusive_scan_u32(ctx, c_sorted, woff, E, tot, s))) return fail(rc);
-  if ((rc = exclusive_scan_u32(ctx, row_flag, row_idx, E, tot + 1, s))) return fail(rc);
-  uint64_t PR[2];
-  if ((rc = d2h(PR, tot, 2, s))) return fail(rc);
-  int herr = 0;
-  if ((rc = d2h(&herr, err, 1, s))) return fail(rc);
-  if (herr) { set_error("input out of range: aid outside [0, n_items) or type outside {0,1,2}"); return fail(OTTOHIP_ERANGE); }
-  const uint64_t P = PR[0];
-  const int64_t Rn = (int64_t)PR[1];
-  uint64_t *poff, *row_begin;
+void ottohip_emit_free(ottohip_emit* E) { delete E; }
+
+int ottohip_covis_reduce_received(ottohip_ctx* ctx, const ottohip_rule* rules, int n_rules,
+                                  const ottohip_covis_params* params, int32_t n_files_total, const uint32_t* words,
+                                  int64_t n_words, const uint64_t* pieces, int64_t n_pieces, ottohip_table** out,
+                                  void* stream) {
+  if (!ctx || !rules || !params || !out || n_words < 0 || n_pieces < 0 || (n_words > 0 && !words) ||
+      (n_pieces > 0 && !pieces)) {
+    set_error("ottohip_covis_reduce_received: bad arguments"); return OTTOHIP_EINVAL;
+  }
+  *out = nullptr;
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  ctx->reset_timing();
+  RulesDev R;
+  Layout Lt;
+  OH_TRY(setup_rules(rules, n_rules, params, std::max(n_files_total, 1), R, Lt));
+  if (n_words >= ((int64_t)1 << 40) || n_pieces >= ((int64_t)1 << 32)) { set_error("received input too large"); return OTTOHIP_ELIMIT; }
+  ottohip_table* T = new_table(ctx, n_rules, params->n_items);
+  auto fail = [&](int rc) { ottohip_table_free(T); return rc; };
+  if (n_words == 0) { *out = T; return 0; }
+  Workspace& ws = ctx->ws;
+  const int64_t n = n_pieces;
+  uint32_t *key, *val, *k1, *v1, *len, *lsort, *head;
+  uint64_t *src_off, *dst, *row_idx, *tot, *row_begin;
   uint32_t* row_key;
-  if ((rc = ws.get("poff", (size_t)E, &poff)) || (rc = ws.get("row_key", (size_t)std::max<int64_t>(Rn, 1), &row_key)) ||
-      (rc = ws.get("row_begin", (size_t)std::max<int64_t>(Rn, 1), &row_begin)))
+  int* err;
+  int rc;
+  if ((rc = ws.get("pc_key", (size_t)n, &key)) || (rc = ws.get("pc_val", (size_t)n, &val)) ||
+      (rc = ws.get("pc_k1", (size_t)n, &k1)) || (rc = ws.get("pc_v1", (size_t)n, &v1)) ||
+      (rc = ws.get("pc_len", (size_t)n, &len)) || (rc = ws.get("pc_lsort", (size_t)n, &lsort)) ||
+      (rc = ws.get("pc_head", (size_t)n, &head)) || (rc = ws.get("pc_src", (size_t)n, &src_off)) ||
+      (rc = ws.get("pc_dst", (size_t)n, &dst)) || (rc = ws.get("pc_ridx", (size_t)n, &row_idx)) ||
+      (rc = ws.get("pc_tot", 4, &tot)) || (rc = ws.get("err", 4, &err)) ||
+      (rc = ws.get("row_key", (size_t)n, &row_key)) || (rc = ws.get("row_begin", (size_t)n, &row_begin)))
     return fail(rc);
-  k_rows<<<grid_for(E), 256, 0, s>>>(rks, poss, E, INV, woff, row_flag, row_idx, poff, row_key, row_begin);
-  ctx->end(ph, s);
-  if (P == 0) { *out = T; return 0; }
-
-  // ---- S4 emit
+  const int kbits = Lt.A + 2;
+  int ph = ctx->begin("assemble", s, 8.0 * (double)n_words + 24.0 * (double)n);
+  hipMemsetAsync(err, 0, sizeof(int), s);
+  k_piece_keys<<<grid_for(n), 256, 0, s>>>(pieces, n, key, val, len, 3u << Lt.A, err);
+  // source offsets of the pieces (received order), then pieces by row key (stable: by source)
+  if ((rc = exclusive_scan_u32(ctx, len, src_off, n, tot, s))) return fail(rc);
+  uint32_t *ks = key, *vs = val;
+  if ((rc = radix_sort_pairs(ctx, ks, vs, k1, v1, n, kbits, s))) return fail(rc);
+  k_piece_order<<<grid_for(n), 256, 0, s>>>(ks, vs, len, n, lsort, head);
+  if ((rc = exclusive_scan_u32(ctx, lsort, dst, n, tot + 1, s)) || (rc = exclusive_scan_u32(ctx, head, row_idx, n, tot + 2, s)))
+    return fail(rc);
+  uint64_t tt[3];
+  int herr = 0;
+  if ((rc = d2h(tt, tot, 3, s)) || (rc = d2h(&herr, err, 1, s))) return fail(rc);
+  if (herr) { set_error("reduce_received: piece row key out of range"); return fail(OTTOHIP_ERANGE); }
+  if ((int64_t)tt[0] != n_words) {
+    set_error("reduce_received: pieces hold %llu words, %lld received", (unsigned long long)tt[0], (long long)n_words);
+    return fail(OTTOHIP_EINVAL);
+  }
+  const uint64_t P = tt[0];
+  const int64_t Rn = (int64_t)tt[2];
   uint32_t *w0, *w1;
   if ((rc = ws.get("words0", (size_t)P, &w0)) || (rc = ws.get("words1", (size_t)P, &w1))) return fail(rc);
-  ph = ctx->begin("emit", s, 8.0 * E + 12.0 * E + 4.0 * (double)P);
-  k_emit<<<grid_for(NB, 4), 256, 0, s>>>(off, first, NB, evp, R, Lt, fb, ev->n_files, cnt, poff, w0);
-  if (nl > 0)
-    k_emit_long<<<nl, 64, 0, s>>>(off, long_list, d_loff, lscr, lpscr, evp, R, Lt, fb, ev->n_files, cnt, poff, w0);
-  if (hipGetLastError() != hipSuccess) { set_error("k_emit launch failed"); return fail(OTTOHIP_EHIP); }
+  k_piece_rows<<<grid_for(n), 256, 0, s>>>(ks, head, row_idx, dst, n, row_key, row_begin);
+  k_piece_copy<<<(unsigned)std::min<int64_t>(ceil_div(n, 4), (int64_t)ctx->n_cu * 16), 256, 0, s>>>(
+      vs, len, src_off, dst, n, words, w0);
+  if (hipGetLastError() != hipSuccess) { set_error("assemble launch failed"); return fail(OTTOHIP_EHIP); }
   ctx->end(ph, s);
-
-  // ---- S5 reduce
-  if (ctx->spare.cap >= P) {
-    T->b = ctx->spare;
-    ctx->spare = TableBufs();
-  } else {
-    (void)hipDeviceSynchronize();
-    ctx->spare.release();
-    if ((rc = T->b.alloc(P))) return fail(rc);
-  }
-  unsigned long long *stats, *lcount;
-  if ((rc = ws.get("stats", MAX_RULES * 4, &stats)) || (rc = ws.get("lcount", 8, &lcount))) return fail(rc);
-  hipMemsetAsync(stats, 0, MAX_RULES * 4 * 8, s);
-  hipMemsetAsync(T->b.rule, 0xFF, P, s);  // rows are written at their task's word offsets: holes stay 0xFF
-  OutRows O;
-  O.rule = T->b.rule; O.aid = T->b.aid; O.aid_next = T->b.aid_next; O.count = T->b.count; O.count_ge2 = T->b.count_ge2;
-  O.cap = P; O.stats = stats;
-
-  ph = ctx->begin("reduce", s, 4.0 * (double)P);
-  // level 0 task lists come from the rows
-  uint64_t cap0 = (uint64_t)std::max<int64_t>(Rn, 1);
-  TaskLists TL;
-  TL.n = lcount;
-  auto get_lists = [&](uint64_t capl, const char* split_name) -> int {
-    static const char* names[N_SORT] = {"t_sort0", "t_sort1", "t_sort2", "t_sort3", "t_sort4"};
-    for (int c = 0; c < N_SORT; ++c)
-      if (int r = ws.get(names[c], capl * sizeof(Task), reinterpret_cast<void**>(&TL.sort[c]))) return r;
-    if (int r = ws.get("t_hash", capl * sizeof(Task), reinterpret_cast<void**>(&TL.hash))) return r;
-    if (int r = ws.get(split_name, capl * sizeof(Task), reinterpret_cast<void**>(&TL.split))) return r;
-    TL.cap = capl;
-    return 0;
-  };
-  if ((rc = get_lists(cap0, "t_splitA"))) return fail(rc);
-  hipMemsetAsync(lcount, 0, 8 * 8, s);
-  k_classify_rows<<<grid_for(Rn), 256, 0, s>>>(row_begin, Rn, P, Lt.WB, TL, err);
-  const int agg_grid = ctx->n_cu * 8;
-  bool srcA = true;
-  bool drained = false;
-  const bool dbg = getenv("OTTOHIP_DEBUG") != nullptr;
-  if (dbg) fprintf(stderr, "[ottohip] E=%lld P=%llu rows=%lld nlong=%d\n", (long long)E, (unsigned long long)P, (long long)Rn, nl);
-  for (int level = 0; level < 40; ++level) {
-    unsigned long long nlist[N_SORT + 2];
-    if ((rc = d2h(nlist, lcount, N_SORT + 2, s))) return fail(rc);
-    if ((rc = d2h(&herr, err, 1, s))) return fail(rc);
-    if (herr) { set_error("task list overflow / row too large (err=%d)", herr); return fail(OTTOHIP_ELIMIT); }
-    if (dbg)
-      fprintf(stderr, "[ottohip] level %d: sort %llu/%llu/%llu/%llu/%llu hash %llu split %llu\n", level, nlist[0],
-              nlist[1], nlist[2], nlist[3], nlist[4], nlist[N_SORT], nlist[N_SORT + 1]);
-    const unsigned sgrid = (unsigned)ctx->n_cu * 32;
-#define OH_SORT(c, M)                                                                                      \
-    if (nlist[c])                                                                                          \
-      k_agg_sort<M><<<(unsigned)std::min<uint64_t>(ceil_div((int64_t)nlist[c], 4), sgrid), 256, 0, s>>>(   \
-          TL.sort[c], (int64_t)nlist[c], w0, w1, row_key, R, Lt, n_rules, O);
-    OH_SORT(0, 1) OH_SORT(1, 2) OH_SORT(2, 4) OH_SORT(3, 8) OH_SORT(4, 16)
-#undef OH_SORT
-    if (nlist[N_SORT]) {  // tasks that overflow the LDS table are appended to the split list
-      k_agg_hash<<<(unsigned)std::min<uint64_t>(nlist[N_SORT], (uint64_t)agg_grid), AGG_T, 0, s>>>(
-          TL.hash, (int64_t)nlist[N_SORT], w0, w1, row_key, R, Lt, n_rules, O, TL.split, lcount + N_SORT + 1);
-      if ((rc = d2h(nlist, lcount, N_SORT + 2, s))) return fail(rc);
-    }
-    const int64_t ns = (int64_t)nlist[N_SORT + 1];
-    if (dbg) fprintf(stderr, "[ottohip] level %d: split after hash overflow %lld\n", level, (long long)ns);
-    if (ns == 0) { drained = true; break; }
-    if ((uint64_t)ns > TL.cap) { set_error("split list overflow"); return fail(OTTOHIP_ELIMIT); }
-    Task* cur_split = TL.split;
-    // chunk / digit bases
-    uint32_t *nch, *ndg;
-    uint64_t *chb, *dgb, *tot2;
-    if ((rc = ws.get("sp_nch", (size_t)ns, &nch)) || (rc = ws.get("sp_ndg", (size_t)ns, &ndg)) ||
-        (rc = ws.get("sp_chb", (size_t)ns + 1, &chb)) || (rc = ws.get("sp_dgb", (size_t)ns + 1, &dgb)) ||
-        (rc = ws.get("sp_tot", 2, &tot2)))
-      return fail(rc);
-    k_split_prepare<<<grid_for(ns), 256, 0, s>>>(cur_split, ns, Lt.WB, nch, ndg);
-    if ((rc = exclusive_scan_u32(ctx, nch, chb, ns, tot2, s)) || (rc = exclusive_scan_u32(ctx, ndg, dgb, ns, tot2 + 1, s)))
-      return fail(rc);
-    uint64_t tt[2];
-    if ((rc = d2h(tt, tot2, 2, s))) return fail(rc);
-    const int64_t nchunks = (int64_t)tt[0], ndig = (int64_t)tt[1];
-    uint32_t* dcount;
-    uint64_t* doff;
-    unsigned long long* dcur;
-    if ((rc = ws.get("sp_dcount", (size_t)ndig, &dcount)) || (rc = ws.get("sp_doff", (size_t)ndig, &doff)) ||
-        (rc = ws.get("sp_dcur", (size_t)ndig, &dcur)))
-      return fail(rc);
-    hipMemsetAsync(dcount, 0, ndig * 4, s);
-    k_split_hist<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, dgb, w0, w1, Lt.WB, dcount);
-    if ((rc = exclusive_scan_u32(ctx, dcount, doff, ndig, nullptr, s))) return fail(rc);
-    k_split_cursor<<<grid_for(ns * 64), 256, 0, s>>>(cur_split, ns, dgb, doff, dcur, Lt.WB);
-    k_split_scatter<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, dgb, w0, w1, Lt.WB, dcur);
-    // next lists (a sub-bucket is one task in exactly one list: ndig bounds every list)
-    const uint64_t capn = (uint64_t)ndig;
-    if ((rc = get_lists(std::max(cap0, capn), srcA ? "t_splitB" : "t_splitA"))) return fail(rc);
-    hipMemsetAsync(lcount, 0, 8 * 8, s);
-    k_split_classify<<<grid_for(ndig), 256, 0, s>>>(cur_split, ns, dgb, dcount, doff, ndig, Lt.WB, TL, err);
-    srcA = !srcA;
-    if (hipGetLastError() != hipSuccess) { set_error("split launch failed"); return fail(OTTOHIP_EHIP); }
-  }
-  ctx->end(ph, s);
-  if (!drained) { set_error("reduce: split levels did not converge"); return fail(OTTOHIP_ELIMIT); }
-  unsigned long long st[MAX_RULES * 4];
-  if ((rc = d2h(st, stats, MAX_RULES * 4, s))) return fail(rc);
-  if (hipGetLastError() != hipSuccess) { set_error("reduce failed"); return fail(OTTOHIP_EHIP); }
-  unsigned long long sum_pairs = 0, U = 0;
-  for (int r = 0; r < n_rules; ++r) { sum_pairs += st[r * 4 + 1]; U += st[r * 4 + 0]; }
-  T->n_rows = (int64_t)U;
-  T->n_slots = (int64_t)P;
-  if (sum_pairs != P || U > P) {  // conservation: every emitted pair is counted exactly once
-    set_error("reduce: %llu pairs counted of %llu emitted (rows %llu)", sum_pairs, (unsigned long long)P, U);
-    return fail(OTTOHIP_EHIP);
-  }
-  for (int r = 0; r < n_rules; ++r) {
-    T->stats[r].n_rows = (int64_t)st[r * 4 + 0];
-    T->stats[r].n_pairs = (int64_t)st[r * 4 + 1];
-    T->stats[r].file_rows = (int64_t)st[r * 4 + 2];
-    T->stats[r].file_rows_ge2 = (int64_t)st[r * 4 + 3];
-  }
+  if ((rc = covis_reduce(ctx, w0, w1, P, row_begin, row_key, Rn, R, Lt, n_rules, T, s))) return fail(rc);
   *out = T;
+  return 0;
+}
+
+int ottohip_table_set_file_stats(ottohip_table* t, int rule, int64_t file_rows, int64_t file_rows_ge2) {
+  if (!t || rule < 0 || rule >= t->n_rules || file_rows < 0 || file_rows_ge2 < 0) {
+    set_error("table_set_file_stats: bad args"); return OTTOHIP_EINVAL;
+  }
+  t->stats[rule].file_rows = file_rows;
+  t->stats[rule].file_rows_ge2 = file_rows_ge2;
   return 0;
 }
 

@@ -140,6 +140,11 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
   return v;
 }
 
+// owner rank of an aid for the multi-GPU layout: multiplicative hash, range-reduced (no modulo)
+__host__ __device__ __forceinline__ uint32_t owner_dev(uint32_t aid, uint32_t n_parts) {
+  return (uint32_t)(((uint64_t)(aid * 0x9E3779B1u) * n_parts) >> 32);
+}
+
 // Packed event: high 32 = ts ^ 0x80000000 (orders like signed ts), low 32 = aid << 2 | type.
 // Sorting packed events ascending orders a session by (ts, aid, type); equal words are the
 // exact duplicates removed by df.unique() (model/count_co_events.py:92).

@@ -308,7 +308,7 @@ __global__ void k_gather_counts(const uint32_t* __restrict__ rk, const uint32_t*
 }
 
 __global__ void k_rows(const uint32_t* __restrict__ rk, const uint32_t* __restrict__ pos, int64_t n, uint32_t INV,
-                       const uint64_t* __restrict__ woff, const uint32_t* __restrict__ row_flag,
+                       uint32_t kmask, const uint64_t* __restrict__ woff, const uint32_t* __restrict__ row_flag,
                        const uint64_t* __restrict__ row_idx, uint64_t* __restrict__ poff,
                        uint32_t* __restrict__ row_key, uint64_t* __restrict__ row_begin) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -318,8 +318,92 @@ __global__ void k_rows(const uint32_t* __restrict__ rk, const uint32_t* __restri
   poff[pos[k]] = woff[k];
   if (row_flag[k]) {
     const uint64_t r = row_idx[k];
-    row_key[r] = key;
+    row_key[r] = key & kmask;  // (type, aid); owner bits (multi-GPU layout) dropped
     row_begin[r] = woff[k];
+  }
+}
+
+// multi-GPU layout: row keys become (owner(aid), type, aid) so every owner's rows and words
+// are contiguous (the all-to-all send segments); invalid events sort after every owner
+__global__ void k_owner_key(uint32_t* __restrict__ rk, int64_t n, uint32_t INV, int A, uint32_t G, uint32_t INV2) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t key = rk[k];
+  rk[k] = key == INV ? INV2 : ((owner_dev(key & ((1u << A) - 1u), G) << (A + 2)) | key);
+}
+
+// first row of every owner (rows are owner-major); first_row[G] = R
+__global__ void k_part_bounds(const uint32_t* __restrict__ row_key, int64_t R, int A, uint32_t G,
+                              uint64_t* __restrict__ first_row) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r > R) return;
+  const int64_t prev = r == 0 ? -1 : (int64_t)owner_dev(row_key[r - 1] & ((1u << A) - 1u), G);
+  const int64_t cur = r == R ? (int64_t)G : (int64_t)owner_dev(row_key[r] & ((1u << A) - 1u), G);
+  for (int64_t o = prev + 1; o <= cur; ++o) first_row[o] = (uint64_t)r;
+}
+
+__global__ void k_part_words(const uint64_t* __restrict__ first_row, const uint64_t* __restrict__ row_begin, int64_t R,
+                             uint64_t P, uint32_t G, uint64_t* __restrict__ first_word) {
+  const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o > G) return;
+  const uint64_t r = first_row[o];
+  first_word[o] = r < (uint64_t)R ? row_begin[r] : P;
+}
+
+// rows of one rank -> piece records (row_key << 32 | n_words), the all-to-all companion of the words
+__global__ void k_piece_pack(const uint32_t* __restrict__ row_key, const uint64_t* __restrict__ row_begin, int64_t R,
+                             uint64_t P, uint64_t* __restrict__ pieces) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const uint64_t e = r + 1 < R ? row_begin[r + 1] : P;
+  pieces[r] = ((uint64_t)row_key[r] << 32) | (e - row_begin[r]);
+}
+
+// ---- received pieces (one per (source, row)) -> one contiguous word range per row
+// piece record: u64 (row_key << 32) | n_words
+__global__ void k_piece_keys(const uint64_t* __restrict__ pieces, int64_t n, uint32_t* __restrict__ key,
+                             uint32_t* __restrict__ val, uint32_t* __restrict__ len, uint32_t kmax,
+                             int* __restrict__ err) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t p = pieces[i];
+  const uint32_t k = (uint32_t)(p >> 32);
+  if (k >= kmax) atomicOr(err, 1);
+  key[i] = k;
+  val[i] = (uint32_t)i;
+  len[i] = (uint32_t)p;
+}
+
+__global__ void k_piece_order(const uint32_t* __restrict__ key, const uint32_t* __restrict__ val,
+                              const uint32_t* __restrict__ len, int64_t n, uint32_t* __restrict__ len_sorted,
+                              uint32_t* __restrict__ head) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  len_sorted[i] = len[val[i]];
+  head[i] = (i == 0 || key[i] != key[i - 1]) ? 1u : 0u;
+}
+
+__global__ void k_piece_rows(const uint32_t* __restrict__ key, const uint32_t* __restrict__ head,
+                             const uint64_t* __restrict__ row_idx, const uint64_t* __restrict__ dst, int64_t n,
+                             uint32_t* __restrict__ row_key, uint64_t* __restrict__ row_begin) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !head[i]) return;
+  row_key[row_idx[i]] = key[i];
+  row_begin[row_idx[i]] = dst[i];
+}
+
+// one wave per piece (grid-stride): copy its words to the row's range
+__global__ __launch_bounds__(256) void k_piece_copy(const uint32_t* __restrict__ val, const uint32_t* __restrict__ len,
+                                                    const uint64_t* __restrict__ src_off,
+                                                    const uint64_t* __restrict__ dst, int64_t n,
+                                                    const uint32_t* __restrict__ in, uint32_t* __restrict__ out) {
+  const int l = threadIdx.x & 63;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n;
+       i += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+    const uint32_t p = val[i];
+    const uint64_t s0 = src_off[p], d0 = dst[i];
+    const uint32_t m = len[p];
+    for (uint32_t k = l; k < m; k += 64) out[d0 + k] = in[s0 + k];
   }
 }
 
@@ -362,7 +446,7 @@ __device__ __forceinline__ void emit_session(const SessView& S, int64_t e0, cons
 
 __global__ __launch_bounds__(256) void k_emit(const int64_t* __restrict__ off, const int64_t* __restrict__ first,
                                               int64_t NB, const uint64_t* __restrict__ ev, RulesDev R, Layout L,
-                                              const int64_t* __restrict__ fb, int nf,
+                                              const int64_t* __restrict__ fb, int nf, const uint32_t* __restrict__ fid,
                                               const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ poff,
                                               uint32_t* __restrict__ words) {
   __shared__ uint64_t sev[4][LCAP];
@@ -381,7 +465,7 @@ __global__ __launch_bounds__(256) void k_emit(const int64_t* __restrict__ off, c
     SessView S;
     S.ev = sev[w]; S.pref = spref[w]; S.pstride = LCAP + 1;
     S.nv = load_session(ev + e0, n, sev[w], spref[w], LCAP + 1);
-    emit_session(S, e0, R, L, (uint32_t)f, cnt, poff, words);
+    emit_session(S, e0, R, L, fid[f], cnt, poff, words);
     __builtin_amdgcn_wave_barrier();
   }
 }
@@ -391,6 +475,7 @@ __global__ __launch_bounds__(64) void k_emit_long(const int64_t* __restrict__ of
                                                   uint64_t* __restrict__ scratch, uint32_t* __restrict__ pscratch,
                                                   const uint64_t* __restrict__ ev, RulesDev R, Layout L,
                                                   const int64_t* __restrict__ fb, int nf,
+                                                  const uint32_t* __restrict__ fid,
                                                   const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ poff,
                                                   uint32_t* __restrict__ words) {
   const int64_t s = list[blockIdx.x];
@@ -402,7 +487,7 @@ __global__ __launch_bounds__(64) void k_emit_long(const int64_t* __restrict__ of
   uint32_t* pref = pscratch + 3 * (so + blockIdx.x);
   S.ev = evs; S.pref = pref; S.pstride = n + 1;
   S.nv = load_session(ev + e0, n, evs, pref, n + 1);
-  emit_session(S, e0, R, L, (uint32_t)file_of(fb, nf, s), cnt, poff, words);
+  emit_session(S, e0, R, L, fid[file_of(fb, nf, s)], cnt, poff, words);
 }
 
 // ------------------------------------------------------------------ S5 reduce

@@ -21,10 +21,6 @@ constexpr int PK_CHUNK = PK_T * PK_PER;    // slots per block
 constexpr int PK_MAXP = 256;               // max owners
 constexpr uint32_t REC_AID_MASK = (1u << 29) - 1u;
 
-__device__ __forceinline__ uint32_t owner_dev(uint32_t aid, uint32_t n_parts) {
-  return (uint32_t)(((uint64_t)(aid * 0x9E3779B1u) * n_parts) >> 32);
-}
-
 // per block, rows per owner -> cnt[owner * nblk + block] (owner-major, so one exclusive scan
 // gives every block's base offset inside every owner's segment)
 __global__ __launch_bounds__(PK_T) void k_own_hist(const uint8_t* __restrict__ rule, const int32_t* __restrict__ aid,
@@ -101,17 +97,21 @@ __global__ void k_rec_gather(const uint4* __restrict__ rec, const uint32_t* __re
   head[i] = (i == 0 || rec_key(rec[p]) != rec_key(rec[perm[i - 1]])) ? 1u : 0u;
 }
 
-// one thread per run head: sum the run (<= one record per source rank), write the row and
-// fold per-rule row / pair totals with one atomic per wave and rule
-__global__ void k_rec_reduce(const uint4* __restrict__ srt, int64_t n, const uint32_t* __restrict__ head,
-                             const uint64_t* __restrict__ idx, int n_rules, uint8_t* __restrict__ o_rule,
-                             int32_t* __restrict__ o_aid, int32_t* __restrict__ o_next, uint32_t* __restrict__ o_cnt,
-                             uint32_t* __restrict__ o_ge2, unsigned long long* __restrict__ stats,
-                             int* __restrict__ err) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  int r = -1;
-  uint32_t c = 0;
-  if (i < n && head[i]) {
+// one thread per run head (grid-stride): sum the run (<= one record per source rank) and write
+// the row; per-rule row / pair totals stay in registers and leave with one atomic per block
+__global__ __launch_bounds__(256) void k_rec_reduce(const uint4* __restrict__ srt, int64_t n,
+                                                    const uint32_t* __restrict__ head,
+                                                    const uint64_t* __restrict__ idx, int n_rules,
+                                                    uint8_t* __restrict__ o_rule, int32_t* __restrict__ o_aid,
+                                                    int32_t* __restrict__ o_next, uint32_t* __restrict__ o_cnt,
+                                                    uint32_t* __restrict__ o_ge2, unsigned long long* __restrict__ stats,
+                                                    int* __restrict__ err) {
+  __shared__ unsigned long long part[MAX_RULES * 2];
+  if (threadIdx.x < MAX_RULES * 2) part[threadIdx.x] = 0;
+  __syncthreads();
+  uint64_t rows[MAX_RULES] = {}, pairs[MAX_RULES] = {};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (!head[i]) continue;
     const uint4 a = srt[i];
     uint64_t cs = a.z, gs = a.w;
     for (int64_t j = i + 1; j < n && !head[j]; ++j) {
@@ -121,23 +121,28 @@ __global__ void k_rec_reduce(const uint4* __restrict__ srt, int64_t n, const uin
     }
     if (cs > 0xFFFFFFFFull) atomicOr(err, 2);
     const uint64_t o = idx[i];
-    r = (int)(a.x >> 29);
+    const int r = (int)(a.x >> 29);
     o_rule[o] = (uint8_t)r;
     o_aid[o] = (int32_t)(a.x & REC_AID_MASK);
     o_next[o] = (int32_t)a.y;
     o_cnt[o] = (uint32_t)cs;
     o_ge2[o] = (uint32_t)gs;
-    c = (uint32_t)cs;
+#pragma unroll
+    for (int q = 0; q < MAX_RULES; ++q)
+      if (q == r) { rows[q] += 1; pairs[q] += cs; }
   }
-  for (int q = 0; q < n_rules; ++q) {
-    const uint64_t m = __ballot(r == q);
-    if (!m) continue;
-    const uint64_t pairs = wave_sum64(r == q ? (uint64_t)c : 0ull);
-    if (lane_id() == 0) {
-      atomicAdd(&stats[q * 4 + 0], (unsigned long long)__popcll(m));
-      atomicAdd(&stats[q * 4 + 1], (unsigned long long)pairs);
+#pragma unroll
+  for (int q = 0; q < MAX_RULES; ++q) {
+    if (q >= n_rules) break;
+    const uint64_t rw = wave_sum64(rows[q]), pr = wave_sum64(pairs[q]);
+    if (lane_id() == 0 && rw) {
+      atomicAdd(&part[2 * q], (unsigned long long)rw);
+      atomicAdd(&part[2 * q + 1], (unsigned long long)pr);
     }
   }
+  __syncthreads();
+  if (threadIdx.x < 2 * n_rules && part[threadIdx.x])
+    atomicAdd(&stats[(threadIdx.x >> 1) * 4 + (threadIdx.x & 1)], part[threadIdx.x]);
 }
 
 }  // namespace ottohip
@@ -255,7 +260,7 @@ int ottohip_table_from_records(ottohip_ctx* ctx, const void* records, int64_t n,
     ctx->spare.release();
     if ((rc = T->b.alloc(std::max<uint64_t>(U, 1)))) return fail(rc);
   }
-  k_rec_reduce<<<grid_for(n), 256, 0, s>>>(srt, n, head, idx, n_rules, T->b.rule, T->b.aid, T->b.aid_next,
+  k_rec_reduce<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), (int64_t)ctx->n_cu * 8), 256, 0, s>>>(srt, n, head, idx, n_rules, T->b.rule, T->b.aid, T->b.aid_next,
                                            T->b.count, T->b.count_ge2, stats, err);
   if (hipGetLastError() != hipSuccess) { set_error("merge launch failed"); return fail(OTTOHIP_EHIP); }
   ctx->end(ph, s);

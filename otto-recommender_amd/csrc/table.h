@@ -36,6 +36,7 @@ struct TableBufs {
 
 struct ottohip_ctx : public Ctx {
   TableBufs spare;  // buffers of the last freed table, reused by the next count
+  uint64_t gen = 0;  // count calls so far (emit handles refer to the workspace of one call)
 };
 
 struct ottohip_table {

@@ -17,7 +17,7 @@ import numpy as np
 from . import _lib
 from . import config
 
-REC_WORDS = 4  # record = u32 {rule << 29 | aid, aid_next, count, count_ge2}
+REC_WORDS = 4  # table-row record = u32 {rule << 29 | aid, aid_next, count, count_ge2}
 
 
 def owner_of(aid, n_parts: int) -> np.ndarray:
@@ -54,9 +54,10 @@ def _comm_device(group=None):
     return torch.device("cpu")
 
 
-def exchange_records(send, send_counts, group=None):
-    """All-to-all-v of records: send [n, 4] int32 grouped by destination (send_counts[p] rows
-    for rank p, in rank order). Returns the received [m, 4] records, grouped by source rank."""
+def exchange(send, send_counts, group=None, return_counts=False):
+    """All-to-all-v along dim 0: send holds send_counts[p] leading-dim entries for rank p, in
+    rank order. Returns what every rank sent to this one, concatenated in source-rank order
+    (and, with return_counts, the per-source entry counts)."""
     import torch
     import torch.distributed as dist
     dev = _comm_device(group)
@@ -66,9 +67,15 @@ def exchange_records(send, send_counts, group=None):
     recv_counts = [int(x) for x in rc.tolist()]
     # gloo (CPU tests, single-GPU rehearsals) exchanges host copies; RCCL moves device memory
     src = send if send.device == dev else send.to(dev)
-    recv = torch.empty((sum(recv_counts), REC_WORDS), dtype=torch.int32, device=dev)
+    recv = torch.empty((sum(recv_counts),) + tuple(send.shape[1:]), dtype=send.dtype, device=dev)
     dist.all_to_all_single(recv, src.contiguous(), recv_counts, [int(c) for c in send_counts], group=group)
-    return recv if recv.device == send.device else recv.to(send.device)
+    recv = recv if recv.device == send.device else recv.to(send.device)
+    return (recv, recv_counts) if return_counts else recv
+
+
+def exchange_records(send, send_counts, group=None):
+    """All-to-all-v of table-row records [n, 4] int32 grouped by destination rank."""
+    return exchange(send, send_counts, group)
 
 
 def allreduce_file_stats(per_rule, group=None) -> list:
@@ -110,11 +117,90 @@ def table_from_records(recs, names, n_items: int, file_stats=None, ctx=None, str
     return CovisTable(h, names, ctx)
 
 
-def count_co_events_sharded(events, group=None, names=None, n_items: int = config.N_ITEMS_OTTO, dedup: bool = True,
-                            stream=None, ctx=None):
-    """count_co_events_fused on this rank's files, then the owner exchange and merge.
-    Returns this rank's shard of the global table (rows with owner(aid) == rank), carrying the
-    global per-file row statistics."""
+def emit_for_owners(events, n_parts: int, file_ids=None, n_files_total: int | None = None, names=None,
+                    n_items: int = config.N_ITEMS_OTTO, dedup: bool = True, stream=None, ctx=None):
+    """Pair words of this rank's files, laid out owner-major (ottohip_covis_emit + emit_write).
+    Returns (words int32 [P], words_per_owner, pieces int64 [rows], pieces_per_owner, names)."""
+    import torch
+    from .covis import reference_rules
+    ctx = ctx or _lib.context()
+    names, rules = reference_rules(names)
+    p = _lib.CovisParams()
+    p.min_dt, p.max_dt, p.n_items, p.dedup = config.MIN_TIME_TO_NEXT, config.MAX_TIME_TO_NEXT, int(n_items), int(dedup)
+    ev = events.abi()
+    nf = ev.n_files
+    fids = (ctypes.c_int32 * nf)(*(range(nf) if file_ids is None else [int(f) for f in file_ids]))
+    n_tot = nf if n_files_total is None else int(n_files_total)
+    em = ctypes.c_void_p()
+    wpp = (ctypes.c_int64 * n_parts)()
+    rpp = (ctypes.c_int64 * n_parts)()
+    lib = _lib.load()
+    sh = _lib.stream_handle(stream)
+    _lib.check(lib.ottohip_covis_emit(ctx.h, ctypes.byref(ev), rules, len(names), ctypes.byref(p), fids, n_tot, n_parts,
+                                      ctypes.byref(em), wpp, rpp, sh))
+    try:
+        dev = torch.device("cuda", ctx.device)
+        words = torch.empty(sum(wpp), dtype=torch.int32, device=dev)
+        pieces = torch.empty(sum(rpp), dtype=torch.int64, device=dev)
+        _lib.check(lib.ottohip_emit_write(em, _lib.ptr(words) if words.numel() else None,
+                                          _lib.ptr(pieces) if pieces.numel() else None, sh))
+    finally:
+        lib.ottohip_emit_free(em)
+    return words, list(wpp), pieces, list(rpp), names
+
+
+def reduce_received(words, pieces, names, n_files_total: int, n_items: int = config.N_ITEMS_OTTO, dedup: bool = True,
+                    stream=None, ctx=None):
+    """Assemble the received segments (one word range per row) and reduce them to a table."""
+    from .covis import CovisTable, reference_rules
+    ctx = ctx or _lib.context()
+    names, rules = reference_rules(names)
+    p = _lib.CovisParams()
+    p.min_dt, p.max_dt, p.n_items, p.dedup = config.MIN_TIME_TO_NEXT, config.MAX_TIME_TO_NEXT, int(n_items), int(dedup)
+    h = ctypes.c_void_p()
+    nw, npc = int(words.numel()), int(pieces.numel())
+    _lib.check(_lib.load().ottohip_covis_reduce_received(ctx.h, rules, len(names), ctypes.byref(p), int(n_files_total),
+                                                         _lib.ptr(words) if nw else None, nw,
+                                                         _lib.ptr(pieces) if npc else None, npc, ctypes.byref(h),
+                                                         _lib.stream_handle(stream)))
+    return CovisTable(h, names, ctx)
+
+
+def set_file_stats(table, file_stats):
+    """Install global per-file row statistics [(file_rows, file_rows_ge2)] per rule on a shard."""
+    for r, (fr, fr2) in enumerate(file_stats):
+        _lib.check(_lib.load().ottohip_table_set_file_stats(table.h, r, int(fr), int(fr2)))
+
+
+def count_co_events_sharded(events, file_ids, n_files_total: int, group=None, names=None,
+                            n_items: int = config.N_ITEMS_OTTO, dedup: bool = True, stream=None, ctx=None):
+    """The N-GPU build: this rank's whole files (global ids file_ids) -> pair words laid out by
+    owner -> all-to-all-v of words and row pieces (RCCL) -> assemble + reduce of the owner's
+    rows. Returns this rank's shard (rows with owner(aid) == rank) of the single-GPU table;
+    its file_rows / file_rows_ge2 are the GLOBAL per-file row counts (all-reduced), which is
+    what concat_files_w_stats compares against its thresholds (:131, :135)."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    words, wpp, pieces, ppp, names = emit_for_owners(events, world, file_ids, n_files_total, names, n_items, dedup,
+                                                      stream, ctx)
+    rw = exchange(words, wpp, group)
+    del words
+    rp = exchange(pieces, ppp, group)
+    del pieces
+    tab = reduce_received(rw, rp, names, n_files_total, n_items, dedup, stream, ctx)
+    del rw, rp
+    fs = allreduce_file_stats([(tab.stats(r)["file_rows"], tab.stats(r)["file_rows_ge2"]) for r in range(len(names))],
+                              group)
+    set_file_stats(tab, fs)
+    tab.rank, tab.world = rank, world
+    return tab
+
+
+def merge_tables_by_owner(events, group=None, names=None, n_items: int = config.N_ITEMS_OTTO, dedup: bool = True,
+                          stream=None, ctx=None):
+    """Row-level alternative (also the A7 train+test table merge): count this rank's files to
+    a table, then exchange table rows by owner and merge-sum them."""
     import torch.distributed as dist
     from .covis import count_co_events_fused
     world = dist.get_world_size(group)

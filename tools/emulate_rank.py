@@ -44,32 +44,54 @@ def main():
     ev = synth.Events(off, cat("session"), cat("aid"), cat("ts"), cat("type"))
     dev = gc.DeviceEvents.from_host(ev, fb)
     ctx = _lib.context()
-    res = []
+    G = args.world
+    # (1) this rank's emit: S1-S4 of its own files, words laid out by owner
     for rep in range(args.reps):
         ctx.set_timing(True)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        local = gc.count_co_events_fused(dev, ctx=ctx)
-        ph = ctx.timings()
-        recs, counts = gd.pack_by_owner(local, args.world)
-        ph += ctx.timings()
-        names = local.names
-        st = [local.stats(n) for n in names]
-        local.free()
+        w, wpp, pc, ppp, names = gd.emit_for_owners(dev, G, mine, n_files, ctx=ctx)
         torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        shard = gd.table_from_records(recs, names, 1855603, [(s["file_rows"], s["file_rows_ge2"]) for s in st], ctx=ctx)
-        ph += ctx.timings()
-        torch.cuda.synchronize()
-        t2 = time.perf_counter()
+        t_emit = time.perf_counter() - t0
+        ph_emit = ctx.timings()
         ctx.set_timing(False)
-        res = {"world": args.world, "rank": args.rank, "files": len(mine), "events": int(ev.n_events),
-               "local_pairs": int(sum(s["n_pairs"] for s in st)), "local_rows": int(sum(s["n_rows"] for s in st)),
-               "records": int(recs.shape[0]), "per_owner": counts,
-               "count_pack_s": t1 - t0, "merge_s": t2 - t1,
-               "phases_ms": {n: round(ms, 3) for n, ms, _ in ph}}
+        del w, pc
+    del dev
+    # (2) what owner `rank` receives: its segment of every file's words (emit of ALL files, untimed)
+    full = [synth.generate(int(fb_all[f + 1] - fb_all[f]), int(fb_all[f]), 0) for f in range(n_files)]
+    off = np.zeros(n_sess + 1, np.int64)
+    base = 0
+    for f, p in enumerate(full):
+        off[fb_all[f]:fb_all[f + 1] + 1] = p.session_offsets + base
+        base += p.n_events
+    catf = lambda k: np.concatenate([getattr(p, k) for p in full])
+    evf = synth.Events(off, catf("session"), catf("aid"), catf("ts"), catf("type"))
+    del full
+    devf = gc.DeviceEvents.from_host(evf, fb_all)
+    del evf
+    w, wpp, pc, ppp, names = gd.emit_for_owners(devf, G, None, n_files, ctx=ctx)
+    del devf
+    o = args.rank
+    ws = w[sum(wpp[:o]):sum(wpp[:o + 1])].clone()
+    ps = pc[sum(ppp[:o]):sum(ppp[:o + 1])].clone()
+    del w, pc
+    torch.cuda.empty_cache()
+    for rep in range(args.reps):
+        ctx.set_timing(True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        shard = gd.reduce_received(ws, ps, names, n_files, ctx=ctx)
+        torch.cuda.synchronize()
+        t_red = time.perf_counter() - t0
+        ph_red = ctx.timings()
+        ctx.set_timing(False)
+        rows = sum(shard.stats(n)["n_rows"] for n in names)
         shard.free()
-        del recs
+    res = {"world": G, "rank": args.rank, "files": len(mine), "events": int(ev.n_events),
+           "send_words": int(sum(wpp)), "recv_words": int(ws.numel()), "recv_pieces": int(ps.numel()),
+           "shard_rows": int(rows), "emit_s": t_emit, "reduce_received_s": t_red,
+           "send_bytes_remote": 4 * int(sum(wpp) - wpp[args.rank]) + 8 * int(sum(ppp) - ppp[args.rank]),
+           "phases_ms": {n: round(ms, 3) for n, ms, _ in ph_emit + ph_red}}
     print(json.dumps(res))
 
 
