@@ -257,9 +257,9 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     OH_TRY(T->b.alloc(P));
   }
   unsigned long long *stats, *lcount;
-  OH_TRY(ws.get("stats", MAX_RULES * 4, &stats));
+  OH_TRY(ws.get("stats", (size_t)STAT_STRIPES * STAT_STRIDE, &stats));
   OH_TRY(ws.get("lcount", 8, &lcount));
-  hipMemsetAsync(stats, 0, MAX_RULES * 4 * 8, s);
+  hipMemsetAsync(stats, 0, (size_t)STAT_STRIPES * STAT_STRIDE * 8, s);
   hipMemsetAsync(err, 0, sizeof(int), s);
   hipMemsetAsync(T->b.rule, 0xFF, P, s);  // rows are written at their task's word offsets: holes stay 0xFF
   OutRows O;
@@ -348,8 +348,11 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   }
   ctx->end(ph, s);
   if (!drained) { set_error("reduce: split levels did not converge"); return OTTOHIP_ELIMIT; }
-  unsigned long long st[MAX_RULES * 4];
-  if ((rc = d2h(st, stats, MAX_RULES * 4, s))) return rc;
+  std::vector<unsigned long long> stv((size_t)STAT_STRIPES * STAT_STRIDE);
+  if ((rc = d2h(stv.data(), stats, stv.size(), s))) return rc;
+  unsigned long long st[MAX_RULES * 4] = {};
+  for (int k = 0; k < STAT_STRIPES; ++k)
+    for (int j = 0; j < MAX_RULES * 4; ++j) st[j] += stv[(size_t)k * STAT_STRIDE + j];
   if (hipGetLastError() != hipSuccess) { set_error("reduce failed"); return OTTOHIP_EHIP; }
   unsigned long long sum_pairs = 0, U = 0;
   for (int r = 0; r < n_rules; ++r) { sum_pairs += st[r * 4 + 1]; U += st[r * 4 + 0]; }
@@ -581,8 +584,18 @@ int ottohip_covis_reduce_received(ottohip_ctx* ctx, const ottohip_rule* rules, i
   uint32_t *w0, *w1;
   if ((rc = ws.get("words0", (size_t)P, &w0)) || (rc = ws.get("words1", (size_t)P, &w1))) return fail(rc);
   k_piece_rows<<<grid_for(n), 256, 0, s>>>(ks, head, row_idx, dst, n, row_key, row_begin);
-  k_piece_copy<<<(unsigned)std::min<int64_t>(ceil_div(n, 4), (int64_t)ctx->n_cu * 16), 256, 0, s>>>(
-      vs, len, src_off, dst, n, words, w0);
+  {
+    uint32_t *nch, *cmap;
+    uint64_t* cb;
+    if ((rc = ws.get("pc_nch", (size_t)n, &nch)) || (rc = ws.get("pc_cb", (size_t)n, &cb))) return fail(rc);
+    k_piece_nchunks<<<grid_for(n), 256, 0, s>>>(lsort, n, nch);
+    if ((rc = exclusive_scan_u32(ctx, nch, cb, n, tot + 3, s))) return fail(rc);
+    uint64_t nc = 0;
+    if ((rc = d2h(&nc, tot + 3, 1, s))) return fail(rc);
+    if ((rc = ws.get("pc_cmap", (size_t)std::max<uint64_t>(nc, 1), &cmap))) return fail(rc);
+    k_chunk_map<<<grid_for(n), 256, 0, s>>>(nch, cb, n, cmap);
+    k_piece_copy<<<grid_for((int64_t)nc, 4), 256, 0, s>>>(cmap, cb, (int64_t)nc, vs, len, src_off, dst, words, w0);
+  }
   if (hipGetLastError() != hipSuccess) { set_error("assemble launch failed"); return fail(OTTOHIP_EHIP); }
   ctx->end(ph, s);
   if ((rc = covis_reduce(ctx, w0, w1, P, row_begin, row_key, Rn, R, Lt, n_rules, T, s))) return fail(rc);

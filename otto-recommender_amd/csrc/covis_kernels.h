@@ -28,6 +28,8 @@ constexpr int SMALL = 2048;       // up to SMALL words: one workgroup, LDS hash
 constexpr int SPLIT_TARGET = 256; // split buckets aim at this many words
 constexpr int HASH_REM = 11;      // buckets whose remaining key bits <= 11 hash directly
 constexpr uint32_t W_EMPTY = 0xFFFFFFFFu;
+constexpr int STAT_STRIPES = 256;            // copies of the per-rule statistics
+constexpr int STAT_STRIDE = MAX_RULES * 4;   // u64 per copy (256 B: one L2 line pair per stripe)
 
 struct RulesDev {
   int32_t lo[MAX_RULES], hi[MAX_RULES];    // window on dt = ts_j - ts_i, inclusive
@@ -59,7 +61,7 @@ struct OutRows {
   uint32_t* count;
   uint32_t* count_ge2;
   uint64_t cap;
-  unsigned long long* stats;  // [MAX_RULES][4]: rows, pairs, file_rows, file_rows_ge2
+  unsigned long long* stats;  // [STAT_STRIPES][MAX_RULES][4]: rows, pairs, file_rows, file_rows_ge2
 };
 
 // ------------------------------------------------------------------ block maps
@@ -392,19 +394,40 @@ __global__ void k_piece_rows(const uint32_t* __restrict__ key, const uint32_t* _
   row_begin[row_idx[i]] = dst[i];
 }
 
-// one wave per piece (grid-stride): copy its words to the row's range
-__global__ __launch_bounds__(256) void k_piece_copy(const uint32_t* __restrict__ val, const uint32_t* __restrict__ len,
+// copies are cut into chunks of PC_CH words so hot rows (millions of words) spread over waves
+constexpr uint32_t PC_CH = 2048;
+__global__ void k_piece_nchunks(const uint32_t* __restrict__ lsort, int64_t n, uint32_t* __restrict__ nch) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) nch[i] = (lsort[i] + PC_CH - 1) / PC_CH;
+}
+__global__ void k_chunk_map(const uint32_t* __restrict__ nch, const uint64_t* __restrict__ cb, int64_t n,
+                            uint32_t* __restrict__ cmap) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  for (uint32_t j = 0; j < nch[i]; ++j) cmap[cb[i] + j] = (uint32_t)i;
+}
+// one wave per chunk, 4 independent loads in flight per lane
+__global__ __launch_bounds__(256) void k_piece_copy(const uint32_t* __restrict__ cmap, const uint64_t* __restrict__ cb,
+                                                    int64_t n_chunks, const uint32_t* __restrict__ val,
+                                                    const uint32_t* __restrict__ len,
                                                     const uint64_t* __restrict__ src_off,
-                                                    const uint64_t* __restrict__ dst, int64_t n,
+                                                    const uint64_t* __restrict__ dst,
                                                     const uint32_t* __restrict__ in, uint32_t* __restrict__ out) {
   const int l = threadIdx.x & 63;
-  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n;
-       i += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-    const uint32_t p = val[i];
-    const uint64_t s0 = src_off[p], d0 = dst[i];
-    const uint32_t m = len[p];
-    for (uint32_t k = l; k < m; k += 64) out[d0 + k] = in[s0 + k];
+  const int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (c >= n_chunks) return;
+  const uint32_t i = cmap[c];
+  const uint32_t p = val[i];
+  const uint32_t o = (uint32_t)(c - (int64_t)cb[i]) * PC_CH;
+  const uint32_t m = min(len[p] - o, PC_CH);
+  const uint32_t* src = in + src_off[p] + o;
+  uint32_t* d = out + dst[i] + o;
+  uint32_t k = l;
+  for (; k + 192 < m; k += 256) {
+    const uint32_t a0 = src[k], a1 = src[k + 64], a2 = src[k + 128], a3 = src[k + 192];
+    d[k] = a0; d[k + 64] = a1; d[k + 128] = a2; d[k + 192] = a3;
   }
+  for (; k < m; k += 64) d[k] = src[k];
 }
 
 // ------------------------------------------------------------------ S4 emit
@@ -521,8 +544,11 @@ struct RuleAcc {
     for (int r = 0; r < MAX_RULES; ++r)
       if (r == rule) { rows[r] += 1; pairs[r] += c; nf1[r] += nf & 0xFFFFu; nf2[r] += nf >> 16; }
   }
-  // wave reduction, then one device atomic per nonzero statistic
-  __device__ void flush(unsigned long long* stats, int n_rules) {
+  // wave reduction, then one device atomic per nonzero statistic into this wave's stripe of
+  // the striped statistics array (STAT_STRIPES copies: same-address atomics serialise in L2)
+  __device__ void flush(unsigned long long* stats_striped, int n_rules) {
+    const uint32_t gwave = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    unsigned long long* stats = stats_striped + (size_t)(gwave & (STAT_STRIPES - 1)) * STAT_STRIDE;
     for (int r = 0; r < n_rules; ++r) {
       unsigned long long v[4] = {rows[0], pairs[0], nf1[0], nf2[0]};
 #pragma unroll
