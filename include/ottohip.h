@@ -115,6 +115,19 @@ int ottohip_table_finalize(ottohip_ctx* ctx, const ottohip_table* t, int rule,
                            const ottohip_merge_params* mp, int32_t* aid, int32_t* aid_next,
                            int32_t* count, int64_t* n_out, void* stream);
 
+/* R1: per-aid top-first_n of a final co-visitation table with the reference's features
+ * (get_df_count_for_co_event_type, model/retrieve.py:18-63). Input: the table in FILE order
+ * (device, n rows; row position drives perc_pop). Outputs (device, capacity n): rows with
+ * rank <= first_n in (aid asc, rank asc) order; *n_out = rows written.
+ *   count_pop = Int16(min((c - min) / (q - min), 1) * 1e4), q = 0.9999 quantile ('nearest')
+ *   perc_pop  = Int16(row_nr / n * 1e4), row_nr 1-based file position
+ *   rank      = ordinal rank of count desc within aid (ties: file order)
+ *   count_rel = Int8(c / max count of the aid * 100) */
+int ottohip_topk_per_aid(ottohip_ctx* ctx, const int32_t* aid, const int32_t* aid_next, const int32_t* count,
+                         int64_t n, int32_t n_items, int first_n, int32_t* out_aid, int32_t* out_aid_next,
+                         int32_t* out_count, int16_t* out_count_pop, int16_t* out_perc_pop, int16_t* out_rank,
+                         int8_t* out_count_rel, int64_t* n_out, void* stream);
+
 /* ---- Multi-GPU exchange -------------------------------------------------
  * The reference is single-process; these calls replace the cross-file groupby of
  * concat_files_w_stats (model/count_co_events.py:168) when files are dealt over G ranks.

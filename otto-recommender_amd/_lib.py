@@ -64,6 +64,8 @@ SIGNATURES = {
     "ottohip_table_finalize": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.POINTER(MergeParams), _VP, _VP, _VP,
                                               ctypes.POINTER(_I64), _VP]),
     "ottohip_table_set_file_stats": (ctypes.c_int, [_VP, ctypes.c_int, _I64, _I64]),
+    "ottohip_topk_per_aid": (ctypes.c_int, [_VP, _VP, _VP, _VP, _I64, _I32, ctypes.c_int] + [_VP] * 7 +
+                             [ctypes.POINTER(_I64), _VP]),
     "ottohip_owner_of": (ctypes.c_int, [_I32, ctypes.c_int]),
     "ottohip_table_pack_by_owner": (ctypes.c_int, [_VP, _VP, ctypes.c_int, _VP, ctypes.POINTER(_I64), _VP]),
     "ottohip_table_from_records": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _I32, ctypes.POINTER(RuleStats),
