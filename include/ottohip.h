@@ -128,6 +128,47 @@ int ottohip_topk_per_aid(ottohip_ctx* ctx, const int32_t* aid, const int32_t* ai
                          int32_t* out_count, int16_t* out_count_pop, int16_t* out_perc_pop, int16_t* out_rank,
                          int8_t* out_count_rel, int64_t* n_out, void* stream);
 
+/* ---- Config-5 candidate generation (R3-R6, R8 order) and recall (R9) ----------------------
+ * Candidate columns of retrieve_and_gen_feats (model/retrieve.py:422-657) for every session of
+ * a session-sorted event table (raw rows, no dedup: :477 takes the file as read). Sources per
+ * aid are CSR lists built with ottohip_lists_build:
+ *   q = 0..4 : R1 top-N lists of the 5 co-count tables (CO_EVENTS_TO_COUNT order), rank = R1 rank
+ *   q = 5, 6 : kNN lists of the all-types and carts/orders Word2Vec models, rank = rank_w2vec
+ * pop_off / pop_aid: per dense cluster index, the aids whose min cl50 rank <= 20 (C3);
+ * session_cl: dense cluster index per session (-1 = none). Output per session (CSR): aid_next,
+ * ts_order_aid (999 for popularity-only rows) and flags (bit i = i-th of src_self,
+ * src_click_to_click, src_click_to_cart_or_buy, src_cart_to_cart, src_cart_to_buy,
+ * src_buy_to_buy, src_w2vec_all, src_w2vec_1_2, src_pop_cl50), rows sorted by
+ * (ts_order_aid, aid_next). Ordinal-rank ties: aid ascending (deterministic choice). */
+typedef struct {
+  const uint32_t* off[7];   /* [n_items + 1] or NULL (source absent) */
+  const int32_t* nxt[7];
+  const int16_t* rank[7];
+  int32_t n_items;
+  const uint32_t* pop_off;  /* [n_clusters + 1] or NULL */
+  const int32_t* pop_aid;
+  int32_t n_clusters;
+  int32_t max_list_total;   /* max over aids of the summed list lengths (<= 127) */
+} ottohip_cand_lists;
+typedef struct ottohip_candidates ottohip_candidates;
+/* rows (key, nxt, rank) -> CSR by key, stable: out_off [n_keys + 1], out_nxt / out_rank [n] */
+int ottohip_lists_build(ottohip_ctx* ctx, const int32_t* key, const int32_t* nxt, const int16_t* rank, int64_t n,
+                        int32_t n_keys, uint32_t* out_off, int32_t* out_nxt, int16_t* out_rank, void* stream);
+int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets, int64_t n_sessions,
+                                const int32_t* aid, const int32_t* ts, const int8_t* type,
+                                const ottohip_cand_lists* lists, const int32_t* session_cl,
+                                ottohip_candidates** out, void* stream);
+int ottohip_candidates_info(const ottohip_candidates* c, int64_t* n_sessions, int64_t* n_cand);
+int ottohip_candidates_copy(const ottohip_candidates* c, uint64_t* off, int32_t* aid_next, int16_t* ts_order,
+                            uint16_t* flags, void* stream);
+void ottohip_candidates_free(ottohip_candidates* c);
+/* R9 (model/eval_retrieved.py:45-118) for the candidates whose flags intersect src_mask (0 = all):
+ * labels per type t as CSR lab_off[t * (n_sessions + 1) + s] into lab_aid (unique per session/type).
+ * sums_out[t * 5 + {0..4}] = sum over sessions of min(hit@20, max_k), min(hit@100, max_k),
+ * min(hit@200, max_k), min(hit@all, max_k), min(true, max_k). */
+int ottohip_candidates_recall(ottohip_ctx* ctx, const ottohip_candidates* c, const int64_t* lab_off,
+                              const int32_t* lab_aid, uint32_t src_mask, int max_k, int64_t* sums_out, void* stream);
+
 /* ---- Multi-GPU exchange -------------------------------------------------
  * The reference is single-process; these calls replace the cross-file groupby of
  * concat_files_w_stats (model/count_co_events.py:168) when files are dealt over G ranks.

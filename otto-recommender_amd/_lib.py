@@ -66,6 +66,13 @@ SIGNATURES = {
     "ottohip_table_set_file_stats": (ctypes.c_int, [_VP, ctypes.c_int, _I64, _I64]),
     "ottohip_topk_per_aid": (ctypes.c_int, [_VP, _VP, _VP, _VP, _I64, _I32, ctypes.c_int] + [_VP] * 7 +
                              [ctypes.POINTER(_I64), _VP]),
+    "ottohip_lists_build": (ctypes.c_int, [_VP, _VP, _VP, _VP, _I64, _I32, _VP, _VP, _VP, _VP]),
+    "ottohip_candidates_generate": (ctypes.c_int, [_VP, _VP, _I64, _VP, _VP, _VP, _VP, _VP, ctypes.POINTER(_VP), _VP]),
+    "ottohip_candidates_info": (ctypes.c_int, [_VP, ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
+    "ottohip_candidates_copy": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
+    "ottohip_candidates_free": (None, [_VP]),
+    "ottohip_candidates_recall": (ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_uint32, ctypes.c_int,
+                                                 ctypes.POINTER(_I64), _VP]),
     "ottohip_owner_of": (ctypes.c_int, [_I32, ctypes.c_int]),
     "ottohip_table_pack_by_owner": (ctypes.c_int, [_VP, _VP, ctypes.c_int, _VP, ctypes.POINTER(_I64), _VP]),
     "ottohip_table_from_records": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _I32, ctypes.POINTER(RuleStats),

@@ -1,0 +1,238 @@
+"""Config-5 candidate generation and recall on MI355X.
+
+Mirrors the candidate part of model/retrieve.py (retrieve_and_gen_feats :422-657 without the
+ranker features: get_session_aid_pairs_unique :138-232, get_all_aid_pairs :244-290, the trim
+rule :490-516, the source flags :549-559, the cl50 popularity candidates :571-585 and the final
+(session, ts_order_aid) order :647) and the recall of model/eval_retrieved.py:45-118.
+Everything runs in libottohip.so (csrc/candidates.hip); pandas/pyarrow only at the boundary.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from . import config
+
+SRC_NAMES = ["src_self", "src_click_to_click", "src_click_to_cart_or_buy", "src_cart_to_cart", "src_cart_to_buy",
+             "src_buy_to_buy", "src_w2vec_all", "src_w2vec_1_2", "src_pop_cl50"]
+SRC_BIT = {n: 1 << i for i, n in enumerate(SRC_NAMES)}
+
+
+class CandLists(ctypes.Structure):
+    _fields_ = [("off", ctypes.c_void_p * 7), ("nxt", ctypes.c_void_p * 7), ("rank", ctypes.c_void_p * 7),
+                ("n_items", ctypes.c_int32), ("pop_off", ctypes.c_void_p), ("pop_aid", ctypes.c_void_p),
+                ("n_clusters", ctypes.c_int32), ("max_list_total", ctypes.c_int32)]
+
+
+def _dev(ctx):
+    import torch
+    return torch.device("cuda", ctx.device)
+
+
+def build_lists(key, nxt, rank, n_keys: int, ctx=None, stream=None):
+    """Rows (key, nxt[, rank]) -> CSR by key (stable): torch (off u32 as int32 [n_keys+1], nxt, rank)."""
+    import torch
+    ctx = ctx or _lib.context()
+    dev = _dev(ctx)
+    k = torch.as_tensor(key).to(dev, torch.int32).contiguous()
+    x = torch.as_tensor(nxt).to(dev, torch.int32).contiguous()
+    r = None if rank is None else torch.as_tensor(rank).to(dev, torch.int16).contiguous()
+    n = int(k.numel())
+    off = torch.empty(n_keys + 1, dtype=torch.int32, device=dev)
+    on = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    orr = torch.empty(max(n, 1), dtype=torch.int16, device=dev) if r is not None else None
+    _lib.check(_lib.load().ottohip_lists_build(ctx.h, _lib.ptr(k) if n else None, _lib.ptr(x) if n else None,
+                                               _lib.ptr(r) if (r is not None and n) else None, n, int(n_keys),
+                                               _lib.ptr(off), _lib.ptr(on) if n else None,
+                                               _lib.ptr(orr) if (orr is not None and n) else None,
+                                               _lib.stream_handle(stream)))
+    return off, on[:n], (orr[:n] if orr is not None else None)
+
+
+class CandidateSources:
+    """Device CSR lists per aid for the 7 pair sources + the cl50 popularity lists.
+    r1: {rule name: (aid, aid_next, rank)} (R1 outputs); knn_all / knn_12: (aid, aid_next, rank);
+    pop: (cluster index, aid) rows of the clusters' top aids (min cl50 rank <= 20)."""
+
+    def __init__(self, r1: dict, knn_all, knn_12, pop=None, n_clusters: int = 0, n_items: int = config.N_ITEMS_OTTO,
+                 ctx=None):
+        import torch
+        self.ctx = ctx or _lib.context()
+        self.n_items = int(n_items)
+        self.keep = []
+        srcs = [r1.get(n) for n in config.CO_EVENTS_TO_COUNT] + [knn_all, knn_12]
+        self.abi = CandLists()
+        total = 0
+        for q, src in enumerate(srcs):
+            if src is None:
+                self.abi.off[q] = self.abi.nxt[q] = self.abi.rank[q] = None
+                continue
+            a, b, r = src
+            off, nx, rk = build_lists(a, b, r, self.n_items, self.ctx)
+            self.keep += [off, nx, rk]
+            self.abi.off[q], self.abi.nxt[q], self.abi.rank[q] = _lib.ptr(off), _lib.ptr(nx), _lib.ptr(rk)
+            if nx.numel():
+                total += int((off[1:] - off[:-1]).max().item())
+        self.abi.n_items = self.n_items
+        self.abi.max_list_total = total
+        self.n_clusters = int(n_clusters)
+        if pop is not None and self.n_clusters > 0:
+            c, a = pop
+            off, nx, _ = build_lists(c, a, None, self.n_clusters, self.ctx)
+            self.keep += [off, nx]
+            self.abi.pop_off, self.abi.pop_aid, self.abi.n_clusters = _lib.ptr(off), _lib.ptr(nx), self.n_clusters
+        else:
+            self.abi.pop_off = self.abi.pop_aid = None
+            self.abi.n_clusters = 0
+
+
+class Candidates:
+    """Device CSR of candidates per session: off [S+1], aid_next, ts_order_aid, flags."""
+
+    def __init__(self, h, ctx):
+        self.h, self.ctx = h, ctx
+        ns, nc = ctypes.c_int64(), ctypes.c_int64()
+        _lib.check(_lib.load().ottohip_candidates_info(h, ctypes.byref(ns), ctypes.byref(nc)))
+        self.n_sessions, self.n_cand = int(ns.value), int(nc.value)
+
+    def free(self):
+        if self.h:
+            _lib.load().ottohip_candidates_free(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def to_torch(self, stream=None) -> dict:
+        import torch
+        dev = _dev(self.ctx)
+        off = torch.empty(self.n_sessions + 1, dtype=torch.int64, device=dev)
+        nc = max(self.n_cand, 1)
+        nxt = torch.empty(nc, dtype=torch.int32, device=dev)
+        ordr = torch.empty(nc, dtype=torch.int16, device=dev)
+        flags = torch.empty(nc, dtype=torch.int16, device=dev)
+        _lib.check(_lib.load().ottohip_candidates_copy(self.h, _lib.ptr(off), _lib.ptr(nxt), _lib.ptr(ordr),
+                                                       _lib.ptr(flags), _lib.stream_handle(stream)))
+        k = self.n_cand
+        return {"off": off, "aid_next": nxt[:k], "ts_order_aid": ordr[:k], "flags": flags[:k]}
+
+    def to_pandas(self, session_ids=None):
+        """DataFrame[session, aid_next:int32, ts_order_aid:int16, src_*:int8] in output order."""
+        import pandas as pd
+        t = {k: v.cpu().numpy() for k, v in self.to_torch().items()}
+        sess = np.arange(self.n_sessions) if session_ids is None else np.asarray(session_ids)
+        out = {"session": np.repeat(sess, np.diff(t["off"])), "aid_next": t["aid_next"],
+               "ts_order_aid": t["ts_order_aid"]}
+        f = t["flags"].view(np.uint16)
+        for i, n in enumerate(SRC_NAMES):
+            out[n] = ((f >> i) & 1).astype(np.int8)
+        return pd.DataFrame(out)
+
+    def recall(self, labels_off, labels_aid, src: str | None = None, max_k: int = 20, stream=None) -> dict:
+        """R9 on the device: labels as CSR [3 * (S+1)] offsets (int64) + aids (int32)."""
+        import torch
+        dev = _dev(self.ctx)
+        lo = torch.as_tensor(labels_off).to(dev, torch.int64).contiguous()
+        la = torch.as_tensor(labels_aid).to(dev, torch.int32).contiguous()
+        sums = (ctypes.c_int64 * 15)()
+        mask = 0 if src in (None, "src_any") else SRC_BIT[src]
+        _lib.check(_lib.load().ottohip_candidates_recall(self.ctx.h, self.h, _lib.ptr(lo),
+                                                         _lib.ptr(la) if la.numel() else None, mask, int(max_k), sums,
+                                                         _lib.stream_handle(stream)))
+        return recall_from_sums(list(sums))
+
+
+def recall_from_sums(s) -> dict:
+    """model/eval_retrieved.py:81-110: per type sums -> recall@k, total weighted 0.1/0.3/0.6."""
+    res = {}
+    for t, nm in enumerate(["clicks", "carts", "orders"]):
+        h20, h100, h200, hall, tru = s[t * 5:(t + 1) * 5]
+        res[nm] = {k: (v / tru if tru else 0.0) for k, v in
+                   (("top20", h20), ("top100", h100), ("top200", h200), ("topall", hall))}
+    res["total"] = {k: 0.1 * res["clicks"][k] + 0.3 * res["carts"][k] + 0.6 * res["orders"][k] for k in res["clicks"]}
+    return res
+
+
+def generate(offsets, aid, ts, type_, sources: CandidateSources, session_cl=None, stream=None) -> Candidates:
+    """Candidates for every session of a session-sorted event table (device or host columns)."""
+    import torch
+    ctx = sources.ctx
+    dev = _dev(ctx)
+    t = lambda x, d: torch.as_tensor(np.asarray(x) if not isinstance(x, torch.Tensor) else x).to(dev, d).contiguous()
+    off = t(offsets, torch.int64)
+    off = off - off[0]
+    a, s_, y = t(aid, torch.int32), t(ts, torch.int32), t(type_, torch.int8)
+    S = int(off.numel()) - 1
+    cl = None if session_cl is None else t(session_cl, torch.int32)
+    h = ctypes.c_void_p()
+    _lib.check(_lib.load().ottohip_candidates_generate(ctx.h, _lib.ptr(off), S, _lib.ptr(a), _lib.ptr(s_), _lib.ptr(y),
+                                                       ctypes.addressof(sources.abi), _lib.ptr(cl) if cl is not None else None,
+                                                       ctypes.byref(h), _lib.stream_handle(stream)))
+    return Candidates(h, ctx)
+
+
+def labels_csr(labels, session_ids):
+    """labels DataFrame[session, aid, type] -> (off [3*(S+1)] int64, aid int32), unique per (session, type),
+    sessions in the order of session_ids."""
+    S = len(session_ids)
+    pos = {int(s): i for i, s in enumerate(session_ids)}
+    lab = labels.drop_duplicates(["session", "aid", "type"])
+    idx = lab["session"].map(pos)
+    lab = lab[idx.notna()].assign(si=idx[idx.notna()].astype(np.int64))
+    offs, aids = [], []
+    base = 0
+    for t in range(3):
+        d = lab[lab["type"] == t].sort_values(["si", "aid"], kind="stable")
+        cnt = np.bincount(d["si"].to_numpy(), minlength=S)
+        o = np.zeros(S + 1, np.int64)
+        np.cumsum(cnt, out=o[1:])
+        offs.append(o + base)
+        aids.append(d["aid"].to_numpy().astype(np.int32))
+        base += len(d)
+    return np.concatenate(offs), np.concatenate(aids) if aids else np.zeros(0, np.int32)
+
+
+def retrieve_candidates(df_sessions_aids_full, aid_pairs_co_events: dict, df_knns_w2vec_all, df_knns_w2vec_1_2,
+                        df_session_cl=None, df_pop_cl50=None, n_items: int | None = None):
+    """Candidate-only variant of retrieve_and_gen_feats (model/retrieve.py:422-657), pandas in/out.
+    df_sessions_aids_full [session, aid, ts, type]; aid_pairs_co_events {name: R1 frame}; kNN frames
+    [aid, aid_next, dist_w2vec*, rank_w2vec*]; df_session_cl [session, cl50]; df_pop_cl50 [aid, cl50, rank_*_cl50].
+    Returns DataFrame[session, aid_next, ts_order_aid, src_*] sorted by (session, ts_order_aid, aid_next)."""
+    from .synth import events_from_columns
+    d = df_sessions_aids_full
+    ev = events_from_columns(d["session"].to_numpy(), d["aid"].to_numpy(), d["ts"].to_numpy(), d["type"].to_numpy())
+    sess_ids = ev.session[ev.session_offsets[:-1]] if ev.n_sessions else np.zeros(0, np.int32)
+    mx = [int(ev.aid.max()) + 1 if len(ev.aid) else 1]
+    r1 = {}
+    for n, df in aid_pairs_co_events.items():
+        r1[n] = (df["aid"].to_numpy(), df["aid_next"].to_numpy(), df[f"{n}_rank"].to_numpy())
+        mx.append(int(df["aid"].max()) + 1 if len(df) else 1)
+
+    def knn(df):
+        rc = [c for c in df.columns if c.startswith("rank_w2vec")][0]
+        mx.append(int(df["aid"].max()) + 1 if len(df) else 1)
+        return df["aid"].to_numpy(), df["aid_next"].to_numpy(), df[rc].to_numpy()
+
+    ka, k12 = knn(df_knns_w2vec_all), knn(df_knns_w2vec_1_2)
+    n_items = max(mx + [n_items or 0, config.N_ITEMS_OTTO])
+    pop, ncl, scl = None, 0, None
+    if df_session_cl is not None and df_pop_cl50 is not None:
+        rank_cols = [c for c in df_pop_cl50.columns if c.startswith("rank_") and c.endswith("_cl50")]
+        p = df_pop_cl50[df_pop_cl50[rank_cols].min(axis=1) <= 20] if rank_cols else df_pop_cl50
+        clusters = np.unique(np.concatenate([p["cl50"].to_numpy(), df_session_cl["cl50"].dropna().to_numpy()]))
+        cmap = {int(c): i for i, c in enumerate(clusters)}
+        pop = (p["cl50"].map(cmap).to_numpy(), p["aid"].to_numpy())
+        ncl = len(clusters)
+        m = dict(zip(df_session_cl["session"].to_numpy().tolist(), df_session_cl["cl50"].to_numpy().tolist()))
+        scl = np.array([cmap.get(int(m[s]), -1) if s in m and m[s] == m[s] else -1 for s in sess_ids.tolist()],
+                       np.int32)
+    src = CandidateSources(r1, ka, k12, pop, ncl, n_items)
+    c = generate(ev.session_offsets, ev.aid, ev.ts, ev.type, src, scl)
+    out = c.to_pandas(sess_ids)
+    c.free()
+    return out

@@ -1,0 +1,593 @@
+// Config-5 candidate generation (model/retrieve.py:138-232, 244-290, 477-595; candidate
+// columns only) and the retrieval recall of model/eval_retrieved.py:45-118.
+//
+//   k_cand_aids   (R3)  one wave per session: distinct aids, per-type counts / last ts, the six
+//                       ordinal ranks, the keep filter (:199-206), best order and the trim
+//                       threshold of R5 (:490-503) -> kept (aid, ts_order_aid, type mask, th)
+//   k_cand_build  (R4-R6, R8) one wave per session: for every kept aid its self pair and its
+//                       list entries (5 co-count top-N lists, 2 kNN lists) are merged per aid_next
+//                       in a small LDS hash (pair level: min rank <= th or aid_next == aid), kept
+//                       pairs are folded per (session, aid_next) in the session's LDS hash (OR of
+//                       sources and type masks, min ts_order_aid), the session's cl50 popularity
+//                       list is added (:571-585), and the result is sorted by (ts_order_aid,
+//                       aid_next) (:647, with aid_next as the deterministic tie-break)
+//   k_cand_recall (R9)  one wave per session and type: filtered rank of each label, hit@k
+//
+// Ordinal-rank ties are broken by aid ascending (polars leaves them to groupby row order).
+#include <algorithm>
+#include "prims.h"
+#include "table.h"
+
+namespace ottohip {
+
+constexpr int CS_MAXE = 512;      // events per session handled by k_cand_aids
+constexpr int CS_SRC = 7;         // 5 co-count lists + 2 kNN lists
+constexpr int CS_MINI = 256;      // per-aid merge slots (>= 2 x the longest per-aid list total)
+constexpr int CS_NLAST = 99;      // RETRIEVE_N_LAST_* / RETRIEVE_N_MOST_FREQUENT (config.py:76-79)
+constexpr uint32_t CS_EMPTY = 0xFFFFFFFFu;
+constexpr int CS_NONE = 0x7FFFFFFF;
+
+struct CandLists {
+  const uint32_t* off[CS_SRC];   // per source: [n_items + 1] offsets into nxt / rank (by aid)
+  const int32_t* nxt[CS_SRC];
+  const int16_t* rank[CS_SRC];
+  int32_t n_items;
+  const uint32_t* pop_off;       // [n_clusters + 1]
+  const int32_t* pop_aid;
+  int32_t n_clusters;
+};
+
+// kept aid record: aid, info = ts_order_aid (16 b) | type mask << 16 (3 b) | th << 19 (5 b)
+struct KeptAid { int32_t aid; uint32_t info; };
+
+__device__ __forceinline__ bool rank_before(int ka, int32_t aa, int kb, int32_t ab) {  // desc key, asc aid
+  return ka > kb || (ka == kb && aa < ab);
+}
+
+__global__ __launch_bounds__(64) void k_cand_aids(const int64_t* __restrict__ off, int64_t S,
+                                                  const int32_t* __restrict__ aid, const int32_t* __restrict__ ts,
+                                                  const int8_t* __restrict__ type, KeptAid* __restrict__ kept,
+                                                  uint32_t* __restrict__ n_kept, int* __restrict__ err) {
+  __shared__ int32_t ea[CS_MAXE], et[CS_MAXE];
+  __shared__ int8_t ey[CS_MAXE];
+  __shared__ int32_t ua[CS_MAXE], un[4][CS_MAXE], ut[4][CS_MAXE];  // n / max ts: [all, clicks, carts, orders]
+  __shared__ uint32_t m_sh;
+  const int l = threadIdx.x;
+  const int64_t s = blockIdx.x;
+  if (s >= S) return;
+  const int64_t e0 = off[s];
+  const int n = (int)(off[s + 1] - e0);
+  if (n > CS_MAXE) {
+    if (l == 0) { atomicOr(err, 1); n_kept[s] = 0; }
+    return;
+  }
+  for (int i = l; i < n; i += 64) { ea[i] = aid[e0 + i]; et[i] = ts[e0 + i]; ey[i] = type[e0 + i]; }
+  if (l == 0) m_sh = 0;
+  __syncthreads();
+  // distinct aids (first occurrence), compacted in event order
+  int base = 0;
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + l;
+    bool first = i < n;
+    if (first) {
+      const int32_t a = ea[i];
+      for (int j = 0; j < i; ++j)
+        if (ea[j] == a) { first = false; break; }
+    }
+    const uint64_t b = __ballot(first);
+    if (first) ua[base + (int)mbcnt(b)] = ea[i];
+    base += (int)__popcll(b);
+  }
+  const int m = base;
+  __syncthreads();
+  for (int u = l; u < m; u += 64) {
+    const int32_t a = ua[u];
+    int cnt[4] = {0, 0, 0, 0}, mt[4] = {INT32_MIN, INT32_MIN, INT32_MIN, INT32_MIN};
+    for (int i = 0; i < n; ++i) {
+      if (ea[i] != a) continue;
+      const int y = ey[i] + 1;
+      const int32_t t = et[i];
+      cnt[0]++; mt[0] = max(mt[0], t);
+#pragma unroll
+      for (int q = 1; q < 4; ++q)
+        if (q == y) { cnt[q]++; mt[q] = max(mt[q], t); }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { un[q][u] = cnt[q]; ut[q][u] = mt[q]; }
+  }
+  __syncthreads();
+  for (int u = l; u < m; u += 64) {
+    const int32_t a = ua[u];
+    int r_ts = 1, r_n = 1, r_nc = 1, r_no = 1, r_t[3] = {1, 1, 1};
+    const bool has[3] = {un[1][u] > 0, un[2][u] > 0, un[3][u] > 0};
+    for (int v = 0; v < m; ++v) {
+      const int32_t b = ua[v];
+      r_ts += rank_before(ut[0][v], b, ut[0][u], a);
+      r_n += rank_before(un[0][v], b, un[0][u], a);
+      r_nc += rank_before(un[2][v], b, un[2][u], a);
+      r_no += rank_before(un[3][v], b, un[3][u], a);
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        if (un[q + 1][v] > 0) r_t[q] += rank_before(ut[q + 1][v], b, ut[q + 1][u], a);
+    }
+    // :199-206 keep filter (null ranks never pass)
+    const bool keep = (has[0] && r_t[0] <= CS_NLAST) || (has[1] && r_t[1] <= CS_NLAST) ||
+                      (has[2] && r_t[2] <= CS_NLAST) || r_n <= CS_NLAST || r_nc <= CS_NLAST || r_no <= CS_NLAST;
+    // :496-503 best order (min ignores nulls) and th = max(3, 20 - 17/19 (best - 1)) (f64 as polars)
+    int best = min(r_n, r_ts);
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (has[q]) best = min(best, r_t[q]);
+    double th = 20.0 - (17.0 / 19.0) * (double)(best - 1);
+    if (th < 3.0) th = 3.0;
+    const uint32_t thi = (uint32_t)floor(th);  // integer rank <= th  <=>  rank <= floor(th)
+    const uint32_t tm = (has[0] ? 1u : 0u) | (has[1] ? 2u : 0u) | (has[2] ? 4u : 0u);
+    if (keep) {
+      const uint32_t k = atomicAdd(&m_sh, 1u);
+      KeptAid r;
+      r.aid = a;
+      r.info = (uint32_t)min(r_ts, 0xFFFF) | (tm << 16) | (thi << 19);
+      kept[e0 + k] = r;
+    }
+  }
+  __syncthreads();
+  if (l == 0) n_kept[s] = m_sh;
+}
+
+__device__ __forceinline__ uint32_t cs_hash(uint32_t x, uint32_t mask) { return (x * 0x9E3779B1u >> 9) & mask; }
+
+// one wave per session (WAVES sessions per block); pass 0 counts, pass 1 writes at cand_off
+template <int HC, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __restrict__ off,
+                                                          const int64_t* __restrict__ sess, int64_t n_sess,
+                                                          const KeptAid* __restrict__ kept,
+                                                          const uint32_t* __restrict__ n_kept,
+                                                          const int32_t* __restrict__ session_cl, CandLists L,
+                                                          int pass, uint32_t* __restrict__ n_cand,
+                                                          const uint64_t* __restrict__ cand_off,
+                                                          int32_t* __restrict__ o_next, int16_t* __restrict__ o_ord,
+                                                          uint16_t* __restrict__ o_flags,
+                                                          int32_t* __restrict__ overflow,
+                                                          uint32_t* __restrict__ n_overflow) {
+  __shared__ uint32_t hk[WAVES][HC], hm[WAVES][HC], ho[WAVES][HC];
+  __shared__ uint64_t sk[WAVES][HC];
+  __shared__ uint32_t mk[WAVES][CS_MINI], mb[WAVES][CS_MINI], mr[WAVES][CS_MINI];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int64_t gi = (int64_t)blockIdx.x * WAVES + w;
+  if (gi >= n_sess) return;
+  const int64_t s = sess ? sess[gi] : gi;
+  uint32_t* K = hk[w];
+  uint32_t* Mk = hm[w];
+  uint32_t* Ord = ho[w];
+  for (int i = l; i < HC; i += 64) { K[i] = CS_EMPTY; Mk[i] = 0; Ord[i] = 0xFFFFFFFFu; }
+  for (int i = l; i < CS_MINI; i += 64) { mk[w][i] = CS_EMPTY; mb[w][i] = 0; mr[w][i] = 0x7FFFFFFF; }
+  __builtin_amdgcn_wave_barrier();
+  bool full = false;
+  auto insert = [&](uint32_t x, uint32_t bits, uint32_t ord) {
+    uint32_t h = cs_hash(x, HC - 1);
+    for (int p = 0; p < HC; ++p) {
+      uint32_t k = __hip_atomic_load(&K[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (k == CS_EMPTY) {
+        const uint32_t prev = atomicCAS(&K[h], CS_EMPTY, x);
+        if (prev == CS_EMPTY || prev == x) k = x;
+        else k = prev;
+      }
+      if (k == x) { atomicOr(&Mk[h], bits); atomicMin(&Ord[h], ord); return; }
+      h = (h + 1) & (HC - 1);
+    }
+    full = true;
+  };
+  const int64_t e0 = off[s];
+  const uint32_t nk = n_kept[s];
+  for (uint32_t k = 0; k < nk; ++k) {
+    const KeptAid r = kept[e0 + k];
+    const uint32_t a = (uint32_t)r.aid;
+    const uint32_t ord = r.info & 0xFFFFu, tm = (r.info >> 16) & 7u, th = r.info >> 19;
+    uint32_t beg[CS_SRC], len[CS_SRC], tot = 1;  // element 0 = the self pair
+#pragma unroll
+    for (int q = 0; q < CS_SRC; ++q) {
+      if (L.off[q] && r.aid < L.n_items) { beg[q] = L.off[q][a]; len[q] = L.off[q][a + 1] - beg[q]; }
+      else { beg[q] = 0; len[q] = 0; }
+      tot += len[q];
+    }
+    uint32_t* MK = mk[w];
+    uint32_t* MB = mb[w];
+    uint32_t* MR = mr[w];
+    for (uint32_t e = l; e < tot; e += 64) {
+      uint32_t x = a, bit = 1u, rk = 0;
+      if (e > 0) {
+        uint32_t j = e - 1;
+        int q = 0;
+#pragma unroll
+        for (int z = 0; z < CS_SRC; ++z)
+          if (q == z && j >= len[z]) { j -= len[z]; q = z + 1; }
+        const int32_t* np = L.nxt[0];
+        const int16_t* rp = L.rank[0];
+        uint32_t b0 = beg[0];
+#pragma unroll
+        for (int z = 1; z < CS_SRC; ++z)
+          if (q == z) { np = L.nxt[z]; rp = L.rank[z]; b0 = beg[z]; }
+        x = (uint32_t)np[b0 + j];
+        rk = (uint32_t)rp[b0 + j];
+        bit = 2u << q;
+      }
+      uint32_t h = cs_hash(x, CS_MINI - 1);
+      for (int p = 0; p < CS_MINI; ++p) {
+        uint32_t kk = __hip_atomic_load(&MK[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (kk == CS_EMPTY) {
+          const uint32_t prev = atomicCAS(&MK[h], CS_EMPTY, x);
+          kk = (prev == CS_EMPTY) ? x : prev;
+        }
+        if (kk == x) { atomicOr(&MB[h], bit); atomicMin(&MR[h], rk); break; }
+        h = (h + 1) & (CS_MINI - 1);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (int i = l; i < CS_MINI; i += 64) {
+      const uint32_t x = MK[i];
+      if (x != CS_EMPTY) {
+        // R5 (:512-516) pair kept iff aid_next == aid or best co-count / w2v rank <= th
+        if (x == a || MR[i] <= th) insert(x, MB[i] | (tm << 8), ord);
+        MK[i] = CS_EMPTY; MB[i] = 0; MR[i] = 0x7FFFFFFF;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+  // R6 (:571-585) the cl50 popularity list of the session's cluster; new rows get ts_order 999
+  const int32_t c = session_cl ? session_cl[s] : -1;
+  if (c >= 0 && c < L.n_clusters) {
+    const uint32_t pb = L.pop_off[c], pe = L.pop_off[c + 1];
+    for (uint32_t j = pb + l; j < pe; j += 64) insert((uint32_t)L.pop_aid[j], 1u << 11, 999u);
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  if (__ballot(full)) {  // the session does not fit this tier: retried with a larger table
+    if (pass == 0 && l == 0) {
+      overflow[atomicAdd(n_overflow, 1u)] = (int32_t)s;
+      n_cand[s] = 0;
+    }
+    return;
+  }
+  // compact (ts_order, aid_next, flags) sort keys
+  uint64_t* SK = sk[w];
+  int cnt = 0;
+  for (int i0 = 0; i0 < HC; i0 += 64) {
+    const int i = i0 + l;
+    const bool occ = K[i] != CS_EMPTY;
+    const uint64_t b = __ballot(occ);
+    if (occ && pass == 1) {
+      const uint32_t mk_ = Mk[i];
+      const uint32_t click = (mk_ >> 8) & 1u, cart = (mk_ >> 9) & 1u, order = (mk_ >> 10) & 1u;
+      // flags in SRC order: self, c2c, c2cob, cart2cart, cart2buy, buy2buy, w2v_all, w2v_1_2, pop_cl50
+      uint32_t f = (mk_ & 1u);
+      f |= (((mk_ >> 1) & 1u) & click) << 1;
+      f |= (((mk_ >> 2) & 1u) & click) << 2;
+      f |= (((mk_ >> 3) & 1u) & cart) << 3;
+      f |= (((mk_ >> 4) & 1u) & cart) << 4;
+      f |= (((mk_ >> 5) & 1u) & order) << 5;
+      f |= ((mk_ >> 6) & 3u) << 6;
+      f |= ((mk_ >> 11) & 1u) << 8;
+      SK[cnt + (int)mbcnt(b)] = ((uint64_t)Ord[i] << 48) | ((uint64_t)K[i] << 16) | f;
+    }
+    cnt += (int)__popcll(b);
+  }
+  if (pass == 0) {
+    if (l == 0) n_cand[s] = (uint32_t)cnt;
+    return;
+  }
+  int P2 = 1;
+  while (P2 < cnt) P2 <<= 1;
+  for (int i = cnt + l; i < P2; i += 64) SK[i] = ~0ull;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  for (int k = 2; k <= P2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = l; i < P2; i += 64) {
+        const int p = i ^ j;
+        if (p > i) {
+          const uint64_t x = SK[i], y = SK[p];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) { SK[i] = y; SK[p] = x; }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+  }
+  const uint64_t o = cand_off[s];
+  for (int i = l; i < cnt; i += 64) {
+    const uint64_t v = SK[i];
+    o_next[o + i] = (int32_t)(uint32_t)(v >> 16);
+    o_ord[o + i] = (int16_t)(v >> 48);
+    o_flags[o + i] = (uint16_t)(v & 0x1FFu);
+  }
+}
+
+// R9: one wave per session; per type: filtered rank of each label in the candidate order
+constexpr int RC_MAX = 4096;
+__global__ __launch_bounds__(64) void k_cand_recall(const uint64_t* __restrict__ cand_off,
+                                                    const int32_t* __restrict__ cnext,
+                                                    const uint16_t* __restrict__ cflags, int64_t S,
+                                                    const int64_t* __restrict__ lab_off,  // [3][S + 1]
+                                                    const int32_t* __restrict__ lab_aid, uint32_t fmask,
+                                                    int max_k, unsigned long long* __restrict__ sums,
+                                                    int* __restrict__ err) {
+  __shared__ uint16_t frank[RC_MAX];
+  const int l = threadIdx.x;
+  const int64_t s = blockIdx.x;
+  if (s >= S) return;
+  const uint64_t c0 = cand_off[s], c1 = cand_off[s + 1];
+  const int n = (int)(c1 - c0);
+  if (n > RC_MAX) { if (l == 0) atomicOr(err, 2); return; }
+  // filtered rank (1-based) of every candidate; 0 = filtered out
+  int base = 0;
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + l;
+    const bool in = i < n && (fmask == 0 || (cflags[c0 + i] & fmask) != 0);
+    const uint64_t b = __ballot(in);
+    if (i < n) frank[i] = in ? (uint16_t)(base + (int)mbcnt(b) + 1) : 0;
+    base += (int)__popcll(b);
+  }
+  __syncthreads();
+  for (int t = 0; t < 3; ++t) {
+    const int64_t lb = lab_off[t * (S + 1) + s], le = lab_off[t * (S + 1) + s + 1];
+    uint32_t h20 = 0, h100 = 0, h200 = 0, hall = 0, tru = 0;
+    for (int64_t j = lb + l; j < le; j += 64) {
+      const int32_t y = lab_aid[j];
+      int r = 0;
+      for (int i = 0; i < n; ++i)
+        if (cnext[c0 + i] == y) { r = frank[i]; break; }
+      tru += 1;
+      if (r > 0) { hall += 1; h20 += r <= 20; h100 += r <= 100; h200 += r <= 200; }
+    }
+    h20 = wave_sum(h20); h100 = wave_sum(h100); h200 = wave_sum(h200); hall = wave_sum(hall); tru = wave_sum(tru);
+    if (l == 0 && tru) {
+      const uint32_t K = (uint32_t)max_k;
+      unsigned long long* o = sums + (size_t)(s & 255) * 16 + t * 5;  // striped: 256 copies of [3][5]
+      atomicAdd(&o[0], (unsigned long long)min(h20, K));
+      atomicAdd(&o[1], (unsigned long long)min(h100, K));
+      atomicAdd(&o[2], (unsigned long long)min(h200, K));
+      atomicAdd(&o[3], (unsigned long long)min(hall, K));
+      atomicAdd(&o[4], (unsigned long long)min(tru, K));
+    }
+  }
+}
+
+// ---- per-source lists: rows (key, nxt, rank) -> CSR by key (stable in row order)
+__global__ void k_cl_keys(const int32_t* __restrict__ key, int64_t n, uint32_t n_keys, uint32_t* __restrict__ k,
+                          uint32_t* __restrict__ v, uint32_t* __restrict__ cnt, int* __restrict__ err) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t a = key[i];
+  if (a < 0 || (uint32_t)a >= n_keys) { atomicOr(err, 1); k[i] = 0; v[i] = (uint32_t)i; return; }
+  k[i] = (uint32_t)a;
+  v[i] = (uint32_t)i;
+  atomicAdd(&cnt[a], 1u);
+}
+__global__ void k_cl_gather(const uint32_t* __restrict__ v, int64_t n, const int32_t* __restrict__ nxt,
+                            const int16_t* __restrict__ rank, int32_t* __restrict__ o_nxt,
+                            int16_t* __restrict__ o_rank) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  o_nxt[i] = nxt[v[i]];
+  if (rank) o_rank[i] = rank[v[i]];
+}
+__global__ void k_u64_to_u32(const uint64_t* __restrict__ a, int64_t n, uint32_t* __restrict__ b) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) b[i] = (uint32_t)a[i];
+}
+
+}  // namespace ottohip
+
+using namespace ottohip;
+
+extern "C" {
+
+// rows (key, nxt[, rank]) -> CSR: out_off [n_keys + 1] (u32), out_nxt / out_rank [n] in key order
+int ottohip_lists_build(ottohip_ctx* ctx, const int32_t* key, const int32_t* nxt, const int16_t* rank, int64_t n,
+                        int32_t n_keys, uint32_t* out_off, int32_t* out_nxt, int16_t* out_rank, void* stream) {
+  if (!ctx || n < 0 || n_keys < 1 || !out_off || (n > 0 && (!key || !nxt || !out_nxt || (rank && !out_rank)))) {
+    set_error("lists_build: bad arguments"); return OTTOHIP_EINVAL;
+  }
+  if (n >= ((int64_t)1 << 32)) { set_error("lists_build: n >= 2^32"); return OTTOHIP_ELIMIT; }
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  Workspace& ws = ctx->ws;
+  uint32_t *k0, *v0, *k1, *v1, *cnt;
+  uint64_t* off64;
+  int* err;
+  OH_TRY(ws.get("cl_k0", (size_t)std::max<int64_t>(n, 1), &k0));
+  OH_TRY(ws.get("cl_v0", (size_t)std::max<int64_t>(n, 1), &v0));
+  OH_TRY(ws.get("cl_k1", (size_t)std::max<int64_t>(n, 1), &k1));
+  OH_TRY(ws.get("cl_v1", (size_t)std::max<int64_t>(n, 1), &v1));
+  OH_TRY(ws.get("cl_cnt", (size_t)n_keys + 1, &cnt));
+  OH_TRY(ws.get("cl_off", (size_t)n_keys + 1, &off64));
+  OH_TRY(ws.get("cl_err", 1, &err));
+  OH_HIP(hipMemsetAsync(cnt, 0, ((size_t)n_keys + 1) * 4, s));
+  OH_HIP(hipMemsetAsync(err, 0, sizeof(int), s));
+  if (n > 0) {
+    k_cl_keys<<<grid_for(n), 256, 0, s>>>(key, n, (uint32_t)n_keys, k0, v0, cnt, err);
+    uint32_t *k = k0, *v = v0;
+    OH_TRY(radix_sort_pairs(ctx, k, v, k1, v1, n, std::max(1, bits_for((uint64_t)n_keys)), s));
+    k_cl_gather<<<grid_for(n), 256, 0, s>>>(v, n, nxt, rank, out_nxt, out_rank);
+  }
+  OH_TRY(exclusive_scan_u32(ctx, cnt, off64, (int64_t)n_keys + 1, nullptr, s));
+  k_u64_to_u32<<<grid_for((int64_t)n_keys + 1), 256, 0, s>>>(off64, (int64_t)n_keys + 1, out_off);
+  OH_HIP(hipGetLastError());
+  int herr = 0;
+  OH_TRY(d2h(&herr, err, 1, s));
+  if (herr) { set_error("lists_build: key outside [0, n_keys)"); return OTTOHIP_ERANGE; }
+  return 0;
+}
+
+struct ottohip_candidates {
+  int64_t n_sessions = 0, n_cand = 0;
+  uint64_t* off = nullptr;  // [S + 1]
+  int32_t* next = nullptr;
+  int16_t* ord = nullptr;
+  uint16_t* flags = nullptr;
+  void release() {
+    if (off) (void)hipFree(off);
+    if (next) (void)hipFree(next);
+    if (ord) (void)hipFree(ord);
+    if (flags) (void)hipFree(flags);
+    off = nullptr; next = nullptr; ord = nullptr; flags = nullptr;
+  }
+};
+
+int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets, int64_t n_sessions,
+                                const int32_t* aid, const int32_t* ts, const int8_t* type,
+                                const ottohip_cand_lists* lists, const int32_t* session_cl,
+                                ottohip_candidates** out, void* stream) {
+  if (!ctx || !lists || !out || n_sessions < 0 || (n_sessions > 0 && (!session_offsets || !aid || !ts || !type))) {
+    set_error("candidates_generate: bad arguments"); return OTTOHIP_EINVAL;
+  }
+  *out = nullptr;
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  CandLists L;
+  for (int q = 0; q < CS_SRC; ++q) {
+    L.off[q] = lists->off[q]; L.nxt[q] = lists->nxt[q]; L.rank[q] = lists->rank[q];
+    if (L.off[q] && (!L.nxt[q] || !L.rank[q])) { set_error("candidates_generate: list %d incomplete", q); return OTTOHIP_EINVAL; }
+  }
+  L.n_items = lists->n_items;
+  L.pop_off = lists->pop_off; L.pop_aid = lists->pop_aid; L.n_clusters = lists->pop_off ? lists->n_clusters : 0;
+  if (lists->max_list_total + 1 > CS_MINI / 2) {
+    set_error("candidates_generate: per-aid list total %d exceeds %d", lists->max_list_total, CS_MINI / 2 - 1);
+    return OTTOHIP_ELIMIT;
+  }
+  ottohip_candidates* C = new ottohip_candidates();
+  C->n_sessions = n_sessions;
+  auto fail = [&](int rc) { C->release(); delete C; return rc; };
+  const int64_t Sn = n_sessions;
+  if (hipMalloc(&C->off, (Sn + 1) * sizeof(uint64_t)) != hipSuccess) return fail(OTTOHIP_ENOMEM);
+  if (Sn == 0) {
+    OH_HIP(hipMemsetAsync(C->off, 0, sizeof(uint64_t), s));
+    *out = C;
+    return 0;
+  }
+  int64_t E = 0;
+  OH_TRY(d2h(&E, session_offsets + Sn, 1, s));
+  Workspace& ws = ctx->ws;
+  KeptAid* kept;
+  uint32_t *n_kept, *n_cand, *n_ovf;
+  int32_t* ovf;
+  uint64_t* tot;
+  int* err;
+  int rc;
+  if ((rc = ws.get("cs_kept", (size_t)std::max<int64_t>(E, 1), &kept)) ||
+      (rc = ws.get("cs_nkept", (size_t)Sn, &n_kept)) || (rc = ws.get("cs_ncand", (size_t)Sn + 1, &n_cand)) ||
+      (rc = ws.get("cs_novf", 1, &n_ovf)) || (rc = ws.get("cs_ovf", (size_t)Sn, &ovf)) ||
+      (rc = ws.get("cs_tot", 1, &tot)) || (rc = ws.get("cs_err", 1, &err)))
+    return fail(rc);
+  int ph = ctx->begin("cand_aids", s, 9.0 * E);
+  hipMemsetAsync(err, 0, sizeof(int), s);
+  hipMemsetAsync(n_ovf, 0, sizeof(uint32_t), s);
+  hipMemsetAsync(n_cand + Sn, 0, sizeof(uint32_t), s);
+  k_cand_aids<<<(unsigned)Sn, 64, 0, s>>>(session_offsets, Sn, aid, ts, type, kept, n_kept, err);
+  ctx->end(ph, s);
+  ph = ctx->begin("cand_build", s, 0);
+  constexpr int W = 2;
+  k_cand_build<1024, W><<<(unsigned)ceil_div(Sn, W), 64 * W, 0, s>>>(session_offsets, nullptr, Sn, kept, n_kept,
+                                                                       session_cl, L, 0, n_cand, nullptr, nullptr,
+                                                                       nullptr, nullptr, ovf, n_ovf);
+  uint32_t novf = 0;
+  int herr = 0;
+  if ((rc = d2h(&novf, n_ovf, 1, s)) || (rc = d2h(&herr, err, 1, s))) return fail(rc);
+  if (herr) { set_error("candidates_generate: a session has more than %d events", CS_MAXE); return fail(OTTOHIP_ELIMIT); }
+  int64_t* ovf64 = nullptr;
+  uint32_t* n_ovf2 = nullptr;
+  int32_t* ovf2 = nullptr;
+  if (novf) {  // sessions beyond the 1024-slot tier: sorted list, 4096-slot tier
+    if ((rc = ws.get("cs_novf2", 1, &n_ovf2)) || (rc = ws.get("cs_ovf2", (size_t)novf, &ovf2)) ||
+        (rc = ws.get("cs_ovf64", (size_t)novf, &ovf64)))
+      return fail(rc);
+    std::vector<int32_t> ho(novf);
+    if ((rc = d2h(ho.data(), ovf, novf, s))) return fail(rc);
+    std::sort(ho.begin(), ho.end());
+    std::vector<int64_t> ho64(ho.begin(), ho.end());
+    OH_HIP(hipMemcpyAsync(ovf64, ho64.data(), novf * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    OH_HIP(hipMemsetAsync(n_ovf2, 0, sizeof(uint32_t), s));
+    k_cand_build<4096, 1><<<novf, 64, 0, s>>>(session_offsets, ovf64, novf, kept, n_kept, session_cl, L, 0, n_cand,
+                                               nullptr, nullptr, nullptr, nullptr, ovf2, n_ovf2);
+    uint32_t novf2 = 0;
+    if ((rc = d2h(&novf2, n_ovf2, 1, s))) return fail(rc);
+    if (novf2) { set_error("candidates_generate: %u sessions exceed 4096 candidates", novf2); return fail(OTTOHIP_ELIMIT); }
+  }
+  if ((rc = exclusive_scan_u32(ctx, n_cand, C->off, Sn + 1, tot, s))) return fail(rc);
+  uint64_t nc = 0;
+  if ((rc = d2h(&nc, tot, 1, s))) return fail(rc);
+  C->n_cand = (int64_t)nc;
+  const size_t cap = (size_t)std::max<uint64_t>(nc, 1);
+  if (hipMalloc(&C->next, cap * 4) || hipMalloc(&C->ord, cap * 2) || hipMalloc(&C->flags, cap * 2)) {
+    (void)hipGetLastError();
+    return fail(OTTOHIP_ENOMEM);
+  }
+  k_cand_build<1024, W><<<(unsigned)ceil_div(Sn, W), 64 * W, 0, s>>>(session_offsets, nullptr, Sn, kept, n_kept,
+                                                                       session_cl, L, 1, n_cand, C->off, C->next,
+                                                                       C->ord, C->flags, ovf, n_ovf);
+  if (novf)
+    k_cand_build<4096, 1><<<novf, 64, 0, s>>>(session_offsets, ovf64, novf, kept, n_kept, session_cl, L, 1, n_cand,
+                                               C->off, C->next, C->ord, C->flags, ovf2, n_ovf2);
+  if (hipGetLastError() != hipSuccess) { set_error("k_cand_build launch failed"); return fail(OTTOHIP_EHIP); }
+  ctx->end(ph, s);
+  *out = C;
+  return 0;
+}
+
+int ottohip_candidates_info(const ottohip_candidates* c, int64_t* n_sessions, int64_t* n_cand) {
+  if (!c) { set_error("candidates_info: NULL"); return OTTOHIP_EINVAL; }
+  if (n_sessions) *n_sessions = c->n_sessions;
+  if (n_cand) *n_cand = c->n_cand;
+  return 0;
+}
+
+int ottohip_candidates_copy(const ottohip_candidates* c, uint64_t* off, int32_t* aid_next, int16_t* ts_order,
+                            uint16_t* flags, void* stream) {
+  if (!c) { set_error("candidates_copy: NULL"); return OTTOHIP_EINVAL; }
+  hipStream_t s = S(stream);
+  if (off) OH_HIP(hipMemcpyAsync(off, c->off, (c->n_sessions + 1) * 8, hipMemcpyDeviceToDevice, s));
+  if (c->n_cand > 0) {
+    if (aid_next) OH_HIP(hipMemcpyAsync(aid_next, c->next, c->n_cand * 4, hipMemcpyDeviceToDevice, s));
+    if (ts_order) OH_HIP(hipMemcpyAsync(ts_order, c->ord, c->n_cand * 2, hipMemcpyDeviceToDevice, s));
+    if (flags) OH_HIP(hipMemcpyAsync(flags, c->flags, c->n_cand * 2, hipMemcpyDeviceToDevice, s));
+  }
+  return 0;
+}
+
+void ottohip_candidates_free(ottohip_candidates* c) {
+  if (!c) return;
+  (void)hipDeviceSynchronize();
+  c->release();
+  delete c;
+}
+
+int ottohip_candidates_recall(ottohip_ctx* ctx, const ottohip_candidates* c, const int64_t* lab_off,
+                              const int32_t* lab_aid, uint32_t src_mask, int max_k, int64_t* sums_out, void* stream) {
+  if (!ctx || !c || !sums_out || (c->n_sessions > 0 && !lab_off)) { set_error("candidates_recall: bad args"); return OTTOHIP_EINVAL; }
+  for (int i = 0; i < 15; ++i) sums_out[i] = 0;
+  if (c->n_sessions == 0) return 0;
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  unsigned long long* sums;
+  int* err;
+  OH_TRY(ctx->ws.get("rc_sums", 256 * 16, &sums));
+  OH_TRY(ctx->ws.get("rc_err", 1, &err));
+  OH_HIP(hipMemsetAsync(sums, 0, 256 * 16 * 8, s));
+  OH_HIP(hipMemsetAsync(err, 0, sizeof(int), s));
+  k_cand_recall<<<(unsigned)c->n_sessions, 64, 0, s>>>(c->off, c->next, c->flags, c->n_sessions, lab_off, lab_aid,
+                                                       src_mask, max_k, sums, err);
+  OH_HIP(hipGetLastError());
+  std::vector<unsigned long long> h(256 * 16);
+  OH_TRY(d2h(h.data(), sums, h.size(), s));
+  int herr = 0;
+  OH_TRY(d2h(&herr, err, 1, s));
+  if (herr) { set_error("candidates_recall: a session has more than %d candidates", RC_MAX); return OTTOHIP_ELIMIT; }
+  for (int k = 0; k < 256; ++k)
+    for (int i = 0; i < 15; ++i) sums_out[i] += (int64_t)h[(size_t)k * 16 + i];
+  return 0;
+}
+
+}  // extern "C"

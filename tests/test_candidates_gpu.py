@@ -1,0 +1,120 @@
+"""GPU parity of config-5 candidate generation (csrc/candidates.hip) and recall against the
+pandas restatement in oracle/retrieve.py (model/retrieve.py:138-290, 477-595, 647;
+model/eval_retrieved.py:45-118). Candidate rows and flags: exact; recall: exact ratios of
+identical integer sums. Parity unpinned beyond the restatement: the reference has no tests."""
+import numpy as np
+import pandas as pd
+import pytest
+
+import covis as oracle
+import retrieve as oracle_retrieve
+import otto_recommender_amd.synth as synth
+
+pytestmark = pytest.mark.gpu
+RULES = oracle_retrieve.RULES
+
+
+def _fixture(n_sessions=3000, seed=7, first=4242):
+    ev = synth.generate(n_sessions, first_session=first, seed=seed)
+    df = ev.to_pandas()
+    # R1 tables from the session counts (no MIN_COUNT thresholds, to get rich lists at this size)
+    per = oracle.count_co_events_file(ev.session_offsets, ev.aid, ev.ts, ev.type)
+    r1 = {}
+    for n in RULES:
+        a, b, c = per[n]
+        o = np.lexsort((b, a, -c.astype(np.int64)))
+        first_n = 10 if n.startswith("click_to") else 20
+        t = oracle_retrieve.get_df_count_for_co_event_type(a[o], b[o], c[o].astype(np.int32), first_n)
+        r1[n] = pd.DataFrame({"aid": t["aid"], "aid_next": t["aid_next"], f"{n}_rank": t["rank"]})
+    rng = np.random.default_rng(seed)
+    uni = np.unique(ev.aid)
+    knn = []
+    for name in ("all", "1_2"):
+        q = uni[rng.random(len(uni)) < 0.8]
+        nb = rng.choice(uni, size=(len(q), 19))
+        rows = {"aid": np.repeat(q, 20), "aid_next": np.concatenate([q[:, None], nb], 1).ravel(),
+                f"rank_w2vec_{name}": np.tile(np.arange(1, 21, dtype=np.int8), len(q)),
+                f"dist_w2vec_{name}": np.zeros(len(q) * 20, np.int32)}
+        k = pd.DataFrame(rows).drop_duplicates(["aid", "aid_next"])
+        knn.append(k)
+    sess = np.unique(ev.session)
+    cl = pd.DataFrame({"session": sess, "cl50": rng.integers(-1, 6, len(sess))})
+    cl = cl[rng.random(len(cl)) < 0.9]
+    pop = []
+    for c in range(-1, 6):
+        aids = rng.choice(uni, size=rng.integers(5, 40), replace=False)
+        pop.append(pd.DataFrame({"aid": aids, "cl50": c, "rank_clicks_cl50": rng.integers(1, 40, len(aids))}))
+    pop = pd.concat(pop)
+    return ev, df, r1, knn[0], knn[1], cl, pop
+
+
+def _labels(df, seed=3):
+    rng = np.random.default_rng(seed)
+    rows = []
+    for s, g in df.groupby("session"):
+        a = g["aid"].to_numpy()
+        rows.append((s, int(rng.choice(a)), 0))
+        for t, k in ((1, rng.integers(0, 3)), (2, rng.integers(0, 2))):
+            for x in rng.choice(a, size=k):
+                rows.append((s, int(x), t))
+        if rng.random() < 0.3:
+            rows.append((s, int(rng.integers(0, 1855603)), 1))
+    return pd.DataFrame(rows, columns=["session", "aid", "type"]).drop_duplicates()
+
+
+def test_candidates_match_restatement(gpu):
+    from otto_recommender_amd import candidates as gcand
+    ev, df, r1, ka, k12, cl, pop = _fixture()
+    pop_f = pop[pop["rank_clicks_cl50"] <= 20]
+    ref = oracle_retrieve.candidates(df, r1, ka.rename(columns={"rank_w2vec_all": "rank"}),
+                                     k12.rename(columns={"rank_w2vec_1_2": "rank"}), cl, pop_f[["cl50", "aid"]])
+    got = gcand.retrieve_candidates(df, r1, ka, k12, cl, pop)
+    assert len(got) == len(ref)
+    for c in ["session", "aid_next", "ts_order_aid"] + gcand.SRC_NAMES:
+        np.testing.assert_array_equal(got[c].to_numpy().astype(np.int64), ref[c].to_numpy().astype(np.int64),
+                                      err_msg=c)
+    assert got["src_pop_cl50"].sum() > 0 and got["src_w2vec_all"].sum() > 0 and got["src_click_to_click"].sum() > 0
+
+
+def test_candidates_without_popularity_and_recall(gpu):
+    from otto_recommender_amd import candidates as gcand
+    ev, df, r1, ka, k12, cl, pop = _fixture(2000, seed=11, first=99)
+    ref = oracle_retrieve.candidates(df, r1, ka.rename(columns={"rank_w2vec_all": "rank"}),
+                                     k12.rename(columns={"rank_w2vec_1_2": "rank"}))
+    src = gcand.CandidateSources({n: (t["aid"].to_numpy(), t["aid_next"].to_numpy(), t[f"{n}_rank"].to_numpy())
+                                  for n, t in r1.items()},
+                                 (ka["aid"].to_numpy(), ka["aid_next"].to_numpy(), ka["rank_w2vec_all"].to_numpy()),
+                                 (k12["aid"].to_numpy(), k12["aid_next"].to_numpy(), k12["rank_w2vec_1_2"].to_numpy()))
+    c = gcand.generate(ev.session_offsets, ev.aid, ev.ts, ev.type, src)
+    sess = ev.session[ev.session_offsets[:-1]]
+    got = c.to_pandas(sess)
+    for col in ["session", "aid_next", "ts_order_aid"] + gcand.SRC_NAMES:
+        np.testing.assert_array_equal(got[col].to_numpy().astype(np.int64), ref[col].to_numpy().astype(np.int64))
+    labels = _labels(df)
+    lo, la = gcand.labels_csr(labels, sess)
+    for s in (None, "src_self", "src_click_to_click", "src_w2vec_all"):
+        r = c.recall(lo, la, src=s)
+        e = oracle_retrieve.recall(ref, labels, src=s)
+        for t in ("clicks", "carts", "orders", "total"):
+            for k in ("20", "100", "200", "all"):
+                assert abs(r[t][f"top{k}"] - e[t][f"top{k}"]) < 1e-12, (s, t, k)
+    c.free()
+
+
+def test_candidates_edge_sessions(gpu):
+    """single-event sessions, sessions of 200 distinct aids (> 99: the keep filter trims),
+    repeated aids with all three types."""
+    from otto_recommender_amd import candidates as gcand
+    rows = [(1, 5, 100, 0)]
+    rows += [(2, 1000 + i, 1000 + i, i % 3) for i in range(200)]
+    rows += [(3, 7, 10, 0), (3, 7, 20, 1), (3, 7, 30, 2), (3, 8, 15, 0), (3, 8, 15, 0)]
+    df = pd.DataFrame(rows, columns=["session", "aid", "ts", "type"])
+    empty = {n: pd.DataFrame({"aid": np.zeros(0, np.int32), "aid_next": np.zeros(0, np.int32),
+                              f"{n}_rank": np.zeros(0, np.int16)}) for n in RULES}
+    kn = lambda nm: pd.DataFrame({"aid": np.array([7, 7, 1001], np.int32), "aid_next": np.array([7, 9, 5], np.int32),
+                                  f"rank_w2vec_{nm}": np.array([1, 2, 1], np.int8)})
+    ref = oracle_retrieve.candidates(df, empty, kn("all").rename(columns={"rank_w2vec_all": "rank"}),
+                                     kn("1_2").rename(columns={"rank_w2vec_1_2": "rank"}))
+    got = gcand.retrieve_candidates(df, empty, kn("all"), kn("1_2"))
+    for col in ["session", "aid_next", "ts_order_aid"] + gcand.SRC_NAMES:
+        np.testing.assert_array_equal(got[col].to_numpy().astype(np.int64), ref[col].to_numpy().astype(np.int64))
