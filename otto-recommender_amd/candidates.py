@@ -48,7 +48,8 @@ def build_lists(key, nxt, rank, n_keys: int, ctx=None, stream=None):
                                                _lib.ptr(off), _lib.ptr(on) if n else None,
                                                _lib.ptr(orr) if (orr is not None and n) else None,
                                                _lib.stream_handle(stream)))
-    return off, on[:n], (orr[:n] if orr is not None else None)
+    # empty lists keep a 1-element buffer: a zero-element tensor reports data_ptr() == 0
+    return off, (on[:n] if n else on), ((orr[:n] if n else orr) if orr is not None else None)
 
 
 class CandidateSources:
@@ -73,7 +74,7 @@ class CandidateSources:
             off, nx, rk = build_lists(a, b, r, self.n_items, self.ctx)
             self.keep += [off, nx, rk]
             self.abi.off[q], self.abi.nxt[q], self.abi.rank[q] = _lib.ptr(off), _lib.ptr(nx), _lib.ptr(rk)
-            if nx.numel():
+            if int(off[-1].item()) > 0:
                 total += int((off[1:] - off[:-1]).max().item())
         self.abi.n_items = self.n_items
         self.abi.max_list_total = total
