@@ -169,6 +169,40 @@ void ottohip_candidates_free(ottohip_candidates* c);
 int ottohip_candidates_recall(ottohip_ctx* ctx, const ottohip_candidates* c, const int64_t* lab_off,
                               const int32_t* lab_aid, uint32_t src_mask, int max_k, int64_t* sums_out, void* stream);
 
+/* ---- Pop-cluster source (C1-C3) and session-item similarity (R7) -------------------------
+ * C1 compute_sessions_embeddings (model/kmeans_sessions.py:40-86): per session
+ *    round6(sum w e_aid / sum w), w = f32(max(0.1, 1 - (max_ts - ts)/259200) * {0.1,0.3,0.6}[type]);
+ *    row_of_aid maps an aid to its embedding row (-1 = no embedding: adds 0, keeps its weight).
+ *    out: [n_sessions x dim] f32. fp32 accumulation in event order (polars' order is unspecified). */
+int ottohip_session_embeddings(ottohip_ctx* ctx, const int64_t* session_offsets, int64_t n_sessions,
+                               const int32_t* aid, const int32_t* ts, const int8_t* type, const int32_t* row_of_aid,
+                               int32_t n_aid_map, const float* emb, int dim, float* out, void* stream);
+/* C2 KMeans (model/kmeans_sessions.py:140-171): one Lloyd iteration on X [n x dim] with centroids
+ * [k x dim] updated in place (empty clusters keep theirs); *shift2 = squared centroid shift (the
+ * sklearn / dask-ml convergence quantity). Sums are 2^-24 fixed point: order-independent. k <= 64. */
+int ottohip_kmeans_step(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* centroids, int k,
+                        int32_t* labels, double* shift2, double* inertia, void* stream);
+int ottohip_kmeans_assign(ottohip_ctx* ctx, const float* X, int64_t n, int dim, const float* centroids, int k,
+                          int32_t* labels, double* inertia, void* stream);
+/* C3 count_popularity (model/count_popularity.py:53-85) for one clustering: per (cluster, aid)
+ * n_{clicks,carts,orders} and *_7d (ts > ts_7d), ordinal rank desc within the cluster (ties: aid
+ * asc) clipped to 999, rows with min rank <= keep_top_k. session_cl: dense cluster per session. */
+typedef struct ottohip_pop ottohip_pop;
+int ottohip_popularity_ranks(ottohip_ctx* ctx, const int64_t* session_offsets, int64_t n_sessions,
+                             const int32_t* aid, const int32_t* ts, const int8_t* type, const int32_t* session_cl,
+                             int32_t n_items, int32_t n_clusters, int32_t ts_7d, int keep_top_k,
+                             ottohip_pop** out, int64_t* n_out, void* stream);
+/* rows sorted by (cluster, aid); ranks6 [n x 6]: clicks, carts, orders, clicks_7d, carts_7d, orders_7d */
+int ottohip_pop_copy(const ottohip_pop* p, int32_t* aid, int32_t* cluster, int16_t* ranks6, void* stream);
+void ottohip_pop_free(ottohip_pop* p);
+/* R7 (model/retrieve.py:604-625): cos and Euclidean distance between the session embedding and
+ * each candidate's item embedding; a session without an embedding (sess_has[s] == 0) or an item
+ * without one gives cos 0, eucl -1 (the inner joins + fill_null of :621-625). */
+int ottohip_session_item_similarity(ottohip_ctx* ctx, const int64_t* cand_off, int64_t n_sessions,
+                                    const int32_t* aid_next, const float* sess_emb, const uint8_t* sess_has,
+                                    const int32_t* row_of_aid, int32_t n_aid_map, const float* emb, int dim,
+                                    float* cos_out, float* eucl_out, void* stream);
+
 /* ---- Multi-GPU exchange -------------------------------------------------
  * The reference is single-process; these calls replace the cross-file groupby of
  * concat_files_w_stats (model/count_co_events.py:168) when files are dealt over G ranks.

@@ -73,6 +73,17 @@ SIGNATURES = {
     "ottohip_candidates_free": (None, [_VP]),
     "ottohip_candidates_recall": (ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_uint32, ctypes.c_int,
                                                  ctypes.POINTER(_I64), _VP]),
+    "ottohip_session_embeddings": (ctypes.c_int, [_VP, _VP, _I64, _VP, _VP, _VP, _VP, _I32, _VP, ctypes.c_int, _VP, _VP]),
+    "ottohip_kmeans_step": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP, ctypes.c_int, _VP,
+                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), _VP]),
+    "ottohip_kmeans_assign": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP, ctypes.c_int, _VP,
+                                             ctypes.POINTER(ctypes.c_double), _VP]),
+    "ottohip_popularity_ranks": (ctypes.c_int, [_VP, _VP, _I64, _VP, _VP, _VP, _VP, _I32, _I32, _I32, ctypes.c_int,
+                                                ctypes.POINTER(_VP), ctypes.POINTER(_I64), _VP]),
+    "ottohip_pop_copy": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
+    "ottohip_pop_free": (None, [_VP]),
+    "ottohip_session_item_similarity": (ctypes.c_int, [_VP, _VP, _I64, _VP, _VP, _VP, _VP, _I32, _VP, ctypes.c_int,
+                                                       _VP, _VP, _VP]),
     "ottohip_owner_of": (ctypes.c_int, [_I32, ctypes.c_int]),
     "ottohip_table_pack_by_owner": (ctypes.c_int, [_VP, _VP, ctypes.c_int, _VP, ctypes.POINTER(_I64), _VP]),
     "ottohip_table_from_records": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _I32, ctypes.POINTER(RuleStats),

@@ -1,0 +1,464 @@
+// Pop-cluster source of config 5 and the session-item similarity R7.
+//
+//   C1 k_sess_emb     compute_sessions_embeddings (model/kmeans_sessions.py:40-86): one wave per
+//                     session, w = f32(max(0.1, 1 - (max_ts - ts) / 259200) * {0.1, 0.3, 0.6}[type]),
+//                     e_s = round6(sum w e_aid / sum w); aids without an embedding add 0 but keep w
+//   C2 k_km_assign    Lloyd step of KMeans (model/kmeans_sessions.py:140-171): nearest centroid
+//                     per session (centroids in LDS) and per-cluster sums accumulated in 2^-24 fixed
+//                     point with int64 atomics, so the update is independent of the atomic order
+//   C3 k_pop_*        count_popularity.py:53-85: per (cluster, aid) counts by type and over the
+//                     last 7 days, ordinal rank desc within the cluster (ties: aid asc), clip 999,
+//                     keep min rank <= keep_top_k
+//   R7 k_sim          model/retrieve.py:604-625: dot, norms, cos and Euclidean distance between the
+//                     session embedding and each candidate's item embedding (fp32)
+#include <algorithm>
+#include <cmath>
+#include "prims.h"
+#include "table.h"
+
+namespace ottohip {
+
+constexpr int EMB_MAXD = 128;
+
+// ---------------------------------------------------------------- C1
+__global__ __launch_bounds__(64) void k_sess_emb(const int64_t* __restrict__ off, int64_t S,
+                                                 const int32_t* __restrict__ aid, const int32_t* __restrict__ ts,
+                                                 const int8_t* __restrict__ type, const int32_t* __restrict__ row_of_aid,
+                                                 int32_t n_aid_map, const float* __restrict__ emb, int dim,
+                                                 float* __restrict__ out) {
+  const int l = threadIdx.x;
+  const int64_t s = blockIdx.x;
+  if (s >= S) return;
+  const int64_t e0 = off[s], e1 = off[s + 1];
+  int32_t mx = INT32_MIN;
+  for (int64_t e = e0 + l; e < e1; e += 64) mx = max(mx, ts[e]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+  float acc0 = 0.f, acc1 = 0.f, wsum = 0.f;
+  const float wt[3] = {0.1f, 0.3f, 0.6f};
+  for (int64_t e = e0; e < e1; ++e) {
+    double wtime = 1.0 - (double)(mx - ts[e]) / 259200.0;
+    if (wtime < 0.10) wtime = 0.10;
+    const int y = type[e];
+    const float w = (float)(wtime * (double)wt[y < 0 ? 0 : (y > 2 ? 2 : y)]);
+    const int32_t a = aid[e];
+    const int32_t r = (a >= 0 && a < n_aid_map) ? row_of_aid[a] : -1;
+    wsum += w;
+    if (r >= 0) {
+      const float* v = emb + (int64_t)r * dim;
+      if (l < dim) acc0 += v[l] * w;
+      if (l + 64 < dim) acc1 += v[l + 64] * w;
+    }
+  }
+  float* o = out + s * dim;
+  if (l < dim) o[l] = (float)(nearbyint((double)(acc0 / wsum) * 1e6) / 1e6);
+  if (l + 64 < dim) o[l + 64] = (float)(nearbyint((double)(acc1 / wsum) * 1e6) / 1e6);
+}
+
+// ---------------------------------------------------------------- C2
+constexpr int KM_MAXK = 64;
+constexpr double KM_FX = 16777216.0;  // 2^24 fixed point for the cluster sums
+
+// one thread per row; centroids (k x dim f32) and their squared norms in LDS
+// per-block sums in LDS (int64 fixed point), flushed with one device atomic per (cluster, dim)
+__global__ __launch_bounds__(256) void k_km_assign(const float* __restrict__ X, int64_t n, int dim,
+                                                   const float* __restrict__ C, int k, int32_t* __restrict__ label,
+                                                   unsigned long long* __restrict__ sums,
+                                                   unsigned long long* __restrict__ cnt, double* __restrict__ inertia) {
+  extern __shared__ unsigned long long smem64[];
+  unsigned long long* ls = smem64;                       // k * dim sums (fixed point, two's complement)
+  unsigned long long* lc = smem64 + k * dim;             // k counts
+  float* Cs = reinterpret_cast<float*>(smem64 + k * dim + k);  // k * dim
+  float* cn = Cs + k * dim;                              // k
+  for (int i = threadIdx.x; i < k * dim; i += blockDim.x) { Cs[i] = C[i]; ls[i] = 0ull; }
+  for (int i = threadIdx.x; i < k; i += blockDim.x) lc[i] = 0ull;
+  __syncthreads();
+  for (int c = threadIdx.x; c < k; c += blockDim.x) {
+    float s = 0.f;
+    for (int d = 0; d < dim; ++d) s += Cs[c * dim + d] * Cs[c * dim + d];
+    cn[c] = s;
+  }
+  __syncthreads();
+  double part = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float* x = X + i * dim;
+    float xn = 0.f;
+    float best = INFINITY;
+    int bc = 0;
+    // |x - c|^2 = |x|^2 - 2 x.c + |c|^2; dims streamed once, all k dot products accumulated
+    float dot[KM_MAXK];
+#pragma unroll
+    for (int c = 0; c < KM_MAXK; ++c) dot[c] = 0.f;
+    for (int d = 0; d < dim; ++d) {
+      const float xv = x[d];
+      xn += xv * xv;
+#pragma unroll
+      for (int c = 0; c < KM_MAXK; ++c)
+        if (c < k) dot[c] += xv * Cs[c * dim + d];
+    }
+#pragma unroll
+    for (int c = 0; c < KM_MAXK; ++c) {
+      if (c < k) {
+        const float dd = xn - 2.f * dot[c] + cn[c];
+        if (dd < best) { best = dd; bc = c; }  // ties: lowest cluster index
+      }
+    }
+    label[i] = bc;
+    part += (double)fmaxf(best, 0.f);
+    if (sums) {
+      for (int d = 0; d < dim; ++d)
+        atomicAdd(&ls[bc * dim + d], (unsigned long long)(long long)llrint((double)x[d] * KM_FX));
+      atomicAdd(&lc[bc], 1ull);
+    }
+  }
+  __syncthreads();
+  if (sums) {
+    for (int i = threadIdx.x; i < k * dim; i += blockDim.x)
+      if (ls[i]) atomicAdd(&sums[i], ls[i]);
+    for (int i = threadIdx.x; i < k; i += blockDim.x)
+      if (lc[i]) atomicAdd(&cnt[i], lc[i]);
+  }
+  // inertia: block partial in fixed order over waves then one atomic (f64; reporting only)
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint64_t b = __double_as_longlong(part);
+    const uint32_t lo = __shfl_xor((uint32_t)b, o), hi = __shfl_xor((uint32_t)(b >> 32), o);
+    part += __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+  }
+  if ((threadIdx.x & 63) == 0) atomicAdd(inertia, part);
+}
+
+// ---------------------------------------------------------------- C3
+// counters: [6][n_clusters * n_items] u32: n_clicks, n_carts, n_orders, *_7d
+__global__ void k_pop_count(const int64_t* __restrict__ off, int64_t S, const int32_t* __restrict__ aid,
+                            const int32_t* __restrict__ ts, const int8_t* __restrict__ type,
+                            const int32_t* __restrict__ session_cl, int32_t n_items, int32_t n_clusters,
+                            int32_t ts_7d, uint32_t* __restrict__ cnt, uint32_t* __restrict__ present,
+                            int* __restrict__ err) {
+  const int64_t s = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (s >= S) return;
+  const int c = session_cl[s];
+  if (c < 0 || c >= n_clusters) { if ((threadIdx.x & 63) == 0) atomicOr(err, 1); return; }
+  const int64_t NS = (int64_t)n_clusters * n_items;
+  for (int64_t e = off[s] + (threadIdx.x & 63); e < off[s + 1]; e += 64) {
+    const int32_t a = aid[e];
+    const int y = type[e];
+    if (a < 0 || a >= n_items || y < 0 || y > 2) { atomicOr(err, 2); continue; }
+    const int64_t slot = (int64_t)c * n_items + a;
+    atomicAdd(&cnt[y * NS + slot], 1u);
+    if (ts[e] > ts_7d) atomicAdd(&cnt[(3 + y) * NS + slot], 1u);
+    present[slot] = 1u;
+  }
+}
+
+__global__ void k_pop_pairs(const uint32_t* __restrict__ present, const uint64_t* __restrict__ idx, int64_t NS,
+                            uint32_t* __restrict__ pair_slot) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < NS && present[i]) pair_slot[idx[i]] = (uint32_t)i;
+}
+
+// LSD keys for one counter: aid asc, then count desc, then cluster asc (stable)
+__global__ void k_pop_key(const uint32_t* __restrict__ pair_slot, const uint32_t* __restrict__ val, int64_t n,
+                          const uint32_t* __restrict__ cnt, int32_t n_items, int which, uint32_t* __restrict__ key) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t slot = pair_slot[val ? val[i] : i];
+  if (which == 0) key[i] = slot % (uint32_t)n_items;       // aid
+  else if (which == 1) key[i] = ~cnt[slot];                // count desc
+  else key[i] = slot / (uint32_t)n_items;                  // cluster
+}
+
+__global__ void k_pop_iota(uint32_t* __restrict__ v, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) v[i] = (uint32_t)i;
+}
+
+__global__ void k_pop_rank(const uint32_t* __restrict__ pair_slot, const uint32_t* __restrict__ val, int64_t n,
+                           int32_t n_items, const uint64_t* __restrict__ cl_first, uint16_t* __restrict__ rank) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t p = val[i];
+  const uint32_t c = pair_slot[p] / (uint32_t)n_items;
+  const int64_t r = i - (int64_t)cl_first[c] + 1;
+  rank[p] = (uint16_t)(r > 999 ? 999 : r);
+}
+
+__global__ void k_pop_cluster_hist(const uint32_t* __restrict__ pair_slot, int64_t n, int32_t n_items,
+                                   uint32_t* __restrict__ hist) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) atomicAdd(&hist[pair_slot[i] / (uint32_t)n_items], 1u);
+}
+
+__global__ void k_pop_keep(const uint16_t* __restrict__ rank, int64_t n, int keep_top_k, uint32_t* __restrict__ keep) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int m = 999;
+#pragma unroll
+  for (int t = 0; t < 6; ++t) m = min(m, (int)rank[t * n + i]);
+  keep[i] = m <= keep_top_k ? 1u : 0u;
+}
+
+__global__ void k_pop_out(const uint32_t* __restrict__ pair_slot, const uint16_t* __restrict__ rank,
+                          const uint32_t* __restrict__ keep, const uint64_t* __restrict__ oidx, int64_t n,
+                          int32_t n_items, int32_t* __restrict__ o_aid, int32_t* __restrict__ o_cl,
+                          int16_t* __restrict__ o_rank) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !keep[i]) return;
+  const uint64_t o = oidx[i];
+  o_aid[o] = (int32_t)(pair_slot[i] % (uint32_t)n_items);
+  o_cl[o] = (int32_t)(pair_slot[i] / (uint32_t)n_items);
+#pragma unroll
+  for (int t = 0; t < 6; ++t) o_rank[o * 6 + t] = (int16_t)rank[t * n + i];
+}
+
+// ---------------------------------------------------------------- R7
+__global__ __launch_bounds__(256) void k_sim(const int64_t* __restrict__ cand_off, int64_t S,
+                                             const int32_t* __restrict__ cnext, const float* __restrict__ sess_emb,
+                                             const uint8_t* __restrict__ sess_has, const int32_t* __restrict__ row_of_aid,
+                                             int32_t n_aid_map, const float* __restrict__ emb, int dim,
+                                             float* __restrict__ cos_out, float* __restrict__ eucl_out) {
+  const int64_t s = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (s >= S) return;
+  const int l = threadIdx.x & 63;
+  const float* q = sess_emb + s * dim;
+  const bool hs = sess_has == nullptr || sess_has[s];
+  for (int64_t i = cand_off[s] + l; i < cand_off[s + 1]; i += 64) {
+    const int32_t a = cnext[i];
+    const int32_t r = (a >= 0 && a < n_aid_map) ? row_of_aid[a] : -1;
+    if (!hs || r < 0) { cos_out[i] = 0.f; eucl_out[i] = -1.f; continue; }  // inner joins miss: fill 0 / -1
+    const float* v = emb + (int64_t)r * dim;
+    float dot = 0.f, nq = 0.f, nv = 0.f, d2 = 0.f;
+    for (int d = 0; d < dim; ++d) {
+      const float x = q[d], y = v[d];
+      dot += x * y; nq += x * x; nv += y * y;
+      const float z = x - y;
+      d2 += z * z;
+    }
+    cos_out[i] = dot / (sqrtf(nq) * sqrtf(nv));
+    eucl_out[i] = sqrtf(d2);
+  }
+}
+
+}  // namespace ottohip
+
+using namespace ottohip;
+
+extern "C" {
+
+int ottohip_session_embeddings(ottohip_ctx* ctx, const int64_t* session_offsets, int64_t n_sessions,
+                               const int32_t* aid, const int32_t* ts, const int8_t* type, const int32_t* row_of_aid,
+                               int32_t n_aid_map, const float* emb, int dim, float* out, void* stream) {
+  if (!ctx || n_sessions < 0 || dim < 1 || dim > EMB_MAXD || (n_sessions > 0 && (!session_offsets || !aid || !ts ||
+      !type || !row_of_aid || !emb || !out))) {
+    set_error("session_embeddings: bad arguments (dim <= %d)", EMB_MAXD); return OTTOHIP_EINVAL;
+  }
+  if (n_sessions == 0) return 0;
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  int ph = ctx->begin("sess_emb", s, 0);
+  k_sess_emb<<<(unsigned)n_sessions, 64, 0, s>>>(session_offsets, n_sessions, aid, ts, type, row_of_aid, n_aid_map,
+                                                emb, dim, out);
+  OH_HIP(hipGetLastError());
+  ctx->end(ph, s);
+  return 0;
+}
+
+// One Lloyd iteration: labels, new centroids (empty clusters keep theirs), center shift^2, inertia.
+int ottohip_kmeans_step(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* centroids, int k,
+                        int32_t* labels, double* shift2, double* inertia, void* stream) {
+  if (!ctx || !X || !centroids || !labels || n < 1 || dim < 1 || dim > EMB_MAXD || k < 1 || k > KM_MAXK) {
+    set_error("kmeans_step: bad arguments (k <= %d, dim <= %d)", KM_MAXK, EMB_MAXD); return OTTOHIP_EINVAL;
+  }
+  if (((size_t)k * dim + k) * (sizeof(float) + 8) > 65536) { set_error("kmeans_step: k * dim too large for LDS"); return OTTOHIP_ELIMIT; }
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  unsigned long long* sums;
+  unsigned long long* cnt;
+  double* inr;
+  OH_TRY(ctx->ws.get("km_sums", (size_t)k * dim, &sums));
+  OH_TRY(ctx->ws.get("km_cnt", (size_t)k, &cnt));
+  OH_TRY(ctx->ws.get("km_inertia", 1, &inr));
+  OH_HIP(hipMemsetAsync(sums, 0, (size_t)k * dim * 8, s));
+  OH_HIP(hipMemsetAsync(cnt, 0, (size_t)k * 8, s));
+  OH_HIP(hipMemsetAsync(inr, 0, 8, s));
+  const size_t lds = ((size_t)k * dim + k) * (sizeof(float) + 8);
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n, 256), (int64_t)ctx->n_cu * 4);
+  k_km_assign<<<grid, 256, lds, s>>>(X, n, dim, centroids, k, labels, sums, cnt, inr);
+  OH_HIP(hipGetLastError());
+  std::vector<unsigned long long> hs((size_t)k * dim);
+  std::vector<unsigned long long> hc(k);
+  std::vector<float> hcen((size_t)k * dim);
+  OH_TRY(d2h(hs.data(), sums, hs.size(), s));
+  OH_TRY(d2h(hc.data(), cnt, hc.size(), s));
+  OH_TRY(d2h(hcen.data(), centroids, hcen.size(), s));
+  double inertia_h = 0.0;
+  OH_TRY(d2h(&inertia_h, inr, 1, s));
+  double sh = 0.0;
+  for (int c = 0; c < k; ++c) {
+    if (hc[c] == 0) continue;
+    for (int d = 0; d < dim; ++d) {
+      const float nv = (float)((double)(long long)hs[(size_t)c * dim + d] / KM_FX / (double)hc[c]);
+      const double df = (double)nv - (double)hcen[(size_t)c * dim + d];
+      sh += df * df;
+      hcen[(size_t)c * dim + d] = nv;
+    }
+  }
+  OH_HIP(hipMemcpyAsync(centroids, hcen.data(), hcen.size() * sizeof(float), hipMemcpyHostToDevice, s));
+  OH_HIP(hipStreamSynchronize(s));
+  if (shift2) *shift2 = sh;
+  if (inertia) *inertia = inertia_h;
+  return 0;
+}
+
+// labels only (final assignment after the last update, as sklearn's labels_)
+int ottohip_kmeans_assign(ottohip_ctx* ctx, const float* X, int64_t n, int dim, const float* centroids, int k,
+                          int32_t* labels, double* inertia, void* stream) {
+  if (!ctx || !X || !centroids || !labels || n < 1 || dim < 1 || dim > EMB_MAXD || k < 1 || k > KM_MAXK) {
+    set_error("kmeans_assign: bad arguments"); return OTTOHIP_EINVAL;
+  }
+  if (((size_t)k * dim + k) * (sizeof(float) + 8) > 65536) { set_error("kmeans_assign: k * dim too large for LDS"); return OTTOHIP_ELIMIT; }
+  hipStream_t s = S(stream);
+  double* inr;
+  OH_TRY(ctx->ws.get("km_inertia", 1, &inr));
+  OH_HIP(hipMemsetAsync(inr, 0, 8, s));
+  const size_t lds = ((size_t)k * dim + k) * (sizeof(float) + 8);
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n, 256), (int64_t)ctx->n_cu * 4);
+  k_km_assign<<<grid, 256, lds, s>>>(X, n, dim, centroids, k, labels, nullptr, nullptr, inr);
+  OH_HIP(hipGetLastError());
+  double h = 0.0;
+  OH_TRY(d2h(&h, inr, 1, s));
+  if (inertia) *inertia = h;
+  return 0;
+}
+
+struct ottohip_pop {
+  int64_t n = 0;
+  int32_t* aid = nullptr;
+  int32_t* cl = nullptr;
+  int16_t* rank = nullptr;  // [n][6]
+};
+
+int ottohip_popularity_ranks(ottohip_ctx* ctx, const int64_t* session_offsets, int64_t n_sessions,
+                             const int32_t* aid, const int32_t* ts, const int8_t* type, const int32_t* session_cl,
+                             int32_t n_items, int32_t n_clusters, int32_t ts_7d, int keep_top_k,
+                             ottohip_pop** out, int64_t* n_out, void* stream) {
+  if (!ctx || !out || !n_out || n_sessions < 0 || n_items < 1 || n_clusters < 1 ||
+      (n_sessions > 0 && (!session_offsets || !aid || !ts || !type || !session_cl))) {
+    set_error("popularity_ranks: bad arguments"); return OTTOHIP_EINVAL;
+  }
+  const int64_t NS = (int64_t)n_clusters * n_items;
+  if (NS >= ((int64_t)1 << 32)) { set_error("popularity_ranks: n_clusters * n_items >= 2^32"); return OTTOHIP_ELIMIT; }
+  *out = nullptr;
+  *n_out = 0;
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  Workspace& ws = ctx->ws;
+  uint32_t *cnt, *present;
+  uint64_t *pidx, *tot;
+  int* err;
+  OH_TRY(ws.get("pop_cnt", (size_t)NS * 6, &cnt));
+  OH_TRY(ws.get("pop_present", (size_t)NS, &present));
+  OH_TRY(ws.get("pop_pidx", (size_t)NS, &pidx));
+  OH_TRY(ws.get("pop_tot", 2, &tot));
+  OH_TRY(ws.get("pop_err", 1, &err));
+  int ph = ctx->begin("pop_ranks", s, 0);
+  OH_HIP(hipMemsetAsync(cnt, 0, (size_t)NS * 6 * 4, s));
+  OH_HIP(hipMemsetAsync(present, 0, (size_t)NS * 4, s));
+  OH_HIP(hipMemsetAsync(err, 0, sizeof(int), s));
+  if (n_sessions > 0)
+    k_pop_count<<<(unsigned)ceil_div(n_sessions, 4), 256, 0, s>>>(session_offsets, n_sessions, aid, ts, type, session_cl,
+                                                                   n_items, n_clusters, ts_7d, cnt, present, err);
+  OH_TRY(exclusive_scan_u32(ctx, present, pidx, NS, tot, s));
+  uint64_t np_ = 0;
+  int herr = 0;
+  OH_TRY(d2h(&np_, tot, 1, s));
+  OH_TRY(d2h(&herr, err, 1, s));
+  if (herr) { set_error("popularity_ranks: cluster, aid or type out of range"); return OTTOHIP_ERANGE; }
+  ottohip_pop* P = new ottohip_pop();
+  const int64_t n = (int64_t)np_;
+  if (n == 0) { *out = P; return 0; }
+  uint32_t *slot, *k0, *v0, *k1, *v1, *hist, *keep;
+  uint16_t* rank;
+  uint64_t *cl_first, *oidx;
+  auto fail = [&](int rc) { delete P; return rc; };
+  int rc;
+  if ((rc = ws.get("pop_slot", (size_t)n, &slot)) || (rc = ws.get("pop_k0", (size_t)n, &k0)) ||
+      (rc = ws.get("pop_v0", (size_t)n, &v0)) || (rc = ws.get("pop_k1", (size_t)n, &k1)) ||
+      (rc = ws.get("pop_v1", (size_t)n, &v1)) || (rc = ws.get("pop_rank", (size_t)n * 6, &rank)) ||
+      (rc = ws.get("pop_hist", (size_t)n_clusters + 1, &hist)) || (rc = ws.get("pop_clf", (size_t)n_clusters + 1, &cl_first)) ||
+      (rc = ws.get("pop_keep", (size_t)n, &keep)) || (rc = ws.get("pop_oidx", (size_t)n, &oidx)))
+    return fail(rc);
+  k_pop_pairs<<<grid_for(NS), 256, 0, s>>>(present, pidx, NS, slot);
+  hipMemsetAsync(hist, 0, ((size_t)n_clusters + 1) * 4, s);
+  k_pop_cluster_hist<<<grid_for(n), 256, 0, s>>>(slot, n, n_items, hist);
+  if ((rc = exclusive_scan_u32(ctx, hist, cl_first, (int64_t)n_clusters + 1, nullptr, s))) return fail(rc);
+  const int cbits = std::max(1, bits_for((uint64_t)n_clusters));
+  for (int t = 0; t < 6; ++t) {
+    const uint32_t* c = cnt + (size_t)t * NS;
+    uint32_t *k = k0, *v = v0;
+    // pairs are in (cluster, aid) order, so aid asc is the stable base: sort by count desc, then cluster
+    k_pop_key<<<grid_for(n), 256, 0, s>>>(slot, nullptr, n, c, n_items, 1, k);
+    k_pop_iota<<<grid_for(n), 256, 0, s>>>(v, n);
+    if ((rc = radix_sort_pairs(ctx, k, v, k1, v1, n, 32, s))) return fail(rc);
+    uint32_t* kn = (k == k0) ? k1 : k0;
+    k_pop_key<<<grid_for(n), 256, 0, s>>>(slot, v, n, c, n_items, 2, kn);
+    k = kn;
+    if ((rc = radix_sort_pairs(ctx, k, v, k == k0 ? k1 : k0, v == v0 ? v1 : v0, n, cbits, s))) return fail(rc);
+    k_pop_rank<<<grid_for(n), 256, 0, s>>>(slot, v, n, n_items, cl_first, rank + (size_t)t * n);
+  }
+  k_pop_keep<<<grid_for(n), 256, 0, s>>>(rank, n, keep_top_k, keep);
+  if ((rc = exclusive_scan_u32(ctx, keep, oidx, n, tot + 1, s))) return fail(rc);
+  uint64_t nk = 0;
+  if ((rc = d2h(&nk, tot + 1, 1, s))) return fail(rc);
+  P->n = (int64_t)nk;
+  if (hipMalloc(&P->aid, std::max<uint64_t>(nk, 1) * 4) || hipMalloc(&P->cl, std::max<uint64_t>(nk, 1) * 4) ||
+      hipMalloc(&P->rank, std::max<uint64_t>(nk, 1) * 12)) {
+    (void)hipGetLastError();
+    return fail(OTTOHIP_ENOMEM);
+  }
+  k_pop_out<<<grid_for(n), 256, 0, s>>>(slot, rank, keep, oidx, n, n_items, P->aid, P->cl, P->rank);
+  OH_HIP(hipGetLastError());
+  ctx->end(ph, s);
+  *out = P;
+  *n_out = P->n;
+  return 0;
+}
+
+int ottohip_pop_copy(const ottohip_pop* p, int32_t* aid, int32_t* cl, int16_t* ranks6, void* stream) {
+  if (!p) { set_error("pop_copy: NULL"); return OTTOHIP_EINVAL; }
+  if (p->n == 0) return 0;
+  hipStream_t s = S(stream);
+  if (aid) OH_HIP(hipMemcpyAsync(aid, p->aid, p->n * 4, hipMemcpyDeviceToDevice, s));
+  if (cl) OH_HIP(hipMemcpyAsync(cl, p->cl, p->n * 4, hipMemcpyDeviceToDevice, s));
+  if (ranks6) OH_HIP(hipMemcpyAsync(ranks6, p->rank, p->n * 12, hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
+void ottohip_pop_free(ottohip_pop* p) {
+  if (!p) return;
+  (void)hipDeviceSynchronize();
+  if (p->aid) (void)hipFree(p->aid);
+  if (p->cl) (void)hipFree(p->cl);
+  if (p->rank) (void)hipFree(p->rank);
+  delete p;
+}
+
+int ottohip_session_item_similarity(ottohip_ctx* ctx, const int64_t* cand_off, int64_t n_sessions,
+                                    const int32_t* aid_next, const float* sess_emb, const uint8_t* sess_has,
+                                    const int32_t* row_of_aid, int32_t n_aid_map, const float* emb, int dim,
+                                    float* cos_out, float* eucl_out, void* stream) {
+  if (!ctx || n_sessions < 0 || dim < 1 || (n_sessions > 0 && (!cand_off || !sess_emb || !row_of_aid || !emb ||
+      !cos_out || !eucl_out))) {
+    set_error("session_item_similarity: bad arguments"); return OTTOHIP_EINVAL;
+  }
+  if (n_sessions == 0) return 0;
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  int ph = ctx->begin("r7_sim", s, 0);
+  k_sim<<<(unsigned)ceil_div(n_sessions, 4), 256, 0, s>>>(cand_off, n_sessions, aid_next, sess_emb, sess_has,
+                                                          row_of_aid, n_aid_map, emb, dim, cos_out, eucl_out);
+  OH_HIP(hipGetLastError());
+  ctx->end(ph, s);
+  return 0;
+}
+
+}  // extern "C"
