@@ -97,6 +97,38 @@ def bench_knn(steps: int, warmup: int, n_items: int, n_q: int, with_cpu: bool) -
     return out
 
 
+def bench_candidates(n_sessions: int, steps: int, kmeans_iter: int) -> dict:
+    """BASELINE configs[4]: end-to-end candidate generation (co-visit + W2V kNN + pop-cluster) for
+    the test split of n_sessions synthetic sessions, 1 GPU; value = candidate rows / s."""
+    import torch
+    import otto_recommender_amd.synth as synth
+    from otto_recommender_amd import pipeline, config as cfg
+    ev = synth.generate(n_sessions)
+    train, test, labels = synth.split_test_labels(ev)
+    del ev
+    words = synth.item_words()
+    emb_all = synth.embeddings(len(words), seed=1)
+    emb_12 = synth.embeddings(len(words), seed=3)
+    res, dts = None, []
+    for _ in range(max(steps, 1)):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        T = {}
+        res = pipeline.run(train, test, labels, words, emb_all, words, emb_12, kmeans_iter=kmeans_iter, timings=T)
+        torch.cuda.synchronize()
+        dts.append(time.perf_counter() - t0)
+    dt = min(dts)
+    return {"metric": "candidates/sec, end-to-end candidate generation (co-visit + W2V kNN + pop-cluster)",
+            "value": res["candidates"] / dt, "unit": "candidates/s", "ms_per_step": dt * 1e3,
+            "config": {"workload": "configs[4] on 1 GPU: train + truncated test split of synthetic sessions",
+                       "sessions": n_sessions, "test_sessions": res["test_sessions"], "candidates": res["candidates"],
+                       "co_visit_pairs": res["pairs"], "kmeans_iter": res["kmeans_iter"]},
+            "recall@20": {k: round(v["top20"], 6) for k, v in res["recall"].items()},
+            "recall_topall": {k: round(v["topall"], 6) for k, v in res["recall"].items()},
+            "stages_s": {k: round(v, 4) for k, v in res["timings_s"].items()},
+            "data": "synthetic (otto-synth seed 0, embeddings seeds 1/3, labels by the OTTO protocol)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -107,8 +139,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--knn-steps", type=int, default=2, help="0 disables the configs[2] kNN measurement")
-    ap.add_argument("--workload", choices=["covis", "knn"], default="covis",
-                    help="covis: configs[1] line (+ the kNN sub-object); knn: only configs[2]")
+    ap.add_argument("--workload", choices=["covis", "knn", "candidates"], default="covis",
+                    help="covis: configs[1] line (+ the kNN sub-object); knn: only configs[2]; "
+                         "candidates: configs[4] end-to-end on 1 GPU")
+    ap.add_argument("--cand-sessions", type=int, default=12_900_000)
+    ap.add_argument("--kmeans-iter", type=int, default=100)
     ap.add_argument("--knn-items", type=int, default=1_855_603)
     ap.add_argument("--knn-queries", type=int, default=600_000)
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
@@ -121,6 +156,10 @@ def main():
     from otto_recommender_amd import covis as gc
     from otto_recommender_amd import _lib
 
+    if args.workload == "candidates":
+        torch.cuda.set_device(0)
+        print(json.dumps(bench_candidates(args.cand_sessions, args.steps, args.kmeans_iter)))
+        return
     if args.workload == "knn":
         torch.cuda.set_device(0)
         print(json.dumps(bench_knn(max(args.knn_steps, 1), 1, args.knn_items, args.knn_queries, not args.no_cpu)))

@@ -1,0 +1,103 @@
+"""Config-5 end-to-end candidate generation (BASELINE.json configs[4]) on the device:
+
+  co-visitation over train + test (count_co_events_fused)  -> finalize (A6) -> R1 top-N lists
+  Word2Vec kNN of both models (first 600k vocabulary rows)   -> B3 lists
+  session embeddings (C1) -> KMeans k=50 (C2) -> popularity ranks cl50 / cl1 (C3)
+  candidates for the test sessions (R3-R6) -> recall@20 (R9)
+
+Mirrors the order of the reference's scripts (model/count_co_events.py, model/w2vec_aids.py,
+model/kmeans_sessions.py, model/count_popularity.py, model/retrieve.py, model/eval_retrieved.py)
+with every stage on the GPU; tables stay resident in HBM between stages.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+
+from . import _lib, config
+from . import covis as gc
+from . import retrieve as gr
+from . import candidates as gcand
+from . import popularity as gp
+from .w2vec import KnnIndex
+
+
+def _concat(parts):
+    from .synth import Events
+    offs, base = [np.zeros(1, np.int64)], 0
+    for p in parts:
+        o = p.session_offsets - p.session_offsets[0]
+        offs.append(o[1:] + base)
+        base += int(o[-1])
+    cat = lambda k: np.concatenate([getattr(p, k) for p in parts])
+    return Events(np.concatenate(offs), cat("session"), cat("aid"), cat("ts"), cat("type"))
+
+
+def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int = config.N_ITEMS_OTTO,
+        n_clusters: int = 50, kmeans_iter: int = 100, knn_queries: int = config.W2VEC_SEARCH_SIMILAR_FOR_FIRST_N_AIDS,
+        ctx=None, timings: dict | None = None) -> dict:
+    import torch
+    from .synth import file_session_bounds
+    ctx = ctx or _lib.context()
+    dev = torch.device("cuda", ctx.device)
+    T = timings if timings is not None else {}
+
+    def mark(name, t0):
+        torch.cuda.synchronize()
+        T[name] = T.get(name, 0.0) + time.perf_counter() - t0
+        return time.perf_counter()
+
+    t = time.perf_counter()
+    # ---- co-visitation over train + test files (model/count_co_events.py:201-226)
+    allev = _concat([train, test])
+    fb = np.concatenate([file_session_bounds(train.n_sessions),
+                         file_session_bounds(test.n_sessions)[1:] + train.n_sessions])
+    dev_all = gc.DeviceEvents.from_host(allev, fb)
+    tab = gc.count_co_events_fused(dev_all, n_items=n_items, ctx=ctx)
+    pairs = sum(tab.stats(n)["n_pairs"] for n in tab.names)
+    r1 = {}
+    for n in tab.names:
+        a, b, c = tab.finalize(n)
+        r = gr.topk_per_aid(a, b, c, config.RETRIEVAL_FIRST_N_CO_COUNTS[n], n_items=n_items, ctx=ctx)
+        r1[n] = (r["aid"], r["aid_next"], r["rank"])
+    tab.free()
+    t = mark("covis+R1", t)
+    # ---- kNN of both Word2Vec models (model/retrieve.py:683-687)
+    knn = []
+    for words, emb in ((words_all, emb_all), (words_12, emb_12)):
+        idx = KnnIndex(emb, ctx)
+        nq = min(knn_queries, idx.n_items)
+        i, _ = idx.search(None, n_q=nq, k=config.W2VEC_K)
+        w = torch.as_tensor(np.asarray(words, np.int32)).to(dev)
+        valid = i >= 0
+        q_aid = w[:nq].view(nq, 1).expand(nq, config.W2VEC_K)[valid]
+        nb = w[i.clamp(min=0).long()][valid]
+        rk = torch.arange(1, config.W2VEC_K + 1, device=dev, dtype=torch.int16).view(1, -1).expand(nq, -1)[valid]
+        knn.append((q_aid.contiguous(), nb.contiguous(), rk.contiguous()))
+        idx.free()
+    t = mark("knn", t)
+    # ---- pop-cluster source: C1 embeddings of all sessions, C2 KMeans, C3 ranks (cl50 and cl1)
+    se = gp.compute_sessions_embeddings(allev.session_offsets, allev.aid, allev.ts, allev.type, words_all, emb_all,
+                                        n_items, ctx)
+    km = gp.KMeans(n_clusters=n_clusters, max_iter=kmeans_iter).fit(se, ctx)
+    labels_all = km.labels_
+    pop50 = gp.count_popularity(allev.session_offsets, allev.aid, allev.ts, allev.type, labels_all, n_clusters,
+                                n_items, ctx=ctx)
+    t = mark("pop_cluster", t)
+    # ---- candidates for the test sessions + recall
+    rk_cols = [c for c in pop50.columns if c.startswith("rank_")]
+    p = pop50[pop50[rk_cols].min(axis=1) <= 20]
+    src = gcand.CandidateSources(r1, knn[0], knn[1], (p["cl50"].to_numpy(), p["aid"].to_numpy()), n_clusters,
+                                 n_items, ctx)
+    test_cl = labels_all[train.n_sessions:]
+    cands = gcand.generate(test.session_offsets, test.aid, test.ts, test.type, src, test_cl)
+    t = mark("candidates", t)
+    sess = test.session[test.session_offsets[:-1] - test.session_offsets[0]]
+    lo, la = gcand.labels_csr(labels, sess)
+    rec = cands.recall(lo, la)
+    t = mark("recall", t)
+    out = {"pairs": int(pairs), "candidates": cands.n_cand, "test_sessions": int(test.n_sessions),
+           "kmeans_iter": km.n_iter_, "recall": rec, "timings_s": T}
+    cands.free()
+    return out

@@ -223,3 +223,48 @@ def events_from_columns(sess, aid, ts, ty) -> Events:
         starts = np.zeros(1, np.int64)
     return Events(starts, sess, np.asarray(aid, np.int32), np.asarray(ts, np.int32),
                   np.asarray(ty, np.int8), int(sess[0]) if len(sess) else 0)
+
+
+def _mix(x: np.ndarray) -> np.ndarray:
+    """splitmix64 finaliser on uint64 arrays (counter-based draws for the test split)."""
+    x = x.astype(np.uint64)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def split_test_labels(ev: Events, test_days: int = 7, seed: int = 2):
+    """Config 5: sessions starting in the last `test_days` days become test
+    sessions, truncated at a uniform cut in [1, n-1]; labels follow the OTTO protocol: the next
+    click after the cut, and every cart / order after it (unique aids per type).
+    Returns (train Events, test Events, labels DataFrame[session, aid, type])."""
+    import pandas as pd
+    off = ev.session_offsets - ev.session_offsets[0]
+    lens = np.diff(off)
+    start = ev.ts[off[:-1]]
+    t_split = int(start.max()) - test_days * 24 * 3600  # the last week of session starts
+    sid = ev.session[off[:-1]].astype(np.int64)
+    is_test = (start >= t_split) & (lens >= 2)
+    u = (_mix(sid.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(seed)) >> np.uint64(11)).astype(np.float64)
+    u /= float(1 << 53)
+    cut = np.where(is_test, 1 + np.floor(u * (lens - 1)).astype(np.int64), lens)  # events kept per session
+    pos = np.arange(len(ev.aid)) - np.repeat(off[:-1], lens)
+    keep_ev = pos < np.repeat(cut, lens)
+    test_ev = np.repeat(is_test, lens)
+    tr, te = keep_ev & ~test_ev, keep_ev & test_ev
+    lab_ev = ~keep_ev
+
+    def sub(mask, sess_mask):
+        l2 = np.where(sess_mask, np.add.reduceat(mask.astype(np.int64), off[:-1]) if len(off) > 1 else 0, 0)
+        l2 = l2[sess_mask]
+        o = np.zeros(len(l2) + 1, np.int64)
+        np.cumsum(l2, out=o[1:])
+        return Events(o, ev.session[mask], ev.aid[mask], ev.ts[mask], ev.type[mask])
+
+    train, test = sub(tr, ~is_test), sub(te, is_test)
+    ls, la, lt = ev.session[lab_ev], ev.aid[lab_ev], ev.type[lab_ev]
+    df = pd.DataFrame({"session": ls, "aid": la, "type": lt.astype(np.int8), "ts": ev.ts[lab_ev]})
+    clicks = df[df["type"] == 0].sort_values(["session", "ts"], kind="stable").drop_duplicates("session")
+    rest = df[df["type"] > 0].drop_duplicates(["session", "aid", "type"])
+    labels = pd.concat([clicks, rest])[["session", "aid", "type"]].sort_values(["session", "type", "aid"])
+    return train, test, labels.reset_index(drop=True)
