@@ -145,19 +145,23 @@ def concat_files_w_stats(name: str, parts: list, loaded_from_cache: bool = False
                          max_rows_groupby: int = MAX_ROWS_POLARS_GROUPBY,
                          optim_rows: int = OPTIM_ROWS_POLARS_GROUPBY,
                          max_pairs: int = MAX_CO_EVENT_PAIRS_TO_SAVE_DISK,
-                         click_filter_rows: int = 100_000_000):
-    """Restates model/count_co_events.py:103-181 on in-memory parts [(aid, aid_next, count)...]
-    concatenated in the given order. Branch (2) slices in concat order; the reference's
-    nondeterminism there (polars groupby row order) is replaced by the deterministic
-    (count desc, aid, aid_next) order. Returns (aid:int32, aid_next:int32, count:int32)."""
-    a = np.concatenate([p[0] for p in parts]).astype(np.int32) if parts else np.zeros(0, np.int32)
-    b = np.concatenate([p[1] for p in parts]).astype(np.int32) if parts else np.zeros(0, np.int32)
-    c = np.concatenate([p[2] for p in parts]).astype(np.int64) if parts else np.zeros(0, np.int64)
+                         click_filter_rows: int = 100_000_000, part_mode: str = "rows"):
+    """Restates model/count_co_events.py:103-181 on in-memory per-file tables
+    [(aid, aid_next, count)...] concatenated in the given order. Branch (2) slices in concat
+    order; the reference's nondeterminism there (polars groupby row order) is replaced by the
+    deterministic (count desc, aid, aid_next) order. part_mode="files" cuts branch (2)'s parts
+    at whole-file boundaries instead (file p*nf//n_parts starts part p), the device path's
+    definition (covis.concat_files_w_stats_fused). Returns (aid:int32, aid_next:int32, count:int32)."""
+    nf = len(parts)
+    cat = lambda k, dt, sel: (np.concatenate([parts[f][k] for f in sel]).astype(dt) if len(sel)
+                              else np.zeros(0, dt))
+    a, b, c = cat(0, np.int32, range(nf)), cat(1, np.int32, range(nf)), cat(2, np.int64, range(nf))
+    fid = np.concatenate([np.full(len(parts[f][0]), f, np.int64) for f in range(nf)]) if nf else np.zeros(0, np.int64)
     n = len(a)
     # :131-132 lossy per-part filter for click_to tables
     if "click_to" in name and n > click_filter_rows and not loaded_from_cache:
         keep = c >= MIN_COUNT_IN_PART.get(name, 1)
-        a, b, c = a[keep], b[keep], c[keep]
+        a, b, c, fid = a[keep], b[keep], c[keep], fid[keep]
         n = len(a)
     # :135-166 groupby by parts
     if n > max_rows_groupby and not loaded_from_cache:
@@ -165,10 +169,14 @@ def concat_files_w_stats(name: str, parts: list, loaded_from_cache: bool = False
         n_parts = math.ceil(n / rows_part)
         max_rows_part = int(max_rows_groupby / n * rows_part)
         rows_part = math.ceil(n / n_parts)
+        if part_mode == "files":
+            bnd = [(p * nf) // n_parts for p in range(n_parts + 1)]
+            sel = [(fid >= bnd[i]) & (fid < bnd[i + 1]) for i in range(n_parts)]
+        else:
+            sel = [slice(i * rows_part, (i + 1) * rows_part) for i in range(n_parts)]
         pa, pb, pc = [], [], []
-        for i in range(n_parts):
-            sa, sb, sc = _groupby_sum(a[i * rows_part:(i + 1) * rows_part], b[i * rows_part:(i + 1) * rows_part],
-                                      c[i * rows_part:(i + 1) * rows_part])
+        for m in sel:
+            sa, sb, sc = _groupby_sum(a[m], b[m], c[m])
             keep = sc >= MIN_COUNT_IN_PART.get(name, 1)
             sa, sb, sc = _sort_count_desc(sa[keep], sb[keep], sc[keep])
             pa.append(sa[:max_rows_part]); pb.append(sb[:max_rows_part]); pc.append(sc[:max_rows_part])

@@ -55,6 +55,14 @@ class DeviceEvents:
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=False)
         return DeviceEvents(t(off), t(ev.aid), t(ev.ts), t(ev.type), file_bounds, ev.n_sessions, ev.n_events)
 
+    def subset_files(self, f0: int, f1: int) -> "DeviceEvents":
+        """Files [f0, f1) as a device view (offsets rebased; event columns are views)."""
+        s0, s1 = int(self.file_bounds[f0]), int(self.file_bounds[f1])
+        off = self.offsets[s0:s1 + 1]
+        e0, e1 = int(off[0].item()), int(off[-1].item())
+        return DeviceEvents((off - e0).contiguous(), self.aid[e0:e1], self.ts[e0:e1], self.type[e0:e1],
+                            self.file_bounds[f0:f1 + 1] - self.file_bounds[f0], s1 - s0, e1 - e0)
+
     def abi(self) -> _lib.Events:
         e = _lib.Events()
         e.session_offsets = _lib.ptr(self.offsets)
@@ -115,9 +123,13 @@ class CovisTable:
             a, b, c, c2 = a[o], b[o], c[o], c2[o]
         return a, b, c, c2
 
-    def finalize(self, name, stream=None, max_rows=None):
+    def finalize(self, name, stream=None, max_rows=None, params: dict | None = None):
         """concat_files_w_stats' final step (:131-175) on the device for one rule:
-        returns torch (aid, aid_next, count:int32) in (count desc, aid, aid_next) order."""
+        returns torch (aid, aid_next, count:int32) in (count desc, aid, aid_next) order.
+        params overrides ottohip_merge_params fields (click_rule, min_count, max_rows,
+        filter_rows, max_rows_groupby); the default is the reference's configuration. Raises
+        OttoHipError(ELIMIT) where the reference takes its part-wise branch (:135-166): use
+        concat_files_w_stats_fused for that case."""
         import torch
         rname = self.names[self._rule(name)]
         mp = _lib.MergeParams()
@@ -127,6 +139,8 @@ class CovisTable:
         mp.max_rows = config.MAX_CO_EVENT_PAIRS_TO_SAVE_DISK if max_rows is None else int(max_rows)
         mp.filter_rows = config.CLICK_FILTER_ROWS
         mp.max_rows_groupby = config.MAX_ROWS_POLARS_GROUPBY
+        for k, v in (params or {}).items():
+            setattr(mp, k, int(v))
         n = min(self.stats(name)["n_rows"], mp.max_rows)
         dev = torch.device("cuda", self.ctx.device)
         a = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
@@ -153,6 +167,59 @@ def count_co_events_fused(events: DeviceEvents, names=None, n_items: int = confi
     _lib.check(_lib.load().ottohip_covis_count(ctx.h, ctypes.byref(ev), rules, len(names), ctypes.byref(p),
                                                ctypes.byref(h), _lib.stream_handle(stream)))
     return CovisTable(h, names, ctx)
+
+
+def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTable | None = None,
+                               n_items: int = config.N_ITEMS_OTTO, max_rows_groupby: int = config.MAX_ROWS_POLARS_GROUPBY,
+                               optim_rows: int = config.OPTIM_ROWS_POLARS_GROUPBY,
+                               max_pairs: int = config.MAX_CO_EVENT_PAIRS_TO_SAVE_DISK,
+                               click_filter_rows: int = config.CLICK_FILTER_ROWS, ctx=None):
+    """model/count_co_events.py:103-181 for one rule over the files of `events`, all branches:
+    (1) per-file count >= 2 for click_to_* tables when N > 1e8 (count_ge2), (2) when still
+    N > max_rows_groupby, part-wise groupby -> keep count >= MIN_COUNT_IN_PART -> count desc
+    -> head(int(max_rows_groupby / N * optim_rows)) per part, (3) groupby, MIN_COUNT_TO_SAVE,
+    count desc, head(max_pairs). The reference slices parts by rows in polars' (unspecified)
+    row order, which makes branch (2) nondeterministic; here a part is a
+    run of consecutive whole files, ceil(N / optim_rows) parts of equal file counts. Returns
+    torch (aid, aid_next, count:int32) in (count desc, aid, aid_next) order."""
+    import math
+    import torch
+    from . import dist as gd
+    ctx = ctx or _lib.context()
+    own = table is None
+    tab = table if table is not None else count_co_events_fused(events, [name], n_items=n_items, ctx=ctx)
+    st = tab.stats(name)
+    use_ge2 = "click_to" in name and st["file_rows"] > click_filter_rows
+    N = st["file_rows_ge2"] if use_ge2 else st["file_rows"]
+    base = {"filter_rows": click_filter_rows, "max_rows_groupby": max_rows_groupby}
+    if N <= max_rows_groupby:
+        out = tab.finalize(name, max_rows=max_pairs, params=base)
+        if own:
+            tab.free()
+        return out
+    if own:
+        tab.free()
+    n_parts = math.ceil(N / optim_rows)
+    max_rows_part = int(max_rows_groupby / N * optim_rows)
+    nf = len(events.file_bounds) - 1
+    bounds = [(p * nf) // n_parts for p in range(n_parts + 1)]
+    part = {"click_rule": 1 if use_ge2 else 0, "filter_rows": -1, "max_rows_groupby": 1 << 62,
+            "min_count": config.MIN_COUNT_IN_PART.get(name, 1)}
+    recs = []
+    for f0, f1 in zip(bounds[:-1], bounds[1:]):
+        if f1 <= f0:
+            continue
+        t = count_co_events_fused(events.subset_files(f0, f1), [name], n_items=n_items, ctx=ctx)
+        a, b, c = t.finalize(name, max_rows=max_rows_part, params=part)
+        recs.append(torch.stack([a, b, c, torch.zeros_like(c)], 1))
+        t.free()
+    r = torch.cat(recs) if recs else torch.zeros((0, 4), dtype=torch.int32, device=events.aid.device)
+    merged = gd.table_from_records(r.contiguous(), [name], n_items, ctx=ctx)
+    out = merged.finalize(name, max_rows=max_pairs,
+                          params={"click_rule": 0, "filter_rows": -1, "max_rows_groupby": 1 << 62,
+                                  "min_count": config.MIN_COUNT_TO_SAVE.get(name, 1)})
+    merged.free()
+    return out
 
 
 def _n_items_for(aid: np.ndarray) -> int:

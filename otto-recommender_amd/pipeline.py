@@ -58,7 +58,7 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
     pairs = sum(tab.stats(n)["n_pairs"] for n in tab.names)
     r1 = {}
     for n in tab.names:
-        a, b, c = tab.finalize(n)
+        a, b, c = gc.concat_files_w_stats_fused(dev_all, n, table=tab, n_items=n_items, ctx=ctx)
         r = gr.topk_per_aid(a, b, c, config.RETRIEVAL_FIRST_N_CO_COUNTS[n], n_items=n_items, ctx=ctx)
         r1[n] = (r["aid"], r["aid_next"], r["rank"])
     tab.free()

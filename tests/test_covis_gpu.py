@@ -227,3 +227,22 @@ def test_finalize_matches_merge_restatement(gpu):
         np.testing.assert_array_equal(a, ra, err_msg=n)
         np.testing.assert_array_equal(b, rb, err_msg=n)
         np.testing.assert_array_equal(c, rc, err_msg=n)
+
+
+def test_concat_files_w_stats_part_branch(gpu):
+    """A6 branch (2) (count_co_events.py:135-166) at test scale: thresholds scaled down so the
+    click filter (1) and the part-wise groupby (2) both trigger; parts are whole-file runs
+    (oracle part_mode="files"). Bit-exact against the restatement."""
+    from otto_recommender_amd import covis as gc
+    ev = synth.generate(30_000, first_session=2024)
+    fb = synth.file_session_bounds(ev.n_sessions, per_file=3_000)
+    per_file = oracle.count_co_events_files(ev.session_offsets, ev.aid, ev.ts, ev.type, fb)
+    dev = gc.DeviceEvents.from_host(ev, fb)
+    # c2c: filter (1) + 7 parts; c2cob: 4 parts without (1); cart_to_cart: (3) only
+    kw = dict(max_rows_groupby=300_000, optim_rows=250_000, max_pairs=200_000, click_filter_rows=1_000_000)
+    for n in ("click_to_click", "click_to_cart_or_buy", "cart_to_cart"):
+        ra, rb, rc = oracle.concat_files_w_stats(n, [p[n] for p in per_file], part_mode="files", **kw)
+        a, b, c = (x.cpu().numpy() for x in gc.concat_files_w_stats_fused(dev, n, **kw))
+        np.testing.assert_array_equal(a, ra, err_msg=n)
+        np.testing.assert_array_equal(b, rb, err_msg=n)
+        np.testing.assert_array_equal(c, rc, err_msg=n)
