@@ -180,22 +180,27 @@ def generate(offsets, aid, ts, type_, sources: CandidateSources, session_cl=None
 def labels_csr(labels, session_ids):
     """labels DataFrame[session, aid, type] -> (off [3*(S+1)] int64, aid int32), unique per (session, type),
     sessions in the order of session_ids."""
-    S = len(session_ids)
-    pos = {int(s): i for i, s in enumerate(session_ids)}
-    lab = labels.drop_duplicates(["session", "aid", "type"])
-    idx = lab["session"].map(pos)
-    lab = lab[idx.notna()].assign(si=idx[idx.notna()].astype(np.int64))
-    offs, aids = [], []
-    base = 0
+    sid = np.asarray(session_ids, np.int64)
+    S = len(sid)
+    order = np.argsort(sid, kind="stable")
+    ss = sid[order]
+    ls = labels["session"].to_numpy().astype(np.int64)
+    la = labels["aid"].to_numpy().astype(np.int64)
+    lt = labels["type"].to_numpy().astype(np.int64)
+    j = np.searchsorted(ss, ls)
+    ok = (j < S) & (ss[np.minimum(j, S - 1)] == ls) & (lt >= 0) & (lt <= 2)
+    si = order[np.minimum(j, S - 1)][ok]
+    la, lt = la[ok], lt[ok]
+    key = (lt << 60) | (si << 32) | la  # type, session index, aid (aid < 2^31 checked by the device ABI)
+    key = np.unique(key)
+    t_, s_, a_ = key >> 60, (key >> 32) & ((1 << 28) - 1), key & 0xFFFFFFFF
+    offs = []
     for t in range(3):
-        d = lab[lab["type"] == t].sort_values(["si", "aid"], kind="stable")
-        cnt = np.bincount(d["si"].to_numpy(), minlength=S)
+        cnt = np.bincount(s_[t_ == t], minlength=S)
         o = np.zeros(S + 1, np.int64)
         np.cumsum(cnt, out=o[1:])
-        offs.append(o + base)
-        aids.append(d["aid"].to_numpy().astype(np.int32))
-        base += len(d)
-    return np.concatenate(offs), np.concatenate(aids) if aids else np.zeros(0, np.int32)
+        offs.append(o + int((t_ < t).sum()))
+    return np.concatenate(offs), a_.astype(np.int32)
 
 
 def retrieve_candidates(df_sessions_aids_full, aid_pairs_co_events: dict, df_knns_w2vec_all, df_knns_w2vec_1_2,

@@ -54,15 +54,18 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
     fb = np.concatenate([file_session_bounds(train.n_sessions),
                          file_session_bounds(test.n_sessions)[1:] + train.n_sessions])
     dev_all = gc.DeviceEvents.from_host(allev, fb)
+    t = mark("upload", t)
     tab = gc.count_co_events_fused(dev_all, n_items=n_items, ctx=ctx)
     pairs = sum(tab.stats(n)["n_pairs"] for n in tab.names)
+    t = mark("covis_count", t)
     r1 = {}
     for n in tab.names:
         a, b, c = gc.concat_files_w_stats_fused(dev_all, n, table=tab, n_items=n_items, ctx=ctx)
+        t = mark(f"merge_{n}", t)
         r = gr.topk_per_aid(a, b, c, config.RETRIEVAL_FIRST_N_CO_COUNTS[n], n_items=n_items, ctx=ctx)
         r1[n] = (r["aid"], r["aid_next"], r["rank"])
+        t = mark("R1", t)
     tab.free()
-    t = mark("covis+R1", t)
     # ---- kNN of both Word2Vec models (model/retrieve.py:683-687)
     knn = []
     for words, emb in ((words_all, emb_all), (words_12, emb_12)):
@@ -78,23 +81,28 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
         idx.free()
     t = mark("knn", t)
     # ---- pop-cluster source: C1 embeddings of all sessions, C2 KMeans, C3 ranks (cl50 and cl1)
-    se = gp.compute_sessions_embeddings(allev.session_offsets, allev.aid, allev.ts, allev.type, words_all, emb_all,
+    se = gp.compute_sessions_embeddings(dev_all.offsets, dev_all.aid, dev_all.ts, dev_all.type, words_all, emb_all,
                                         n_items, ctx)
+    t = mark("C1_embeddings", t)
     km = gp.KMeans(n_clusters=n_clusters, max_iter=kmeans_iter).fit(se, ctx)
     labels_all = km.labels_
-    pop50 = gp.count_popularity(allev.session_offsets, allev.aid, allev.ts, allev.type, labels_all, n_clusters,
+    t = mark("C2_kmeans", t)
+    pop50 = gp.count_popularity(dev_all.offsets, dev_all.aid, dev_all.ts, dev_all.type, labels_all, n_clusters,
                                 n_items, ctx=ctx)
-    t = mark("pop_cluster", t)
+    t = mark("C3_popularity", t)
     # ---- candidates for the test sessions + recall
     rk_cols = [c for c in pop50.columns if c.startswith("rank_")]
     p = pop50[pop50[rk_cols].min(axis=1) <= 20]
     src = gcand.CandidateSources(r1, knn[0], knn[1], (p["cl50"].to_numpy(), p["aid"].to_numpy()), n_clusters,
                                  n_items, ctx)
+    t = mark("sources", t)
     test_cl = labels_all[train.n_sessions:]
-    cands = gcand.generate(test.session_offsets, test.aid, test.ts, test.type, src, test_cl)
+    dev_test = dev_all.subset_files(len(fb) - 1 - (len(file_session_bounds(test.n_sessions)) - 1), len(fb) - 1)
+    cands = gcand.generate(dev_test.offsets, dev_test.aid, dev_test.ts, dev_test.type, src, test_cl)
     t = mark("candidates", t)
     sess = test.session[test.session_offsets[:-1] - test.session_offsets[0]]
     lo, la = gcand.labels_csr(labels, sess)
+    t = mark("labels_csr", t)
     rec = cands.recall(lo, la)
     t = mark("recall", t)
     out = {"pairs": int(pairs), "candidates": cands.n_cand, "test_sessions": int(test.n_sessions),
