@@ -25,4 +25,5 @@ def test_pipeline_small(gpu):
             assert 0.0 <= res["recall"][t][k] <= 1.0
         assert res["recall"][t]["top20"] <= res["recall"][t]["top100"] <= res["recall"][t]["topall"]
     assert res["recall"]["total"]["topall"] > 0.1  # self + co-visit candidates recover revisits
-    assert set(T) == {"covis+R1", "knn", "pop_cluster", "candidates", "recall"}
+    for stage in ("covis_count", "R1", "knn", "C1_embeddings", "C2_kmeans", "C3_popularity", "candidates", "recall"):
+        assert stage in T, stage
