@@ -85,16 +85,32 @@ __global__ __launch_bounds__(256) void k_km_assign(const float* __restrict__ X, 
     float xn = 0.f;
     float best = INFINITY;
     int bc = 0;
-    // |x - c|^2 = |x|^2 - 2 x.c + |c|^2; dims streamed once, all k dot products accumulated
+    // |x - c|^2 = |x|^2 - 2 x.c + |c|^2; the row is streamed once (16-B loads), all k dots accumulated
     float dot[KM_MAXK];
 #pragma unroll
     for (int c = 0; c < KM_MAXK; ++c) dot[c] = 0.f;
-    for (int d = 0; d < dim; ++d) {
-      const float xv = x[d];
-      xn += xv * xv;
+    if ((dim & 3) == 0) {
+      const float4* x4 = reinterpret_cast<const float4*>(x);
+      for (int d4 = 0; d4 < (dim >> 2); ++d4) {
+        const float4 v = x4[d4];
+        const float xs[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int c = 0; c < KM_MAXK; ++c)
-        if (c < k) dot[c] += xv * Cs[c * dim + d];
+        for (int u = 0; u < 4; ++u) {
+          const int d = 4 * d4 + u;
+          xn += xs[u] * xs[u];
+#pragma unroll
+          for (int c = 0; c < KM_MAXK; ++c)
+            if (c < k) dot[c] += xs[u] * Cs[c * dim + d];
+        }
+      }
+    } else {
+      for (int d = 0; d < dim; ++d) {
+        const float xv = x[d];
+        xn += xv * xv;
+#pragma unroll
+        for (int c = 0; c < KM_MAXK; ++c)
+          if (c < k) dot[c] += xv * Cs[c * dim + d];
+      }
     }
 #pragma unroll
     for (int c = 0; c < KM_MAXK; ++c) {
@@ -107,7 +123,7 @@ __global__ __launch_bounds__(256) void k_km_assign(const float* __restrict__ X, 
     part += (double)fmaxf(best, 0.f);
     if (sums) {
       for (int d = 0; d < dim; ++d)
-        atomicAdd(&ls[bc * dim + d], (unsigned long long)(long long)llrint((double)x[d] * KM_FX));
+        atomicAdd(&ls[bc * dim + d], (unsigned long long)__float2ll_rn(x[d] * 16777216.0f));  // exact 2^24 scaling
       atomicAdd(&lc[bc], 1ull);
     }
   }
