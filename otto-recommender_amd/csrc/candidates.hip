@@ -22,7 +22,6 @@ namespace ottohip {
 
 constexpr int CS_MAXE = 512;      // events per session handled by k_cand_aids
 constexpr int CS_SRC = 7;         // 5 co-count lists + 2 kNN lists
-constexpr int CS_MINI = 256;      // per-aid merge slots (>= 2 x the longest per-aid list total)
 constexpr int CS_NLAST = 99;      // RETRIEVE_N_LAST_* / RETRIEVE_N_MOST_FREQUENT (config.py:76-79)
 constexpr uint32_t CS_EMPTY = 0xFFFFFFFFu;
 constexpr int CS_NONE = 0x7FFFFFFF;
@@ -134,6 +133,91 @@ __global__ __launch_bounds__(64) void k_cand_aids(const int64_t* __restrict__ of
   if (l == 0) n_kept[s] = m_sh;
 }
 
+// Per-aid union of the 7 source lists (SURVEY.md §8(a) R4-R5 are pair-level: a pair (aid, aid_next)
+// carries every source that lists it and is kept if its best rank passes). One wave per aid:
+// elements (x, source bit, rank) of all lists in LDS, duplicates of x folded (OR of bits, min rank),
+// unique entries written at the aid's element offset; ucnt[a] = number of unique entries.
+constexpr int ML_MAX = 256;  // elements per aid across the 7 lists
+__global__ __launch_bounds__(256) void k_ml_build(CandLists L, const uint32_t* __restrict__ eoff,
+                                                  int32_t* __restrict__ mx, uint16_t* __restrict__ mbr,
+                                                  uint32_t* __restrict__ ucnt, int* __restrict__ err) {
+  __shared__ uint32_t ex[4][ML_MAX];
+  __shared__ uint16_t eb[4][ML_MAX];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int64_t a = (int64_t)blockIdx.x * 4 + w;
+  if (a >= L.n_items) return;
+  uint32_t beg[CS_SRC], len[CS_SRC], tot = 0;
+#pragma unroll
+  for (int q = 0; q < CS_SRC; ++q) {
+    if (L.off[q]) { beg[q] = L.off[q][a]; len[q] = L.off[q][a + 1] - beg[q]; } else { beg[q] = 0; len[q] = 0; }
+    tot += len[q];
+  }
+  if (tot > ML_MAX) { if (l == 0) { atomicOr(err, 4); ucnt[a] = 0; } return; }
+  for (uint32_t e = l; e < tot; e += 64) {
+    uint32_t j = e;
+    int q = 0;
+#pragma unroll
+    for (int z = 0; z < CS_SRC; ++z)
+      if (q == z && j >= len[z]) { j -= len[z]; q = z + 1; }
+    const int32_t* np = L.nxt[0];
+    const int16_t* rp = L.rank[0];
+    uint32_t b0 = beg[0];
+#pragma unroll
+    for (int z = 1; z < CS_SRC; ++z)
+      if (q == z) { np = L.nxt[z]; rp = L.rank[z]; b0 = beg[z]; }
+    const int r = rp[b0 + j];
+    ex[w][e] = (uint32_t)np[b0 + j];
+    eb[w][e] = (uint16_t)((2u << q) << 8 | (uint32_t)(r < 0 ? 0 : (r > 255 ? 255 : r)));
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const uint32_t o = eoff[a];
+  uint32_t base = 0;
+  for (uint32_t e0 = 0; e0 < tot; e0 += 64) {
+    const uint32_t e = e0 + l;
+    bool first = e < tot;
+    uint32_t bits = 0, rk = 255;
+    if (first) {
+      const uint32_t x = ex[w][e];
+      for (uint32_t f = 0; f < tot; ++f) {
+        if (ex[w][f] != x) continue;
+        if (f < e) { first = false; break; }
+        bits |= eb[w][f] >> 8;
+        rk = min(rk, (uint32_t)(eb[w][f] & 0xFFu));
+      }
+    }
+    const uint64_t b = __ballot(first);
+    if (first) {
+      const uint32_t k = base + (uint32_t)mbcnt(b);
+      mx[o + k] = (int32_t)ex[w][e];
+      mbr[o + k] = (uint16_t)(bits << 8 | rk);
+    }
+    base += (uint32_t)__popcll(b);
+  }
+  if (l == 0) ucnt[a] = base;
+}
+
+__global__ void k_ml_total(CandLists L, uint32_t* __restrict__ tot) {
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= L.n_items) return;
+  uint32_t t = 0;
+#pragma unroll
+  for (int q = 0; q < CS_SRC; ++q)
+    if (L.off[q]) t += L.off[q][a + 1] - L.off[q][a];
+  tot[a] = t;
+}
+
+struct MergedLists {
+  const uint32_t* eoff;   // [n_items] element offset of the aid
+  const uint32_t* ucnt;   // [n_items] unique entries
+  const int32_t* mx;
+  const uint16_t* mbr;    // source bits << 8 | min rank
+  int32_t n_items;
+  const uint32_t* pop_off;
+  const int32_t* pop_aid;
+  int32_t n_clusters;
+};
+
 __device__ __forceinline__ uint32_t cs_hash(uint32_t x, uint32_t mask) { return (x * 0x9E3779B1u >> 9) & mask; }
 
 // one wave per session (WAVES sessions per block); pass 0 counts, pass 1 writes at cand_off
@@ -142,7 +226,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
                                                           const int64_t* __restrict__ sess, int64_t n_sess,
                                                           const KeptAid* __restrict__ kept,
                                                           const uint32_t* __restrict__ n_kept,
-                                                          const int32_t* __restrict__ session_cl, CandLists L,
+                                                          const int32_t* __restrict__ session_cl, MergedLists L,
                                                           int pass, uint32_t* __restrict__ n_cand,
                                                           const uint64_t* __restrict__ cand_off,
                                                           int32_t* __restrict__ o_next, int16_t* __restrict__ o_ord,
@@ -151,7 +235,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
                                                           uint32_t* __restrict__ n_overflow) {
   __shared__ uint32_t hk[WAVES][HC], hm[WAVES][HC], ho[WAVES][HC];
   __shared__ uint64_t sk[WAVES][HC];
-  __shared__ uint32_t mk[WAVES][CS_MINI], mb[WAVES][CS_MINI], mr[WAVES][CS_MINI];
+  __shared__ uint32_t pre[WAVES][65], ka[WAVES][64], ki[WAVES][64], kl[WAVES][64];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int64_t gi = (int64_t)blockIdx.x * WAVES + w;
   if (gi >= n_sess) return;
@@ -159,8 +243,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
   uint32_t* K = hk[w];
   uint32_t* Mk = hm[w];
   uint32_t* Ord = ho[w];
+  uint32_t* PRE = pre[w];
   for (int i = l; i < HC; i += 64) { K[i] = CS_EMPTY; Mk[i] = 0; Ord[i] = 0xFFFFFFFFu; }
-  for (int i = l; i < CS_MINI; i += 64) { mk[w][i] = CS_EMPTY; mb[w][i] = 0; mr[w][i] = 0x7FFFFFFF; }
   __builtin_amdgcn_wave_barrier();
   bool full = false;
   auto insert = [&](uint32_t x, uint32_t bits, uint32_t ord) {
@@ -179,57 +263,46 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
   };
   const int64_t e0 = off[s];
   const uint32_t nk = n_kept[s];
-  for (uint32_t k = 0; k < nk; ++k) {
-    const KeptAid r = kept[e0 + k];
-    const uint32_t a = (uint32_t)r.aid;
-    const uint32_t ord = r.info & 0xFFFFu, tm = (r.info >> 16) & 7u, th = r.info >> 19;
-    uint32_t beg[CS_SRC], len[CS_SRC], tot = 1;  // element 0 = the self pair
-#pragma unroll
-    for (int q = 0; q < CS_SRC; ++q) {
-      if (L.off[q] && r.aid < L.n_items) { beg[q] = L.off[q][a]; len[q] = L.off[q][a + 1] - beg[q]; }
-      else { beg[q] = 0; len[q] = 0; }
-      tot += len[q];
+  // kept aids 64 at a time: lane k owns kept aid k of the batch; the batch's merged-list entries
+  // (+ one self entry per aid) are flattened and spread over the lanes
+  for (uint32_t k0 = 0; k0 < nk; k0 += 64) {
+    const uint32_t kb = min(64u, nk - k0);
+    uint32_t cnt = 0, lo = 0;
+    KeptAid r;
+    r.aid = 0; r.info = 0;
+    if ((uint32_t)l < kb) {
+      r = kept[e0 + k0 + l];
+      if (r.aid < L.n_items) { lo = L.eoff[r.aid]; cnt = L.ucnt[r.aid]; }
+      cnt += 1;  // the self pair (aid, aid)
     }
-    uint32_t* MK = mk[w];
-    uint32_t* MB = mb[w];
-    uint32_t* MR = mr[w];
-    for (uint32_t e = l; e < tot; e += 64) {
-      uint32_t x = a, bit = 1u, rk = 0;
-      if (e > 0) {
-        uint32_t j = e - 1;
-        int q = 0;
-#pragma unroll
-        for (int z = 0; z < CS_SRC; ++z)
-          if (q == z && j >= len[z]) { j -= len[z]; q = z + 1; }
-        const int32_t* np = L.nxt[0];
-        const int16_t* rp = L.rank[0];
-        uint32_t b0 = beg[0];
-#pragma unroll
-        for (int z = 1; z < CS_SRC; ++z)
-          if (q == z) { np = L.nxt[z]; rp = L.rank[z]; b0 = beg[z]; }
-        x = (uint32_t)np[b0 + j];
-        rk = (uint32_t)rp[b0 + j];
-        bit = 2u << q;
-      }
-      uint32_t h = cs_hash(x, CS_MINI - 1);
-      for (int p = 0; p < CS_MINI; ++p) {
-        uint32_t kk = __hip_atomic_load(&MK[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (kk == CS_EMPTY) {
-          const uint32_t prev = atomicCAS(&MK[h], CS_EMPTY, x);
-          kk = (prev == CS_EMPTY) ? x : prev;
-        }
-        if (kk == x) { atomicOr(&MB[h], bit); atomicMin(&MR[h], rk); break; }
-        h = (h + 1) & (CS_MINI - 1);
-      }
-    }
+    const uint32_t incl = wave_incl_scan(cnt);
+    PRE[l + 1] = incl;
+    if (l == 0) PRE[0] = 0;
+    ka[w][l] = (uint32_t)r.aid;  // read back by the lanes that expand this aid's entries
+    ki[w][l] = r.info;
+    kl[w][l] = lo;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    for (int i = l; i < CS_MINI; i += 64) {
-      const uint32_t x = MK[i];
-      if (x != CS_EMPTY) {
-        // R5 (:512-516) pair kept iff aid_next == aid or best co-count / w2v rank <= th
-        if (x == a || MR[i] <= th) insert(x, MB[i] | (tm << 8), ord);
-        MK[i] = CS_EMPTY; MB[i] = 0; MR[i] = 0x7FFFFFFF;
+    const uint32_t T = __shfl(incl, 63);
+    for (uint32_t e = l; e < T; e += 64) {
+      uint32_t lo_k = 0, hi_k = kb;  // owner: largest k with PRE[k] <= e
+      while (hi_k - lo_k > 1) {
+        const uint32_t m = (lo_k + hi_k) >> 1;
+        if (PRE[m] <= e) lo_k = m; else hi_k = m;
+      }
+      const int kk = (int)lo_k;
+      const uint32_t a = ka[w][kk];
+      const uint32_t info = ki[w][kk];
+      const uint32_t base = kl[w][kk];
+      const uint32_t j = e - PRE[kk];
+      const uint32_t ord = info & 0xFFFFu, tm = (info >> 16) & 7u, th = info >> 19;
+      if (j == 0) {
+        insert(a, 1u | (tm << 8), ord);
+      } else {
+        const uint32_t x = (uint32_t)L.mx[base + j - 1];
+        const uint32_t br = L.mbr[base + j - 1];
+        // R5 (:512-516) pair kept iff aid_next == aid or its best co-count / w2v rank <= th
+        if (x == a || (br & 0xFFu) <= th) insert(x, (br >> 8) | (x == a ? 1u : 0u) | (tm << 8), ord);
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -454,10 +527,6 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
   }
   L.n_items = lists->n_items;
   L.pop_off = lists->pop_off; L.pop_aid = lists->pop_aid; L.n_clusters = lists->pop_off ? lists->n_clusters : 0;
-  if (lists->max_list_total + 1 > CS_MINI / 2) {
-    set_error("candidates_generate: per-aid list total %d exceeds %d", lists->max_list_total, CS_MINI / 2 - 1);
-    return OTTOHIP_ELIMIT;
-  }
   ottohip_candidates* C = new ottohip_candidates();
   C->n_sessions = n_sessions;
   auto fail = [&](int rc) { C->release(); delete C; return rc; };
@@ -482,8 +551,37 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
       (rc = ws.get("cs_novf", 1, &n_ovf)) || (rc = ws.get("cs_ovf", (size_t)Sn, &ovf)) ||
       (rc = ws.get("cs_tot", 1, &tot)) || (rc = ws.get("cs_err", 1, &err)))
     return fail(rc);
-  int ph = ctx->begin("cand_aids", s, 9.0 * E);
   hipMemsetAsync(err, 0, sizeof(int), s);
+  // per-aid merged source lists (once per call)
+  MergedLists M;
+  M.n_items = L.n_items;
+  M.pop_off = L.pop_off; M.pop_aid = L.pop_aid; M.n_clusters = L.n_clusters;
+  {
+    uint32_t *tot_e, *ucnt, *eoff32;
+    uint64_t *eoff, *etot;
+    int32_t* mx;
+    uint16_t* mbr;
+    const int64_t NI = std::max<int32_t>(L.n_items, 1);
+    if ((rc = ws.get("ml_tot", (size_t)NI + 1, &tot_e)) || (rc = ws.get("ml_eoff", (size_t)NI + 1, &eoff)) ||
+        (rc = ws.get("ml_eoff32", (size_t)NI + 1, &eoff32)) || (rc = ws.get("ml_ucnt", (size_t)NI, &ucnt)) ||
+        (rc = ws.get("ml_etot", 1, &etot)))
+      return fail(rc);
+    int ph0 = ctx->begin("cand_merge_lists", s, 0);
+    hipMemsetAsync(tot_e + NI, 0, 4, s);
+    k_ml_total<<<grid_for(NI), 256, 0, s>>>(L, tot_e);
+    if ((rc = exclusive_scan_u32(ctx, tot_e, eoff, NI + 1, etot, s))) return fail(rc);
+    uint64_t ne = 0;
+    if ((rc = d2h(&ne, etot, 1, s))) return fail(rc);
+    if (ne >= ((uint64_t)1 << 32)) { set_error("candidates_generate: > 2^32 list entries"); return fail(OTTOHIP_ELIMIT); }
+    if ((rc = ws.get("ml_x", (size_t)std::max<uint64_t>(ne, 1), &mx)) ||
+        (rc = ws.get("ml_br", (size_t)std::max<uint64_t>(ne, 1), &mbr)))
+      return fail(rc);
+    k_u64_to_u32<<<grid_for(NI + 1), 256, 0, s>>>(eoff, NI + 1, eoff32);
+    k_ml_build<<<(unsigned)ceil_div(NI, 4), 256, 0, s>>>(L, eoff32, mx, mbr, ucnt, err);
+    ctx->end(ph0, s);
+    M.eoff = eoff32; M.ucnt = ucnt; M.mx = mx; M.mbr = mbr;
+  }
+  int ph = ctx->begin("cand_aids", s, 9.0 * E);
   hipMemsetAsync(n_ovf, 0, sizeof(uint32_t), s);
   hipMemsetAsync(n_cand + Sn, 0, sizeof(uint32_t), s);
   k_cand_aids<<<(unsigned)Sn, 64, 0, s>>>(session_offsets, Sn, aid, ts, type, kept, n_kept, err);
@@ -491,12 +589,13 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
   ph = ctx->begin("cand_build", s, 0);
   constexpr int W = 2;
   k_cand_build<1024, W><<<(unsigned)ceil_div(Sn, W), 64 * W, 0, s>>>(session_offsets, nullptr, Sn, kept, n_kept,
-                                                                       session_cl, L, 0, n_cand, nullptr, nullptr,
+                                                                       session_cl, M, 0, n_cand, nullptr, nullptr,
                                                                        nullptr, nullptr, ovf, n_ovf);
   uint32_t novf = 0;
   int herr = 0;
   if ((rc = d2h(&novf, n_ovf, 1, s)) || (rc = d2h(&herr, err, 1, s))) return fail(rc);
-  if (herr) { set_error("candidates_generate: a session has more than %d events", CS_MAXE); return fail(OTTOHIP_ELIMIT); }
+  if (herr & 1) { set_error("candidates_generate: a session has more than %d events", CS_MAXE); return fail(OTTOHIP_ELIMIT); }
+  if (herr & 4) { set_error("candidates_generate: an aid has more than %d list entries", ML_MAX); return fail(OTTOHIP_ELIMIT); }
   int64_t* ovf64 = nullptr;
   uint32_t* n_ovf2 = nullptr;
   int32_t* ovf2 = nullptr;
@@ -510,7 +609,7 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
     std::vector<int64_t> ho64(ho.begin(), ho.end());
     OH_HIP(hipMemcpyAsync(ovf64, ho64.data(), novf * sizeof(int64_t), hipMemcpyHostToDevice, s));
     OH_HIP(hipMemsetAsync(n_ovf2, 0, sizeof(uint32_t), s));
-    k_cand_build<4096, 1><<<novf, 64, 0, s>>>(session_offsets, ovf64, novf, kept, n_kept, session_cl, L, 0, n_cand,
+    k_cand_build<4096, 1><<<novf, 64, 0, s>>>(session_offsets, ovf64, novf, kept, n_kept, session_cl, M, 0, n_cand,
                                                nullptr, nullptr, nullptr, nullptr, ovf2, n_ovf2);
     uint32_t novf2 = 0;
     if ((rc = d2h(&novf2, n_ovf2, 1, s))) return fail(rc);
@@ -526,10 +625,10 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
     return fail(OTTOHIP_ENOMEM);
   }
   k_cand_build<1024, W><<<(unsigned)ceil_div(Sn, W), 64 * W, 0, s>>>(session_offsets, nullptr, Sn, kept, n_kept,
-                                                                       session_cl, L, 1, n_cand, C->off, C->next,
+                                                                       session_cl, M, 1, n_cand, C->off, C->next,
                                                                        C->ord, C->flags, ovf, n_ovf);
   if (novf)
-    k_cand_build<4096, 1><<<novf, 64, 0, s>>>(session_offsets, ovf64, novf, kept, n_kept, session_cl, L, 1, n_cand,
+    k_cand_build<4096, 1><<<novf, 64, 0, s>>>(session_offsets, ovf64, novf, kept, n_kept, session_cl, M, 1, n_cand,
                                                C->off, C->next, C->ord, C->flags, ovf2, n_ovf2);
   if (hipGetLastError() != hipSuccess) { set_error("k_cand_build launch failed"); return fail(OTTOHIP_EHIP); }
   ctx->end(ph, s);

@@ -60,7 +60,10 @@ constexpr int KM_MAXK = 64;
 constexpr double KM_FX = 16777216.0;  // 2^24 fixed point for the cluster sums
 
 // one thread per row; centroids (k x dim f32) and their squared norms in LDS
-// per-block sums in LDS (int64 fixed point), flushed with one device atomic per (cluster, dim)
+// per-block sums in LDS (int64 fixed point), flushed with one device atomic per (cluster, dim).
+// KP = k rounded up to a multiple of 8: padded centroids are 0 with |c|^2 = +inf (never chosen),
+// so the distance loop has no per-cluster predicate.
+template <int KP>
 __global__ __launch_bounds__(256) void k_km_assign(const float* __restrict__ X, int64_t n, int dim,
                                                    const float* __restrict__ C, int k, int32_t* __restrict__ label,
                                                    unsigned long long* __restrict__ sums,
@@ -68,15 +71,16 @@ __global__ __launch_bounds__(256) void k_km_assign(const float* __restrict__ X, 
   extern __shared__ unsigned long long smem64[];
   unsigned long long* ls = smem64;                       // k * dim sums (fixed point, two's complement)
   unsigned long long* lc = smem64 + k * dim;             // k counts
-  float* Cs = reinterpret_cast<float*>(smem64 + k * dim + k);  // k * dim
-  float* cn = Cs + k * dim;                              // k
+  float* Cs = reinterpret_cast<float*>(smem64 + k * dim + k);  // KP * dim
+  float* cn = Cs + KP * dim;                             // KP
   for (int i = threadIdx.x; i < k * dim; i += blockDim.x) { Cs[i] = C[i]; ls[i] = 0ull; }
   for (int i = threadIdx.x; i < k; i += blockDim.x) lc[i] = 0ull;
   __syncthreads();
-  for (int c = threadIdx.x; c < k; c += blockDim.x) {
+  for (int i = k * dim + threadIdx.x; i < KP * dim; i += blockDim.x) Cs[i] = 0.f;
+  for (int c = threadIdx.x; c < KP; c += blockDim.x) {
     float s = 0.f;
-    for (int d = 0; d < dim; ++d) s += Cs[c * dim + d] * Cs[c * dim + d];
-    cn[c] = s;
+    for (int d = 0; d < dim && c < k; ++d) s += Cs[c * dim + d] * Cs[c * dim + d];
+    cn[c] = c < k ? s : INFINITY;
   }
   __syncthreads();
   double part = 0.0;
@@ -86,9 +90,9 @@ __global__ __launch_bounds__(256) void k_km_assign(const float* __restrict__ X, 
     float best = INFINITY;
     int bc = 0;
     // |x - c|^2 = |x|^2 - 2 x.c + |c|^2; the row is streamed once (16-B loads), all k dots accumulated
-    float dot[KM_MAXK];
+    float dot[KP];
 #pragma unroll
-    for (int c = 0; c < KM_MAXK; ++c) dot[c] = 0.f;
+    for (int c = 0; c < KP; ++c) dot[c] = 0.f;
     if ((dim & 3) == 0) {
       const float4* x4 = reinterpret_cast<const float4*>(x);
       for (int d4 = 0; d4 < (dim >> 2); ++d4) {
@@ -99,8 +103,7 @@ __global__ __launch_bounds__(256) void k_km_assign(const float* __restrict__ X, 
           const int d = 4 * d4 + u;
           xn += xs[u] * xs[u];
 #pragma unroll
-          for (int c = 0; c < KM_MAXK; ++c)
-            if (c < k) dot[c] += xs[u] * Cs[c * dim + d];
+          for (int c = 0; c < KP; ++c) dot[c] += xs[u] * Cs[c * dim + d];
         }
       }
     } else {
@@ -108,16 +111,13 @@ __global__ __launch_bounds__(256) void k_km_assign(const float* __restrict__ X, 
         const float xv = x[d];
         xn += xv * xv;
 #pragma unroll
-        for (int c = 0; c < KM_MAXK; ++c)
-          if (c < k) dot[c] += xv * Cs[c * dim + d];
+        for (int c = 0; c < KP; ++c) dot[c] += xv * Cs[c * dim + d];
       }
     }
 #pragma unroll
-    for (int c = 0; c < KM_MAXK; ++c) {
-      if (c < k) {
-        const float dd = xn - 2.f * dot[c] + cn[c];
-        if (dd < best) { best = dd; bc = c; }  // ties: lowest cluster index
-      }
+    for (int c = 0; c < KP; ++c) {
+      const float dd = xn - 2.f * dot[c] + cn[c];
+      if (dd < best) { best = dd; bc = c; }  // ties: lowest cluster index
     }
     label[i] = bc;
     part += (double)fmaxf(best, 0.f);
@@ -141,6 +141,17 @@ __global__ __launch_bounds__(256) void k_km_assign(const float* __restrict__ X, 
     part += __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
   }
   if ((threadIdx.x & 63) == 0) atomicAdd(inertia, part);
+}
+
+static void launch_km_assign(int k, unsigned grid, size_t lds, hipStream_t s, const float* X, int64_t n, int dim,
+                             const float* C, int32_t* labels, unsigned long long* sums, unsigned long long* cnt,
+                             double* inr) {
+  switch ((k + 7) / 8) {
+#define KM_CASE(q) case q: k_km_assign<8 * q><<<grid, 256, lds, s>>>(X, n, dim, C, k, labels, sums, cnt, inr); break;
+    KM_CASE(1) KM_CASE(2) KM_CASE(3) KM_CASE(4) KM_CASE(5) KM_CASE(6) KM_CASE(7) KM_CASE(8)
+#undef KM_CASE
+    default: break;
+  }
 }
 
 // ---------------------------------------------------------------- C3
@@ -284,7 +295,9 @@ int ottohip_kmeans_step(ottohip_ctx* ctx, const float* X, int64_t n, int dim, fl
   if (!ctx || !X || !centroids || !labels || n < 1 || dim < 1 || dim > EMB_MAXD || k < 1 || k > KM_MAXK) {
     set_error("kmeans_step: bad arguments (k <= %d, dim <= %d)", KM_MAXK, EMB_MAXD); return OTTOHIP_EINVAL;
   }
-  if (((size_t)k * dim + k) * (sizeof(float) + 8) > 65536) { set_error("kmeans_step: k * dim too large for LDS"); return OTTOHIP_ELIMIT; }
+  if (((size_t)k * dim + k) * 8 + ((size_t)((k + 7) / 8 * 8) * (dim + 1)) * sizeof(float) > 65536) {
+    set_error("kmeans_step: k * dim too large for LDS"); return OTTOHIP_ELIMIT;
+  }
   hipStream_t s = S(stream);
   OH_HIP(hipSetDevice(ctx->device));
   unsigned long long* sums;
@@ -296,9 +309,9 @@ int ottohip_kmeans_step(ottohip_ctx* ctx, const float* X, int64_t n, int dim, fl
   OH_HIP(hipMemsetAsync(sums, 0, (size_t)k * dim * 8, s));
   OH_HIP(hipMemsetAsync(cnt, 0, (size_t)k * 8, s));
   OH_HIP(hipMemsetAsync(inr, 0, 8, s));
-  const size_t lds = ((size_t)k * dim + k) * (sizeof(float) + 8);
+  const size_t lds = ((size_t)k * dim + k) * 8 + ((size_t)((k + 7) / 8 * 8) * (dim + 1)) * sizeof(float);
   const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n, 256), (int64_t)ctx->n_cu * 4);
-  k_km_assign<<<grid, 256, lds, s>>>(X, n, dim, centroids, k, labels, sums, cnt, inr);
+  launch_km_assign(k, grid, lds, s, X, n, dim, centroids, labels, sums, cnt, inr);
   OH_HIP(hipGetLastError());
   std::vector<unsigned long long> hs((size_t)k * dim);
   std::vector<unsigned long long> hc(k);
@@ -331,14 +344,16 @@ int ottohip_kmeans_assign(ottohip_ctx* ctx, const float* X, int64_t n, int dim, 
   if (!ctx || !X || !centroids || !labels || n < 1 || dim < 1 || dim > EMB_MAXD || k < 1 || k > KM_MAXK) {
     set_error("kmeans_assign: bad arguments"); return OTTOHIP_EINVAL;
   }
-  if (((size_t)k * dim + k) * (sizeof(float) + 8) > 65536) { set_error("kmeans_assign: k * dim too large for LDS"); return OTTOHIP_ELIMIT; }
+  if (((size_t)k * dim + k) * 8 + ((size_t)((k + 7) / 8 * 8) * (dim + 1)) * sizeof(float) > 65536) {
+    set_error("kmeans_assign: k * dim too large for LDS"); return OTTOHIP_ELIMIT;
+  }
   hipStream_t s = S(stream);
   double* inr;
   OH_TRY(ctx->ws.get("km_inertia", 1, &inr));
   OH_HIP(hipMemsetAsync(inr, 0, 8, s));
-  const size_t lds = ((size_t)k * dim + k) * (sizeof(float) + 8);
+  const size_t lds = ((size_t)k * dim + k) * 8 + ((size_t)((k + 7) / 8 * 8) * (dim + 1)) * sizeof(float);
   const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n, 256), (int64_t)ctx->n_cu * 4);
-  k_km_assign<<<grid, 256, lds, s>>>(X, n, dim, centroids, k, labels, nullptr, nullptr, inr);
+  launch_km_assign(k, grid, lds, s, X, n, dim, centroids, labels, nullptr, nullptr, inr);
   OH_HIP(hipGetLastError());
   double h = 0.0;
   OH_TRY(d2h(&h, inr, 1, s));
