@@ -143,6 +143,7 @@ def main():
                     help="covis: configs[1] line (+ the kNN sub-object); knn: only configs[2]; "
                          "candidates: configs[4] end-to-end on 1 GPU")
     ap.add_argument("--cand-sessions", type=int, default=12_900_000)
+    ap.add_argument("--cand-steps", type=int, default=1, help="0 disables the configs[4] candidates sub-object")
     ap.add_argument("--kmeans-iter", type=int, default=100)
     ap.add_argument("--knn-items", type=int, default=1_855_603)
     ap.add_argument("--knn-queries", type=int, default=600_000)
@@ -286,6 +287,9 @@ def main():
         del dev
         torch.cuda.empty_cache()
         out["knn"] = bench_knn(args.knn_steps, 1, args.knn_items, args.knn_queries, not args.no_cpu)
+    if args.cand_steps > 0 and world == 1:
+        torch.cuda.empty_cache()
+        out["candidates"] = bench_candidates(args.cand_sessions, args.cand_steps, args.kmeans_iter)
     print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
