@@ -15,6 +15,7 @@
 //
 // Ordinal-rank ties are broken by aid ascending (polars leaves them to groupby row order).
 #include <algorithm>
+#include <cstdlib>
 #include "prims.h"
 #include "table.h"
 
@@ -232,7 +233,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
                                                           int32_t* __restrict__ o_next, int16_t* __restrict__ o_ord,
                                                           uint16_t* __restrict__ o_flags,
                                                           int32_t* __restrict__ overflow,
-                                                          uint32_t* __restrict__ n_overflow) {
+                                                          uint32_t* __restrict__ n_overflow, int dbg) {
   __shared__ uint32_t hk[WAVES][HC], hm[WAVES][HC], ho[WAVES][HC];
   __shared__ uint64_t sk[WAVES][HC];
   __shared__ uint32_t pre[WAVES][65], ka[WAVES][64], ki[WAVES][64], kl[WAVES][64];
@@ -250,13 +251,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
   auto insert = [&](uint32_t x, uint32_t bits, uint32_t ord) {
     uint32_t h = cs_hash(x, HC - 1);
     for (int p = 0; p < HC; ++p) {
-      uint32_t k = __hip_atomic_load(&K[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (k == CS_EMPTY) {
-        const uint32_t prev = atomicCAS(&K[h], CS_EMPTY, x);
-        if (prev == CS_EMPTY || prev == x) k = x;
-        else k = prev;
-      }
-      if (k == x) { atomicOr(&Mk[h], bits); atomicMin(&Ord[h], ord); return; }
+      const uint32_t prev = atomicCAS(&K[h], CS_EMPTY, x);  // claim or find in one LDS round trip
+      if (prev == CS_EMPTY || prev == x) { atomicOr(&Mk[h], bits); atomicMin(&Ord[h], ord); return; }
       h = (h + 1) & (HC - 1);
     }
     full = true;
@@ -283,34 +279,46 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
     kl[w][l] = lo;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const uint32_t T = __shfl(incl, 63);
-    for (uint32_t e = l; e < T; e += 64) {
+    const uint32_t T = (dbg & 4) ? 0u : __shfl(incl, 63);
+    // element e -> (owner kept aid, its info, list entry); the next element's global loads are
+    // issued before the current one is inserted (the loop is latency-bound)
+    auto fetch = [&](uint32_t e, uint32_t& a, uint32_t& info, uint32_t& j, uint32_t& x, uint32_t& br) {
       uint32_t lo_k = 0, hi_k = kb;  // owner: largest k with PRE[k] <= e
       while (hi_k - lo_k > 1) {
         const uint32_t m = (lo_k + hi_k) >> 1;
         if (PRE[m] <= e) lo_k = m; else hi_k = m;
       }
       const int kk = (int)lo_k;
-      const uint32_t a = ka[w][kk];
-      const uint32_t info = ki[w][kk];
-      const uint32_t base = kl[w][kk];
-      const uint32_t j = e - PRE[kk];
-      const uint32_t ord = info & 0xFFFFu, tm = (info >> 16) & 7u, th = info >> 19;
-      if (j == 0) {
-        insert(a, 1u | (tm << 8), ord);
-      } else {
-        const uint32_t x = (uint32_t)L.mx[base + j - 1];
-        const uint32_t br = L.mbr[base + j - 1];
-        // R5 (:512-516) pair kept iff aid_next == aid or its best co-count / w2v rank <= th
-        if (x == a || (br & 0xFFu) <= th) insert(x, (br >> 8) | (x == a ? 1u : 0u) | (tm << 8), ord);
+      a = ka[w][kk];
+      info = ki[w][kk];
+      j = e - PRE[kk];
+      x = a; br = 0;
+      if (j > 0) {
+        const uint32_t base = kl[w][kk];
+        x = (uint32_t)L.mx[base + j - 1];
+        br = L.mbr[base + j - 1];
       }
+    };
+    uint32_t a0 = 0, i0 = 0, j0 = 0, x0 = 0, b0 = 0;
+    if ((uint32_t)l < T) fetch(l, a0, i0, j0, x0, b0);
+    for (uint32_t e = l; e < T; e += 64) {
+      uint32_t a1 = 0, i1 = 0, j1 = 0, x1 = 0, b1 = 0;
+      if (e + 64 < T) fetch(e + 64, a1, i1, j1, x1, b1);
+      const uint32_t ord = i0 & 0xFFFFu, tm = (i0 >> 16) & 7u, th = i0 >> 19;
+      if (j0 == 0) {
+        insert(a0, 1u | (tm << 8), ord);
+      } else if (x0 == a0 || (b0 & 0xFFu) <= th) {
+        // R5 (:512-516) pair kept iff aid_next == aid or its best co-count / w2v rank <= th
+        insert(x0, (b0 >> 8) | (x0 == a0 ? 1u : 0u) | (tm << 8), ord);
+      }
+      a0 = a1; i0 = i1; j0 = j1; x0 = x1; b0 = b1;
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   }
   // R6 (:571-585) the cl50 popularity list of the session's cluster; new rows get ts_order 999
   const int32_t c = session_cl ? session_cl[s] : -1;
-  if (c >= 0 && c < L.n_clusters) {
+  if (c >= 0 && c < L.n_clusters && !(dbg & 2)) {
     const uint32_t pb = L.pop_off[c], pe = L.pop_off[c + 1];
     for (uint32_t j = pb + l; j < pe; j += 64) insert((uint32_t)L.pop_aid[j], 1u << 11, 999u);
   }
@@ -352,6 +360,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
   }
   int P2 = 1;
   while (P2 < cnt) P2 <<= 1;
+  if (dbg & 1) P2 = 1;  // (profiling) skip the sort
   for (int i = cnt + l; i < P2; i += 64) SK[i] = ~0ull;
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -552,6 +561,7 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
       (rc = ws.get("cs_tot", 1, &tot)) || (rc = ws.get("cs_err", 1, &err)))
     return fail(rc);
   hipMemsetAsync(err, 0, sizeof(int), s);
+  static const int dbg = getenv("OTTOHIP_CAND_DBG") ? atoi(getenv("OTTOHIP_CAND_DBG")) : 0;  // profiling ablations
   // per-aid merged source lists (once per call)
   MergedLists M;
   M.n_items = L.n_items;
@@ -590,7 +600,7 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
   constexpr int W = 2;
   k_cand_build<1024, W><<<(unsigned)ceil_div(Sn, W), 64 * W, 0, s>>>(session_offsets, nullptr, Sn, kept, n_kept,
                                                                        session_cl, M, 0, n_cand, nullptr, nullptr,
-                                                                       nullptr, nullptr, ovf, n_ovf);
+                                                                       nullptr, nullptr, ovf, n_ovf, dbg);
   uint32_t novf = 0;
   int herr = 0;
   if ((rc = d2h(&novf, n_ovf, 1, s)) || (rc = d2h(&herr, err, 1, s))) return fail(rc);
@@ -610,7 +620,7 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
     OH_HIP(hipMemcpyAsync(ovf64, ho64.data(), novf * sizeof(int64_t), hipMemcpyHostToDevice, s));
     OH_HIP(hipMemsetAsync(n_ovf2, 0, sizeof(uint32_t), s));
     k_cand_build<4096, 1><<<novf, 64, 0, s>>>(session_offsets, ovf64, novf, kept, n_kept, session_cl, M, 0, n_cand,
-                                               nullptr, nullptr, nullptr, nullptr, ovf2, n_ovf2);
+                                               nullptr, nullptr, nullptr, nullptr, ovf2, n_ovf2, dbg);
     uint32_t novf2 = 0;
     if ((rc = d2h(&novf2, n_ovf2, 1, s))) return fail(rc);
     if (novf2) { set_error("candidates_generate: %u sessions exceed 4096 candidates", novf2); return fail(OTTOHIP_ELIMIT); }
@@ -626,10 +636,10 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
   }
   k_cand_build<1024, W><<<(unsigned)ceil_div(Sn, W), 64 * W, 0, s>>>(session_offsets, nullptr, Sn, kept, n_kept,
                                                                        session_cl, M, 1, n_cand, C->off, C->next,
-                                                                       C->ord, C->flags, ovf, n_ovf);
+                                                                       C->ord, C->flags, ovf, n_ovf, dbg);
   if (novf)
     k_cand_build<4096, 1><<<novf, 64, 0, s>>>(session_offsets, ovf64, novf, kept, n_kept, session_cl, M, 1, n_cand,
-                                               C->off, C->next, C->ord, C->flags, ovf2, n_ovf2);
+                                               C->off, C->next, C->ord, C->flags, ovf2, n_ovf2, dbg);
   if (hipGetLastError() != hipSuccess) { set_error("k_cand_build launch failed"); return fail(OTTOHIP_EHIP); }
   ctx->end(ph, s);
   *out = C;

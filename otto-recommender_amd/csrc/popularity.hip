@@ -209,10 +209,15 @@ __global__ void k_pop_rank(const uint32_t* __restrict__ pair_slot, const uint32_
   rank[p] = (uint16_t)(r > 999 ? 999 : r);
 }
 
-__global__ void k_pop_cluster_hist(const uint32_t* __restrict__ pair_slot, int64_t n, int32_t n_items,
-                                   uint32_t* __restrict__ hist) {
+// pairs are in slot = (cluster, aid) order: the first pair of each cluster from the boundaries
+// (a histogram here would be a few same-address atomics per pair)
+__global__ void k_pop_cluster_first(const uint32_t* __restrict__ pair_slot, int64_t n, int32_t n_items,
+                                    int32_t n_clusters, uint64_t* __restrict__ cl_first) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) atomicAdd(&hist[pair_slot[i] / (uint32_t)n_items], 1u);
+  if (i > n) return;
+  const int64_t prev = i == 0 ? -1 : (int64_t)(pair_slot[i - 1] / (uint32_t)n_items);
+  const int64_t cur = i == n ? (int64_t)n_clusters : (int64_t)(pair_slot[i] / (uint32_t)n_items);
+  for (int64_t c = prev + 1; c <= cur; ++c) cl_first[c] = (uint64_t)i;
 }
 
 __global__ void k_pop_keep(const uint16_t* __restrict__ rank, int64_t n, int keep_top_k, uint32_t* __restrict__ keep) {
@@ -419,9 +424,8 @@ int ottohip_popularity_ranks(ottohip_ctx* ctx, const int64_t* session_offsets, i
       (rc = ws.get("pop_keep", (size_t)n, &keep)) || (rc = ws.get("pop_oidx", (size_t)n, &oidx)))
     return fail(rc);
   k_pop_pairs<<<grid_for(NS), 256, 0, s>>>(present, pidx, NS, slot);
-  hipMemsetAsync(hist, 0, ((size_t)n_clusters + 1) * 4, s);
-  k_pop_cluster_hist<<<grid_for(n), 256, 0, s>>>(slot, n, n_items, hist);
-  if ((rc = exclusive_scan_u32(ctx, hist, cl_first, (int64_t)n_clusters + 1, nullptr, s))) return fail(rc);
+  (void)hist;
+  k_pop_cluster_first<<<grid_for(n + 1), 256, 0, s>>>(slot, n, n_items, n_clusters, cl_first);
   const int cbits = std::max(1, bits_for((uint64_t)n_clusters));
   for (int t = 0; t < 6; ++t) {
     const uint32_t* c = cnt + (size_t)t * NS;
