@@ -151,60 +151,57 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
     __builtin_amdgcn_s_barrier();  // tile t visible to all waves; slot (t+2)%3 = (t-1)%3 is free
     if (t + 2 < nT) issue(t + 2);
     const uint4* T = ring + (int)(t % KN_RING) * (KN_IT * KN_CH);
-    // one row-block (32 items) = 8 k-steps x 2 MFMAs sharing the item fragment; software-pipelined
-    // one row-block deep: the MFMAs of block rb+1 are issued before the epilogue of block rb, so
-    // the top-K branch of rb runs while the matrix core works on rb+1
-    auto mma = [&](int rb, f32x16& A, f32x16& B) {
-      A = f32x16{};
-      B = f32x16{};
-      const int row = rb * 32 + r;
-      bf16x8 cur = __builtin_bit_cast(bf16x8, T[row * KN_CH + ((0 + h) ^ (row & 15))]);
+#pragma unroll
+    for (int rp = 0; rp < KN_IT / 64; ++rp) {  // two row-blocks of 32 items at a time
+      f32x16 accA[2] = {}, accB[2] = {};
+      const int row0 = (2 * rp) * 32 + r, row1 = row0 + 32;
+      bf16x8 cur0 = __builtin_bit_cast(bf16x8, T[row0 * KN_CH + ((0 + h) ^ (row0 & 15))]);
+      bf16x8 cur1 = __builtin_bit_cast(bf16x8, T[row1 * KN_CH + ((0 + h) ^ (row1 & 15))]);
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
-        bf16x8 nx = cur;
-        if (s < 7) nx = __builtin_bit_cast(bf16x8, T[row * KN_CH + ((2 * s + 2 + h) ^ (row & 15))]);
-        A = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, bqa[s], A, 0, 0, 0);
-        B = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, bqb[s], B, 0, 0, 0);
-        cur = nx;
+        bf16x8 nx0 = cur0, nx1 = cur1;
+        if (s < 7) {  // next k-step's fragments are read while this step's MFMAs run
+          nx0 = __builtin_bit_cast(bf16x8, T[row0 * KN_CH + ((2 * s + 2 + h) ^ (row0 & 15))]);
+          nx1 = __builtin_bit_cast(bf16x8, T[row1 * KN_CH + ((2 * s + 2 + h) ^ (row1 & 15))]);
+        }
+        accA[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur0, bqa[s], accA[0], 0, 0, 0);
+        accB[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur0, bqb[s], accB[0], 0, 0, 0);
+        accA[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur1, bqa[s], accA[1], 0, 0, 0);
+        accB[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur1, bqb[s], accB[1], 0, 0, 0);
+        cur0 = nx0;
+        cur1 = nx1;
       }
-    };
-    auto epi = [&](int rb, f32x16& A, f32x16& B) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {  // A -> rows + offx, B -> rows + offy of this lane's query
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(A[i]), __float_as_uint(B[i]), false, false);
-        A[i] = __uint_as_float(sw[0]);
-        B[i] = __uint_as_float(sw[1]);
-      }
-      float m = fmaxf(A[0], B[0]);
+      for (int u = 0; u < 2; ++u) {
 #pragma unroll
-      for (int i = 1; i < 16; ++i) m = fmaxf(m, fmaxf(A[i], B[i]));
-      if (ABL == 1) { thr = fmaxf(thr, m * 1e-30f); return; }  // ablation build: no candidate handling
-      if (PRE) {  // group g = tile % KN_C keeps its maximum in sc[g]
-        const int gsel = (int)(t % KN_C);
+        for (int i = 0; i < 16; ++i) {  // accA -> rows + offx, accB -> rows + offy of this lane's query
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(accA[u][i]), __float_as_uint(accB[u][i]),
+                                                           false, false);
+          accA[u][i] = __uint_as_float(sw[0]);
+          accB[u][i] = __uint_as_float(sw[1]);
+        }
+        float m = fmaxf(accA[u][0], accB[u][0]);
 #pragma unroll
-        for (int g = 0; g < KN_C; ++g)
-          if (g == gsel) sc[g] = fmaxf(sc[g], m);
-        return;
-      }
-      if (m > thr) {
-        const int64_t ib = t * KN_IT + rb * 32;
+        for (int i = 1; i < 16; ++i) m = fmaxf(m, fmaxf(accA[u][i], accB[u][i]));
+        if (ABL == 1) { thr = fmaxf(thr, m * 1e-30f); continue; }  // ablation build: no candidate handling
+        if (PRE) {  // group g = tile % KN_C keeps its maximum in sc[g]
+          const int gsel = (int)(t % KN_C);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int64_t base = ib + (i & 3) + 8 * (i >> 2);
-          if (A[i] > thr && base + offx < V) insert(A[i], (uint32_t)(base + offx));
-          if (B[i] > thr && base + offy < V) insert(B[i], (uint32_t)(base + offy));
+          for (int g = 0; g < KN_C; ++g)
+            if (g == gsel) sc[g] = fmaxf(sc[g], m);
+          continue;
+        }
+        if (m > thr) {
+          const int64_t ib = t * KN_IT + (2 * rp + u) * 32;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int64_t base = ib + (i & 3) + 8 * (i >> 2);
+            if (accA[u][i] > thr && base + offx < V) insert(accA[u][i], (uint32_t)(base + offx));
+            if (accB[u][i] > thr && base + offy < V) insert(accB[u][i], (uint32_t)(base + offy));
+          }
         }
       }
-    };
-    f32x16 XA, XB, YA, YB;
-    mma(0, XA, XB);
-    mma(1, YA, YB);
-    epi(0, XA, XB);
-    mma(2, XA, XB);
-    epi(1, YA, YB);
-    mma(3, YA, YB);
-    epi(2, XA, XB);
-    epi(3, YA, YB);
+    }
   }
   if (ABL == 1 && thr == 12345.f) ix[0] = 0;  // keep the ablated scores live
   if (PRE) {
