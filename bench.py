@@ -21,6 +21,16 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+PMC_FILE = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
+
+
+def pmc_traffic(key: str):
+    """Measured HBM bytes per launch/step (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate --pmc
+    passes of this same command; see profiles/r1_pmc_traffic.json), or None if not collected."""
+    try:
+        return float(json.load(open(PMC_FILE))[key]["traffic_bytes"])
+    except Exception:
+        return None
 
 
 def cpu_baseline(ev_sessions: int, n_files: int, seed: int = 0) -> dict:
@@ -76,7 +86,9 @@ def bench_knn(steps: int, warmup: int, n_items: int, n_q: int, with_cpu: bool) -
            "dtype": "bf16 (fp32 accumulate, fp32 rerank)",
            "roofline": {"bound": "mfma", "kernel": "k_knn_main", "achieved": flops / (main_ms / 1e3) / 1e12,
                         "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                        "frac": flops / (main_ms / 1e3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, "traffic": None,
+                        "frac": flops / (main_ms / 1e3) / 1e12 / MFMA_BF16_PEAK_TFLOPS,
+                        "traffic": pmc_traffic("k_knn_main") if n_items == 1_855_603 and n_q == 600_000 else None,
+                        "traffic_note": "HBM/fabric bytes per launch (every 512-query workgroup streams the item matrix)",
                         "flops_model": "2*Q*V*100 (K padding to 128 and the top-k epilogue not counted)"},
            "phases_ms": {k: round(v, 3) for k, v in ph.items()},
            "reference_faiss_ivf_queries_per_s": 705}
@@ -257,8 +269,11 @@ def main():
     # byte model of SURVEY.md §8(d): B = 9E + 8(S+1) + 16P + 12U
     b_model = 9.0 * n_events + 8.0 * (n_sess + 1) + 16.0 * pairs + 12.0 * rows
     dom = max(phases, key=lambda p: p[1]) if phases else ("step", t_step * 1e3, b_model)
-    dom_bytes = dom[2] if dom[2] > 0 else b_model
+    # algorithmic bytes of the dominant phase; reduce = read every pair word once (4P) + write
+    # every output row once (17U: rule u8, aid, aid_next, count, count_ge2)
+    dom_bytes = (4.0 * pairs / world + 17.0 * rows / world) if dom[0] == "reduce" else (dom[2] if dom[2] > 0 else b_model)
     achieved = dom_bytes / (dom[1] / 1e3) / 1e9
+    traffic = pmc_traffic("covis_reduce_phase") if (dom[0] == "reduce" and world == 1) else None
     out = {
         "metric": "co-visit pairs/sec + candidates/sec at 220M events, 1/2/4/8 MI355X",
         "value": pairs / t_step,
@@ -281,7 +296,8 @@ def main():
         "step_roofline": {"bound": "hbm", "model_bytes": b_model, "achieved": b_model / t_step / 1e9,
                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": b_model / t_step / 1e9 / HBM_PEAK_GBS},
         "roofline": {"bound": "hbm", "kernel": dom[0], "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "algorithmic_bytes": dom_bytes,
+                     "traffic_source": "profiles/r1_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE)"},
         "phases_ms": {p[0]: round(p[1], 3) for p in phases},
         "gen_s": round(gen_s, 1),
     }
