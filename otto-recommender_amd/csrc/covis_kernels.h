@@ -177,7 +177,7 @@ __device__ __forceinline__ int load_session(const uint64_t* __restrict__ src, in
     const bool valid = v != EV_INVALID;
     const int t = (int)(v & 3u);
     const uint64_t m0 = __ballot(valid && t == 0), m1 = __ballot(valid && t == 1), m2 = __ballot(valid && t == 2);
-    if (k < n) {
+    if (k < n && pref) {
       pref[0 * pstride + k] = base0 + mbcnt(m0);
       pref[1 * pstride + k] = base1 + mbcnt(m1);
       pref[2 * pstride + k] = base2 + mbcnt(m2);
@@ -185,7 +185,7 @@ __device__ __forceinline__ int load_session(const uint64_t* __restrict__ src, in
     base0 += (uint32_t)__popcll(m0); base1 += (uint32_t)__popcll(m1); base2 += (uint32_t)__popcll(m2);
     nv += (int)__popcll(__ballot(valid));
   }
-  if (l == 0) {  // pref[t][nv] = totals (invalid slots carry no types, so totals at n == at nv)
+  if (l == 0 && pref) {  // pref[t][nv] = totals (invalid slots carry no types, so totals at n == at nv)
     pref[0 * pstride + nv] = base0; pref[1 * pstride + nv] = base1; pref[2 * pstride + nv] = base2;
   }
   __builtin_amdgcn_wave_barrier();
@@ -472,8 +472,7 @@ __global__ __launch_bounds__(256) void k_emit(const int64_t* __restrict__ off, c
                                               const int64_t* __restrict__ fb, int nf, const uint32_t* __restrict__ fid,
                                               const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ poff,
                                               uint32_t* __restrict__ words) {
-  __shared__ uint64_t sev[4][LCAP];
-  __shared__ uint32_t spref[4][3 * (LCAP + 1)];
+  __shared__ uint64_t sev[4][LCAP];  // emission needs no per-type prefix counts: 16 KiB per block
   const int w = threadIdx.x >> 6;
   const int64_t g = (int64_t)blockIdx.x * 4 + w;
   if (g >= NB) return;
@@ -486,8 +485,8 @@ __global__ __launch_bounds__(256) void k_emit(const int64_t* __restrict__ off, c
     const int n = (int)(off[s + 1] - e0);
     if (n > LCAP || n == 0) continue;
     SessView S;
-    S.ev = sev[w]; S.pref = spref[w]; S.pstride = LCAP + 1;
-    S.nv = load_session(ev + e0, n, sev[w], spref[w], LCAP + 1);
+    S.ev = sev[w]; S.pref = nullptr; S.pstride = LCAP + 1;
+    S.nv = load_session(ev + e0, n, sev[w], nullptr, LCAP + 1);
     emit_session(S, e0, R, L, fid[f], cnt, poff, words);
     __builtin_amdgcn_wave_barrier();
   }
