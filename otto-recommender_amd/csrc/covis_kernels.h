@@ -431,9 +431,12 @@ __global__ __launch_bounds__(256) void k_piece_copy(const uint32_t* __restrict__
 }
 
 // ------------------------------------------------------------------ S4 emit
+// cnt / poff are indexed [e0 + i]: global arrays with e0 = the session's first event, or the
+// block's LDS copies with e0 = the session's offset inside the block
 __device__ __forceinline__ void emit_session(const SessView& S, int64_t e0, const RulesDev& R, const Layout& L,
                                              uint32_t file, const uint32_t* __restrict__ cnt,
-                                             const uint64_t* __restrict__ poff, uint32_t* __restrict__ words) {
+                                             const uint64_t* __restrict__ poff, uint32_t* __restrict__ words,
+                                             int dbg = 0) {
   const int l = lane_id();
   const int sg = l >> 4, sl = l & 15;
   const int shiftR = L.A + L.F;
@@ -448,7 +451,7 @@ __device__ __forceinline__ void emit_session(const SessView& S, int64_t e0, cons
     for (int q = 0; q < nr; ++q) {
       const int r = R.rule_of_type[t][q];
       const int jb = lower_ts(S.ev, S.nv, tsi + R.lo[r]);
-      const int je = upper_ts(S.ev, S.nv, tsi + R.hi[r]);
+      const int je = (dbg & 2) ? jb : upper_ts(S.ev, S.nv, tsi + R.hi[r]);
       const uint32_t hi = ((uint32_t)q << shiftR) | file;
       for (int j0 = jb; j0 < je; j0 += 16) {
         const int j = j0 + sl;
@@ -460,35 +463,68 @@ __device__ __forceinline__ void emit_session(const SessView& S, int64_t e0, cons
           word = hi | ((uint32_t)ev_aid(ej) << L.F);
         }
         const uint32_t bal = (uint32_t)(__ballot(match) >> (sg * 16)) & 0xFFFFu;
-        if (match) words[out + (uint64_t)__popc(bal & ((1u << sl) - 1u))] = word;
+        if (match && !(dbg & 1)) words[out + (uint64_t)__popc(bal & ((1u << sl) - 1u))] = word;
         out += (uint64_t)__popc(bal);
       }
     }
   }
 }
 
+// One wave per 256-event block (the sessions that start in it). The block's events, pair counts
+// and word offsets are staged into LDS with three coalesced loads, so a session costs no global
+// round trips before its words are written (the per-session dependent loads made this kernel
+// latency-bound); blocks spanning more than EMIT_STAGE events take the per-session path.
+constexpr int EMIT_STAGE = 512;
 __global__ __launch_bounds__(256) void k_emit(const int64_t* __restrict__ off, const int64_t* __restrict__ first,
                                               int64_t NB, const uint64_t* __restrict__ ev, RulesDev R, Layout L,
                                               const int64_t* __restrict__ fb, int nf, const uint32_t* __restrict__ fid,
                                               const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ poff,
-                                              uint32_t* __restrict__ words) {
-  __shared__ uint64_t sev[4][LCAP];  // emission needs no per-type prefix counts: 16 KiB per block
-  const int w = threadIdx.x >> 6;
+                                              uint32_t* __restrict__ words, int dbg) {
+  __shared__ uint64_t sev[4][EMIT_STAGE];
+  __shared__ uint64_t spo[4][EMIT_STAGE];
+  __shared__ uint32_t scn[4][EMIT_STAGE];
+  __shared__ int64_t sof[4][EV_BLOCK + 2];  // session offsets of the block (<= EV_BLOCK + 1 sessions)
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int64_t g = (int64_t)blockIdx.x * 4 + w;
   if (g >= NB) return;
   const int64_t s0 = first[g], s1 = first[g + 1];
   if (s0 >= s1) return;
+  const bool so_staged = s1 - s0 <= EV_BLOCK + 1;
+  if (so_staged)
+    for (int64_t k = l; k <= s1 - s0; k += 64) sof[w][k] = off[s0 + k];
+  const int64_t E0 = off[s0], E1 = off[s1];
+  const bool staged = E1 - E0 <= EMIT_STAGE;
+  if (staged) {
+    for (int64_t k = l; k < E1 - E0; k += 64) {
+      sev[w][k] = ev[E0 + k];
+      scn[w][k] = cnt[E0 + k];
+      spo[w][k] = poff[E0 + k];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   int f = file_of(fb, nf, s0);
+  int64_t e0 = E0;
   for (int64_t s = s0; s < s1; ++s) {
     while (f + 1 < nf && fb[f + 1] <= s) ++f;
-    const int64_t e0 = off[s];
-    const int n = (int)(off[s + 1] - e0);
-    if (n > LCAP || n == 0) continue;
+    const int64_t e1 = so_staged ? sof[w][s + 1 - s0] : off[s + 1];
+    const int n = (int)(e1 - e0);
+    if (n > LCAP || n == 0) { e0 = e1; continue; }
     SessView S;
-    S.ev = sev[w]; S.pref = nullptr; S.pstride = LCAP + 1;
-    S.nv = load_session(ev + e0, n, sev[w], nullptr, LCAP + 1);
-    emit_session(S, e0, R, L, fid[f], cnt, poff, words);
+    S.pref = nullptr; S.pstride = LCAP + 1;
+    if (staged) {
+      S.ev = sev[w] + (e0 - E0);
+      int lo = 0, hi = n;  // valid events first, EV_INVALID (dedup) at the tail
+      while (lo < hi) { const int m = (lo + hi) >> 1; if (S.ev[m] != EV_INVALID) lo = m + 1; else hi = m; }
+      S.nv = lo;
+      emit_session(S, e0 - E0, R, L, fid[f], scn[w], spo[w], words, dbg);
+    } else {
+      S.ev = sev[w];
+      S.nv = load_session(ev + e0, n, sev[w], nullptr, LCAP + 1);
+      emit_session(S, e0, R, L, fid[f], cnt, poff, words, dbg);
+    }
     __builtin_amdgcn_wave_barrier();
+    e0 = e1;
   }
 }
 
