@@ -475,44 +475,47 @@ __device__ __forceinline__ void emit_session(const SessView& S, int64_t e0, cons
 // round trips before its words are written (the per-session dependent loads made this kernel
 // latency-bound); blocks spanning more than EMIT_STAGE events take the per-session path.
 constexpr int EMIT_STAGE = 512;
+// STAGED = 1 handles blocks spanning <= EMIT_STAGE events from LDS, STAGED = 0 the others from
+// global memory (two instantiations, so each keeps plain LDS / global addressing)
+template <int STAGED>
 __global__ __launch_bounds__(256) void k_emit(const int64_t* __restrict__ off, const int64_t* __restrict__ first,
                                               int64_t NB, const uint64_t* __restrict__ ev, RulesDev R, Layout L,
                                               const int64_t* __restrict__ fb, int nf, const uint32_t* __restrict__ fid,
                                               const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ poff,
                                               uint32_t* __restrict__ words, int dbg) {
-  __shared__ uint64_t sev[4][EMIT_STAGE];
-  __shared__ uint64_t spo[4][EMIT_STAGE];
-  __shared__ uint32_t scn[4][EMIT_STAGE];
-  __shared__ int64_t sof[4][EV_BLOCK + 2];  // session offsets of the block (<= EV_BLOCK + 1 sessions)
+  constexpr int SE = STAGED ? EMIT_STAGE : 1;
+  __shared__ uint64_t sev[4][STAGED ? EMIT_STAGE : LCAP];
+  __shared__ uint64_t spo[4][SE];
+  __shared__ uint32_t scn[4][SE];
+  __shared__ int64_t sof[4][STAGED ? EV_BLOCK + 2 : 1];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int64_t g = (int64_t)blockIdx.x * 4 + w;
   if (g >= NB) return;
   const int64_t s0 = first[g], s1 = first[g + 1];
   if (s0 >= s1) return;
-  const bool so_staged = s1 - s0 <= EV_BLOCK + 1;
-  if (so_staged)
-    for (int64_t k = l; k <= s1 - s0; k += 64) sof[w][k] = off[s0 + k];
   const int64_t E0 = off[s0], E1 = off[s1];
-  const bool staged = E1 - E0 <= EMIT_STAGE;
-  if (staged) {
+  const bool fits = E1 - E0 <= EMIT_STAGE && s1 - s0 <= EV_BLOCK + 1;
+  if (fits != (STAGED != 0)) return;
+  if (STAGED) {
+    for (int64_t k = l; k <= s1 - s0; k += 64) sof[w][k] = off[s0 + k];
     for (int64_t k = l; k < E1 - E0; k += 64) {
       sev[w][k] = ev[E0 + k];
       scn[w][k] = cnt[E0 + k];
       spo[w][k] = poff[E0 + k];
     }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   int f = file_of(fb, nf, s0);
   int64_t e0 = E0;
   for (int64_t s = s0; s < s1; ++s) {
     while (f + 1 < nf && fb[f + 1] <= s) ++f;
-    const int64_t e1 = so_staged ? sof[w][s + 1 - s0] : off[s + 1];
+    const int64_t e1 = STAGED ? sof[w][s + 1 - s0] : off[s + 1];
     const int n = (int)(e1 - e0);
     if (n > LCAP || n == 0) { e0 = e1; continue; }
     SessView S;
     S.pref = nullptr; S.pstride = LCAP + 1;
-    if (staged) {
+    if (STAGED) {
       S.ev = sev[w] + (e0 - E0);
       int lo = 0, hi = n;  // valid events first, EV_INVALID (dedup) at the tail
       while (lo < hi) { const int m = (lo + hi) >> 1; if (S.ev[m] != EV_INVALID) lo = m + 1; else hi = m; }
