@@ -488,7 +488,15 @@ __global__ __launch_bounds__(256) void k_emit(const int64_t* __restrict__ off, c
   __shared__ uint64_t spo[4][SE];
   __shared__ uint32_t scn[4][SE];
   __shared__ int64_t sof[4][STAGED ? EV_BLOCK + 2 : 1];
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  // the rule tables are indexed by per-lane event types: from LDS they cost lgkmcnt waits only;
+  // as dynamically indexed kernel arguments they were global loads whose vmcnt(0) waits also
+  // drained every outstanding word store (vmcnt counts stores on CDNA)
+  __shared__ RulesDev sR;
+  if (threadIdx.x == 0) sR = R;
+  __syncthreads();
+  // wave-uniform values made provably uniform: the block / session / file bookkeeping then uses
+  // scalar loads (lgkmcnt), never vmcnt waits that would drain the word stores
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
   const int64_t g = (int64_t)blockIdx.x * 4 + w;
   if (g >= NB) return;
   const int64_t s0 = first[g], s1 = first[g + 1];
@@ -507,9 +515,17 @@ __global__ __launch_bounds__(256) void k_emit(const int64_t* __restrict__ off, c
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   }
   int f = file_of(fb, nf, s0);
+  // file of the session: reloaded only when a file boundary is crossed (a per-session global
+  // load would wait on vmcnt and so drain the previous session's word stores)
+  int64_t next_b = f + 1 < nf ? fb[f + 1] : INT64_MAX;
+  uint32_t cur_fid = fid[f];
   int64_t e0 = E0;
   for (int64_t s = s0; s < s1; ++s) {
-    while (f + 1 < nf && fb[f + 1] <= s) ++f;
+    if (s >= next_b) {
+      while (f + 1 < nf && fb[f + 1] <= s) ++f;
+      next_b = f + 1 < nf ? fb[f + 1] : INT64_MAX;
+      cur_fid = fid[f];
+    }
     const int64_t e1 = STAGED ? sof[w][s + 1 - s0] : off[s + 1];
     const int n = (int)(e1 - e0);
     if (n > LCAP || n == 0) { e0 = e1; continue; }
@@ -520,11 +536,11 @@ __global__ __launch_bounds__(256) void k_emit(const int64_t* __restrict__ off, c
       int lo = 0, hi = n;  // valid events first, EV_INVALID (dedup) at the tail
       while (lo < hi) { const int m = (lo + hi) >> 1; if (S.ev[m] != EV_INVALID) lo = m + 1; else hi = m; }
       S.nv = lo;
-      emit_session(S, e0 - E0, R, L, fid[f], scn[w], spo[w], words, dbg);
+      emit_session(S, e0 - E0, sR, L, cur_fid, scn[w], spo[w], words, dbg);
     } else {
       S.ev = sev[w];
       S.nv = load_session(ev + e0, n, sev[w], nullptr, LCAP + 1);
-      emit_session(S, e0, R, L, fid[f], cnt, poff, words, dbg);
+      emit_session(S, e0, sR, L, cur_fid, cnt, poff, words, dbg);
     }
     __builtin_amdgcn_wave_barrier();
     e0 = e1;
