@@ -231,15 +231,20 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
 static int covis_emit_words(ottohip_ctx* ctx, const Front& F, const ottohip_events* ev, uint32_t* w0, hipStream_t s) {
   int ph = ctx->begin("emit", s, 8.0 * F.E + 12.0 * F.E + 4.0 * (double)F.P);
   static const int dbg = getenv("OTTOHIP_EMIT_DBG") ? atoi(getenv("OTTOHIP_EMIT_DBG")) : 0;  // profiling ablations
-  k_emit<1><<<grid_for(F.NB, 4), 256, 0, s>>>(F.off, F.first, F.NB, F.evp, F.R, F.Lt, F.fb, ev->n_files, F.fid,
-                                               F.cnt, F.poff, w0, dbg);
-  k_emit<0><<<grid_for(F.NB, 4), 256, 0, s>>>(F.off, F.first, F.NB, F.evp, F.R, F.Lt, F.fb, ev->n_files, F.fid,
-                                               F.cnt, F.poff, w0, dbg);
+  int* eerr;
+  OH_TRY(ctx->ws.get("emit_err", 4, &eerr));
+  OH_HIP(hipMemsetAsync(eerr, 0, sizeof(int), s));
+  if (F.NB > 0)
+    k_emit<<<(unsigned)F.NB, 64, 0, s>>>(F.off, F.first, F.NB, F.evp, F.R, F.Lt, F.fb, ev->n_files, F.fid, F.cnt,
+                                         F.poff, w0, eerr, dbg);
   if (F.nl > 0)
     k_emit_long<<<F.nl, 64, 0, s>>>(F.off, F.long_list, F.d_loff, F.lscr, F.lpscr, F.evp, F.R, F.Lt, F.fb,
                                      ev->n_files, F.fid, F.cnt, F.poff, w0);
   if (hipGetLastError() != hipSuccess) { set_error("k_emit launch failed"); return OTTOHIP_EHIP; }
   ctx->end(ph, s);
+  int herr = 0;
+  OH_TRY(d2h(&herr, eerr, 1, s));
+  if (herr) { set_error("emit: pairs written per event disagree with the count stage (err=%d)", herr); return OTTOHIP_EHIP; }
   return 0;
 }
 

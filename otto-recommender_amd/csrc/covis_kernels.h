@@ -470,80 +470,262 @@ __device__ __forceinline__ void emit_session(const SessView& S, int64_t e0, cons
   }
 }
 
-// One wave per 256-event block (the sessions that start in it). The block's events, pair counts
-// and word offsets are staged into LDS with three coalesced loads, so a session costs no global
-// round trips before its words are written (the per-session dependent loads made this kernel
-// latency-bound); blocks spanning more than EMIT_STAGE events take the per-session path.
-constexpr int EMIT_STAGE = 512;
-// STAGED = 1 handles blocks spanning <= EMIT_STAGE events from LDS, STAGED = 0 the others from
-// global memory (two instantiations, so each keeps plain LDS / global addressing)
-template <int STAGED>
-__global__ __launch_bounds__(256) void k_emit(const int64_t* __restrict__ off, const int64_t* __restrict__ first,
-                                              int64_t NB, const uint64_t* __restrict__ ev, RulesDev R, Layout L,
-                                              const int64_t* __restrict__ fb, int nf, const uint32_t* __restrict__ fid,
-                                              const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ poff,
-                                              uint32_t* __restrict__ words, int dbg) {
-  constexpr int SE = STAGED ? EMIT_STAGE : 1;
-  __shared__ uint64_t sev[4][STAGED ? EMIT_STAGE : LCAP];
-  __shared__ uint64_t spo[4][SE];
-  __shared__ uint32_t scn[4][SE];
-  __shared__ int64_t sof[4][STAGED ? EV_BLOCK + 2 : 1];
-  // the rule tables are indexed by per-lane event types: from LDS they cost lgkmcnt waits only;
-  // as dynamically indexed kernel arguments they were global loads whose vmcnt(0) waits also
-  // drained every outstanding word store (vmcnt counts stores on CDNA)
+// One wave per 256-event block (the sessions that start in it), processed in batches of whole
+// sessions holding <= EB_CAP events. Per batch:
+//   pass 1  events -> registers (coalesced), session of each event, per-type prefix counts
+//   pass 2  per session, its events are re-laid out in LDS as three ts-sorted lists, one per
+//           event type (a stable partition of the session's (ts, aid, type) order)
+//   pass 3  per event and (rule, next type in the rule's mask): the window [jb, je) is a
+//           binary search in that type's list, so every entry in it qualifies except the
+//           event's own run (the identity of :23-27). These segments become records
+//           (flattened start, list position, exclusion, output address); the wave then expands
+//           the records 64 pairs at a time: each lane finds its record by binary search and
+//           writes one word. Every lane writes a word in every round but the last of a flush,
+//           independent of session length or of how selective a rule's type mask is.
+// Sessions of more than LCAP events take k_emit_long.
+constexpr int EB_CAP = 512;    // events per batch (positions fit 10 bits)
+constexpr int EB_RCAP = 128;   // segment records per flush
+constexpr uint32_t EB_NONE = 1023u;
+
+struct EmitLds {
+  uint64_t tev[EB_CAP];                 // type-partitioned events of the batch
+  uint32_t rpre[EB_RCAP], rhi[EB_RCAP], rj[EB_RCAP];
+  uint64_t rout[EB_RCAP];
+  uint16_t ss[65];                      // session start (batch-relative); ss[f] = batch size
+  uint16_t sb[4][64];                   // per session: start of the type-t list; sb[3] = end of valid
+  uint16_t pst[3][64], pen[3][64];      // per-type prefix counts at session start / end
+  uint32_t sfile[64];
+  uint16_t espos[EB_CAP];               // per batch event: position in tev (EB_NONE: invalid)
+  uint8_t esid[EB_CAP];                 // per batch event: session index in the batch
+};
+
+__device__ __forceinline__ int lds_lower_ts(const uint64_t* tev, int a, int b, int64_t x) {  // first k: ts >= x
+  while (a < b) {
+    const int m = (a + b) >> 1;
+    if ((int64_t)ev_ts(tev[m]) < x) a = m + 1; else b = m;
+  }
+  return a;
+}
+__device__ __forceinline__ int lds_upper_ts(const uint64_t* tev, int a, int b, int64_t x) {  // first k: ts > x
+  while (a < b) {
+    const int m = (a + b) >> 1;
+    if ((int64_t)ev_ts(tev[m]) <= x) a = m + 1; else b = m;
+  }
+  return a;
+}
+
+// expand records [0, nrec) holding tot pairs: lane k of round c writes pair c + k
+__device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, int F, uint32_t* __restrict__ words,
+                                           int dbg) {
+  const uint32_t l = lane_id();
+  for (uint32_t c = 0; c < tot; c += 64) {
+    const uint32_t p = c + l;
+    if (p < tot) {
+      int o = 0;
+#pragma unroll
+      for (int st = EB_RCAP / 2; st >= 1; st >>= 1)
+        if (o + st < nrec && S.rpre[o + st] <= p) o += st;
+      const uint32_t off = p - S.rpre[o];
+      const uint32_t jj = S.rj[o];
+      uint32_t j = (jj & 1023u) + off;
+      if (j >= ((jj >> 10) & 1023u)) j += jj >> 21;
+      const uint32_t word = S.rhi[o] | ((uint32_t)ev_aid(S.tev[j]) << F);
+      if (!(dbg & 1)) words[S.rout[o] + off] = word;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void k_emit(const int64_t* __restrict__ off, const int64_t* __restrict__ first,
+                                             int64_t NB, const uint64_t* __restrict__ ev, RulesDev R, Layout L,
+                                             const int64_t* __restrict__ fb, int nf, const uint32_t* __restrict__ fid,
+                                             const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ poff,
+                                             uint32_t* __restrict__ words, int* __restrict__ err, int dbg) {
+  __shared__ EmitLds S;
   __shared__ RulesDev sR;
-  if (threadIdx.x == 0) sR = R;
-  __syncthreads();
-  // wave-uniform values made provably uniform: the block / session / file bookkeeping then uses
-  // scalar loads (lgkmcnt), never vmcnt waits that would drain the word stores
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
-  const int64_t g = (int64_t)blockIdx.x * 4 + w;
+  const int l = threadIdx.x;
+  if (l == 0) sR = R;
+  const int64_t g = blockIdx.x;
   if (g >= NB) return;
   const int64_t s0 = first[g], s1 = first[g + 1];
   if (s0 >= s1) return;
-  const int64_t E0 = off[s0], E1 = off[s1];
-  const bool fits = E1 - E0 <= EMIT_STAGE && s1 - s0 <= EV_BLOCK + 1;
-  if (fits != (STAGED != 0)) return;
-  if (STAGED) {
-    for (int64_t k = l; k <= s1 - s0; k += 64) sof[w][k] = off[s0 + k];
-    for (int64_t k = l; k < E1 - E0; k += 64) {
-      sev[w][k] = ev[E0 + k];
-      scn[w][k] = cnt[E0 + k];
-      spo[w][k] = poff[E0 + k];
+  const int shiftR = L.A + L.F;
+  int maxq = 0;
+#pragma unroll
+  for (int t = 0; t < 3; ++t) maxq = max(maxq, R.n_of_type[t]);
+  int fcur = file_of(fb, nf, s0);
+  int64_t next_b = fcur + 1 < nf ? fb[fcur + 1] : INT64_MAX;
+  uint32_t fid_cur = fid[fcur];
+  __syncthreads();
+
+  int64_t b = s0;
+  while (b < s1) {
+    // ---- batch: sessions [b, b + nsess) with <= EB_CAP events, none longer than LCAP
+    const int64_t base = off[b];
+    const int64_t s = b + l;
+    const bool in_s = s < s1;
+    const int64_t so = in_s ? off[s] : 0, se = in_s ? off[s + 1] : 0;
+    const bool ok = in_s && se - base <= EB_CAP && se - so <= LCAP;
+    const uint64_t bad = __ballot(!ok);
+    const int nsess = bad ? (int)__builtin_ctzll(bad) : 64;
+    if (nsess == 0) { ++b; continue; }  // session b is long (k_emit_long)
+    const int nb_ev = (int)(__shfl((int)(se - base), nsess - 1));
+    const int64_t E0 = base;
+    if (l < nsess) S.ss[l] = (uint16_t)(so - base);
+    if (l == 0) S.ss[nsess] = (uint16_t)nb_ev;
+    // file of every session (one file for the whole batch unless a file boundary is crossed)
+    const int64_t s_last = b + nsess - 1;
+    if (s_last < next_b) {
+      if (l < nsess) S.sfile[l] = fid_cur;
+    } else {
+      int fk = fcur;
+      if (l < nsess) {
+        while (fk + 1 < nf && fb[fk + 1] <= s) ++fk;
+        S.sfile[l] = fid[fk];
+      }
+      fcur = __shfl(fk, nsess - 1);
+      next_b = fcur + 1 < nf ? fb[fcur + 1] : INT64_MAX;
+      fid_cur = fid[fcur];
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  }
-  int f = file_of(fb, nf, s0);
-  // file of the session: reloaded only when a file boundary is crossed (a per-session global
-  // load would wait on vmcnt and so drain the previous session's word stores)
-  int64_t next_b = f + 1 < nf ? fb[f + 1] : INT64_MAX;
-  uint32_t cur_fid = fid[f];
-  int64_t e0 = E0;
-  for (int64_t s = s0; s < s1; ++s) {
-    if (s >= next_b) {
-      while (f + 1 < nf && fb[f + 1] <= s) ++f;
-      next_b = f + 1 < nf ? fb[f + 1] : INT64_MAX;
-      cur_fid = fid[f];
+
+    // ---- pass 1: events, sessions, per-type prefixes
+    constexpr int NCH = EB_CAP / 64;
+    const int nch = (nb_ev + 63) >> 6;
+    uint64_t vv[NCH];
+    uint32_t sid[NCH], pr[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int idx = c * 64 + l;
+      vv[c] = (c < nch && idx < nb_ev) ? ev[E0 + idx] : EV_INVALID;
     }
-    const int64_t e1 = STAGED ? sof[w][s + 1 - s0] : off[s + 1];
-    const int n = (int)(e1 - e0);
-    if (n > LCAP || n == 0) { e0 = e1; continue; }
-    SessView S;
-    S.pref = nullptr; S.pstride = LCAP + 1;
-    if (STAGED) {
-      S.ev = sev[w] + (e0 - E0);
-      int lo = 0, hi = n;  // valid events first, EV_INVALID (dedup) at the tail
-      while (lo < hi) { const int m = (lo + hi) >> 1; if (S.ev[m] != EV_INVALID) lo = m + 1; else hi = m; }
-      S.nv = lo;
-      emit_session(S, e0 - E0, sR, L, cur_fid, scn[w], spo[w], words, dbg);
-    } else {
-      S.ev = sev[w];
-      S.nv = load_session(ev + e0, n, sev[w], nullptr, LCAP + 1);
-      emit_session(S, e0, sR, L, cur_fid, cnt, poff, words, dbg);
+    uint32_t base0 = 0, base1 = 0, base2 = 0;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      if (c >= nch) break;
+      const int idx = c * 64 + l;
+      const bool in = idx < nb_ev;
+      const int t = in ? ev_type(vv[c]) : 3;
+      int k = 0;
+#pragma unroll
+      for (int st = 32; st >= 1; st >>= 1)
+        if (k + st < nsess && (int)S.ss[k + st] <= idx) k += st;
+      const uint64_t m0 = __ballot(t == 0), m1 = __ballot(t == 1), m2 = __ballot(t == 2);
+      const uint32_t P0 = base0 + mbcnt(m0), P1 = base1 + mbcnt(m1), P2 = base2 + mbcnt(m2);
+      if (in && idx == (int)S.ss[k]) { S.pst[0][k] = P0; S.pst[1][k] = P1; S.pst[2][k] = P2; }
+      if (in && idx == (int)S.ss[k + 1] - 1) {
+        S.pen[0][k] = P0 + (t == 0); S.pen[1][k] = P1 + (t == 1); S.pen[2][k] = P2 + (t == 2);
+      }
+      base0 += (uint32_t)__popcll(m0); base1 += (uint32_t)__popcll(m1); base2 += (uint32_t)__popcll(m2);
+      sid[c] = (uint32_t)k;
+      pr[c] = t == 0 ? P0 : (t == 1 ? P1 : P2);
     }
     __builtin_amdgcn_wave_barrier();
-    e0 = e1;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (l < nsess) {
+      const uint32_t a = S.ss[l];
+      if (S.ss[l + 1] > a) {
+        const uint32_t c0 = S.pen[0][l] - S.pst[0][l], c1 = S.pen[1][l] - S.pst[1][l], c2 = S.pen[2][l] - S.pst[2][l];
+        S.sb[0][l] = a; S.sb[1][l] = a + c0; S.sb[2][l] = a + c0 + c1; S.sb[3][l] = a + c0 + c1 + c2;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // ---- pass 2: type-partitioned lists
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      if (c >= nch) break;
+      const int idx = c * 64 + l;
+      const int t = ev_type(vv[c]);
+      if (idx < nb_ev) {
+        uint32_t pos = EB_NONE;
+        if (t < 3) {
+          const uint32_t k = sid[c];
+          pos = S.sb[t][k] + pr[c] - S.pst[t][k];
+          S.tev[pos] = vv[c];
+        }
+        S.espos[idx] = (uint16_t)pos;
+        S.esid[idx] = (uint8_t)sid[c];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // ---- pass 3: segments -> records -> words
+    int nrec = 0;
+    uint32_t tot = 0;
+#pragma unroll 1
+    for (int c = 0; c < nch; ++c) {
+      const int idx = c * 64 + l;
+      const bool in = idx < nb_ev;
+      const uint32_t sp = in ? S.espos[idx] : EB_NONE;
+      const bool valid = sp != EB_NONE;
+      const uint64_t v = valid ? S.tev[sp] : EV_INVALID;
+      const int t = ev_type(v);
+      const uint32_t k = in ? S.esid[idx] : 0u;
+      const uint64_t eout = valid ? poff[E0 + idx] : 0;
+      const uint32_t ecnt = valid ? cnt[E0 + idx] : 0;
+      const int64_t tsi = ev_ts(v);
+      const uint32_t file = S.sfile[k];
+      // the event's own run in its list (exact twins stay adjacent when dedup is off)
+      uint32_t rlo = sp, rhi = sp + 1;
+      if (valid) {
+        const uint32_t lb = S.sb[t][k], ub = S.sb[t + 1][k];
+        while (rlo > lb && S.tev[rlo - 1] == v) --rlo;
+        while (rhi < ub && S.tev[rhi] == v) ++rhi;
+      }
+      const int nq = valid ? sR.n_of_type[t] : 0;
+      uint32_t eo = 0;
+#pragma unroll 1
+      for (int q = 0; q < maxq; ++q) {
+        const int r = q < nq ? sR.rule_of_type[t][q] : 0;
+        const uint32_t msk = q < nq ? sR.mask[r] : 0u;
+        const int32_t lo = sR.lo[r], hi = sR.hi[r];
+#pragma unroll 1
+        for (int tt = 0; tt < 3; ++tt) {
+          const bool act = (msk >> tt) & 1u;
+          if (!__ballot(act)) continue;
+          uint32_t len = 0, jb = 0, xlo = EB_NONE, xlen = 0;
+          if (act) {
+            const int a = S.sb[tt][k], e = S.sb[tt + 1][k];
+            jb = (uint32_t)lds_lower_ts(S.tev, a, e, tsi + lo);
+            const uint32_t je = (uint32_t)lds_upper_ts(S.tev, (int)jb, e, tsi + hi);
+            len = je - jb;
+            if (tt == t && lo <= 0 && hi >= 0) { xlo = rlo; xlen = rhi - rlo; len -= xlen; }
+          }
+          const uint64_t m = __ballot(len > 0);
+          const int nn = (int)__popcll(m);
+          if (nn == 0) continue;
+          if (nrec + nn > EB_RCAP) {
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            emit_flush(S, nrec, tot, L.F, words, dbg);
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            nrec = 0; tot = 0;
+          }
+          const uint32_t incl = wave_incl_scan(len);
+          if (len > 0) {
+            const int ri = nrec + (int)mbcnt(m);
+            S.rpre[ri] = tot + incl - len;
+            S.rhi[ri] = ((uint32_t)q << shiftR) | file;
+            S.rj[ri] = jb | (xlo << 10) | (xlen << 21);
+            S.rout[ri] = eout + eo;
+          }
+          eo += len;
+          nrec += nn;
+          tot += __shfl(incl, 63);
+        }
+      }
+      if (valid && eo != ecnt) atomicOr(err, 4);
+    }
+    if (nrec > 0) {
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      emit_flush(S, nrec, tot, L.F, words, dbg);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    b += nsess;
   }
 }
 
