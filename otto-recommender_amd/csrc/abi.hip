@@ -96,8 +96,8 @@ static int setup_rules(const ottohip_rule* rules, int n_rules, const ottohip_cov
   Lt.BR = bits_for((uint64_t)max_per_type);
   Lt.WB = Lt.BR + Lt.A + Lt.F;
   Lt.amask = (1u << Lt.A) - 1u;
-  if (Lt.WB > 32) {
-    set_error("word layout %d rule + %d aid + %d file bits > 32: reduce files per call", Lt.BR, Lt.A, Lt.F);
+  if (Lt.WB > 31) {  // W_EMPTY (all ones) must stay above every word
+    set_error("word layout %d rule + %d aid + %d file bits > 31: reduce files per call", Lt.BR, Lt.A, Lt.F);
     return OTTOHIP_ELIMIT;
   }
   return 0;
@@ -302,9 +302,20 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     if ((rc = d2h(nlist, lcount, N_SORT + 2, s))) return rc;
     if ((rc = d2h(&herr, err, 1, s))) return rc;
     if (herr) { set_error("task list overflow / row too large (err=%d)", herr); return OTTOHIP_ELIMIT; }
-    if (dbg)
+    if (dbg) {
       fprintf(stderr, "[ottohip] level %d: sort %llu/%llu/%llu/%llu/%llu hash %llu split %llu\n", level, nlist[0],
               nlist[1], nlist[2], nlist[3], nlist[4], nlist[N_SORT], nlist[N_SORT + 1]);
+      Task* lists[N_SORT + 2] = {TL.sort[0], TL.sort[1], TL.sort[2], TL.sort[3], TL.sort[4], TL.hash, TL.split};
+      fprintf(stderr, "[ottohip] level %d words:", level);
+      for (int c = 0; c < N_SORT + 2; ++c) {
+        std::vector<Task> tv(nlist[c]);
+        if (nlist[c]) (void)d2h(tv.data(), lists[c], nlist[c], s);
+        unsigned long long sw = 0, mx = 0;
+        for (auto& t : tv) { sw += t.len; mx = std::max<unsigned long long>(mx, t.len); }
+        fprintf(stderr, " %llu(max %llu)", sw, mx);
+      }
+      fprintf(stderr, "\n");
+    }
     const unsigned sgrid = (unsigned)ctx->n_cu * 32;
 #define OH_SORT(c, M)                                                                                      \
     if (nlist[c])                                                                                          \
@@ -342,10 +353,10 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
         (rc = ws.get("sp_dcur", (size_t)ndig, &dcur)))
       return rc;
     hipMemsetAsync(dcount, 0, ndig * 4, s);
-    k_split_hist<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, dgb, w0, w1, Lt.WB, dcount);
+    k_split_hist<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, dgb, w0, w1, Lt.F, dcount);
     if ((rc = exclusive_scan_u32(ctx, dcount, doff, ndig, nullptr, s))) return rc;
     k_split_cursor<<<grid_for(ns * 64), 256, 0, s>>>(cur_split, ns, dgb, doff, dcur, Lt.WB);
-    k_split_scatter<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, dgb, w0, w1, Lt.WB, dcur);
+    k_split_scatter<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, dgb, w0, w1, Lt.F, dcur);
     // next lists (a sub-bucket is one task in exactly one list: ndig bounds every list)
     const uint64_t capn = (uint64_t)ndig;
     if ((rc = get_lists(std::max(cap0, capn), srcA ? "t_splitB" : "t_splitA"))) return rc;

@@ -8,11 +8,14 @@
 //               row key = (type_i, aid_i)
 //   S3 rows     stable LSD radix sort of events by row key; exclusive scan of counts gives
 //               each event its run of output words: rows (aid-major) are contiguous
-//   S4 emit     wave per block of sessions, 16-lane subgroups per event: write one u32 word
+//   S4 emit     wave per block of sessions, batches of whole sessions: events re-laid out in
+//               LDS as per-type ts-sorted lists, so a (rule, next type) window is one contiguous
+//               range; the ranges are expanded 64 pairs per round, one u32 word
 //               (rule | aid_next | file) per qualifying pair at its row position
-//   S5 reduce   rows <= 64 words: one wave; <= 2048 words: one workgroup, two-phase LDS hash
-//               (per-file counts, then folded over files); larger rows: MSD split by the
-//               word's top bits (256-way) until buckets fit
+//   S5 reduce   rows <= 1024 words: one wave, register bitonic sort + run-length scans
+//               (per-file counts folded over files); larger rows: split 2^k-way by a hash of
+//               the word's (rule, aid_next) part; split buckets still above 1024 words go to a
+//               workgroup LDS hash (overflow: split again with the next level's hash)
 // Output: per (rule, aid, aid_next): count (sum over files), count_ge2 (sum of per-file
 // counts >= 2) and per-rule file-row statistics for the merge rule of :131-135.
 #pragma once
@@ -22,11 +25,7 @@ namespace ottohip {
 
 constexpr int EV_BLOCK = 256;     // events per wave block (sessions starting in it)
 constexpr int LCAP = 512;         // sessions up to LCAP events run from LDS
-constexpr int TINY = 64;          // rows/buckets up to TINY words: one wave, in registers
-constexpr int WAVE_MAX = 512;     // up to WAVE_MAX words: one wave, LDS hash (16 KiB per wave)
-constexpr int SMALL = 2048;       // up to SMALL words: one workgroup, LDS hash
-constexpr int SPLIT_TARGET = 256; // split buckets aim at this many words
-constexpr int HASH_REM = 11;      // buckets whose remaining key bits <= 11 hash directly
+constexpr int SPLIT_TARGET = 512; // hashed split buckets aim at this many words
 constexpr uint32_t W_EMPTY = 0xFFFFFFFFu;
 constexpr int STAT_STRIPES = 256;            // copies of the per-rule statistics
 constexpr int STAT_STRIDE = MAX_RULES * 4;   // u64 per copy (256 B: one L2 line pair per stripe)
@@ -804,52 +803,6 @@ struct RuleAcc {
   }
 };
 
-// one wave per task with len <= 64
-__global__ __launch_bounds__(256) void k_agg_tiny(const Task* __restrict__ tasks, int64_t n_tasks,
-                                                  const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
-                                                  const uint32_t* __restrict__ row_key, RulesDev R, Layout L,
-                                                  int n_rules, OutRows O) {
-  const int l = lane_id();
-  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  RuleAcc acc;
-  acc.zero();
-  for (int64_t ti = gw; ti < n_tasks; ti += nw) {
-    const Task T = tasks[ti];
-    const int len = (int)T.len;
-    const uint32_t* W = T.buf ? w1 : w0;
-    const uint32_t w = l < len ? W[T.begin + l] : W_EMPTY;
-    // per-file count of this word and first-occurrence flag
-    uint32_t cf = 0; bool first = l < len;
-    for (int j = 0; j < len; ++j) {
-      const uint32_t u = __shfl(w, j);
-      cf += u == w;
-      first &= !(u == w && j < l);
-    }
-    const uint32_t k2 = w >> L.F;
-    uint32_t call = 0, c2 = 0, nf = 0; bool firstk = true;
-    const uint64_t fm = __ballot(first);
-    for (int j = 0; j < len; ++j) {
-      if (!((fm >> j) & 1ull)) continue;  // wave-uniform skip
-      const uint32_t u = __shfl(w, j);
-      const uint32_t cj = __shfl(cf, j);
-      if ((u >> L.F) == k2) {
-        call += cj; c2 += cj >= 2 ? cj : 0; nf += 1u + ((cj >= 2 ? 1u : 0u) << 16);
-        firstk &= !(j < l);
-      }
-    }
-    const bool emit = first && firstk;
-    const uint64_t m = __ballot(emit);
-    const RowInfo ri = row_info(row_key, T.row, L.A);
-    if (emit) {  // a task's outputs (<= its words) go to its own word range: no cursor
-      const int rule = R.rule_of_type[ri.type][k2 >> L.A];
-      put_row(O, T.begin + mbcnt(m), rule, ri.aid, (int32_t)(k2 & L.amask), call, c2);
-      acc.add(rule, call, nf);
-    }
-  }
-  acc.flush(O.stats, n_rules);
-}
-
 // one workgroup per task: LDS hash of (rule|aid_next|file) counts, then folded over files.
 // Phase A slots: u64 (word << 32 | count); phase B: u64 (key2 << 32 | count) + u64 (count_ge2 << 32 | nf2 << 16 | nf1)
 constexpr int AGG_T = 256;
@@ -859,28 +812,7 @@ constexpr unsigned long long SLOT_EMPTY = 0xFFFFFFFF00000000ull;
 __device__ __forceinline__ unsigned long long lds_load(unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// Open addressing with linear probing over u64 slots (key << 32 | count). Returns the slot, or
-// HASH_FULL after probing every slot (the caller sends the task to a split: never spins).
-constexpr uint32_t HASH_FULL = 0xFFFFFFFFu;
-__device__ __forceinline__ uint32_t hash_insert(unsigned long long* slots, uint32_t key, uint32_t inc, uint32_t cm,
-                                                bool* created = nullptr) {
-  uint32_t h = hslot(key, cm);
-  unsigned long long v = lds_load(&slots[h]);
-  for (uint32_t probes = 0; probes <= cm;) {
-    const uint32_t k = (uint32_t)(v >> 32);
-    if (k == key) { atomicAdd(&slots[h], (unsigned long long)inc); return h; }
-    if (k == W_EMPTY) {
-      const unsigned long long old = atomicCAS(&slots[h], v, ((unsigned long long)key << 32) | inc);
-      if (old == v) { if (created) *created = true; return h; }
-      v = old;  // lost the race: look at what the winner wrote
-      continue;
-    }
-    h = (h + 1) & cm;
-    ++probes;
-    v = lds_load(&slots[h]);
-  }
-  return HASH_FULL;
-}
+constexpr uint32_t HASH_FULL = 0xFFFFFFFFu;  // hash_insert_batch: table full
 
 // ---- register sort path: one wave per task of <= 64*M words, no LDS, no atomics
 __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
@@ -939,91 +871,164 @@ __device__ __forceinline__ void wave_scan_elems(uint32_t (&x)[M]) {
   for (int m = 0; m < M; ++m) x[m] = MAX ? (x[m] > excl ? x[m] : excl) : x[m] + excl;
 }
 
+// exclusive value before element e = lane*M + m of a per-element inclusive prefix x
+template <int M>
+__device__ __forceinline__ uint32_t excl_at(const uint32_t (&x)[M], int m, uint32_t lane_prev_tot) {
+  return m > 0 ? x[m - 1] : lane_prev_tot;
+}
+
+// One wave per task of <= 64*M words (rows and split buckets): bitonic sort in registers, then
+// run-length folding with prefix / max scans only (no LDS, no atomics on the data path).
+//   w-runs (equal words = one (rule, aid_next, file)): per-file count cf
+//   k-runs (equal rule|aid_next): count = sum cf, count_ge2 = sum of cf >= 2,
+//                                 nf1 = w-runs, nf2 = w-runs with cf >= 2
+// The next task's words are loaded while the current one is folded. Per-rule statistics go
+// through a per-wave LDS accumulator (one lane, after wave sums of packed 16-bit fields: a
+// task holds <= 1024 words), so no per-thread accumulator arrays take registers.
 template <int M>
 __global__ __launch_bounds__(256) void k_agg_sort(const Task* __restrict__ tasks, int64_t n_tasks,
                                                   const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
                                                   const uint32_t* __restrict__ row_key, RulesDev R, Layout L,
                                                   int n_rules, OutRows O) {
+  __shared__ unsigned long long sacc[4][MAX_RULES * 4];
+  __shared__ RulesDev sR;
   const uint32_t l = lane_id();
-  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) sR = R;
+  for (int i = (int)l; i < MAX_RULES * 4; i += 64) sacc[wv][i] = 0;
+  __syncthreads();
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  RuleAcc acc;
-  acc.zero();
-  for (int64_t ti = gw; ti < n_tasks; ti += nw) {
-    const Task T = tasks[ti];
-    const uint32_t* W = (T.buf ? w1 : w0) + T.begin;
-    uint32_t v[M];
+  int64_t ti = __builtin_amdgcn_readfirstlane((int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+  const int F = L.F, A = L.A;
+  uint32_t v[M];
+  Task T;
+  uint32_t rk = 0;
+  auto fetch = [&](int64_t t, Task& TT, uint32_t (&vv)[M], uint32_t& rkk) {
+    TT = tasks[t];
+    const uint32_t* W = (TT.buf ? w1 : w0) + TT.begin;
 #pragma unroll
     for (int m = 0; m < M; ++m) {  // coalesced load (element m*64 + l), then sorted anyway
       const uint32_t i = (uint32_t)(m * 64) + l;
-      v[m] = i < T.len ? W[i] : W_EMPTY;
+      vv[m] = i < TT.len ? W[i] : W_EMPTY;
     }
+    rkk = row_key[TT.row];
+  };
+  if (ti < n_tasks) fetch(ti, T, v, rk);
+  while (ti < n_tasks) {
+    const int64_t tn = ti + nw;
+    Task Tn;
+    uint32_t vn[M];
+    uint32_t rkn = 0;
+    if (tn < n_tasks) fetch(tn, Tn, vn, rkn);
+    const uint32_t len = T.len;
     wave_bitonic_sort<M>(v);
-    // neighbours: previous element (e-1) and next element (e+1)
-    uint32_t prv[M], nxt[M];
+    const uint32_t pl = __shfl_up(v[M - 1], 1), nl = __shfl_down(v[0], 1);
+    // (1) per-file count cf: start of the element's w-run by a max scan
+    uint32_t a[M], b[M], c[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const uint32_t e = l * M + m;
+      const uint32_t prv = m > 0 ? v[m - 1] : pl;
+      a[m] = (e < len && (e == 0 || prv != v[m])) ? e + 1 : 0u;
+    }
+    wave_scan_elems<M, true>(a);
+    // (2) X = cf | cf_ge2 << 16 and Y = 1 | ge2 << 16 at each w-run end
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const uint32_t e = l * M + m;
+      const uint32_t nxt = m < M - 1 ? v[m + 1] : nl;
+      const bool wend = e < len && (e + 1 == len || nxt != v[m]);
+      const uint32_t cf = e + 2 - a[m];
+      b[m] = wend ? (cf | ((cf >= 2 ? cf : 0u) << 16)) : 0u;
+      c[m] = wend ? (1u | ((cf >= 2 ? 1u : 0u) << 16)) : 0u;
+    }
+    // (3) k-run sums: inclusive prefix minus the prefix before the k-run's start (max scan)
+    wave_scan_elems<M, false>(b);
     {
-      const uint32_t pl = __shfl_up(v[M - 1], 1), nl = __shfl_down(v[0], 1);
+      const uint32_t lt = __shfl_up(b[M - 1], 1), lprev = l == 0 ? 0u : lt;
 #pragma unroll
       for (int m = 0; m < M; ++m) {
-        prv[m] = m > 0 ? v[m - 1] : (l == 0 ? W_EMPTY : pl);
-        nxt[m] = m < M - 1 ? v[m + 1] : (l == 63 ? W_EMPTY : nl);
+        const uint32_t e = l * M + m;
+        const uint32_t prv = m > 0 ? v[m - 1] : pl;
+        a[m] = (e < len && (e == 0 || (prv >> F) != (v[m] >> F))) ? excl_at<M>(b, m, lprev) : 0u;
       }
     }
-    // w-runs: start index scan; count at each run end
-    uint32_t st[M];
+    wave_scan_elems<M, true>(a);
 #pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const uint32_t e = l * M + m;
-      const bool start = v[m] != W_EMPTY && (e == 0 || prv[m] != v[m]);
-      st[m] = start ? e + 1 : 0;  // +1 so that 0 means "none"
+    for (int m = 0; m < M; ++m) b[m] -= a[m];
+    wave_scan_elems<M, false>(c);
+    {
+      const uint32_t lt = __shfl_up(c[M - 1], 1), lprev = l == 0 ? 0u : lt;
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const uint32_t e = l * M + m;
+        const uint32_t prv = m > 0 ? v[m - 1] : pl;
+        a[m] = (e < len && (e == 0 || (prv >> F) != (v[m] >> F))) ? excl_at<M>(c, m, lprev) : 0u;
+      }
     }
-    wave_scan_elems<M, true>(st);
-    uint32_t X[M], Y[M];
+    wave_scan_elems<M, true>(a);
 #pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const uint32_t e = l * M + m;
-      const bool wend = v[m] != W_EMPTY && nxt[m] != v[m];
-      const uint32_t cf = e + 2 - st[m];  // e - start + 1
-      X[m] = wend ? (cf | ((cf >= 2 ? cf : 0u) << 16)) : 0u;
-      Y[m] = wend ? (1u | ((cf >= 2 ? 1u : 0u) << 16)) : 0u;
-    }
-    // fold per-file counts over (rule, aid_next) runs: prefix sums minus the value before the run
-    uint32_t PX[M], PY[M], BX[M], BY[M];
-#pragma unroll
-    for (int m = 0; m < M; ++m) { PX[m] = X[m]; PY[m] = Y[m]; }
-    wave_scan_elems<M, false>(PX);
-    wave_scan_elems<M, false>(PY);
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const uint32_t e = l * M + m;
-      const bool kstart = v[m] != W_EMPTY && (e == 0 || (prv[m] >> L.F) != (v[m] >> L.F));
-      BX[m] = kstart ? PX[m] - X[m] : 0u;
-      BY[m] = kstart ? PY[m] - Y[m] : 0u;
-    }
-    wave_scan_elems<M, true>(BX);
-    wave_scan_elems<M, true>(BY);
-    const RowInfo ri = row_info(row_key, T.row, L.A);
+    for (int m = 0; m < M; ++m) c[m] -= a[m];
+    // (4) one output row per k-run end, written into the task's own word range
+    const int type = (int)(rk >> A);
+    const int32_t aid = (int32_t)(rk & ((1u << A) - 1u));
     uint32_t nmine = 0;
-    bool kend[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      kend[m] = v[m] != W_EMPTY && (nxt[m] == W_EMPTY || (nxt[m] >> L.F) != (v[m] >> L.F));
-      nmine += kend[m];
+      const uint32_t e = l * M + m;
+      const uint32_t nxt = m < M - 1 ? v[m + 1] : nl;
+      nmine += (e < len && (e + 1 == len || (nxt >> F) != (v[m] >> F))) ? 1u : 0u;
     }
     const uint32_t incl = wave_incl_scan(nmine);
     uint64_t p = T.begin + incl - nmine;
+    const int nq = sR.n_of_type[type];
+    uint32_t s0a = 0, s0b = 0, s1a = 0, s1b = 0;  // local rules 0 / 1: rows | nf1 << 16, pairs | nf2 << 16
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      if (!kend[m]) continue;
-      const uint32_t sx = PX[m] - BX[m], sy = PY[m] - BY[m];
-      const uint32_t k2 = v[m] >> L.F;
-      const int rule = R.rule_of_type[ri.type][k2 >> L.A];
-      const uint32_t c = sx & 0xFFFFu, c2 = sx >> 16;
-      put_row(O, p++, rule, ri.aid, (int32_t)(k2 & L.amask), c, c2);
-      acc.add(rule, c, sy);
+      const uint32_t e = l * M + m;
+      const uint32_t nxt = m < M - 1 ? v[m + 1] : nl;
+      if (!(e < len && (e + 1 == len || (nxt >> F) != (v[m] >> F)))) continue;
+      const uint32_t k2 = v[m] >> F;
+      const uint32_t q = k2 >> A;
+      const uint32_t cnt = b[m] & 0xFFFFu, c2 = b[m] >> 16;
+      put_row(O, p++, sR.rule_of_type[type][q], aid, (int32_t)(k2 & L.amask), cnt, c2);
+      const uint32_t ra = 1u | ((c[m] & 0xFFFFu) << 16), rb = cnt | (c[m] & 0xFFFF0000u);
+      if (q == 0) { s0a += ra; s0b += rb; } else if (q == 1) { s1a += ra; s1b += rb; }
     }
+    // per-rule statistics (local rules >= 2 are recounted here: only with > 2 rules per type)
+    for (int q = 0; q < nq; ++q) {
+      uint32_t sa = q == 0 ? s0a : s1a, sb = q == 0 ? s0b : s1b;
+      if (q >= 2) {
+        sa = 0; sb = 0;
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          const uint32_t e = l * M + m;
+          const uint32_t nxt = m < M - 1 ? v[m + 1] : nl;
+          if (!(e < len && (e + 1 == len || (nxt >> F) != (v[m] >> F)))) continue;
+          if ((v[m] >> F) >> A != (uint32_t)q) continue;
+          sa += 1u | ((c[m] & 0xFFFFu) << 16);
+          sb += (b[m] & 0xFFFFu) | (c[m] & 0xFFFF0000u);
+        }
+      }
+      sa = wave_sum(sa);
+      sb = wave_sum(sb);
+      if (l == 0 && sa) {
+        unsigned long long* acc = sacc[wv] + sR.rule_of_type[type][q] * 4;
+        acc[0] += sa & 0xFFFFu; acc[1] += sb & 0xFFFFu; acc[2] += sa >> 16; acc[3] += sb >> 16;
+      }
+    }
+    T = Tn;
+    rk = rkn;
+#pragma unroll
+    for (int m = 0; m < M; ++m) v[m] = vn[m];
+    ti = tn;
   }
-  acc.flush(O.stats, n_rules);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const uint32_t gwave = blockIdx.x * (blockDim.x >> 6) + wv;
+  unsigned long long* stats = O.stats + (size_t)(gwave & (STAT_STRIPES - 1)) * STAT_STRIDE;
+  for (int i = (int)l; i < n_rules * 4; i += 64)
+    if (sacc[wv][i]) atomicAdd(&stats[i], sacc[wv][i]);
 }
 
 // Task lists filled by classification kernels (wave-aggregated pushes)
@@ -1073,113 +1078,6 @@ __device__ __forceinline__ uint32_t hash_insert_batch(unsigned long long* slots,
   return created;
 }
 
-// one wave per task with TINY < len <= WAVE_MAX: words prefetched to registers, private LDS
-// region per wave (no workgroup barriers), two-phase hash as k_agg_hash
-constexpr int WCAP = 1024;  // phase-A slots per wave (phase B uses 2 * WCAP u64)
-__global__ __launch_bounds__(256) void k_agg_wave(const Task* __restrict__ tasks, int64_t n_tasks,
-                                                  const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
-                                                  const uint32_t* __restrict__ row_key, RulesDev R, Layout L,
-                                                  int n_rules, OutRows O) {
-  __shared__ unsigned long long lds[4][2 * WCAP];  // 64 KiB: 16 KiB per wave
-  const int l = lane_id();
-  const int wv = threadIdx.x >> 6;
-  unsigned long long* A = lds[wv];
-  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  RuleAcc acc;
-  acc.zero();
-  constexpr int NW = WAVE_MAX / 64;  // words per lane
-  for (int64_t ti = gw; ti < n_tasks; ti += nw) {
-    const Task T = tasks[ti];
-    const uint32_t* W = (T.buf ? w1 : w0) + T.begin;
-    uint32_t w[NW];
-#pragma unroll
-    for (int j = 0; j < NW; ++j) {
-      const uint32_t i = (uint32_t)(l + 64 * j);
-      w[j] = i < T.len ? W[i] : W_EMPTY;
-    }
-    uint32_t dbound = T.len;
-    if (T.rem < 31 && (1u << T.rem) < dbound) dbound = 1u << T.rem;
-    uint32_t cap = 64;
-    while (cap < 2 * dbound) cap <<= 1;
-    const uint32_t cm = cap - 1;
-    for (uint32_t i = l; i < cap; i += 64) A[i] = SLOT_EMPTY;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    {
-      uint32_t inc[NW], slot[NW];
-#pragma unroll
-      for (int j = 0; j < NW; ++j) {  // a wave-uniform word becomes one add of the wave's count
-        const bool act = w[j] != W_EMPTY;
-        const uint32_t wu = __builtin_amdgcn_readfirstlane(w[j]);
-        const uint64_t am = __ballot(act);
-        inc[j] = 1u;
-        if (am && __ballot(act && w[j] == wu) == am) {
-          inc[j] = (uint32_t)__popcll(am);
-          if (l != 0) w[j] = W_EMPTY;
-        }
-      }
-      hash_insert_batch<NW>(A, w, inc, cm, slot);
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    constexpr int SL = WCAP / 64;  // 16
-    uint32_t kw[SL], kc[SL];
-#pragma unroll
-    for (int q = 0; q < SL; ++q) {
-      const uint32_t slot = (uint32_t)(l + 64 * q);
-      const unsigned long long v = slot < cap ? lds_load(&A[slot]) : SLOT_EMPTY;
-      kw[q] = (uint32_t)(v >> 32);
-      kc[q] = (uint32_t)v;
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    unsigned long long* B = A;
-    unsigned long long* B2 = A + cap;
-    for (uint32_t i = l; i < cap; i += 64) { B[i] = SLOT_EMPTY; B2[i] = 0; }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-#pragma unroll
-    for (int q0 = 0; q0 < SL; q0 += 8) {
-      uint32_t k2[8], c8[8], slot[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        k2[j] = kw[q0 + j] == W_EMPTY ? W_EMPTY : kw[q0 + j] >> L.F;
-        c8[j] = kc[q0 + j];
-      }
-      if (64u * q0 >= cap) break;
-      hash_insert_batch<8>(B, k2, c8, cm, slot);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (slot[j] == HASH_FULL) continue;
-        const uint32_t c = c8[j];
-        atomicAdd(&B2[slot[j]], ((unsigned long long)(c >= 2 ? c : 0u) << 32) | 1ull | ((c >= 2 ? 1ull : 0ull) << 16));
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    const RowInfo ri = row_info(row_key, T.row, L.A);
-    uint64_t p = T.begin;
-    for (uint32_t i0 = 0; i0 < cap; i0 += 64) {
-      const uint32_t i = i0 + l;
-      const unsigned long long v = lds_load(&B[i]);
-      const uint32_t k2 = (uint32_t)(v >> 32);
-      const bool valid = k2 != W_EMPTY;
-      const uint64_t m = __ballot(valid);
-      if (valid) {
-        const unsigned long long v2 = lds_load(&B2[i]);
-        const int rule = R.rule_of_type[ri.type][k2 >> L.A];
-        const uint32_t c = (uint32_t)v, c2 = (uint32_t)(v2 >> 32), nf = (uint32_t)v2;
-        put_row(O, p + mbcnt(m), rule, ri.aid, (int32_t)(k2 & L.amask), c, c2);
-        acc.add(rule, c, nf);
-      }
-      p += (uint64_t)__popcll(m);
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-  acc.flush(O.stats, n_rules);
-}
-
 constexpr int N_SORT = 5;  // register-sort classes: 64, 128, 256, 512, 1024 words
 constexpr int SORT_MAX = 64 << (N_SORT - 1);
 struct TaskLists {
@@ -1204,8 +1102,7 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
   for (int64_t ti = blockIdx.x; ti < n_tasks; ti += gridDim.x) {
     const Task T = tasks[ti];
     const uint32_t* W = (T.buf ? w1 : w0) + T.begin;
-    uint32_t dbound = T.len;
-    if (T.rem < 31 && (1u << T.rem) < dbound) dbound = 1u << T.rem;
+    const uint32_t dbound = T.len;
     // optimistic: more keys possible than fit; give up at 3/4 fill and send the task to a split
     const bool optimistic = 2 * dbound > (uint32_t)HCAP;
     uint32_t cap = 64;
@@ -1318,23 +1215,24 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
 // ---- classification of rows and split buckets into task lists
 
 // class of a task: [0, N_SORT) register sort of <= 64 << c words; N_SORT workgroup hash
-// (bounded key range, or a split bucket that stayed large: skewed, hashed optimistically and
-// sent back to a split on overflow); N_SORT + 1 split (rows)
-__device__ __forceinline__ int task_class(uint64_t len, uint32_t rem, bool is_row) {
+// (a split bucket that stayed far above its expected size: skewed towards a few hot keys,
+// hashed optimistically and sent back to a split on overflow); N_SORT + 1 split (rows, and
+// buckets that are large only because the parent needed more than one split's digits).
+constexpr int SPLIT_LEVELS = 4;
+__device__ __forceinline__ int task_class(uint64_t len, uint32_t level, bool split) {
   for (int c = 0; c < N_SORT; ++c)
     if (len <= (uint64_t)(64 << c)) return c;
-  if (rem <= (uint32_t)HASH_REM || !is_row) return N_SORT;
-  return N_SORT + 1;
+  return (split && level < (uint32_t)SPLIT_LEVELS) ? N_SORT + 1 : N_SORT;
 }
 // Block-aggregated push: every thread of the (256-thread) block must call it once. Per list:
 // LDS counter per block, then one device atomic per list per block.
 constexpr int N_LISTS = N_SORT + 2;
 __device__ __forceinline__ void push_task_block(const TaskLists& TL, bool valid, uint64_t begin, uint64_t len,
-                                                uint32_t row, uint32_t rem, uint32_t buf, bool is_row, int* err) {
+                                                uint32_t row, uint32_t rem, uint32_t buf, bool split, int* err) {
   __shared__ uint32_t bcnt[N_LISTS];
   __shared__ unsigned long long bbase[N_LISTS];
   if (valid && len > 0xFFFFFFFFull) { atomicOr(err, 2); valid = false; }
-  const int c = valid ? task_class(len, rem, is_row) : -1;
+  const int c = valid ? task_class(len, rem, split) : -1;
   if (threadIdx.x < N_LISTS) bcnt[threadIdx.x] = 0;
   __syncthreads();
   uint32_t my = 0;
@@ -1365,29 +1263,34 @@ __global__ void k_classify_rows(const uint64_t* __restrict__ row_begin, int64_t 
   const bool valid = r < R;
   uint64_t b = 0, e = 0;
   if (valid) { b = row_begin[r]; e = r + 1 < R ? row_begin[r + 1] : P; }
-  push_task_block(TL, valid && e > b, b, e - b, (uint32_t)r, (uint32_t)WB, 0u, true, err);
+  push_task_block(TL, valid && e > b, b, e - b, (uint32_t)r, 0u, 0u, true, err);
 }
 
 // split: per task k digit bits, chunks of SPLIT_CH words
 constexpr int SPLIT_CH = 16384;
 constexpr int SPLIT_T = 256;
 
-// Bits for one split: enough for ~1024-word buckets, at most 8 and never below HASH_REM
-// remaining bits (such buckets hash with a guaranteed fit).
-__device__ __forceinline__ int split_bits(const Task& t, int WB) {
-  (void)WB;
+// Bits for one split: enough for SPLIT_TARGET-word buckets, 1..8.
+__device__ __forceinline__ int split_bits(const Task& t) {
   int k = 1;
   while (k < 8 && ((uint64_t)t.len >> k) > (uint64_t)SPLIT_TARGET) ++k;
-  const int maxk = (int)t.rem - HASH_REM;
-  if (k > maxk) k = maxk;
-  return k < 1 ? 1 : k;
+  return k;
+}
+// Split digit: the top k bits of a hash of the word's (rule, aid_next) part, seeded by the
+// split level. Every word of one output row (all its files) lands in the same bucket, buckets
+// are balanced whatever the aid_next distribution, and a bucket split again at the next level
+// spreads over fresh digits. Row order inside the table is not part of the contract.
+__device__ __forceinline__ uint32_t split_digit(uint32_t w, int F, uint32_t level, int k) {
+  uint32_t x = (w >> F) ^ (level * 0x9E3779B9u);
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x >> (32 - k);
 }
 __global__ void k_split_prepare(const Task* __restrict__ tasks, int64_t n, int WB, uint32_t* __restrict__ nchunks,
                                 uint32_t* __restrict__ ndigits) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   nchunks[i] = (uint32_t)ceil_div((int64_t)tasks[i].len, SPLIT_CH);
-  ndigits[i] = 1u << split_bits(tasks[i], WB);
+  ndigits[i] = 1u << split_bits(tasks[i]);
 }
 
 __device__ __forceinline__ int64_t find_task(const uint64_t* chunk_base, int64_t n, uint64_t c) {
@@ -1403,19 +1306,18 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_hist(const Task* __restrict__
                                                         const uint64_t* __restrict__ chunk_base,
                                                         const uint64_t* __restrict__ digit_base,
                                                         const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
-                                                        int WB, uint32_t* __restrict__ dcount) {
+                                                        int F, uint32_t* __restrict__ dcount) {
   __shared__ uint32_t h[256];
   const int64_t t = find_task(chunk_base, n, blockIdx.x);
   const Task T = tasks[t];
-  const int k = split_bits(T, WB);
-  const int sh = (int)T.rem - k;
+  const int k = split_bits(T);
   const uint32_t dm = (1u << k) - 1u;
   const uint64_t c0 = (uint64_t)(blockIdx.x - chunk_base[t]) * SPLIT_CH;
   const uint64_t c1 = c0 + SPLIT_CH < T.len ? c0 + SPLIT_CH : T.len;
   const uint32_t* W = (T.buf ? w1 : w0) + T.begin;
   for (int i = threadIdx.x; i < 256; i += SPLIT_T) h[i] = 0;
   __syncthreads();
-  for (uint64_t i = c0 + threadIdx.x; i < c1; i += SPLIT_T) atomicAdd(&h[(W[i] >> sh) & dm], 1u);
+  for (uint64_t i = c0 + threadIdx.x; i < c1; i += SPLIT_T) atomicAdd(&h[split_digit(W[i], F, T.rem, k)], 1u);
   __syncthreads();
   for (int d = threadIdx.x; d <= (int)dm; d += SPLIT_T)
     if (h[d]) atomicAdd(&dcount[digit_base[t] + d], h[d]);
@@ -1428,7 +1330,7 @@ __global__ void k_split_cursor(const Task* __restrict__ tasks, int64_t n, const 
   if (t >= n) return;
   const Task T = tasks[t];
   const uint64_t db = digit_base[t];
-  const int nd = 1 << split_bits(T, WB);
+  const int nd = 1 << split_bits(T);
   const uint64_t d0 = doff[db];
   for (int d = lane_id(); d < nd; d += 64) cur[db + d] = T.begin + (doff[db + d] - d0);
 }
@@ -1438,16 +1340,14 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
                                                            const uint64_t* __restrict__ chunk_base,
                                                            const uint64_t* __restrict__ digit_base,
                                                            uint32_t* __restrict__ w0, uint32_t* __restrict__ w1,
-                                                           int WB, unsigned long long* __restrict__ cur) {
+                                                           int F, unsigned long long* __restrict__ cur) {
   __shared__ uint32_t h[256], st[256], fill[256];
   __shared__ unsigned long long gb[256];
   __shared__ uint32_t stage[SUB];
   __shared__ uint32_t wsum[SPLIT_T / 64];
   const int64_t t = find_task(chunk_base, n, blockIdx.x);
   const Task T = tasks[t];
-  const int k = split_bits(T, WB);
-  const int sh = (int)T.rem - k;
-  const uint32_t dm = (1u << k) - 1u;
+  const int k = split_bits(T);
   const uint64_t c0 = (uint64_t)(blockIdx.x - chunk_base[t]) * SPLIT_CH;
   const uint64_t c1 = c0 + SPLIT_CH < T.len ? c0 + SPLIT_CH : T.len;
   const uint32_t* Win = (T.buf ? w1 : w0) + T.begin;
@@ -1457,7 +1357,7 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
     const int m = (int)((c1 - s0) < (uint64_t)SUB ? (c1 - s0) : (uint64_t)SUB);
     h[tid] = 0; fill[tid] = 0;
     __syncthreads();
-    for (int i = tid; i < m; i += SPLIT_T) atomicAdd(&h[(Win[s0 + i] >> sh) & dm], 1u);
+    for (int i = tid; i < m; i += SPLIT_T) atomicAdd(&h[split_digit(Win[s0 + i], F, T.rem, k)], 1u);
     __syncthreads();
     {  // exclusive scan of h over 256 digits -> st; reserve global ranges
       const uint32_t v = h[tid];
@@ -1472,13 +1372,13 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
     __syncthreads();
     for (int i = tid; i < m; i += SPLIT_T) {
       const uint32_t w = Win[s0 + i];
-      const uint32_t d = (w >> sh) & dm;
+      const uint32_t d = split_digit(w, F, T.rem, k);
       stage[st[d] + atomicAdd(&fill[d], 1u)] = w;
     }
     __syncthreads();
     for (int p = tid; p < m; p += SPLIT_T) {
       const uint32_t w = stage[p];
-      const uint32_t d = (w >> sh) & dm;
+      const uint32_t d = split_digit(w, F, T.rem, k);
       Wout[gb[d] + (p - st[d])] = w;
     }
     __syncthreads();
@@ -1494,14 +1394,15 @@ __global__ void k_split_classify(const Task* __restrict__ tasks, int64_t n, cons
   Task T;
   T.begin = 0; T.rem = 0; T.row = 0; T.buf = 0; T.len = 0;
   uint64_t b = 0;
-  int k = 0;
   if (c) {
     const int64_t t = find_task(digit_base, n, (uint64_t)i);
     T = tasks[t];
-    k = split_bits(T, WB);
     b = T.begin + (doff[i] - doff[digit_base[t]]);
   }
-  push_task_block(TL, c != 0, b, c, T.row, T.rem - (uint32_t)k, T.buf ^ 1u, false, err);
+  // a bucket within 4x of its expected size is split again (its parent was too large for one
+  // split's 8 bits); one far above it holds a few hot keys and goes to the hash path
+  const bool again = c != 0 && (uint64_t)c <= 4 * (((uint64_t)T.len >> split_bits(T)) + 1);
+  push_task_block(TL, c != 0, b, c, T.row, T.rem + 1u, T.buf ^ 1u, again, err);
 }
 
 // ------------------------------------------------------------------ per-rule compaction
