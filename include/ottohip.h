@@ -267,6 +267,9 @@ int ottohip_test_exclusive_scan_u32(ottohip_ctx* ctx, const uint32_t* in, uint64
                                     uint64_t* total_host, void* stream);
 int ottohip_test_radix_sort_pairs(ottohip_ctx* ctx, uint32_t* keys, uint32_t* vals, int64_t n,
                                   int bits, void* stream);
+/* cross-lane moves of one wave on in[64] (device): out[k*64 + l] for k = 0..5 the value of lane
+ * l ^ (1 << k); k = 6, 7: inclusive sum / max scan; k = 8, 9: lanes l-1 / l+1 (0 off the ends) */
+int ottohip_test_lanes(const uint32_t* in, uint32_t* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -100,6 +100,7 @@ SIGNATURES = {
     "ottohip_knn_index_free": (None, [_VP]),
     "ottohip_test_exclusive_scan_u32": (ctypes.c_int, [_VP, _VP, _VP, _I64, ctypes.POINTER(ctypes.c_uint64), _VP]),
     "ottohip_test_radix_sort_pairs": (ctypes.c_int, [_VP, _VP, _VP, _I64, ctypes.c_int, _VP]),
+    "ottohip_test_lanes": (ctypes.c_int, [_VP, _VP, _VP]),
 }
 
 _LIB = None

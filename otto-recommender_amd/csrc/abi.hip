@@ -145,13 +145,19 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
   const int64_t* off = ev->session_offsets;
   F.off = off;
 
-  // ---- S1 prep
+  // ---- S1 prep + S2 count (fused; sessions longer than LCAP: separate per-session kernels)
+  uint32_t *rk, *pos, *rk2, *pos2;
   OH_TRY(ws.get("ev", (size_t)E, &F.evp));
-  int ph = ctx->begin("prep", s, 9.0 * E + 8.0 * (Sn + 1) + 8.0 * E);
+  OH_TRY(ws.get("cnt", (size_t)E, &F.cnt));
+  OH_TRY(ws.get("rk", (size_t)E, &rk));
+  OH_TRY(ws.get("pos", (size_t)E, &pos));
+  OH_TRY(ws.get("rk2", (size_t)E, &rk2));
+  OH_TRY(ws.get("pos2", (size_t)E, &pos2));
+  int ph = ctx->begin("prep_count", s, 9.0 * E + 8.0 * (Sn + 1) + 8.0 * E + 12.0 * E);
   k_block_first<<<grid_for(Sn + 1), 256, 0, s>>>(off, Sn, NB, F.first, F.long_list, n_long);
-  k_prep<<<grid_for(NB, 4), 256, 0, s>>>(off, F.first, NB, ev->aid, ev->ts, ev->type, F.evp, params->n_items,
-                                          params->dedup, err);
-  if (hipGetLastError() != hipSuccess) { set_error("k_prep launch failed"); return OTTOHIP_EHIP; }
+  k_prep_count<<<(unsigned)NB, 64, 0, s>>>(off, F.first, NB, ev->aid, ev->ts, ev->type, F.evp, params->n_items,
+                                           params->dedup, err, R, Lt.A, F.cnt, rk, pos);
+  if (hipGetLastError() != hipSuccess) { set_error("k_prep_count launch failed"); return OTTOHIP_EHIP; }
   int32_t nl = 0;
   OH_TRY(d2h(&nl, n_long, 1, s));
   F.nl = nl;
@@ -173,21 +179,9 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
     OH_HIP(hipMemcpy(F.d_loff, loff.data(), (nl + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
     k_prep_long<<<nl, 64, 0, s>>>(off, F.long_list, F.d_loff, F.lscr, ev->aid, ev->ts, ev->type, F.evp,
                                   params->n_items, params->dedup, err);
-  }
-  ctx->end(ph, s);
-
-  // ---- S2 count
-  uint32_t *rk, *pos, *rk2, *pos2;
-  OH_TRY(ws.get("cnt", (size_t)E, &F.cnt));
-  OH_TRY(ws.get("rk", (size_t)E, &rk));
-  OH_TRY(ws.get("pos", (size_t)E, &pos));
-  OH_TRY(ws.get("rk2", (size_t)E, &rk2));
-  OH_TRY(ws.get("pos2", (size_t)E, &pos2));
-  ph = ctx->begin("count", s, 8.0 * E + 12.0 * E);
-  k_count<<<grid_for(NB, 4), 256, 0, s>>>(off, F.first, NB, F.evp, R, Lt.A, F.cnt, rk, pos);
-  if (nl > 0)
     k_count_long<<<nl, 64, 0, s>>>(off, F.long_list, F.d_loff, F.lscr, F.lpscr, F.evp, R, Lt.A, F.cnt, rk, pos);
-  if (hipGetLastError() != hipSuccess) { set_error("k_count launch failed"); return OTTOHIP_EHIP; }
+    if (hipGetLastError() != hipSuccess) { set_error("long-session launch failed"); return OTTOHIP_EHIP; }
+  }
   ctx->end(ph, s);
 
   // ---- S3 rows (aid-major transpose; owner-major first when n_parts > 1)
@@ -444,6 +438,28 @@ int ottohip_test_exclusive_scan_u32(ottohip_ctx* ctx, const uint32_t* in, uint64
   OH_TRY(ctx->ws.get("test_total", 1, &tot));
   OH_TRY(exclusive_scan_u32(ctx, in, out, n, tot, S(stream)));
   if (total_host) OH_TRY(d2h(total_host, tot, 1, S(stream)));
+  return 0;
+}
+
+__global__ void k_test_lanes(const uint32_t* __restrict__ in, uint32_t* __restrict__ out) {
+  const uint32_t l = lane_id();
+  const uint32_t v = in[l];
+  out[0 * 64 + l] = xor_lane<1>(v);
+  out[1 * 64 + l] = xor_lane<2>(v);
+  out[2 * 64 + l] = xor_lane<4>(v);
+  out[3 * 64 + l] = xor_lane<8>(v);
+  out[4 * 64 + l] = xor_lane<16>(v);
+  out[5 * 64 + l] = xor_lane<32>(v);
+  out[6 * 64 + l] = dpp_incl_scan<false>(v);
+  out[7 * 64 + l] = dpp_incl_scan<true>(v);
+  out[8 * 64 + l] = lane_prev(v);
+  out[9 * 64 + l] = lane_next(v);
+}
+
+int ottohip_test_lanes(const uint32_t* in, uint32_t* out, void* stream) {
+  if (!in || !out) return OTTOHIP_EINVAL;
+  k_test_lanes<<<1, 64, 0, S(stream)>>>(in, out);
+  OH_HIP(hipGetLastError());
   return 0;
 }
 

@@ -107,15 +107,64 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
   uint32_t lo = __shfl((uint32_t)v, src), hi = __shfl((uint32_t)(v >> 32), src);
   return ((uint64_t)hi << 32) | lo;
 }
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-  const uint32_t l = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t t = __shfl_up(v, d);
-    if (l >= (uint32_t)d) v += t;
+// ---- cross-lane moves without the LDS crossbar: DPP (GFX9 control codes: quad_perm 0x00-0xFF,
+// row_shl:n 0x100+n (lane i <- i+n), row_shr:n 0x110+n (lane i <- i-n), row_ror:n 0x120+n) and
+// the gfx950 half-row / half-wave swaps
+template <int J>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {  // value of lane (this ^ J)
+  if constexpr (J == 1) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
+  } else if constexpr (J == 2) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
+  } else if constexpr (J == 4) {
+    const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x104, 0xF, 0xF, true);
+    const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x114, 0xF, 0xF, true);
+    return (lane_id() & 4u) ? dn : up;
+  } else if constexpr (J == 8) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, true);  // row_ror:8
+  } else if constexpr (J == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (lane_id() & 16u) ? r[0] : r[1];
+  } else {
+    static_assert(J == 32, "xor_lane: J in {1,2,4,8,16,32}");
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (lane_id() & 32u) ? r[0] : r[1];
   }
+}
+// J folds to a constant once the caller's loops are unrolled
+__device__ __forceinline__ uint32_t xor_lane_n(uint32_t v, int J) {
+  switch (J) {
+    case 1: return xor_lane<1>(v);
+    case 2: return xor_lane<2>(v);
+    case 4: return xor_lane<4>(v);
+    case 8: return xor_lane<8>(v);
+    case 16: return xor_lane<16>(v);
+    case 32: return xor_lane<32>(v);
+    default: return __shfl_xor(v, J);
+  }
+}
+// inclusive scan over the wave (sum / max) by DPP row shifts and row broadcasts
+template <bool MAX>
+__device__ __forceinline__ uint32_t dpp_step(uint32_t v, uint32_t t) { return MAX ? (v > t ? v : t) : v + t; }
+template <bool MAX>
+__device__ __forceinline__ uint32_t dpp_incl_scan(uint32_t v) {
+  v = dpp_step<MAX>(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));
+  v = dpp_step<MAX>(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false));
+  v = dpp_step<MAX>(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false));
+  v = dpp_step<MAX>(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false));
+  v = dpp_step<MAX>(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+  v = dpp_step<MAX>(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31
   return v;
 }
+// value of lane l-1 (0 in lane 0) / lane l+1 (0 in lane 63)
+__device__ __forceinline__ uint32_t lane_prev(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);  // wave_shr:1
+}
+__device__ __forceinline__ uint32_t lane_next(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);  // wave_shl:1
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) { return dpp_incl_scan<false>(v); }
 __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v) {
   const uint32_t l = lane_id();
 #pragma unroll
@@ -127,9 +176,7 @@ __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v) {
   return v;
 }
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-  return v;
+  return (uint32_t)__builtin_amdgcn_readlane((int)dpp_incl_scan<false>(v), 63);
 }
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 #pragma unroll

@@ -125,24 +125,6 @@ __device__ __forceinline__ void prep_session(const int32_t* __restrict__ aid, co
   for (int k = base + l; k < n; k += 64) out[k] = EV_INVALID;
 }
 
-__global__ __launch_bounds__(256) void k_prep(const int64_t* __restrict__ off, const int64_t* __restrict__ first,
-                                              int64_t NB, const int32_t* __restrict__ aid,
-                                              const int32_t* __restrict__ ts, const int8_t* __restrict__ ty,
-                                              uint64_t* __restrict__ ev, int n_items, int dedup, int* err) {
-  __shared__ uint64_t sh[4][2][LCAP];
-  const int w = threadIdx.x >> 6;
-  const int64_t g = (int64_t)blockIdx.x * 4 + w;
-  if (g >= NB) return;
-  const int64_t s0 = first[g], s1 = first[g + 1];
-  for (int64_t s = s0; s < s1; ++s) {
-    const int64_t e0 = off[s];
-    const int n = (int)(off[s + 1] - e0);
-    if (n > LCAP || n == 0) continue;
-    prep_session(aid, ts, ty, e0, n, sh[w][0], sh[w][1], ev + e0, n_items, dedup, err);
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
 __global__ __launch_bounds__(64) void k_prep_long(const int64_t* __restrict__ off, const int32_t* __restrict__ list,
                                                   const int64_t* __restrict__ scratch_off,
                                                   uint64_t* __restrict__ scratch, const int32_t* __restrict__ aid,
@@ -257,27 +239,6 @@ __device__ __forceinline__ void count_session(const SessView& S, int64_t e0, int
   }
 }
 
-__global__ __launch_bounds__(256) void k_count(const int64_t* __restrict__ off, const int64_t* __restrict__ first,
-                                               int64_t NB, const uint64_t* __restrict__ ev, RulesDev R, int A,
-                                               uint32_t* __restrict__ cnt, uint32_t* __restrict__ rk,
-                                               uint32_t* __restrict__ pos) {
-  __shared__ uint64_t sev[4][LCAP];
-  __shared__ uint32_t spref[4][3 * (LCAP + 1)];
-  const int w = threadIdx.x >> 6;
-  const int64_t g = (int64_t)blockIdx.x * 4 + w;
-  if (g >= NB) return;
-  for (int64_t s = first[g]; s < first[g + 1]; ++s) {
-    const int64_t e0 = off[s];
-    const int n = (int)(off[s + 1] - e0);
-    if (n > LCAP || n == 0) continue;
-    SessView S;
-    S.ev = sev[w]; S.pref = spref[w]; S.pstride = LCAP + 1;
-    S.nv = load_session(ev + e0, n, sev[w], spref[w], LCAP + 1);
-    count_session(S, e0, n, R, A, cnt, rk, pos);
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
 __global__ __launch_bounds__(64) void k_count_long(const int64_t* __restrict__ off, const int32_t* __restrict__ list,
                                                    const int64_t* __restrict__ scratch_off,
                                                    uint64_t* __restrict__ scratch, uint32_t* __restrict__ pscratch,
@@ -294,6 +255,216 @@ __global__ __launch_bounds__(64) void k_count_long(const int64_t* __restrict__ o
   S.ev = evs; S.pref = pref; S.pstride = n + 1;
   S.nv = load_session(ev + e0, n, evs, pref, n + 1);
   count_session(S, e0, n, R, A, cnt, rk, pos);
+}
+
+// ------------------------------------------------------------------ S1+S2 fused
+__device__ __forceinline__ int lds_lower_ts(const uint64_t* tev, int a, int b, int64_t x) {  // first k: ts >= x
+  while (a < b) {
+    const int m = (a + b) >> 1;
+    if ((int64_t)ev_ts(tev[m]) < x) a = m + 1; else b = m;
+  }
+  return a;
+}
+__device__ __forceinline__ int lds_upper_ts(const uint64_t* tev, int a, int b, int64_t x) {  // first k: ts > x
+  while (a < b) {
+    const int m = (a + b) >> 1;
+    if ((int64_t)ev_ts(tev[m]) <= x) a = m + 1; else b = m;
+  }
+  return a;
+}
+
+// One wave per 256-event block, batches of whole sessions (<= PB_CAP events, none longer than
+// LCAP: those take k_prep_long / k_count_long). Per batch, all in LDS:
+//   load + pack (aid, ts, type) coalesced; sort each session by the packed key (a session whose
+//   ts never decreases only reorders within runs of equal ts: rank inside the run; any other
+//   session is ranked against all of its events); drop exact duplicates (df.unique(), :92);
+//   store the packed events; per-type prefix counts; per event and rule the partner count in
+//   the window (binary searches on ts) and the row key.
+constexpr int PB_CAP = 512;
+struct PrepLds {
+  uint64_t key[PB_CAP];   // packed raw events, then the final (sorted, deduplicated) session layout
+  uint64_t srt[PB_CAP];   // sorted events before deduplication
+  uint16_t pref[3][PB_CAP + 1];
+  uint16_t ss[65];        // session starts in the batch; ss[nsess] = batch size
+  uint16_t pst[64], pen[64];
+  uint8_t esid[PB_CAP];
+  uint8_t uns[64];        // session has a ts decrease: full ranking
+};
+
+__global__ __launch_bounds__(64) void k_prep_count(const int64_t* __restrict__ off, const int64_t* __restrict__ first,
+                                                   int64_t NB, const int32_t* __restrict__ aid,
+                                                   const int32_t* __restrict__ ts, const int8_t* __restrict__ ty,
+                                                   uint64_t* __restrict__ ev, int n_items, int dedup, int* err,
+                                                   RulesDev R, int A, uint32_t* __restrict__ cnt,
+                                                   uint32_t* __restrict__ rk, uint32_t* __restrict__ pos) {
+  __shared__ PrepLds S;
+  __shared__ RulesDev sR;
+  const int l = threadIdx.x;
+  if (l == 0) sR = R;
+  const int64_t g = blockIdx.x;
+  if (g >= NB) return;
+  const int64_t s0 = first[g], s1 = first[g + 1];
+  __syncthreads();
+  const uint32_t INV = 3u << A;
+  int64_t b = s0;
+  while (b < s1) {
+    const int64_t base = off[b];
+    const int64_t s = b + l;
+    const bool in_s = s < s1;
+    const int64_t so = in_s ? off[s] : 0, se = in_s ? off[s + 1] : 0;
+    const bool ok = in_s && se - base <= PB_CAP && se - so <= LCAP;
+    const uint64_t bad = __ballot(!ok);
+    const int nsess = bad ? (int)__builtin_ctzll(bad) : 64;
+    if (nsess == 0) { ++b; continue; }  // long session: k_prep_long / k_count_long
+    const int nb_ev = __shfl((int)(se - base), nsess - 1);
+    const int64_t E0 = base;
+    if (l < nsess) { S.ss[l] = (uint16_t)(so - base); S.uns[l] = 0; }
+    if (l == 0) S.ss[nsess] = (uint16_t)nb_ev;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int nch = (nb_ev + 63) >> 6;
+    // ---- load, pack, session of each event
+#pragma unroll 1
+    for (int c = 0; c < nch; ++c) {
+      const int idx = c * 64 + l;
+      if (idx >= nb_ev) continue;
+      const int32_t a = aid[E0 + idx], t = ts[E0 + idx], y = ty[E0 + idx];
+      if (a < 0 || a >= n_items || y < 0 || y > 2) atomicOr(err, 1);
+      S.key[idx] = ev_pack(a < 0 ? 0 : a, t, y & 3);
+      int k = 0;
+#pragma unroll
+      for (int st = 32; st >= 1; st >>= 1)
+        if (k + st < nsess && (int)S.ss[k + st] <= idx) k += st;
+      S.esid[idx] = (uint8_t)k;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll 1
+    for (int c = 0; c < nch; ++c) {
+      const int idx = c * 64 + l;
+      if (idx >= nb_ev) continue;
+      const int k = S.esid[idx];
+      if (idx > (int)S.ss[k] && ev_ts(S.key[idx]) < ev_ts(S.key[idx - 1])) S.uns[k] = 1;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // ---- sort each session (stable rank by the packed key)
+#pragma unroll 1
+    for (int c = 0; c < nch; ++c) {
+      const int idx = c * 64 + l;
+      if (idx >= nb_ev) continue;
+      const int k = S.esid[idx];
+      const uint64_t v = S.key[idx];
+      int lo = S.ss[k], hi = S.ss[k + 1];
+      if (!S.uns[k]) {  // ts non-decreasing: only the run of equal ts can be out of order
+        const int32_t t = ev_ts(v);
+        int a = idx, e = idx + 1;
+        while (a > lo && ev_ts(S.key[a - 1]) == t) --a;
+        while (e < hi && ev_ts(S.key[e]) == t) ++e;
+        lo = a; hi = e;
+      }
+      int r = lo;
+      for (int j = lo; j < hi; ++j) {
+        const uint64_t u = S.key[j];
+        r += (u < v) | ((u == v) & (j < idx));
+      }
+      S.srt[r] = v;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // ---- deduplicate: kept events first, EV_INVALID tail (positions stay inside the session)
+    uint32_t P = 0;
+#pragma unroll 1
+    for (int c = 0; c < nch; ++c) {
+      const int idx = c * 64 + l;
+      const bool in = idx < nb_ev;
+      const int k = in ? S.esid[idx] : 0;
+      const bool keep = in && (!dedup || idx == (int)S.ss[k] || S.srt[idx - 1] != S.srt[idx]);
+      const uint64_t m = __ballot(keep);
+      const uint32_t Pi = P + mbcnt(m);
+      if (in && idx == (int)S.ss[k]) S.pst[k] = (uint16_t)Pi;
+      if (in && idx == (int)S.ss[k + 1] - 1) S.pen[k] = (uint16_t)(Pi + (keep ? 1u : 0u));
+      if (in) S.key[idx] = EV_INVALID;
+      P += (uint32_t)__popcll(m);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    P = 0;
+#pragma unroll 1
+    for (int c = 0; c < nch; ++c) {
+      const int idx = c * 64 + l;
+      const bool in = idx < nb_ev;
+      const int k = in ? S.esid[idx] : 0;
+      const bool keep = in && (!dedup || idx == (int)S.ss[k] || S.srt[idx - 1] != S.srt[idx]);
+      const uint64_t m = __ballot(keep);
+      if (keep) S.key[S.ss[k] + (P + mbcnt(m)) - S.pst[k]] = S.srt[idx];
+      P += (uint32_t)__popcll(m);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // ---- store; per-type prefix counts over the batch
+    uint32_t b0 = 0, b1 = 0, b2 = 0;
+#pragma unroll 1
+    for (int c = 0; c < nch; ++c) {
+      const int idx = c * 64 + l;
+      const bool in = idx < nb_ev;
+      const uint64_t v = in ? S.key[idx] : EV_INVALID;
+      if (in) ev[E0 + idx] = v;
+      const int t = ev_type(v);
+      const uint64_t m0 = __ballot(t == 0), m1 = __ballot(t == 1), m2 = __ballot(t == 2);
+      if (in) {
+        S.pref[0][idx] = (uint16_t)(b0 + mbcnt(m0));
+        S.pref[1][idx] = (uint16_t)(b1 + mbcnt(m1));
+        S.pref[2][idx] = (uint16_t)(b2 + mbcnt(m2));
+      }
+      b0 += (uint32_t)__popcll(m0); b1 += (uint32_t)__popcll(m1); b2 += (uint32_t)__popcll(m2);
+    }
+    if (l == 0) { S.pref[0][nb_ev] = (uint16_t)b0; S.pref[1][nb_ev] = (uint16_t)b1; S.pref[2][nb_ev] = (uint16_t)b2; }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // ---- partner counts and row keys
+#pragma unroll 1
+    for (int c = 0; c < nch; ++c) {
+      const int idx = c * 64 + l;
+      if (idx >= nb_ev) continue;
+      const int k = S.esid[idx];
+      const uint64_t e = S.key[idx];
+      uint32_t cn = 0, key = INV;
+      if (e != EV_INVALID) {
+        const int lo = S.ss[k], hi = lo + (S.pen[k] - S.pst[k]);  // valid events of the session
+        const int t = ev_type(e);
+        const int64_t tsi = ev_ts(e);
+        int run = -1;
+        for (int q = 0; q < sR.n_of_type[t]; ++q) {
+          const int r = sR.rule_of_type[t][q];
+          const int jb = lds_lower_ts(S.key, lo, hi, tsi + sR.lo[r]);
+          const int je = lds_upper_ts(S.key, jb, hi, tsi + sR.hi[r]);
+          if (je <= jb) continue;
+          uint32_t m = 0;
+#pragma unroll
+          for (int tt = 0; tt < 3; ++tt)
+            if ((sR.mask[r] >> tt) & 1u) m += (uint32_t)S.pref[tt][je] - (uint32_t)S.pref[tt][jb];
+          if (((sR.mask[r] >> t) & 1u) && sR.lo[r] <= 0 && sR.hi[r] >= 0) {
+            if (run < 0) {  // the identity row of :23-27 (and exact twins when dedup is off)
+              int a = idx, z = idx + 1;
+              while (a > lo && S.key[a - 1] == e) --a;
+              while (z < hi && S.key[z] == e) ++z;
+              run = z - a;
+            }
+            m -= (uint32_t)run;
+          }
+          cn += m;
+        }
+        if (cn) key = ((uint32_t)t << A) | (uint32_t)ev_aid(e);
+      }
+      cnt[E0 + idx] = cn;
+      rk[E0 + idx] = key;
+      pos[E0 + idx] = (uint32_t)(E0 + idx);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    b += nsess;
+  }
 }
 
 // ------------------------------------------------------------------ S3 rows
@@ -497,21 +668,6 @@ struct EmitLds {
   uint16_t espos[EB_CAP];               // per batch event: position in tev (EB_NONE: invalid)
   uint8_t esid[EB_CAP];                 // per batch event: session index in the batch
 };
-
-__device__ __forceinline__ int lds_lower_ts(const uint64_t* tev, int a, int b, int64_t x) {  // first k: ts >= x
-  while (a < b) {
-    const int m = (a + b) >> 1;
-    if ((int64_t)ev_ts(tev[m]) < x) a = m + 1; else b = m;
-  }
-  return a;
-}
-__device__ __forceinline__ int lds_upper_ts(const uint64_t* tev, int a, int b, int64_t x) {  // first k: ts > x
-  while (a < b) {
-    const int m = (a + b) >> 1;
-    if ((int64_t)ev_ts(tev[m]) <= x) a = m + 1; else b = m;
-  }
-  return a;
-}
 
 // expand records [0, nrec) holding tot pairs: lane k of round c writes pair c + k
 __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, int F, uint32_t* __restrict__ words,
@@ -815,15 +971,7 @@ __device__ __forceinline__ unsigned long long lds_load(unsigned long long* p) {
 constexpr uint32_t HASH_FULL = 0xFFFFFFFFu;  // hash_insert_batch: table full
 
 // ---- register sort path: one wave per task of <= 64*M words, no LDS, no atomics
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
-  const uint32_t l = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t t = __shfl_up(v, d);
-    if (l >= (uint32_t)d) v = v > t ? v : t;
-  }
-  return v;
-}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) { return dpp_incl_scan<true>(v); }
 
 // Bitonic sort of 64*M keys held as v[m] = element (lane*M + m), ascending.
 template <int M>
@@ -838,7 +986,7 @@ __device__ __forceinline__ void wave_bitonic_sort(uint32_t (&v)[M]) {
 #pragma unroll
         for (int m = 0; m < M; ++m) {
           const uint32_t e = l * M + m;
-          const uint32_t o = __shfl_xor(v[m], j / M);
+          const uint32_t o = xor_lane_n(v[m], j / M);
           const bool up = (e & k) == 0, lower = (e & j) == 0;
           v[m] = (lower == up) ? (v[m] < o ? v[m] : o) : (v[m] > o ? v[m] : o);
         }
@@ -864,9 +1012,8 @@ __device__ __forceinline__ void wave_scan_elems(uint32_t (&x)[M]) {
 #pragma unroll
   for (int m = 1; m < M; ++m) x[m] = MAX ? (x[m] > x[m - 1] ? x[m] : x[m - 1]) : x[m] + x[m - 1];
   const uint32_t tot = x[M - 1];
-  uint32_t incl = MAX ? wave_incl_max(tot) : wave_incl_scan(tot);
-  uint32_t excl = __shfl_up(incl, 1);
-  if (lane_id() == 0) excl = 0;
+  const uint32_t incl = dpp_incl_scan<MAX>(tot);
+  const uint32_t excl = lane_prev(incl);
 #pragma unroll
   for (int m = 0; m < M; ++m) x[m] = MAX ? (x[m] > excl ? x[m] : excl) : x[m] + excl;
 }
@@ -922,7 +1069,7 @@ __global__ __launch_bounds__(256) void k_agg_sort(const Task* __restrict__ tasks
     if (tn < n_tasks) fetch(tn, Tn, vn, rkn);
     const uint32_t len = T.len;
     wave_bitonic_sort<M>(v);
-    const uint32_t pl = __shfl_up(v[M - 1], 1), nl = __shfl_down(v[0], 1);
+    const uint32_t pl = lane_prev(v[M - 1]), nl = lane_next(v[0]);
     // (1) per-file count cf: start of the element's w-run by a max scan
     uint32_t a[M], b[M], c[M];
 #pragma unroll
@@ -945,7 +1092,7 @@ __global__ __launch_bounds__(256) void k_agg_sort(const Task* __restrict__ tasks
     // (3) k-run sums: inclusive prefix minus the prefix before the k-run's start (max scan)
     wave_scan_elems<M, false>(b);
     {
-      const uint32_t lt = __shfl_up(b[M - 1], 1), lprev = l == 0 ? 0u : lt;
+      const uint32_t lprev = lane_prev(b[M - 1]);
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         const uint32_t e = l * M + m;
@@ -958,7 +1105,7 @@ __global__ __launch_bounds__(256) void k_agg_sort(const Task* __restrict__ tasks
     for (int m = 0; m < M; ++m) b[m] -= a[m];
     wave_scan_elems<M, false>(c);
     {
-      const uint32_t lt = __shfl_up(c[M - 1], 1), lprev = l == 0 ? 0u : lt;
+      const uint32_t lprev = lane_prev(c[M - 1]);
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         const uint32_t e = l * M + m;

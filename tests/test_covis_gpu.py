@@ -74,6 +74,26 @@ def test_radix_sort_pairs_stable(gpu, n, bits):
 
 
 # ---------------------------------------------------------------- known answers / goldens
+def test_lane_primitives(gpu):
+    """DPP / permlane cross-lane moves and scans used by the reduce (csrc/common.h)."""
+    import torch
+    import otto_recommender_amd._lib as L
+    rng = np.random.default_rng(7)
+    x = rng.integers(0, 1 << 20, 64, dtype=np.int64).astype(np.uint32)
+    xt = torch.from_numpy(x.view(np.int32)).cuda()
+    out = torch.zeros(10 * 64, dtype=torch.int32, device="cuda")
+    L.check(L.load().ottohip_test_lanes(L.ptr(xt), L.ptr(out), L.stream_handle()))
+    torch.cuda.synchronize()
+    o = out.cpu().numpy().view(np.uint32).reshape(10, 64)
+    lanes = np.arange(64)
+    for k in range(6):
+        assert np.array_equal(o[k], x[lanes ^ (1 << k)]), k
+    assert np.array_equal(o[6], np.cumsum(x.astype(np.uint64)).astype(np.uint32))
+    assert np.array_equal(o[7], np.maximum.accumulate(x))
+    assert np.array_equal(o[8], np.concatenate([[0], x[:-1]]))
+    assert np.array_equal(o[9], np.concatenate([x[1:], [0]]))
+
+
 def test_kat_appendix_a(gpu):
     g = json.load(open(os.path.join(GOLD, "kat_appendix_a.json")))
     a = np.array(g["events"])
