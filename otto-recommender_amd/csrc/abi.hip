@@ -327,35 +327,32 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     if (ns == 0) { drained = true; break; }
     if ((uint64_t)ns > TL.cap) { set_error("split list overflow"); return OTTOHIP_ELIMIT; }
     Task* cur_split = TL.split;
-    // chunk / digit bases
-    uint32_t *nch, *ndg;
-    uint64_t *chb, *dgb, *tot2;
+    // chunk / digit / count-matrix bases
+    uint32_t *nch, *ndg, *nen;
+    uint64_t *chb, *dgb, *mtb, *tot2;
     if ((rc = ws.get("sp_nch", (size_t)ns, &nch)) || (rc = ws.get("sp_ndg", (size_t)ns, &ndg)) ||
-        (rc = ws.get("sp_chb", (size_t)ns + 1, &chb)) || (rc = ws.get("sp_dgb", (size_t)ns + 1, &dgb)) ||
-        (rc = ws.get("sp_tot", 2, &tot2)))
+        (rc = ws.get("sp_nen", (size_t)ns, &nen)) || (rc = ws.get("sp_chb", (size_t)ns + 1, &chb)) ||
+        (rc = ws.get("sp_dgb", (size_t)ns + 1, &dgb)) || (rc = ws.get("sp_mtb", (size_t)ns + 1, &mtb)) ||
+        (rc = ws.get("sp_tot", 3, &tot2)))
       return rc;
-    k_split_prepare<<<grid_for(ns), 256, 0, s>>>(cur_split, ns, Lt.WB, nch, ndg);
-    if ((rc = exclusive_scan_u32(ctx, nch, chb, ns, tot2, s)) || (rc = exclusive_scan_u32(ctx, ndg, dgb, ns, tot2 + 1, s)))
+    k_split_prepare<<<grid_for(ns), 256, 0, s>>>(cur_split, ns, nch, ndg, nen);
+    if ((rc = exclusive_scan_u32(ctx, nch, chb, ns, tot2, s)) || (rc = exclusive_scan_u32(ctx, ndg, dgb, ns, tot2 + 1, s)) ||
+        (rc = exclusive_scan_u32(ctx, nen, mtb, ns, tot2 + 2, s)))
       return rc;
-    uint64_t tt[2];
-    if ((rc = d2h(tt, tot2, 2, s))) return rc;
-    const int64_t nchunks = (int64_t)tt[0], ndig = (int64_t)tt[1];
-    uint32_t* dcount;
-    uint64_t* doff;
-    unsigned long long* dcur;
-    if ((rc = ws.get("sp_dcount", (size_t)ndig, &dcount)) || (rc = ws.get("sp_doff", (size_t)ndig, &doff)) ||
-        (rc = ws.get("sp_dcur", (size_t)ndig, &dcur)))
-      return rc;
-    hipMemsetAsync(dcount, 0, ndig * 4, s);
-    k_split_hist<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, dgb, w0, w1, Lt.F, dcount);
-    if ((rc = exclusive_scan_u32(ctx, dcount, doff, ndig, nullptr, s))) return rc;
-    k_split_cursor<<<grid_for(ns * 64), 256, 0, s>>>(cur_split, ns, dgb, doff, dcur, Lt.WB);
-    k_split_scatter<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, dgb, w0, w1, Lt.F, dcur);
+    uint64_t tt[3];
+    if ((rc = d2h(tt, tot2, 3, s))) return rc;
+    const int64_t nchunks = (int64_t)tt[0], ndig = (int64_t)tt[1], nent = (int64_t)tt[2];
+    uint32_t* hmat;
+    uint64_t* hoff;
+    if ((rc = ws.get("sp_hmat", (size_t)nent, &hmat)) || (rc = ws.get("sp_hoff", (size_t)nent + 1, &hoff))) return rc;
+    k_split_hist<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, mtb, w0, w1, Lt.F, hmat);
+    if ((rc = exclusive_scan_u32(ctx, hmat, hoff, nent, hoff + nent, s))) return rc;
+    k_split_scatter<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, mtb, hoff, w0, w1, Lt.F);
     // next lists (a sub-bucket is one task in exactly one list: ndig bounds every list)
     const uint64_t capn = (uint64_t)ndig;
     if ((rc = get_lists(std::max(cap0, capn), srcA ? "t_splitB" : "t_splitA"))) return rc;
     hipMemsetAsync(lcount, 0, 8 * 8, s);
-    k_split_classify<<<grid_for(ndig), 256, 0, s>>>(cur_split, ns, dgb, dcount, doff, ndig, Lt.WB, TL, err);
+    k_split_classify<<<grid_for(ndig), 256, 0, s>>>(cur_split, ns, dgb, mtb, hoff, ndig, TL, err);
     srcA = !srcA;
     if (hipGetLastError() != hipSuccess) { set_error("split launch failed"); return OTTOHIP_EHIP; }
   }

@@ -973,33 +973,40 @@ constexpr uint32_t HASH_FULL = 0xFFFFFFFFu;  // hash_insert_batch: table full
 // ---- register sort path: one wave per task of <= 64*M words, no LDS, no atomics
 __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) { return dpp_incl_scan<true>(v); }
 
-// Bitonic sort of 64*M keys held as v[m] = element (lane*M + m), ascending.
+// median of three: with c = 0 it is min(a, b), with c = ~0 max(a, b) (one VALU op)
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// Bitonic sort of 64*M keys held as v[m] = element (lane*M + m), ascending. Every
+// compare-exchange is one v_med3_u32 against a sentinel (0: keep the min, ~0: keep the max)
+// that depends only on the lane and the stage; partners in other lanes come by DPP / permlane.
 template <int M>
 __device__ __forceinline__ void wave_bitonic_sort(uint32_t (&v)[M]) {
   constexpr int N = 64 * M;
-  const uint32_t l = lane_id();
+  uint32_t l = lane_id();
+  asm volatile("" : "+v"(l));  // keeps the per-stage sentinels from being hoisted into registers
 #pragma unroll
   for (int k = 2; k <= N; k <<= 1) {
 #pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
-      if (j >= M) {  // partner in lane l ^ (j / M), same register
+      // sentinels by arithmetic on the lane bits (no lane-mask registers): 0 = keep the min
+      const int kb = __builtin_ctz(k), jb = __builtin_ctz(j);
+      if (j >= M) {  // partner in lane l ^ (j / M), same register; direction from lane bits only
+        const uint32_t sent = 0u - ((((l * M) >> kb) ^ ((l * M) >> jb)) & 1u);
 #pragma unroll
-        for (int m = 0; m < M; ++m) {
-          const uint32_t e = l * M + m;
-          const uint32_t o = xor_lane_n(v[m], j / M);
-          const bool up = (e & k) == 0, lower = (e & j) == 0;
-          v[m] = (lower == up) ? (v[m] < o ? v[m] : o) : (v[m] > o ? v[m] : o);
-        }
+        for (int m = 0; m < M; ++m) v[m] = umed3(v[m], xor_lane_n(v[m], j / M), sent);
       } else {  // partner in this lane
+        const uint32_t lane_slo = 0u - (((l * M) >> kb) & 1u);  // used when k >= M
 #pragma unroll
         for (int m = 0; m < M; ++m) {
           if (m & j) continue;
-          const uint32_t e = l * M + m;
-          const bool up = (e & k) == 0;
+          const uint32_t slo = k < M ? ((m & k) ? ~0u : 0u) : lane_slo;
           const uint32_t a = v[m], b = v[m ^ j];
-          const bool sw = up ? (a > b) : (a < b);
-          v[m] = sw ? b : a;
-          v[m ^ j] = sw ? a : b;
+          v[m] = umed3(a, b, slo);
+          v[m ^ j] = umed3(a, b, ~slo);
         }
       }
     }
@@ -1054,9 +1061,10 @@ __global__ __launch_bounds__(256) void k_agg_sort(const Task* __restrict__ tasks
     TT = tasks[t];
     const uint32_t* W = (TT.buf ? w1 : w0) + TT.begin;
 #pragma unroll
-    for (int m = 0; m < M; ++m) {  // coalesced load (element m*64 + l), then sorted anyway
-      const uint32_t i = (uint32_t)(m * 64) + l;
-      vv[m] = i < TT.len ? W[i] : W_EMPTY;
+    for (int m = 0; m < M; ++m) {  // coalesced load (element m*64 + l), then sorted anyway;
+      const uint32_t i = (uint32_t)(m * 64) + l;  // clamped index: no branch around the load
+      const uint32_t x = W[i < TT.len ? i : TT.len - 1];
+      vv[m] = i < TT.len ? x : W_EMPTY;
     }
     rkk = row_key[TT.row];
   };
@@ -1432,12 +1440,17 @@ __device__ __forceinline__ uint32_t split_digit(uint32_t w, int F, uint32_t leve
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
   return x >> (32 - k);
 }
-__global__ void k_split_prepare(const Task* __restrict__ tasks, int64_t n, int WB, uint32_t* __restrict__ nchunks,
-                                uint32_t* __restrict__ ndigits) {
+// Split of one level, no global atomics: per task, chunks of SPLIT_CH words and 2^k digits; a
+// (digit-major, chunk-minor) matrix of per-chunk digit counts is scanned once, which gives every
+// chunk its exact output offset per digit and every sub-bucket its range.
+__global__ void k_split_prepare(const Task* __restrict__ tasks, int64_t n, uint32_t* __restrict__ nchunks,
+                                uint32_t* __restrict__ ndigits, uint32_t* __restrict__ nent) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  nchunks[i] = (uint32_t)ceil_div((int64_t)tasks[i].len, SPLIT_CH);
-  ndigits[i] = 1u << split_bits(tasks[i]);
+  const uint32_t nch = (uint32_t)ceil_div((int64_t)tasks[i].len, SPLIT_CH), nd = 1u << split_bits(tasks[i]);
+  nchunks[i] = nch;
+  ndigits[i] = nd;
+  nent[i] = nch * nd;
 }
 
 __device__ __forceinline__ int64_t find_task(const uint64_t* chunk_base, int64_t n, uint64_t c) {
@@ -1451,62 +1464,65 @@ __device__ __forceinline__ int64_t find_task(const uint64_t* chunk_base, int64_t
 
 __global__ __launch_bounds__(SPLIT_T) void k_split_hist(const Task* __restrict__ tasks, int64_t n,
                                                         const uint64_t* __restrict__ chunk_base,
-                                                        const uint64_t* __restrict__ digit_base,
+                                                        const uint64_t* __restrict__ mat_base,
                                                         const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
-                                                        int F, uint32_t* __restrict__ dcount) {
+                                                        int F, uint32_t* __restrict__ hmat) {
   __shared__ uint32_t h[256];
   const int64_t t = find_task(chunk_base, n, blockIdx.x);
   const Task T = tasks[t];
   const int k = split_bits(T);
-  const uint32_t dm = (1u << k) - 1u;
-  const uint64_t c0 = (uint64_t)(blockIdx.x - chunk_base[t]) * SPLIT_CH;
+  const uint32_t nd = 1u << k, nch = (uint32_t)ceil_div((int64_t)T.len, SPLIT_CH);
+  const uint32_t c = (uint32_t)(blockIdx.x - chunk_base[t]);
+  const uint64_t c0 = (uint64_t)c * SPLIT_CH;
   const uint64_t c1 = c0 + SPLIT_CH < T.len ? c0 + SPLIT_CH : T.len;
   const uint32_t* W = (T.buf ? w1 : w0) + T.begin;
   for (int i = threadIdx.x; i < 256; i += SPLIT_T) h[i] = 0;
   __syncthreads();
   for (uint64_t i = c0 + threadIdx.x; i < c1; i += SPLIT_T) atomicAdd(&h[split_digit(W[i], F, T.rem, k)], 1u);
   __syncthreads();
-  for (int d = threadIdx.x; d <= (int)dm; d += SPLIT_T)
-    if (h[d]) atomicAdd(&dcount[digit_base[t] + d], h[d]);
+  for (uint32_t d = threadIdx.x; d < nd; d += SPLIT_T) hmat[mat_base[t] + (uint64_t)d * nch + c] = h[d];
 }
 
-// one wave per split task: sub-bucket starts of its 2^k digits (cursor for the scatter)
-__global__ void k_split_cursor(const Task* __restrict__ tasks, int64_t n, const uint64_t* __restrict__ digit_base,
-                               const uint64_t* __restrict__ doff, unsigned long long* __restrict__ cur, int WB) {
-  const int64_t t = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (t >= n) return;
-  const Task T = tasks[t];
-  const uint64_t db = digit_base[t];
-  const int nd = 1 << split_bits(T);
-  const uint64_t d0 = doff[db];
-  for (int d = lane_id(); d < nd; d += 64) cur[db + d] = T.begin + (doff[db + d] - d0);
-}
-
-constexpr int SUB = 4096;  // scatter sub-tile (staged in LDS in digit order)
+constexpr int SUB = 4096;             // scatter sub-tile (staged in LDS in digit order)
+constexpr int SUB_PER_T = SUB / SPLIT_T;  // words per thread per sub-tile, held in registers
 __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restrict__ tasks, int64_t n,
                                                            const uint64_t* __restrict__ chunk_base,
-                                                           const uint64_t* __restrict__ digit_base,
-                                                           uint32_t* __restrict__ w0, uint32_t* __restrict__ w1,
-                                                           int F, unsigned long long* __restrict__ cur) {
+                                                           const uint64_t* __restrict__ mat_base,
+                                                           const uint64_t* __restrict__ hoff,
+                                                           uint32_t* __restrict__ w0, uint32_t* __restrict__ w1, int F) {
   __shared__ uint32_t h[256], st[256], fill[256];
-  __shared__ unsigned long long gb[256];
+  __shared__ uint64_t gb[256];
   __shared__ uint32_t stage[SUB];
   __shared__ uint32_t wsum[SPLIT_T / 64];
   const int64_t t = find_task(chunk_base, n, blockIdx.x);
   const Task T = tasks[t];
   const int k = split_bits(T);
-  const uint64_t c0 = (uint64_t)(blockIdx.x - chunk_base[t]) * SPLIT_CH;
+  const uint32_t nd = 1u << k, nch = (uint32_t)ceil_div((int64_t)T.len, SPLIT_CH);
+  const uint32_t c = (uint32_t)(blockIdx.x - chunk_base[t]);
+  const uint64_t c0 = (uint64_t)c * SPLIT_CH;
   const uint64_t c1 = c0 + SPLIT_CH < T.len ? c0 + SPLIT_CH : T.len;
   const uint32_t* Win = (T.buf ? w1 : w0) + T.begin;
   uint32_t* Wout = T.buf ? w0 : w1;
   const int tid = threadIdx.x;
+  const uint64_t mb = mat_base[t];
+  if ((uint32_t)tid < nd) gb[tid] = T.begin + (hoff[mb + (uint64_t)tid * nch + c] - hoff[mb]);
   for (uint64_t s0 = c0; s0 < c1; s0 += SUB) {
     const int m = (int)((c1 - s0) < (uint64_t)SUB ? (c1 - s0) : (uint64_t)SUB);
+    uint32_t wr[SUB_PER_T], dg[SUB_PER_T];
+#pragma unroll
+    for (int j = 0; j < SUB_PER_T; ++j) {  // the sub-tile is read once, into registers
+      const int i = tid + j * SPLIT_T;
+      wr[j] = i < m ? Win[s0 + i] : 0u;
+    }
     h[tid] = 0; fill[tid] = 0;
     __syncthreads();
-    for (int i = tid; i < m; i += SPLIT_T) atomicAdd(&h[split_digit(Win[s0 + i], F, T.rem, k)], 1u);
+#pragma unroll
+    for (int j = 0; j < SUB_PER_T; ++j) {
+      dg[j] = split_digit(wr[j], F, T.rem, k);
+      if (tid + j * SPLIT_T < m) atomicAdd(&h[dg[j]], 1u);
+    }
     __syncthreads();
-    {  // exclusive scan of h over 256 digits -> st; reserve global ranges
+    {  // exclusive scan of h over 256 digits -> st
       const uint32_t v = h[tid];
       const uint32_t incl = wave_incl_scan(v);
       if ((tid & 63) == 63) wsum[tid >> 6] = incl;
@@ -1514,14 +1530,11 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
       uint32_t pre = 0;
       for (int q = 0; q < (tid >> 6); ++q) pre += wsum[q];
       st[tid] = pre + incl - v;
-      if (v) gb[tid] = atomicAdd(&cur[digit_base[t] + tid], (unsigned long long)v);
     }
     __syncthreads();
-    for (int i = tid; i < m; i += SPLIT_T) {
-      const uint32_t w = Win[s0 + i];
-      const uint32_t d = split_digit(w, F, T.rem, k);
-      stage[st[d] + atomicAdd(&fill[d], 1u)] = w;
-    }
+#pragma unroll
+    for (int j = 0; j < SUB_PER_T; ++j)
+      if (tid + j * SPLIT_T < m) stage[st[dg[j]] + atomicAdd(&fill[dg[j]], 1u)] = wr[j];
     __syncthreads();
     for (int p = tid; p < m; p += SPLIT_T) {
       const uint32_t w = stage[p];
@@ -1529,22 +1542,26 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
       Wout[gb[d] + (p - st[d])] = w;
     }
     __syncthreads();
+    gb[tid] += h[tid];  // this chunk's cursor per digit moves past the sub-tile
   }
 }
 
 // one thread per (split task, digit): push the non-empty sub-buckets as next-level tasks
 __global__ void k_split_classify(const Task* __restrict__ tasks, int64_t n, const uint64_t* __restrict__ digit_base,
-                                 const uint32_t* __restrict__ dcount, const uint64_t* __restrict__ doff,
-                                 int64_t n_digits_total, int WB, TaskLists TL, int* err) {
+                                 const uint64_t* __restrict__ mat_base, const uint64_t* __restrict__ hoff,
+                                 int64_t n_digits_total, TaskLists TL, int* err) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t c = i < n_digits_total ? dcount[i] : 0u;
   Task T;
   T.begin = 0; T.rem = 0; T.row = 0; T.buf = 0; T.len = 0;
-  uint64_t b = 0;
-  if (c) {
+  uint64_t b = 0, c = 0;
+  if (i < n_digits_total) {
     const int64_t t = find_task(digit_base, n, (uint64_t)i);
     T = tasks[t];
-    b = T.begin + (doff[i] - doff[digit_base[t]]);
+    const uint64_t d = (uint64_t)i - digit_base[t], nch = (uint64_t)ceil_div((int64_t)T.len, SPLIT_CH);
+    const uint64_t mb = mat_base[t];
+    const uint64_t lo = hoff[mb + d * nch], hi = hoff[mb + (d + 1) * nch];
+    c = hi - lo;
+    b = T.begin + (lo - hoff[mb]);
   }
   // a bucket within 4x of its expected size is split again (its parent was too large for one
   // split's 8 bits); one far above it holds a few hot keys and goes to the hash path
