@@ -267,6 +267,10 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   OutRows O;
   O.rule = T->b.rule; O.aid = T->b.aid; O.aid_next = T->b.aid_next; O.count = T->b.count; O.count_ge2 = T->b.count_ge2;
   O.cap = P; O.stats = stats;
+  // profiling ablation: OTTOHIP_REDUCE_DBG=1 drops the register-sort kernels' row stores
+  static const int rdbg = getenv("OTTOHIP_REDUCE_DBG") ? atoi(getenv("OTTOHIP_REDUCE_DBG")) : 0;
+  OutRows Osort = O;
+  if (rdbg & 1) Osort.cap = 0;
   int herr = 0;
 
   int ph = ctx->begin("reduce", s, 4.0 * (double)P);
@@ -314,7 +318,7 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
 #define OH_SORT(c, M)                                                                                      \
     if (nlist[c])                                                                                          \
       k_agg_sort<M><<<(unsigned)std::min<uint64_t>(ceil_div((int64_t)nlist[c], 4), sgrid), 256, 0, s>>>(   \
-          TL.sort[c], (int64_t)nlist[c], w0, w1, row_key, R, Lt, n_rules, O);
+          TL.sort[c], (int64_t)nlist[c], w0, w1, row_key, R, Lt, n_rules, Osort);
     OH_SORT(0, 1) OH_SORT(1, 2) OH_SORT(2, 4) OH_SORT(3, 8) OH_SORT(4, 16)
 #undef OH_SORT
     if (nlist[N_SORT]) {  // tasks that overflow the LDS table are appended to the split list

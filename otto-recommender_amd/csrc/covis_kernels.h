@@ -1478,7 +1478,17 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_hist(const Task* __restrict__
   const uint32_t* W = (T.buf ? w1 : w0) + T.begin;
   for (int i = threadIdx.x; i < 256; i += SPLIT_T) h[i] = 0;
   __syncthreads();
-  for (uint64_t i = c0 + threadIdx.x; i < c1; i += SPLIT_T) atomicAdd(&h[split_digit(W[i], F, T.rem, k)], 1u);
+  for (uint64_t i0 = c0; i0 < c1; i0 += 8 * SPLIT_T) {  // 8 loads in flight per thread
+    uint32_t wr[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint64_t i = i0 + threadIdx.x + j * SPLIT_T;
+      wr[j] = i < c1 ? W[i] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (i0 + threadIdx.x + j * SPLIT_T < c1) atomicAdd(&h[split_digit(wr[j], F, T.rem, k)], 1u);
+  }
   __syncthreads();
   for (uint32_t d = threadIdx.x; d < nd; d += SPLIT_T) hmat[mat_base[t] + (uint64_t)d * nch + c] = h[d];
 }
