@@ -25,7 +25,7 @@ namespace ottohip {
 
 constexpr int EV_BLOCK = 256;     // events per wave block (sessions starting in it)
 constexpr int LCAP = 512;         // sessions up to LCAP events run from LDS
-constexpr int SPLIT_TARGET = 512; // hashed split buckets aim at this many words
+constexpr int SPLIT_MEAN = 420;   // hashed split buckets average at most this many words
 constexpr uint32_t W_EMPTY = 0xFFFFFFFFu;
 constexpr int STAT_STRIPES = 256;            // copies of the per-rule statistics
 constexpr int STAT_STRIDE = MAX_RULES * 4;   // u64 per copy (256 B: one L2 line pair per stripe)
@@ -1425,20 +1425,20 @@ __global__ void k_classify_rows(const uint64_t* __restrict__ row_begin, int64_t 
 constexpr int SPLIT_CH = 16384;
 constexpr int SPLIT_T = 256;
 
-// Bits for one split: enough for SPLIT_TARGET-word buckets, 1..8.
-__device__ __forceinline__ int split_bits(const Task& t) {
-  int k = 1;
-  while (k < 8 && ((uint64_t)t.len >> k) > (uint64_t)SPLIT_TARGET) ++k;
-  return k;
+// Digits of one split: ceil(len / SPLIT_MEAN), 2..256 (any count, not only powers of two), so
+// hashed buckets average <= SPLIT_MEAN words and almost all fit the 512-word register sort.
+__device__ __forceinline__ uint32_t split_ndig(const Task& t) {
+  const uint64_t d = ((uint64_t)t.len + SPLIT_MEAN - 1) / SPLIT_MEAN;
+  return d < 2 ? 2u : (d > 256 ? 256u : (uint32_t)d);
 }
-// Split digit: the top k bits of a hash of the word's (rule, aid_next) part, seeded by the
-// split level. Every word of one output row (all its files) lands in the same bucket, buckets
-// are balanced whatever the aid_next distribution, and a bucket split again at the next level
+// Split digit: a hash of the word's (rule, aid_next) part, seeded by the split level, scaled to
+// nd digits. Every word of one output row (all its files) lands in the same bucket, buckets are
+// balanced whatever the aid_next distribution, and a bucket split again at the next level
 // spreads over fresh digits. Row order inside the table is not part of the contract.
-__device__ __forceinline__ uint32_t split_digit(uint32_t w, int F, uint32_t level, int k) {
+__device__ __forceinline__ uint32_t split_digit(uint32_t w, int F, uint32_t level, uint32_t nd) {
   uint32_t x = (w >> F) ^ (level * 0x9E3779B9u);
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
-  return x >> (32 - k);
+  return (uint32_t)(((uint64_t)x * nd) >> 32);
 }
 // Split of one level, no global atomics: per task, chunks of SPLIT_CH words and 2^k digits; a
 // (digit-major, chunk-minor) matrix of per-chunk digit counts is scanned once, which gives every
@@ -1447,7 +1447,7 @@ __global__ void k_split_prepare(const Task* __restrict__ tasks, int64_t n, uint3
                                 uint32_t* __restrict__ ndigits, uint32_t* __restrict__ nent) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint32_t nch = (uint32_t)ceil_div((int64_t)tasks[i].len, SPLIT_CH), nd = 1u << split_bits(tasks[i]);
+  const uint32_t nch = (uint32_t)ceil_div((int64_t)tasks[i].len, SPLIT_CH), nd = split_ndig(tasks[i]);
   nchunks[i] = nch;
   ndigits[i] = nd;
   nent[i] = nch * nd;
@@ -1470,8 +1470,7 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_hist(const Task* __restrict__
   __shared__ uint32_t h[256];
   const int64_t t = find_task(chunk_base, n, blockIdx.x);
   const Task T = tasks[t];
-  const int k = split_bits(T);
-  const uint32_t nd = 1u << k, nch = (uint32_t)ceil_div((int64_t)T.len, SPLIT_CH);
+  const uint32_t nd = split_ndig(T), nch = (uint32_t)ceil_div((int64_t)T.len, SPLIT_CH);
   const uint32_t c = (uint32_t)(blockIdx.x - chunk_base[t]);
   const uint64_t c0 = (uint64_t)c * SPLIT_CH;
   const uint64_t c1 = c0 + SPLIT_CH < T.len ? c0 + SPLIT_CH : T.len;
@@ -1487,7 +1486,7 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_hist(const Task* __restrict__
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      if (i0 + threadIdx.x + j * SPLIT_T < c1) atomicAdd(&h[split_digit(wr[j], F, T.rem, k)], 1u);
+      if (i0 + threadIdx.x + j * SPLIT_T < c1) atomicAdd(&h[split_digit(wr[j], F, T.rem, nd)], 1u);
   }
   __syncthreads();
   for (uint32_t d = threadIdx.x; d < nd; d += SPLIT_T) hmat[mat_base[t] + (uint64_t)d * nch + c] = h[d];
@@ -1506,8 +1505,7 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
   __shared__ uint32_t wsum[SPLIT_T / 64];
   const int64_t t = find_task(chunk_base, n, blockIdx.x);
   const Task T = tasks[t];
-  const int k = split_bits(T);
-  const uint32_t nd = 1u << k, nch = (uint32_t)ceil_div((int64_t)T.len, SPLIT_CH);
+  const uint32_t nd = split_ndig(T), nch = (uint32_t)ceil_div((int64_t)T.len, SPLIT_CH);
   const uint32_t c = (uint32_t)(blockIdx.x - chunk_base[t]);
   const uint64_t c0 = (uint64_t)c * SPLIT_CH;
   const uint64_t c1 = c0 + SPLIT_CH < T.len ? c0 + SPLIT_CH : T.len;
@@ -1528,7 +1526,7 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < SUB_PER_T; ++j) {
-      dg[j] = split_digit(wr[j], F, T.rem, k);
+      dg[j] = split_digit(wr[j], F, T.rem, nd);
       if (tid + j * SPLIT_T < m) atomicAdd(&h[dg[j]], 1u);
     }
     __syncthreads();
@@ -1548,7 +1546,7 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
     __syncthreads();
     for (int p = tid; p < m; p += SPLIT_T) {
       const uint32_t w = stage[p];
-      const uint32_t d = split_digit(w, F, T.rem, k);
+      const uint32_t d = split_digit(w, F, T.rem, nd);
       Wout[gb[d] + (p - st[d])] = w;
     }
     __syncthreads();
@@ -1575,7 +1573,7 @@ __global__ void k_split_classify(const Task* __restrict__ tasks, int64_t n, cons
   }
   // a bucket within 4x of its expected size is split again (its parent was too large for one
   // split's 8 bits); one far above it holds a few hot keys and goes to the hash path
-  const bool again = c != 0 && (uint64_t)c <= 4 * (((uint64_t)T.len >> split_bits(T)) + 1);
+  const bool again = c != 0 && (uint64_t)c <= 4 * ((uint64_t)T.len / split_ndig(T) + 1);
   push_task_block(TL, c != 0, b, c, T.row, T.rem + 1u, T.buf ^ 1u, again, err);
 }
 
