@@ -22,6 +22,9 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 PMC_FILE = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
+# kernels of each co-visitation phase (HIP-event timed on the launch stream; rocprof sums agree)
+PHASE_KERNELS = {"prep_count": "k_block_first + k_prep_count", "rows": "radix sort (k_rs_*), k_gather_counts, scans, k_rows",
+                 "emit": "k_emit", "reduce": "k_classify_rows, k_agg_sort<M>, k_agg_hash, k_split_*, scans"}
 
 
 def pmc_traffic(key: str):
@@ -268,12 +271,24 @@ def main():
         return
     # byte model of SURVEY.md §8(d): B = 9E + 8(S+1) + 16P + 12U
     b_model = 9.0 * n_events + 8.0 * (n_sess + 1) + 16.0 * pairs + 12.0 * rows
+    # algorithmic bytes per phase (one launch group per build; DESIGN.md §5 derives each):
+    #   prep_count  read aid/ts/type + offsets (9E + 8S), write ev, cnt, row key, position (20E)
+    #   rows        read row keys + counts (8E), write word offsets (8E) + row keys / starts (12U_r)
+    #   emit        read ev, cnt, word offsets + offsets (20E + 8S), write one 4-B word per pair (4P)
+    #   reduce      read every pair word once (4P), write every output row once (17U)
+    E_, S_ = n_events / world, n_sess / world
+    alg = {"prep_count": 29.0 * E_ + 8.0 * S_, "rows": 16.0 * E_, "emit": 20.0 * E_ + 8.0 * S_ + 4.0 * pairs / world,
+           "reduce": 4.0 * pairs / world + 17.0 * rows / world}
+    ph_ms = {p[0]: p[1] for p in phases}
     dom = max(phases, key=lambda p: p[1]) if phases else ("step", t_step * 1e3, b_model)
-    # algorithmic bytes of the dominant phase; reduce = read every pair word once (4P) + write
-    # every output row once (17U: rule u8, aid, aid_next, count, count_ge2)
-    dom_bytes = (4.0 * pairs / world + 17.0 * rows / world) if dom[0] == "reduce" else (dom[2] if dom[2] > 0 else b_model)
-    achieved = dom_bytes / (dom[1] / 1e3) / 1e9
-    traffic = pmc_traffic("covis_reduce_phase") if (dom[0] == "reduce" and world == 1) else None
+
+    def roof(ph):
+        a = alg.get(ph, b_model) / (ph_ms[ph] / 1e3) / 1e9
+        tr = pmc_traffic(f"covis_{ph}_phase") if world == 1 else None
+        return {"bound": "hbm", "kernel": ph, "kernels": PHASE_KERNELS.get(ph, ph), "achieved": a,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": a / HBM_PEAK_GBS, "traffic": tr,
+                "algorithmic_bytes": alg.get(ph, b_model), "ms": ph_ms[ph],
+                "traffic_source": f"{os.path.relpath(PMC_FILE, ROOT)} (rocprofv3 --pmc FETCH_SIZE x2, WRITE_SIZE)"}
     out = {
         "metric": "co-visit pairs/sec + candidates/sec at 220M events, 1/2/4/8 MI355X",
         "value": pairs / t_step,
@@ -295,9 +310,8 @@ def main():
         "events_per_s": n_events / t_step,
         "step_roofline": {"bound": "hbm", "model_bytes": b_model, "achieved": b_model / t_step / 1e9,
                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": b_model / t_step / 1e9 / HBM_PEAK_GBS},
-        "roofline": {"bound": "hbm", "kernel": dom[0], "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "algorithmic_bytes": dom_bytes,
-                     "traffic_source": "profiles/r1_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE)"},
+        "roofline": roof(dom[0]),
+        "phase_rooflines": {ph: roof(ph) for ph in ph_ms if ph in alg},
         "phases_ms": {p[0]: round(p[1], 3) for p in phases},
         "gen_s": round(gen_s, 1),
     }
