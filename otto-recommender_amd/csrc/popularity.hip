@@ -59,37 +59,48 @@ __global__ __launch_bounds__(64) void k_sess_emb(const int64_t* __restrict__ off
 constexpr int KM_MAXK = 64;
 constexpr double KM_FX = 16777216.0;  // 2^24 fixed point for the cluster sums
 
-// one thread per row; centroids (k x dim f32) and their squared norms in LDS
-// per-block sums in LDS (int64 fixed point), flushed with one device atomic per (cluster, dim).
-// KP = k rounded up to a multiple of 8: padded centroids are 0 with |c|^2 = +inf (never chosen),
-// so the distance loop has no per-cluster predicate.
+// Centroids transposed to [dim][KP] with squared norms (padding: 0 and +inf, never chosen), so the
+// assignment kernel reads them with wave-uniform scalar loads (SGPR operands of the FMAs).
+__global__ void k_km_prep(const float* __restrict__ C, int k, int dim, int KP, float* __restrict__ Ct,
+                          float* __restrict__ cn) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < KP * dim) {
+    const int d = i / KP, c = i % KP;
+    Ct[i] = c < k ? C[c * dim + d] : 0.f;
+  }
+  if (i < KP) {
+    float s = 0.f;
+    for (int d = 0; d < dim && i < k; ++d) s += C[i * dim + d] * C[i * dim + d];
+    cn[i] = i < k ? s : INFINITY;
+  }
+}
+
+// One lane per row for the distances: |x - c|^2 = |x|^2 - 2 x.c + |c|^2, the row streamed once
+// (16-B loads), all KP dots accumulated against scalar-loaded centroid columns. Then the wave
+// walks its 64 rows with lanes over dimensions and adds each row into its cluster's per-block
+// sums in LDS (2^-24 fixed point, int64: the update is independent of the atomic order),
+// flushed with one device atomic per (cluster, dim).
 template <int KP>
 __global__ __launch_bounds__(256) void k_km_assign(const float* __restrict__ X, int64_t n, int dim,
-                                                   const float* __restrict__ C, int k, int32_t* __restrict__ label,
-                                                   unsigned long long* __restrict__ sums,
+                                                   const float* __restrict__ Ct, const float* __restrict__ cn, int k,
+                                                   int32_t* __restrict__ label, unsigned long long* __restrict__ sums,
                                                    unsigned long long* __restrict__ cnt, double* __restrict__ inertia) {
   extern __shared__ unsigned long long smem64[];
-  unsigned long long* ls = smem64;                       // k * dim sums (fixed point, two's complement)
-  unsigned long long* lc = smem64 + k * dim;             // k counts
-  float* Cs = reinterpret_cast<float*>(smem64 + k * dim + k);  // KP * dim
-  float* cn = Cs + KP * dim;                             // KP
-  for (int i = threadIdx.x; i < k * dim; i += blockDim.x) { Cs[i] = C[i]; ls[i] = 0ull; }
-  for (int i = threadIdx.x; i < k; i += blockDim.x) lc[i] = 0ull;
-  __syncthreads();
-  for (int i = k * dim + threadIdx.x; i < KP * dim; i += blockDim.x) Cs[i] = 0.f;
-  for (int c = threadIdx.x; c < KP; c += blockDim.x) {
-    float s = 0.f;
-    for (int d = 0; d < dim && c < k; ++d) s += Cs[c * dim + d] * Cs[c * dim + d];
-    cn[c] = c < k ? s : INFINITY;
+  unsigned long long* ls = smem64;            // k * dim sums (fixed point, two's complement)
+  unsigned long long* lc = smem64 + k * dim;  // k counts
+  if (sums) {
+    for (int i = threadIdx.x; i < k * dim; i += blockDim.x) ls[i] = 0ull;
+    for (int i = threadIdx.x; i < k; i += blockDim.x) lc[i] = 0ull;
   }
   __syncthreads();
+  const int l = threadIdx.x & 63;
   double part = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const float* x = X + i * dim;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); i0 < n; i0 += stride) {
+    const int64_t i = i0 + l;
+    const bool valid = i < n;
+    const float* x = X + (valid ? i : i0) * dim;
     float xn = 0.f;
-    float best = INFINITY;
-    int bc = 0;
-    // |x - c|^2 = |x|^2 - 2 x.c + |c|^2; the row is streamed once (16-B loads), all k dots accumulated
     float dot[KP];
 #pragma unroll
     for (int c = 0; c < KP; ++c) dot[c] = 0.f;
@@ -97,34 +108,57 @@ __global__ __launch_bounds__(256) void k_km_assign(const float* __restrict__ X, 
       const float4* x4 = reinterpret_cast<const float4*>(x);
       for (int d4 = 0; d4 < (dim >> 2); ++d4) {
         const float4 v = x4[d4];
-        const float xs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll 1
+        for (int u = 0; u < 4; ++u) {  // one centroid column (KP SGPRs) at a time
+          const float xv = u == 0 ? v.x : (u == 1 ? v.y : (u == 2 ? v.z : v.w));
+          const float* col = Ct + (4 * d4 + u) * KP;
+          xn += xv * xv;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int d = 4 * d4 + u;
-          xn += xs[u] * xs[u];
-#pragma unroll
-          for (int c = 0; c < KP; ++c) dot[c] += xs[u] * Cs[c * dim + d];
+          for (int c = 0; c < KP; ++c) dot[c] += xv * col[c];
         }
       }
     } else {
       for (int d = 0; d < dim; ++d) {
         const float xv = x[d];
+        const float* col = Ct + d * KP;
         xn += xv * xv;
 #pragma unroll
-        for (int c = 0; c < KP; ++c) dot[c] += xv * Cs[c * dim + d];
+        for (int c = 0; c < KP; ++c) dot[c] += xv * col[c];
       }
     }
+    float best = INFINITY;
+    int bc = 0;
 #pragma unroll
     for (int c = 0; c < KP; ++c) {
       const float dd = xn - 2.f * dot[c] + cn[c];
       if (dd < best) { best = dd; bc = c; }  // ties: lowest cluster index
     }
-    label[i] = bc;
-    part += (double)fmaxf(best, 0.f);
-    if (sums) {
-      for (int d = 0; d < dim; ++d)
-        atomicAdd(&ls[bc * dim + d], (unsigned long long)__float2ll_rn(x[d] * 16777216.0f));  // exact 2^24 scaling
-      atomicAdd(&lc[bc], 1ull);
+    if (valid) {
+      label[i] = bc;
+      part += (double)fmaxf(best, 0.f);
+    }
+    if (sums) {  // rows of this wave, lanes over dimensions
+      const int nr = (int)min<int64_t>(64, n - i0);
+      for (int r0 = 0; r0 < nr; r0 += 8) {  // 8 rows' loads in flight
+        float xa[8], xb[8];
+        int cc[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int r = r0 + q < nr ? r0 + q : nr - 1;
+          cc[q] = __shfl(bc, r);
+          const float* xr = X + (i0 + r) * dim;
+          xa[q] = l < dim ? xr[l] : 0.f;
+          xb[q] = l + 64 < dim ? xr[l + 64] : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          if (r0 + q >= nr) break;
+          unsigned long long* row = ls + cc[q] * dim;  // exact 2^24 scaling
+          if (l < dim) atomicAdd(&row[l], (unsigned long long)__float2ll_rn(xa[q] * 16777216.0f));
+          if (l + 64 < dim) atomicAdd(&row[l + 64], (unsigned long long)__float2ll_rn(xb[q] * 16777216.0f));
+          if (l == 0) atomicAdd(&lc[cc[q]], 1ull);
+        }
+      }
     }
   }
   __syncthreads();
@@ -143,15 +177,23 @@ __global__ __launch_bounds__(256) void k_km_assign(const float* __restrict__ X, 
   if ((threadIdx.x & 63) == 0) atomicAdd(inertia, part);
 }
 
-static void launch_km_assign(int k, unsigned grid, size_t lds, hipStream_t s, const float* X, int64_t n, int dim,
-                             const float* C, int32_t* labels, unsigned long long* sums, unsigned long long* cnt,
-                             double* inr) {
-  switch ((k + 7) / 8) {
-#define KM_CASE(q) case q: k_km_assign<8 * q><<<grid, 256, lds, s>>>(X, n, dim, C, k, labels, sums, cnt, inr); break;
+static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int64_t n, int dim, const float* C,
+                            int32_t* labels, unsigned long long* sums, unsigned long long* cnt, double* inr) {
+  const int KP = (k + 7) / 8 * 8;
+  float *Ct, *cn;
+  OH_TRY(ctx->ws.get("km_ct", (size_t)KP * dim, &Ct));
+  OH_TRY(ctx->ws.get("km_cn", (size_t)KP, &cn));
+  k_km_prep<<<grid_for((int64_t)KP * dim), 256, 0, s>>>(C, k, dim, KP, Ct, cn);
+  const size_t lds = sums ? ((size_t)k * dim + k) * 8 : 8;
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n, 256), (int64_t)ctx->n_cu * 4);
+  switch (KP / 8) {
+#define KM_CASE(q) case q: k_km_assign<8 * q><<<grid, 256, lds, s>>>(X, n, dim, Ct, cn, k, labels, sums, cnt, inr); break;
     KM_CASE(1) KM_CASE(2) KM_CASE(3) KM_CASE(4) KM_CASE(5) KM_CASE(6) KM_CASE(7) KM_CASE(8)
 #undef KM_CASE
     default: break;
   }
+  OH_HIP(hipGetLastError());
+  return 0;
 }
 
 // ---------------------------------------------------------------- C3
@@ -300,7 +342,7 @@ int ottohip_kmeans_step(ottohip_ctx* ctx, const float* X, int64_t n, int dim, fl
   if (!ctx || !X || !centroids || !labels || n < 1 || dim < 1 || dim > EMB_MAXD || k < 1 || k > KM_MAXK) {
     set_error("kmeans_step: bad arguments (k <= %d, dim <= %d)", KM_MAXK, EMB_MAXD); return OTTOHIP_EINVAL;
   }
-  if (((size_t)k * dim + k) * 8 + ((size_t)((k + 7) / 8 * 8) * (dim + 1)) * sizeof(float) > 65536) {
+  if (((size_t)k * dim + k) * 8 > 65536) {
     set_error("kmeans_step: k * dim too large for LDS"); return OTTOHIP_ELIMIT;
   }
   hipStream_t s = S(stream);
@@ -314,10 +356,7 @@ int ottohip_kmeans_step(ottohip_ctx* ctx, const float* X, int64_t n, int dim, fl
   OH_HIP(hipMemsetAsync(sums, 0, (size_t)k * dim * 8, s));
   OH_HIP(hipMemsetAsync(cnt, 0, (size_t)k * 8, s));
   OH_HIP(hipMemsetAsync(inr, 0, 8, s));
-  const size_t lds = ((size_t)k * dim + k) * 8 + ((size_t)((k + 7) / 8 * 8) * (dim + 1)) * sizeof(float);
-  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n, 256), (int64_t)ctx->n_cu * 4);
-  launch_km_assign(k, grid, lds, s, X, n, dim, centroids, labels, sums, cnt, inr);
-  OH_HIP(hipGetLastError());
+  OH_TRY(launch_km_assign(ctx, k, s, X, n, dim, centroids, labels, sums, cnt, inr));
   std::vector<unsigned long long> hs((size_t)k * dim);
   std::vector<unsigned long long> hc(k);
   std::vector<float> hcen((size_t)k * dim);
@@ -349,17 +388,12 @@ int ottohip_kmeans_assign(ottohip_ctx* ctx, const float* X, int64_t n, int dim, 
   if (!ctx || !X || !centroids || !labels || n < 1 || dim < 1 || dim > EMB_MAXD || k < 1 || k > KM_MAXK) {
     set_error("kmeans_assign: bad arguments"); return OTTOHIP_EINVAL;
   }
-  if (((size_t)k * dim + k) * 8 + ((size_t)((k + 7) / 8 * 8) * (dim + 1)) * sizeof(float) > 65536) {
-    set_error("kmeans_assign: k * dim too large for LDS"); return OTTOHIP_ELIMIT;
-  }
+
   hipStream_t s = S(stream);
   double* inr;
   OH_TRY(ctx->ws.get("km_inertia", 1, &inr));
   OH_HIP(hipMemsetAsync(inr, 0, 8, s));
-  const size_t lds = ((size_t)k * dim + k) * 8 + ((size_t)((k + 7) / 8 * 8) * (dim + 1)) * sizeof(float);
-  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n, 256), (int64_t)ctx->n_cu * 4);
-  launch_km_assign(k, grid, lds, s, X, n, dim, centroids, labels, nullptr, nullptr, inr);
-  OH_HIP(hipGetLastError());
+  OH_TRY(launch_km_assign(ctx, k, s, X, n, dim, centroids, labels, nullptr, nullptr, inr));
   double h = 0.0;
   OH_TRY(d2h(&h, inr, 1, s));
   if (inertia) *inertia = h;
