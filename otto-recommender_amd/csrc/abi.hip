@@ -346,12 +346,15 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     uint64_t tt[3];
     if ((rc = d2h(tt, tot2, 3, s))) return rc;
     const int64_t nchunks = (int64_t)tt[0], ndig = (int64_t)tt[1], nent = (int64_t)tt[2];
-    uint32_t* hmat;
+    uint32_t *hmat, *ctask;
     uint64_t* hoff;
-    if ((rc = ws.get("sp_hmat", (size_t)nent, &hmat)) || (rc = ws.get("sp_hoff", (size_t)nent + 1, &hoff))) return rc;
-    k_split_hist<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, mtb, w0, w1, Lt.F, hmat);
+    if ((rc = ws.get("sp_hmat", (size_t)nent, &hmat)) || (rc = ws.get("sp_hoff", (size_t)nent + 1, &hoff)) ||
+        (rc = ws.get("sp_ctask", (size_t)nchunks, &ctask)))
+      return rc;
+    k_split_chunk_task<<<grid_for(ns), 256, 0, s>>>(chb, nch, ns, ctask);
+    k_split_hist<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, w0, w1, Lt.F, hmat);
     if ((rc = exclusive_scan_u32(ctx, hmat, hoff, nent, hoff + nent, s))) return rc;
-    k_split_scatter<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, mtb, hoff, w0, w1, Lt.F);
+    k_split_scatter<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, hoff, w0, w1, Lt.F);
     // next lists (a sub-bucket is one task in exactly one list: ndig bounds every list)
     const uint64_t capn = (uint64_t)ndig;
     if ((rc = get_lists(std::max(cap0, capn), srcA ? "t_splitB" : "t_splitA"))) return rc;

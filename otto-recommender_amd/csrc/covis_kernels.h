@@ -667,19 +667,31 @@ struct EmitLds {
   uint32_t sfile[64];
   uint16_t espos[EB_CAP];               // per batch event: position in tev (EB_NONE: invalid)
   uint8_t esid[EB_CAP];                 // per batch event: session index in the batch
+  uint32_t mark[64];                    // flush round id at the window positions where a record starts
 };
 
-// expand records [0, nrec) holding tot pairs: lane k of round c writes pair c + k
+// expand records [0, nrec) holding tot pairs: lane k of round c writes pair c + k. Record starts
+// are strictly increasing (a record holds >= 1 pair). Each lane keeps the starts of records l and
+// l + 64 in registers and marks the window position of a start that falls in the round, so a
+// lane's record is the last one of earlier rounds plus the marks at or below the lane: one LDS
+// write and read per round instead of a binary search per pair.
 __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, int F, uint32_t* __restrict__ words,
-                                           int dbg) {
+                                           int dbg, uint32_t& rid) {
   const uint32_t l = lane_id();
+  const uint32_t sa = (int)l < nrec ? S.rpre[l] : 0xFFFFFFFFu;
+  const uint32_t sb = (int)l + 64 < nrec ? S.rpre[l + 64] : 0xFFFFFFFFu;
+  int ob = -1;  // last record starting before the round's window
   for (uint32_t c = 0; c < tot; c += 64) {
+    ++rid;
+    if (sa - c < 64u) S.mark[sa - c] = rid;
+    if (sb - c < 64u) S.mark[sb - c] = rid;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const uint64_t mm = __ballot(S.mark[l] == rid);
+    const int o = ob + (int)__popcll(mm & (~0ull >> (63u - l)));
+    ob += (int)__popcll(mm);
     const uint32_t p = c + l;
     if (p < tot) {
-      int o = 0;
-#pragma unroll
-      for (int st = EB_RCAP / 2; st >= 1; st >>= 1)
-        if (o + st < nrec && S.rpre[o + st] <= p) o += st;
       const uint32_t off = p - S.rpre[o];
       const uint32_t jj = S.rj[o];
       uint32_t j = (jj & 1023u) + off;
@@ -707,6 +719,8 @@ __global__ __launch_bounds__(64) void k_emit(const int64_t* __restrict__ off, co
   int maxq = 0;
 #pragma unroll
   for (int t = 0; t < 3; ++t) maxq = max(maxq, R.n_of_type[t]);
+  S.mark[l] = 0u;
+  uint32_t rid = 0;  // flush round id (marks of earlier rounds never match)
   int fcur = file_of(fb, nf, s0);
   int64_t next_b = fcur + 1 < nf ? fb[fcur + 1] : INT64_MAX;
   uint32_t fid_cur = fid[fcur];
@@ -853,7 +867,7 @@ __global__ __launch_bounds__(64) void k_emit(const int64_t* __restrict__ off, co
           if (nrec + nn > EB_RCAP) {
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            emit_flush(S, nrec, tot, L.F, words, dbg);
+            emit_flush(S, nrec, tot, L.F, words, dbg, rid);
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             nrec = 0; tot = 0;
@@ -876,7 +890,7 @@ __global__ __launch_bounds__(64) void k_emit(const int64_t* __restrict__ off, co
     if (nrec > 0) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      emit_flush(S, nrec, tot, L.F, words, dbg);
+      emit_flush(S, nrec, tot, L.F, words, dbg, rid);
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1462,13 +1476,24 @@ __device__ __forceinline__ int64_t find_task(const uint64_t* chunk_base, int64_t
   return lo;
 }
 
+// chunk -> task map of one split level: every hist / scatter block reads its task with one load
+// instead of a binary search over the chunk bases (~20 dependent loads at 5e5 tasks)
+__global__ void k_split_chunk_task(const uint64_t* __restrict__ chunk_base, const uint32_t* __restrict__ nchunks,
+                                   int64_t n, uint32_t* __restrict__ chunk_task) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const uint64_t b = chunk_base[t];
+  for (uint32_t c = 0; c < nchunks[t]; ++c) chunk_task[b + c] = (uint32_t)t;
+}
+
 __global__ __launch_bounds__(SPLIT_T) void k_split_hist(const Task* __restrict__ tasks, int64_t n,
                                                         const uint64_t* __restrict__ chunk_base,
+                                                        const uint32_t* __restrict__ chunk_task,
                                                         const uint64_t* __restrict__ mat_base,
                                                         const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
                                                         int F, uint32_t* __restrict__ hmat) {
   __shared__ uint32_t h[256];
-  const int64_t t = find_task(chunk_base, n, blockIdx.x);
+  const int64_t t = chunk_task[blockIdx.x];
   const Task T = tasks[t];
   const uint32_t nd = split_ndig(T), nch = (uint32_t)ceil_div((int64_t)T.len, SPLIT_CH);
   const uint32_t c = (uint32_t)(blockIdx.x - chunk_base[t]);
@@ -1496,6 +1521,7 @@ constexpr int SUB = 4096;             // scatter sub-tile (staged in LDS in digi
 constexpr int SUB_PER_T = SUB / SPLIT_T;  // words per thread per sub-tile, held in registers
 __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restrict__ tasks, int64_t n,
                                                            const uint64_t* __restrict__ chunk_base,
+                                                           const uint32_t* __restrict__ chunk_task,
                                                            const uint64_t* __restrict__ mat_base,
                                                            const uint64_t* __restrict__ hoff,
                                                            uint32_t* __restrict__ w0, uint32_t* __restrict__ w1, int F) {
@@ -1503,7 +1529,7 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
   __shared__ uint64_t gb[256];
   __shared__ uint32_t stage[SUB];
   __shared__ uint32_t wsum[SPLIT_T / 64];
-  const int64_t t = find_task(chunk_base, n, blockIdx.x);
+  const int64_t t = chunk_task[blockIdx.x];
   const Task T = tasks[t];
   const uint32_t nd = split_ndig(T), nch = (uint32_t)ceil_div((int64_t)T.len, SPLIT_CH);
   const uint32_t c = (uint32_t)(blockIdx.x - chunk_base[t]);
@@ -1514,13 +1540,25 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
   const int tid = threadIdx.x;
   const uint64_t mb = mat_base[t];
   if ((uint32_t)tid < nd) gb[tid] = T.begin + (hoff[mb + (uint64_t)tid * nch + c] - hoff[mb]);
+  uint32_t wr[SUB_PER_T], dg[SUB_PER_T];
+  {
+    const int m0 = (int)((c1 - c0) < (uint64_t)SUB ? (c1 - c0) : (uint64_t)SUB);
+#pragma unroll
+    for (int j = 0; j < SUB_PER_T; ++j) {  // each sub-tile is read once, into registers
+      const int i = tid + j * SPLIT_T;
+      wr[j] = i < m0 ? Win[c0 + i] : 0u;
+    }
+  }
   for (uint64_t s0 = c0; s0 < c1; s0 += SUB) {
     const int m = (int)((c1 - s0) < (uint64_t)SUB ? (c1 - s0) : (uint64_t)SUB);
-    uint32_t wr[SUB_PER_T], dg[SUB_PER_T];
+    // the next sub-tile is loaded while this one is ranked and written out
+    const uint64_t s1 = s0 + SUB;
+    const int mn = s1 < c1 ? (int)((c1 - s1) < (uint64_t)SUB ? (c1 - s1) : (uint64_t)SUB) : 0;
+    uint32_t wn[SUB_PER_T];
 #pragma unroll
-    for (int j = 0; j < SUB_PER_T; ++j) {  // the sub-tile is read once, into registers
+    for (int j = 0; j < SUB_PER_T; ++j) {
       const int i = tid + j * SPLIT_T;
-      wr[j] = i < m ? Win[s0 + i] : 0u;
+      wn[j] = i < mn ? Win[s1 + i] : 0u;
     }
     h[tid] = 0; fill[tid] = 0;
     __syncthreads();
@@ -1551,6 +1589,8 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
     }
     __syncthreads();
     gb[tid] += h[tid];  // this chunk's cursor per digit moves past the sub-tile
+#pragma unroll
+    for (int j = 0; j < SUB_PER_T; ++j) wr[j] = wn[j];
   }
 }
 
