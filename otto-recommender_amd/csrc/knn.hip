@@ -173,16 +173,13 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
+        // per-lane maxima first: swapping the two maxima gives this lane's query maximum over the
+        // 32 rows, and the 16-register redistribution runs only when some lane has a candidate
+        float mA = accA[u][0], mB = accB[u][0];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {  // accA -> rows + offx, accB -> rows + offy of this lane's query
-          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(accA[u][i]), __float_as_uint(accB[u][i]),
-                                                           false, false);
-          accA[u][i] = __uint_as_float(sw[0]);
-          accB[u][i] = __uint_as_float(sw[1]);
-        }
-        float m = fmaxf(accA[u][0], accB[u][0]);
-#pragma unroll
-        for (int i = 1; i < 16; ++i) m = fmaxf(m, fmaxf(accA[u][i], accB[u][i]));
+        for (int i = 1; i < 16; ++i) { mA = fmaxf(mA, accA[u][i]); mB = fmaxf(mB, accB[u][i]); }
+        const auto msw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mA), __float_as_uint(mB), false, false);
+        const float m = fmaxf(__uint_as_float(msw[0]), __uint_as_float(msw[1]));
         if (ABL == 1) { thr = fmaxf(thr, m * 1e-30f); continue; }  // ablation build: no candidate handling
         if (PRE) {  // group g = tile % KN_C keeps its maximum in sc[g]
           const int gsel = (int)(t % KN_C);
@@ -190,6 +187,15 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
           for (int g = 0; g < KN_C; ++g)
             if (g == gsel) sc[g] = fmaxf(sc[g], m);
           continue;
+        }
+        if (__ballot(m > thr)) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {  // accA -> rows + offx, accB -> rows + offy of this lane's query
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(accA[u][i]), __float_as_uint(accB[u][i]),
+                                                             false, false);
+            accA[u][i] = __uint_as_float(sw[0]);
+            accB[u][i] = __uint_as_float(sw[1]);
+          }
         }
         if (m > thr) {
           const int64_t ib = t * KN_IT + (2 * rp + u) * 32;

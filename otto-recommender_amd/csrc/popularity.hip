@@ -68,7 +68,7 @@ __global__ void k_km_prep(const float* __restrict__ C, int k, int dim, int KP, f
     const int d = i / KP, c = i % KP;
     Ct[i] = c < k ? C[c * dim + d] : 0.f;
   }
-  if (i < KP) {
+  if (i < KM_MAXK) {  // 64 entries: the MFMA kernel reads two full blocks of 32
     float s = 0.f;
     for (int d = 0; d < dim && i < k; ++d) s += C[i * dim + d] * C[i * dim + d];
     cn[i] = i < k ? s : INFINITY;
@@ -177,13 +177,186 @@ __global__ __launch_bounds__(256) void k_km_assign(const float* __restrict__ X, 
   if ((threadIdx.x & 63) == 0) atomicAdd(inertia, part);
 }
 
+// C2 on the matrix cores (k <= 64, dim <= 128, dim % 4 == 0): a wave scores a tile of 32 rows
+// against 32 centroids per v_mfma_f32_32x32x2f32 (NB = 1 or 2 centroid blocks). Lane (i, h)
+// loads 16-B pieces of row i (dims 8q + 4h .. 8q + 4h + 3); the same dims of its centroid column
+// come from LDS, so MFMA (q, u) pairs dim 8q + u (h = 0) with dim 8q + 4 + u (h = 1). The MFMA is
+// an exact f32 fma chain: only the summation order differs from k_km_assign. The argmin is over
+// |c|^2 - 2 x.c (|x|^2 is common to the row, as in sklearn's Lloyd step), ties to the lowest
+// cluster; (value, index) pairs are reduced over the 32 columns by DPP / permlane butterflies.
+// Per-cluster sums as in k_km_assign (2^-24 fixed point, order-independent).
+typedef float km_f32x16 __attribute__((ext_vector_type(16)));
+constexpr int KM_MT = 512;  // threads per block (8 waves)
+constexpr int KM_NQ = 16;   // 16-B pieces per row half (dim <= 128)
+
+__device__ __forceinline__ uint32_t km_ord(float x) {  // order-preserving f32 -> u32
+  const uint32_t b = __float_as_uint(x);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float km_unord(uint32_t o) {
+  return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
+}
+
+template <int NB>
+__global__ __launch_bounds__(KM_MT) void k_km_assign_mfma(const float* __restrict__ X, int64_t n, int dim, int nq,
+                                                        const float* __restrict__ C, const float* __restrict__ cn,
+                                                        int k, int32_t* __restrict__ label,
+                                                        unsigned long long* __restrict__ sums,
+                                                        unsigned long long* __restrict__ cnt,
+                                                        double* __restrict__ inertia) {
+  extern __shared__ unsigned long long smem64[];
+  float4* Bl = reinterpret_cast<float4*>(smem64);                              // [NB][nq][64]
+  int32_t* labl = reinterpret_cast<int32_t*>(Bl + NB * nq * 64);                // [waves][32]
+  float* cnl = reinterpret_cast<float*>(labl + (KM_MT / 64) * 32);             // [64]
+  unsigned long long* ls = reinterpret_cast<unsigned long long*>(cnl + 64);    // k * dim sums, k counts
+  unsigned long long* lc = ls + k * dim;
+  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6, h = l >> 5, i32 = l & 31;
+  for (int e = tid; e < NB * nq * 64; e += KM_MT) {
+    const int ll = e & 63, q = (e >> 6) % nq, b = (e >> 6) / nq;
+    const int c = b * 32 + (ll & 31), d0 = 8 * q + 4 * (ll >> 5);
+    float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < k && d0 < dim) f = *reinterpret_cast<const float4*>(C + (int64_t)c * dim + d0);
+    Bl[e] = f;
+  }
+  if (tid < 64) cnl[tid] = cn[tid];
+  if (sums)
+    for (int i = tid; i < k * dim + k; i += KM_MT) ls[i] = 0ull;
+  __syncthreads();
+  const float cA = cnl[i32], cB = cnl[32 + i32];
+  double part = 0.0;
+  const int64_t ntile = (n + 31) >> 5;
+  const int64_t nwv = (int64_t)gridDim.x * (KM_MT / 64);
+  for (int64_t t = (int64_t)blockIdx.x * (KM_MT / 64) + wv; t < ntile; t += nwv) {
+    const int64_t r0 = t << 5;
+    const float* x = X + (r0 + i32 < n ? r0 + i32 : n - 1) * dim;
+    float4 a[KM_NQ];
+#pragma unroll
+    for (int q = 0; q < KM_NQ; ++q) {
+      const int d0 = 8 * q + 4 * h;
+      a[q] = (q < nq && d0 < dim) ? *reinterpret_cast<const float4*>(x + d0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float xs = 0.f;
+#pragma unroll
+    for (int q = 0; q < KM_NQ; ++q) xs += a[q].x * a[q].x + a[q].y * a[q].y + a[q].z * a[q].z + a[q].w * a[q].w;
+    xs += __shfl_xor(xs, 32);
+    km_f32x16 acc0 = {}, acc1 = {};
+#pragma unroll
+    for (int q = 0; q < KM_NQ; ++q) {
+      if (q < nq) {
+        const float4 b0 = Bl[q * 64 + l];
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].x, b0.x, acc0, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].y, b0.y, acc0, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].z, b0.z, acc0, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].w, b0.w, acc0, 0, 0, 0);
+        if (NB == 2) {
+          const float4 b1 = Bl[(nq + q) * 64 + l];
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].x, b1.x, acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].y, b1.y, acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].z, b1.z, acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].w, b1.w, acc1, 0, 0, 0);
+        }
+      }
+    }
+    // accumulator register r of lane (column i32, half h) holds row (r & 3) + 8 (r >> 2) + 4 h
+    uint32_t kv[16], ki[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      kv[r] = km_ord(cA - 2.f * acc0[r]);
+      ki[r] = (uint32_t)i32;
+      if (NB == 2) {
+        const uint32_t o = km_ord(cB - 2.f * acc1[r]);
+        if (o < kv[r]) { kv[r] = o; ki[r] = 32u + (uint32_t)i32; }
+      }
+    }
+#pragma unroll
+    for (int sft = 1; sft < 32; sft <<= 1) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const uint32_t ov = xor_lane_n(kv[r], sft), oi = xor_lane_n(ki[r], sft);
+        const bool tk = ov < kv[r] || (ov == kv[r] && oi < ki[r]);
+        kv[r] = tk ? ov : kv[r];
+        ki[r] = tk ? oi : ki[r];
+      }
+    }
+    uint32_t mv = kv[0], mi = ki[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r)
+      if (i32 == r) { mv = kv[r]; mi = ki[r]; }
+    const int R = (i32 & 3) + 8 * ((i32 >> 2) & 3) + 4 * h;  // lanes i32 < 16: the row of register i32
+    const float xr = __shfl(xs, R);
+    if (i32 < 16) {
+      labl[wv * 32 + R] = (int32_t)mi;
+      if (r0 + R < n) {
+        label[r0 + R] = (int32_t)mi;
+        part += (double)fmaxf(xr + km_unord(mv), 0.f);
+      }
+    }
+    if (sums) {  // the tile's rows, lanes over dimensions
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      const int nr = (int)min<int64_t>(32, n - r0);
+      for (int rr = 0; rr < nr; rr += 8) {  // 8 rows' loads in flight
+        float xa[8], xb[8];
+        int cc[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int r = rr + q < nr ? rr + q : nr - 1;
+          cc[q] = labl[wv * 32 + r];
+          const float* xq = X + (r0 + r) * dim;
+          xa[q] = l < dim ? xq[l] : 0.f;
+          xb[q] = l + 64 < dim ? xq[l + 64] : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          if (rr + q >= nr) break;
+          unsigned long long* row = ls + cc[q] * dim;  // exact 2^24 scaling
+          if (l < dim) atomicAdd(&row[l], (unsigned long long)__float2ll_rn(xa[q] * 16777216.0f));
+          if (l + 64 < dim) atomicAdd(&row[l + 64], (unsigned long long)__float2ll_rn(xb[q] * 16777216.0f));
+          if (l == 0) atomicAdd(&lc[cc[q]], 1ull);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();  // labl is rewritten by the next tile
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+  }
+  __syncthreads();
+  if (sums) {
+    for (int i = tid; i < k * dim; i += KM_MT)
+      if (ls[i]) atomicAdd(&sums[i], ls[i]);
+    for (int i = tid; i < k; i += KM_MT)
+      if (lc[i]) atomicAdd(&cnt[i], lc[i]);
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint64_t b = __double_as_longlong(part);
+    const uint32_t lo = __shfl_xor((uint32_t)b, o), hi = __shfl_xor((uint32_t)(b >> 32), o);
+    part += __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+  }
+  if (l == 0) atomicAdd(inertia, part);
+}
+
 static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int64_t n, int dim, const float* C,
                             int32_t* labels, unsigned long long* sums, unsigned long long* cnt, double* inr) {
   const int KP = (k + 7) / 8 * 8;
   float *Ct, *cn;
   OH_TRY(ctx->ws.get("km_ct", (size_t)KP * dim, &Ct));
-  OH_TRY(ctx->ws.get("km_cn", (size_t)KP, &cn));
-  k_km_prep<<<grid_for((int64_t)KP * dim), 256, 0, s>>>(C, k, dim, KP, Ct, cn);
+  OH_TRY(ctx->ws.get("km_cn", (size_t)KM_MAXK, &cn));
+  k_km_prep<<<grid_for(std::max<int64_t>((int64_t)KP * dim, KM_MAXK)), 256, 0, s>>>(C, k, dim, KP, Ct, cn);
+  static const bool km_valu = getenv("OTTOHIP_KM_VALU") != nullptr;  // A/B switch: the VALU kernel
+  if (!km_valu && k <= 64 && dim <= 8 * KM_NQ && (dim & 3) == 0 && ((uintptr_t)X & 15) == 0 &&
+      ((uintptr_t)C & 15) == 0) {
+    const int nq = (dim + 7) / 8, NB = k <= 32 ? 1 : 2;
+    const size_t lds = (size_t)NB * nq * 64 * 16 + (KM_MT / 64) * 32 * 4 + 64 * 4 +
+                       (sums ? ((size_t)k * dim + k) * 8 : 8);
+    const int64_t ntile = ceil_div(n, 32);
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(ntile, KM_MT / 64),
+                                                                           (int64_t)ctx->n_cu * 2));
+    auto kern = NB == 1 ? k_km_assign_mfma<1> : k_km_assign_mfma<2>;
+    OH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds));
+    kern<<<grid, KM_MT, lds, s>>>(X, n, dim, nq, C, cn, k, labels, sums, cnt, inr);
+    OH_HIP(hipGetLastError());
+    return 0;
+  }
   const size_t lds = sums ? ((size_t)k * dim + k) * 8 : 8;
   const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n, 256), (int64_t)ctx->n_cu * 4);
   switch (KP / 8) {

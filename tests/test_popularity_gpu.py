@@ -45,6 +45,19 @@ def test_kmeans_matches_restatement(gpu):
     assert abs(km.n_iter_ - it_ref) <= 2
 
 
+def test_kmeans_two_centroid_blocks(gpu):
+    """k > 32: the MFMA assignment scores two 32-centroid blocks per row tile."""
+    from otto_recommender_amd import popularity as gp
+    rng = np.random.default_rng(5)
+    centers = rng.normal(scale=3, size=(50, 100))
+    X = (centers[rng.integers(0, 50, 12000)] + rng.normal(size=(12000, 100))).astype(np.float32)
+    km = gp.KMeans(n_clusters=45, max_iter=100, tol=1e-3, random_state=42).fit(X)
+    lab_ref, C_ref, it_ref = oracle_pop.kmeans(X, 45)
+    assert np.mean(km.labels_.cpu().numpy() == lab_ref) >= 0.999
+    np.testing.assert_allclose(km.cluster_centers_.cpu().numpy(), C_ref, atol=1e-3)
+    assert abs(km.n_iter_ - it_ref) <= 2
+
+
 def test_popularity_ranks_exact(gpu):
     from otto_recommender_amd import popularity as gp
     ev = _events(4000, first=12345)
