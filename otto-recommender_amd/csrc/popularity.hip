@@ -341,8 +341,10 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
   OH_TRY(ctx->ws.get("km_ct", (size_t)KP * dim, &Ct));
   OH_TRY(ctx->ws.get("km_cn", (size_t)KM_MAXK, &cn));
   k_km_prep<<<grid_for(std::max<int64_t>((int64_t)KP * dim, KM_MAXK)), 256, 0, s>>>(C, k, dim, KP, Ct, cn);
-  static const bool km_valu = getenv("OTTOHIP_KM_VALU") != nullptr;  // A/B switch: the VALU kernel
-  if (!km_valu && k <= 64 && dim <= 8 * KM_NQ && (dim & 3) == 0 && ((uintptr_t)X & 15) == 0 &&
+  // the MFMA kernel measured 6.4 ms per Lloyd step at 12.9 M x 100, k = 50, against 5.1 ms for
+  // the VALU kernel below (argmin butterflies and half the rows per wave): opt-in A/B switch only
+  static const bool km_mfma = getenv("OTTOHIP_KM_MFMA") != nullptr;
+  if (km_mfma && k <= 64 && dim <= 8 * KM_NQ && (dim & 3) == 0 && ((uintptr_t)X & 15) == 0 &&
       ((uintptr_t)C & 15) == 0) {
     const int nq = (dim + 7) / 8, NB = k <= 32 ? 1 : 2;
     const size_t lds = (size_t)NB * nq * 64 * 16 + (KM_MT / 64) * 32 * 4 + 64 * 4 +
