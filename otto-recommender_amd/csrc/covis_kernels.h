@@ -1540,25 +1540,13 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
   const int tid = threadIdx.x;
   const uint64_t mb = mat_base[t];
   if ((uint32_t)tid < nd) gb[tid] = T.begin + (hoff[mb + (uint64_t)tid * nch + c] - hoff[mb]);
-  uint32_t wr[SUB_PER_T], dg[SUB_PER_T];
-  {
-    const int m0 = (int)((c1 - c0) < (uint64_t)SUB ? (c1 - c0) : (uint64_t)SUB);
-#pragma unroll
-    for (int j = 0; j < SUB_PER_T; ++j) {  // each sub-tile is read once, into registers
-      const int i = tid + j * SPLIT_T;
-      wr[j] = i < m0 ? Win[c0 + i] : 0u;
-    }
-  }
   for (uint64_t s0 = c0; s0 < c1; s0 += SUB) {
     const int m = (int)((c1 - s0) < (uint64_t)SUB ? (c1 - s0) : (uint64_t)SUB);
-    // the next sub-tile is loaded while this one is ranked and written out
-    const uint64_t s1 = s0 + SUB;
-    const int mn = s1 < c1 ? (int)((c1 - s1) < (uint64_t)SUB ? (c1 - s1) : (uint64_t)SUB) : 0;
-    uint32_t wn[SUB_PER_T];
+    uint32_t wr[SUB_PER_T], dg[SUB_PER_T];
 #pragma unroll
-    for (int j = 0; j < SUB_PER_T; ++j) {
+    for (int j = 0; j < SUB_PER_T; ++j) {  // the sub-tile is read once, into registers
       const int i = tid + j * SPLIT_T;
-      wn[j] = i < mn ? Win[s1 + i] : 0u;
+      wr[j] = i < m ? Win[s0 + i] : 0u;
     }
     h[tid] = 0; fill[tid] = 0;
     __syncthreads();
@@ -1589,8 +1577,6 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
     }
     __syncthreads();
     gb[tid] += h[tid];  // this chunk's cursor per digit moves past the sub-tile
-#pragma unroll
-    for (int j = 0; j < SUB_PER_T; ++j) wr[j] = wn[j];
   }
 }
 
