@@ -729,8 +729,9 @@ extern "C" int ottohip_table_finalize(ottohip_ctx* ctx, const ottohip_table* t, 
   OH_TRY(ws.get("fin_v1", (size_t)m, &v1));
   k_fin_compact<<<grid_for(n), 256, 0, s>>>(flag, idx, n, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2,
                                             use_ge2 ? 1 : 0, sa, sb, sc);
-  // LSD: aid_next asc, then aid asc, then count desc (stable) -> (count desc, aid, aid_next)
-  const int abits = 31;
+  // LSD: aid_next asc, then aid asc, then count desc (stable) -> (count desc, aid, aid_next);
+  // aids are < n_items, so their passes cover bits_for(n_items) bits (3 x 8 at 1.86 M items)
+  const int abits = std::max(1, bits_for((uint64_t)t->n_items));
   uint32_t *k = k0, *v = v0;
   k_iota_key<<<grid_for((int64_t)m), 256, 0, s>>>(sb, (int64_t)m, k, v);
   OH_TRY(radix_sort_pairs(ctx, k, v, k == k0 ? k1 : k0, v == v0 ? v1 : v0, (int64_t)m, abits, s));
