@@ -101,8 +101,11 @@ void ottohip_table_free(ottohip_table* t);
  * keep count >= min_count (MIN_COUNT_TO_SAVE, config.py:56-62), order by count desc with
  * the deterministic tie-break (aid asc, aid_next asc), keep the first max_rows rows
  * (MAX_CO_EVENT_PAIRS_TO_SAVE_DISK). Writes up to max_rows rows; *n_out = rows written.
- * Returns OTTOHIP_ELIMIT if the reference would take its part-wise branch (:135-166),
- * which is not implemented on the device yet. */
+ * Returns OTTOHIP_ELIMIT if the reference would take its part-wise branch (:135-166) on this
+ * table: the host layer runs that branch as whole-file parts (covis.concat_files_w_stats_fused
+ * and, sharded, dist.concat_files_w_stats_sharded), each part counted and finalized with this
+ * call. OTTOHIP_EINVAL if the per-file filter applies and min_count_in_part != 2 (the table's
+ * count_ge2 column is accumulated with the per-file threshold 2 of config.py:63). */
 typedef struct {
   int32_t click_rule;        /* 'click_to' in name */
   int32_t min_count_in_part; /* MIN_COUNT_IN_PART (2) */
@@ -114,6 +117,28 @@ typedef struct {
 int ottohip_table_finalize(ottohip_ctx* ctx, const ottohip_table* t, int rule,
                            const ottohip_merge_params* mp, int32_t* aid, int32_t* aid_next,
                            int32_t* count, int64_t* n_out, void* stream);
+
+/* concat_files_w_stats (model/count_co_events.py:103-181) over n_tables finished tables given as
+ * columns (device; n_rows HOST [n_tables]) concatenated in order: the per-file tables of one
+ * folder (files_stats=None, :114) or the two thresholded folder tables of the train+test merge
+ * (A7, :218-226, files_stats=[train, test]). With N = total rows:
+ *   (1) click_rule && N > filter_rows && !loaded_from_cache: drop rows with count < min_count_in_part;
+ *   (2) rows > max_rows_groupby && !loaded_from_cache: ceil(rows / optim_rows) slices of
+ *       ceil(rows / n_parts) consecutive rows, each groupby-sum -> count >= min_count_in_part ->
+ *       count desc -> head(int(max_rows_groupby / rows * optim_rows)), concatenated;
+ *   (3) groupby-sum -> count >= min_count -> count desc -> head(max_rows).
+ * Row order inside a table is the caller's (the reference's slices follow file row order);
+ * ties at every sort are (aid asc, aid_next asc). Output capacity min(N, max_rows) rows. */
+int ottohip_concat_tables(ottohip_ctx* ctx, int n_tables, const int32_t* const* aid, const int32_t* const* aid_next,
+                          const uint32_t* const* count, const int64_t* n_rows, int32_t n_items,
+                          const ottohip_merge_params* mp, int64_t optim_rows, int loaded_from_cache,
+                          int32_t* out_aid, int32_t* out_aid_next, int32_t* out_count, int64_t* n_out, void* stream);
+/* Histogram of (x[i] >> shift) & mask over i in [lo, hi) of a device array whose equal keys are
+ * contiguous (e.g. the count column of a finalize output, or its aid column inside one count):
+ * hist (device, n_bins u64) is overwritten. The sharded finalize all-reduces these to find the
+ * global head(max_rows) cut. OTTOHIP_ERANGE if a key >= n_bins. */
+int ottohip_run_hist(ottohip_ctx* ctx, const int32_t* x, int64_t lo, int64_t hi, int shift, uint32_t mask,
+                     int64_t n_bins, uint64_t* hist, void* stream);
 
 /* R1: per-aid top-first_n of a final co-visitation table with the reference's features
  * (get_df_count_for_co_event_type, model/retrieve.py:18-63). Input: the table in FILE order

@@ -12,6 +12,7 @@ Contents
   REFERENCE_RULES           config.py:41-49,81-88 restated
   count_co_events_file()    C restatement (covis_oracle.c) of count_co_events.py:91-94, one file
   concat_files_w_stats()    numpy restatement of count_co_events.py:103-181 (merge semantics A6)
+  merge_train_test()        count_co_events.py:209-226 (A6 per folder, then A6 on [train, test]) (A7)
 """
 from __future__ import annotations
 
@@ -187,6 +188,20 @@ def concat_files_w_stats(name: str, parts: list, loaded_from_cache: bool = False
     a, b, c = _sort_count_desc(a[keep], b[keep], c[keep])
     a, b, c = a[:max_pairs], b[:max_pairs], c[:max_pairs]
     return a, b, c.astype(np.int32)
+
+
+def merge_train_test(name: str, train_parts: list, test_parts: list, train_mode: str = "rows",
+                     test_mode: str = "rows", **kw):
+    """Restates the stage orchestration of model/count_co_events.py:209-226 (A7) for one rule:
+    concat_files_w_stats per folder (:214-215), each with its OWN N for the :131 and :135
+    triggers and its own MIN_COUNT_TO_SAVE cut, then concat_files_w_stats on the concatenation
+    [train table, test table] of the two thresholded folder tables (:218-226). Branch (2) of the
+    final merge slices rows of that concatenation (part_mode="rows"), which is deterministic
+    here: both inputs are in (count desc, aid, aid_next) order. *_mode: branch-(2) part
+    definition of each folder merge ("files" = the fused device path's whole-file parts)."""
+    t = concat_files_w_stats(name, train_parts, part_mode=train_mode, **kw)
+    s = concat_files_w_stats(name, test_parts, part_mode=test_mode, **kw)
+    return concat_files_w_stats(name, [t, s], part_mode="rows", **kw)
 
 
 def canonical_digest(tables: dict) -> dict:

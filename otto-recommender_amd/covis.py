@@ -222,6 +222,60 @@ def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTabl
     return out
 
 
+def _merge_params(name: str, max_pairs: int, click_filter_rows: int, max_rows_groupby: int) -> "_lib.MergeParams":
+    mp = _lib.MergeParams()
+    mp.click_rule = 1 if "click_to" in name else 0
+    mp.min_count_in_part = config.MIN_COUNT_IN_PART.get(name, 1)
+    mp.min_count = config.MIN_COUNT_TO_SAVE.get(name, 1)
+    mp.max_rows = int(max_pairs)
+    mp.filter_rows = int(click_filter_rows)
+    mp.max_rows_groupby = int(max_rows_groupby)
+    return mp
+
+
+def concat_tables_w_stats(name: str, tables, n_items: int = config.N_ITEMS_OTTO,
+                          max_rows_groupby: int = config.MAX_ROWS_POLARS_GROUPBY,
+                          optim_rows: int = config.OPTIM_ROWS_POLARS_GROUPBY,
+                          max_pairs: int = config.MAX_CO_EVENT_PAIRS_TO_SAVE_DISK,
+                          click_filter_rows: int = config.CLICK_FILTER_ROWS, loaded_from_cache: bool = False,
+                          stream=None, ctx=None):
+    """model/count_co_events.py:103-181 on finished tables [(aid, aid_next, count) device int32
+    tensors, ...] concatenated in the given order (ottohip_concat_tables): the per-file tables of
+    a folder, or -- the train+test merge of :218-226 (A7) -- the two thresholded folder tables.
+    Branch (2) slices rows of the concatenation as the reference does (:146-155). Returns torch
+    (aid, aid_next, count:int32) in (count desc, aid, aid_next) order."""
+    import torch
+    ctx = ctx or _lib.context()
+    dev = torch.device("cuda", ctx.device)
+    cols = [tuple(torch.as_tensor(x, dtype=torch.int32).to(dev).contiguous() for x in t) for t in tables]
+    nt = len(cols)
+    n = [int(t[0].numel()) for t in cols]
+    for t in cols:
+        if not (t[0].numel() == t[1].numel() == t[2].numel()):
+            raise ValueError("concat_tables_w_stats: ragged table columns")
+    P = ctypes.c_void_p * max(nt, 1)
+    pa, pb, pc = P(*[_lib.ptr(t[0]) for t in cols]), P(*[_lib.ptr(t[1]) for t in cols]), P(*[_lib.ptr(t[2]) for t in cols])
+    nr = (ctypes.c_int64 * max(nt, 1))(*n)
+    mp = _merge_params(name, max_pairs, click_filter_rows, max_rows_groupby)
+    cap = max(1, min(sum(n), int(max_pairs)))
+    a = torch.empty(cap, dtype=torch.int32, device=dev)
+    b = torch.empty(cap, dtype=torch.int32, device=dev)
+    c = torch.empty(cap, dtype=torch.int32, device=dev)
+    n_out = ctypes.c_int64(0)
+    _lib.check(_lib.load().ottohip_concat_tables(ctx.h, nt, pa, pb, pc, nr, int(n_items), ctypes.byref(mp),
+                                                 int(optim_rows), 1 if loaded_from_cache else 0, _lib.ptr(a),
+                                                 _lib.ptr(b), _lib.ptr(c), ctypes.byref(n_out),
+                                                 _lib.stream_handle(stream)))
+    k = int(n_out.value)
+    return a[:k], b[:k], c[:k]
+
+
+def merge_train_test(name: str, train, test, n_items: int = config.N_ITEMS_OTTO, ctx=None, **kw):
+    """A7 (model/count_co_events.py:218-226): concat_files_w_stats on the two thresholded folder
+    tables [train, test] (each the output of A6 over its own folder's files)."""
+    return concat_tables_w_stats(name, [train, test], n_items=n_items, ctx=ctx, **kw)
+
+
 def _n_items_for(aid: np.ndarray) -> int:
     return max(config.N_ITEMS_OTTO, int(aid.max()) + 1 if len(aid) else 1)
 
@@ -270,6 +324,39 @@ def count_co_events_all_files(dir_sessions, dir_stats, skip_if_exists=True):
             a, b, c, _ = tab.to_numpy(n, sort=False)
             _write_table(p, a, b, c, np.uint32)
         tab.free()
+
+
+def _read_table(path):
+    import pyarrow.parquet as pq
+    t = pq.read_table(path, columns=["aid", "aid_next", "count"])
+    return tuple(np.ascontiguousarray(t.column(k).to_numpy().astype(dt, copy=False))
+                 for k, dt in (("aid", np.int32), ("aid_next", np.int32), ("count", np.uint32)))
+
+
+def concat_files_w_stats(name, dir_stats, files_stats=None, n_items: int | None = None, **kw):
+    """model/count_co_events.py:103-181 with the reference's signature and files: reads
+    {dir_stats}/tmp/{name}.parquet if present (loaded_from_cache, :106-110), else the tables listed
+    in files_stats (:111-112), else every {dir_stats}/{name}/*.parquet in sorted order (:113-114);
+    runs A6 on the device (ottohip_concat_tables) and writes {dir_stats}/{name}.parquet
+    [aid:int32, aid_next:int32, count:int32] in count-desc order (:179). The build needs no
+    out-of-memory retry, so it never writes the tmp cache itself."""
+    import torch
+    file_tmp = f"{dir_stats}/tmp/{name}.parquet"
+    cached = os.path.exists(file_tmp)
+    if cached:
+        paths = [file_tmp]
+    elif files_stats is not None:
+        paths = list(files_stats)
+    else:
+        paths = sorted(glob.glob(f"{dir_stats}/{name}/*.parquet"))
+    tabs = [_read_table(p) for p in paths]
+    if n_items is None:
+        n_items = max([config.N_ITEMS_OTTO] + [int(max(t[0].max(), t[1].max())) + 1 for t in tabs if len(t[0])])
+    if any(len(t[2]) and int(t[2].max()) > 0x7FFFFFFF for t in tabs):
+        raise ValueError("concat_files_w_stats: a per-file count exceeds int32")
+    dev_tabs = [tuple(torch.from_numpy(x.view(np.int32)) for x in t) for t in tabs]
+    a, b, c = concat_tables_w_stats(name, dev_tabs, n_items=n_items, loaded_from_cache=cached, **kw)
+    _write_table(f"{dir_stats}/{name}.parquet", a.cpu().numpy(), b.cpu().numpy(), c.cpu().numpy(), np.int32)
 
 
 def count_co_events_build(dir_sessions, dir_stats, names=None):

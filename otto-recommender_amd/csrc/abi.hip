@@ -700,6 +700,11 @@ extern "C" int ottohip_table_finalize(ottohip_ctx* ctx, const ottohip_table* t, 
   const ottohip_rule_stats& st = t->stats[rule];
   const bool use_ge2 = mp->click_rule && st.file_rows > mp->filter_rows;
   const int64_t n_after = use_ge2 ? st.file_rows_ge2 : st.file_rows;
+  if (use_ge2 && mp->min_count_in_part != 2) {  // count_ge2 is accumulated with the per-file threshold 2
+    set_error("finalize: min_count_in_part=%d, but the table's per-file filter column is count >= 2",
+              (int)mp->min_count_in_part);
+    return OTTOHIP_EINVAL;
+  }
   if (n_after > mp->max_rows_groupby) {
     set_error("rule %d: %lld per-file rows > %lld: the reference's part-wise branch (count_co_events.py:135-166) "
               "is not implemented on the device", rule, (long long)n_after, (long long)mp->max_rows_groupby);

@@ -180,10 +180,18 @@ def count_co_events_sharded(events, file_ids, n_files_total: int, group=None, na
     its file_rows / file_rows_ge2 are the GLOBAL per-file row counts (all-reduced), which is
     what concat_files_w_stats compares against its thresholds (:131, :135)."""
     import torch.distributed as dist
+    import torch
+    from .covis import reference_rules
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    words, wpp, pieces, ppp, names = emit_for_owners(events, world, file_ids, n_files_total, names, n_items, dedup,
-                                                      stream, ctx)
+    if len(events.file_bounds) > 1:
+        words, wpp, pieces, ppp, names = emit_for_owners(events, world, file_ids, n_files_total, names, n_items, dedup,
+                                                          stream, ctx)
+    else:  # no files on this rank (e.g. one part of the part-wise merge): it still joins every exchange
+        names = reference_rules(names)[0]
+        dev = torch.device("cuda", (ctx or _lib.context()).device)
+        words, pieces = torch.empty(0, dtype=torch.int32, device=dev), torch.empty(0, dtype=torch.int64, device=dev)
+        wpp, ppp = [0] * world, [0] * world
     rw = exchange(words, wpp, group)
     del words
     rp = exchange(pieces, ppp, group)
@@ -218,3 +226,184 @@ def merge_tables_by_owner(events, group=None, names=None, n_items: int = config.
     tab = table_from_records(recv, names, n_items, fs, ctx=local.ctx, stream=stream)
     tab.rank, tab.world = rank, world
     return tab
+
+
+# ---------------------------------------------------------------- sharded A6
+_HUGE = 1 << 62
+
+
+def _allreduce_sum(t, group=None):
+    import torch.distributed as dist
+    dev = _comm_device(group)
+    x = t.to(dev) if t.device != dev else t.clone()
+    dist.all_reduce(x, group=group)
+    return x.to(t.device) if x.device != t.device else x
+
+
+def run_hist(x, lo: int, hi: int, shift: int, mask: int, n_bins: int, ctx=None, stream=None):
+    """Device u64 histogram of (x >> shift) & mask over x[lo:hi] (runs of equal keys contiguous)."""
+    import torch
+    ctx = ctx or _lib.context()
+    h = torch.empty(int(n_bins), dtype=torch.int64, device=x.device)
+    _lib.check(_lib.load().ottohip_run_hist(ctx.h, _lib.ptr(x) if x.numel() else None, int(lo), int(hi), int(shift),
+                                            int(mask) & 0xFFFFFFFF, int(n_bins), _lib.ptr(h), _lib.stream_handle(stream)))
+    return h
+
+
+def head_cut(aid, count, max_rows: int, n_items: int, group=None, ctx=None, stream=None) -> int:
+    """Length of this shard's share of the GLOBAL head(max_rows) of the (count desc, aid asc,
+    aid_next asc) order, given the shard's rows already in that order (a finalize output).
+    Exact and collective (every rank calls it): the cut count c* is found by a two-level 16-bit
+    radix select over all-reduced count histograms, ties at c* by an all-reduced histogram over
+    aid (all rows of one aid live on its owner, so the owner of the cut aid keeps the first r
+    of them). A shard's kept rows are always a prefix of its order."""
+    import torch
+    import torch.distributed as dist
+    m = int(count.numel())
+    tot = _allreduce_sum(torch.tensor([m], dtype=torch.int64), group)
+    if int(tot.item()) <= max_rows:
+        return m
+    K = int(max_rows)
+    if K <= 0:
+        return 0
+    # level 1: count >> 16
+    h1 = run_hist(count, 0, m, 16, 0xFFFF, 1 << 16, ctx, stream)
+    g1 = _allreduce_sum(h1, group).cpu().numpy()
+    h1 = h1.cpu().numpy()
+    above = np.concatenate([np.cumsum(g1[::-1])[::-1][1:], [0]])  # global rows with a larger high part
+    hi = int(np.flatnonzero(above + g1 >= K).max())
+    lo1 = int(h1[hi + 1:].sum())
+    # level 2: count & 0xFFFF among rows of that high part
+    h2 = run_hist(count, lo1, lo1 + int(h1[hi]), 0, 0xFFFF, 1 << 16, ctx, stream)
+    g2 = _allreduce_sum(h2, group).cpu().numpy()
+    h2 = h2.cpu().numpy()
+    above2 = int(above[hi]) + np.concatenate([np.cumsum(g2[::-1])[::-1][1:], [0]])
+    lo = int(np.flatnonzero(above2 + g2 >= K).max())
+    need = K - int(above2[lo])  # rows of count c* = hi << 16 | lo still to keep, 1 <= need <= g2[lo]
+    lo_c = lo1 + int(h2[lo + 1:].sum())
+    # ties at c*: aid histogram of the count == c* rows (a contiguous aid-ascending range)
+    h3 = run_hist(aid, lo_c, lo_c + int(h2[lo]), 0, 0xFFFFFFFF, n_items, ctx, stream)
+    g3 = _allreduce_sum(h3, group)
+    cg = torch.cumsum(g3, 0)
+    a_star = int(torch.searchsorted(cg, torch.tensor([need], dtype=cg.dtype, device=cg.device)).item())
+    before = int(cg[a_star].item()) - int(g3[a_star].item())
+    mine = int(h3[:a_star].sum().item())
+    own = int(h3[a_star].item())
+    return lo_c + mine + (need - before if own > 0 else 0)
+
+
+def _records(a, b, c):
+    import torch
+    c = c.to(torch.int32)
+    return torch.stack([a.to(torch.int32), b.to(torch.int32), c, c], 1).contiguous()
+
+
+def all_gather_rows(cols, group=None):
+    """All-gather of variable-length (aid, aid_next, count) device columns, in rank order."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    dev = _comm_device(group)
+    n = torch.tensor([int(cols[0].numel())], dtype=torch.int64, device=dev)
+    ns = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    ns = [int(x.item()) for x in ns]
+    mx = max(max(ns), 1)
+    x = torch.zeros((mx, 3), dtype=torch.int32, device=dev)
+    if ns[dist.get_rank(group)]:
+        x[:ns[dist.get_rank(group)]] = torch.stack(list(cols), 1).to(dev)
+    out = [torch.empty_like(x) for _ in range(world)]
+    dist.all_gather(out, x, group=group)
+    rows = torch.cat([o[:k] for o, k in zip(out, ns)]).to(cols[0].device)
+    return rows[:, 0].contiguous(), rows[:, 1].contiguous(), rows[:, 2].contiguous()
+
+
+def finalize_sharded(table, name, max_rows=None, params: dict | None = None, gather: bool = True,
+                     n_items: int = config.N_ITEMS_OTTO, group=None, stream=None):
+    """A6 step (3) of concat_files_w_stats (model/count_co_events.py:168-175) on an owner-sharded
+    table whose file statistics are the GLOBAL ones (count_co_events_sharded installs them): each
+    rank thresholds and orders its rows, head_cut finds the exact global head(max_rows) share of
+    every rank, and with gather=True the shares are all-gathered and ordered into the global
+    final table, identical on every rank and identical to the single-GPU finalize (the
+    consumers -- R1 per aid, candidate generation per session -- need it whole on every rank).
+    gather=False returns this rank's share only (still in global order)."""
+    ctx = table.ctx
+    mr = config.MAX_CO_EVENT_PAIRS_TO_SAVE_DISK if max_rows is None else int(max_rows)
+    p = dict(params or {})
+    p["max_rows_groupby"] = _HUGE
+    a, b, c = table.finalize(name, max_rows=_HUGE, params=p, stream=stream)
+    k = head_cut(a, c, mr, n_items, group, ctx, stream)
+    a, b, c = a[:k], b[:k], c[:k]
+    if not gather:
+        return a, b, c
+    return _order_rows(all_gather_rows((a, b, c), group), name, n_items, ctx, stream)
+
+
+def _order_rows(cols, name, n_items, ctx, stream=None):
+    """(count desc, aid, aid_next) order of disjoint rows (one device finalize, no threshold)."""
+    t = table_from_records(_records(*cols), [name], n_items, ctx=ctx, stream=stream)
+    out = t.finalize(name, max_rows=_HUGE, params={"click_rule": 0, "min_count": 1, "filter_rows": _HUGE,
+                                                    "max_rows_groupby": _HUGE}, stream=stream)
+    t.free()
+    return out
+
+
+def concat_files_w_stats_sharded(events, file_ids, n_files_total: int, name: str, table=None, group=None,
+                                 n_items: int = config.N_ITEMS_OTTO,
+                                 max_rows_groupby: int = config.MAX_ROWS_POLARS_GROUPBY,
+                                 optim_rows: int = config.OPTIM_ROWS_POLARS_GROUPBY,
+                                 max_pairs: int = config.MAX_CO_EVENT_PAIRS_TO_SAVE_DISK,
+                                 click_filter_rows: int = config.CLICK_FILTER_ROWS, gather: bool = True,
+                                 stream=None, ctx=None):
+    """concat_files_w_stats (model/count_co_events.py:103-181) for one rule over files dealt to
+    ranks: the N-GPU form of covis.concat_files_w_stats_fused, same results on every rank.
+    (1) per-file count >= 2 when the GLOBAL N > click_filter_rows; (2) when still > max_rows_groupby,
+    ceil(N / optim_rows) parts of whole global files (file p * nf // n_parts starts part p, as in
+    the fused path), each counted sharded (every rank counts its files of the part), thresholded
+    at MIN_COUNT_IN_PART and cut to its GLOBAL head(int(max_rows_groupby / N * optim_rows)); the
+    owner-local part outputs are merge-summed locally (ownership is by aid, so no exchange); (3)
+    MIN_COUNT_TO_SAVE and the global head(max_pairs) (finalize_sharded)."""
+    import math
+    import torch
+    ctx = ctx or _lib.context()
+    file_ids = [int(f) for f in file_ids]
+    own = table is None
+    tab = table if table is not None else count_co_events_sharded(events, file_ids, n_files_total, group, [name],
+                                                                  n_items, stream=stream, ctx=ctx)
+    st = tab.stats(name)
+    use_ge2 = "click_to" in name and st["file_rows"] > click_filter_rows
+    N = st["file_rows_ge2"] if use_ge2 else st["file_rows"]
+    base = {"filter_rows": click_filter_rows}
+    if N <= max_rows_groupby:
+        out = finalize_sharded(tab, name, max_pairs, base, gather, n_items, group, stream)
+        if own:
+            tab.free()
+        return out
+    if own:
+        tab.free()
+    n_parts = math.ceil(N / optim_rows)
+    max_rows_part = int(max_rows_groupby / N * optim_rows)
+    bounds = [(p * n_files_total) // n_parts for p in range(n_parts + 1)]
+    part = {"click_rule": 1 if use_ge2 else 0, "filter_rows": -1,
+            "min_count": config.MIN_COUNT_IN_PART.get(name, 1)}
+    fid = np.asarray(file_ids, np.int64)
+    if np.any(np.diff(fid) <= 0):
+        raise ValueError("file_ids must be increasing (the rank's files in events order)")
+    pieces = []
+    for f0, f1 in zip(bounds[:-1], bounds[1:]):
+        if f1 <= f0:
+            continue
+        l0, l1 = int(np.searchsorted(fid, f0)), int(np.searchsorted(fid, f1))
+        t = count_co_events_sharded(events.subset_files(l0, l1), file_ids[l0:l1], n_files_total, group, [name],
+                                    n_items, stream=stream, ctx=ctx)
+        pieces.append(finalize_sharded(t, name, max_rows_part, part, False, n_items, group, stream))
+        t.free()
+    dev = torch.device("cuda", ctx.device)
+    cat = [torch.cat([p[i] for p in pieces]) if pieces else torch.zeros(0, dtype=torch.int32, device=dev)
+           for i in range(3)]
+    merged = table_from_records(_records(*cat), [name], n_items, ctx=ctx, stream=stream)
+    out = finalize_sharded(merged, name, max_pairs, {"click_rule": 0, "filter_rows": _HUGE,
+                                                     "min_count": config.MIN_COUNT_TO_SAVE.get(name, 1)},
+                           gather, n_items, group, stream)
+    merged.free()
+    return out

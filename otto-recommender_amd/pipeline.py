@@ -1,6 +1,6 @@
 """Config-5 end-to-end candidate generation (BASELINE.json configs[4]) on the device:
 
-  co-visitation over train + test (count_co_events_fused)  -> finalize (A6) -> R1 top-N lists
+  co-visitation per folder (count_co_events_fused) -> A6 per folder -> A7 train+test merge -> R1
   Word2Vec kNN of both models (first 600k vocabulary rows)   -> B3 lists
   session embeddings (C1) -> KMeans k=50 (C2) -> popularity ranks cl50 / cl1 (C3)
   candidates for the test sessions (R3-R6) -> recall@20 (R9)
@@ -36,12 +36,13 @@ def _concat(parts):
 
 def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int = config.N_ITEMS_OTTO,
         n_clusters: int = 50, kmeans_iter: int = 100, knn_queries: int = config.W2VEC_SEARCH_SIMILAR_FOR_FIRST_N_AIDS,
-        ctx=None, timings: dict | None = None) -> dict:
+        ctx=None, timings: dict | None = None, keep_tables: bool = False) -> dict:
     import torch
     from .synth import file_session_bounds
     ctx = ctx or _lib.context()
     dev = torch.device("cuda", ctx.device)
     T = timings if timings is not None else {}
+    tables = {}
 
     def mark(name, t0):
         torch.cuda.synchronize()
@@ -49,23 +50,35 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
         return time.perf_counter()
 
     t = time.perf_counter()
-    # ---- co-visitation over train + test files (model/count_co_events.py:201-226)
+    # ---- co-visitation (model/count_co_events.py:201-226): count each folder (:204-205), A6 per
+    # folder with its own file statistics (:212-216), then A6 on [train, test] (A7, :218-226)
     allev = _concat([train, test])
-    fb = np.concatenate([file_session_bounds(train.n_sessions),
-                         file_session_bounds(test.n_sessions)[1:] + train.n_sessions])
+    fb_tr = file_session_bounds(train.n_sessions)
+    fb = np.concatenate([fb_tr, file_session_bounds(test.n_sessions)[1:] + train.n_sessions])
+    n_tr_files = len(fb_tr) - 1
     dev_all = gc.DeviceEvents.from_host(allev, fb)
     t = mark("upload", t)
-    tab = gc.count_co_events_fused(dev_all, n_items=n_items, ctx=ctx)
-    pairs = sum(tab.stats(n)["n_pairs"] for n in tab.names)
-    t = mark("covis_count", t)
+    folders = [dev_all.subset_files(0, n_tr_files), dev_all.subset_files(n_tr_files, len(fb) - 1)]
+    merged = {n: [] for n in config.CO_EVENTS_TO_COUNT}
+    pairs = 0
+    for folder in folders:
+        tab = gc.count_co_events_fused(folder, n_items=n_items, ctx=ctx)
+        pairs += sum(tab.stats(n)["n_pairs"] for n in tab.names)
+        t = mark("covis_count", t)
+        for n in tab.names:
+            merged[n].append(gc.concat_files_w_stats_fused(folder, n, table=tab, n_items=n_items, ctx=ctx))
+            t = mark(f"merge_{n}", t)
+        tab.free()
     r1 = {}
-    for n in tab.names:
-        a, b, c = gc.concat_files_w_stats_fused(dev_all, n, table=tab, n_items=n_items, ctx=ctx)
-        t = mark(f"merge_{n}", t)
+    for n in config.CO_EVENTS_TO_COUNT:
+        a, b, c = gc.merge_train_test(n, merged[n][0], merged[n][1], n_items=n_items, ctx=ctx)
+        merged[n] = None
+        t = mark("merge_train_test", t)
         r = gr.topk_per_aid(a, b, c, config.RETRIEVAL_FIRST_N_CO_COUNTS[n], n_items=n_items, ctx=ctx)
         r1[n] = (r["aid"], r["aid_next"], r["rank"])
+        if keep_tables:
+            tables[n] = (a, b, c)
         t = mark("R1", t)
-    tab.free()
     # ---- kNN of both Word2Vec models (model/retrieve.py:683-687)
     knn = []
     for words, emb in ((words_all, emb_all), (words_12, emb_12)):
@@ -107,5 +120,13 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
     t = mark("recall", t)
     out = {"pairs": int(pairs), "candidates": cands.n_cand, "test_sessions": int(test.n_sessions),
            "kmeans_iter": km.n_iter_, "recall": rec, "timings_s": T}
+    if keep_tables:  # host copies of every stage's output, for the parity tests
+        h = lambda x: x.cpu().numpy()
+        out["intermediates"] = {
+            "tables": {n: tuple(h(x) for x in v) for n, v in tables.items()},
+            "r1": {n: tuple(h(x) for x in v) for n, v in r1.items()},
+            "knn": [tuple(h(x) for x in v) for v in knn],
+            "cluster_labels": h(labels_all), "pop": p[["cl50", "aid"]].reset_index(drop=True),
+            "candidates": cands.to_pandas(sess)}
     cands.free()
     return out

@@ -27,3 +27,62 @@ def test_pipeline_small(gpu):
     assert res["recall"]["total"]["topall"] > 0.1  # self + co-visit candidates recover revisits
     for stage in ("covis_count", "R1", "knn", "C1_embeddings", "C2_kmeans", "C3_popularity", "candidates", "recall"):
         assert stage in T, stage
+
+
+def test_pipeline_recall_parity(gpu):
+    """Config 5 (BASELINE configs[4]) at test scale, stage by stage against the oracle on the same
+    inputs: A7 tables (oracle.merge_train_test: A6 per folder, then A6 on [train, test]), R1
+    (model/retrieve.py:18-63), C3 given the device clustering, candidates (R3-R6, R8) from the
+    same R1 / kNN / pop lists, and recall@20/100/200/all per type (model/eval_retrieved.py:45-118)
+    -- all exact. kNN sets are checked against the exact oracle in tests/test_knn.py."""
+    import pandas as pd
+    import covis as oracle
+    import retrieve as oracle_retrieve
+    import popularity as oracle_pop
+    import otto_recommender_amd.synth as synth
+    from otto_recommender_amd import pipeline, config
+    ev = synth.generate(24_000, first_session=31)
+    train, test, labels = synth.split_test_labels(ev)
+    words = synth.item_words()
+    emb = synth.embeddings(len(words), seed=1)
+    emb2 = synth.embeddings(len(words), seed=3)
+    res = pipeline.run(train, test, labels, words, emb, words, emb2, n_clusters=6, kmeans_iter=15,
+                       knn_queries=30_000, keep_tables=True)
+    im = res["intermediates"]
+    per_tr = oracle.count_co_events_file(train.session_offsets, train.aid, train.ts, train.type)
+    per_te = oracle.count_co_events_file(test.session_offsets, test.aid, test.ts, test.type)
+    r1 = {}
+    for n in config.CO_EVENTS_TO_COUNT:
+        ref = oracle.merge_train_test(n, [per_tr[n]], [per_te[n]])
+        for x, y in zip(im["tables"][n], ref):
+            np.testing.assert_array_equal(x, y, err_msg=f"A7 {n}")
+        t = oracle_retrieve.get_df_count_for_co_event_type(*ref, config.RETRIEVAL_FIRST_N_CO_COUNTS[n])
+        for x, k in zip(im["r1"][n], ("aid", "aid_next", "rank")):
+            np.testing.assert_array_equal(x, t[k], err_msg=f"R1 {n} {k}")
+        r1[n] = pd.DataFrame({"aid": t["aid"], "aid_next": t["aid_next"], f"{n}_rank": t["rank"]})
+    assert sum(len(im["tables"][n][0]) for n in r1) > 0
+    # C3 on the device clustering of all (train + test) sessions
+    allv = pipeline._concat([train, test])
+    sess_all = allv.session[allv.session_offsets[:-1]]
+    cl = im["cluster_labels"]
+    pop_ref = oracle_pop.popularity_ranks(allv.session, allv.aid, allv.ts, allv.type,
+                                          dict(zip(sess_all.tolist(), cl.tolist())))
+    rk = [c for c in pop_ref.columns if c.startswith("rank_")]
+    pop_ref = pop_ref[pop_ref[rk].min(axis=1) <= 20].sort_values(["cl50", "aid"])
+    got_pop = im["pop"].sort_values(["cl50", "aid"])
+    np.testing.assert_array_equal(got_pop["cl50"].to_numpy(), pop_ref["cl50"].to_numpy())
+    np.testing.assert_array_equal(got_pop["aid"].to_numpy(), pop_ref["aid"].to_numpy())
+    # candidates of the test sessions from the same sources
+    knn = [pd.DataFrame({"aid": a, "aid_next": b, "rank": r}) for a, b, r in im["knn"]]
+    sess_te = test.session[test.session_offsets[:-1] - test.session_offsets[0]]
+    scl = pd.DataFrame({"session": sess_te, "cl50": cl[train.n_sessions:]})
+    ref_c = oracle_retrieve.candidates(test.to_pandas(), r1, knn[0], knn[1], scl, im["pop"])
+    got_c = im["candidates"]
+    assert len(got_c) == len(ref_c) == res["candidates"]
+    for c in ["session", "aid_next", "ts_order_aid"] + [c for c in ref_c.columns if c.startswith("src_")]:
+        np.testing.assert_array_equal(got_c[c].to_numpy().astype(np.int64), ref_c[c].to_numpy().astype(np.int64),
+                                      err_msg=c)
+    rec = oracle_retrieve.recall(ref_c, labels)
+    for t in ("clicks", "carts", "orders", "total"):
+        for k in ("top20", "top100", "top200", "topall"):
+            assert abs(res["recall"][t][k] - rec[t][k]) < 1e-12, (t, k)
