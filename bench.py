@@ -36,22 +36,24 @@ def pmc_traffic(key: str):
         return None
 
 
-def cpu_baseline(ev_sessions: int, n_files: int, seed: int = 0) -> dict:
-    """The CPU restatement (oracle/covis_oracle.c, single thread) timed on a bounded sample:
-    the first n_files 100k-session files of the same synthetic stream."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import covis as oracle  # checker / baseline only
-    import otto_recommender_amd.synth as synth
-    n = min(ev_sessions, n_files * synth.SESSIONS_PER_FILE)
-    ev = synth.generate(n, 0, seed)
-    fb = synth.file_session_bounds(n)
-    t0 = time.perf_counter()
-    per_file = oracle.count_co_events_files(ev.session_offsets, ev.aid, ev.ts, ev.type, fb)
-    dt = time.perf_counter() - t0
-    pairs = sum(int(p[k][2].sum()) for p in per_file for k in p)
-    return {"value": pairs / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
-            "sample": f"first {len(fb) - 1} files ({n} sessions, {ev.n_events} events, {pairs} pairs) "
-                      f"of the same stream, oracle/covis_oracle.c per-file count, {dt:.1f} s"}
+def cpu_baseline(seed: int = 0, pandas_files: int = 10) -> dict:
+    """The CPU path timed on this host's cores in a child process (oracle/cpu_baseline.py, which
+    never touches the GPU): the C restatement over whole files of the same stream on every usable
+    core (OpenMP, the strong CPU baseline: `value`), and the pandas op-for-op restatement of the
+    reference's dataframe pipeline as a process pool over `pandas_files` files
+    (`reference_algorithm`). BASELINE.md §2."""
+    import subprocess
+    cfg = json.dumps({"seed": seed, "pandas_files": pandas_files})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline.py"), cfg], capture_output=True,
+                       text=True, timeout=900)
+    if r.returncode != 0:
+        return {"error": r.stderr[-2000:]}
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    out = dict(res["port"])
+    out["host_cpus"] = res["host"]
+    if "pandas" in res:
+        out["reference_algorithm"] = res["pandas"]
+    return out
 
 
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16, /opt/skills/guides/MI355X_MICROARCH.md
@@ -98,13 +100,16 @@ def bench_knn(steps: int, warmup: int, n_items: int, n_q: int, with_cpu: bool) -
     if with_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import knn as oracle_knn  # checker / baseline only
+        from cpu_baseline import host_cores
+        hc = host_cores()
+        torch.set_num_threads(hc["usable"])
         nq_cpu = 2000
         t0 = time.perf_counter()
         ri, _ = oracle_knn.topk_exact(emb, np.arange(nq_cpu), 20)
         tc = time.perf_counter() - t0
         gi = idx[:nq_cpu].cpu().numpy()
         out["sample_exact_match"] = float(np.mean([set(a) == set(b) for a, b in zip(gi, ri)]))
-        out["cpu_baseline"] = {"value": nq_cpu / tc, "unit": "queries/s", "cores": torch.get_num_threads(),
+        out["cpu_baseline"] = {"value": nq_cpu / tc, "unit": "queries/s", "cores": torch.get_num_threads(), "host_cpus": hc,
                                "kind": "port",
                                "sample": f"{nq_cpu} queries, exact brute force (oracle/knn.py: torch-CPU fp32 "
                                          f"preselect + fp64 rerank), {tc:.1f} s"}
@@ -154,7 +159,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--events", type=int, default=220_000_000)
-    ap.add_argument("--cpu-files", type=int, default=5)
+    ap.add_argument("--pandas-files", type=int, default=10, help="files of the pandas reference-algorithm baseline")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--knn-steps", type=int, default=2, help="0 disables the configs[2] kNN measurement")
@@ -316,12 +321,14 @@ def main():
         "gen_s": round(gen_s, 1),
     }
     if not args.no_cpu and world == 1:
-        out["cpu_baseline"] = cpu_baseline(n_sess, args.cpu_files, args.seed)
+        out["cpu_baseline"] = cpu_baseline(args.seed, args.pandas_files)
     if args.knn_steps > 0 and world == 1:
         del dev
+        ctx.trim()  # each sub-benchmark starts from an empty workspace (its own buffers only)
         torch.cuda.empty_cache()
         out["knn"] = bench_knn(args.knn_steps, 1, args.knn_items, args.knn_queries, not args.no_cpu)
     if args.cand_steps > 0 and world == 1:
+        ctx.trim()
         torch.cuda.empty_cache()
         out["candidates"] = bench_candidates(args.cand_sessions, args.cand_steps, args.kmeans_iter)
     print(json.dumps(out))

@@ -75,6 +75,9 @@ typedef struct {
 int ottohip_ctx_create(int device, ottohip_ctx** out);
 void ottohip_ctx_destroy(ottohip_ctx* ctx);
 const char* ottohip_last_error(void);
+/* release the context's workspace and spare table buffers (device memory back to the runtime);
+ * the next call re-allocates what it needs. Live tables are not affected. */
+int ottohip_ctx_trim(ottohip_ctx* ctx);
 /* phase timing (HIP events on the call's stream): enable, then read after a call */
 int ottohip_ctx_set_timing(ottohip_ctx* ctx, int enable);
 int ottohip_ctx_timing(ottohip_ctx* ctx, int idx, const char** name, float* ms, double* bytes);

@@ -174,3 +174,39 @@ int oracle_pair_stats(int64_t n_sessions, const int64_t* offsets, int64_t* join_
   *join_rows = acc;
   return 0;
 }
+
+/* CPU baseline (bench.py cpu_baseline leg): the per-file stage of count_co_events_all_files
+ * (model/count_co_events.py:80-100) over n_files consecutive session ranges, files in parallel
+ * over n_threads OpenMP threads (one file per thread at a time, dynamic schedule). Each file is
+ * counted exactly like oracle_count_co_events and its tables are built, then released;
+ * totals[r * 2 + 0] = sum of per-file rows, totals[r * 2 + 1] = qualifying pairs of rule r. */
+int oracle_count_files_omp(int64_t n_files, const int64_t* file_session_bounds, const int64_t* offsets,
+                           const int32_t* aid, const int32_t* ts, const int8_t* type, int n_rules,
+                           const int32_t* this_type, const uint32_t* next_mask, const int32_t* max_abs_dt,
+                           int32_t min_dt, int32_t max_dt, int n_threads, int64_t* totals) {
+  if (n_rules < 1 || n_rules > 16) return -1;
+  memset(totals, 0, (size_t)n_rules * 2 * sizeof(int64_t));
+  int rc = 0;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads)
+  for (int64_t f = 0; f < n_files; ++f) {
+    const int64_t s0 = file_session_bounds[f], s1 = file_session_bounds[f + 1];
+    const int64_t e0 = offsets[s0] - offsets[0];
+    oracle_table t[16];
+    int r0 = oracle_count_co_events(s1 - s0, offsets + s0, aid + e0, ts + e0, type + e0, n_rules, this_type,
+                                    next_mask, max_abs_dt, min_dt, max_dt, t);
+    for (int r = 0; r < n_rules; ++r) {
+      int64_t pairs = 0;
+      for (int64_t i = 0; r0 == 0 && i < t[r].n; ++i) pairs += t[r].count[i];
+#pragma omp atomic
+      totals[r * 2] += t[r].n;
+#pragma omp atomic
+      totals[r * 2 + 1] += pairs;
+      oracle_free_table(&t[r]);
+    }
+    if (r0) {
+#pragma omp critical
+      rc = r0;
+    }
+  }
+  return rc;
+}

@@ -53,6 +53,7 @@ SIGNATURES = {
     "ottohip_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_VP)]),
     "ottohip_ctx_destroy": (None, [_VP]),
     "ottohip_last_error": (ctypes.c_char_p, []),
+    "ottohip_ctx_trim": (ctypes.c_int, [_VP]),
     "ottohip_ctx_set_timing": (ctypes.c_int, [_VP, ctypes.c_int]),
     "ottohip_ctx_timing": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                           ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_double)]),
@@ -166,6 +167,10 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def trim(self):
+        """Return the workspace and spare table buffers to the device (ottohip_ctx_trim)."""
+        check(load().ottohip_ctx_trim(self.h))
 
     def set_timing(self, on: bool):
         check(load().ottohip_ctx_set_timing(self.h, 1 if on else 0))

@@ -415,6 +415,15 @@ void ottohip_ctx_destroy(ottohip_ctx* ctx) {
   delete ctx;
 }
 
+int ottohip_ctx_trim(ottohip_ctx* ctx) {
+  if (!ctx) return OTTOHIP_EINVAL;
+  OH_HIP(hipSetDevice(ctx->device));
+  OH_HIP(hipDeviceSynchronize());
+  ctx->ws.release();
+  ctx->spare.release();
+  return 0;
+}
+
 int ottohip_ctx_set_timing(ottohip_ctx* ctx, int enable) {
   if (!ctx) return OTTOHIP_EINVAL;
   ctx->timing = enable != 0;
