@@ -117,9 +117,11 @@ def bench_knn(steps: int, warmup: int, n_items: int, n_q: int, with_cpu: bool) -
     return out
 
 
-def bench_candidates(n_sessions: int, steps: int, kmeans_iter: int) -> dict:
+def bench_candidates(n_sessions: int, steps: int, kmeans_iter: int, group=None) -> dict:
     """BASELINE configs[4]: end-to-end candidate generation (co-visit + W2V kNN + pop-cluster) for
-    the test split of n_sessions synthetic sessions, 1 GPU; value = candidate rows / s."""
+    the test split of n_sessions synthetic sessions; value = candidate rows / s of the whole job.
+    group: the sharded pipeline over every rank (files, kNN queries, KMeans rows, C3 counters and
+    test sessions split; pipeline.run(group=...)), timed as the max over ranks."""
     import torch
     import otto_recommender_amd.synth as synth
     from otto_recommender_amd import pipeline, config as cfg
@@ -134,9 +136,18 @@ def bench_candidates(n_sessions: int, steps: int, kmeans_iter: int) -> dict:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         T = {}
-        res = pipeline.run(train, test, labels, words, emb_all, words, emb_12, kmeans_iter=kmeans_iter, timings=T)
+        res = pipeline.run(train, test, labels, words, emb_all, words, emb_12, kmeans_iter=kmeans_iter, timings=T,
+                           group=group)
         torch.cuda.synchronize()
         dts.append(time.perf_counter() - t0)
+    world = 1
+    if group is not None:  # slowest rank
+        import torch.distributed as dist
+        world = dist.get_world_size(group)
+        cdev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+        m = torch.tensor(dts, dtype=torch.float64, device=cdev)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group)
+        dts = m.tolist()
     # inputs resident in HBM: the host->device upload of the event table and the host conversion
     # of the label frame to CSR are input preparation, reported but not in the timed step
     prep = res["timings_s"].get("upload", 0.0) + res["timings_s"].get("labels_csr", 0.0)
@@ -144,7 +155,8 @@ def bench_candidates(n_sessions: int, steps: int, kmeans_iter: int) -> dict:
     return {"metric": "candidates/sec, end-to-end candidate generation (co-visit + W2V kNN + pop-cluster)",
             "value": res["candidates"] / dt, "unit": "candidates/s", "ms_per_step": dt * 1e3,
             "input_prep_s": round(prep, 4),
-            "config": {"workload": "configs[4] on 1 GPU: train + truncated test split of synthetic sessions",
+            "n_gpus": world,
+            "config": {"workload": f"configs[4] on {world} GPU(s): train + truncated test split of synthetic sessions",
                        "sessions": n_sessions, "test_sessions": res["test_sessions"], "candidates": res["candidates"],
                        "co_visit_pairs": res["pairs"], "kmeans_iter": res["kmeans_iter"]},
             "recall@20": {k: round(v["top20"], 6) for k, v in res["recall"].items()},
@@ -271,7 +283,15 @@ def main():
         t_step = float(t_max.item()); pairs, rows, n_events = (float(x) for x in tot.tolist())
     else:
         n_events = ev.n_events
-    if rank != 0:
+    if rank != 0:  # the other ranks join the sharded config-5 run, then leave
+        if args.cand_steps > 0:
+            del dev, tab
+            ctx.trim()
+            torch.cuda.empty_cache()
+            try:
+                bench_candidates(args.cand_sessions, args.cand_steps, args.kmeans_iter, dist.group.WORLD)
+            except Exception:  # noqa: BLE001  (rank 0 reports the error)
+                pass
         dist.destroy_process_group()
         return
     # byte model of SURVEY.md §8(d): B = 9E + 8(S+1) + 16P + 12U
@@ -327,10 +347,18 @@ def main():
         ctx.trim()  # each sub-benchmark starts from an empty workspace (its own buffers only)
         torch.cuda.empty_cache()
         out["knn"] = bench_knn(args.knn_steps, 1, args.knn_items, args.knn_queries, not args.no_cpu)
-    if args.cand_steps > 0 and world == 1:
+    if args.cand_steps > 0:
+        if world > 1:
+            del dev
         ctx.trim()
         torch.cuda.empty_cache()
-        out["candidates"] = bench_candidates(args.cand_sessions, args.cand_steps, args.kmeans_iter)
+        try:  # the sub-object must not cost the main line
+            cand = bench_candidates(args.cand_sessions, args.cand_steps, args.kmeans_iter,
+                                    dist.group.WORLD if world > 1 else None)
+        except Exception as e:  # noqa: BLE001
+            cand = {"error": f"{type(e).__name__}: {e}"[:2000]}
+        if rank == 0:
+            out["candidates"] = cand
     print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

@@ -212,6 +212,35 @@ int ottohip_kmeans_step(ottohip_ctx* ctx, const float* X, int64_t n, int dim, fl
                         int32_t* labels, double* shift2, double* inertia, void* stream);
 int ottohip_kmeans_assign(ottohip_ctx* ctx, const float* X, int64_t n, int dim, const float* centroids, int k,
                           int32_t* labels, double* inertia, void* stream);
+/* The Lloyd iteration in parts, for sklearn's _kmeans_single_lloyd (KMeans(init='random',
+ * n_init='auto'), model/kmeans_sessions.py:152-159) and for row-sharded KMeans (SURVEY.md §8(e):
+ * the host all-reduces sums / counts between partial and update):
+ *   partial   E-step on this rank's rows: labels (in: previous, out: nearest centroid, ties to the
+ *             lowest index), sums (device k*dim, 2^-24 fixed point) and counts (device k) of the rows
+ *             per label (overwritten), *inertia, *n_changed = rows whose label changed;
+ *   update    centroids = sums / counts for clusters with counts > 0, *shift2 = squared shift;
+ *   farthest  the m rows farthest from their labelled centroid (rows / d2 HOST, distance desc);
+ *   relocate  _relocate_empty_clusters_dense on the sums: vector j (vecs, device m*dim) leaves cluster
+ *             old_new[2j] and becomes the only member of the empty cluster old_new[2j+1] (HOST);
+ *   inertia   sum of |x - centroid[label]|^2 for the given labels. */
+int ottohip_kmeans_partial(ottohip_ctx* ctx, const float* X, int64_t n, int dim, const float* centroids, int k,
+                           int32_t* labels, int64_t* sums, int64_t* counts, double* inertia, int64_t* n_changed,
+                           void* stream);
+int ottohip_kmeans_update(ottohip_ctx* ctx, float* centroids, const int64_t* sums, const int64_t* counts, int k,
+                          int dim, double* shift2, void* stream);
+int ottohip_kmeans_farthest(ottohip_ctx* ctx, const float* X, int64_t n, int dim, const float* centroids,
+                            const int32_t* labels, int m, int64_t* rows, float* d2, void* stream);
+int ottohip_kmeans_relocate(ottohip_ctx* ctx, int64_t* sums, int64_t* counts, int k, int dim, const float* vecs,
+                            const int32_t* old_new, int m, void* stream);
+int ottohip_kmeans_inertia(ottohip_ctx* ctx, const float* X, int64_t n, int dim, const float* centroids,
+                           const int32_t* labels, double* inertia, void* stream);
+/* column statistics and centering for KMeans.fit (sklearn subtracts the column mean before the
+ * runs and scales tol by the mean column variance): sum_x[d] = sum x, sum_sq[d] = sum (x - center[d])^2
+ * (center NULL = 0), both device int64 in 2^-24 fixed point (exact: shards all-reduce them); dim <= 128 */
+int ottohip_col_sums(ottohip_ctx* ctx, const float* X, int64_t n, int dim, const float* center, int64_t* sum_x,
+                     int64_t* sum_sq, void* stream);
+int ottohip_center_rows(ottohip_ctx* ctx, const float* X, int64_t n, int dim, const float* mean, float* out,
+                        void* stream);
 /* C3 count_popularity (model/count_popularity.py:53-85) for one clustering: per (cluster, aid)
  * n_{clicks,carts,orders} and *_7d (ts > ts_7d), ordinal rank desc within the cluster (ties: aid
  * asc) clipped to 999, rows with min rank <= keep_top_k. session_cl: dense cluster per session. */
@@ -220,6 +249,15 @@ int ottohip_popularity_ranks(ottohip_ctx* ctx, const int64_t* session_offsets, i
                              const int32_t* aid, const int32_t* ts, const int8_t* type, const int32_t* session_cl,
                              int32_t n_items, int32_t n_clusters, int32_t ts_7d, int keep_top_k,
                              ottohip_pop** out, int64_t* n_out, void* stream);
+/* C3 in two parts, for sessions sharded over ranks: pop_counts ADDS this rank's
+ * per (cluster, aid) counters into counts (device u32 [6][n_clusters * n_items]: clicks, carts, orders,
+ * then the *_7d ones); the host all-reduces them; popularity_from_counts ranks them exactly as
+ * ottohip_popularity_ranks does (which is pop_counts on zeroed counters + popularity_from_counts). */
+int ottohip_pop_counts(ottohip_ctx* ctx, const int64_t* session_offsets, int64_t n_sessions, const int32_t* aid,
+                       const int32_t* ts, const int8_t* type, const int32_t* session_cl, int32_t n_items,
+                       int32_t n_clusters, int32_t ts_7d, uint32_t* counts, void* stream);
+int ottohip_popularity_from_counts(ottohip_ctx* ctx, const uint32_t* counts, int32_t n_items, int32_t n_clusters,
+                                   int keep_top_k, ottohip_pop** out, int64_t* n_out, void* stream);
 /* rows sorted by (cluster, aid); ranks6 [n x 6]: clicks, carts, orders, clicks_7d, carts_7d, orders_7d */
 int ottohip_pop_copy(const ottohip_pop* p, int32_t* aid, int32_t* cluster, int16_t* ranks6, void* stream);
 void ottohip_pop_free(ottohip_pop* p);

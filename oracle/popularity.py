@@ -2,8 +2,10 @@
 
 C1 compute_sessions_embeddings (model/kmeans_sessions.py:40-86) in f64 (the reference sums f32 in
    an unspecified polars order; tests use a stated tolerance);
-C2 Lloyd KMeans with the sklearn 'random' init (RandomState(seed).permutation(n)[:k]) and tol
-   scaled by the mean feature variance (model/kmeans_sessions.py:153-161);
+C2 KMeans of the reference's scikit-learn==1.2 branch (model/kmeans_sessions.py:152-159): sklearn
+   1.2's KMeans.fit / _kmeans_single_lloyd restated in f64 (n_init runs from successive
+   RandomState.permutation seeds, centring, relocation of empty clusters, strict convergence); each
+   run is pinned against the installed scikit-learn (tests/test_oracle.py) given the same seeds;
 C3 count_popularity (model/count_popularity.py:53-85), ordinal ranks with aid-ascending ties;
 R7 session-item similarity (model/retrieve.py:604-625).
 Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
@@ -33,26 +35,68 @@ def sessions_embeddings(offsets, aid, ts, type_, words, emb):
     return out
 
 
-def kmeans(X, k, max_iter=100, tol=1e-3, seed=42):
-    X = np.asarray(X, np.float64)
-    n = len(X)
-    C = X[np.random.RandomState(seed).permutation(n)[:k]].copy()
-    tol_abs = X.var(axis=0).mean() * tol
+def _lloyd(Xc, C, max_iter, tol_abs):
+    """sklearn 1.2 _kmeans_single_lloyd (sklearn/cluster/_kmeans.py) in f64 on centred rows:
+    E-step argmin (ties: lowest index), sums per label, empty clusters relocated to the rows
+    farthest from their centroid (_relocate_empty_clusters_dense; among equal distances the
+    lower row first), M-step; stop on unchanged labels (strict) or squared shift <= tol."""
+    n, k = len(Xc), len(C)
+    labels = np.full(n, -1, np.int64)
+    strict = False
     it = 0
+    xn = (Xc ** 2).sum(1)
     for it in range(1, max_iter + 1):
-        d = (X ** 2).sum(1)[:, None] - 2 * X @ C.T + (C ** 2).sum(1)[None, :]
-        lab = d.argmin(1)
+        new = (xn[:, None] - 2 * Xc @ C.T + (C ** 2).sum(1)[None, :]).argmin(1)
+        counts = np.bincount(new, minlength=k).astype(np.int64)
+        sums = np.zeros_like(C)
+        np.add.at(sums, new, Xc)
+        empty = np.flatnonzero(counts == 0)
+        if len(empty):
+            dist = ((Xc - C[new]) ** 2).sum(1)
+            far = np.lexsort((np.arange(n), -dist))[:len(empty)]
+            for e, f in zip(empty, far):
+                sums[new[f]] -= Xc[f]
+                counts[new[f]] -= 1
+                sums[e] = Xc[f]
+                counts[e] = 1
         Cn = C.copy()
-        for c in range(k):
-            m = lab == c
-            if m.any():
-                Cn[c] = X[m].mean(0)
+        nz = counts > 0
+        Cn[nz] = sums[nz] / counts[nz, None]
         shift = ((Cn - C) ** 2).sum()
         C = Cn
+        if np.array_equal(new, labels):
+            strict = True
+            break
+        labels = new
         if shift <= tol_abs:
             break
-    d = (X ** 2).sum(1)[:, None] - 2 * X @ C.T + (C ** 2).sum(1)[None, :]
-    return d.argmin(1), C, it
+    if not strict:
+        labels = (xn[:, None] - 2 * Xc @ C.T + (C ** 2).sum(1)[None, :]).argmin(1)
+    inertia = float(((Xc - C[labels]) ** 2).sum())
+    return labels, C, inertia, it
+
+
+def kmeans_seeds(n, k, n_init, seed):
+    """sklearn 1.2 _init_centroids(init='random'): successive RandomState(seed).permutation(n)[:k]."""
+    rs = np.random.RandomState(seed)
+    return [rs.permutation(n)[:k] for _ in range(n_init)]
+
+
+def kmeans(X, k, max_iter=100, tol=1e-3, seed=42, n_init=10):
+    """KMeans(init='random', n_init=n_init, max_iter, tol, random_state=seed).fit(X) of
+    scikit-learn==1.2 (the reference's branch model/kmeans_sessions.py:152-159) restated in f64:
+    tol scaled by the mean column variance, rows centred on the column means, the lowest-inertia
+    run kept. Returns (labels, centers, n_iter, inertia)."""
+    X = np.asarray(X, np.float64)
+    tol_abs = float(np.mean(np.var(X, axis=0))) * tol
+    mean = X.mean(0)
+    Xc = X - mean
+    best = None
+    for seeds in kmeans_seeds(len(X), k, n_init, seed):
+        lab, C, inertia, it = _lloyd(Xc, Xc[seeds].copy(), max_iter, tol_abs)
+        if best is None or inertia < best[0]:
+            best = (inertia, lab, C + mean, it)
+    return best[1], best[2], best[3], best[0]
 
 
 def popularity_ranks(session, aid, ts, type_, session_cl: dict, keep_top_k=20, suffix="cl50"):

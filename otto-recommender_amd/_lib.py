@@ -82,8 +82,21 @@ SIGNATURES = {
                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), _VP]),
     "ottohip_kmeans_assign": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP, ctypes.c_int, _VP,
                                              ctypes.POINTER(ctypes.c_double), _VP]),
+    "ottohip_kmeans_partial": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP, ctypes.c_int, _VP, _VP, _VP,
+                                              ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64), _VP]),
+    "ottohip_kmeans_update": (ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_int, ctypes.c_int,
+                                             ctypes.POINTER(ctypes.c_double), _VP]),
+    "ottohip_kmeans_farthest": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP, _VP, ctypes.c_int, _VP, _VP, _VP]),
+    "ottohip_kmeans_relocate": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int, ctypes.c_int, _VP, _VP, ctypes.c_int, _VP]),
+    "ottohip_kmeans_inertia": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP, _VP, ctypes.POINTER(ctypes.c_double),
+                                              _VP]),
+    "ottohip_col_sums": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP, _VP, _VP, _VP]),
+    "ottohip_center_rows": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP, _VP, _VP]),
     "ottohip_popularity_ranks": (ctypes.c_int, [_VP, _VP, _I64, _VP, _VP, _VP, _VP, _I32, _I32, _I32, ctypes.c_int,
                                                 ctypes.POINTER(_VP), ctypes.POINTER(_I64), _VP]),
+    "ottohip_pop_counts": (ctypes.c_int, [_VP, _VP, _I64, _VP, _VP, _VP, _VP, _I32, _I32, _I32, _VP, _VP]),
+    "ottohip_popularity_from_counts": (ctypes.c_int, [_VP, _VP, _I32, _I32, ctypes.c_int, ctypes.POINTER(_VP),
+                                                      ctypes.POINTER(_I64), _VP]),
     "ottohip_pop_copy": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
     "ottohip_pop_free": (None, [_VP]),
     "ottohip_session_item_similarity": (ctypes.c_int, [_VP, _VP, _I64, _VP, _VP, _VP, _VP, _I32, _VP, ctypes.c_int,

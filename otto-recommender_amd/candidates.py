@@ -136,6 +136,11 @@ class Candidates:
 
     def recall(self, labels_off, labels_aid, src: str | None = None, max_k: int = 20, stream=None) -> dict:
         """R9 on the device: labels as CSR [3 * (S+1)] offsets (int64) + aids (int32)."""
+        return recall_from_sums(self.recall_sums(labels_off, labels_aid, src, max_k, stream))
+
+    def recall_sums(self, labels_off, labels_aid, src: str | None = None, max_k: int = 20, stream=None) -> list:
+        """The 15 integer sums behind recall (per type: hit@20, @100, @200, @all, true; clipped at
+        max_k per session): additive over session shards."""
         import torch
         dev = _dev(self.ctx)
         lo = torch.as_tensor(labels_off).to(dev, torch.int64).contiguous()
@@ -145,7 +150,7 @@ class Candidates:
         _lib.check(_lib.load().ottohip_candidates_recall(self.ctx.h, self.h, _lib.ptr(lo),
                                                          _lib.ptr(la) if la.numel() else None, mask, int(max_k), sums,
                                                          _lib.stream_handle(stream)))
-        return recall_from_sums(list(sums))
+        return list(sums)
 
 
 def recall_from_sums(s) -> dict:

@@ -84,7 +84,8 @@ template <int KP>
 __global__ __launch_bounds__(256) void k_km_assign(const float* __restrict__ X, int64_t n, int dim,
                                                    const float* __restrict__ Ct, const float* __restrict__ cn, int k,
                                                    int32_t* __restrict__ label, unsigned long long* __restrict__ sums,
-                                                   unsigned long long* __restrict__ cnt, double* __restrict__ inertia) {
+                                                   unsigned long long* __restrict__ cnt, double* __restrict__ inertia,
+                                                   unsigned long long* __restrict__ changed, float* __restrict__ dist) {
   extern __shared__ unsigned long long smem64[];
   unsigned long long* ls = smem64;            // k * dim sums (fixed point, two's complement)
   unsigned long long* lc = smem64 + k * dim;  // k counts
@@ -95,6 +96,7 @@ __global__ __launch_bounds__(256) void k_km_assign(const float* __restrict__ X, 
   __syncthreads();
   const int l = threadIdx.x & 63;
   double part = 0.0;
+  uint32_t nchg = 0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); i0 < n; i0 += stride) {
     const int64_t i = i0 + l;
@@ -134,8 +136,10 @@ __global__ __launch_bounds__(256) void k_km_assign(const float* __restrict__ X, 
       if (dd < best) { best = dd; bc = c; }  // ties: lowest cluster index
     }
     if (valid) {
+      if (changed) nchg += label[i] != bc;  // sklearn's strict-convergence test (labels == labels_old)
       label[i] = bc;
       part += (double)fmaxf(best, 0.f);
+      if (dist) dist[i] = fmaxf(best, 0.f);
     }
     if (sums) {  // rows of this wave, lanes over dimensions
       const int nr = (int)min<int64_t>(64, n - i0);
@@ -175,6 +179,10 @@ __global__ __launch_bounds__(256) void k_km_assign(const float* __restrict__ X, 
     part += __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
   }
   if ((threadIdx.x & 63) == 0) atomicAdd(inertia, part);
+  if (changed) {
+    const uint32_t w = wave_sum(nchg);
+    if ((threadIdx.x & 63) == 0 && w) atomicAdd(changed, (unsigned long long)w);
+  }
 }
 
 // C2 on the matrix cores (k <= 64, dim <= 128, dim % 4 == 0): a wave scores a tile of 32 rows
@@ -335,7 +343,8 @@ __global__ __launch_bounds__(KM_MT) void k_km_assign_mfma(const float* __restric
 }
 
 static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int64_t n, int dim, const float* C,
-                            int32_t* labels, unsigned long long* sums, unsigned long long* cnt, double* inr) {
+                            int32_t* labels, unsigned long long* sums, unsigned long long* cnt, double* inr,
+                            unsigned long long* changed = nullptr, float* dist = nullptr) {
   const int KP = (k + 7) / 8 * 8;
   float *Ct, *cn;
   OH_TRY(ctx->ws.get("km_ct", (size_t)KP * dim, &Ct));
@@ -344,7 +353,7 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
   // the MFMA kernel measured 6.4 ms per Lloyd step at 12.9 M x 100, k = 50, against 5.1 ms for
   // the VALU kernel below (argmin butterflies and half the rows per wave): opt-in A/B switch only
   static const bool km_mfma = getenv("OTTOHIP_KM_MFMA") != nullptr;
-  if (km_mfma && k <= 64 && dim <= 8 * KM_NQ && (dim & 3) == 0 && ((uintptr_t)X & 15) == 0 &&
+  if (km_mfma && !changed && !dist && k <= 64 && dim <= 8 * KM_NQ && (dim & 3) == 0 && ((uintptr_t)X & 15) == 0 &&
       ((uintptr_t)C & 15) == 0) {
     const int nq = (dim + 7) / 8, NB = k <= 32 ? 1 : 2;
     const size_t lds = (size_t)NB * nq * 64 * 16 + (KM_MT / 64) * 32 * 4 + 64 * 4 +
@@ -362,13 +371,98 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
   const size_t lds = sums ? ((size_t)k * dim + k) * 8 : 8;
   const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n, 256), (int64_t)ctx->n_cu * 4);
   switch (KP / 8) {
-#define KM_CASE(q) case q: k_km_assign<8 * q><<<grid, 256, lds, s>>>(X, n, dim, Ct, cn, k, labels, sums, cnt, inr); break;
+#define KM_CASE(q) case q: k_km_assign<8 * q><<<grid, 256, lds, s>>>(X, n, dim, Ct, cn, k, labels, sums, cnt, inr, changed, dist); break;
     KM_CASE(1) KM_CASE(2) KM_CASE(3) KM_CASE(4) KM_CASE(5) KM_CASE(6) KM_CASE(7) KM_CASE(8)
 #undef KM_CASE
     default: break;
   }
   OH_HIP(hipGetLastError());
   return 0;
+}
+
+// squared distance of every row to the centroid of its label (inertia of a given labelling,
+// and the per-row distances sklearn's empty-cluster relocation ranks)
+__global__ __launch_bounds__(256) void k_km_labelled(const float* __restrict__ X, int64_t n, int dim,
+                                                     const float* __restrict__ C, const int32_t* __restrict__ label,
+                                                     float* __restrict__ dist, double* __restrict__ inertia) {
+  double part = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float* x = X + i * dim;
+    const float* c = C + (int64_t)label[i] * dim;
+    float acc = 0.f;
+    for (int d = 0; d < dim; ++d) {
+      const float t = x[d] - c[d];
+      acc += t * t;
+    }
+    if (dist) dist[i] = acc;
+    part += (double)acc;
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint64_t b = __double_as_longlong(part);
+    const uint32_t lo = __shfl_xor((uint32_t)b, o), hi = __shfl_xor((uint32_t)(b >> 32), o);
+    part += __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+  }
+  if ((threadIdx.x & 63) == 0 && inertia) atomicAdd(inertia, part);
+}
+
+// argmax of dist over rows not yet taken: key = ordered(dist) << 32 | ~row (ties: lowest row)
+__global__ __launch_bounds__(256) void k_km_argmax(const float* __restrict__ dist, int64_t n,
+                                                   const int64_t* __restrict__ taken, int n_taken,
+                                                   unsigned long long* __restrict__ best) {
+  unsigned long long b = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    bool t = false;
+    for (int j = 0; j < n_taken; ++j) t |= taken[j] == i;
+    if (t) continue;
+    const unsigned long long key = ((unsigned long long)km_ord(dist[i]) << 32) | (uint32_t)(~(uint32_t)i);
+    b = key > b ? key : b;
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    const unsigned long long v = shfl64(b, (int)(lane_id() ^ o));
+    b = v > b ? v : b;
+  }
+  if (lane_id() == 0 && b) atomicMax(best, b);
+}
+
+// sklearn _relocate_empty_clusters_dense on the fixed-point sums: the vector moves from its old
+// cluster's sums to the empty cluster's
+__global__ void k_km_relocate(unsigned long long* __restrict__ sums, unsigned long long* __restrict__ cnt, int dim,
+                              const float* __restrict__ vecs, const int32_t* __restrict__ moves, int m) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  for (int j = 0; j < m; ++j) {  // sequential over moves (an old cluster may lose several)
+    const int oc = moves[2 * j], nc = moves[2 * j + 1];
+    if (d < dim) {
+      const unsigned long long v = (unsigned long long)__float2ll_rn(vecs[(int64_t)j * dim + d] * 16777216.0f);
+      sums[(int64_t)oc * dim + d] -= v;
+      sums[(int64_t)nc * dim + d] = v;
+    }
+    if (d == 0) { cnt[oc] -= 1ull; cnt[nc] = 1ull; }
+  }
+}
+
+// per column: sum of x and of (x - center)^2 in 2^-24 fixed point (exact, order-independent);
+// threads over columns, blocks over row chunks
+__global__ __launch_bounds__(128) void k_col_sums(const float* __restrict__ X, int64_t n, int dim,
+                                                  const float* __restrict__ center, unsigned long long* __restrict__ s1,
+                                                  unsigned long long* __restrict__ s2) {
+  const int d = threadIdx.x;
+  if (d >= dim) return;
+  const float c = center ? center[d] : 0.f;
+  long long a = 0, b = 0;
+  for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const float x = X[i * dim + d];
+    const float t = x - c;
+    a += __float2ll_rn(x * 16777216.0f);
+    b += __float2ll_rn(t * t * 16777216.0f);
+  }
+  atomicAdd(&s1[d], (unsigned long long)a);
+  atomicAdd(&s2[d], (unsigned long long)b);
+}
+
+__global__ void k_center_rows(const float* __restrict__ X, int64_t n, int dim, const float* __restrict__ mean,
+                              float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n * dim) out[i] = X[i] - mean[i % dim];
 }
 
 // ---------------------------------------------------------------- C3
@@ -392,6 +486,11 @@ __global__ void k_pop_count(const int64_t* __restrict__ off, int64_t S, const in
     if (ts[e] > ts_7d) atomicAdd(&cnt[(3 + y) * NS + slot], 1u);
     present[slot] = 1u;
   }
+}
+
+__global__ void k_pop_present(const uint32_t* __restrict__ cnt, int64_t NS, uint32_t* __restrict__ present) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < NS) present[i] = (cnt[i] | cnt[NS + i] | cnt[2 * NS + i]) != 0u;
 }
 
 __global__ void k_pop_pairs(const uint32_t* __restrict__ present, const uint64_t* __restrict__ idx, int64_t NS,
@@ -557,6 +656,164 @@ int ottohip_kmeans_step(ottohip_ctx* ctx, const float* X, int64_t n, int dim, fl
   return 0;
 }
 
+// E-step + partial M-step of one Lloyd iteration on this rank's rows (the
+// sums are all-reduced by the host layer between this and ottohip_kmeans_update)
+int ottohip_kmeans_partial(ottohip_ctx* ctx, const float* X, int64_t n, int dim, const float* centroids, int k,
+                           int32_t* labels, int64_t* sums, int64_t* counts, double* inertia, int64_t* n_changed,
+                           void* stream) {
+  if (!ctx || (n > 0 && !X) || !centroids || (n > 0 && !labels) || !sums || !counts || n < 0 || dim < 1 ||
+      dim > EMB_MAXD || k < 1 || k > KM_MAXK) {
+    set_error("kmeans_partial: bad arguments (k <= %d, dim <= %d)", KM_MAXK, EMB_MAXD); return OTTOHIP_EINVAL;
+  }
+  if (((size_t)k * dim + k) * 8 > 65536) { set_error("kmeans_partial: k * dim too large for LDS"); return OTTOHIP_ELIMIT; }
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  double* inr;
+  unsigned long long* chg;
+  OH_TRY(ctx->ws.get("km_inertia", 1, &inr));
+  OH_TRY(ctx->ws.get("km_changed", 1, &chg));
+  OH_HIP(hipMemsetAsync(sums, 0, (size_t)k * dim * 8, s));
+  OH_HIP(hipMemsetAsync(counts, 0, (size_t)k * 8, s));
+  OH_HIP(hipMemsetAsync(inr, 0, 8, s));
+  OH_HIP(hipMemsetAsync(chg, 0, 8, s));
+  if (n > 0)
+    OH_TRY(launch_km_assign(ctx, k, s, X, n, dim, centroids, labels, reinterpret_cast<unsigned long long*>(sums),
+                            reinterpret_cast<unsigned long long*>(counts), inr, chg, nullptr));
+  double h = 0.0;
+  unsigned long long c = 0;
+  OH_TRY(d2h(&h, inr, 1, s));
+  OH_TRY(d2h(&c, chg, 1, s));
+  if (inertia) *inertia = h;
+  if (n_changed) *n_changed = (int64_t)c;
+  return 0;
+}
+
+// M-step: centroids = sums / counts for non-empty clusters (empty ones keep theirs), shift^2
+int ottohip_kmeans_update(ottohip_ctx* ctx, float* centroids, const int64_t* sums, const int64_t* counts, int k,
+                          int dim, double* shift2, void* stream) {
+  if (!ctx || !centroids || !sums || !counts || k < 1 || dim < 1) { set_error("kmeans_update: bad arguments"); return OTTOHIP_EINVAL; }
+  hipStream_t s = S(stream);
+  std::vector<long long> hs((size_t)k * dim), hc(k);
+  std::vector<float> hcen((size_t)k * dim);
+  OH_TRY(d2h(hs.data(), reinterpret_cast<const long long*>(sums), hs.size(), s));
+  OH_TRY(d2h(hc.data(), reinterpret_cast<const long long*>(counts), hc.size(), s));
+  OH_TRY(d2h(hcen.data(), centroids, hcen.size(), s));
+  double sh = 0.0;
+  for (int c = 0; c < k; ++c) {
+    if (hc[c] <= 0) continue;
+    for (int d = 0; d < dim; ++d) {
+      const float nv = (float)((double)hs[(size_t)c * dim + d] / KM_FX / (double)hc[c]);
+      const double df = (double)nv - (double)hcen[(size_t)c * dim + d];
+      sh += df * df;
+      hcen[(size_t)c * dim + d] = nv;
+    }
+  }
+  OH_HIP(hipMemcpyAsync(centroids, hcen.data(), hcen.size() * sizeof(float), hipMemcpyHostToDevice, s));
+  OH_HIP(hipStreamSynchronize(s));
+  if (shift2) *shift2 = sh;
+  return 0;
+}
+
+// the m rows farthest from their labelled centroid, (distance desc, row asc)
+int ottohip_kmeans_farthest(ottohip_ctx* ctx, const float* X, int64_t n, int dim, const float* centroids,
+                            const int32_t* labels, int m, int64_t* rows, float* d2, void* stream) {
+  if (!ctx || (n > 0 && (!X || !labels)) || !centroids || m < 0 || m > KM_MAXK || (m > 0 && (!rows || !d2)) ||
+      n < 0 || dim < 1) {
+    set_error("kmeans_farthest: bad arguments"); return OTTOHIP_EINVAL;
+  }
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  const int mm = (int)std::min<int64_t>(m, n);
+  for (int j = mm; j < m; ++j) { rows[j] = -1; d2[j] = -1.f; }
+  if (mm == 0) return 0;
+  float* dist;
+  int64_t* taken;
+  unsigned long long* best;
+  OH_TRY(ctx->ws.get("km_dist", (size_t)n, &dist));
+  OH_TRY(ctx->ws.get("km_taken", (size_t)KM_MAXK, &taken));
+  OH_TRY(ctx->ws.get("km_best", 1, &best));
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n, 256), (int64_t)ctx->n_cu * 8);
+  k_km_labelled<<<grid, 256, 0, s>>>(X, n, dim, centroids, labels, dist, nullptr);
+  for (int j = 0; j < mm; ++j) {
+    OH_HIP(hipMemsetAsync(best, 0, 8, s));
+    k_km_argmax<<<grid, 256, 0, s>>>(dist, n, taken, j, best);
+    unsigned long long b = 0;
+    OH_TRY(d2h(&b, best, 1, s));
+    rows[j] = (int64_t)(uint32_t)~(uint32_t)b;
+    const uint32_t o = (uint32_t)(b >> 32), bits = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
+    memcpy(&d2[j], &bits, 4);
+    OH_HIP(hipMemcpyAsync(taken + j, rows + j, 8, hipMemcpyHostToDevice, s));
+  }
+  OH_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+// sklearn's empty-cluster relocation on the (all-reduced) sums: vecs (device m x dim) move from
+// cluster old_new[2j] to the empty cluster old_new[2j + 1] (old_new HOST)
+int ottohip_kmeans_relocate(ottohip_ctx* ctx, int64_t* sums, int64_t* counts, int k, int dim, const float* vecs,
+                            const int32_t* old_new, int m, void* stream) {
+  if (!ctx || !sums || !counts || m < 0 || (m > 0 && (!vecs || !old_new)) || k < 1 || dim < 1 || dim > 1024) {
+    set_error("kmeans_relocate: bad arguments"); return OTTOHIP_EINVAL;
+  }
+  for (int j = 0; j < 2 * m; ++j)
+    if (old_new[j] < 0 || old_new[j] >= k) { set_error("kmeans_relocate: cluster out of range"); return OTTOHIP_ERANGE; }
+  if (m == 0) return 0;
+  hipStream_t s = S(stream);
+  int32_t* mv;
+  OH_TRY(ctx->ws.get("km_moves", (size_t)2 * m, &mv));
+  OH_HIP(hipMemcpyAsync(mv, old_new, (size_t)2 * m * 4, hipMemcpyHostToDevice, s));
+  k_km_relocate<<<grid_for(dim), 256, 0, s>>>(reinterpret_cast<unsigned long long*>(sums),
+                                              reinterpret_cast<unsigned long long*>(counts), dim, vecs, mv, m);
+  OH_HIP(hipGetLastError());
+  OH_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+// sum over rows of |x - centroid[label]|^2 (sklearn's _inertia for a given labelling)
+int ottohip_kmeans_inertia(ottohip_ctx* ctx, const float* X, int64_t n, int dim, const float* centroids,
+                           const int32_t* labels, double* inertia, void* stream) {
+  if (!ctx || (n > 0 && (!X || !labels)) || !centroids || !inertia || n < 0 || dim < 1) {
+    set_error("kmeans_inertia: bad arguments"); return OTTOHIP_EINVAL;
+  }
+  hipStream_t s = S(stream);
+  double* inr;
+  OH_TRY(ctx->ws.get("km_inertia", 1, &inr));
+  OH_HIP(hipMemsetAsync(inr, 0, 8, s));
+  if (n > 0)
+    k_km_labelled<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), (int64_t)ctx->n_cu * 8), 256, 0, s>>>(
+        X, n, dim, centroids, labels, nullptr, inr);
+  OH_HIP(hipGetLastError());
+  OH_TRY(d2h(inertia, inr, 1, s));
+  return 0;
+}
+
+int ottohip_col_sums(ottohip_ctx* ctx, const float* X, int64_t n, int dim, const float* center, int64_t* sum_x,
+                     int64_t* sum_sq, void* stream) {
+  if (!ctx || (n > 0 && !X) || !sum_x || !sum_sq || n < 0 || dim < 1 || dim > 128) {
+    set_error("col_sums: bad arguments (dim <= 128)"); return OTTOHIP_EINVAL;
+  }
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  OH_HIP(hipMemsetAsync(sum_x, 0, (size_t)dim * 8, s));
+  OH_HIP(hipMemsetAsync(sum_sq, 0, (size_t)dim * 8, s));
+  if (n > 0)
+    k_col_sums<<<(unsigned)std::min<int64_t>(n, (int64_t)ctx->n_cu * 16), 128, 0, s>>>(
+        X, n, dim, center, reinterpret_cast<unsigned long long*>(sum_x), reinterpret_cast<unsigned long long*>(sum_sq));
+  OH_HIP(hipGetLastError());
+  return 0;
+}
+
+int ottohip_center_rows(ottohip_ctx* ctx, const float* X, int64_t n, int dim, const float* mean, float* out,
+                        void* stream) {
+  if (!ctx || (n > 0 && (!X || !out)) || !mean || n < 0 || dim < 1) { set_error("center_rows: bad arguments"); return OTTOHIP_EINVAL; }
+  if (n == 0) return 0;
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  k_center_rows<<<grid_for(n * dim), 256, 0, s>>>(X, n, dim, mean, out);
+  OH_HIP(hipGetLastError());
+  return 0;
+}
+
 // labels only (final assignment after the last update, as sklearn's labels_)
 int ottohip_kmeans_assign(ottohip_ctx* ctx, const float* X, int64_t n, int dim, const float* centroids, int k,
                           int32_t* labels, double* inertia, void* stream) {
@@ -582,46 +839,58 @@ struct ottohip_pop {
   int16_t* rank = nullptr;  // [n][6]
 };
 
-int ottohip_popularity_ranks(ottohip_ctx* ctx, const int64_t* session_offsets, int64_t n_sessions,
-                             const int32_t* aid, const int32_t* ts, const int8_t* type, const int32_t* session_cl,
-                             int32_t n_items, int32_t n_clusters, int32_t ts_7d, int keep_top_k,
-                             ottohip_pop** out, int64_t* n_out, void* stream) {
-  if (!ctx || !out || !n_out || n_sessions < 0 || n_items < 1 || n_clusters < 1 ||
+int ottohip_pop_counts(ottohip_ctx* ctx, const int64_t* session_offsets, int64_t n_sessions, const int32_t* aid,
+                       const int32_t* ts, const int8_t* type, const int32_t* session_cl, int32_t n_items,
+                       int32_t n_clusters, int32_t ts_7d, uint32_t* counts, void* stream) {
+  if (!ctx || !counts || n_sessions < 0 || n_items < 1 || n_clusters < 1 ||
       (n_sessions > 0 && (!session_offsets || !aid || !ts || !type || !session_cl))) {
-    set_error("popularity_ranks: bad arguments"); return OTTOHIP_EINVAL;
+    set_error("pop_counts: bad arguments"); return OTTOHIP_EINVAL;
   }
   const int64_t NS = (int64_t)n_clusters * n_items;
-  if (NS >= ((int64_t)1 << 32)) { set_error("popularity_ranks: n_clusters * n_items >= 2^32"); return OTTOHIP_ELIMIT; }
+  if (NS >= ((int64_t)1 << 32)) { set_error("pop_counts: n_clusters * n_items >= 2^32"); return OTTOHIP_ELIMIT; }
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  uint32_t* present;
+  int* err;
+  OH_TRY(ctx->ws.get("pop_present", (size_t)NS, &present));  // scratch for k_pop_count's presence marks
+  OH_TRY(ctx->ws.get("pop_err", 1, &err));
+  OH_HIP(hipMemsetAsync(err, 0, sizeof(int), s));
+  if (n_sessions > 0)
+    k_pop_count<<<(unsigned)ceil_div(n_sessions, 4), 256, 0, s>>>(session_offsets, n_sessions, aid, ts, type, session_cl,
+                                                                   n_items, n_clusters, ts_7d, counts, present, err);
+  OH_HIP(hipGetLastError());
+  int herr = 0;
+  OH_TRY(d2h(&herr, err, 1, s));
+  if (herr) { set_error("pop_counts: cluster, aid or type out of range"); return OTTOHIP_ERANGE; }
+  return 0;
+}
+
+int ottohip_popularity_from_counts(ottohip_ctx* ctx, const uint32_t* cnt, int32_t n_items, int32_t n_clusters,
+                                   int keep_top_k, ottohip_pop** out, int64_t* n_out, void* stream) {
+  if (!ctx || !cnt || !out || !n_out || n_items < 1 || n_clusters < 1) {
+    set_error("popularity_from_counts: bad arguments"); return OTTOHIP_EINVAL;
+  }
+  const int64_t NS = (int64_t)n_clusters * n_items;
+  if (NS >= ((int64_t)1 << 32)) { set_error("popularity_from_counts: n_clusters * n_items >= 2^32"); return OTTOHIP_ELIMIT; }
   *out = nullptr;
   *n_out = 0;
   hipStream_t s = S(stream);
   OH_HIP(hipSetDevice(ctx->device));
   Workspace& ws = ctx->ws;
-  uint32_t *cnt, *present;
+  uint32_t* present;
   uint64_t *pidx, *tot;
-  int* err;
-  OH_TRY(ws.get("pop_cnt", (size_t)NS * 6, &cnt));
   OH_TRY(ws.get("pop_present", (size_t)NS, &present));
   OH_TRY(ws.get("pop_pidx", (size_t)NS, &pidx));
   OH_TRY(ws.get("pop_tot", 2, &tot));
-  OH_TRY(ws.get("pop_err", 1, &err));
   int ph = ctx->begin("pop_ranks", s, 0);
-  OH_HIP(hipMemsetAsync(cnt, 0, (size_t)NS * 6 * 4, s));
-  OH_HIP(hipMemsetAsync(present, 0, (size_t)NS * 4, s));
-  OH_HIP(hipMemsetAsync(err, 0, sizeof(int), s));
-  if (n_sessions > 0)
-    k_pop_count<<<(unsigned)ceil_div(n_sessions, 4), 256, 0, s>>>(session_offsets, n_sessions, aid, ts, type, session_cl,
-                                                                   n_items, n_clusters, ts_7d, cnt, present, err);
+  k_pop_present<<<grid_for(NS), 256, 0, s>>>(cnt, NS, present);
   OH_TRY(exclusive_scan_u32(ctx, present, pidx, NS, tot, s));
   uint64_t np_ = 0;
-  int herr = 0;
   OH_TRY(d2h(&np_, tot, 1, s));
-  OH_TRY(d2h(&herr, err, 1, s));
-  if (herr) { set_error("popularity_ranks: cluster, aid or type out of range"); return OTTOHIP_ERANGE; }
   ottohip_pop* P = new ottohip_pop();
   const int64_t n = (int64_t)np_;
   if (n == 0) { *out = P; return 0; }
-  uint32_t *slot, *k0, *v0, *k1, *v1, *hist, *keep;
+  uint32_t *slot, *k0, *v0, *k1, *v1, *keep;
   uint16_t* rank;
   uint64_t *cl_first, *oidx;
   auto fail = [&](int rc) { delete P; return rc; };
@@ -629,11 +898,10 @@ int ottohip_popularity_ranks(ottohip_ctx* ctx, const int64_t* session_offsets, i
   if ((rc = ws.get("pop_slot", (size_t)n, &slot)) || (rc = ws.get("pop_k0", (size_t)n, &k0)) ||
       (rc = ws.get("pop_v0", (size_t)n, &v0)) || (rc = ws.get("pop_k1", (size_t)n, &k1)) ||
       (rc = ws.get("pop_v1", (size_t)n, &v1)) || (rc = ws.get("pop_rank", (size_t)n * 6, &rank)) ||
-      (rc = ws.get("pop_hist", (size_t)n_clusters + 1, &hist)) || (rc = ws.get("pop_clf", (size_t)n_clusters + 1, &cl_first)) ||
+      (rc = ws.get("pop_clf", (size_t)n_clusters + 1, &cl_first)) ||
       (rc = ws.get("pop_keep", (size_t)n, &keep)) || (rc = ws.get("pop_oidx", (size_t)n, &oidx)))
     return fail(rc);
   k_pop_pairs<<<grid_for(NS), 256, 0, s>>>(present, pidx, NS, slot);
-  (void)hist;
   k_pop_cluster_first<<<grid_for(n + 1), 256, 0, s>>>(slot, n, n_items, n_clusters, cl_first);
   const int cbits = std::max(1, bits_for((uint64_t)n_clusters));
   for (int t = 0; t < 6; ++t) {
@@ -665,6 +933,23 @@ int ottohip_popularity_ranks(ottohip_ctx* ctx, const int64_t* session_offsets, i
   *out = P;
   *n_out = P->n;
   return 0;
+}
+
+int ottohip_popularity_ranks(ottohip_ctx* ctx, const int64_t* session_offsets, int64_t n_sessions,
+                             const int32_t* aid, const int32_t* ts, const int8_t* type, const int32_t* session_cl,
+                             int32_t n_items, int32_t n_clusters, int32_t ts_7d, int keep_top_k,
+                             ottohip_pop** out, int64_t* n_out, void* stream) {
+  if (!ctx || !out || !n_out || n_items < 1 || n_clusters < 1) { set_error("popularity_ranks: bad arguments"); return OTTOHIP_EINVAL; }
+  const int64_t NS = (int64_t)n_clusters * n_items;
+  if (NS >= ((int64_t)1 << 32)) { set_error("popularity_ranks: n_clusters * n_items >= 2^32"); return OTTOHIP_ELIMIT; }
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  uint32_t* cnt;
+  OH_TRY(ctx->ws.get("pop_cnt", (size_t)NS * 6, &cnt));
+  OH_HIP(hipMemsetAsync(cnt, 0, (size_t)NS * 6 * 4, s));
+  OH_TRY(ottohip_pop_counts(ctx, session_offsets, n_sessions, aid, ts, type, session_cl, n_items, n_clusters, ts_7d,
+                            cnt, stream));
+  return ottohip_popularity_from_counts(ctx, cnt, n_items, n_clusters, keep_top_k, out, n_out, stream);
 }
 
 int ottohip_pop_copy(const ottohip_pop* p, int32_t* aid, int32_t* cl, int16_t* ranks6, void* stream) {

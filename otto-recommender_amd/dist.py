@@ -298,6 +298,17 @@ def _records(a, b, c):
     return torch.stack([a.to(torch.int32), b.to(torch.int32), c, c], 1).contiguous()
 
 
+def all_gather_sizes(n: int, group=None) -> list:
+    """Every rank's n, in rank order."""
+    import torch
+    import torch.distributed as dist
+    dev = _comm_device(group)
+    t = torch.tensor([int(n)], dtype=torch.int64, device=dev)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(out, t, group=group)
+    return [int(x.item()) for x in out]
+
+
 def all_gather_rows(cols, group=None):
     """All-gather of variable-length (aid, aid_next, count) device columns, in rank order."""
     import torch

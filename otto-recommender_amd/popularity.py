@@ -1,10 +1,10 @@
 """Pop-cluster source of config 5 and session-item similarity.
 
   compute_sessions_embeddings   model/kmeans_sessions.py:40-86
-  KMeans (fit / labels_)        model/kmeans_sessions.py:140-171 (Lloyd, sklearn 'random' init
-                                semantics: rows RandomState(random_state).permutation(n)[:k];
-                                tol scaled by the mean feature variance; the reference's dask-ml
-                                k-means|| init is not reproducible)
+  KMeans (fit / labels_)        model/kmeans_sessions.py:140-171, the scikit-learn==1.2 branch
+                                (init='random', n_init='auto' = 10 runs, empty-cluster relocation,
+                                strict convergence); the reference's dask-ml k-means|| default is
+                                not reproducible
   count_popularity              model/count_popularity.py:53-85 (ranks_for_clusters)
   session_item_similarity       model/retrieve.py:604-625
 All compute runs in libottohip.so (csrc/popularity.hip).
@@ -56,42 +56,159 @@ def compute_sessions_embeddings(offsets, aid, ts, type_, words, embeddings, n_it
     return out[:S]
 
 
+FX = float(1 << 24)  # fixed-point scale of the device sums (csrc/popularity.hip KM_FX)
+
+
+def _allreduce(t, group):
+    if group is None:
+        return t
+    from .dist import _allreduce_sum
+    return _allreduce_sum(t, group)
+
+
 class KMeans:
-    """KMeans(n_clusters, max_iter=100, tol=1e-3, random_state=42) on a device matrix."""
+    """KMeans(n_clusters, init='random', n_init='auto', max_iter=100, tol=1e-3, random_state=42):
+    the reference's scikit-learn branch (model/kmeans_sessions.py:152-159, scikit-learn==1.2) on a
+    device matrix, run as sklearn 1.2's KMeans.fit + _kmeans_single_lloyd:
+      - X is centred on its column means; tol is scaled by the mean column variance;
+      - n_init ('auto' = 10 for init='random') runs, each seeded by the rows
+        RandomState(random_state).permutation(n)[:k] of the same RandomState (sklearn 1.2
+        _init_centroids); the run with the lowest inertia is kept;
+      - Lloyd iterations: E-step, per-cluster sums, empty clusters relocated to the rows farthest
+        from their centroid (_relocate_empty_clusters_dense), M-step; stop when no label changed
+        (strict convergence) or the squared centre shift <= tol; without strict convergence the
+        labels are recomputed with the final centres; inertia = sum |x - c[label]|^2.
+    The reference's default dask-ml k-means|| path draws from dask's chunked random streams and is
+    not reproducible. group: rows sharded over ranks: the sums,
+    counts and statistics are all-reduced (exact 2^-24 fixed point), so every rank ends with the
+    single-GPU result. Ties between equal inertias keep the earlier run (sklearn also skips a run
+    that is the same clustering)."""
 
-    def __init__(self, n_clusters: int = 50, max_iter: int = 100, tol: float = 1e-3, random_state: int = 42):
+    def __init__(self, n_clusters: int = 50, max_iter: int = 100, tol: float = 1e-3, random_state: int = 42,
+                 init: str = "random", n_init="auto"):
+        if init != "random":
+            raise ValueError("init='random' (the reference's sklearn branch) is the supported initialisation")
         self.n_clusters, self.max_iter, self.tol, self.random_state = n_clusters, max_iter, tol, random_state
+        self.init = init
+        self.n_init = 10 if n_init == "auto" else int(n_init)
 
-    def fit(self, X, ctx=None, stream=None, group=None):
+    def fit(self, X, ctx=None, stream=None, group=None, global_rows=None):
         import torch
         ctx = ctx or _lib.context()
         dev = torch.device("cuda", ctx.device)
+        lib = _lib.load()
+        sh = _lib.stream_handle(stream)
         X = _t(X, dev, torch.float32)
         n, dim = (int(v) for v in X.shape)
         k = self.n_clusters
-        seeds = np.random.RandomState(self.random_state).permutation(n)[:k]
-        C = X[torch.from_numpy(seeds).to(dev)].clone().contiguous()
-        tol_abs = float(torch.var(X.double(), dim=0, unbiased=False).mean().item()) * self.tol
-        labels = torch.empty(n, dtype=torch.int32, device=dev)
-        lib = _lib.load()
-        sh, inr = ctypes.c_double(), ctypes.c_double()
-        it = 0
-        for it in range(1, self.max_iter + 1):
-            _lib.check(lib.ottohip_kmeans_step(ctx.h, _lib.ptr(X), n, dim, _lib.ptr(C), k, _lib.ptr(labels),
-                                               ctypes.byref(sh), ctypes.byref(inr), _lib.stream_handle(stream)))
-            if sh.value <= tol_abs:
-                break
-        _lib.check(lib.ottohip_kmeans_assign(ctx.h, _lib.ptr(X), n, dim, _lib.ptr(C), k, _lib.ptr(labels),
-                                             ctypes.byref(inr), _lib.stream_handle(stream)))
-        self.cluster_centers_, self.labels_, self.inertia_, self.n_iter_ = C, labels, inr.value, it
+        if group is not None:  # this rank's rows are the global rows `global_rows` (increasing)
+            from .dist import all_gather_sizes
+            n_all = sum(all_gather_sizes(n, group))
+            grows = np.arange(n, dtype=np.int64) if global_rows is None else np.asarray(global_rows, np.int64)
+            if len(grows) != n or np.any(np.diff(grows) <= 0):
+                raise ValueError("global_rows: one increasing global row id per local row")
+        else:
+            n_all, grows = n, np.arange(n, dtype=np.int64)
+        if n_all < k:
+            raise ValueError(f"n_samples={n_all} should be >= n_clusters={k}")
+        # column means (exact fixed-point sums), centring, tol = mean variance * tol
+        s1 = torch.empty(dim, dtype=torch.int64, device=dev)
+        s2 = torch.empty(dim, dtype=torch.int64, device=dev)
+        _lib.check(lib.ottohip_col_sums(ctx.h, _lib.ptr(X), n, dim, None, _lib.ptr(s1), _lib.ptr(s2), sh))
+        s1 = _allreduce(s1, group)
+        mean = (s1.cpu().numpy().astype(np.float64) / FX / n_all).astype(np.float32)
+        mean_d = torch.from_numpy(mean).to(dev)
+        Xc = torch.empty_like(X)
+        _lib.check(lib.ottohip_center_rows(ctx.h, _lib.ptr(X), n, dim, _lib.ptr(mean_d), _lib.ptr(Xc), sh))
+        _lib.check(lib.ottohip_col_sums(ctx.h, _lib.ptr(Xc), n, dim, None, _lib.ptr(s1), _lib.ptr(s2), sh))
+        s1, s2 = _allreduce(s1, group), _allreduce(s2, group)
+        m1 = s1.cpu().numpy().astype(np.float64) / FX / n_all
+        var = s2.cpu().numpy().astype(np.float64) / FX / n_all - m1 * m1
+        tol_abs = float(np.mean(var)) * self.tol
+        rs = np.random.RandomState(self.random_state)
+        sums = torch.empty(k * dim, dtype=torch.int64, device=dev)
+        counts = torch.empty(k, dtype=torch.int64, device=dev)
+        labels = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        best = None
+        inr, chg, shift = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+        for run in range(self.n_init):
+            seeds = rs.permutation(n_all)[:k]
+            C = self._gather_rows(Xc, seeds, grows, group)
+            labels.fill_(-1)
+            strict, it = False, 0
+            for it in range(1, self.max_iter + 1):
+                _lib.check(lib.ottohip_kmeans_partial(ctx.h, _lib.ptr(Xc), n, dim, _lib.ptr(C), k, _lib.ptr(labels),
+                                                      _lib.ptr(sums), _lib.ptr(counts), ctypes.byref(inr),
+                                                      ctypes.byref(chg), sh))
+                sums, counts = _allreduce(sums, group), _allreduce(counts, group)
+                n_changed = int(_allreduce(torch.tensor([chg.value], dtype=torch.int64), group).item())
+                cnt = counts.cpu().numpy()
+                empty = np.flatnonzero(cnt == 0)
+                if len(empty):
+                    self._relocate(Xc, C, labels, sums, counts, empty, grows, group, ctx, sh)
+                _lib.check(lib.ottohip_kmeans_update(ctx.h, _lib.ptr(C), _lib.ptr(sums), _lib.ptr(counts), k, dim,
+                                                     ctypes.byref(shift), sh))
+                if n_changed == 0:
+                    strict = True
+                    break
+                if shift.value <= tol_abs:
+                    break
+            if not strict:  # E-step with the final centres (labels match cluster_centers_)
+                _lib.check(lib.ottohip_kmeans_partial(ctx.h, _lib.ptr(Xc), n, dim, _lib.ptr(C), k, _lib.ptr(labels),
+                                                      _lib.ptr(sums), _lib.ptr(counts), ctypes.byref(inr),
+                                                      ctypes.byref(chg), sh))
+            _lib.check(lib.ottohip_kmeans_inertia(ctx.h, _lib.ptr(Xc), n, dim, _lib.ptr(C), _lib.ptr(labels),
+                                                  ctypes.byref(inr), sh))
+            inertia = float(_allreduce(torch.tensor([inr.value], dtype=torch.float64), group).item())
+            if best is None or inertia < best[0]:
+                best = (inertia, C.clone(), labels[:n].clone(), it)
+        self.inertia_, C, self.labels_, self.n_iter_ = best
+        self.cluster_centers_ = C + mean_d
         return self
+
+    @staticmethod
+    def _gather_rows(Xc, rows, grows, group):
+        """global rows of the (row-sharded) matrix, replicated: each rank fills the ones it owns."""
+        import torch
+        rows = np.asarray(rows, np.int64)
+        C = torch.zeros((len(rows), Xc.shape[1]), dtype=torch.float32, device=Xc.device)
+        loc = np.searchsorted(grows, rows)
+        mine = np.flatnonzero((loc < len(grows)) & (grows[np.minimum(loc, len(grows) - 1)] == rows)) if len(grows) else []
+        if len(mine):
+            C[torch.from_numpy(mine).to(Xc.device)] = Xc[torch.from_numpy(loc[mine]).to(Xc.device)]
+        return _allreduce(C, group).contiguous()
+
+    def _relocate(self, Xc, C, labels, sums, counts, empty, grows, group, ctx, sh):
+        """_relocate_empty_clusters_dense: the len(empty) rows farthest from their centroid (all
+        ranks: distance desc, global row asc) leave their cluster for the empty ones."""
+        import torch
+        m = len(empty)
+        n = int(Xc.shape[0])
+        rows = (ctypes.c_int64 * m)()
+        d2 = (ctypes.c_float * m)()
+        _lib.check(_lib.load().ottohip_kmeans_farthest(ctx.h, _lib.ptr(Xc), n, Xc.shape[1], _lib.ptr(C),
+                                                       _lib.ptr(labels), m, rows, d2, sh))
+        cand = [(float(d2[j]), int(grows[rows[j]]), int(labels[rows[j]].item())) for j in range(m) if rows[j] >= 0]
+        if group is not None:
+            import torch.distributed as dist
+            allc = [None] * dist.get_world_size(group)
+            dist.all_gather_object(allc, cand, group=group)
+            cand = [c for part in allc for c in part]
+        cand.sort(key=lambda c: (-c[0], c[1]))
+        cand = cand[:m]
+        vecs = self._gather_rows(Xc, [c[1] for c in cand], grows, group)
+        moves = np.stack([np.array([c[2] for c in cand], np.int32), np.asarray(empty[:len(cand)], np.int32)], 1).ravel()
+        mv = (ctypes.c_int32 * len(moves))(*moves.tolist())
+        _lib.check(_lib.load().ottohip_kmeans_relocate(ctx.h, _lib.ptr(sums), _lib.ptr(counts), self.n_clusters,
+                                                       Xc.shape[1], _lib.ptr(vecs), mv, len(cand), sh))
 
 
 def count_popularity(offsets, aid, ts, type_, session_cl, n_clusters: int, n_items: int = config.N_ITEMS_OTTO,
                      keep_top_k: int = config.KEEP_TOP_K, ts_max: int | None = None, suffix: str = "cl50",
-                     ctx=None, stream=None):
+                     ctx=None, stream=None, group=None):
     """C3 for one clustering (dense cluster index per session). Returns pandas
-    DataFrame[aid, {suffix}, rank_*_{suffix} (6 columns)], rows sorted by (cluster, aid)."""
+    DataFrame[aid, {suffix}, rank_*_{suffix} (6 columns)], rows sorted by (cluster, aid).
+    group: sessions sharded over ranks; every rank returns the same (global) ranks."""
     import pandas as pd
     import torch
     ctx = ctx or _lib.context()
@@ -102,14 +219,29 @@ def count_popularity(offsets, aid, ts, type_, session_cl, n_clusters: int, n_ite
     cl = _t(session_cl, dev, torch.int32)
     S = int(off.numel()) - 1
     if ts_max is None:
-        ts_max = int(s_.max().item()) if s_.numel() else 0
+        ts_max = int(s_.max().item()) if s_.numel() else -(1 << 31)
+        if group is not None:  # the latest event over every rank's sessions
+            import torch.distributed as dist
+            from .dist import _comm_device
+            t = torch.tensor([ts_max], dtype=torch.int64, device=_comm_device(group))
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+            ts_max = int(t.item())
     ts_7d = int(ts_max) - 7 * 24 * 60 * 60                     # count_popularity.py:54-55
     h = ctypes.c_void_p()
     nout = ctypes.c_int64()
     lib = _lib.load()
-    _lib.check(lib.ottohip_popularity_ranks(ctx.h, _lib.ptr(off), S, _lib.ptr(a), _lib.ptr(s_), _lib.ptr(y), _lib.ptr(cl),
-                                            int(n_items), int(n_clusters), ts_7d, int(keep_top_k), ctypes.byref(h),
-                                            ctypes.byref(nout), _lib.stream_handle(stream)))
+    sh = _lib.stream_handle(stream)
+    if group is None:
+        _lib.check(lib.ottohip_popularity_ranks(ctx.h, _lib.ptr(off), S, _lib.ptr(a), _lib.ptr(s_), _lib.ptr(y),
+                                                _lib.ptr(cl), int(n_items), int(n_clusters), ts_7d, int(keep_top_k),
+                                                ctypes.byref(h), ctypes.byref(nout), sh))
+    else:  # sessions sharded: per-rank counters, all-reduced, ranked identically on every rank
+        cnt = torch.zeros(6 * int(n_clusters) * int(n_items), dtype=torch.int32, device=dev)
+        _lib.check(lib.ottohip_pop_counts(ctx.h, _lib.ptr(off), S, _lib.ptr(a), _lib.ptr(s_), _lib.ptr(y), _lib.ptr(cl),
+                                          int(n_items), int(n_clusters), ts_7d, _lib.ptr(cnt), sh))
+        cnt = _allreduce(cnt, group)
+        _lib.check(lib.ottohip_popularity_from_counts(ctx.h, _lib.ptr(cnt), int(n_items), int(n_clusters),
+                                                      int(keep_top_k), ctypes.byref(h), ctypes.byref(nout), sh))
     n = int(nout.value)
     try:
         oa = torch.empty(max(n, 1), dtype=torch.int32, device=dev)

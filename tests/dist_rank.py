@@ -62,6 +62,34 @@ def covis(out, cfg):
     np.savez(out, **res)
 
 
+def pipeline(out, cfg):
+    import torch.distributed as dist
+    import otto_recommender_amd.synth as synth
+    from otto_recommender_amd import pipeline as pl
+    ev = synth.generate(cfg["sessions"], first_session=cfg.get("first_session", 0))
+    train, test, labels = synth.split_test_labels(ev)
+    words = synth.item_words()
+    emb = synth.embeddings(len(words), seed=1)
+    emb2 = synth.embeddings(len(words), seed=3)
+    res = pl.run(train, test, labels, words, emb, words, emb2, n_clusters=cfg["clusters"], kmeans_iter=cfg["iters"],
+                 knn_queries=cfg["queries"], keep_tables=True, group=dist.group.WORLD, n_init=cfg["n_init"],
+                 per_file=cfg["per_file"])
+    im = res["intermediates"]
+    o = {"candidates_total": np.array([res["candidates"], res["local_candidates"]], np.int64),
+         "recall": np.array([res["recall"][t][k] for t in ("clicks", "carts", "orders", "total")
+                             for k in ("top20", "top100", "top200", "topall")]),
+         "cluster_labels": im["cluster_labels"], "cluster_rows": im["cluster_rows"],
+         "pop": im["pop"].to_numpy().astype(np.int64)}
+    for n, v in im["tables"].items():
+        o[f"table/{n}"] = np.stack([np.asarray(x, np.int64) for x in v], 1)
+    for i, v in enumerate(im["knn"]):
+        o[f"knn/{i}"] = np.stack([np.asarray(x, np.int64) for x in v], 1)
+    c = im["candidates"]
+    o["cand_cols"] = np.array(list(c.columns))
+    o["cand"] = c.to_numpy().astype(np.int64)
+    np.savez(out, **o)
+
+
 def main():
     import torch
     import torch.distributed as dist
@@ -69,7 +97,7 @@ def main():
     torch.cuda.set_device(0)
     dist.init_process_group("gloo")
     try:
-        {"covis": covis}[mode](out, cfg)
+        {"covis": covis, "pipeline": pipeline}[mode](out, cfg)
         dist.barrier()
     finally:
         dist.destroy_process_group()

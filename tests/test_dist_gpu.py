@@ -93,3 +93,45 @@ def test_covis_sharded_two_ranks(gpu, tmp_path):
             np.testing.assert_array_equal(sl[o], ref, err_msg=f"slices {tag} {n}")
             if tag == "scaled" and n in ("click_to_click", "click_to_cart_or_buy"):
                 assert len(ref) == kw["max_pairs"], (n, len(ref))  # the global cut is active
+
+
+def test_pipeline_two_ranks_equals_one_gpu(gpu, tmp_path):
+    """BASELINE configs[4] split over 2 ranks (pipeline.run(group=...)): train/test files dealt per
+    folder, sharded A6 per folder, kNN queries split, KMeans rows sharded with all-reduced exact
+    sums, C3 counters all-reduced, candidates per rank. Every shard-level output must equal the
+    1-GPU run on the same input: A7 tables, kNN lists, cluster labels, pop lists, the union of
+    the per-rank candidates, and recall."""
+    import otto_recommender_amd.synth as synth
+    from otto_recommender_amd import pipeline as pl
+    cfg = {"sessions": 30_000, "first_session": 808, "clusters": 6, "iters": 15, "queries": 20_000, "n_init": 2,
+           "per_file": 2_500}
+    res = _launch("pipeline", cfg, tmp_path, timeout=400)
+    ev = synth.generate(cfg["sessions"], first_session=cfg["first_session"])
+    train, test, labels = synth.split_test_labels(ev)
+    words = synth.item_words()
+    emb = synth.embeddings(len(words), seed=1)
+    emb2 = synth.embeddings(len(words), seed=3)
+    one = pl.run(train, test, labels, words, emb, words, emb2, n_clusters=cfg["clusters"], kmeans_iter=cfg["iters"],
+                 knn_queries=cfg["queries"], keep_tables=True, n_init=cfg["n_init"], per_file=cfg["per_file"])
+    im = one["intermediates"]
+    for r in res:
+        for n, v in im["tables"].items():
+            np.testing.assert_array_equal(r[f"table/{n}"], np.stack([np.asarray(x, np.int64) for x in v], 1), err_msg=n)
+        for i, v in enumerate(im["knn"]):
+            np.testing.assert_array_equal(r[f"knn/{i}"], np.stack([np.asarray(x, np.int64) for x in v], 1))
+        np.testing.assert_array_equal(r["pop"], im["pop"].to_numpy().astype(np.int64))
+        assert r["candidates_total"][0] == one["candidates"]
+        ref_rec = [one["recall"][t][k] for t in ("clicks", "carts", "orders", "total")
+                   for k in ("top20", "top100", "top200", "topall")]
+        np.testing.assert_allclose(r["recall"], ref_rec, rtol=0, atol=1e-12)
+    rows = np.concatenate([r["cluster_rows"] for r in res])
+    lab = np.concatenate([r["cluster_labels"] for r in res])
+    assert sorted(rows.tolist()) == list(range(len(im["cluster_labels"])))
+    np.testing.assert_array_equal(lab[np.argsort(rows)], im["cluster_labels"])
+    cols = list(res[0]["cand_cols"])
+    got = np.concatenate([r["cand"] for r in res])
+    got = got[np.lexsort((got[:, 1], got[:, cols.index("ts_order_aid")], got[:, 0]))]
+    ref = im["candidates"][cols].to_numpy().astype(np.int64)
+    ref = ref[np.lexsort((ref[:, 1], ref[:, cols.index("ts_order_aid")], ref[:, 0]))]
+    np.testing.assert_array_equal(got, ref)
+    assert sum(int(r["candidates_total"][1]) for r in res) == one["candidates"]

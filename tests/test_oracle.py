@@ -76,3 +76,37 @@ def test_merge_restatement_small():
     assert list(zip(a.tolist(), b.tolist(), c.tolist())) == [(1, 2, 11), (2, 1, 11)]
     a, b, c = covis.concat_files_w_stats("click_to_cart_or_buy", parts, click_filter_rows=1)
     assert list(zip(a.tolist(), b.tolist(), c.tolist())) == [(1, 2, 11), (2, 1, 11)]
+
+
+def _kmeans_fixture(seed=4, n=3000, k=12, dup=True):
+    rng = np.random.default_rng(seed)
+    centers = rng.normal(scale=3, size=(k - 3, 20))
+    X = centers[rng.integers(0, k - 3, n)] + rng.normal(size=(n, 20))
+    if dup:  # many identical rows: seeds collide, clusters empty out, relocation runs
+        X[: n // 3] = X[0]
+    return X
+
+
+def test_kmeans_oracle_runs_match_sklearn():
+    """Each Lloyd run of the oracle (oracle/popularity.py, sklearn 1.2 restated) against the installed
+    scikit-learn given the same initial centres: labels, inertia and iteration count. This pins the
+    restatement the GPU KMeans is tested against (tests/test_popularity_gpu.py)."""
+    import warnings
+    from sklearn.cluster import KMeans
+    import popularity as oracle_pop
+    for dup in (False, True):
+        X = _kmeans_fixture(dup=dup)
+        k = 12
+        tol_abs = float(np.mean(np.var(X, axis=0))) * 1e-3
+        mean = X.mean(0)
+        relocated = 0
+        for seeds in oracle_pop.kmeans_seeds(len(X), k, 10, 42):
+            lab, C, inertia, it = oracle_pop._lloyd(X - mean, (X - mean)[seeds].copy(), 100, tol_abs)
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore")
+                km = KMeans(n_clusters=k, init=X[seeds], n_init=1, max_iter=100, tol=1e-3, algorithm="lloyd").fit(X)
+            np.testing.assert_array_equal(lab, km.labels_)
+            assert abs(inertia - km.inertia_) <= 1e-9 * km.inertia_
+            assert it == km.n_iter_
+            relocated += len(np.unique(X[seeds], axis=0)) < k
+        assert (relocated > 0) == dup

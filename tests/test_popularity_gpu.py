@@ -2,9 +2,9 @@
 
 C3 popularity ranks: exact (integer). C1 session embeddings: fp32 sums vs f64 restatement,
 tolerance 3e-6 absolute after round6 (one unit in the 6th decimal plus fp32 output rounding;
-the reference's own polars f32 summation order is unspecified). C2 KMeans: same init and
-convergence rule as the restatement; labels agree on >= 99.9 % of rows (fp32 vs f64 near-ties),
-centroids within 1e-3. R7: rtol 1e-5 vs f64."""
+the reference's own polars f32 summation order is unspecified). C2 KMeans: sklearn 1.2's
+algorithm as restated in the oracle (itself pinned against scikit-learn); labels agree on >= 99.9 %
+of rows (fp32 vs f64 near-ties), centroids within 1e-3, inertia rel 1e-5. R7: rtol 1e-5 vs f64."""
 import numpy as np
 import pandas as pd
 import pytest
@@ -32,30 +32,45 @@ def test_session_embeddings(gpu):
     np.testing.assert_allclose(got, ref, atol=3e-6, rtol=0)
 
 
-def test_kmeans_matches_restatement(gpu):
+def _check_kmeans(X, k, n_init=10, agree=0.999, rel=1e-5):
     from otto_recommender_amd import popularity as gp
+    km = gp.KMeans(n_clusters=k, max_iter=100, tol=1e-3, random_state=42, n_init=n_init).fit(X)
+    lab_ref, C_ref, it_ref, inertia_ref = oracle_pop.kmeans(X, k, n_init=n_init)
+    lab = km.labels_.cpu().numpy()
+    assert np.mean(lab == lab_ref) >= agree, (np.mean(lab == lab_ref), km.inertia_, inertia_ref)
+    if agree >= 0.999:  # (the relocation fixture ends a few boundary rows apart: inertia and labels only)
+        np.testing.assert_allclose(km.cluster_centers_.cpu().numpy(), C_ref, atol=1e-3)
+    assert abs(km.inertia_ - inertia_ref) <= rel * inertia_ref, (km.inertia_, inertia_ref)
+    assert abs(km.n_iter_ - it_ref) <= 2
+
+
+def test_kmeans_matches_restatement(gpu):
+    """sklearn 1.2 KMeans(init='random', n_init='auto'=10) vs the oracle (pinned against the
+    installed scikit-learn run by run in tests/test_oracle.py)."""
     rng = np.random.default_rng(2)
     centers = rng.normal(scale=3, size=(12, 100))
     X = (centers[rng.integers(0, 12, 20000)] + rng.normal(size=(20000, 100))).astype(np.float32)
-    km = gp.KMeans(n_clusters=10, max_iter=100, tol=1e-3, random_state=42).fit(X)
-    lab_ref, C_ref, it_ref = oracle_pop.kmeans(X, 10)
-    lab = km.labels_.cpu().numpy()
-    assert np.mean(lab == lab_ref) >= 0.999
-    np.testing.assert_allclose(km.cluster_centers_.cpu().numpy(), C_ref, atol=1e-3)
-    assert abs(km.n_iter_ - it_ref) <= 2
+    _check_kmeans(X, 10)
+
+
+def test_kmeans_empty_cluster_relocation(gpu):
+    """a third of the rows identical: seeds collide, clusters empty out and are relocated to the
+    farthest rows (_relocate_empty_clusters_dense)"""
+    rng = np.random.default_rng(4)
+    centers = rng.normal(scale=3, size=(9, 100))
+    X = (centers[rng.integers(0, 9, 6000)] + rng.normal(size=(6000, 100))).astype(np.float32)
+    X[:2000] = X[0]
+    # fp32 distances reorder near-equal candidates of the relocation against the f64 oracle: a few
+    # boundary rows may follow (measured 9 of 6000)
+    _check_kmeans(X, 12, agree=0.995, rel=1e-4)
 
 
 def test_kmeans_two_centroid_blocks(gpu):
-    """k > 32: the MFMA assignment scores two 32-centroid blocks per row tile."""
-    from otto_recommender_amd import popularity as gp
+    """k > 32 (two 32-centroid blocks in the MFMA variant, 56 padded columns in the VALU one)."""
     rng = np.random.default_rng(5)
     centers = rng.normal(scale=3, size=(50, 100))
     X = (centers[rng.integers(0, 50, 12000)] + rng.normal(size=(12000, 100))).astype(np.float32)
-    km = gp.KMeans(n_clusters=45, max_iter=100, tol=1e-3, random_state=42).fit(X)
-    lab_ref, C_ref, it_ref = oracle_pop.kmeans(X, 45)
-    assert np.mean(km.labels_.cpu().numpy() == lab_ref) >= 0.999
-    np.testing.assert_allclose(km.cluster_centers_.cpu().numpy(), C_ref, atol=1e-3)
-    assert abs(km.n_iter_ - it_ref) <= 2
+    _check_kmeans(X, 45, n_init=2)
 
 
 def test_popularity_ranks_exact(gpu):
