@@ -1092,52 +1092,41 @@ __global__ __launch_bounds__(256) void k_agg_sort(const Task* __restrict__ tasks
     const uint32_t len = T.len;
     wave_bitonic_sort<M>(v);
     const uint32_t pl = lane_prev(v[M - 1]), nl = lane_next(v[0]);
-    // (1) per-file count cf: start of the element's w-run by a max scan
+    // (1) run flags from the neighbours (a w-run = one word = one (rule, aid_next, file)):
+    //     X = [w-run end] | [singleton w-run] << 11, summed by one scan (fields <= 1024)
     uint32_t a[M], b[M], c[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       const uint32_t e = l * M + m;
-      const uint32_t prv = m > 0 ? v[m - 1] : pl;
-      a[m] = (e < len && (e == 0 || prv != v[m])) ? e + 1 : 0u;
+      const uint32_t prv = m > 0 ? v[m - 1] : pl, nxt = m < M - 1 ? v[m + 1] : nl;
+      const bool valid = e < len;
+      const bool ws = valid && (e == 0 || prv != v[m]);
+      const bool we = valid && (e + 1 == len || nxt != v[m]);
+      c[m] = (we ? 1u : 0u) | ((ws && we) ? (1u << 11) : 0u);
+      b[m] = c[m];
     }
-    wave_scan_elems<M, true>(a);
-    // (2) X = cf | cf_ge2 << 16 and Y = 1 | ge2 << 16 at each w-run end
+    wave_scan_elems<M, false>(b);
+    // (2) at each k-run (rule, aid_next) start: its exclusive X << 10 | position, carried to the
+    //     k-run's end by one max scan (strictly increasing over the starts)
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       const uint32_t e = l * M + m;
-      const uint32_t nxt = m < M - 1 ? v[m + 1] : nl;
-      const bool wend = e < len && (e + 1 == len || nxt != v[m]);
-      const uint32_t cf = e + 2 - a[m];
-      b[m] = wend ? (cf | ((cf >= 2 ? cf : 0u) << 16)) : 0u;
-      c[m] = wend ? (1u | ((cf >= 2 ? 1u : 0u) << 16)) : 0u;
-    }
-    // (3) k-run sums: inclusive prefix minus the prefix before the k-run's start (max scan)
-    wave_scan_elems<M, false>(b);
-    {
-      const uint32_t lprev = lane_prev(b[M - 1]);
-#pragma unroll
-      for (int m = 0; m < M; ++m) {
-        const uint32_t e = l * M + m;
-        const uint32_t prv = m > 0 ? v[m - 1] : pl;
-        a[m] = (e < len && (e == 0 || (prv >> F) != (v[m] >> F))) ? excl_at<M>(b, m, lprev) : 0u;
-      }
+      const uint32_t prv = m > 0 ? v[m - 1] : pl;
+      const bool ks = e < len && (e == 0 || (prv >> F) != (v[m] >> F));
+      a[m] = ks ? (((b[m] - c[m]) << 10) | e) : 0u;
     }
     wave_scan_elems<M, true>(a);
+    // (3) at k-run ends: count = its words, S = its files with one word, nf1 = its files;
+    //     count_ge2 = count - S, nf2 = nf1 - S. b = count | count_ge2 << 16, c = nf1 | nf2 << 16
 #pragma unroll
-    for (int m = 0; m < M; ++m) b[m] -= a[m];
-    wave_scan_elems<M, false>(c);
-    {
-      const uint32_t lprev = lane_prev(c[M - 1]);
-#pragma unroll
-      for (int m = 0; m < M; ++m) {
-        const uint32_t e = l * M + m;
-        const uint32_t prv = m > 0 ? v[m - 1] : pl;
-        a[m] = (e < len && (e == 0 || (prv >> F) != (v[m] >> F))) ? excl_at<M>(c, m, lprev) : 0u;
-      }
+    for (int m = 0; m < M; ++m) {
+      const uint32_t e = l * M + m;
+      const uint32_t d = b[m] - (a[m] >> 10);
+      const uint32_t nf1 = d & 2047u, s1 = (d >> 11) & 2047u;
+      const uint32_t cnt = e + 1 - (a[m] & 1023u);
+      b[m] = cnt | ((cnt - s1) << 16);
+      c[m] = nf1 | ((nf1 - s1) << 16);
     }
-    wave_scan_elems<M, true>(a);
-#pragma unroll
-    for (int m = 0; m < M; ++m) c[m] -= a[m];
     // (4) one output row per k-run end, written into the task's own word range
     const int type = (int)(rk >> A);
     const int32_t aid = (int32_t)(rk & ((1u << A) - 1u));
