@@ -195,14 +195,45 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
     kbits = Lt.A + 2 + bits_for((uint64_t)n_parts + 1);
     if (kbits > 32) { set_error("row key with owner bits > 32 bits"); return OTTOHIP_ELIMIT; }
   }
+  const uint32_t kmask = Lt.A + 2 >= 32 ? ~0u : (1u << (Lt.A + 2)) - 1u;
+  // fused layout: counts ride in the keys' spare bits, one u64 scan carries word offset and row index
+  static const bool rows_legacy = getenv("OTTOHIP_ROWS") && !strcmp(getenv("OTTOHIP_ROWS"), "legacy");
+  const int cshift = (Lt.A + 2 + 7) / 8 * 8;  // first byte above the sorted key bits
+  const bool fused = !rows_legacy && n_parts == 1 && cshift + 8 <= 32 &&
+                     3ull * (uint64_t)params->n_items < (1ull << 24);
+  if (fused) k_key_cnt<<<grid_for(E), 256, 0, s>>>(rk, F.cnt, E, cshift);
   uint32_t *rks = rk, *poss = pos;
   OH_TRY(radix_sort_pairs(ctx, rks, poss, rk2, pos2, E, kbits, s));
+  uint64_t* tot;
+  OH_TRY(ws.get("tot", 4, &tot));
+  if (fused) {
+    const int64_t nb = ceil_div(E, RT_TILE);
+    uint64_t *bsum, *boff;
+    OH_TRY(ws.get("rt_sums", (size_t)nb, &bsum));
+    OH_TRY(ws.get("rt_offs", (size_t)nb, &boff));
+    k_rows_sums<<<(unsigned)nb, RT_T, 0, s>>>(rks, poss, F.cnt, E, kmask, INV, cshift, bsum);
+    OH_TRY(exclusive_scan_u64(ctx, bsum, boff, nb, tot, s));
+    uint64_t X = 0;
+    OH_TRY(d2h(&X, tot, 1, s));
+    int herr = 0;
+    OH_TRY(d2h(&herr, err, 1, s));
+    if (herr) { set_error("input out of range: aid outside [0, n_items) or type outside {0,1,2}"); return OTTOHIP_ERANGE; }
+    F.P = X >> 24;
+    F.Rn = (int64_t)(X & 0xFFFFFFull);
+    OH_TRY(ws.get("poff", (size_t)E, &F.poff));
+    OH_TRY(ws.get("row_key", (size_t)std::max<int64_t>(F.Rn, 1), &F.row_key));
+    OH_TRY(ws.get("row_begin", (size_t)std::max<int64_t>(F.Rn, 1), &F.row_begin));
+    k_rows_tile<<<(unsigned)nb, RT_T, 0, s>>>(rks, poss, F.cnt, E, kmask, INV, cshift, boff, F.poff, F.row_key,
+                                              F.row_begin);
+    OH_HIP(hipGetLastError());
+    ctx->end(ph, s);
+    return 0;
+  }
   uint32_t *c_sorted = (rks == rk) ? rk2 : rk, *row_flag = (poss == pos) ? pos2 : pos;  // reuse the idle pair
   k_gather_counts<<<grid_for(E), 256, 0, s>>>(rks, poss, F.cnt, E, INV, c_sorted, row_flag);
-  uint64_t *woff, *row_idx, *tot;
+  uint64_t *woff, *row_idx;
   OH_TRY(ws.get("woff", (size_t)E, &woff));
   OH_TRY(ws.get("row_idx", (size_t)E, &row_idx));
-  OH_TRY(ws.get("tot", 4, &tot));
   OH_TRY(exclusive_scan_u32(ctx, c_sorted, woff, E, tot, s));
   OH_TRY(exclusive_scan_u32(ctx, row_flag, row_idx, E, tot + 1, s));
   uint64_t PR[2];
@@ -215,8 +246,8 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
   OH_TRY(ws.get("poff", (size_t)E, &F.poff));
   OH_TRY(ws.get("row_key", (size_t)std::max<int64_t>(F.Rn, 1), &F.row_key));
   OH_TRY(ws.get("row_begin", (size_t)std::max<int64_t>(F.Rn, 1), &F.row_begin));
-  k_rows<<<grid_for(E), 256, 0, s>>>(rks, poss, E, INV, Lt.A + 2 >= 32 ? ~0u : (1u << (Lt.A + 2)) - 1u, woff, row_flag, row_idx, F.poff,
-                                     F.row_key, F.row_begin);
+  k_rows<<<grid_for(E), 256, 0, s>>>(rks, poss, E, INV, kmask, woff, row_flag, row_idx, F.poff, F.row_key,
+                                     F.row_begin);
   ctx->end(ph, s);
   return 0;
 }

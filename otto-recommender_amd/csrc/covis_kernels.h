@@ -495,6 +495,90 @@ __global__ void k_rows(const uint32_t* __restrict__ rk, const uint32_t* __restri
   }
 }
 
+// ---- fused row layout (one GPU, rows < 2^24, A <= 21): the event's pair count rides in the
+// row key's spare high bits through the radix sort (saturated at RK_CSAT: larger counts, from
+// long sessions, are gathered), then one pass of block sums and one pass of per-block scans
+// give every event its word offset and every row its key and first word, with X = cnt << 24 |
+// [row start] scanned as one u64: no c_sorted / row_flag arrays, no second scan, no gather.
+constexpr uint32_t RK_CSAT = 255u;  // the key byte above the sorted digits (LSD passes sort whole bytes)
+constexpr int RT_T = 256, RT_I = 8, RT_TILE = RT_T * RT_I;
+
+__global__ void k_key_cnt(uint32_t* __restrict__ rk, const uint32_t* __restrict__ cnt, int64_t n, int shift) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t c = cnt[i];
+  rk[i] |= (c < RK_CSAT ? c : RK_CSAT) << shift;
+}
+
+__device__ __forceinline__ uint64_t rows_x(const uint32_t* __restrict__ rks, const uint32_t* __restrict__ poss,
+                                           const uint32_t* __restrict__ cnt, int64_t k, uint32_t kmask, uint32_t INV,
+                                           int shift, uint32_t& key, bool& start) {
+  const uint32_t kk = rks[k];
+  key = kk & kmask;
+  if (key == INV) { start = false; return 0; }
+  start = k == 0 || (rks[k - 1] & kmask) != key;
+  uint32_t c = kk >> shift;
+  if (c == RK_CSAT) c = cnt[poss[k]];
+  return ((uint64_t)c << 24) | (start ? 1u : 0u);
+}
+
+__global__ __launch_bounds__(RT_T) void k_rows_sums(const uint32_t* __restrict__ rks, const uint32_t* __restrict__ poss,
+                                                    const uint32_t* __restrict__ cnt, int64_t n, uint32_t kmask,
+                                                    uint32_t INV, int shift, uint64_t* __restrict__ sums) {
+  const int64_t base = (int64_t)blockIdx.x * RT_TILE + (int64_t)threadIdx.x * RT_I;
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < RT_I; ++i) {
+    if (base + i >= n) break;
+    uint32_t key;
+    bool st;
+    s += rows_x(rks, poss, cnt, base + i, kmask, INV, shift, key, st);
+  }
+  __shared__ uint64_t ws[RT_T / 64];
+  s = wave_sum64(s);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) sums[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ __launch_bounds__(RT_T) void k_rows_tile(const uint32_t* __restrict__ rks, const uint32_t* __restrict__ poss,
+                                                    const uint32_t* __restrict__ cnt, int64_t n, uint32_t kmask,
+                                                    uint32_t INV, int shift, const uint64_t* __restrict__ offs,
+                                                    uint64_t* __restrict__ poff, uint32_t* __restrict__ row_key,
+                                                    uint64_t* __restrict__ row_begin) {
+  const int64_t base = (int64_t)blockIdx.x * RT_TILE + (int64_t)threadIdx.x * RT_I;
+  uint64_t x[RT_I];
+  uint32_t key[RT_I];
+  bool st[RT_I];
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < RT_I; ++i) {
+    x[i] = 0; key[i] = INV; st[i] = false;
+    if (base + i < n) x[i] = rows_x(rks, poss, cnt, base + i, kmask, INV, shift, key[i], st[i]);
+    s += x[i];
+  }
+  __shared__ uint64_t ws[RT_T / 64];
+  const uint64_t incl = wave_incl_scan64(s);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) ws[w] = incl;
+  __syncthreads();
+  uint64_t run = offs[blockIdx.x] + incl - s;
+  for (int k = 0; k < w; ++k) run += ws[k];
+#pragma unroll
+  for (int i = 0; i < RT_I; ++i) {
+    if (key[i] != INV) {
+      const uint64_t woff = run >> 24;
+      poff[poss[base + i]] = woff;
+      if (st[i]) {
+        const uint64_t r = run & 0xFFFFFFull;
+        row_key[r] = key[i];
+        row_begin[r] = woff;
+      }
+    }
+    run += x[i];
+  }
+}
+
 // multi-GPU layout: row keys become (owner(aid), type, aid) so every owner's rows and words
 // are contiguous (the all-to-all send segments); invalid events sort after every owner
 __global__ void k_owner_key(uint32_t* __restrict__ rk, int64_t n, uint32_t INV, int A, uint32_t G, uint32_t INV2) {
