@@ -136,6 +136,12 @@ int ottohip_concat_tables(ottohip_ctx* ctx, int n_tables, const int32_t* const* 
                           const uint32_t* const* count, const int64_t* n_rows, int32_t n_items,
                           const ottohip_merge_params* mp, int64_t optim_rows, int loaded_from_cache,
                           int32_t* out_aid, int32_t* out_aid_next, int32_t* out_count, int64_t* n_out, void* stream);
+/* Order-independent digest of one rule's rows, for full-size parity checks (out HOST [5], u64
+ * wrapping sums over rows): sum mix(key, 1) * count, sum mix(key, 2) * count_ge2, sum count,
+ * sum count_ge2, rows; key = rule << 48 | aid << 24 | aid_next, mix = the splitmix64 finaliser of
+ * key ^ seed. The CPU oracle computes the first four from per-file tables without a merge
+ * (they are linear over files: oracle/covis_oracle.c oracle_count_files_omp). */
+int ottohip_table_digest(ottohip_ctx* ctx, const ottohip_table* t, int rule, uint64_t* out, void* stream);
 /* Histogram of (x[i] >> shift) & mask over i in [lo, hi) of a device array whose equal keys are
  * contiguous (e.g. the count column of a finalize output, or its aid column inside one count):
  * hist (device, n_bins u64) is overwritten. The sharded finalize all-reduces these to find the

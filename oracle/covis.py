@@ -204,6 +204,31 @@ def merge_train_test(name: str, train_parts: list, test_parts: list, train_mode:
     return concat_files_w_stats(name, [t, s], part_mode="rows", **kw)
 
 
+def files_digest(offsets, aid, ts, type_, file_bounds, threads: int = 0, rules=REFERENCE_RULES) -> dict:
+    """Per rule, the linear checksums of every file's table (oracle_count_files_omp): equal to
+    ottohip_table_digest of the cross-file merged table (count / count_ge2) without a merge.
+    {name: {d_count, d_count_ge2, pairs, pairs_ge2, file_rows, file_rows_ge2}}."""
+    lib = _lib()
+    names, this, mask, wmax = _rule_arrays(rules)
+    f = lib.oracle_count_files_omp
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_int64] + [ctypes.c_void_p] * 5 + [ctypes.c_int] + [ctypes.c_void_p] * 3 + [
+        ctypes.c_int32, ctypes.c_int32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    off = np.ascontiguousarray(offsets, np.int64)
+    fb = np.ascontiguousarray(file_bounds, np.int64)
+    aid = np.ascontiguousarray(aid, np.int32); ts = np.ascontiguousarray(ts, np.int32)
+    type_ = np.ascontiguousarray(type_, np.int8)
+    tot = np.zeros(2 * len(names), np.int64)
+    dig = np.zeros(6 * len(names), np.uint64)
+    rc = f(len(fb) - 1, fb.ctypes.data, off.ctypes.data, aid.ctypes.data, ts.ctypes.data, type_.ctypes.data,
+           len(names), this.ctypes.data, mask.ctypes.data, wmax.ctypes.data, MIN_TIME_TO_NEXT, MAX_TIME_TO_NEXT,
+           int(threads or os.cpu_count() or 1), tot.ctypes.data, dig.ctypes.data)
+    if rc:
+        raise RuntimeError(f"oracle_count_files_omp failed ({rc})")
+    keys = ["d_count", "d_count_ge2", "pairs", "pairs_ge2", "file_rows", "file_rows_ge2"]
+    return {n: {k: int(dig[r * 6 + i]) for i, k in enumerate(keys)} for r, n in enumerate(names)}
+
+
 def canonical_digest(tables: dict) -> dict:
     """sha256 of the canonical (rule, aid, aid_next, count) stream, plus rows and Σcount."""
     import hashlib

@@ -180,12 +180,26 @@ int oracle_pair_stats(int64_t n_sessions, const int64_t* offsets, int64_t* join_
  * over n_threads OpenMP threads (one file per thread at a time, dynamic schedule). Each file is
  * counted exactly like oracle_count_co_events and its tables are built, then released;
  * totals[r * 2 + 0] = sum of per-file rows, totals[r * 2 + 1] = qualifying pairs of rule r. */
+/* splitmix64 finaliser of (rule << 48 | aid << 24 | aid_next) ^ seed: the row hash of the
+ * order-independent table digests (same function as ottohip_table_digest) */
+static uint64_t row_mix(uint64_t rule, uint32_t a, uint32_t b, uint64_t seed) {
+  uint64_t x = ((rule << 48) | ((uint64_t)a << 24) | (uint64_t)b) ^ seed;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+/* digest (optional, [n_rules][6] u64, wrapping sums): per rule over every file's table rows
+ *   sum mix(key, 1) * c, sum mix(key, 2) * c * [c >= 2], sum c, sum c * [c >= 2], rows, rows with c >= 2
+ * -- all linear over files, so they equal the same sums over the cross-file merged table with
+ * count = sum_f c_f and count_ge2 = sum_f c_f [c_f >= 2] (the build's table) without a merge. */
 int oracle_count_files_omp(int64_t n_files, const int64_t* file_session_bounds, const int64_t* offsets,
                            const int32_t* aid, const int32_t* ts, const int8_t* type, int n_rules,
                            const int32_t* this_type, const uint32_t* next_mask, const int32_t* max_abs_dt,
-                           int32_t min_dt, int32_t max_dt, int n_threads, int64_t* totals) {
+                           int32_t min_dt, int32_t max_dt, int n_threads, int64_t* totals, uint64_t* digest) {
   if (n_rules < 1 || n_rules > 16) return -1;
   memset(totals, 0, (size_t)n_rules * 2 * sizeof(int64_t));
+  if (digest) memset(digest, 0, (size_t)n_rules * 6 * sizeof(uint64_t));
   int rc = 0;
 #pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads)
   for (int64_t f = 0; f < n_files; ++f) {
@@ -196,11 +210,25 @@ int oracle_count_files_omp(int64_t n_files, const int64_t* file_session_bounds, 
                                     next_mask, max_abs_dt, min_dt, max_dt, t);
     for (int r = 0; r < n_rules; ++r) {
       int64_t pairs = 0;
-      for (int64_t i = 0; r0 == 0 && i < t[r].n; ++i) pairs += t[r].count[i];
+      uint64_t d[6] = {0, 0, 0, 0, 0, 0};
+      for (int64_t i = 0; r0 == 0 && i < t[r].n; ++i) {
+        const uint64_t c = t[r].count[i];
+        pairs += (int64_t)c;
+        if (digest) {
+          const uint64_t g = c >= 2 ? c : 0;
+          d[0] += row_mix((uint64_t)r, (uint32_t)t[r].aid[i], (uint32_t)t[r].aid_next[i], 1) * c;
+          d[1] += row_mix((uint64_t)r, (uint32_t)t[r].aid[i], (uint32_t)t[r].aid_next[i], 2) * g;
+          d[2] += c; d[3] += g; d[4] += 1; d[5] += g ? 1 : 0;
+        }
+      }
 #pragma omp atomic
       totals[r * 2] += t[r].n;
 #pragma omp atomic
       totals[r * 2 + 1] += pairs;
+      for (int k = 0; digest && k < 6; ++k) {
+#pragma omp atomic
+        digest[r * 6 + k] += d[k];
+      }
       oracle_free_table(&t[r]);
     }
     if (r0) {

@@ -58,13 +58,13 @@ def port(n_files: int, threads: int, seed: int) -> dict:
     f = lib.oracle_count_files_omp
     f.restype = ctypes.c_int
     f.argtypes = [ctypes.c_int64] + [ctypes.c_void_p] * 5 + [ctypes.c_int] + [ctypes.c_void_p] * 3 + [
-        ctypes.c_int32, ctypes.c_int32, ctypes.c_int, ctypes.c_void_p]
+        ctypes.c_int32, ctypes.c_int32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
     off = np.ascontiguousarray(ev.session_offsets, np.int64)
     fb = np.ascontiguousarray(fb, np.int64)
     t0 = time.perf_counter()
     rc = f(len(fb) - 1, fb.ctypes.data, off.ctypes.data, ev.aid.ctypes.data, ev.ts.ctypes.data, ev.type.ctypes.data,
            len(names), this.ctypes.data, mask.ctypes.data, wmax.ctypes.data, oracle.MIN_TIME_TO_NEXT,
-           oracle.MAX_TIME_TO_NEXT, threads, tot.ctypes.data)
+           oracle.MAX_TIME_TO_NEXT, threads, tot.ctypes.data, None)
     dt = time.perf_counter() - t0
     if rc:
         raise RuntimeError(f"oracle_count_files_omp failed ({rc})")

@@ -123,6 +123,14 @@ class CovisTable:
             a, b, c, c2 = a[o], b[o], c[o], c2[o]
         return a, b, c, c2
 
+    def digest(self, name, stream=None) -> dict:
+        """ottohip_table_digest: order-independent checksums of one rule's rows."""
+        out = (ctypes.c_uint64 * 5)()
+        _lib.check(_lib.load().ottohip_table_digest(self.ctx.h, self.h, self._rule(name), out,
+                                                    _lib.stream_handle(stream)))
+        return {"d_count": int(out[0]), "d_count_ge2": int(out[1]), "pairs": int(out[2]), "pairs_ge2": int(out[3]),
+                "rows": int(out[4])}
+
     def finalize(self, name, stream=None, max_rows=None, params: dict | None = None):
         """concat_files_w_stats' final step (:131-175) on the device for one rule:
         returns torch (aid, aid_next, count:int32) in (count desc, aid, aid_next) order.

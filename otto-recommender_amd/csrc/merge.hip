@@ -50,6 +50,35 @@ __global__ void k_run_hist(const int32_t* __restrict__ x, int64_t lo, int64_t hi
   if (i + 1 == hi || ((((uint32_t)x[i + 1]) >> shift) & mask) != k) atomicAdd(&hist[k], (unsigned long long)(i + 1));
 }
 
+// order-independent digest of one rule's rows (the oracle's per-file sums are linear, so they
+// equal these without a merge; oracle/covis_oracle.c row_mix is the same function)
+__device__ __forceinline__ uint64_t row_mix(uint64_t rule, uint32_t a, uint32_t b, uint64_t seed) {
+  uint64_t x = ((rule << 48) | ((uint64_t)a << 24) | (uint64_t)b) ^ seed;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_table_digest(const uint8_t* __restrict__ rule, const int32_t* __restrict__ aid,
+                                                      const int32_t* __restrict__ aid_next,
+                                                      const uint32_t* __restrict__ count,
+                                                      const uint32_t* __restrict__ count_ge2, int64_t n, int r,
+                                                      unsigned long long* __restrict__ out) {
+  uint64_t d[5] = {0, 0, 0, 0, 0};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (rule[i] != (uint8_t)r) continue;
+    const uint64_t c = count[i], g = count_ge2[i];
+    d[0] += row_mix((uint64_t)r, (uint32_t)aid[i], (uint32_t)aid_next[i], 1) * c;
+    d[1] += row_mix((uint64_t)r, (uint32_t)aid[i], (uint32_t)aid_next[i], 2) * g;
+    d[2] += c; d[3] += g; d[4] += 1;
+  }
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const uint64_t v = wave_sum64(d[k]);
+    if (lane_id() == 0 && v) atomicAdd(&out[k], (unsigned long long)v);
+  }
+}
+
 }  // namespace ottohip
 
 using namespace ottohip;
@@ -189,5 +218,20 @@ extern "C" int ottohip_run_hist(ottohip_ctx* ctx, const int32_t* x, int64_t lo, 
   int herr = 0;
   OH_TRY(d2h(&herr, err, 1, s));
   if (herr) { set_error("run_hist: key >= n_bins"); return OTTOHIP_ERANGE; }
+  return 0;
+}
+
+extern "C" int ottohip_table_digest(ottohip_ctx* ctx, const ottohip_table* t, int rule, uint64_t* out, void* stream) {
+  if (!ctx || !t || !out || rule < 0 || rule >= t->n_rules) { set_error("table_digest: bad arguments"); return OTTOHIP_EINVAL; }
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  unsigned long long* d;
+  OH_TRY(ctx->ws.get("digest", 5, &d));
+  OH_HIP(hipMemsetAsync(d, 0, 5 * 8, s));
+  if (t->n_slots > 0)
+    k_table_digest<<<(unsigned)std::min<int64_t>(ceil_div(t->n_slots, 256), (int64_t)ctx->n_cu * 8), 256, 0, s>>>(
+        t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, t->n_slots, rule, d);
+  OH_HIP(hipGetLastError());
+  OH_TRY(d2h(reinterpret_cast<unsigned long long*>(out), d, 5, s));
   return 0;
 }

@@ -266,3 +266,24 @@ def test_concat_files_w_stats_part_branch(gpu):
         np.testing.assert_array_equal(a, ra, err_msg=n)
         np.testing.assert_array_equal(b, rb, err_msg=n)
         np.testing.assert_array_equal(c, rc, err_msg=n)
+
+
+@pytest.mark.slow
+def test_full_220m_digest(gpu):
+    """BASELINE configs[1] at full size (220M events, 135 files of 100k sessions, all five rules):
+    per rule the order-independent checksums of the device table (sum of mix(key) x count and of
+    mix(key) x count_ge2, sum count, sum count_ge2) and its per-file row statistics against
+    tests/golden/digest_220m.json, computed by the C oracle from every file's table
+    (tests/golden/make_golden.py --full)."""
+    g = json.load(open(os.path.join(GOLD, "digest_220m.json")))
+    n_sess, n_ev = synth.sessions_for_events(220_000_000, 0, g["seed"])
+    assert (n_sess, n_ev) == (g["sessions"], g["events"])
+    ev = synth.generate(n_sess, 0, g["seed"])
+    tab = _gpu_tables(ev, synth.file_session_bounds(n_sess))
+    for n in NAMES:
+        d, st, ref = tab.digest(n), tab.stats(n), g["rules"][n]
+        for k in ("d_count", "d_count_ge2", "pairs", "pairs_ge2"):
+            assert d[k] == ref[k], (n, k)
+        assert st["n_pairs"] == ref["pairs"] and st["n_rows"] == d["rows"]
+        assert (st["file_rows"], st["file_rows_ge2"]) == (ref["file_rows"], ref["file_rows_ge2"]), n
+    tab.free()

@@ -75,3 +75,20 @@ def test_knn_rejects_out_of_range_rows(gpu):
         ix.search(np.array([0, 100]), k=5)
     with pytest.raises(L.OttoHipError):
         ix.search(None, n_q=101, k=5)
+
+
+@pytest.mark.slow
+def test_knn_full_size_config3(gpu):
+    """BASELINE configs[2] at full size: 1,855,603 items x 100, the first 600,000 rows as queries
+    (config.py:125), k = 20; 2,500 queries sampled over the whole query range (both ends included)
+    checked against the exact oracle."""
+    from otto_recommender_amd.w2vec import KnnIndex
+    emb = synth.embeddings(1_855_603)
+    ix = KnnIndex(emb)
+    i, d = ix.search(None, n_q=600_000, k=20)
+    rng = np.random.default_rng(11)
+    rows = np.unique(np.concatenate([[0, 1, 599_998, 599_999], rng.choice(600_000, 2_496, replace=False)]))
+    gi, gd = i[rows].cpu().numpy(), d[rows].cpu().numpy()
+    assert np.all(gi[:, 0] == rows) and np.all(gd[:, 0] == 0)
+    _check(emb, rows, 20, gi, gd)
+    ix.free()
