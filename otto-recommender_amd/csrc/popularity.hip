@@ -204,6 +204,12 @@ __device__ __forceinline__ uint32_t km_ord(float x) {  // order-preserving f32 -
 __device__ __forceinline__ float km_unord(uint32_t o) {
   return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
 }
+// x * 2^24 rounded to the nearest integer as int64: one f32 -> i32 conversion when |x| < 128
+// (the product is exact and below 2^31), the general f32 -> i64 sequence otherwise
+__device__ __forceinline__ long long km_fx(float x) {
+  const float y = x * 16777216.0f;
+  return fabsf(x) < 128.f ? (long long)__float2int_rn(y) : __float2ll_rn(y);
+}
 
 template <int NB>
 __global__ __launch_bounds__(KM_MT) void k_km_assign_mfma(const float* __restrict__ X, int64_t n, int dim, int nq,
@@ -211,7 +217,9 @@ __global__ __launch_bounds__(KM_MT) void k_km_assign_mfma(const float* __restric
                                                         int k, int32_t* __restrict__ label,
                                                         unsigned long long* __restrict__ sums,
                                                         unsigned long long* __restrict__ cnt,
-                                                        double* __restrict__ inertia) {
+                                                        double* __restrict__ inertia,
+                                                        unsigned long long* __restrict__ changed,
+                                                        float* __restrict__ dist) {
   extern __shared__ unsigned long long smem64[];
   float4* Bl = reinterpret_cast<float4*>(smem64);                              // [NB][nq][64]
   int32_t* labl = reinterpret_cast<int32_t*>(Bl + NB * nq * 64);                // [waves][32]
@@ -232,6 +240,7 @@ __global__ __launch_bounds__(KM_MT) void k_km_assign_mfma(const float* __restric
   __syncthreads();
   const float cA = cnl[i32], cB = cnl[32 + i32];
   double part = 0.0;
+  uint32_t nchg = 0;
   const int64_t ntile = (n + 31) >> 5;
   const int64_t nwv = (int64_t)gridDim.x * (KM_MT / 64);
   for (int64_t t = (int64_t)blockIdx.x * (KM_MT / 64) + wv; t < ntile; t += nwv) {
@@ -265,38 +274,51 @@ __global__ __launch_bounds__(KM_MT) void k_km_assign_mfma(const float* __restric
         }
       }
     }
-    // accumulator register r of lane (column i32, half h) holds row (r & 3) + 8 (r >> 2) + 4 h
-    uint32_t kv[16], ki[16];
+    // accumulator register r of lane (column i32, half h) holds row (r & 3) + 8 (r >> 2) + 4 h.
+    // Key = ordered score << 32 | cluster (ties to the lower cluster). The 16 rows x 32 columns
+    // are reduced by register halving: at each of the xor-16/8/4/2 steps a lane keeps half of its
+    // registers and takes the partner's minimum of the other half (8 + 4 + 2 + 1 exchanges), then
+    // one xor-1 step: lane l ends with the row of register ((l >> 1) & 15), paired with l ^ 1.
+    uint64_t kk[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      kv[r] = km_ord(cA - 2.f * acc0[r]);
-      ki[r] = (uint32_t)i32;
+      uint64_t a0 = ((uint64_t)km_ord(cA - 2.f * acc0[r]) << 32) | (uint32_t)i32;
       if (NB == 2) {
-        const uint32_t o = km_ord(cB - 2.f * acc1[r]);
-        if (o < kv[r]) { kv[r] = o; ki[r] = 32u + (uint32_t)i32; }
+        const uint64_t a1 = ((uint64_t)km_ord(cB - 2.f * acc1[r]) << 32) | (uint32_t)(32 + i32);
+        a0 = a1 < a0 ? a1 : a0;
       }
+      kk[r] = a0;
     }
 #pragma unroll
-    for (int sft = 1; sft < 32; sft <<= 1) {
+    for (int st = 0; st < 4; ++st) {
+      const int half = 8 >> st, J = 16 >> st;
+      const bool up = (l & J) != 0;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const uint32_t ov = xor_lane_n(kv[r], sft), oi = xor_lane_n(ki[r], sft);
-        const bool tk = ov < kv[r] || (ov == kv[r] && oi < ki[r]);
-        kv[r] = tk ? ov : kv[r];
-        ki[r] = tk ? oi : ki[r];
+      for (int j = 0; j < half; ++j) {
+        const uint64_t send = up ? kk[j] : kk[j + half];
+        const uint64_t keep = up ? kk[j + half] : kk[j];
+        const uint32_t rlo = xor_lane_n((uint32_t)send, J), rhi = xor_lane_n((uint32_t)(send >> 32), J);
+        const uint64_t recv = ((uint64_t)rhi << 32) | rlo;
+        kk[j] = recv < keep ? recv : keep;
       }
     }
-    uint32_t mv = kv[0], mi = ki[0];
-#pragma unroll
-    for (int r = 1; r < 16; ++r)
-      if (i32 == r) { mv = kv[r]; mi = ki[r]; }
-    const int R = (i32 & 3) + 8 * ((i32 >> 2) & 3) + 4 * h;  // lanes i32 < 16: the row of register i32
+    {
+      const uint32_t rlo = xor_lane<1>((uint32_t)kk[0]), rhi = xor_lane<1>((uint32_t)(kk[0] >> 32));
+      const uint64_t recv = ((uint64_t)rhi << 32) | rlo;
+      kk[0] = recv < kk[0] ? recv : kk[0];
+    }
+    const int rr = (l >> 1) & 15;
+    const int R = (rr & 3) + 8 * (rr >> 2) + 4 * h;
     const float xr = __shfl(xs, R);
-    if (i32 < 16) {
+    const uint32_t mi = (uint32_t)kk[0];
+    if ((l & 1) == 0) {
       labl[wv * 32 + R] = (int32_t)mi;
       if (r0 + R < n) {
+        if (changed) nchg += label[r0 + R] != (int32_t)mi;
         label[r0 + R] = (int32_t)mi;
-        part += (double)fmaxf(xr + km_unord(mv), 0.f);
+        const float dd = fmaxf(xr + km_unord((uint32_t)(kk[0] >> 32)), 0.f);
+        part += (double)dd;
+        if (dist) dist[r0 + R] = dd;
       }
     }
     if (sums) {  // the tile's rows, lanes over dimensions
@@ -318,8 +340,8 @@ __global__ __launch_bounds__(KM_MT) void k_km_assign_mfma(const float* __restric
         for (int q = 0; q < 8; ++q) {
           if (rr + q >= nr) break;
           unsigned long long* row = ls + cc[q] * dim;  // exact 2^24 scaling
-          if (l < dim) atomicAdd(&row[l], (unsigned long long)__float2ll_rn(xa[q] * 16777216.0f));
-          if (l + 64 < dim) atomicAdd(&row[l + 64], (unsigned long long)__float2ll_rn(xb[q] * 16777216.0f));
+          if (l < dim) atomicAdd(&row[l], (unsigned long long)km_fx(xa[q]));
+          if (l + 64 < dim) atomicAdd(&row[l + 64], (unsigned long long)km_fx(xb[q]));
           if (l == 0) atomicAdd(&lc[cc[q]], 1ull);
         }
       }
@@ -340,6 +362,10 @@ __global__ __launch_bounds__(KM_MT) void k_km_assign_mfma(const float* __restric
     part += __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
   }
   if (l == 0) atomicAdd(inertia, part);
+  if (changed) {
+    const uint32_t w = wave_sum(nchg);
+    if (l == 0 && w) atomicAdd(changed, (unsigned long long)w);
+  }
 }
 
 static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int64_t n, int dim, const float* C,
@@ -352,8 +378,8 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
   k_km_prep<<<grid_for(std::max<int64_t>((int64_t)KP * dim, KM_MAXK)), 256, 0, s>>>(C, k, dim, KP, Ct, cn);
   // the MFMA kernel measured 6.4 ms per Lloyd step at 12.9 M x 100, k = 50, against 5.1 ms for
   // the VALU kernel below (argmin butterflies and half the rows per wave): opt-in A/B switch only
-  static const bool km_mfma = getenv("OTTOHIP_KM_MFMA") != nullptr;
-  if (km_mfma && !changed && !dist && k <= 64 && dim <= 8 * KM_NQ && (dim & 3) == 0 && ((uintptr_t)X & 15) == 0 &&
+  static const bool km_valu = getenv("OTTOHIP_KM_VALU") != nullptr;  // A/B switch
+  if (!km_valu && k <= 64 && dim <= 8 * KM_NQ && (dim & 3) == 0 && ((uintptr_t)X & 15) == 0 &&
       ((uintptr_t)C & 15) == 0) {
     const int nq = (dim + 7) / 8, NB = k <= 32 ? 1 : 2;
     const size_t lds = (size_t)NB * nq * 64 * 16 + (KM_MT / 64) * 32 * 4 + 64 * 4 +
@@ -364,7 +390,7 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
     auto kern = NB == 1 ? k_km_assign_mfma<1> : k_km_assign_mfma<2>;
     OH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)lds));
-    kern<<<grid, KM_MT, lds, s>>>(X, n, dim, nq, C, cn, k, labels, sums, cnt, inr);
+    kern<<<grid, KM_MT, lds, s>>>(X, n, dim, nq, C, cn, k, labels, sums, cnt, inr, changed, dist);
     OH_HIP(hipGetLastError());
     return 0;
   }
