@@ -234,12 +234,27 @@ int ottohip_kmeans_partial(ottohip_ctx* ctx, const float* X, int64_t n, int dim,
                            void* stream);
 int ottohip_kmeans_update(ottohip_ctx* ctx, float* centroids, const int64_t* sums, const int64_t* counts, int k,
                           int dim, double* shift2, void* stream);
+/* partial + update of one GPU in a single call with one device->host copy (sklearn 1.2
+ * _kmeans_single_lloyd, model/kmeans_sessions.py:152-159): out (HOST double[4]) = inertia, changed
+ * labels, shift^2, empty clusters. When a cluster is empty the centroids are NOT updated (out[2] =
+ * -1): relocate, then update (sklearn relocates before the M-step). */
+int ottohip_kmeans_lloyd_iter(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* centroids, int k,
+                              int32_t* labels, int64_t* sums, int64_t* counts, double* out, void* stream);
 int ottohip_kmeans_farthest(ottohip_ctx* ctx, const float* X, int64_t n, int dim, const float* centroids,
                             const int32_t* labels, int m, int64_t* rows, float* d2, void* stream);
 int ottohip_kmeans_relocate(ottohip_ctx* ctx, int64_t* sums, int64_t* counts, int k, int dim, const float* vecs,
                             const int32_t* old_new, int m, void* stream);
 int ottohip_kmeans_inertia(ottohip_ctx* ctx, const float* X, int64_t n, int dim, const float* centroids,
                            const int32_t* labels, double* inertia, void* stream);
+/* sklearn KMeans(init='random') initial centres: numpy RandomState(seed) (legacy MT19937)
+ * replica. ottohip_rs_permutation_head(rs, n, k, out) == rs.permutation(n)[:k] (out HOST int64[k])
+ * and advances the stream exactly as numpy does, so successive calls give the n_init runs'
+ * seeds (model/kmeans_sessions.py:152-159 -> sklearn 1.2 _init_centroids). Host-only, thread-safe
+ * per handle; n < 2^32. */
+typedef struct ottohip_rs ottohip_rs;
+int ottohip_rs_create(uint32_t seed, ottohip_rs** out);
+int ottohip_rs_permutation_head(ottohip_rs* rs, int64_t n, int k, int64_t* out);
+void ottohip_rs_destroy(ottohip_rs* rs);
 /* column statistics and centering for KMeans.fit (sklearn subtracts the column mean before the
  * runs and scales tol by the mean column variance): sum_x[d] = sum x, sum_sq[d] = sum (x - center[d])^2
  * (center NULL = 0), both device int64 in 2^-24 fixed point (exact: shards all-reduce them); dim <= 128 */

@@ -87,6 +87,11 @@ SIGNATURES = {
                                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64), _VP]),
     "ottohip_kmeans_update": (ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_int, ctypes.c_int,
                                              ctypes.POINTER(ctypes.c_double), _VP]),
+    "ottohip_rs_create": (ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(_VP)]),
+    "ottohip_rs_permutation_head": (ctypes.c_int, [_VP, _I64, ctypes.c_int, _VP]),
+    "ottohip_rs_destroy": (None, [_VP]),
+    "ottohip_kmeans_lloyd_iter": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP, ctypes.c_int, _VP, _VP, _VP,
+                                                 ctypes.POINTER(ctypes.c_double), _VP]),
     "ottohip_kmeans_farthest": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP, _VP, ctypes.c_int, _VP, _VP, _VP]),
     "ottohip_kmeans_relocate": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int, ctypes.c_int, _VP, _VP, ctypes.c_int, _VP]),
     "ottohip_kmeans_inertia": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP, _VP, ctypes.POINTER(ctypes.c_double),

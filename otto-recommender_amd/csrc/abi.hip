@@ -1,7 +1,9 @@
 // Host orchestration of the co-visitation engine and the C-ABI of include/ottohip.h.
 #include <cstdarg>
 #include <cstdlib>
+#include <ctime>
 #include <algorithm>
+#include <mutex>
 #include "prims.h"
 #include "covis_kernels.h"
 #include "table.h"
@@ -20,6 +22,88 @@ void set_error(const char* fmt, ...) {
 
 namespace ottohip {
 Ctx* ctx_base(ottohip_ctx* c) { return c; }
+
+static bool alloc_log_on() {
+  static const bool on = getenv("OTTOHIP_ALLOC_LOG") != nullptr;
+  return on;
+}
+double alloc_log_begin() {
+  if (!alloc_log_on()) return 0.0;
+  timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+void alloc_log_end(double t0, const char* what, const char* name, size_t bytes) {
+  if (!alloc_log_on()) return;
+  timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  size_t fr = 0, tot = 0;
+  (void)hipMemGetInfo(&fr, &tot);
+  fprintf(stderr, "[ottohip alloc] %s %-14s %10.3f MB  %8.2f ms  free %.1f GB\n", what, name, bytes / 1e6,
+          1e3 * (t.tv_sec + 1e-9 * t.tv_nsec - t0), fr / 1e9);
+}
+
+// ---- device block cache (common.h)
+static std::mutex g_cache_mu;
+static std::multimap<size_t, void*> g_cache_free;  // size -> block
+static std::map<void*, size_t> g_cache_live;       // block -> size
+
+hipError_t dev_alloc(void** p, size_t bytes, const char* what) {
+  std::lock_guard<std::mutex> lk(g_cache_mu);
+  auto it = g_cache_free.lower_bound(bytes);
+  if (it != g_cache_free.end() && it->first <= 2 * bytes) {
+    *p = it->second;
+    g_cache_live[it->second] = it->first;
+    g_cache_free.erase(it);
+    return hipSuccess;
+  }
+  const double t0 = alloc_log_begin();
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess && !g_cache_free.empty()) {  // give the cached blocks back and retry once
+    (void)hipGetLastError();
+    (void)hipDeviceSynchronize();
+    for (auto& kv : g_cache_free) (void)hipFree(kv.second);
+    g_cache_free.clear();
+    e = hipMalloc(p, bytes);
+  }
+  alloc_log_end(t0, "hipMalloc", what, bytes);
+  if (e != hipSuccess) { (void)hipGetLastError(); *p = nullptr; return e; }
+  g_cache_live[*p] = bytes;
+  return hipSuccess;
+}
+
+// cached bytes are capped (OTTOHIP_CACHE_GB, default 128) so memory the library no longer uses
+// stays available to other allocators in the process (torch)
+static size_t cache_cap() {
+  static const size_t cap = (size_t)((getenv("OTTOHIP_CACHE_GB") ? atof(getenv("OTTOHIP_CACHE_GB")) : 128.0) * 1e9);
+  return cap;
+}
+
+void dev_free(void* p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_cache_mu);
+  auto it = g_cache_live.find(p);
+  if (it == g_cache_live.end()) { (void)hipFree(p); return; }
+  g_cache_free.emplace(it->second, p);
+  g_cache_live.erase(it);
+  size_t tot = 0;
+  for (auto& kv : g_cache_free) tot += kv.first;
+  while (tot > cache_cap() && !g_cache_free.empty()) {  // largest blocks go back first
+    auto last = std::prev(g_cache_free.end());
+    tot -= last->first;
+    (void)hipDeviceSynchronize();
+    (void)hipFree(last->second);
+    g_cache_free.erase(last);
+  }
+}
+
+void dev_trim() {
+  std::lock_guard<std::mutex> lk(g_cache_mu);
+  if (g_cache_free.empty()) return;
+  (void)hipDeviceSynchronize();
+  for (auto& kv : g_cache_free) (void)hipFree(kv.second);
+  g_cache_free.clear();
+}
 }
 
 
@@ -285,9 +369,11 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     T->b = ctx->spare;
     ctx->spare = TableBufs();
   } else {
+    const double t0 = alloc_log_begin();
     (void)hipDeviceSynchronize();
     ctx->spare.release();
     OH_TRY(T->b.alloc(P));
+    alloc_log_end(t0, "table", "slots", (size_t)P * 17);
   }
   unsigned long long *stats, *lcount;
   OH_TRY(ws.get("stats", (size_t)STAT_STRIPES * STAT_STRIDE, &stats));
@@ -441,6 +527,7 @@ void ottohip_ctx_destroy(ottohip_ctx* ctx) {
   hipDeviceSynchronize();
   ctx->ws.release();
   ctx->spare.release();
+  dev_trim();
   for (auto e : ctx->event_pool) hipEventDestroy(e);
   if (ctx->pinned) hipHostFree(ctx->pinned);
   delete ctx;
@@ -452,6 +539,7 @@ int ottohip_ctx_trim(ottohip_ctx* ctx) {
   OH_HIP(hipDeviceSynchronize());
   ctx->ws.release();
   ctx->spare.release();
+  dev_trim();
   return 0;
 }
 

@@ -511,10 +511,10 @@ struct ottohip_candidates {
   int16_t* ord = nullptr;
   uint16_t* flags = nullptr;
   void release() {
-    if (off) (void)hipFree(off);
-    if (next) (void)hipFree(next);
-    if (ord) (void)hipFree(ord);
-    if (flags) (void)hipFree(flags);
+    dev_free(off);
+    dev_free(next);
+    dev_free(ord);
+    dev_free(flags);
     off = nullptr; next = nullptr; ord = nullptr; flags = nullptr;
   }
 };
@@ -540,7 +540,7 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
   C->n_sessions = n_sessions;
   auto fail = [&](int rc) { C->release(); delete C; return rc; };
   const int64_t Sn = n_sessions;
-  if (hipMalloc(&C->off, (Sn + 1) * sizeof(uint64_t)) != hipSuccess) return fail(OTTOHIP_ENOMEM);
+  if (dev_alloc(reinterpret_cast<void**>(&C->off), (Sn + 1) * sizeof(uint64_t), "cand_off") != hipSuccess) return fail(OTTOHIP_ENOMEM);
   if (Sn == 0) {
     OH_HIP(hipMemsetAsync(C->off, 0, sizeof(uint64_t), s));
     *out = C;
@@ -630,10 +630,10 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
   if ((rc = d2h(&nc, tot, 1, s))) return fail(rc);
   C->n_cand = (int64_t)nc;
   const size_t cap = (size_t)std::max<uint64_t>(nc, 1);
-  if (hipMalloc(&C->next, cap * 4) || hipMalloc(&C->ord, cap * 2) || hipMalloc(&C->flags, cap * 2)) {
-    (void)hipGetLastError();
+  if (dev_alloc(reinterpret_cast<void**>(&C->next), cap * 4, "cand_next") ||
+      dev_alloc(reinterpret_cast<void**>(&C->ord), cap * 2, "cand_ord") ||
+      dev_alloc(reinterpret_cast<void**>(&C->flags), cap * 2, "cand_flags"))
     return fail(OTTOHIP_ENOMEM);
-  }
   k_cand_build<1024, W><<<(unsigned)ceil_div(Sn, W), 64 * W, 0, s>>>(session_offsets, nullptr, Sn, kept, n_kept,
                                                                        session_cl, M, 1, n_cand, C->off, C->next,
                                                                        C->ord, C->flags, ovf, n_ovf, dbg);

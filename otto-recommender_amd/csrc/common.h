@@ -34,6 +34,19 @@ Ctx* ctx_base(ottohip_ctx* c);  // abi.hip
     if (rc_ != 0) return rc_;        \
   } while (0)
 
+// OTTOHIP_ALLOC_LOG=1: every device (re)allocation with its host-side duration on stderr
+double alloc_log_begin();
+void alloc_log_end(double t0, const char* what, const char* name, size_t bytes);
+
+// Device block cache of the library (abi.hip): freed blocks are kept and handed out again
+// (best fit within 2x of the request), so repeated calls do not go back to hipMalloc / hipFree,
+// whose cost at 100+ GB resident is erratic (0.5-2 s stalls measured on the box). Blocks are
+// reused in stream order: the library issues a call's work on one stream. dev_trim() returns
+// every cached block to the driver (ottohip_ctx_trim / ottohip_ctx_destroy).
+hipError_t dev_alloc(void** p, size_t bytes, const char* what);
+void dev_free(void* p);
+void dev_trim();
+
 // Named, grow-only device buffers owned by a context (no allocation inside launches).
 struct Workspace {
   struct Buf { void* p = nullptr; size_t bytes = 0; };
@@ -41,9 +54,9 @@ struct Workspace {
   int get(const char* name, size_t bytes, void** out) {
     Buf& b = bufs[name];
     if (b.bytes < bytes) {
-      if (b.p) { (void)hipDeviceSynchronize(); (void)hipFree(b.p); b.p = nullptr; b.bytes = 0; }
+      if (b.p) { (void)hipDeviceSynchronize(); dev_free(b.p); b.p = nullptr; b.bytes = 0; }
       size_t want = bytes < 256 ? 256 : bytes;
-      hipError_t e = hipMalloc(&b.p, want);
+      hipError_t e = dev_alloc(&b.p, want, name);
       if (e != hipSuccess) {
         set_error("workspace '%s': hipMalloc(%zu) failed: %s", name, want, hipGetErrorString(e));
         return OTTOHIP_ENOMEM;
@@ -57,7 +70,7 @@ struct Workspace {
     return get(name, n * sizeof(T), reinterpret_cast<void**>(out));
   }
   void release() {
-    for (auto& kv : bufs) if (kv.second.p) hipFree(kv.second.p);
+    for (auto& kv : bufs) if (kv.second.p) dev_free(kv.second.p);
     bufs.clear();
   }
 };

@@ -299,7 +299,7 @@ int ottohip_knn_index_create(ottohip_ctx* c, const float* emb, int64_t n_items, 
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   ottohip_knn_index* ix = new ottohip_knn_index();
   ix->device = ctx->device; ix->n_items = n_items; ix->dim = dim; ix->emb = emb;
-  if (hipMalloc(&ix->packed, (size_t)n_items * KN_KD * 2) != hipSuccess) {
+  if (dev_alloc(reinterpret_cast<void**>(&ix->packed), (size_t)n_items * KN_KD * 2, "knn_packed") != hipSuccess) {
     delete ix; set_error("knn_index_create: allocation failed"); return OTTOHIP_ENOMEM;
   }
   k_knn_pack<<<(unsigned)ceil_div(n_items * 64, 256), 256, 0, s>>>(emb, n_items, dim, nullptr, n_items, 0, ix->packed,
@@ -313,7 +313,7 @@ void ottohip_knn_index_free(ottohip_knn_index* ix) {
   if (!ix) return;
   (void)hipSetDevice(ix->device);
   (void)hipDeviceSynchronize();
-  (void)hipFree(ix->packed);
+  dev_free(ix->packed);
   delete ix;
 }
 

@@ -466,6 +466,47 @@ __global__ void k_km_relocate(unsigned long long* __restrict__ sums, unsigned lo
   }
 }
 
+// M-step on the device (one block): centroids = sums / counts for non-empty clusters, squared
+// centre shift reduced in a fixed order (deterministic), number of empty clusters. With
+// commit_if_full, a step that finds an empty cluster leaves the centroids untouched: the host
+// relocates (sklearn's order: relocation before the update) and calls the update again.
+// st: [0] shift^2 (double), [1] empty clusters (u64)
+constexpr int KM_UT = 256;
+__global__ __launch_bounds__(KM_UT) void k_km_update(float* __restrict__ C, const long long* __restrict__ sums,
+                                                     const long long* __restrict__ cnt, int k, int dim,
+                                                     int commit_if_full, double* __restrict__ st) {
+  __shared__ double red[KM_UT];
+  __shared__ int n_empty;
+  const int tid = threadIdx.x;
+  if (tid == 0) n_empty = 0;
+  __syncthreads();
+  for (int c = tid; c < k; c += KM_UT)
+    if (cnt[c] <= 0) atomicAdd(&n_empty, 1);
+  __syncthreads();
+  const int ne = n_empty;
+  const bool commit = !(commit_if_full && ne > 0);
+  double sh = 0.0;
+  if (commit)
+    for (int i = tid; i < k * dim; i += KM_UT) {
+      const int c = i / dim;
+      if (cnt[c] <= 0) continue;
+      const float nv = (float)((double)sums[i] / KM_FX / (double)cnt[c]);
+      const double df = (double)nv - (double)C[i];
+      sh += df * df;
+      C[i] = nv;
+    }
+  red[tid] = sh;
+  __syncthreads();
+  for (int o = KM_UT / 2; o >= 1; o >>= 1) {
+    if (tid < o) red[tid] += red[tid + o];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    st[0] = commit ? red[0] : -1.0;
+    reinterpret_cast<unsigned long long*>(st)[1] = (unsigned long long)ne;
+  }
+}
+
 // per column: sum of x and of (x - center)^2 in 2^-24 fixed point (exact, order-independent);
 // threads over columns, blocks over row chunks
 __global__ __launch_bounds__(128) void k_col_sums(const float* __restrict__ X, int64_t n, int dim,
@@ -612,6 +653,67 @@ __global__ __launch_bounds__(256) void k_sim(const int64_t* __restrict__ cand_of
   }
 }
 
+
+// ---------------------------------------------------------------- KMeans init seeds (host)
+// sklearn 1.2 KMeans(init='random') draws the initial centres of run r as
+// RandomState(random_state).permutation(n)[:k], the runs drawing successively from one stream
+// (model/kmeans_sessions.py:152-159 -> sklearn _init_centroids). numpy's legacy permutation is
+// arange(n) shuffled by Fisher-Yates from the top, j = random_interval(i) (mask-and-reject over
+// 32-bit MT19937 outputs). Only the first k positions are needed: the draws are stored, then the
+// swaps are replayed backwards from position p < k, so each of the k values is traced to its
+// origin with a bitmap of the traced positions instead of a random-access pass over n values.
+struct RsState {
+  uint32_t key[624];
+  int pos = 624;
+  std::vector<uint32_t> J;
+  std::vector<uint64_t> bits;
+};
+static void rs_seed(RsState& r, uint32_t seed) {
+  for (int p = 0; p < 624; ++p) {
+    r.key[p] = seed;
+    seed = 1812433253u * (seed ^ (seed >> 30)) + (uint32_t)p + 1u;
+  }
+  r.pos = 624;
+}
+static void rs_gen(RsState& r) {
+  constexpr int N = 624, M = 397;
+  constexpr uint32_t A = 0x9908b0dfu, U = 0x80000000u, L = 0x7fffffffu;
+  uint32_t* k = r.key;
+  int i = 0;
+  for (; i < N - M; ++i) {
+    const uint32_t y = (k[i] & U) | (k[i + 1] & L);
+    k[i] = k[i + M] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
+  }
+  for (; i < N - 1; ++i) {
+    const uint32_t y = (k[i] & U) | (k[i + 1] & L);
+    k[i] = k[i + (M - N)] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
+  }
+  const uint32_t y = (k[N - 1] & U) | (k[0] & L);
+  k[N - 1] = k[M - 1] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
+  r.pos = 0;
+}
+static inline uint32_t rs_next32(RsState& r) {
+  if (r.pos == 624) rs_gen(r);
+  uint32_t y = r.key[r.pos++];
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= y >> 18;
+  return y;
+}
+static inline uint32_t rs_interval(RsState& r, uint32_t mx) {  // numpy random_interval, max < 2^32
+  if (mx == 0) return 0;
+  uint32_t mask = mx;
+  mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+  uint32_t v;
+  while ((v = (rs_next32(r) & mask)) > mx) {}
+  return v;
+}
+}  // namespace ottohip
+
+struct ottohip_rs : public ottohip::RsState {};
+
+namespace ottohip {
 }  // namespace ottohip
 
 using namespace ottohip;
@@ -694,23 +796,19 @@ int ottohip_kmeans_partial(ottohip_ctx* ctx, const float* X, int64_t n, int dim,
   if (((size_t)k * dim + k) * 8 > 65536) { set_error("kmeans_partial: k * dim too large for LDS"); return OTTOHIP_ELIMIT; }
   hipStream_t s = S(stream);
   OH_HIP(hipSetDevice(ctx->device));
-  double* inr;
-  unsigned long long* chg;
-  OH_TRY(ctx->ws.get("km_inertia", 1, &inr));
-  OH_TRY(ctx->ws.get("km_changed", 1, &chg));
+  double* st;  // [inertia, changed]
+  OH_TRY(ctx->ws.get("km_stats", 4, &st));
+  unsigned long long* chg = reinterpret_cast<unsigned long long*>(st + 1);
   OH_HIP(hipMemsetAsync(sums, 0, (size_t)k * dim * 8, s));
   OH_HIP(hipMemsetAsync(counts, 0, (size_t)k * 8, s));
-  OH_HIP(hipMemsetAsync(inr, 0, 8, s));
-  OH_HIP(hipMemsetAsync(chg, 0, 8, s));
+  OH_HIP(hipMemsetAsync(st, 0, 2 * 8, s));
   if (n > 0)
     OH_TRY(launch_km_assign(ctx, k, s, X, n, dim, centroids, labels, reinterpret_cast<unsigned long long*>(sums),
-                            reinterpret_cast<unsigned long long*>(counts), inr, chg, nullptr));
-  double h = 0.0;
-  unsigned long long c = 0;
-  OH_TRY(d2h(&h, inr, 1, s));
-  OH_TRY(d2h(&c, chg, 1, s));
-  if (inertia) *inertia = h;
-  if (n_changed) *n_changed = (int64_t)c;
+                            reinterpret_cast<unsigned long long*>(counts), st, chg, nullptr));
+  double h[2] = {0.0, 0.0};
+  OH_TRY(d2h(h, st, 2, s));
+  if (inertia) *inertia = h[0];
+  if (n_changed) { unsigned long long c; memcpy(&c, &h[1], 8); *n_changed = (int64_t)c; }
   return 0;
 }
 
@@ -719,24 +817,51 @@ int ottohip_kmeans_update(ottohip_ctx* ctx, float* centroids, const int64_t* sum
                           int dim, double* shift2, void* stream) {
   if (!ctx || !centroids || !sums || !counts || k < 1 || dim < 1) { set_error("kmeans_update: bad arguments"); return OTTOHIP_EINVAL; }
   hipStream_t s = S(stream);
-  std::vector<long long> hs((size_t)k * dim), hc(k);
-  std::vector<float> hcen((size_t)k * dim);
-  OH_TRY(d2h(hs.data(), reinterpret_cast<const long long*>(sums), hs.size(), s));
-  OH_TRY(d2h(hc.data(), reinterpret_cast<const long long*>(counts), hc.size(), s));
-  OH_TRY(d2h(hcen.data(), centroids, hcen.size(), s));
-  double sh = 0.0;
-  for (int c = 0; c < k; ++c) {
-    if (hc[c] <= 0) continue;
-    for (int d = 0; d < dim; ++d) {
-      const float nv = (float)((double)hs[(size_t)c * dim + d] / KM_FX / (double)hc[c]);
-      const double df = (double)nv - (double)hcen[(size_t)c * dim + d];
-      sh += df * df;
-      hcen[(size_t)c * dim + d] = nv;
-    }
+  double* st;
+  OH_TRY(ctx->ws.get("km_ustats", 2, &st));
+  k_km_update<<<1, KM_UT, 0, s>>>(centroids, reinterpret_cast<const long long*>(sums),
+                                  reinterpret_cast<const long long*>(counts), k, dim, 0, st);
+  OH_HIP(hipGetLastError());
+  double h[2];
+  OH_TRY(d2h(h, st, 2, s));
+  if (shift2) *shift2 = h[0];
+  return 0;
+}
+
+// One whole Lloyd iteration on one GPU with a single device->host copy: E-step (labels, fixed-point
+// sums, counts, changed labels, inertia) and, unless a cluster came out empty, the M-step.
+// out[0] inertia, [1] changed labels, [2] shift^2 (-1: not updated), [3] empty clusters. With
+// out[3] > 0 the centroids are unchanged; sums / counts are ready for ottohip_kmeans_relocate and
+// ottohip_kmeans_update (sklearn 1.2 _kmeans_single_lloyd order).
+int ottohip_kmeans_lloyd_iter(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* centroids, int k,
+                              int32_t* labels, int64_t* sums, int64_t* counts, double* out, void* stream) {
+  if (!ctx || !X || !centroids || !labels || !sums || !counts || !out || n < 1 || dim < 1 || dim > EMB_MAXD ||
+      k < 1 || k > KM_MAXK) {
+    set_error("kmeans_lloyd_iter: bad arguments (k <= %d, dim <= %d)", KM_MAXK, EMB_MAXD); return OTTOHIP_EINVAL;
   }
-  OH_HIP(hipMemcpyAsync(centroids, hcen.data(), hcen.size() * sizeof(float), hipMemcpyHostToDevice, s));
-  OH_HIP(hipStreamSynchronize(s));
-  if (shift2) *shift2 = sh;
+  if (((size_t)k * dim + k) * 8 > 65536) { set_error("kmeans_lloyd_iter: k * dim too large for LDS"); return OTTOHIP_ELIMIT; }
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  double* st;  // [inertia, changed, shift, empty]
+  OH_TRY(ctx->ws.get("km_stats", 4, &st));
+  OH_HIP(hipMemsetAsync(sums, 0, (size_t)k * dim * 8, s));
+  OH_HIP(hipMemsetAsync(counts, 0, (size_t)k * 8, s));
+  OH_HIP(hipMemsetAsync(st, 0, 4 * 8, s));
+  OH_TRY(launch_km_assign(ctx, k, s, X, n, dim, centroids, labels, reinterpret_cast<unsigned long long*>(sums),
+                          reinterpret_cast<unsigned long long*>(counts), st,
+                          reinterpret_cast<unsigned long long*>(st + 1), nullptr));
+  k_km_update<<<1, KM_UT, 0, s>>>(centroids, reinterpret_cast<const long long*>(sums),
+                                  reinterpret_cast<const long long*>(counts), k, dim, 1, st + 2);
+  OH_HIP(hipGetLastError());
+  double h[4];
+  OH_TRY(d2h(h, st, 4, s));
+  unsigned long long c, e;
+  memcpy(&c, &h[1], 8);
+  memcpy(&e, &h[3], 8);
+  out[0] = h[0];
+  out[1] = (double)c;
+  out[2] = h[2];
+  out[3] = (double)e;
   return 0;
 }
 
@@ -919,7 +1044,7 @@ int ottohip_popularity_from_counts(ottohip_ctx* ctx, const uint32_t* cnt, int32_
   uint32_t *slot, *k0, *v0, *k1, *v1, *keep;
   uint16_t* rank;
   uint64_t *cl_first, *oidx;
-  auto fail = [&](int rc) { delete P; return rc; };
+  auto fail = [&](int rc) { dev_free(P->aid); dev_free(P->cl); dev_free(P->rank); delete P; return rc; };
   int rc;
   if ((rc = ws.get("pop_slot", (size_t)n, &slot)) || (rc = ws.get("pop_k0", (size_t)n, &k0)) ||
       (rc = ws.get("pop_v0", (size_t)n, &v0)) || (rc = ws.get("pop_k1", (size_t)n, &k1)) ||
@@ -948,11 +1073,10 @@ int ottohip_popularity_from_counts(ottohip_ctx* ctx, const uint32_t* cnt, int32_
   uint64_t nk = 0;
   if ((rc = d2h(&nk, tot + 1, 1, s))) return fail(rc);
   P->n = (int64_t)nk;
-  if (hipMalloc(&P->aid, std::max<uint64_t>(nk, 1) * 4) || hipMalloc(&P->cl, std::max<uint64_t>(nk, 1) * 4) ||
-      hipMalloc(&P->rank, std::max<uint64_t>(nk, 1) * 12)) {
-    (void)hipGetLastError();
+  if (dev_alloc(reinterpret_cast<void**>(&P->aid), std::max<uint64_t>(nk, 1) * 4, "pop_aid") ||
+      dev_alloc(reinterpret_cast<void**>(&P->cl), std::max<uint64_t>(nk, 1) * 4, "pop_cl") ||
+      dev_alloc(reinterpret_cast<void**>(&P->rank), std::max<uint64_t>(nk, 1) * 12, "pop_rank"))
     return fail(OTTOHIP_ENOMEM);
-  }
   k_pop_out<<<grid_for(n), 256, 0, s>>>(slot, rank, keep, oidx, n, n_items, P->aid, P->cl, P->rank);
   OH_HIP(hipGetLastError());
   ctx->end(ph, s);
@@ -991,9 +1115,9 @@ int ottohip_pop_copy(const ottohip_pop* p, int32_t* aid, int32_t* cl, int16_t* r
 void ottohip_pop_free(ottohip_pop* p) {
   if (!p) return;
   (void)hipDeviceSynchronize();
-  if (p->aid) (void)hipFree(p->aid);
-  if (p->cl) (void)hipFree(p->cl);
-  if (p->rank) (void)hipFree(p->rank);
+  dev_free(p->aid);
+  dev_free(p->cl);
+  dev_free(p->rank);
   delete p;
 }
 
@@ -1016,4 +1140,42 @@ int ottohip_session_item_similarity(ottohip_ctx* ctx, const int64_t* cand_off, i
   return 0;
 }
 
+
+int ottohip_rs_create(uint32_t seed, ottohip_rs** out) {
+  if (!out) { set_error("rs_create: out is NULL"); return OTTOHIP_EINVAL; }
+  ottohip_rs* r = new ottohip_rs();
+  rs_seed(*r, seed);
+  *out = r;
+  return 0;
+}
+
+void ottohip_rs_destroy(ottohip_rs* r) { delete r; }
+
+int ottohip_rs_permutation_head(ottohip_rs* r, int64_t n, int k, int64_t* out) {
+  if (!r || n < 0 || k < 0 || k > n || (k > 0 && !out)) { set_error("rs_permutation_head: bad arguments"); return OTTOHIP_EINVAL; }
+  if (n > (int64_t)0xFFFFFFFFll) { set_error("rs_permutation_head: n >= 2^32"); return OTTOHIP_ELIMIT; }
+  if (n <= 1) { for (int p = 0; p < k; ++p) out[p] = p; return 0; }
+  std::vector<uint32_t>& J = r->J;
+  J.resize((size_t)n);
+  for (int64_t i = n - 1; i >= 1; --i) J[(size_t)i] = rs_interval(*r, (uint32_t)i);  // the shuffle's draw order
+  std::vector<uint64_t>& B = r->bits;
+  B.assign((size_t)((n + 63) >> 6), 0ull);
+  std::vector<int64_t> ptr((size_t)k);
+  for (int p = 0; p < k; ++p) { ptr[(size_t)p] = p; B[(size_t)p >> 6] |= 1ull << (p & 63); }
+  auto test = [&](int64_t x) { return (B[(size_t)x >> 6] >> (x & 63)) & 1ull; };
+  auto flip = [&](int64_t x) { B[(size_t)x >> 6] ^= 1ull << (x & 63); };
+  for (int64_t i = 1; i < n; ++i) {  // swaps replayed last-to-first: value at i <-> value at J[i]
+    const int64_t j = J[(size_t)i];
+    if (j == i) continue;
+    const uint64_t bi = test(i), bj = test(j);
+    if (!(bi | bj)) continue;
+    for (int p = 0; p < k; ++p) {
+      if (ptr[(size_t)p] == i) ptr[(size_t)p] = j;
+      else if (ptr[(size_t)p] == j) ptr[(size_t)p] = i;
+    }
+    if (bi != bj) { flip(i); flip(j); }
+  }
+  for (int p = 0; p < k; ++p) out[p] = ptr[(size_t)p];
+  return 0;
+}
 }  // extern "C"

@@ -14,17 +14,19 @@ struct TableBufs {
   uint32_t* count = nullptr;
   uint32_t* count_ge2 = nullptr;
   void release() {
-    if (rule) (void)hipFree(rule);
-    if (aid) (void)hipFree(aid);
-    if (aid_next) (void)hipFree(aid_next);
-    if (count) (void)hipFree(count);
-    if (count_ge2) (void)hipFree(count_ge2);
+    dev_free(rule);
+    dev_free(aid);
+    dev_free(aid_next);
+    dev_free(count);
+    dev_free(count_ge2);
     *this = TableBufs();
   }
   int alloc(uint64_t n) {
-    if (hipMalloc(&rule, n) || hipMalloc(&aid, n * 4) || hipMalloc(&aid_next, n * 4) || hipMalloc(&count, n * 4) ||
-        hipMalloc(&count_ge2, n * 4)) {
-      (void)hipGetLastError();
+    if (dev_alloc(reinterpret_cast<void**>(&rule), n, "tab_rule") ||
+        dev_alloc(reinterpret_cast<void**>(&aid), n * 4, "tab_aid") ||
+        dev_alloc(reinterpret_cast<void**>(&aid_next), n * 4, "tab_aid_next") ||
+        dev_alloc(reinterpret_cast<void**>(&count), n * 4, "tab_count") ||
+        dev_alloc(reinterpret_cast<void**>(&count_ge2), n * 4, "tab_count_ge2")) {
       release();
       set_error("table allocation for %llu rows failed", (unsigned long long)n);
       return OTTOHIP_ENOMEM;

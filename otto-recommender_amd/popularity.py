@@ -66,6 +66,34 @@ def _allreduce(t, group):
     return _allreduce_sum(t, group)
 
 
+def _permutation_heads(seed: int, n: int, k: int, runs: int):
+    """numpy RandomState(seed).permutation(n)[:k] for `runs` successive calls (sklearn 1.2's
+    KMeans(init='random') seeds of its n_init runs), by the library's MT19937 replica
+    (ottohip_rs_permutation_head). The next run's draw is computed in a worker thread (ctypes
+    releases the GIL) while the current run iterates on the GPU."""
+    from concurrent.futures import ThreadPoolExecutor
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    _lib.check(lib.ottohip_rs_create(int(seed) & 0xFFFFFFFF, ctypes.byref(h)))
+
+    def draw():
+        out = np.empty(k, np.int64)
+        _lib.check(lib.ottohip_rs_permutation_head(h, int(n), int(k), out.ctypes.data))
+        return out
+
+    ex = ThreadPoolExecutor(1)
+    try:
+        fut = ex.submit(draw)
+        for r in range(runs):
+            cur = fut.result()
+            if r + 1 < runs:
+                fut = ex.submit(draw)
+            yield cur
+    finally:
+        ex.shutdown(wait=True)
+        lib.ottohip_rs_destroy(h)
+
+
 class KMeans:
     """KMeans(n_clusters, init='random', n_init='auto', max_iter=100, tol=1e-3, random_state=42):
     the reference's scikit-learn branch (model/kmeans_sessions.py:152-159, scikit-learn==1.2) on a
@@ -125,29 +153,42 @@ class KMeans:
         m1 = s1.cpu().numpy().astype(np.float64) / FX / n_all
         var = s2.cpu().numpy().astype(np.float64) / FX / n_all - m1 * m1
         tol_abs = float(np.mean(var)) * self.tol
-        rs = np.random.RandomState(self.random_state)
+        seed_stream = _permutation_heads(self.random_state, n_all, k, self.n_init)
         sums = torch.empty(k * dim, dtype=torch.int64, device=dev)
         counts = torch.empty(k, dtype=torch.int64, device=dev)
         labels = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
         best = None
         inr, chg, shift = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+        st4 = (ctypes.c_double * 4)()
         for run in range(self.n_init):
-            seeds = rs.permutation(n_all)[:k]
+            seeds = next(seed_stream)
             C = self._gather_rows(Xc, seeds, grows, group)
             labels.fill_(-1)
             strict, it = False, 0
             for it in range(1, self.max_iter + 1):
-                _lib.check(lib.ottohip_kmeans_partial(ctx.h, _lib.ptr(Xc), n, dim, _lib.ptr(C), k, _lib.ptr(labels),
-                                                      _lib.ptr(sums), _lib.ptr(counts), ctypes.byref(inr),
-                                                      ctypes.byref(chg), sh))
-                sums, counts = _allreduce(sums, group), _allreduce(counts, group)
-                n_changed = int(_allreduce(torch.tensor([chg.value], dtype=torch.int64), group).item())
-                cnt = counts.cpu().numpy()
-                empty = np.flatnonzero(cnt == 0)
-                if len(empty):
-                    self._relocate(Xc, C, labels, sums, counts, empty, grows, group, ctx, sh)
-                _lib.check(lib.ottohip_kmeans_update(ctx.h, _lib.ptr(C), _lib.ptr(sums), _lib.ptr(counts), k, dim,
-                                                     ctypes.byref(shift), sh))
+                if group is None:  # E-step + M-step, one device->host copy per iteration
+                    _lib.check(lib.ottohip_kmeans_lloyd_iter(ctx.h, _lib.ptr(Xc), n, dim, _lib.ptr(C), k,
+                                                             _lib.ptr(labels), _lib.ptr(sums), _lib.ptr(counts), st4,
+                                                             sh))
+                    n_changed = int(st4[1])
+                    shift.value = st4[2]
+                    if st4[3] > 0:  # empty clusters: relocate, then the M-step
+                        empty = np.flatnonzero(counts.cpu().numpy() == 0)
+                        self._relocate(Xc, C, labels, sums, counts, empty, grows, group, ctx, sh)
+                        _lib.check(lib.ottohip_kmeans_update(ctx.h, _lib.ptr(C), _lib.ptr(sums), _lib.ptr(counts), k,
+                                                             dim, ctypes.byref(shift), sh))
+                else:
+                    _lib.check(lib.ottohip_kmeans_partial(ctx.h, _lib.ptr(Xc), n, dim, _lib.ptr(C), k,
+                                                          _lib.ptr(labels), _lib.ptr(sums), _lib.ptr(counts),
+                                                          ctypes.byref(inr), ctypes.byref(chg), sh))
+                    sums, counts = _allreduce(sums, group), _allreduce(counts, group)
+                    n_changed = int(_allreduce(torch.tensor([chg.value], dtype=torch.int64), group).item())
+                    cnt = counts.cpu().numpy()
+                    empty = np.flatnonzero(cnt == 0)
+                    if len(empty):
+                        self._relocate(Xc, C, labels, sums, counts, empty, grows, group, ctx, sh)
+                    _lib.check(lib.ottohip_kmeans_update(ctx.h, _lib.ptr(C), _lib.ptr(sums), _lib.ptr(counts), k,
+                                                         dim, ctypes.byref(shift), sh))
                 if n_changed == 0:
                     strict = True
                     break
@@ -162,6 +203,7 @@ class KMeans:
             inertia = float(_allreduce(torch.tensor([inr.value], dtype=torch.float64), group).item())
             if best is None or inertia < best[0]:
                 best = (inertia, C.clone(), labels[:n].clone(), it)
+        seed_stream.close()
         self.inertia_, C, self.labels_, self.n_iter_ = best
         self.cluster_centers_ = C + mean_d
         return self

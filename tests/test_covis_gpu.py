@@ -249,6 +249,28 @@ def test_finalize_matches_merge_restatement(gpu):
         np.testing.assert_array_equal(c, rc, err_msg=n)
 
 
+@pytest.mark.parametrize("n_items", [200, 60_000, 1 << 21])
+def test_finalize_radix_parity_small_items(gpu, n_items):
+    """The finalize aid sort runs ceil(bits_for(n_items) / 8) radix passes: 1 (n_items <= 256),
+    2 and 3 passes, so the result lands in either buffer of the ping-pong pair; finalize order
+    (count desc, aid, aid_next) must come out right for both parities."""
+    ev = synth.generate(6_000, first_session=31)
+    aid = (ev.aid.astype(np.int64) * 2654435761 % n_items).astype(np.int32)
+    ev = synth.events_from_columns(np.repeat(np.arange(ev.n_sessions), np.diff(ev.session_offsets)),
+                                   aid, ev.ts, ev.type)
+    fb = np.array([0, 3_000, ev.n_sessions], np.int64)
+    tab = _gpu_tables(ev, fb, n_items=n_items)
+    per_file = oracle.count_co_events_files(ev.session_offsets, ev.aid, ev.ts, ev.type, fb)
+    for n in NAMES:
+        ra, rb, rc = oracle.concat_files_w_stats(n, [p[n] for p in per_file])
+        a, b, c = (x.cpu().numpy() for x in tab.finalize(n))
+        assert len(ra) > 0, n
+        np.testing.assert_array_equal(a, ra, err_msg=n)
+        np.testing.assert_array_equal(b, rb, err_msg=n)
+        np.testing.assert_array_equal(c, rc, err_msg=n)
+    tab.free()
+
+
 def test_concat_files_w_stats_part_branch(gpu):
     """A6 branch (2) (count_co_events.py:135-166) at test scale: thresholds scaled down so the
     click filter (1) and the part-wise groupby (2) both trigger; parts are whole-file runs

@@ -110,3 +110,24 @@ def test_kmeans_oracle_runs_match_sklearn():
             assert it == km.n_iter_
             relocated += len(np.unique(X[seeds], axis=0)) < k
         assert (relocated > 0) == dup
+
+
+def test_kmeans_seed_replica_matches_numpy():
+    """ottohip_rs_permutation_head (host code of libottohip.so, no GPU call) reproduces
+    numpy RandomState(seed).permutation(n)[:k] over successive calls: the n_init runs' initial
+    centres of sklearn 1.2 KMeans(init='random') (model/kmeans_sessions.py:152-159)."""
+    import ctypes
+    import otto_recommender_amd._lib as L
+    lib = L.load()
+    for seed, n, k, runs in ((42, 1, 1, 2), (42, 2, 2, 3), (7, 1000, 50, 4), (42, 300_001, 50, 3),
+                             (0, (1 << 16) + 1, 64, 2)):
+        h = ctypes.c_void_p()
+        L.check(lib.ottohip_rs_create(seed, ctypes.byref(h)))
+        rs = np.random.RandomState(seed)
+        try:
+            for _ in range(runs):
+                out = np.empty(k, np.int64)
+                L.check(lib.ottohip_rs_permutation_head(h, n, k, out.ctypes.data))
+                np.testing.assert_array_equal(out, rs.permutation(n)[:k])
+        finally:
+            lib.ottohip_rs_destroy(h)

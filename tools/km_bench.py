@@ -28,11 +28,18 @@ lib = _lib.load()
 sh = _lib.stream_handle()
 
 
-MODE = os.environ.get("KM_MODE", "partial")  # partial (sklearn loop) | step (ottohip_kmeans_step: no change count)
+MODE = os.environ.get("KM_MODE", "partial")  # partial (sklearn loop) | step (ottohip_kmeans_step) | lloyd (fused)
 sh2 = ctypes.c_double()
 
 
+st4 = (ctypes.c_double * 4)()
+
+
 def step():
+    if MODE == "lloyd":
+        _lib.check(lib.ottohip_kmeans_lloyd_iter(ctx.h, _lib.ptr(X), n, dim, _lib.ptr(C), k, _lib.ptr(labels),
+                                                 _lib.ptr(sums), _lib.ptr(counts), st4, sh))
+        return
     if MODE == "step":
         _lib.check(lib.ottohip_kmeans_step(ctx.h, _lib.ptr(X), n, dim, _lib.ptr(C), k, _lib.ptr(labels),
                                            ctypes.byref(sh2), ctypes.byref(inr), sh))
