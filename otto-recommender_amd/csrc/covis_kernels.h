@@ -1144,6 +1144,7 @@ __global__ __launch_bounds__(256) void k_agg_sort(const Task* __restrict__ tasks
                                                   int n_rules, OutRows O) {
   __shared__ unsigned long long sacc[4][MAX_RULES * 4];
   __shared__ RulesDev sR;
+  __shared__ uint32_t stg[4][3][64 * M];  // per wave: output rows of one task (key2, counts, file counts)
   const uint32_t l = lane_id();
   const int wv = threadIdx.x >> 6;
   if (threadIdx.x == 0) sR = R;
@@ -1211,54 +1212,73 @@ __global__ __launch_bounds__(256) void k_agg_sort(const Task* __restrict__ tasks
       b[m] = cnt | ((cnt - s1) << 16);
       c[m] = nf1 | ((nf1 - s1) << 16);
     }
-    // (4) one output row per k-run end, written into the task's own word range
+    // (4) one output row per k-run end: (key2, count | count_ge2 << 16, nf1 | nf2 << 16) staged in
+    //     this wave's LDS rows at its rank among the k-run ends, then written out linearly into the
+    //     task's own word range (coalesced stores on a task-uniform base)
     const int type = (int)(rk >> A);
     const int32_t aid = (int32_t)(rk & ((1u << A) - 1u));
-    uint32_t nmine = 0;
+    uint32_t kend = 0;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       const uint32_t e = l * M + m;
       const uint32_t nxt = m < M - 1 ? v[m + 1] : nl;
-      nmine += (e < len && (e + 1 == len || (nxt >> F) != (v[m] >> F))) ? 1u : 0u;
+      kend |= (e < len && (e + 1 == len || (nxt >> F) != (v[m] >> F))) ? (1u << m) : 0u;
     }
+    const uint32_t nmine = (uint32_t)__builtin_popcount(kend);
     const uint32_t incl = wave_incl_scan(nmine);
-    uint64_t p = T.begin + incl - nmine;
-    const int nq = sR.n_of_type[type];
-    uint32_t s0a = 0, s0b = 0, s1a = 0, s1b = 0;  // local rules 0 / 1: rows | nf1 << 16, pairs | nf2 << 16
+    const uint32_t nout = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    {
+      uint32_t idx = incl - nmine;
 #pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const uint32_t e = l * M + m;
-      const uint32_t nxt = m < M - 1 ? v[m + 1] : nl;
-      if (!(e < len && (e + 1 == len || (nxt >> F) != (v[m] >> F)))) continue;
-      const uint32_t k2 = v[m] >> F;
-      const uint32_t q = k2 >> A;
-      const uint32_t cnt = b[m] & 0xFFFFu, c2 = b[m] >> 16;
-      put_row(O, p++, sR.rule_of_type[type][q], aid, (int32_t)(k2 & L.amask), cnt, c2);
-      const uint32_t ra = 1u | ((c[m] & 0xFFFFu) << 16), rb = cnt | (c[m] & 0xFFFF0000u);
-      if (q == 0) { s0a += ra; s0b += rb; } else if (q == 1) { s1a += ra; s1b += rb; }
-    }
-    // per-rule statistics (local rules >= 2 are recounted here: only with > 2 rules per type)
-    for (int q = 0; q < nq; ++q) {
-      uint32_t sa = q == 0 ? s0a : s1a, sb = q == 0 ? s0b : s1b;
-      if (q >= 2) {
-        sa = 0; sb = 0;
-#pragma unroll
-        for (int m = 0; m < M; ++m) {
-          const uint32_t e = l * M + m;
-          const uint32_t nxt = m < M - 1 ? v[m + 1] : nl;
-          if (!(e < len && (e + 1 == len || (nxt >> F) != (v[m] >> F)))) continue;
-          if ((v[m] >> F) >> A != (uint32_t)q) continue;
-          sa += 1u | ((c[m] & 0xFFFFu) << 16);
-          sb += (b[m] & 0xFFFFu) | (c[m] & 0xFFFF0000u);
+      for (int m = 0; m < M; ++m) {
+        if (kend & (1u << m)) {
+          stg[wv][0][idx] = v[m] >> F;
+          stg[wv][1][idx] = b[m];
+          stg[wv][2][idx] = c[m];
+          ++idx;
         }
       }
-      sa = wave_sum(sa);
-      sb = wave_sum(sb);
-      if (l == 0 && sa) {
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int nq = sR.n_of_type[type];
+    const int r0 = sR.rule_of_type[type][0], r1 = sR.rule_of_type[type][1];
+    uint32_t s0a = 0, s0b = 0, s1a = 0, s1b = 0;  // local rules 0 / 1: rows | nf1 << 16, pairs | nf2 << 16
+    const bool store = O.cap != 0;
+    uint8_t* o_rule = O.rule + T.begin;
+    int32_t* o_aid = O.aid + T.begin;
+    int32_t* o_next = O.aid_next + T.begin;
+    uint32_t* o_cnt = O.count + T.begin;
+    uint32_t* o_c2 = O.count_ge2 + T.begin;
+    for (uint32_t i = l; i < nout; i += 64) {
+      const uint32_t k2 = stg[wv][0][i], bb = stg[wv][1][i], cc = stg[wv][2][i];
+      const uint32_t q = k2 >> A;
+      const uint32_t cnt = bb & 0xFFFFu;
+      if (store) {
+        o_rule[i] = (uint8_t)(q == 0 ? r0 : (q == 1 ? r1 : sR.rule_of_type[type][q]));
+        o_aid[i] = aid;
+        o_next[i] = (int32_t)(k2 & L.amask);
+        o_cnt[i] = cnt;
+        o_c2[i] = bb >> 16;
+      }
+      const uint32_t ra = 1u | ((cc & 0xFFFFu) << 16), rb = cnt | (cc & 0xFFFF0000u);
+      if (q == 0) { s0a += ra; s0b += rb; }
+      else if (q == 1) { s1a += ra; s1b += rb; }
+      else {  // more than 2 rules of one type (not in the reference's five)
         unsigned long long* acc = sacc[wv] + sR.rule_of_type[type][q] * 4;
+        atomicAdd(acc + 0, 1ull); atomicAdd(acc + 1, (unsigned long long)cnt);
+        atomicAdd(acc + 2, (unsigned long long)(cc & 0xFFFFu)); atomicAdd(acc + 3, (unsigned long long)(cc >> 16));
+      }
+    }
+    for (int q = 0; q < (nq < 2 ? nq : 2); ++q) {
+      const uint32_t sa = wave_sum(q == 0 ? s0a : s1a), sb = wave_sum(q == 0 ? s0b : s1b);
+      if (l == 0 && sa) {
+        unsigned long long* acc = sacc[wv] + (q == 0 ? r0 : r1) * 4;
         acc[0] += sa & 0xFFFFu; acc[1] += sb & 0xFFFFu; acc[2] += sa >> 16; acc[3] += sb >> 16;
       }
     }
+    __builtin_amdgcn_wave_barrier();  // the staging rows are rewritten by the next task
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     T = Tn;
     rk = rkn;
 #pragma unroll

@@ -292,13 +292,17 @@ __global__ __launch_bounds__(KM_MT) void k_km_assign_mfma(const float* __restric
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
       const int half = 8 >> st, J = 16 >> st;
-      const bool up = (l & J) != 0;
+      // lane-dependent choice by bit-select (v_bfi), not a select of array elements: the latter
+      // is turned into a dynamically indexed register array (compare/select chains)
+      const uint32_t upm = (l & J) ? ~0u : 0u;
 #pragma unroll
       for (int j = 0; j < half; ++j) {
-        const uint64_t send = up ? kk[j] : kk[j + half];
-        const uint64_t keep = up ? kk[j + half] : kk[j];
-        const uint32_t rlo = xor_lane_n((uint32_t)send, J), rhi = xor_lane_n((uint32_t)(send >> 32), J);
-        const uint64_t recv = ((uint64_t)rhi << 32) | rlo;
+        const uint32_t alo = (uint32_t)kk[j], ahi = (uint32_t)(kk[j] >> 32);
+        const uint32_t blo = (uint32_t)kk[j + half], bhi = (uint32_t)(kk[j + half] >> 32);
+        const uint32_t slo = (alo & upm) | (blo & ~upm), shi = (ahi & upm) | (bhi & ~upm);
+        const uint32_t klo = (blo & upm) | (alo & ~upm), khi = (bhi & upm) | (ahi & ~upm);
+        const uint32_t rlo = xor_lane_n(slo, J), rhi = xor_lane_n(shi, J);
+        const uint64_t recv = ((uint64_t)rhi << 32) | rlo, keep = ((uint64_t)khi << 32) | klo;
         kk[j] = recv < keep ? recv : keep;
       }
     }
@@ -336,12 +340,29 @@ __global__ __launch_bounds__(KM_MT) void k_km_assign_mfma(const float* __restric
           xa[q] = l < dim ? xq[l] : 0.f;
           xb[q] = l + 64 < dim ? xq[l + 64] : 0.f;
         }
+        // exact 2^24 scaling: one f32 -> i32 conversion per value while every |x| < 128 (the
+        // product is exact and below 2^31); the general f32 -> i64 sequence only for a wave
+        // that holds a larger value
+        bool big = false;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) big |= fabsf(xa[q]) >= 128.f || fabsf(xb[q]) >= 128.f;
+        long long fa[8], fb[8];
+        if (__builtin_expect(__ballot(big) != 0, 0)) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) { fa[q] = __float2ll_rn(xa[q] * 16777216.0f); fb[q] = __float2ll_rn(xb[q] * 16777216.0f); }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            fa[q] = (long long)__float2int_rn(xa[q] * 16777216.0f);
+            fb[q] = (long long)__float2int_rn(xb[q] * 16777216.0f);
+          }
+        }
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           if (rr + q >= nr) break;
-          unsigned long long* row = ls + cc[q] * dim;  // exact 2^24 scaling
-          if (l < dim) atomicAdd(&row[l], (unsigned long long)km_fx(xa[q]));
-          if (l + 64 < dim) atomicAdd(&row[l + 64], (unsigned long long)km_fx(xb[q]));
+          unsigned long long* row = ls + cc[q] * dim;
+          if (l < dim) atomicAdd(&row[l], (unsigned long long)fa[q]);
+          if (l + 64 < dim) atomicAdd(&row[l + 64], (unsigned long long)fb[q]);
           if (l == 0) atomicAdd(&lc[cc[q]], 1ull);
         }
       }
