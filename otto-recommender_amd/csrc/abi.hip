@@ -471,7 +471,11 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     k_split_chunk_task<<<grid_for(ns), 256, 0, s>>>(chb, nch, ns, ctask);
     k_split_hist<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, w0, w1, Lt.F, hmat);
     if ((rc = exclusive_scan_u32(ctx, hmat, hoff, nent, hoff + nent, s))) return rc;
-    k_split_scatter<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, hoff, w0, w1, Lt.F);
+    static const int sub = getenv("OTTOHIP_SPLIT_SUB") ? atoi(getenv("OTTOHIP_SPLIT_SUB")) : 4096;  // A/B switch
+    if (sub == 8192)
+      k_split_scatter<8192><<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, hoff, w0, w1, Lt.F);
+    else
+      k_split_scatter<4096><<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, hoff, w0, w1, Lt.F);
     // next lists (a sub-bucket is one task in exactly one list: ndig bounds every list)
     const uint64_t capn = (uint64_t)ndig;
     if ((rc = get_lists(std::max(cap0, capn), srcA ? "t_splitB" : "t_splitA"))) return rc;

@@ -1610,15 +1610,15 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_hist(const Task* __restrict__
   for (uint32_t d = threadIdx.x; d < nd; d += SPLIT_T) hmat[mat_base[t] + (uint64_t)d * nch + c] = h[d];
 }
 
-constexpr int SUB = 4096;             // scatter sub-tile (staged in LDS in digit order)
-constexpr int SUB_PER_T = SUB / SPLIT_T;  // words per thread per sub-tile, held in registers
+// SUB: scatter sub-tile (staged in LDS in digit order); SUB / SPLIT_T words per thread in registers
+template <int SUB>
 __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restrict__ tasks, int64_t n,
                                                            const uint64_t* __restrict__ chunk_base,
                                                            const uint32_t* __restrict__ chunk_task,
                                                            const uint64_t* __restrict__ mat_base,
                                                            const uint64_t* __restrict__ hoff,
                                                            uint32_t* __restrict__ w0, uint32_t* __restrict__ w1, int F) {
-  __shared__ uint32_t h[256], st[256], fill[256];
+  __shared__ uint32_t h[256], st[256];
   __shared__ uint64_t gb[256];
   __shared__ uint32_t stage[SUB];
   __shared__ uint32_t wsum[SPLIT_T / 64];
@@ -1630,6 +1630,7 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
   const uint64_t c1 = c0 + SPLIT_CH < T.len ? c0 + SPLIT_CH : T.len;
   const uint32_t* Win = (T.buf ? w1 : w0) + T.begin;
   uint32_t* Wout = T.buf ? w0 : w1;
+  constexpr int SUB_PER_T = SUB / SPLIT_T;
   const int tid = threadIdx.x;
   const uint64_t mb = mat_base[t];
   if ((uint32_t)tid < nd) gb[tid] = T.begin + (hoff[mb + (uint64_t)tid * nch + c] - hoff[mb]);
@@ -1641,12 +1642,15 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
       const int i = tid + j * SPLIT_T;
       wr[j] = i < m ? Win[s0 + i] : 0u;
     }
-    h[tid] = 0; fill[tid] = 0;
+    h[tid] = 0;
     __syncthreads();
+    // the histogram atomic returns the word's rank among this sub-tile's words of its digit: the
+    // staging slot (order inside a bucket is free), no second counter pass
+    uint32_t rk[SUB_PER_T];
 #pragma unroll
     for (int j = 0; j < SUB_PER_T; ++j) {
       dg[j] = split_digit(wr[j], F, T.rem, nd);
-      if (tid + j * SPLIT_T < m) atomicAdd(&h[dg[j]], 1u);
+      rk[j] = tid + j * SPLIT_T < m ? atomicAdd(&h[dg[j]], 1u) : 0u;
     }
     __syncthreads();
     {  // exclusive scan of h over 256 digits -> st
@@ -1661,7 +1665,7 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < SUB_PER_T; ++j)
-      if (tid + j * SPLIT_T < m) stage[st[dg[j]] + atomicAdd(&fill[dg[j]], 1u)] = wr[j];
+      if (tid + j * SPLIT_T < m) stage[st[dg[j]] + rk[j]] = wr[j];
     __syncthreads();
     for (int p = tid; p < m; p += SPLIT_T) {
       const uint32_t w = stage[p];

@@ -36,6 +36,10 @@ st4 = (ctypes.c_double * 4)()
 
 
 def step():
+    if MODE == "assign":  # E-step without the per-cluster sums
+        _lib.check(lib.ottohip_kmeans_assign(ctx.h, _lib.ptr(X), n, dim, _lib.ptr(C), k, _lib.ptr(labels),
+                                             ctypes.byref(inr), sh))
+        return
     if MODE == "lloyd":
         _lib.check(lib.ottohip_kmeans_lloyd_iter(ctx.h, _lib.ptr(X), n, dim, _lib.ptr(C), k, _lib.ptr(labels),
                                                  _lib.ptr(sums), _lib.ptr(counts), st4, sh))
