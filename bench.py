@@ -21,7 +21,18 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
-PMC_FILE = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
+# latest committed PMC traffic summary (tools/evidence_r2.sh -> profiles/r<NN>_pmc_traffic.json)
+def _latest_pmc_file():
+    import re
+    best = (-1, os.path.join(ROOT, "profiles", "none"))
+    for f in os.listdir(os.path.join(ROOT, "profiles")):
+        m = re.fullmatch(r"r(\d+)_pmc_traffic\.json", f)
+        if m and int(m.group(1)) > best[0]:
+            best = (int(m.group(1)), os.path.join(ROOT, "profiles", f))
+    return best[1]
+
+
+PMC_FILE = _latest_pmc_file()
 # kernels of each co-visitation phase (HIP-event timed on the launch stream; rocprof sums agree)
 PHASE_KERNELS = {"prep_count": "k_block_first + k_prep_count", "rows": "radix sort (k_rs_*), k_gather_counts, scans, k_rows",
                  "emit": "k_emit", "reduce": "k_classify_rows, k_agg_sort<M>, k_agg_hash, k_split_*, scans"}
@@ -29,7 +40,7 @@ PHASE_KERNELS = {"prep_count": "k_block_first + k_prep_count", "rows": "radix so
 
 def pmc_traffic(key: str):
     """Measured HBM bytes per launch/step (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate --pmc
-    passes of this same command; see profiles/r1_pmc_traffic.json), or None if not collected."""
+    passes of this same command; see PMC_FILE), or None if not collected."""
     try:
         return float(json.load(open(PMC_FILE))[key]["traffic_bytes"])
     except Exception:

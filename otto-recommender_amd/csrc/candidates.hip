@@ -25,7 +25,7 @@ constexpr int CS_MAXE = 512;      // events per session handled by k_cand_aids
 constexpr int CS_SRC = 7;         // 5 co-count lists + 2 kNN lists
 constexpr int CS_NLAST = 99;      // RETRIEVE_N_LAST_* / RETRIEVE_N_MOST_FREQUENT (config.py:76-79)
 constexpr uint32_t CS_EMPTY = 0xFFFFFFFFu;
-constexpr int CS_NONE = 0x7FFFFFFF;
+constexpr uint64_t CS_OVF_BIT = 1ull << 63;  // pool offset flag: the region lies in the overflow pool
 
 struct CandLists {
   const uint32_t* off[CS_SRC];   // per source: [n_items + 1] offsets into nxt / rank (by aid)
@@ -325,8 +325,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   if (__ballot(full)) {  // the session does not fit this tier: retried with a larger table
-    if (pass == 0 && l == 0) {
-      overflow[atomicAdd(n_overflow, 1u)] = (int32_t)s;
+    if (l == 0) {
+      if (overflow) overflow[atomicAdd(n_overflow, 1u)] = (int32_t)s;
       n_cand[s] = 0;
     }
     return;
@@ -378,13 +378,66 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
   }
-  const uint64_t o = cand_off[s];
+  const uint64_t o = cand_off[s] & ~CS_OVF_BIT;
+  if (l == 0) n_cand[s] = (uint32_t)cnt;
   for (int i = l; i < cnt; i += 64) {
     const uint64_t v = SK[i];
     o_next[o + i] = (int32_t)(uint32_t)(v >> 16);
     o_ord[o + i] = (int16_t)(v >> 48);
     o_flags[o + i] = (uint16_t)(v & 0x1FFu);
   }
+}
+
+// Single-pass layout: an upper bound of every session's candidates (its kept aids' merged-list
+// entries + self pairs + its cluster's popularity list, capped at the tier's table size) gives
+// each session a region of a pool; the build pass writes its sorted candidates there and its
+// count, and a compaction copies the regions into the session-ordered CSR (no count pass).
+__global__ void k_cand_bound(const int64_t* __restrict__ off, int64_t S, const KeptAid* __restrict__ kept,
+                             const uint32_t* __restrict__ n_kept, const int32_t* __restrict__ session_cl,
+                             MergedLists L, uint32_t cap, uint32_t* __restrict__ ub) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  const int64_t e0 = off[s];
+  const uint32_t nk = n_kept[s];
+  uint64_t t = 0;
+  for (uint32_t k = 0; k < nk && t < cap; ++k) {
+    const int32_t a = kept[e0 + k].aid;
+    t += 1u + (a < L.n_items ? L.ucnt[a] : 0u);
+  }
+  const int32_t c = session_cl ? session_cl[s] : -1;
+  if (c >= 0 && c < L.n_clusters) t += L.pop_off[c + 1] - L.pop_off[c];
+  ub[s] = (uint32_t)(t < cap ? t : cap);
+}
+
+// one wave per session: pool region [src_off, + n) -> CSR [dst_off, + n)
+__global__ __launch_bounds__(256) void k_cand_compact(const uint64_t* __restrict__ src_off,
+                                                      const uint64_t* __restrict__ dst_off, int64_t S,
+                                                      const int32_t* __restrict__ p_next, const int16_t* __restrict__ p_ord,
+                                                      const uint16_t* __restrict__ p_flags,
+                                                      const int32_t* __restrict__ q_next, const int16_t* __restrict__ q_ord,
+                                                      const uint16_t* __restrict__ q_flags,
+                                                      int32_t* __restrict__ o_next, int16_t* __restrict__ o_ord,
+                                                      uint16_t* __restrict__ o_flags) {
+  const int64_t s = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (s >= S) return;
+  const int l = threadIdx.x & 63;
+  const uint64_t so = src_off[s], d0 = dst_off[s], n = dst_off[s + 1] - d0;
+  const bool ovf = (so & CS_OVF_BIT) != 0;
+  const uint64_t b = so & ~CS_OVF_BIT;
+  const int32_t* xn = ovf ? q_next : p_next;
+  const int16_t* xo = ovf ? q_ord : p_ord;
+  const uint16_t* xf = ovf ? q_flags : p_flags;
+  for (uint64_t i = l; i < n; i += 64) {
+    o_next[d0 + i] = xn[b + i];
+    o_ord[d0 + i] = xo[b + i];
+    o_flags[d0 + i] = xf[b + i];
+  }
+}
+
+__global__ void k_cand_ovf_src(const int32_t* __restrict__ ovf_sess, int64_t n, uint32_t cap,
+                               uint64_t* __restrict__ src_off) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) src_off[ovf_sess[i]] = CS_OVF_BIT | ((uint64_t)i * cap);
 }
 
 // R9: one wave per session; per type: filtered rank of each label in the candidate order
@@ -597,30 +650,53 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
   k_cand_aids<<<(unsigned)Sn, 64, 0, s>>>(session_offsets, Sn, aid, ts, type, kept, n_kept, err);
   ctx->end(ph, s);
   ph = ctx->begin("cand_build", s, 0);
-  constexpr int W = 2;
-  k_cand_build<1024, W><<<(unsigned)ceil_div(Sn, W), 64 * W, 0, s>>>(session_offsets, nullptr, Sn, kept, n_kept,
-                                                                       session_cl, M, 0, n_cand, nullptr, nullptr,
-                                                                       nullptr, nullptr, ovf, n_ovf, dbg);
+  constexpr int W = 2, HC1 = 1024, HC2 = 4096;
+  // per-session pool regions from an upper bound (tier-1 table size at most), one build pass
+  uint32_t* ub;
+  uint64_t *pool_off, *ptot;
+  if ((rc = ws.get("cs_ub", (size_t)Sn, &ub)) || (rc = ws.get("cs_pool_off", (size_t)Sn + 1, &pool_off)) ||
+      (rc = ws.get("cs_ptot", 1, &ptot)))
+    return fail(rc);
+  k_cand_bound<<<grid_for(Sn), 256, 0, s>>>(session_offsets, Sn, kept, n_kept, session_cl, M, (uint32_t)HC1, ub);
+  if ((rc = exclusive_scan_u32(ctx, ub, pool_off, Sn, ptot, s))) return fail(rc);
+  uint64_t npool = 0;
+  if ((rc = d2h(&npool, ptot, 1, s))) return fail(rc);
+  int32_t* p_next;
+  int16_t* p_ord;
+  uint16_t* p_flags;
+  const size_t pcap = (size_t)std::max<uint64_t>(npool, 1);
+  if ((rc = ws.get("cs_pool_next", pcap, &p_next)) || (rc = ws.get("cs_pool_ord", pcap, &p_ord)) ||
+      (rc = ws.get("cs_pool_flags", pcap, &p_flags)))
+    return fail(rc);
+  k_cand_build<HC1, W><<<(unsigned)ceil_div(Sn, W), 64 * W, 0, s>>>(session_offsets, nullptr, Sn, kept, n_kept,
+                                                                     session_cl, M, 1, n_cand, pool_off, p_next, p_ord,
+                                                                     p_flags, ovf, n_ovf, dbg);
   uint32_t novf = 0;
   int herr = 0;
   if ((rc = d2h(&novf, n_ovf, 1, s)) || (rc = d2h(&herr, err, 1, s))) return fail(rc);
   if (herr & 1) { set_error("candidates_generate: a session has more than %d events", CS_MAXE); return fail(OTTOHIP_ELIMIT); }
   if (herr & 4) { set_error("candidates_generate: an aid has more than %d list entries", ML_MAX); return fail(OTTOHIP_ELIMIT); }
-  int64_t* ovf64 = nullptr;
-  uint32_t* n_ovf2 = nullptr;
-  int32_t* ovf2 = nullptr;
-  if (novf) {  // sessions beyond the 1024-slot tier: sorted list, 4096-slot tier
+  int32_t* q_next = p_next;
+  int16_t* q_ord = p_ord;
+  uint16_t* q_flags = p_flags;
+  if (novf) {  // sessions beyond the 1024-slot tier: the 4096-slot tier, regions in an overflow pool
+    int64_t* ovf64 = nullptr;
+    uint32_t* n_ovf2 = nullptr;
+    int32_t* ovf2 = nullptr;
     if ((rc = ws.get("cs_novf2", 1, &n_ovf2)) || (rc = ws.get("cs_ovf2", (size_t)novf, &ovf2)) ||
-        (rc = ws.get("cs_ovf64", (size_t)novf, &ovf64)))
+        (rc = ws.get("cs_ovf64", (size_t)novf, &ovf64)) || (rc = ws.get("cs_q_next", (size_t)novf * HC2, &q_next)) ||
+        (rc = ws.get("cs_q_ord", (size_t)novf * HC2, &q_ord)) || (rc = ws.get("cs_q_flags", (size_t)novf * HC2, &q_flags)))
       return fail(rc);
     std::vector<int32_t> ho(novf);
     if ((rc = d2h(ho.data(), ovf, novf, s))) return fail(rc);
     std::sort(ho.begin(), ho.end());
     std::vector<int64_t> ho64(ho.begin(), ho.end());
+    OH_HIP(hipMemcpyAsync(ovf, ho.data(), novf * sizeof(int32_t), hipMemcpyHostToDevice, s));
     OH_HIP(hipMemcpyAsync(ovf64, ho64.data(), novf * sizeof(int64_t), hipMemcpyHostToDevice, s));
     OH_HIP(hipMemsetAsync(n_ovf2, 0, sizeof(uint32_t), s));
-    k_cand_build<4096, 1><<<novf, 64, 0, s>>>(session_offsets, ovf64, novf, kept, n_kept, session_cl, M, 0, n_cand,
-                                               nullptr, nullptr, nullptr, nullptr, ovf2, n_ovf2, dbg);
+    k_cand_ovf_src<<<grid_for(novf), 256, 0, s>>>(ovf, novf, (uint32_t)HC2, pool_off);
+    k_cand_build<HC2, 1><<<novf, 64, 0, s>>>(session_offsets, ovf64, novf, kept, n_kept, session_cl, M, 1, n_cand,
+                                             pool_off, q_next, q_ord, q_flags, ovf2, n_ovf2, dbg);
     uint32_t novf2 = 0;
     if ((rc = d2h(&novf2, n_ovf2, 1, s))) return fail(rc);
     if (novf2) { set_error("candidates_generate: %u sessions exceed 4096 candidates", novf2); return fail(OTTOHIP_ELIMIT); }
@@ -634,12 +710,8 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
       dev_alloc(reinterpret_cast<void**>(&C->ord), cap * 2, "cand_ord") ||
       dev_alloc(reinterpret_cast<void**>(&C->flags), cap * 2, "cand_flags"))
     return fail(OTTOHIP_ENOMEM);
-  k_cand_build<1024, W><<<(unsigned)ceil_div(Sn, W), 64 * W, 0, s>>>(session_offsets, nullptr, Sn, kept, n_kept,
-                                                                       session_cl, M, 1, n_cand, C->off, C->next,
-                                                                       C->ord, C->flags, ovf, n_ovf, dbg);
-  if (novf)
-    k_cand_build<4096, 1><<<novf, 64, 0, s>>>(session_offsets, ovf64, novf, kept, n_kept, session_cl, M, 1, n_cand,
-                                               C->off, C->next, C->ord, C->flags, ovf2, n_ovf2, dbg);
+  k_cand_compact<<<(unsigned)ceil_div(Sn, 4), 256, 0, s>>>(pool_off, C->off, Sn, p_next, p_ord, p_flags, q_next, q_ord,
+                                                          q_flags, C->next, C->ord, C->flags);
   if (hipGetLastError() != hipSuccess) { set_error("k_cand_build launch failed"); return fail(OTTOHIP_EHIP); }
   ctx->end(ph, s);
   *out = C;
