@@ -236,8 +236,11 @@ int ottohip_kmeans_update(ottohip_ctx* ctx, float* centroids, const int64_t* sum
                           int dim, double* shift2, void* stream);
 /* partial + update of one GPU in a single call with one device->host copy (sklearn 1.2
  * _kmeans_single_lloyd, model/kmeans_sessions.py:152-159): out (HOST double[4]) = inertia, changed
- * labels, shift^2, empty clusters. When a cluster is empty the centroids are NOT updated (out[2] =
- * -1): relocate, then update (sklearn relocates before the M-step). */
+ * labels, shift^2, empty clusters. sums / counts are INCREMENTAL: on entry they hold the exact
+ * fixed-point sums / counts of the rows under `labels` (all zero with labels = -1 at the start of a
+ * run) and on return those of the new labels (only rows whose label changed are moved). When a
+ * cluster is empty the centroids are NOT updated (out[2] = -1): relocate on a copy of sums /
+ * counts, then update (sklearn relocates before the M-step). */
 int ottohip_kmeans_lloyd_iter(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* centroids, int k,
                               int32_t* labels, int64_t* sums, int64_t* counts, double* out, void* stream);
 int ottohip_kmeans_farthest(ottohip_ctx* ctx, const float* X, int64_t n, int dim, const float* centroids,

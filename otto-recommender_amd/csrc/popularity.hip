@@ -219,11 +219,11 @@ __global__ __launch_bounds__(KM_MT) void k_km_assign_mfma(const float* __restric
                                                         unsigned long long* __restrict__ cnt,
                                                         double* __restrict__ inertia,
                                                         unsigned long long* __restrict__ changed,
-                                                        float* __restrict__ dist) {
+                                                        float* __restrict__ dist, int inc) {
   extern __shared__ unsigned long long smem64[];
   float4* Bl = reinterpret_cast<float4*>(smem64);                              // [NB][nq][64]
-  int32_t* labl = reinterpret_cast<int32_t*>(Bl + NB * nq * 64);                // [waves][32]
-  float* cnl = reinterpret_cast<float*>(labl + (KM_MT / 64) * 32);             // [64]
+  int32_t* labl = reinterpret_cast<int32_t*>(Bl + NB * nq * 64);                // [waves][3][32]: row, new, old
+  float* cnl = reinterpret_cast<float*>(labl + (KM_MT / 64) * 96);             // [64]
   unsigned long long* ls = reinterpret_cast<unsigned long long*>(cnl + 64);    // k * dim sums, k counts
   unsigned long long* lc = ls + k * dim;
   const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6, h = l >> 5, i32 = l & 31;
@@ -315,27 +315,39 @@ __global__ __launch_bounds__(KM_MT) void k_km_assign_mfma(const float* __restric
     const int R = (rr & 3) + 8 * (rr >> 2) + 4 * h;
     const float xr = __shfl(xs, R);
     const uint32_t mi = (uint32_t)kk[0];
-    if ((l & 1) == 0) {
-      labl[wv * 32 + R] = (int32_t)mi;
-      if (r0 + R < n) {
-        if (changed) nchg += label[r0 + R] != (int32_t)mi;
-        label[r0 + R] = (int32_t)mi;
-        const float dd = fmaxf(xr + km_unord((uint32_t)(kk[0] >> 32)), 0.f);
-        part += (double)dd;
-        if (dist) dist[r0 + R] = dd;
-      }
+    int32_t old = -1;
+    const bool mine = (l & 1) == 0 && r0 + R < n;
+    if (mine) {
+      if (changed || inc) old = label[r0 + R];
+      if (changed) nchg += old != (int32_t)mi;
+      label[r0 + R] = (int32_t)mi;
+      const float dd = fmaxf(xr + km_unord((uint32_t)(kk[0] >> 32)), 0.f);
+      part += (double)dd;
+      if (dist) dist[r0 + R] = dd;
     }
-    if (sums) {  // the tile's rows, lanes over dimensions
+    if (sums) {
+      // rows whose vector enters a cluster's sums: every row, or (incremental) the rows whose
+      // label changed, which also leave their previous cluster; listed in LDS, lanes over dims
+      const bool in_list = mine && (!inc || old != (int32_t)mi);
+      const uint64_t bm = __ballot(in_list);
+      if (in_list) {
+        const int p = (int)mbcnt(bm);
+        labl[wv * 96 + p] = R;
+        labl[wv * 96 + 32 + p] = (int32_t)mi;
+        labl[wv * 96 + 64 + p] = inc ? old : -1;
+      }
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      const int nr = (int)min<int64_t>(32, n - r0);
+      const int nr = (int)__popcll(bm);
       for (int rr = 0; rr < nr; rr += 8) {  // 8 rows' loads in flight
         float xa[8], xb[8];
-        int cc[8];
+        int cc[8], co[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-          const int r = rr + q < nr ? rr + q : nr - 1;
-          cc[q] = labl[wv * 32 + r];
+          const int pq = rr + q < nr ? rr + q : nr - 1;
+          const int r = labl[wv * 96 + pq];
+          cc[q] = labl[wv * 96 + 32 + pq];
+          co[q] = labl[wv * 96 + 64 + pq];
           const float* xq = X + (r0 + r) * dim;
           xa[q] = l < dim ? xq[l] : 0.f;
           xb[q] = l + 64 < dim ? xq[l + 64] : 0.f;
@@ -364,6 +376,12 @@ __global__ __launch_bounds__(KM_MT) void k_km_assign_mfma(const float* __restric
           if (l < dim) atomicAdd(&row[l], (unsigned long long)fa[q]);
           if (l + 64 < dim) atomicAdd(&row[l + 64], (unsigned long long)fb[q]);
           if (l == 0) atomicAdd(&lc[cc[q]], 1ull);
+          if (co[q] >= 0) {  // two's-complement deltas: the block's sums may go below zero
+            unsigned long long* orow = ls + co[q] * dim;
+            if (l < dim) atomicAdd(&orow[l], (unsigned long long)(-fa[q]));
+            if (l + 64 < dim) atomicAdd(&orow[l + 64], (unsigned long long)(-fb[q]));
+            if (l == 0) atomicAdd(&lc[co[q]], ~0ull);
+          }
         }
       }
       __builtin_amdgcn_wave_barrier();  // labl is rewritten by the next tile
@@ -389,9 +407,12 @@ __global__ __launch_bounds__(KM_MT) void k_km_assign_mfma(const float* __restric
   }
 }
 
+// inc: sums / cnt hold the exact sums / counts of the rows under `labels` (the previous labels) and
+// are updated by the rows whose label changes (MFMA kernel); otherwise they are accumulated from
+// scratch by every row (the caller zeroes them)
 static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int64_t n, int dim, const float* C,
                             int32_t* labels, unsigned long long* sums, unsigned long long* cnt, double* inr,
-                            unsigned long long* changed = nullptr, float* dist = nullptr) {
+                            unsigned long long* changed = nullptr, float* dist = nullptr, int inc = 0) {
   const int KP = (k + 7) / 8 * 8;
   float *Ct, *cn;
   OH_TRY(ctx->ws.get("km_ct", (size_t)KP * dim, &Ct));
@@ -403,7 +424,7 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
   if (!km_valu && k <= 64 && dim <= 8 * KM_NQ && (dim & 3) == 0 && ((uintptr_t)X & 15) == 0 &&
       ((uintptr_t)C & 15) == 0) {
     const int nq = (dim + 7) / 8, NB = k <= 32 ? 1 : 2;
-    const size_t lds = (size_t)NB * nq * 64 * 16 + (KM_MT / 64) * 32 * 4 + 64 * 4 +
+    const size_t lds = (size_t)NB * nq * 64 * 16 + (KM_MT / 64) * 96 * 4 + 64 * 4 +
                        (sums ? ((size_t)k * dim + k) * 8 : 8);
     const int64_t ntile = ceil_div(n, 32);
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(ntile, KM_MT / 64),
@@ -411,9 +432,13 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
     auto kern = NB == 1 ? k_km_assign_mfma<1> : k_km_assign_mfma<2>;
     OH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)lds));
-    kern<<<grid, KM_MT, lds, s>>>(X, n, dim, nq, C, cn, k, labels, sums, cnt, inr, changed, dist);
+    kern<<<grid, KM_MT, lds, s>>>(X, n, dim, nq, C, cn, k, labels, sums, cnt, inr, changed, dist, inc);
     OH_HIP(hipGetLastError());
     return 0;
+  }
+  if (inc && sums) {  // the VALU kernel accumulates from scratch
+    OH_HIP(hipMemsetAsync(sums, 0, (size_t)k * dim * 8, s));
+    OH_HIP(hipMemsetAsync(cnt, 0, (size_t)k * 8, s));
   }
   const size_t lds = sums ? ((size_t)k * dim + k) * 8 : 8;
   const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n, 256), (int64_t)ctx->n_cu * 4);
@@ -850,7 +875,9 @@ int ottohip_kmeans_update(ottohip_ctx* ctx, float* centroids, const int64_t* sum
 }
 
 // One whole Lloyd iteration on one GPU with a single device->host copy: E-step (labels, fixed-point
-// sums, counts, changed labels, inertia) and, unless a cluster came out empty, the M-step.
+// sums, counts, changed labels, inertia) and, unless a cluster came out empty, the M-step. sums /
+// counts are incremental: on entry they hold the exact sums / counts of the rows under `labels`
+// (zero with labels = -1 at the start of a run); only rows whose label changes move their vector.
 // out[0] inertia, [1] changed labels, [2] shift^2 (-1: not updated), [3] empty clusters. With
 // out[3] > 0 the centroids are unchanged; sums / counts are ready for ottohip_kmeans_relocate and
 // ottohip_kmeans_update (sklearn 1.2 _kmeans_single_lloyd order).
@@ -865,12 +892,10 @@ int ottohip_kmeans_lloyd_iter(ottohip_ctx* ctx, const float* X, int64_t n, int d
   OH_HIP(hipSetDevice(ctx->device));
   double* st;  // [inertia, changed, shift, empty]
   OH_TRY(ctx->ws.get("km_stats", 4, &st));
-  OH_HIP(hipMemsetAsync(sums, 0, (size_t)k * dim * 8, s));
-  OH_HIP(hipMemsetAsync(counts, 0, (size_t)k * 8, s));
   OH_HIP(hipMemsetAsync(st, 0, 4 * 8, s));
   OH_TRY(launch_km_assign(ctx, k, s, X, n, dim, centroids, labels, reinterpret_cast<unsigned long long*>(sums),
                           reinterpret_cast<unsigned long long*>(counts), st,
-                          reinterpret_cast<unsigned long long*>(st + 1), nullptr));
+                          reinterpret_cast<unsigned long long*>(st + 1), nullptr, 1));
   k_km_update<<<1, KM_UT, 0, s>>>(centroids, reinterpret_cast<const long long*>(sums),
                                   reinterpret_cast<const long long*>(counts), k, dim, 1, st + 2);
   OH_HIP(hipGetLastError());

@@ -164,6 +164,8 @@ class KMeans:
             seeds = next(seed_stream)
             C = self._gather_rows(Xc, seeds, grows, group)
             labels.fill_(-1)
+            sums.zero_()  # the one-GPU iteration keeps sums / counts of the current labels incrementally
+            counts.zero_()
             strict, it = False, 0
             for it in range(1, self.max_iter + 1):
                 if group is None:  # E-step + M-step, one device->host copy per iteration
@@ -172,10 +174,11 @@ class KMeans:
                                                              sh))
                     n_changed = int(st4[1])
                     shift.value = st4[2]
-                    if st4[3] > 0:  # empty clusters: relocate, then the M-step
-                        empty = np.flatnonzero(counts.cpu().numpy() == 0)
-                        self._relocate(Xc, C, labels, sums, counts, empty, grows, group, ctx, sh)
-                        _lib.check(lib.ottohip_kmeans_update(ctx.h, _lib.ptr(C), _lib.ptr(sums), _lib.ptr(counts), k,
+                    if st4[3] > 0:  # empty clusters: relocate on a copy (sums / counts follow the labels), M-step
+                        rs_, rc_ = sums.clone(), counts.clone()
+                        empty = np.flatnonzero(rc_.cpu().numpy() == 0)
+                        self._relocate(Xc, C, labels, rs_, rc_, empty, grows, group, ctx, sh)
+                        _lib.check(lib.ottohip_kmeans_update(ctx.h, _lib.ptr(C), _lib.ptr(rs_), _lib.ptr(rc_), k,
                                                              dim, ctypes.byref(shift), sh))
                 else:
                     _lib.check(lib.ottohip_kmeans_partial(ctx.h, _lib.ptr(Xc), n, dim, _lib.ptr(C), k,
