@@ -111,7 +111,6 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
 #pragma unroll
   for (int j = 0; j < KN_C; ++j) { sc[j] = -INFINITY; ix[j] = 0xFFFFFFFFu; }
   float thr = -INFINITY;
-  int tpos = 0;
   constexpr bool PRE = ABL == 2;
   const int64_t nTall = ceil_div(V, KN_IT);
   const int64_t nT = PRE ? (nTall - 1 + PRE_STRIDE - 1) / PRE_STRIDE : nTall;  // tiles scanned
@@ -124,6 +123,7 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
   // LDS chunk p = u*512 + tid holds item row p>>4, source chunk (p & 15) ^ (row & 15);
   // rows past V read row V-1 (valid memory; their scores are masked below)
   auto issue = [&](int64_t t) {
+    if (ABL == 3 && t >= KN_RING) return;  // ablation: item stream off after the first tiles (timing only)
     uint4* dst = ring + (int)(t % KN_RING) * (KN_IT * KN_CH);
     const int64_t tt = PRE ? t * PRE_STRIDE : t;
 #pragma unroll
@@ -134,14 +134,26 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
       __builtin_amdgcn_global_load_lds(items + item * KN_CH + (c ^ (row & 15)), dst + u * KN_T + w * 64, 16, 0, 0);
     }
   };
-  auto insert = [&](float s_, uint32_t item) {
+  // the list is kept sorted descending, so the threshold is its last score and an insert is a
+  // branch-free shift: slot j takes slot j-1 if s beats it, else s if s beats slot j (score: one
+  // v_med3 of (sc[j-1], s, sc[j]); index: two selects). A lane-dependent "replace the minimum"
+  // slot becomes a compare/select chain over every slot instead.
+  auto insert = [&](float s_, uint32_t item) __attribute__((always_inline)) {
+    bool cj = s_ > sc[KN_C - 1];
 #pragma unroll
-    for (int j = 0; j < KN_C; ++j)
-      if (j == tpos) { sc[j] = s_; ix[j] = item; }
-    thr = sc[0]; tpos = 0;
-#pragma unroll
-    for (int j = 1; j < KN_C; ++j)
-      if (sc[j] < thr) { thr = sc[j]; tpos = j; }
+    for (int jj = 0; jj < KN_C - 1; ++jj) {  // downwards: slot j - 1 still holds its old value
+      const int j = KN_C - 1 - jj;
+      const bool cp = s_ > sc[j - 1];
+      uint32_t a = ix[j - 1], b = ix[j];
+      asm("" : "+v"(a), "+v"(b));  // keeps the selects on values: a select of the two slots' addresses
+                                   // would leave ix[] as a memory array (LDS / scratch)
+      ix[j] = cp ? a : (cj ? item : b);
+      sc[j] = __builtin_amdgcn_fmed3f(sc[j - 1], s_, sc[j]);
+      cj = cp;
+    }
+    ix[0] = cj ? item : ix[0];
+    sc[0] = fmaxf(sc[0], s_);
+    thr = sc[KN_C - 1];
   };
   issue(0);
   if (nT > 1) issue(1);
@@ -151,26 +163,27 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
     __builtin_amdgcn_s_barrier();  // tile t visible to all waves; slot (t+2)%3 = (t-1)%3 is free
     if (t + 2 < nT) issue(t + 2);
     const uint4* T = ring + (int)(t % KN_RING) * (KN_IT * KN_CH);
-#pragma unroll
-    for (int rp = 0; rp < KN_IT / 64; ++rp) {  // two row-blocks of 32 items at a time
-      f32x16 accA[2] = {}, accB[2] = {};
-      const int row0 = (2 * rp) * 32 + r, row1 = row0 + 32;
-      bf16x8 cur0 = __builtin_bit_cast(bf16x8, T[row0 * KN_CH + ((0 + h) ^ (row0 & 15))]);
-      bf16x8 cur1 = __builtin_bit_cast(bf16x8, T[row1 * KN_CH + ((0 + h) ^ (row1 & 15))]);
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        bf16x8 nx0 = cur0, nx1 = cur1;
-        if (s < 7) {  // next k-step's fragments are read while this step's MFMAs run
-          nx0 = __builtin_bit_cast(bf16x8, T[row0 * KN_CH + ((2 * s + 2 + h) ^ (row0 & 15))]);
-          nx1 = __builtin_bit_cast(bf16x8, T[row1 * KN_CH + ((2 * s + 2 + h) ^ (row1 & 15))]);
-        }
-        accA[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur0, bqa[s], accA[0], 0, 0, 0);
-        accB[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur0, bqb[s], accB[0], 0, 0, 0);
-        accA[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur1, bqa[s], accA[1], 0, 0, 0);
-        accB[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur1, bqb[s], accB[1], 0, 0, 0);
-        cur0 = nx0;
-        cur1 = nx1;
-      }
+    // item fragments run two k-steps ahead over the tile's 16 (row-block pair, k-step) steps, so a
+    // step's LDS reads have two steps of MFMAs to land (one step's 4 MFMAs did not cover them)
+    bf16x8 F0[16], F1[16];
+    auto ld = [&](int g) __attribute__((always_inline)) {
+      const int row0 = (2 * (g >> 3)) * 32 + r, row1 = row0 + 32, s_ = g & 7;
+      F0[g] = __builtin_bit_cast(bf16x8, T[row0 * KN_CH + ((2 * s_ + h) ^ (row0 & 15))]);
+      F1[g] = __builtin_bit_cast(bf16x8, T[row1 * KN_CH + ((2 * s_ + h) ^ (row1 & 15))]);
+    };
+    ld(0);
+    ld(1);
+    f32x16 accA[2], accB[2];
+#pragma clang loop unroll(full)
+    for (int g = 0; g < 16; ++g) {
+      const int rp = g >> 3, s = g & 7;
+      if (g + 2 < 16) ld(g + 2);
+      if (s == 0) { accA[0] = {}; accA[1] = {}; accB[0] = {}; accB[1] = {}; }
+      accA[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F0[g], bqa[s], accA[0], 0, 0, 0);
+      accB[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F0[g], bqb[s], accB[0], 0, 0, 0);
+      accA[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F1[g], bqa[s], accA[1], 0, 0, 0);
+      accB[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F1[g], bqb[s], accB[1], 0, 0, 0);
+      if (s != 7) continue;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         // per-lane maxima first: swapping the two maxima gives this lane's query maximum over the
@@ -180,12 +193,12 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
         for (int i = 1; i < 16; ++i) { mA = fmaxf(mA, accA[u][i]); mB = fmaxf(mB, accB[u][i]); }
         const auto msw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mA), __float_as_uint(mB), false, false);
         const float m = fmaxf(__uint_as_float(msw[0]), __uint_as_float(msw[1]));
-        if (ABL == 1) { thr = fmaxf(thr, m * 1e-30f); continue; }  // ablation build: no candidate handling
+        if (ABL == 1 || ABL == 3) { thr = fmaxf(thr, m * 1e-30f); continue; }  // ablation builds: no candidate handling
         if (PRE) {  // group g = tile % KN_C keeps its maximum in sc[g]
           const int gsel = (int)(t % KN_C);
 #pragma unroll
-          for (int g = 0; g < KN_C; ++g)
-            if (g == gsel) sc[g] = fmaxf(sc[g], m);
+          for (int gg = 0; gg < KN_C; ++gg)
+            if (gg == gsel) sc[gg] = fmaxf(sc[gg], m);
           continue;
         }
         if (__ballot(m > thr)) {
@@ -198,18 +211,32 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
           }
         }
         if (m > thr) {
+          // this lane's 32 scores of the block as unique keys: the row slot j (0..31) replaces the
+          // 5 low mantissa bits (32 ulp, far below the bf16 inputs' error), so the best remaining
+          // candidate is one max over keys below the last one taken, and its key names its row
           const int64_t ib = t * KN_IT + (2 * rp + u) * 32;
+          float kf[32];
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            const int64_t base = ib + (i & 3) + 8 * (i >> 2);
-            if (accA[u][i] > thr && base + offx < V) insert(accA[u][i], (uint32_t)(base + offx));
-            if (accB[u][i] > thr && base + offy < V) insert(accB[u][i], (uint32_t)(base + offy));
+            kf[i] = __uint_as_float((__float_as_uint(accA[u][i]) & ~31u) | (uint32_t)i);
+            kf[16 + i] = __uint_as_float((__float_as_uint(accB[u][i]) & ~31u) | (uint32_t)(16 + i));
+          }
+          float last = INFINITY;
+          while (true) {
+            float cur = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < 32; ++j) cur = fmaxf(cur, kf[j] < last ? kf[j] : -INFINITY);
+            if (!(cur > thr)) break;
+            const uint32_t j = __float_as_uint(cur) & 31u, i = j & 15u;
+            const int64_t item = ib + (i & 3) + 8 * (i >> 2) + (j < 16 ? offx : offy);
+            if (item < V) insert(cur, (uint32_t)item);
+            last = cur;
           }
         }
       }
     }
   }
-  if (ABL == 1 && thr == 12345.f) ix[0] = 0;  // keep the ablated scores live
+  if ((ABL == 1 || ABL == 3) && thr == 12345.f) ix[0] = 0;  // keep the ablated scores live
   if (PRE) {
     float b = sc[0];
 #pragma unroll
@@ -356,7 +383,7 @@ int ottohip_knn_topk(ottohip_ctx* c, const ottohip_knn_index* ix, const int32_t*
     ctx->end(ph, s);
   }
   ph = ctx->begin("knn_main", s, 2.0 * (double)n_q * (double)ix->n_items * ix->dim);
-  auto kmain = abl ? k_knn_main<1> : k_knn_main<0>;
+  auto kmain = abl == 3 ? k_knn_main<3> : (abl ? k_knn_main<1> : k_knn_main<0>);
   kmain<<<grid, KN_T, 0, s>>>(reinterpret_cast<const uint4*>(ix->packed), ix->n_items,
                               reinterpret_cast<const uint4*>(qp), n_q, cand, thr);
   ctx->end(ph, s);
