@@ -70,9 +70,10 @@ def cpu_baseline(seed: int = 0, pandas_files: int = 10) -> dict:
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16, /opt/skills/guides/MI355X_MICROARCH.md
 
 
-def bench_knn(steps: int, warmup: int, n_items: int, n_q: int, with_cpu: bool) -> dict:
-    """BASELINE configs[2]: W2V top-20 kNN, 1.8M x 100 items, first 600k vocabulary rows as
-    queries (config.py:125; model/w2vec_aids.py:203), one model per step."""
+def bench_knn(steps: int, warmup: int, n_items: int, n_q: int, with_cpu: bool, group=None) -> dict:
+    """BASELINE configs[2]: exact top-20 kNN of the first n_q vocabulary rows. group: the queries
+    are split in equal ranges over the ranks (the item matrix replicated on every GPU, SURVEY.md
+    §8(e)); value = all ranks' queries / the slowest rank's time."""
     import torch
     import otto_recommender_amd.synth as synth
     from otto_recommender_amd import _lib
@@ -81,34 +82,60 @@ def bench_knn(steps: int, warmup: int, n_items: int, n_q: int, with_cpu: bool) -
     emb = synth.embeddings(n_items)
     n_q = min(n_q, n_items)
     index = KnnIndex(emb, ctx)
+    world, rank, rows, n_mine = 1, 0, None, n_q
+    if group is not None:
+        import torch.distributed as dist
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        q0, q1 = n_q * rank // world, n_q * (rank + 1) // world
+        rows = torch.arange(q0, q1, dtype=torch.int32, device=torch.device("cuda", ctx.device))
+        n_mine = q1 - q0
+
+    def search():
+        return index.search(rows, k=20) if rows is not None else index.search(None, n_q=n_q, k=20)
+
+    def barrier():
+        if group is not None:
+            import torch.distributed as dist
+            dist.barrier(group)
+
     for _ in range(warmup):
-        index.search(None, n_q=n_q, k=20)
+        search()
     torch.cuda.synchronize()
+    barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
-        idx, d2 = index.search(None, n_q=n_q, k=20)
+        idx, d2 = search()
     torch.cuda.synchronize()
+    barrier()
     dt = (time.perf_counter() - t0) / steps
+    if group is not None:  # slowest rank
+        import torch.distributed as dist
+        cdev = torch.device("cuda", ctx.device) if dist.get_backend(group) == "nccl" else "cpu"
+        m = torch.tensor([dt], dtype=torch.float64, device=cdev)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group)
+        dt = float(m.item())
     ctx.set_timing(True)
-    index.search(None, n_q=n_q, k=20)
+    search()
     ph = {n: ms for n, ms, _ in ctx.timings()}
     ctx.set_timing(False)
-    flops = 2.0 * n_q * n_items * emb.shape[1]
+    flops = 2.0 * n_mine * n_items * emb.shape[1]  # this rank's launch
     main_ms = ph.get("knn_main", dt * 1e3)
     out = {"metric": "W2V top-20 kNN queries/s (exact, bf16 MFMA + fp32 rerank)", "value": n_q / dt,
-           "unit": "queries/s", "ms_per_step": dt * 1e3, "steps": steps,
+           "unit": "queries/s", "ms_per_step": dt * 1e3, "steps": steps, "n_gpus": world,
            "config": {"workload": "configs[2]: 1.86M items x 100-d, 600k queries, k=20", "items": n_items,
                       "queries": n_q, "k": 20},
            "dtype": "bf16 (fp32 accumulate, fp32 rerank)",
            "roofline": {"bound": "mfma", "kernel": "k_knn_main", "achieved": flops / (main_ms / 1e3) / 1e12,
                         "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": flops / (main_ms / 1e3) / 1e12 / MFMA_BF16_PEAK_TFLOPS,
-                        "traffic": pmc_traffic("k_knn_main") if n_items == 1_855_603 and n_q == 600_000 else None,
+                        "traffic": pmc_traffic("k_knn_main") if n_items == 1_855_603 and n_mine == 600_000 else None,
                         "traffic_note": "HBM/fabric bytes per launch (every 512-query workgroup streams the item matrix)",
                         "flops_model": "2*Q*V*100 (K padding to 128 and the top-k epilogue not counted)"},
            "phases_ms": {k: round(v, 3) for k, v in ph.items()},
            "reference_faiss_ivf_queries_per_s": 705}
-    if with_cpu:
+    if world > 1:
+        out["config"]["parallelism"] = f"queries split over {world} GPU(s), item matrix replicated"
+    if with_cpu and world == 1:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import knn as oracle_knn  # checker / baseline only
         from cpu_baseline import host_cores
@@ -296,11 +323,15 @@ def main():
         t_step = float(t_max.item()); pairs, rows, n_events = (float(x) for x in tot.tolist())
     else:
         n_events = ev.n_events
-    if rank != 0:  # the other ranks join the sharded config-5 run, then leave
-        if args.cand_steps > 0:
-            del dev, tab
+    if rank != 0:  # the other ranks join the sharded kNN and config-5 runs, then leave
+        del dev, tab
+        ctx.trim()
+        torch.cuda.empty_cache()
+        if args.knn_steps > 0:
+            bench_knn(args.knn_steps, 1, args.knn_items, args.knn_queries, False, dist.group.WORLD)
             ctx.trim()
             torch.cuda.empty_cache()
+        if args.cand_steps > 0:
             try:
                 bench_candidates(args.cand_sessions, args.cand_steps, args.kmeans_iter, dist.group.WORLD)
             except Exception:  # noqa: BLE001  (rank 0 reports the error)
@@ -355,13 +386,14 @@ def main():
     }
     if not args.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(args.seed, args.pandas_files)
-    if args.knn_steps > 0 and world == 1:
+    if args.knn_steps > 0:
         del dev
         ctx.trim()  # each sub-benchmark starts from an empty workspace (its own buffers only)
         torch.cuda.empty_cache()
-        out["knn"] = bench_knn(args.knn_steps, 1, args.knn_items, args.knn_queries, not args.no_cpu)
+        out["knn"] = bench_knn(args.knn_steps, 1, args.knn_items, args.knn_queries, not args.no_cpu and world == 1,
+                               dist.group.WORLD if world > 1 else None)
     if args.cand_steps > 0:
-        if world > 1:
+        if world > 1 and args.knn_steps == 0:
             del dev
         ctx.trim()
         torch.cuda.empty_cache()
