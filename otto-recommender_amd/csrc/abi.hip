@@ -390,6 +390,12 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   if (rdbg & 1) Osort.cap = 0;
   int herr = 0;
 
+  static const int split_mean = getenv("OTTOHIP_SPLIT_MEAN") ? atoi(getenv("OTTOHIP_SPLIT_MEAN")) : SPLIT_MEAN;
+  if (split_mean != SPLIT_MEAN) {
+    const uint32_t v = (uint32_t)std::max(64, split_mean);
+    OH_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_split_mean), &v, sizeof v, 0, hipMemcpyHostToDevice, s));
+    OH_HIP(hipStreamSynchronize(s));
+  }
   int ph = ctx->begin("reduce", s, 4.0 * (double)P);
   // level 0 task lists come from the rows
   uint64_t cap0 = (uint64_t)std::max<int64_t>(Rn, 1);

@@ -25,7 +25,8 @@ namespace ottohip {
 
 constexpr int EV_BLOCK = 256;     // events per wave block (sessions starting in it)
 constexpr int LCAP = 512;         // sessions up to LCAP events run from LDS
-constexpr int SPLIT_MEAN = 420;   // hashed split buckets average at most this many words
+constexpr int SPLIT_MEAN = 420;   // hashed split buckets average at most this many words (default)
+__constant__ uint32_t c_split_mean = SPLIT_MEAN;  // OTTOHIP_SPLIT_MEAN overrides it (A/B switch, abi.hip)
 constexpr uint32_t W_EMPTY = 0xFFFFFFFFu;
 constexpr int STAT_STRIPES = 256;            // copies of the per-rule statistics
 constexpr int STAT_STRIDE = MAX_RULES * 4;   // u64 per copy (256 B: one L2 line pair per stripe)
@@ -1536,7 +1537,7 @@ constexpr int SPLIT_T = 256;
 // hashed buckets average <= SPLIT_MEAN words and almost all fit the 512-word register sort.
 constexpr int SPLIT_DMAX = 256;  // digits per split level (1024 measured slower: 47.6 vs 46.1 ms reduce)
 __device__ __forceinline__ uint32_t split_ndig(const Task& t) {
-  const uint64_t d = ((uint64_t)t.len + SPLIT_MEAN - 1) / SPLIT_MEAN;
+  const uint64_t d = ((uint64_t)t.len + c_split_mean - 1) / c_split_mean;
   return d < 2 ? 2u : (d > (uint64_t)SPLIT_DMAX ? (uint32_t)SPLIT_DMAX : (uint32_t)d);
 }
 // Split digit: a hash of the word's (rule, aid_next) part, seeded by the split level, scaled to
