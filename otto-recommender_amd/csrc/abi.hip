@@ -414,6 +414,12 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   hipMemsetAsync(lcount, 0, 8 * 8, s);
   k_classify_rows<<<grid_for(Rn), 256, 0, s>>>(row_begin, Rn, P, Lt.WB, TL, err);
   const int agg_grid = ctx->n_cu * 8;
+  static const bool overlap = !(getenv("OTTOHIP_REDUCE_OVERLAP") && !strcmp(getenv("OTTOHIP_REDUCE_OVERLAP"), "0"));
+  hipStream_t s2 = nullptr;
+  if (overlap) {
+    OH_TRY(ctx->aux_stream());
+    s2 = ctx->aux;
+  }
   bool srcA = true;
   bool drained = false;
   const bool dbg = getenv("OTTOHIP_DEBUG") != nullptr;
@@ -438,12 +444,18 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
       fprintf(stderr, "\n");
     }
     const unsigned sgrid = (unsigned)ctx->n_cu * 32;
+    // the register-sort tasks of this level run on the aux stream, beside this level's hash and
+    // split on s (VALU-bound sorts next to the LDS/HBM-bound split); their task lists are only
+    // rewritten by the next level's classify, which waits for them (ev_join)
+    hipStream_t ss = s2 ? s2 : s;
+    if (s2) { OH_HIP(hipEventRecord(ctx->ev_fork, s)); OH_HIP(hipStreamWaitEvent(s2, ctx->ev_fork, 0)); }
 #define OH_SORT(c, M)                                                                                      \
     if (nlist[c])                                                                                          \
-      k_agg_sort<M><<<(unsigned)std::min<uint64_t>(ceil_div((int64_t)nlist[c], 4), sgrid), 256, 0, s>>>(   \
+      k_agg_sort<M><<<(unsigned)std::min<uint64_t>(ceil_div((int64_t)nlist[c], 4), sgrid), 256, 0, ss>>>(  \
           TL.sort[c], (int64_t)nlist[c], w0, w1, row_key, R, Lt, n_rules, Osort);
     OH_SORT(0, 1) OH_SORT(1, 2) OH_SORT(2, 4) OH_SORT(3, 8) OH_SORT(4, 16)
 #undef OH_SORT
+    if (s2) OH_HIP(hipEventRecord(ctx->ev_join, s2));
     if (nlist[N_SORT]) {  // tasks that overflow the LDS table are appended to the split list
       k_agg_hash<<<(unsigned)std::min<uint64_t>(nlist[N_SORT], (uint64_t)agg_grid), AGG_T, 0, s>>>(
           TL.hash, (int64_t)nlist[N_SORT], w0, w1, row_key, R, Lt, n_rules, O, TL.split, lcount + N_SORT + 1);
@@ -451,7 +463,11 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     }
     const int64_t ns = (int64_t)nlist[N_SORT + 1];
     if (dbg) fprintf(stderr, "[ottohip] level %d: split after hash overflow %lld\n", level, (long long)ns);
-    if (ns == 0) { drained = true; break; }
+    if (ns == 0) {
+      if (s2) OH_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0));
+      drained = true;
+      break;
+    }
     if ((uint64_t)ns > TL.cap) { set_error("split list overflow"); return OTTOHIP_ELIMIT; }
     Task* cur_split = TL.split;
     // chunk / digit / count-matrix bases
@@ -482,7 +498,9 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
       k_split_scatter<8192><<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, hoff, w0, w1, Lt.F);
     else
       k_split_scatter<4096><<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, hoff, w0, w1, Lt.F);
-    // next lists (a sub-bucket is one task in exactly one list: ndig bounds every list)
+    // next lists (a sub-bucket is one task in exactly one list: ndig bounds every list); this
+    // level's sorts still read the current lists
+    if (s2) OH_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0));
     const uint64_t capn = (uint64_t)ndig;
     if ((rc = get_lists(std::max(cap0, capn), srcA ? "t_splitB" : "t_splitA"))) return rc;
     hipMemsetAsync(lcount, 0, 8 * 8, s);
@@ -538,6 +556,7 @@ void ottohip_ctx_destroy(ottohip_ctx* ctx) {
   ctx->ws.release();
   ctx->spare.release();
   dev_trim();
+  if (ctx->aux) { hipStreamDestroy(ctx->aux); hipEventDestroy(ctx->ev_fork); hipEventDestroy(ctx->ev_join); }
   for (auto e : ctx->event_pool) hipEventDestroy(e);
   if (ctx->pinned) hipHostFree(ctx->pinned);
   delete ctx;

@@ -86,6 +86,19 @@ struct Ctx {
   std::vector<Phase> phases;
   std::vector<hipEvent_t> event_pool;
   size_t event_used = 0;
+  // second stream of the reduce (register-sort tasks overlap the split of the same level)
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  int aux_stream() {
+    if (aux) return 0;
+    if (hipStreamCreateWithFlags(&aux, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) != hipSuccess) {
+      set_error("aux stream creation failed");
+      return OTTOHIP_EHIP;
+    }
+    return 0;
+  }
   hipEvent_t take_event() {
     if (event_used == event_pool.size()) {
       hipEvent_t e; hipEventCreate(&e); event_pool.push_back(e);
