@@ -401,16 +401,19 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   uint64_t cap0 = (uint64_t)std::max<int64_t>(Rn, 1);
   TaskLists TL;
   TL.n = lcount;
-  auto get_lists = [&](uint64_t capl, const char* split_name) -> int {
-    static const char* names[N_SORT] = {"t_sort0", "t_sort1", "t_sort2", "t_sort3", "t_sort4"};
+  // task lists double-buffered by level parity: level l's sorts (aux stream) may still read theirs
+  // while level l + 1's classify fills the other set
+  auto get_lists = [&](uint64_t capl, const char* split_name, int parity) -> int {
+    static const char* names[2][N_SORT] = {{"t_sort0", "t_sort1", "t_sort2", "t_sort3", "t_sort4"},
+                                           {"t_sort0b", "t_sort1b", "t_sort2b", "t_sort3b", "t_sort4b"}};
     for (int c = 0; c < N_SORT; ++c)
-      if (int r = ws.get(names[c], capl * sizeof(Task), reinterpret_cast<void**>(&TL.sort[c]))) return r;
-    if (int r = ws.get("t_hash", capl * sizeof(Task), reinterpret_cast<void**>(&TL.hash))) return r;
+      if (int r = ws.get(names[parity][c], capl * sizeof(Task), reinterpret_cast<void**>(&TL.sort[c]))) return r;
+    if (int r = ws.get(parity ? "t_hashb" : "t_hash", capl * sizeof(Task), reinterpret_cast<void**>(&TL.hash))) return r;
     if (int r = ws.get(split_name, capl * sizeof(Task), reinterpret_cast<void**>(&TL.split))) return r;
     TL.cap = capl;
     return 0;
   };
-  if ((rc = get_lists(cap0, "t_splitA"))) return rc;
+  if ((rc = get_lists(cap0, "t_splitA", 0))) return rc;
   hipMemsetAsync(lcount, 0, 8 * 8, s);
   k_classify_rows<<<grid_for(Rn), 256, 0, s>>>(row_begin, Rn, P, Lt.WB, TL, err);
   const int agg_grid = ctx->n_cu * 8;
@@ -455,7 +458,7 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
           TL.sort[c], (int64_t)nlist[c], w0, w1, row_key, R, Lt, n_rules, Osort);
     OH_SORT(0, 1) OH_SORT(1, 2) OH_SORT(2, 4) OH_SORT(3, 8) OH_SORT(4, 16)
 #undef OH_SORT
-    if (s2) OH_HIP(hipEventRecord(ctx->ev_join, s2));
+    if (s2) OH_HIP(hipEventRecord(ctx->ev_join[level & 1], s2));
     if (nlist[N_SORT]) {  // tasks that overflow the LDS table are appended to the split list
       k_agg_hash<<<(unsigned)std::min<uint64_t>(nlist[N_SORT], (uint64_t)agg_grid), AGG_T, 0, s>>>(
           TL.hash, (int64_t)nlist[N_SORT], w0, w1, row_key, R, Lt, n_rules, O, TL.split, lcount + N_SORT + 1);
@@ -464,7 +467,7 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     const int64_t ns = (int64_t)nlist[N_SORT + 1];
     if (dbg) fprintf(stderr, "[ottohip] level %d: split after hash overflow %lld\n", level, (long long)ns);
     if (ns == 0) {
-      if (s2) OH_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0));
+      if (s2) OH_HIP(hipStreamWaitEvent(s, ctx->ev_join[level & 1], 0));
       drained = true;
       break;
     }
@@ -498,11 +501,11 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
       k_split_scatter<8192><<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, hoff, w0, w1, Lt.F);
     else
       k_split_scatter<4096><<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, hoff, w0, w1, Lt.F);
-    // next lists (a sub-bucket is one task in exactly one list: ndig bounds every list); this
-    // level's sorts still read the current lists
-    if (s2) OH_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0));
+    // next lists (a sub-bucket is one task in exactly one list: ndig bounds every list): the other
+    // parity's set, last read by the sorts of level - 1
+    if (s2 && level >= 1) OH_HIP(hipStreamWaitEvent(s, ctx->ev_join[(level + 1) & 1], 0));
     const uint64_t capn = (uint64_t)ndig;
-    if ((rc = get_lists(std::max(cap0, capn), srcA ? "t_splitB" : "t_splitA"))) return rc;
+    if ((rc = get_lists(std::max(cap0, capn), srcA ? "t_splitB" : "t_splitA", (level + 1) & 1))) return rc;
     hipMemsetAsync(lcount, 0, 8 * 8, s);
     k_split_classify<<<grid_for(ndig), 256, 0, s>>>(cur_split, ns, dgb, mtb, hoff, ndig, TL, err);
     srcA = !srcA;
@@ -556,7 +559,12 @@ void ottohip_ctx_destroy(ottohip_ctx* ctx) {
   ctx->ws.release();
   ctx->spare.release();
   dev_trim();
-  if (ctx->aux) { hipStreamDestroy(ctx->aux); hipEventDestroy(ctx->ev_fork); hipEventDestroy(ctx->ev_join); }
+  if (ctx->aux) {
+    hipStreamDestroy(ctx->aux);
+    hipEventDestroy(ctx->ev_fork);
+    hipEventDestroy(ctx->ev_join[0]);
+    hipEventDestroy(ctx->ev_join[1]);
+  }
   for (auto e : ctx->event_pool) hipEventDestroy(e);
   if (ctx->pinned) hipHostFree(ctx->pinned);
   delete ctx;

@@ -88,12 +88,13 @@ struct Ctx {
   size_t event_used = 0;
   // second stream of the reduce (register-sort tasks overlap the split of the same level)
   hipStream_t aux = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};  // join: by reduce level parity
   int aux_stream() {
     if (aux) return 0;
     if (hipStreamCreateWithFlags(&aux, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&ev_join[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ev_join[1], hipEventDisableTiming) != hipSuccess) {
       set_error("aux stream creation failed");
       return OTTOHIP_EHIP;
     }
