@@ -26,7 +26,7 @@ constexpr int KN_QW = 64;                // queries per wave (two 32-column MFMA
 constexpr int KN_WAVES = 8;
 constexpr int KN_T = 64 * KN_WAVES;      // 512 threads
 constexpr int KN_QB = KN_QW * KN_WAVES;  // 256 queries per workgroup
-constexpr int KN_IT = 128;               // items per LDS tile (4 row-blocks of 32)
+constexpr int KN_IT = 256;               // items per LDS tile (8 row-blocks of 32)
 constexpr int KN_C = 24;                 // candidates per query (k = 20 plus a rerank margin)
 constexpr int KN_CAND = 64;              // rerank width (2 * KN_C candidates, padded)
 constexpr int PRE_STRIDE = 16;           // threshold pre-pass: every 16th item tile
@@ -74,10 +74,11 @@ __global__ void k_knn_pack(const float* __restrict__ emb, int64_t n, int dim, co
 // 64 queries per wave: two 32x32 output blocks (queries qbase + [0, 32) and qbase + [32, 64))
 // share every item fragment; v_permlane32_swap then gives each lane ONE query with all 32 item
 // scores of a row-block, so each query keeps a single register list of KN_C candidates.
-// Item tiles stream into a 3-slot LDS ring by LDS-DMA (global_load_lds_dwordx4, 4 per thread
-// per tile, one tile in flight behind the one being computed): counted vmcnt + raw s_barrier.
-constexpr int KN_RING = 3;
-constexpr int KN_GL = KN_IT * KN_CH / KN_T;  // glds per thread per tile (4)
+// Item tiles of 256 items stream into two LDS slots by LDS-DMA (global_load_lds_dwordx4, 8 per
+// thread per tile; the next tile is in flight while this one is scored): vmcnt + raw s_barrier,
+// one barrier per 256 items.
+constexpr int KN_RING = 2;
+constexpr int KN_GL = KN_IT * KN_CH / KN_T;  // glds per thread per tile (8)
 
 // MODE 0: full scan with top-KN_C inserts, the list starting at thr_io[q] (if given).
 // MODE 1: ablation (scores only).  MODE 2: threshold pre-pass over tiles 0, 16, 32, ... (never
@@ -89,7 +90,7 @@ template <int ABL>
 __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ items, int64_t V,
                                                   const uint4* __restrict__ queries, int64_t nq,
                                                   uint32_t* __restrict__ cand, float* __restrict__ thr_io) {
-  __shared__ uint4 ring[KN_RING * KN_IT * KN_CH];  // 3 x 32 KiB, the only LDS object
+  __shared__ uint4 ring[KN_RING * KN_IT * KN_CH];  // 2 x 64 KiB, the only LDS object
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, r = l & 31, h = l >> 5;
   const int64_t qbase = (int64_t)blockIdx.x * KN_QB + w * 64;
   const auto probe = __builtin_amdgcn_permlane32_swap((unsigned)l, (unsigned)(l + 64), false, false);
@@ -155,17 +156,17 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
     sc[0] = fmaxf(sc[0], s_);
     thr = sc[KN_C - 1];
   };
+  static_assert(KN_RING == 2, "double-buffered tiles: one tile in flight while the other is scored");
   issue(0);
-  if (nT > 1) issue(1);
   for (int64_t t = 0; t < nT; ++t) {
-    if (t + 1 < nT) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // == KN_GL: tile t+1 may fly
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // tile t visible to all waves; slot (t+2)%3 = (t-1)%3 is free
-    if (t + 2 < nT) issue(t + 2);
-    const uint4* T = ring + (int)(t % KN_RING) * (KN_IT * KN_CH);
-    // item fragments run two k-steps ahead over the tile's 16 (row-block pair, k-step) steps, so a
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's share of tile t has landed
+    __builtin_amdgcn_s_barrier();  // tile t visible to all waves; slot (t+1) % 2 = (t-1) % 2 is free
+    if (t + 1 < nT) issue(t + 1);
+    const uint4* T = ring + (int)(t & 1) * (KN_IT * KN_CH);
+    // item fragments run two k-steps ahead over the tile's (row-block pair, k-step) steps, so a
     // step's LDS reads have two steps of MFMAs to land (one step's 4 MFMAs did not cover them)
-    bf16x8 F0[16], F1[16];
+    constexpr int NSTEP = (KN_IT / 64) * 8;  // (row-block pair, k-step) steps of a tile
+    bf16x8 F0[NSTEP], F1[NSTEP];
     auto ld = [&](int g) __attribute__((always_inline)) {
       const int row0 = (2 * (g >> 3)) * 32 + r, row1 = row0 + 32, s_ = g & 7;
       F0[g] = __builtin_bit_cast(bf16x8, T[row0 * KN_CH + ((2 * s_ + h) ^ (row0 & 15))]);
@@ -175,9 +176,9 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
     ld(1);
     f32x16 accA[2], accB[2];
 #pragma clang loop unroll(full)
-    for (int g = 0; g < 16; ++g) {
+    for (int g = 0; g < NSTEP; ++g) {
       const int rp = g >> 3, s = g & 7;
-      if (g + 2 < 16) ld(g + 2);
+      if (g + 2 < NSTEP) ld(g + 2);
       if (s == 0) { accA[0] = {}; accA[1] = {}; accB[0] = {}; accB[1] = {}; }
       accA[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F0[g], bqa[s], accA[0], 0, 0, 0);
       accB[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F0[g], bqb[s], accB[0], 0, 0, 0);
