@@ -5,11 +5,12 @@
 //   1. k_knn_pack: items -> bf16 [V x 128]; columns [0, dim) = v, columns dim, dim+1 = hi/lo
 //      bf16 split of -|v|^2 / 2, rest 0. Queries -> bf16 [Q x 128] with 1, 1 in those columns.
 //      One MFMA product then gives s = q.v - |v|^2/2, and |q - v|^2 = |q|^2 - 2 s ranks like -s.
-//   2. k_knn_main: v_mfma_f32_32x32x16_bf16 with items as A (64-item tiles staged through LDS,
-//      XOR-swizzled 16-B chunks, double-buffered) and 32 queries per wave held in registers
-//      as B; accumulator lane = query, 16 item scores per lane. Each lane keeps the best 32
-//      scores it saw (threshold test, rare register insert): 64 candidates per query.
-//   3. k_knn_rerank: one wave per query recomputes |q - v|^2 exactly in fp32 for the 64
+//   2. k_knn_main<2> (pre-pass, every 16th item tile): a lower bound of each query's KN_C-th
+//      best score. k_knn_main<0>: v_mfma_f32_32x32x16_bf16 with items as A (256-item tiles
+//      streamed into two LDS slots by LDS-DMA, XOR-swizzled 16-B chunks) and 64 queries per
+//      wave held in registers as B; after a lane swap each lane owns one query and keeps its
+//      KN_C best (score, item) in a sorted register list, inserting only above the bound.
+//   3. k_knn_rerank: one wave per query recomputes |q - v|^2 exactly in fp32 for the KN_C
 //      candidates and sorts by (d2, index): the top-k rows and their exact squared distances.
 #include <cmath>
 #include <cstdlib>
@@ -81,11 +82,11 @@ constexpr int KN_RING = 2;
 constexpr int KN_GL = KN_IT * KN_CH / KN_T;  // glds per thread per tile (8)
 
 // MODE 0: full scan with top-KN_C inserts, the list starting at thr_io[q] (if given).
-// MODE 1: ablation (scores only).  MODE 2: threshold pre-pass over tiles 0, 16, 32, ... (never
-//   the last, partial tile): the maxima of the scanned tiles fold into KN_C groups; each group
-//   holds distinct items, one of them scoring >= the group maximum, so min(group maxima) is a
-//   lower bound of the query's KN_C-th best score -> thr_io[q]. MODE 0 then inserts only items
-//   above it (about 3x fewer divergent inserts than starting from -inf).
+// MODE 1: ablation (scores only).  MODE 3: ablation without the item stream (timing only).
+// MODE 2: threshold pre-pass over tiles 0, 16, 32, ... (never the last, partial tile): the
+//   KN_C largest 32-item block maxima of the sampled tiles, a sorted list per query; KN_C
+//   distinct blocks each hold an item scoring >= their maximum, so the KN_C-th of them is a lower
+//   bound of the query's KN_C-th best score -> thr_io[q]. MODE 0 then inserts only items above it.
 template <int ABL>
 __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ items, int64_t V,
                                                   const uint4* __restrict__ queries, int64_t nq,
@@ -195,11 +196,8 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
         const auto msw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mA), __float_as_uint(mB), false, false);
         const float m = fmaxf(__uint_as_float(msw[0]), __uint_as_float(msw[1]));
         if (ABL == 1 || ABL == 3) { thr = fmaxf(thr, m * 1e-30f); continue; }  // ablation builds: no candidate handling
-        if (PRE) {  // group g = tile % KN_C keeps its maximum in sc[g]
-          const int gsel = (int)(t % KN_C);
-#pragma unroll
-          for (int gg = 0; gg < KN_C; ++gg)
-            if (gg == gsel) sc[gg] = fmaxf(sc[gg], m);
+        if (PRE) {  // the sampled blocks' KN_C largest maxima (sorted list, no indices)
+          if (m > thr) insert(m, 0u);
           continue;
         }
         if (__ballot(m > thr)) {
@@ -238,11 +236,9 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
     }
   }
   if ((ABL == 1 || ABL == 3) && thr == 12345.f) ix[0] = 0;  // keep the ablated scores live
-  if (PRE) {
-    float b = sc[0];
-#pragma unroll
-    for (int g = 1; g < KN_C; ++g) b = fminf(b, sc[g]);
-    if (q < nq) thr_io[q] = nextafterf(b, -INFINITY);  // items tying the bound are still inserted
+  if (PRE) {  // KN_C distinct blocks hold an item scoring >= their maximum: the KN_C-th largest
+              // sampled block maximum is a lower bound of the query's KN_C-th best score
+    if (q < nq) thr_io[q] = nextafterf(sc[KN_C - 1], -INFINITY);  // items tying the bound are still inserted
     return;
   }
   if (q < nq) {
