@@ -87,7 +87,9 @@ constexpr int KN_GL = KN_IT * KN_CH / KN_T;  // glds per thread per tile (8)
 //   KN_C largest 32-item block maxima of the sampled tiles, a sorted list per query; KN_C
 //   distinct blocks each hold an item scoring >= their maximum, so the KN_C-th of them is a lower
 //   bound of the query's KN_C-th best score -> thr_io[q]. MODE 0 then inserts only items above it.
-template <int ABL>
+// KS = k-steps of 16 over the packed row: ceil((dim + 2) / 16) rounded up to 7 or 8 (dim 100 -> 7,
+// so the zero padding of columns 112..127 is neither streamed nor multiplied).
+template <int ABL, int KS>
 __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ items, int64_t V,
                                                   const uint4* __restrict__ queries, int64_t nq,
                                                   uint32_t* __restrict__ cand, float* __restrict__ thr_io) {
@@ -98,9 +100,10 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
   const bool semA = __builtin_amdgcn_readfirstlane(probe[1]) == 32u;  // vsrc lane 0 received vdst lane 32
   const int64_t q = semA ? qbase + l : qbase + ((l + 32) & 63);
   const int offx = semA ? 0 : 4, offy = 4 - offx;
-  bf16x8 bqa[8], bqb[8];
+  static_assert(KS >= 1 && KS <= KN_KD / 16, "k-steps");
+  bf16x8 bqa[KS], bqb[KS];
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {
+  for (int s = 0; s < KS; ++s) {
     const int64_t qa = qbase + r, qb = qbase + 32 + r;
     uint4 ua = make_uint4(0, 0, 0, 0), ub = make_uint4(0, 0, 0, 0);
     if (qa < nq) ua = queries[qa * KN_CH + 2 * s + h];
@@ -123,7 +126,8 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
     thr = b;
   }
   // LDS chunk p = u*512 + tid holds item row p>>4, source chunk (p & 15) ^ (row & 15);
-  // rows past V read row V-1 (valid memory; their scores are masked below)
+  // rows past V read row V-1 (valid memory; their scores are masked below); source chunks past
+  // the KS k-steps (zero padding) are not fetched and never read
   auto issue = [&](int64_t t) {
     if (ABL == 3 && t >= KN_RING) return;  // ablation: item stream off after the first tiles (timing only)
     uint4* dst = ring + (int)(t % KN_RING) * (KN_IT * KN_CH);
@@ -133,6 +137,7 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
       const int p = u * KN_T + tid, row = p >> 4, c = p & 15;
       int64_t item = tt * KN_IT + row;
       if (item >= V) item = V - 1;
+      if (KS < KN_KD / 16 && (c ^ (row & 15)) >= 2 * KS) continue;
       __builtin_amdgcn_global_load_lds(items + item * KN_CH + (c ^ (row & 15)), dst + u * KN_T + w * 64, 16, 0, 0);
     }
   };
@@ -166,10 +171,10 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
     const uint4* T = ring + (int)(t & 1) * (KN_IT * KN_CH);
     // item fragments run two k-steps ahead over the tile's (row-block pair, k-step) steps, so a
     // step's LDS reads have two steps of MFMAs to land (one step's 4 MFMAs did not cover them)
-    constexpr int NSTEP = (KN_IT / 64) * 8;  // (row-block pair, k-step) steps of a tile
+    constexpr int NSTEP = (KN_IT / 64) * KS;  // (row-block pair, k-step) steps of a tile
     bf16x8 F0[NSTEP], F1[NSTEP];
     auto ld = [&](int g) __attribute__((always_inline)) {
-      const int row0 = (2 * (g >> 3)) * 32 + r, row1 = row0 + 32, s_ = g & 7;
+      const int row0 = (2 * (g / KS)) * 32 + r, row1 = row0 + 32, s_ = g % KS;
       F0[g] = __builtin_bit_cast(bf16x8, T[row0 * KN_CH + ((2 * s_ + h) ^ (row0 & 15))]);
       F1[g] = __builtin_bit_cast(bf16x8, T[row1 * KN_CH + ((2 * s_ + h) ^ (row1 & 15))]);
     };
@@ -178,14 +183,14 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
     f32x16 accA[2], accB[2];
 #pragma clang loop unroll(full)
     for (int g = 0; g < NSTEP; ++g) {
-      const int rp = g >> 3, s = g & 7;
+      const int rp = g / KS, s = g % KS;
       if (g + 2 < NSTEP) ld(g + 2);
       if (s == 0) { accA[0] = {}; accA[1] = {}; accB[0] = {}; accB[1] = {}; }
       accA[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F0[g], bqa[s], accA[0], 0, 0, 0);
       accB[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F0[g], bqb[s], accB[0], 0, 0, 0);
       accA[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F1[g], bqa[s], accA[1], 0, 0, 0);
       accB[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F1[g], bqb[s], accB[1], 0, 0, 0);
-      if (s != 7) continue;
+      if (s != KS - 1) continue;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         // per-lane maxima first: swapping the two maxima gives this lane's query maximum over the
@@ -371,16 +376,18 @@ int ottohip_knn_topk(ottohip_ctx* c, const ottohip_knn_index* ix, const int32_t*
   const unsigned grid = (unsigned)ceil_div(n_q, KN_QB);
   const int64_t nT = ceil_div(ix->n_items, KN_IT);
   float* thr = nullptr;
+  const bool k8 = ix->dim + 2 > 7 * 16;
   if (!abl && !nopre && (nT - 1) / PRE_STRIDE >= KN_C) {  // enough sampled tiles for KN_C groups
     OH_TRY(ctx->ws.get("knn_thr", (size_t)n_q, &thr));
     const int64_t nS = (nT - 1 + PRE_STRIDE - 1) / PRE_STRIDE;
     ph = ctx->begin("knn_pre", s, 2.0 * (double)n_q * (double)(nS * KN_IT) * ix->dim);
-    k_knn_main<2><<<grid, KN_T, 0, s>>>(reinterpret_cast<const uint4*>(ix->packed), ix->n_items,
+    (k8 ? k_knn_main<2, 8> : k_knn_main<2, 7>)<<<grid, KN_T, 0, s>>>(reinterpret_cast<const uint4*>(ix->packed), ix->n_items,
                                           reinterpret_cast<const uint4*>(qp), n_q, cand, thr);
     ctx->end(ph, s);
   }
   ph = ctx->begin("knn_main", s, 2.0 * (double)n_q * (double)ix->n_items * ix->dim);
-  auto kmain = abl == 3 ? k_knn_main<3> : (abl ? k_knn_main<1> : k_knn_main<0>);
+  auto kmain = k8 ? (abl == 3 ? k_knn_main<3, 8> : (abl ? k_knn_main<1, 8> : k_knn_main<0, 8>))
+                  : (abl == 3 ? k_knn_main<3, 7> : (abl ? k_knn_main<1, 7> : k_knn_main<0, 7>));
   kmain<<<grid, KN_T, 0, s>>>(reinterpret_cast<const uint4*>(ix->packed), ix->n_items,
                               reinterpret_cast<const uint4*>(qp), n_q, cand, thr);
   ctx->end(ph, s);

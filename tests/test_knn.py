@@ -50,6 +50,21 @@ def test_knn_arbitrary_rows_tiny_index_and_ties(gpu):
     assert list(i2.cpu().numpy()[0][5:]) == [-1, -1, -1] and np.all(np.isinf(d2.cpu().numpy()[:, 5:]))
 
 
+@pytest.mark.parametrize("dim", [16, 110, 111, 126])
+def test_knn_dims_around_the_k_step_split(gpu, dim):
+    """dim + 2 <= 112 runs 7 k-steps of 16 (the zero padding is neither streamed nor multiplied),
+    larger dims 8: both sides of the split and the smallest/largest dims."""
+    from otto_recommender_amd.w2vec import KnnIndex
+    rng = np.random.default_rng(dim)
+    emb = rng.normal(size=(9_000, dim)).astype(np.float32)
+    ix = KnnIndex(emb)
+    rows = np.arange(0, 9_000, 7)
+    i, d = ix.search(rows, k=20)
+    gi, gd = i.cpu().numpy(), d.cpu().numpy()
+    assert np.all(gi[:, 0] == rows) and np.all(gd[:, 0] == 0)
+    _check(emb, rows, 20, gi, gd)
+
+
 def test_get_top_k_similar_faiss_frame(gpu):
     from otto_recommender_amd import w2vec
     emb = synth.embeddings(5000, seed=2)
