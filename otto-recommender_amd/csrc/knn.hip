@@ -162,6 +162,60 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
     sc[0] = fmaxf(sc[0], s_);
     thr = sc[KN_C - 1];
   };
+  // one 32-item row-block's scores (accumulators pA = queries qbase + [0, 32), pB = + [32, 64))
+  // into the lists. Per-lane maxima first: swapping the two maxima gives this lane's query maximum
+  // over the 32 rows, and the 16-register redistribution runs only when some lane has a candidate.
+  auto drain = [&](f32x16& pA, f32x16& pB, int64_t ib) __attribute__((always_inline)) {
+    float mA = pA[0], mB = pB[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) { mA = fmaxf(mA, pA[i]); mB = fmaxf(mB, pB[i]); }
+    const auto msw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mA), __float_as_uint(mB), false, false);
+    const float m = fmaxf(__uint_as_float(msw[0]), __uint_as_float(msw[1]));
+    if (ABL == 1 || ABL == 3) { thr = fmaxf(thr, m * 1e-30f); return; }  // ablation builds: no candidate handling
+    if (PRE) {  // the sampled blocks' KN_C largest maxima (sorted list, no indices)
+      if (m > thr) insert(m, 0u);
+      return;
+    }
+    if (__ballot(m > thr)) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {  // pA -> rows + offx, pB -> rows + offy of this lane's query
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(pA[i]), __float_as_uint(pB[i]), false, false);
+        pA[i] = __uint_as_float(sw[0]);
+        pB[i] = __uint_as_float(sw[1]);
+      }
+    }
+    if (m > thr) {
+      // this lane's 32 scores of the block as unique keys: the row slot j (0..31) replaces the
+      // 5 low mantissa bits (32 ulp, far below the bf16 inputs' error), so the best remaining
+      // candidate is one max over keys below the last one taken, and its key names its row
+      float kf[32];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        kf[i] = __uint_as_float((__float_as_uint(pA[i]) & ~31u) | (uint32_t)i);
+        kf[16 + i] = __uint_as_float((__float_as_uint(pB[i]) & ~31u) | (uint32_t)(16 + i));
+      }
+      float last = INFINITY;
+      while (true) {
+        float cur = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) cur = fmaxf(cur, kf[j] < last ? kf[j] : -INFINITY);
+        if (!(cur > thr)) break;
+        const uint32_t j = __float_as_uint(cur) & 31u, i = j & 15u;
+        const int64_t item = ib + (i & 3) + 8 * (i >> 2) + (j < 16 ? offx : offy);
+        if (item < V) insert(cur, (uint32_t)item);
+        last = cur;
+      }
+    }
+  };
+  // Row-blocks are software-pipelined over two accumulator sets: block b accumulates in set b & 1
+  // while block b - 1 (the other set) is drained, so the drain's VALU work issues between block b's
+  // MFMAs instead of after them. A tile holds an even number of blocks, so block 0 of tile t drains
+  // block NBLK - 1 of tile t - 1 (set 1, -inf before the first tile).
+  constexpr int NBLK = KN_IT / 32;
+  static_assert(NBLK % 2 == 0, "even number of row-blocks per tile");
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { acc[1][0][i] = -INFINITY; acc[1][1][i] = -INFINITY; }
   static_assert(KN_RING == 2, "double-buffered tiles: one tile in flight while the other is scored");
   issue(0);
   for (int64_t t = 0; t < nT; ++t) {
@@ -169,77 +223,28 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
     __builtin_amdgcn_s_barrier();  // tile t visible to all waves; slot (t+1) % 2 = (t-1) % 2 is free
     if (t + 1 < nT) issue(t + 1);
     const uint4* T = ring + (int)(t & 1) * (KN_IT * KN_CH);
-    // item fragments run two k-steps ahead over the tile's (row-block pair, k-step) steps, so a
-    // step's LDS reads have two steps of MFMAs to land (one step's 4 MFMAs did not cover them)
-    constexpr int NSTEP = (KN_IT / 64) * KS;  // (row-block pair, k-step) steps of a tile
-    bf16x8 F0[NSTEP], F1[NSTEP];
+    // item fragments (one per (row-block, k-step) step, shared by the two query halves' MFMAs)
+    // are read three steps ahead
+    constexpr int NSTEP = NBLK * KS;
+    constexpr int AHEAD = 3;
+    bf16x8 F[NSTEP];
     auto ld = [&](int g) __attribute__((always_inline)) {
-      const int row0 = (2 * (g / KS)) * 32 + r, row1 = row0 + 32, s_ = g % KS;
-      F0[g] = __builtin_bit_cast(bf16x8, T[row0 * KN_CH + ((2 * s_ + h) ^ (row0 & 15))]);
-      F1[g] = __builtin_bit_cast(bf16x8, T[row1 * KN_CH + ((2 * s_ + h) ^ (row1 & 15))]);
+      const int row = (g / KS) * 32 + r, s_ = g % KS;
+      F[g] = __builtin_bit_cast(bf16x8, T[row * KN_CH + ((2 * s_ + h) ^ (row & 15))]);
     };
-    ld(0);
-    ld(1);
-    f32x16 accA[2], accB[2];
+#pragma unroll
+    for (int g = 0; g < AHEAD; ++g) ld(g);
 #pragma clang loop unroll(full)
     for (int g = 0; g < NSTEP; ++g) {
-      const int rp = g / KS, s = g % KS;
-      if (g + 2 < NSTEP) ld(g + 2);
-      if (s == 0) { accA[0] = {}; accA[1] = {}; accB[0] = {}; accB[1] = {}; }
-      accA[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F0[g], bqa[s], accA[0], 0, 0, 0);
-      accB[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F0[g], bqb[s], accB[0], 0, 0, 0);
-      accA[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F1[g], bqa[s], accA[1], 0, 0, 0);
-      accB[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F1[g], bqb[s], accB[1], 0, 0, 0);
-      if (s != KS - 1) continue;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        // per-lane maxima first: swapping the two maxima gives this lane's query maximum over the
-        // 32 rows, and the 16-register redistribution runs only when some lane has a candidate
-        float mA = accA[u][0], mB = accB[u][0];
-#pragma unroll
-        for (int i = 1; i < 16; ++i) { mA = fmaxf(mA, accA[u][i]); mB = fmaxf(mB, accB[u][i]); }
-        const auto msw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mA), __float_as_uint(mB), false, false);
-        const float m = fmaxf(__uint_as_float(msw[0]), __uint_as_float(msw[1]));
-        if (ABL == 1 || ABL == 3) { thr = fmaxf(thr, m * 1e-30f); continue; }  // ablation builds: no candidate handling
-        if (PRE) {  // the sampled blocks' KN_C largest maxima (sorted list, no indices)
-          if (m > thr) insert(m, 0u);
-          continue;
-        }
-        if (__ballot(m > thr)) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {  // accA -> rows + offx, accB -> rows + offy of this lane's query
-            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(accA[u][i]), __float_as_uint(accB[u][i]),
-                                                             false, false);
-            accA[u][i] = __uint_as_float(sw[0]);
-            accB[u][i] = __uint_as_float(sw[1]);
-          }
-        }
-        if (m > thr) {
-          // this lane's 32 scores of the block as unique keys: the row slot j (0..31) replaces the
-          // 5 low mantissa bits (32 ulp, far below the bf16 inputs' error), so the best remaining
-          // candidate is one max over keys below the last one taken, and its key names its row
-          const int64_t ib = t * KN_IT + (2 * rp + u) * 32;
-          float kf[32];
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            kf[i] = __uint_as_float((__float_as_uint(accA[u][i]) & ~31u) | (uint32_t)i);
-            kf[16 + i] = __uint_as_float((__float_as_uint(accB[u][i]) & ~31u) | (uint32_t)(16 + i));
-          }
-          float last = INFINITY;
-          while (true) {
-            float cur = -INFINITY;
-#pragma unroll
-            for (int j = 0; j < 32; ++j) cur = fmaxf(cur, kf[j] < last ? kf[j] : -INFINITY);
-            if (!(cur > thr)) break;
-            const uint32_t j = __float_as_uint(cur) & 31u, i = j & 15u;
-            const int64_t item = ib + (i & 3) + 8 * (i >> 2) + (j < 16 ? offx : offy);
-            if (item < V) insert(cur, (uint32_t)item);
-            last = cur;
-          }
-        }
-      }
+      const int b = g / KS, s = g % KS, c = b & 1;
+      if (g + AHEAD < NSTEP) ld(g + AHEAD);
+      if (s == 0) { acc[c][0] = {}; acc[c][1] = {}; }
+      acc[c][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[g], bqa[s], acc[c][0], 0, 0, 0);
+      acc[c][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[g], bqb[s], acc[c][1], 0, 0, 0);
+      if (s == KS - 1) drain(acc[c ^ 1][0], acc[c ^ 1][1], t * KN_IT + (int64_t)(b - 1) * 32);
     }
   }
+  drain(acc[1][0], acc[1][1], (nT - 1) * KN_IT + (int64_t)(NBLK - 1) * 32);  // the last block
   if ((ABL == 1 || ABL == 3) && thr == 12345.f) ix[0] = 0;  // keep the ablated scores live
   if (PRE) {  // KN_C distinct blocks hold an item scoring >= their maximum: the KN_C-th largest
               // sampled block maximum is a lower bound of the query's KN_C-th best score
