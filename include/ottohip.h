@@ -343,7 +343,7 @@ int ottohip_covis_reduce_received(ottohip_ctx* ctx, const ottohip_rule* rules, i
  * caller's fp32 embeddings [n_items x dim] (device, kept referenced) into a bf16 MFMA operand;
  * ottohip_knn_topk returns, per query row, the k nearest rows in ascending squared L2
  * distance (ties by row index), distances exact in fp32 (candidates from bf16 MFMA scores,
- * reranked). dim <= 126, k <= 64. query_rows (device, n_q) index the embedding rows
+ * reranked: 24 per query, 4 of margin). dim <= 126, k <= 20. query_rows (device, n_q) index the embedding rows
  * (get_top_k_similar_faiss queries words_q, a subset of words); NULL = rows 0..n_q-1. */
 typedef struct ottohip_knn_index ottohip_knn_index;
 int ottohip_knn_index_create(ottohip_ctx* ctx, const float* emb, int64_t n_items, int dim,

@@ -29,6 +29,7 @@ constexpr int KN_T = 64 * KN_WAVES;      // 512 threads
 constexpr int KN_QB = KN_QW * KN_WAVES;  // 256 queries per workgroup
 constexpr int KN_IT = 256;               // items per LDS tile (8 row-blocks of 32)
 constexpr int KN_C = 24;                 // candidates per query (k = 20 plus a rerank margin)
+constexpr int KN_KMAX = KN_C - 4;        // largest k: 4 candidates of margin for the bf16 scores' error
 constexpr int KN_CAND = 64;              // rerank width (2 * KN_C candidates, padded)
 constexpr int PRE_STRIDE = 16;           // threshold pre-pass: every 16th item tile
 
@@ -353,8 +354,8 @@ void ottohip_knn_index_free(ottohip_knn_index* ix) {
 
 int ottohip_knn_topk(ottohip_ctx* c, const ottohip_knn_index* ix, const int32_t* query_rows, int64_t n_q, int k,
                      int32_t* out_idx, float* out_d2, void* stream) {
-  if (!c || !ix || n_q < 0 || k < 1 || k > KN_CAND || !out_idx || !out_d2) {
-    set_error("knn_topk: bad arguments (1 <= k <= %d)", KN_CAND);
+  if (!c || !ix || n_q < 0 || k < 1 || k > KN_KMAX || !out_idx || !out_d2) {
+    set_error("knn_topk: bad arguments (1 <= k <= %d)", KN_KMAX);
     return OTTOHIP_EINVAL;
   }
   if (n_q == 0) return 0;
