@@ -189,17 +189,38 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
       // this lane's 32 scores of the block as unique keys: the row slot j (0..31) replaces the
       // 5 low mantissa bits (32 ulp, far below the bf16 inputs' error), so the best remaining
       // candidate is one max over keys below the last one taken, and its key names its row
-      float kf[32];
+      // (the keys overwrite the drained accumulators in place)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        kf[i] = __uint_as_float((__float_as_uint(pA[i]) & ~31u) | (uint32_t)i);
-        kf[16 + i] = __uint_as_float((__float_as_uint(pB[i]) & ~31u) | (uint32_t)(16 + i));
+        pA[i] = __uint_as_float((__float_as_uint(pA[i]) & ~31u) | (uint32_t)i);
+        pB[i] = __uint_as_float((__float_as_uint(pB[i]) & ~31u) | (uint32_t)(16 + i));
+      }
+      // the lane's two best keys in one pass (k2 = med3(k1, k2, x) before k1 = max(k1, x)); a
+      // block rarely holds a third candidate for one query, so the general "best key below the
+      // last taken" loop runs only after the second was inserted
+      float k1 = -INFINITY, k2 = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        k2 = __builtin_amdgcn_fmed3f(k1, k2, pA[j]);
+        k1 = fmaxf(k1, pA[j]);
+        k2 = __builtin_amdgcn_fmed3f(k1, k2, pB[j]);
+        k1 = fmaxf(k1, pB[j]);
       }
       float last = INFINITY;
-      while (true) {
-        float cur = -INFINITY;
+      for (int it = 0;; ++it) {  // it is the same on every lane still looping
+        float cur;
+        if (it == 0) {
+          cur = k1;
+        } else if (it == 1) {
+          cur = k2;
+        } else {
+          cur = -INFINITY;
 #pragma unroll
-        for (int j = 0; j < 32; ++j) cur = fmaxf(cur, kf[j] < last ? kf[j] : -INFINITY);
+          for (int j = 0; j < 16; ++j) {
+            cur = fmaxf(cur, pA[j] < last ? pA[j] : -INFINITY);
+            cur = fmaxf(cur, pB[j] < last ? pB[j] : -INFINITY);
+          }
+        }
         if (!(cur > thr)) break;
         const uint32_t j = __float_as_uint(cur) & 31u, i = j & 15u;
         const int64_t item = ib + (i & 3) + 8 * (i >> 2) + (j < 16 ? offx : offy);
