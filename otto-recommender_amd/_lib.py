@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libottohip.so")
+# OTTOHIP_LIB: another build of the same C-ABI (development A/B runs); default the in-tree library
+LIB_PATH = os.environ.get("OTTOHIP_LIB") or os.path.join(_HERE, "libottohip.so")
 
 OTTOHIP_ELIMIT = -5
 

@@ -1072,11 +1072,13 @@ constexpr uint32_t HASH_FULL = 0xFFFFFFFFu;  // hash_insert_batch: table full
 // ---- register sort path: one wave per task of <= 64*M words, no LDS, no atomics
 __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) { return dpp_incl_scan<true>(v); }
 
-// median of three: with c = 0 it is min(a, b), with c = ~0 max(a, b) (one VALU op)
+// median of three: with c = 0 it is min(a, b), with c = ~0 max(a, b). Written in C (the backend
+// folds min(max(min(a, b), c), max(a, b)) into one v_med3_u32): an inline-asm med3 is opaque to
+// the hazard recognizer, which then padded every following DPP move with s_nop
 __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
-  uint32_t r;
-  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
+  const uint32_t mn = a < b ? a : b, mx = a < b ? b : a;
+  const uint32_t t = mn > c ? mn : c;
+  return mx < t ? mx : t;
 }
 
 // Bitonic sort of 64*M keys held as v[m] = element (lane*M + m), ascending. Every
