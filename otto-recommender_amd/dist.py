@@ -11,6 +11,7 @@ backend, gloo on CPU for tests); compute is libottohip.so (csrc/shard.hip).
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -71,6 +72,31 @@ def exchange(send, send_counts, group=None, return_counts=False):
     dist.all_to_all_single(recv, src.contiguous(), recv_counts, [int(c) for c in send_counts], group=group)
     recv = recv if recv.device == send.device else recv.to(send.device)
     return (recv, recv_counts) if return_counts else recv
+
+
+def exchange_async(send, send_counts, group=None):
+    """exchange() with the payload all-to-all left in flight: the entry counts are exchanged at
+    once (the receive size), the payload returns a handle. finish_exchange(handle) waits and
+    returns the received tensor; meanwhile the current stream keeps computing (RCCL runs on its
+    own stream)."""
+    import torch
+    import torch.distributed as dist
+    dev = _comm_device(group)
+    sc = torch.tensor([int(c) for c in send_counts], dtype=torch.int64, device=dev)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=group)
+    recv_counts = [int(x) for x in rc.tolist()]
+    src = send if send.device == dev else send.to(dev)
+    recv = torch.empty((sum(recv_counts),) + tuple(send.shape[1:]), dtype=send.dtype, device=dev)
+    work = dist.all_to_all_single(recv, src.contiguous(), recv_counts, [int(c) for c in send_counts], group=group,
+                                  async_op=True)
+    return work, recv, send.device, src
+
+
+def finish_exchange(handle):
+    work, recv, home, _src = handle  # _src: the send buffer stays referenced until the wait
+    work.wait()
+    return recv if recv.device == home else recv.to(home)
 
 
 def exchange_records(send, send_counts, group=None):
@@ -172,8 +198,30 @@ def set_file_stats(table, file_stats):
         _lib.check(_lib.load().ottohip_table_set_file_stats(table.h, r, int(fr), int(fr2)))
 
 
+def _chunk_files(events, n_chunks: int) -> list:
+    """File bounds of n_chunks contiguous groups of the rank's files, balanced by events (the
+    per-file event counts are read once per DeviceEvents)."""
+    nf = len(events.file_bounds) - 1
+    if nf <= 0:
+        return [0] * (n_chunks + 1)
+    key = ("_chunk_bounds", n_chunks)
+    memo = events.__dict__.setdefault("_memo", {})
+    if key not in memo:
+        import torch
+        fbt = torch.as_tensor(events.file_bounds, dtype=torch.int64, device=events.offsets.device)
+        e = events.offsets[fbt].cpu().numpy().astype(np.int64)  # events before each file bound
+        tot = max(int(e[-1]), 1)
+        b = [0]
+        for c in range(1, n_chunks):
+            b.append(max(b[-1], int(np.searchsorted(e, tot * c / n_chunks, side="left"))))
+        b.append(nf)
+        memo[key] = [min(x, nf) for x in b]
+    return memo[key]
+
+
 def count_co_events_sharded(events, file_ids, n_files_total: int, group=None, names=None,
-                            n_items: int = config.N_ITEMS_OTTO, dedup: bool = True, stream=None, ctx=None):
+                            n_items: int = config.N_ITEMS_OTTO, dedup: bool = True, stream=None, ctx=None,
+                            chunks: int | None = None):
     """The N-GPU build: this rank's whole files (global ids file_ids) -> pair words laid out by
     owner -> all-to-all-v of words and row pieces (RCCL) -> assemble + reduce of the owner's
     rows. Returns this rank's shard (rows with owner(aid) == rank) of the single-GPU table;
@@ -184,18 +232,35 @@ def count_co_events_sharded(events, file_ids, n_files_total: int, group=None, na
     from .covis import reference_rules
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    if len(events.file_bounds) > 1:
-        words, wpp, pieces, ppp, names = emit_for_owners(events, world, file_ids, n_files_total, names, n_items, dedup,
-                                                          stream, ctx)
-    else:  # no files on this rank (e.g. one part of the part-wise merge): it still joins every exchange
-        names = reference_rules(names)[0]
-        dev = torch.device("cuda", (ctx or _lib.context()).device)
-        words, pieces = torch.empty(0, dtype=torch.int32, device=dev), torch.empty(0, dtype=torch.int64, device=dev)
-        wpp, ppp = [0] * world, [0] * world
-    rw = exchange(words, wpp, group)
-    del words
-    rp = exchange(pieces, ppp, group)
-    del pieces
+    # the rank's files in n_chunks contiguous groups (balanced by events): chunk c's all-to-all
+    # runs on RCCL's stream while chunk c + 1 is counted and emitted. Every rank joins n_chunks
+    # exchanges (empty chunks included); the receiver concatenates the chunks' words and pieces in
+    # arrival order, which keeps each piece's words where reduce_received expects them.
+    n_chunks = chunks if chunks is not None else int(os.environ.get("OTTOHIP_DIST_CHUNKS", "2"))
+    nf = len(events.file_bounds) - 1
+    bounds = _chunk_files(events, max(1, n_chunks))
+    names = reference_rules(names)[0]
+    dev = torch.device("cuda", (ctx or _lib.context()).device)
+    fids = list(range(nf)) if file_ids is None else [int(f) for f in file_ids]
+    pending = []
+    for c in range(len(bounds) - 1):
+        f0, f1 = bounds[c], bounds[c + 1]
+        if f1 > f0:
+            sub = events if (f0, f1) == (0, nf) else events.subset_files(f0, f1)
+            words, wpp, pieces, ppp, names = emit_for_owners(sub, world, fids[f0:f1], n_files_total, names, n_items,
+                                                              dedup, stream, ctx)
+        else:  # no files in this chunk (e.g. a rank without files of one part): it still joins the exchange
+            words, pieces = torch.empty(0, dtype=torch.int32, device=dev), torch.empty(0, dtype=torch.int64, device=dev)
+            wpp, ppp = [0] * world, [0] * world
+        if stream is not None:
+            stream.synchronize()  # RCCL orders after the current stream, not a side stream
+        pending.append((exchange_async(words, wpp, group), exchange_async(pieces, ppp, group)))
+        del words, pieces
+    got = [(finish_exchange(hw), finish_exchange(hp)) for hw, hp in pending]
+    del pending
+    rw = got[0][0] if len(got) == 1 else torch.cat([g[0] for g in got])
+    rp = got[0][1] if len(got) == 1 else torch.cat([g[1] for g in got])
+    del got
     tab = reduce_received(rw, rp, names, n_files_total, n_items, dedup, stream, ctx)
     del rw, rp
     fs = allreduce_file_stats([(tab.stats(r)["file_rows"], tab.stats(r)["file_rows_ge2"]) for r in range(len(names))],
