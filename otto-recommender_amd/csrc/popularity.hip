@@ -211,7 +211,9 @@ __device__ __forceinline__ long long km_fx(float x) {
   return fabsf(x) < 128.f ? (long long)__float2int_rn(y) : __float2ll_rn(y);
 }
 
-template <int NB>
+// NQ: 16-B pieces per row half as a constant (13 for dim 100: the row registers of the unused
+// pieces are not allocated, which keeps the kernel at <= 128 VGPRs = 2 blocks per CU)
+template <int NB, int NQ>
 __global__ __launch_bounds__(KM_MT) void k_km_assign_mfma(const float* __restrict__ X, int64_t n, int dim, int nq,
                                                         const float* __restrict__ C, const float* __restrict__ cn,
                                                         int k, int32_t* __restrict__ label,
@@ -246,19 +248,19 @@ __global__ __launch_bounds__(KM_MT) void k_km_assign_mfma(const float* __restric
   for (int64_t t = (int64_t)blockIdx.x * (KM_MT / 64) + wv; t < ntile; t += nwv) {
     const int64_t r0 = t << 5;
     const float* x = X + (r0 + i32 < n ? r0 + i32 : n - 1) * dim;
-    float4 a[KM_NQ];
+    float4 a[NQ];
 #pragma unroll
-    for (int q = 0; q < KM_NQ; ++q) {
+    for (int q = 0; q < NQ; ++q) {
       const int d0 = 8 * q + 4 * h;
       a[q] = (q < nq && d0 < dim) ? *reinterpret_cast<const float4*>(x + d0) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     float xs = 0.f;
 #pragma unroll
-    for (int q = 0; q < KM_NQ; ++q) xs += a[q].x * a[q].x + a[q].y * a[q].y + a[q].z * a[q].z + a[q].w * a[q].w;
+    for (int q = 0; q < NQ; ++q) xs += a[q].x * a[q].x + a[q].y * a[q].y + a[q].z * a[q].z + a[q].w * a[q].w;
     xs += __shfl_xor(xs, 32);
     km_f32x16 acc0 = {}, acc1 = {};
 #pragma unroll
-    for (int q = 0; q < KM_NQ; ++q) {
+    for (int q = 0; q < NQ; ++q) {
       if (q < nq) {
         const float4 b0 = Bl[q * 64 + l];
         acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].x, b0.x, acc0, 0, 0, 0);
@@ -429,7 +431,8 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
     const int64_t ntile = ceil_div(n, 32);
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(ntile, KM_MT / 64),
                                                                            (int64_t)ctx->n_cu * 2));
-    auto kern = NB == 1 ? k_km_assign_mfma<1> : k_km_assign_mfma<2>;
+    auto kern = nq == 13 ? (NB == 1 ? k_km_assign_mfma<1, 13> : k_km_assign_mfma<2, 13>)
+                         : (NB == 1 ? k_km_assign_mfma<1, KM_NQ> : k_km_assign_mfma<2, KM_NQ>);
     OH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)lds));
     kern<<<grid, KM_MT, lds, s>>>(X, n, dim, nq, C, cn, k, labels, sums, cnt, inr, changed, dist, inc);
