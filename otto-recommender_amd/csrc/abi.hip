@@ -380,7 +380,9 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   OH_TRY(ws.get("lcount", 8, &lcount));
   hipMemsetAsync(stats, 0, (size_t)STAT_STRIPES * STAT_STRIDE * 8, s);
   hipMemsetAsync(err, 0, sizeof(int), s);
-  hipMemsetAsync(T->b.rule, 0xFF, P, s);  // rows are written at their task's word offsets: holes stay 0xFF
+  // rows are written at their task's word offsets; each leaf task marks the rest of its range
+  // (rule 0xFF), so the slots need no fill (a debug ablation drops the sort kernels' stores)
+  if (getenv("OTTOHIP_REDUCE_DBG")) hipMemsetAsync(T->b.rule, 0xFF, P, s);
   OutRows O;
   O.rule = T->b.rule; O.aid = T->b.aid; O.aid_next = T->b.aid_next; O.count = T->b.count; O.count_ge2 = T->b.count_ge2;
   O.cap = P; O.stats = stats;

@@ -1273,6 +1273,8 @@ __global__ __launch_bounds__(256) void k_agg_sort(const Task* __restrict__ tasks
         atomicAdd(acc + 2, (unsigned long long)(cc & 0xFFFFu)); atomicAdd(acc + 3, (unsigned long long)(cc >> 16));
       }
     }
+    if (store)  // the rest of the task's word range holds no row (marked here, no table-wide fill)
+      for (uint32_t i = nout + l; i < len; i += 64) o_rule[i] = 0xFF;
     for (int q = 0; q < (nq < 2 ? nq : 2); ++q) {
       const uint32_t sa = wave_sum(q == 0 ? s0a : s1a), sb = wave_sum(q == 0 ? s0b : s1b);
       if (l == 0 && sa) {
@@ -1472,6 +1474,10 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
       put_row(O, p++, rule, ri.aid, (int32_t)(k2 & L.amask), c, c2);
       acc.add(rule, c, nf);
     }
+    // the rest of the task's word range holds no row (no table-wide fill: every word position
+    // belongs to exactly one leaf task, sort or hash)
+    const uint32_t nout = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+    for (uint32_t i = nout + tid; i < T.len; i += AGG_T) O.rule[T.begin + i] = 0xFF;
     __syncthreads();
   }
   acc.flush(O.stats, n_rules);
