@@ -162,11 +162,44 @@ class CovisTable:
         return a[:k], b[:k], c[:k]
 
 
+def _bits_for(n: int) -> int:
+    """bits needed to store values in [0, n) (common.h bits_for)."""
+    return max(0, int(n - 1).bit_length()) if n > 1 else 0
+
+
+def max_files_per_call(names=None, n_items: int = config.N_ITEMS_OTTO) -> int:
+    """Files one device pass can count: a pair word holds rule-within-type | aid_next | file in 31
+    bits (csrc/abi.hip setup_rules), so 2^(31 - rule bits - aid bits) files (512 at 1.86 M items)."""
+    names, rules = reference_rules(names)
+    per_type = max(sum(1 for r in rules if r.this_type == t) for t in range(3))
+    return 1 << (31 - _bits_for(per_type) - max(1, _bits_for(int(n_items))))
+
+
 def count_co_events_fused(events: DeviceEvents, names=None, n_items: int = config.N_ITEMS_OTTO, dedup: bool = True,
-                          stream=None, ctx=None) -> CovisTable:
+                          stream=None, ctx=None, max_files: int | None = None) -> CovisTable:
     """All rules over all files of `events` in one device pass (per-file counts folded into
-    count / count_ge2): count_co_events_all_files + the groupby of concat_files_w_stats."""
+    count / count_ge2): count_co_events_all_files + the groupby of concat_files_w_stats.
+    More files than one pass can tell apart (max_files_per_call) are counted in batches of
+    whole files and the batch tables merge-summed: count, count_ge2 and the per-file row
+    statistics are sums over disjoint file sets."""
     ctx = ctx or _lib.context()
+    cap = max_files or max_files_per_call(names, n_items)
+    nf = len(events.file_bounds) - 1
+    if nf > cap:
+        import torch
+        from . import dist as gd
+        recs, fs = [], None
+        for f0 in range(0, nf, cap):
+            t = count_co_events_fused(events.subset_files(f0, min(nf, f0 + cap)), names, n_items, dedup, stream, ctx,
+                                      max_files=cap)
+            st = [(t.stats(r)["file_rows"], t.stats(r)["file_rows_ge2"]) for r in range(len(t.names))]
+            fs = st if fs is None else [(a + c, b + d) for (a, b), (c, d) in zip(fs, st)]
+            r, _ = gd.pack_by_owner(t, 1, stream)
+            recs.append(r.clone())
+            names = t.names
+            t.free()
+        merged = gd.table_from_records(torch.cat(recs).contiguous(), names, n_items, fs, ctx=ctx, stream=stream)
+        return merged
     names, rules = reference_rules(names)
     p = _lib.CovisParams()
     p.min_dt, p.max_dt, p.n_items, p.dedup = config.MIN_TIME_TO_NEXT, config.MAX_TIME_TO_NEXT, int(n_items), int(dedup)

@@ -219,9 +219,33 @@ def _chunk_files(events, n_chunks: int) -> list:
     return memo[key]
 
 
+def _count_sharded_batches(events, file_ids, n_files_total: int, cap: int, group, names, n_items, dedup, stream, ctx,
+                           chunks):
+    """More global files than a pair word can tell apart: batches of cap global file ids, each
+    counted sharded (batch-local file ids), and every rank merge-sums its own shard tables (the
+    owner partition is the same in every batch, so no exchange)."""
+    import torch
+    fids = np.asarray(file_ids if file_ids is not None else range(len(events.file_bounds) - 1), np.int64)
+    recs, fs, out_names = [], None, None
+    for g0 in range(0, int(n_files_total), cap):
+        g1 = min(int(n_files_total), g0 + cap)
+        sel = np.nonzero((fids >= g0) & (fids < g1))[0]  # the rank's files are in ascending global order
+        lo, hi = (int(sel[0]), int(sel[-1]) + 1) if len(sel) else (0, 0)
+        sub = events.subset_files(lo, hi)
+        t = count_co_events_sharded(sub, (fids[lo:hi] - g0).tolist(), g1 - g0, group, names, n_items, dedup, stream,
+                                    ctx, chunks, max_files=cap)
+        st = [(t.stats(r)["file_rows"], t.stats(r)["file_rows_ge2"]) for r in range(len(t.names))]
+        fs = st if fs is None else [(a + c, b + d) for (a, b), (c, d) in zip(fs, st)]
+        r, _ = pack_by_owner(t, 1, stream)
+        recs.append(r.clone())
+        out_names = t.names
+        t.free()
+    return table_from_records(torch.cat(recs).contiguous(), out_names, n_items, fs, ctx=ctx, stream=stream)
+
+
 def count_co_events_sharded(events, file_ids, n_files_total: int, group=None, names=None,
                             n_items: int = config.N_ITEMS_OTTO, dedup: bool = True, stream=None, ctx=None,
-                            chunks: int | None = None):
+                            chunks: int | None = None, max_files: int | None = None):
     """The N-GPU build: this rank's whole files (global ids file_ids) -> pair words laid out by
     owner -> all-to-all-v of words and row pieces (RCCL) -> assemble + reduce of the owner's
     rows. Returns this rank's shard (rows with owner(aid) == rank) of the single-GPU table;
@@ -230,8 +254,15 @@ def count_co_events_sharded(events, file_ids, n_files_total: int, group=None, na
     import torch.distributed as dist
     import torch
     from .covis import reference_rules
+    from .covis import max_files_per_call
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    cap = max_files or max_files_per_call(names, n_items)
+    if int(n_files_total) > cap:
+        tab = _count_sharded_batches(events, file_ids, n_files_total, cap, group, names, n_items, dedup, stream,
+                                     ctx or _lib.context(), chunks)
+        tab.rank, tab.world = rank, world
+        return tab
     # the rank's files in n_chunks contiguous groups (balanced by events): chunk c's all-to-all
     # runs on RCCL's stream while chunk c + 1 is counted and emitted. Every rank joins n_chunks
     # exchanges (empty chunks included); the receiver concatenates the chunks' words and pieces in

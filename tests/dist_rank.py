@@ -46,13 +46,14 @@ def covis(out, cfg):
     dev = gc.DeviceEvents.from_host(my_ev, my_fb)
     res = {"files": np.asarray(mine, np.int64)}
     tab = gd.count_co_events_sharded(dev, mine, n_files)
-    # the exchange in 1 and 3 file chunks (overlapped all-to-alls) gives the same shard
-    for ch in (1, 3):
-        t2 = gd.count_co_events_sharded(dev, mine, n_files, chunks=ch)
+    # the exchange in 1 and 3 file chunks (overlapped all-to-alls), and global file batches of 2
+    # (more files than a pair word holds: per-batch shards merge-summed per owner), give the same shard
+    for ch, mf in ((1, None), (3, None), (2, 2)):
+        t2 = gd.count_co_events_sharded(dev, mine, n_files, chunks=ch, max_files=mf)
         for n in tab.names:
             for x, y in zip(tab.to_numpy(n), t2.to_numpy(n)):
-                assert np.array_equal(x, y), (ch, n)
-            assert tab.stats(n) == t2.stats(n), (ch, n)
+                assert np.array_equal(x, y), (ch, mf, n)
+            assert tab.stats(n) == t2.stats(n), (ch, mf, n)
         t2.free()
     for n in tab.names:
         a, b, c, c2 = tab.to_numpy(n)

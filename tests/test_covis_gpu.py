@@ -138,6 +138,38 @@ def test_three_files_digests(gpu):
     assert oracle.canonical_digest(ge2) == d["slice_300k_3files_count_ge2"]
 
 
+def test_file_batches_beyond_word_capacity(gpu):
+    """More files than a pair word's file bits hold: whole-file batches merge-summed. The golden
+    3-file digests with one file per batch, and 600 files (past the 512 of one pass at 1.86 M
+    items) equal to 300-file batches."""
+    from otto_recommender_amd import covis as gc
+    assert gc.max_files_per_call() == 512
+    d = json.load(open(os.path.join(GOLD, "digests.json")))
+    ev = synth.generate(300_000)
+    dev = gc.DeviceEvents.from_host(ev, synth.file_session_bounds(ev.n_sessions))
+    tab = gc.count_co_events_fused(dev, max_files=1)
+    cnt, ge2 = {}, {}
+    for n in NAMES:
+        a, b, c, c2 = tab.to_numpy(n)
+        cnt[n] = (a, b, c)
+        k = c2 > 0
+        ge2[n] = (a[k], b[k], c2[k])
+        st = tab.stats(n)
+        assert st["file_rows"] == d["slice_300k_3files_file_rows"][n]
+        assert st["file_rows_ge2"] == d["slice_300k_3files_file_rows_ge2"][n]
+    assert oracle.canonical_digest(cnt) == d["slice_300k_3files_count"]
+    assert oracle.canonical_digest(ge2) == d["slice_300k_3files_count_ge2"]
+    tab.free()
+    ev = synth.generate(30_000, first_session=500)
+    dev = gc.DeviceEvents.from_host(ev, synth.file_session_bounds(ev.n_sessions, per_file=50))
+    t1 = gc.count_co_events_fused(dev)
+    t2 = gc.count_co_events_fused(dev, max_files=300)
+    for n in NAMES:
+        for x, y in zip(t1.to_numpy(n), t2.to_numpy(n)):
+            np.testing.assert_array_equal(x, y, err_msg=n)
+        assert t1.stats(n) == t2.stats(n)
+
+
 # ---------------------------------------------------------------- edge cases
 def test_random_slices_vs_oracle(gpu):
     for first in (0, 777_777, 5_000_000):
