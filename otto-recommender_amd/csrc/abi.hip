@@ -237,10 +237,17 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
   OH_TRY(ws.get("pos", (size_t)E, &pos));
   OH_TRY(ws.get("rk2", (size_t)E, &rk2));
   OH_TRY(ws.get("pos2", (size_t)E, &pos2));
+  // S3's fused row layout (one GPU, rows < 2^24): S2 writes the row keys with their pair counts in
+  // the byte above the sorted key bits, and the sort generates the event positions itself
+  static const bool rows_legacy = getenv("OTTOHIP_ROWS") && !strcmp(getenv("OTTOHIP_ROWS"), "legacy");
+  const int cshift = (Lt.A + 2 + 7) / 8 * 8;  // first byte above the sorted key bits
+  const bool fused = !rows_legacy && n_parts == 1 && cshift + 8 <= 32 &&
+                     3ull * (uint64_t)params->n_items < (1ull << 24);
+  uint32_t* pos_w = fused ? nullptr : pos;
   int ph = ctx->begin("prep_count", s, 9.0 * E + 8.0 * (Sn + 1) + 8.0 * E + 12.0 * E);
   k_block_first<<<grid_for(Sn + 1), 256, 0, s>>>(off, Sn, NB, F.first, F.long_list, n_long);
   k_prep_count<<<(unsigned)NB, 64, 0, s>>>(off, F.first, NB, ev->aid, ev->ts, ev->type, F.evp, params->n_items,
-                                           params->dedup, err, R, Lt.A, F.cnt, rk, pos);
+                                           params->dedup, err, R, Lt.A, F.cnt, rk, pos_w, fused ? cshift : 0);
   if (hipGetLastError() != hipSuccess) { set_error("k_prep_count launch failed"); return OTTOHIP_EHIP; }
   int32_t nl = 0;
   OH_TRY(d2h(&nl, n_long, 1, s));
@@ -263,7 +270,8 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
     OH_HIP(hipMemcpy(F.d_loff, loff.data(), (nl + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
     k_prep_long<<<nl, 64, 0, s>>>(off, F.long_list, F.d_loff, F.lscr, ev->aid, ev->ts, ev->type, F.evp,
                                   params->n_items, params->dedup, err);
-    k_count_long<<<nl, 64, 0, s>>>(off, F.long_list, F.d_loff, F.lscr, F.lpscr, F.evp, R, Lt.A, F.cnt, rk, pos);
+    k_count_long<<<nl, 64, 0, s>>>(off, F.long_list, F.d_loff, F.lscr, F.lpscr, F.evp, R, Lt.A, F.cnt, rk, pos_w,
+                                   fused ? cshift : 0);
     if (hipGetLastError() != hipSuccess) { set_error("long-session launch failed"); return OTTOHIP_EHIP; }
   }
   ctx->end(ph, s);
@@ -280,14 +288,10 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
     if (kbits > 32) { set_error("row key with owner bits > 32 bits"); return OTTOHIP_ELIMIT; }
   }
   const uint32_t kmask = Lt.A + 2 >= 32 ? ~0u : (1u << (Lt.A + 2)) - 1u;
-  // fused layout: counts ride in the keys' spare bits, one u64 scan carries word offset and row index
-  static const bool rows_legacy = getenv("OTTOHIP_ROWS") && !strcmp(getenv("OTTOHIP_ROWS"), "legacy");
-  const int cshift = (Lt.A + 2 + 7) / 8 * 8;  // first byte above the sorted key bits
-  const bool fused = !rows_legacy && n_parts == 1 && cshift + 8 <= 32 &&
-                     3ull * (uint64_t)params->n_items < (1ull << 24);
-  if (fused) k_key_cnt<<<grid_for(E), 256, 0, s>>>(rk, F.cnt, E, cshift);
+  // fused layout: counts ride in the keys' spare bits (written by S2), one u64 scan carries word
+  // offset and row index; the sort's first pass takes the event positions from its own indices
   uint32_t *rks = rk, *poss = pos;
-  OH_TRY(radix_sort_pairs(ctx, rks, poss, rk2, pos2, E, kbits, s));
+  OH_TRY(radix_sort_pairs(ctx, rks, poss, rk2, pos2, E, kbits, s, fused));
   uint64_t* tot;
   OH_TRY(ws.get("tot", 4, &tot));
   if (fused) {

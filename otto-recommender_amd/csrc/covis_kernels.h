@@ -224,9 +224,16 @@ __device__ __forceinline__ uint32_t count_event(const SessView& S, int i, const 
   return c;
 }
 
+// the row key of an event, with (cshift > 0: the fused row layout of S3) its pair count saturated
+// at RK_CSAT in the byte above the sorted key bits
+constexpr uint32_t RK_CSAT = 255u;
+__device__ __forceinline__ uint32_t rk_with_count(uint32_t key, uint32_t c, int cshift) {
+  return cshift ? key | ((c < RK_CSAT ? c : RK_CSAT) << cshift) : key;
+}
+
 __device__ __forceinline__ void count_session(const SessView& S, int64_t e0, int n, const RulesDev& R, int A,
                                               uint32_t* __restrict__ cnt, uint32_t* __restrict__ rk,
-                                              uint32_t* __restrict__ pos) {
+                                              uint32_t* __restrict__ pos, int cshift) {
   const uint32_t INV = 3u << A;
   for (int k = lane_id(); k < n; k += 64) {
     uint32_t c = 0, key = INV;
@@ -235,8 +242,8 @@ __device__ __forceinline__ void count_session(const SessView& S, int64_t e0, int
       if (c) { const uint64_t e = S.ev[k]; key = ((uint32_t)ev_type(e) << A) | (uint32_t)ev_aid(e); }
     }
     cnt[e0 + k] = c;
-    rk[e0 + k] = key;
-    pos[e0 + k] = (uint32_t)(e0 + k);
+    rk[e0 + k] = rk_with_count(key, c, cshift);
+    if (pos) pos[e0 + k] = (uint32_t)(e0 + k);
   }
 }
 
@@ -245,7 +252,7 @@ __global__ __launch_bounds__(64) void k_count_long(const int64_t* __restrict__ o
                                                    uint64_t* __restrict__ scratch, uint32_t* __restrict__ pscratch,
                                                    const uint64_t* __restrict__ ev, RulesDev R, int A,
                                                    uint32_t* __restrict__ cnt, uint32_t* __restrict__ rk,
-                                                   uint32_t* __restrict__ pos) {
+                                                   uint32_t* __restrict__ pos, int cshift) {
   const int64_t s = list[blockIdx.x];
   const int64_t e0 = off[s];
   const int n = (int)(off[s + 1] - e0);
@@ -255,7 +262,7 @@ __global__ __launch_bounds__(64) void k_count_long(const int64_t* __restrict__ o
   uint32_t* pref = pscratch + 3 * (so + blockIdx.x);
   S.ev = evs; S.pref = pref; S.pstride = n + 1;
   S.nv = load_session(ev + e0, n, evs, pref, n + 1);
-  count_session(S, e0, n, R, A, cnt, rk, pos);
+  count_session(S, e0, n, R, A, cnt, rk, pos, cshift);
 }
 
 // ------------------------------------------------------------------ S1+S2 fused
@@ -297,7 +304,7 @@ __global__ __launch_bounds__(64) void k_prep_count(const int64_t* __restrict__ o
                                                    const int32_t* __restrict__ ts, const int8_t* __restrict__ ty,
                                                    uint64_t* __restrict__ ev, int n_items, int dedup, int* err,
                                                    RulesDev R, int A, uint32_t* __restrict__ cnt,
-                                                   uint32_t* __restrict__ rk, uint32_t* __restrict__ pos) {
+                                                   uint32_t* __restrict__ rk, uint32_t* __restrict__ pos, int cshift) {
   __shared__ PrepLds S;
   __shared__ RulesDev sR;
   const int l = threadIdx.x;
@@ -459,8 +466,8 @@ __global__ __launch_bounds__(64) void k_prep_count(const int64_t* __restrict__ o
         if (cn) key = ((uint32_t)t << A) | (uint32_t)ev_aid(e);
       }
       cnt[E0 + idx] = cn;
-      rk[E0 + idx] = key;
-      pos[E0 + idx] = (uint32_t)(E0 + idx);
+      rk[E0 + idx] = rk_with_count(key, cn, cshift);
+      if (pos) pos[E0 + idx] = (uint32_t)(E0 + idx);
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -501,15 +508,8 @@ __global__ void k_rows(const uint32_t* __restrict__ rk, const uint32_t* __restri
 // long sessions, are gathered), then one pass of block sums and one pass of per-block scans
 // give every event its word offset and every row its key and first word, with X = cnt << 24 |
 // [row start] scanned as one u64: no c_sorted / row_flag arrays, no second scan, no gather.
-constexpr uint32_t RK_CSAT = 255u;  // the key byte above the sorted digits (LSD passes sort whole bytes)
+// (RK_CSAT: the key byte above the sorted digits, LSD passes sort whole bytes; written by S1+S2)
 constexpr int RT_T = 256, RT_I = 8, RT_TILE = RT_T * RT_I;
-
-__global__ void k_key_cnt(uint32_t* __restrict__ rk, const uint32_t* __restrict__ cnt, int64_t n, int shift) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t c = cnt[i];
-  rk[i] |= (c < RK_CSAT ? c : RK_CSAT) << shift;
-}
 
 __device__ __forceinline__ uint64_t rows_x(const uint32_t* __restrict__ rks, const uint32_t* __restrict__ poss,
                                            const uint32_t* __restrict__ cnt, int64_t k, uint32_t kmask, uint32_t INV,

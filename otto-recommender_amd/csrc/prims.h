@@ -9,6 +9,8 @@ int exclusive_scan_u64(Ctx* ctx, const uint64_t* in, uint64_t* out, int64_t n, u
                        hipStream_t s);
 // stable LSD sort of (key, val) by key bits [0, bits); ping-pongs with the *_alt buffers and
 // returns the buffers holding the result in keys/vals
+// iota_vals: the input values are their own indices (0..n-1); the first pass generates them
+// instead of reading vals (vals still provides the buffer)
 int radix_sort_pairs(Ctx* ctx, uint32_t*& keys, uint32_t*& vals, uint32_t* keys_alt, uint32_t* vals_alt,
-                     int64_t n, int bits, hipStream_t s);
+                     int64_t n, int bits, hipStream_t s, bool iota_vals = false);
 }  // namespace ottohip

@@ -121,7 +121,7 @@ __global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict_
                                                      const uint32_t* __restrict__ vin,
                                                      uint32_t* __restrict__ kout,
                                                      uint32_t* __restrict__ vout, int64_t n, int shift,
-                                                     const uint64_t* __restrict__ gofs, int nb) {
+                                                     const uint64_t* __restrict__ gofs, int nb, int iota) {
   __shared__ uint32_t wcnt[RS_WAVES][256];
   __shared__ uint32_t bstart[256];
   __shared__ uint32_t wsum[RS_WAVES];
@@ -138,7 +138,7 @@ __global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict_
     const int64_t idx = t0 + w * (RS_R * 64) + r * 64 + l;
     const bool valid = idx < n;
     key[r] = valid ? kin[idx] : 0u;
-    val[r] = valid ? vin[idx] : 0u;
+    val[r] = valid ? (iota ? (uint32_t)idx : vin[idx]) : 0u;
     const uint32_t d = (key[r] >> shift) & 255u;
     uint64_t m = __ballot(valid);
 #pragma unroll
@@ -191,8 +191,12 @@ __global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict_
 }
 
 int radix_sort_pairs(Ctx* ctx, uint32_t*& keys, uint32_t*& vals, uint32_t* keys_alt, uint32_t* vals_alt,
-                     int64_t n, int bits, hipStream_t s) {
-  if (n <= 1 || bits <= 0) return 0;
+                     int64_t n, int bits, hipStream_t s, bool iota_vals) {
+  if (n <= 1 || bits <= 0) {  // nothing to sort; generated values still have to be written
+    if (iota_vals && n > 1) { set_error("radix_sort_pairs: iota values need bits > 0"); return OTTOHIP_EINVAL; }
+    if (iota_vals && n == 1) OH_HIP(hipMemsetAsync(vals, 0, sizeof(uint32_t), s));
+    return 0;
+  }
   if (n >= ((int64_t)1 << 32)) { set_error("radix_sort_pairs: n=%lld too large", (long long)n); return OTTOHIP_ELIMIT; }
   const int nb = (int)ceil_div(n, RS_TILE);
   uint32_t* hist; uint64_t* gofs;
@@ -203,7 +207,7 @@ int radix_sort_pairs(Ctx* ctx, uint32_t*& keys, uint32_t*& vals, uint32_t* keys_
     k_rs_hist<<<nb, RS_T, 0, s>>>(ka, n, shift, hist, nb);
     OH_HIP(hipGetLastError());
     OH_TRY(exclusive_scan_u32(ctx, hist, gofs, (int64_t)nb * 256, nullptr, s));
-    k_rs_scatter<<<nb, RS_T, 0, s>>>(ka, va, kb, vb, n, shift, gofs, nb);
+    k_rs_scatter<<<nb, RS_T, 0, s>>>(ka, va, kb, vb, n, shift, gofs, nb, iota_vals && shift == 0 ? 1 : 0);
     OH_HIP(hipGetLastError());
     std::swap(ka, kb); std::swap(va, vb);
   }
