@@ -187,12 +187,14 @@ __global__ __launch_bounds__(256) void k_km_assign(const float* __restrict__ X, 
 
 // C2 on the matrix cores (k <= 64, dim <= 128, dim % 4 == 0): a wave scores a tile of 32 rows
 // against 32 centroids per v_mfma_f32_32x32x2f32 (NB = 1 or 2 centroid blocks). Lane (i, h)
-// loads 16-B pieces of row i (dims 8q + 4h .. 8q + 4h + 3); the same dims of its centroid column
-// come from LDS, so MFMA (q, u) pairs dim 8q + u (h = 0) with dim 8q + 4 + u (h = 1). The MFMA is
-// an exact f32 fma chain: only the summation order differs from k_km_assign. The argmin is over
-// |c|^2 - 2 x.c (|x|^2 is common to the row, as in sklearn's Lloyd step), ties to the lowest
-// cluster; (value, index) pairs are reduced over the 32 columns by DPP / permlane butterflies.
-// Per-cluster sums as in k_km_assign (2^-24 fixed point, order-independent).
+// loads 16-B pieces of row i (dims 8q + 4h .. 8q + 4h + 3); the same dims of centroid i come
+// from LDS, so MFMA (q, u) pairs dim 8q + u (h = 0) with dim 8q + 4 + u (h = 1). The MFMA is an
+// exact f32 fma chain: only the summation order differs from k_km_assign. Centroids are the A
+// operand and rows the B operand, so lane (i, h) holds row i's scores of 16 (32) clusters: the
+// argmin over |c|^2 - 2 x.c (|x|^2 is common to the row, as in sklearn's Lloyd step; ties to the
+// lowest cluster) is an in-lane min and lowest-index scan plus one exchange with lane i ^ 32
+// (the former row-operand layout needed a 5-step cross-lane butterfly of 64-bit keys:
+// Lloyd step 1.87 -> 1.68 ms). Per-cluster sums as in k_km_assign (2^-24 fixed point).
 typedef float km_f32x16 __attribute__((ext_vector_type(16)));
 constexpr int KM_MT = 512;  // threads per block (8 waves)
 constexpr int KM_NQ = 16;   // 16-B pieces per row half (dim <= 128)
@@ -214,7 +216,7 @@ __device__ __forceinline__ long long km_fx(float x) {
 // NQ: 16-B pieces per row half as a constant (13 for dim 100: the row registers of the unused
 // pieces are not allocated, which keeps the kernel at <= 128 VGPRs = 2 blocks per CU)
 template <int NB, int NQ>
-__global__ __launch_bounds__(KM_MT) void k_km_assign_mfma(const float* __restrict__ X, int64_t n, int dim, int nq,
+__global__ __launch_bounds__(KM_MT, (NQ <= 13 ? 4 : 2)) void k_km_assign_mfma(const float* __restrict__ X, int64_t n, int dim, int nq,
                                                         const float* __restrict__ C, const float* __restrict__ cn,
                                                         int k, int32_t* __restrict__ label,
                                                         unsigned long long* __restrict__ sums,
@@ -258,72 +260,73 @@ __global__ __launch_bounds__(KM_MT) void k_km_assign_mfma(const float* __restric
 #pragma unroll
     for (int q = 0; q < NQ; ++q) xs += a[q].x * a[q].x + a[q].y * a[q].y + a[q].z * a[q].z + a[q].w * a[q].w;
     xs += __shfl_xor(xs, 32);
+    // centroids as the A operand, rows as B: lane (i32, h) ends with row r0 + i32's scores of the
+    // clusters (r & 3) + 8 (r >> 2) + 4 h in register r (+ 32 in acc1), so the argmin is an
+    // in-lane scan plus one exchange with lane i32 + 32 (no cross-lane butterfly over clusters)
     km_f32x16 acc0 = {}, acc1 = {};
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       if (q < nq) {
         const float4 b0 = Bl[q * 64 + l];
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].x, b0.x, acc0, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].y, b0.y, acc0, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].z, b0.z, acc0, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].w, b0.w, acc0, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(b0.x, a[q].x, acc0, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(b0.y, a[q].y, acc0, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(b0.z, a[q].z, acc0, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(b0.w, a[q].w, acc0, 0, 0, 0);
         if (NB == 2) {
           const float4 b1 = Bl[(nq + q) * 64 + l];
-          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].x, b1.x, acc1, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].y, b1.y, acc1, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].z, b1.z, acc1, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].w, b1.w, acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b1.x, a[q].x, acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b1.y, a[q].y, acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b1.z, a[q].z, acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b1.w, a[q].w, acc1, 0, 0, 0);
         }
       }
     }
-    // accumulator register r of lane (column i32, half h) holds row (r & 3) + 8 (r >> 2) + 4 h.
-    // Key = ordered score << 32 | cluster (ties to the lower cluster). The 16 rows x 32 columns
-    // are reduced by register halving: at each of the xor-16/8/4/2 steps a lane keeps half of its
-    // registers and takes the partner's minimum of the other half (8 + 4 + 2 + 1 exchanges), then
-    // one xor-1 step: lane l ends with the row of register ((l >> 1) & 15), paired with l ^ 1.
-    uint64_t kk[16];
+    // score |c|^2 - 2 x.c (exact: 2 x.c is exact, one rounding as before); the minimum, then the
+    // lowest cluster holding it (clusters ascend with r within a block)
+    float m = INFINITY;
+
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // scores in place of the dot products
+      const float4 n0 = *reinterpret_cast<const float4*>(cnl + 8 * j + 4 * h);
+      acc0[4 * j + 0] = n0.x - 2.f * acc0[4 * j + 0];
+      acc0[4 * j + 1] = n0.y - 2.f * acc0[4 * j + 1];
+      acc0[4 * j + 2] = n0.z - 2.f * acc0[4 * j + 2];
+      acc0[4 * j + 3] = n0.w - 2.f * acc0[4 * j + 3];
+      if (NB == 2) {
+        const float4 n1 = *reinterpret_cast<const float4*>(cnl + 32 + 8 * j + 4 * h);
+        acc1[4 * j + 0] = n1.x - 2.f * acc1[4 * j + 0];
+        acc1[4 * j + 1] = n1.y - 2.f * acc1[4 * j + 1];
+        acc1[4 * j + 2] = n1.z - 2.f * acc1[4 * j + 2];
+        acc1[4 * j + 3] = n1.w - 2.f * acc1[4 * j + 3];
+      }
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      uint64_t a0 = ((uint64_t)km_ord(cA - 2.f * acc0[r]) << 32) | (uint32_t)i32;
-      if (NB == 2) {
-        const uint64_t a1 = ((uint64_t)km_ord(cB - 2.f * acc1[r]) << 32) | (uint32_t)(32 + i32);
-        a0 = a1 < a0 ? a1 : a0;
-      }
-      kk[r] = a0;
+      m = fminf(m, acc0[r]);
+      if (NB == 2) m = fminf(m, acc1[r]);
+    }
+    int mc = 64;
+#pragma unroll
+    for (int r = 15; r >= 0; --r) {
+      if (NB == 2) mc = acc1[r] == m ? 32 + (r & 3) + 8 * (r >> 2) + 4 * h : mc;
     }
 #pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      const int half = 8 >> st, J = 16 >> st;
-      // lane-dependent choice by bit-select (v_bfi), not a select of array elements: the latter
-      // is turned into a dynamically indexed register array (compare/select chains)
-      const uint32_t upm = (l & J) ? ~0u : 0u;
-#pragma unroll
-      for (int j = 0; j < half; ++j) {
-        const uint32_t alo = (uint32_t)kk[j], ahi = (uint32_t)(kk[j] >> 32);
-        const uint32_t blo = (uint32_t)kk[j + half], bhi = (uint32_t)(kk[j + half] >> 32);
-        const uint32_t slo = (alo & upm) | (blo & ~upm), shi = (ahi & upm) | (bhi & ~upm);
-        const uint32_t klo = (blo & upm) | (alo & ~upm), khi = (bhi & upm) | (ahi & ~upm);
-        const uint32_t rlo = xor_lane_n(slo, J), rhi = xor_lane_n(shi, J);
-        const uint64_t recv = ((uint64_t)rhi << 32) | rlo, keep = ((uint64_t)khi << 32) | klo;
-        kk[j] = recv < keep ? recv : keep;
-      }
+    for (int r = 15; r >= 0; --r) mc = acc0[r] == m ? (r & 3) + 8 * (r >> 2) + 4 * h : mc;
+    {  // the other half of the row's clusters (lane i32 ^ 32): smaller score, then lower cluster
+      const float pm = __shfl_xor(m, 32);
+      const int pc = __shfl_xor(mc, 32);
+      if (pm < m || (pm == m && pc < mc)) { m = pm; mc = pc; }
     }
-    {
-      const uint32_t rlo = xor_lane<1>((uint32_t)kk[0]), rhi = xor_lane<1>((uint32_t)(kk[0] >> 32));
-      const uint64_t recv = ((uint64_t)rhi << 32) | rlo;
-      kk[0] = recv < kk[0] ? recv : kk[0];
-    }
-    const int rr = (l >> 1) & 15;
-    const int R = (rr & 3) + 8 * (rr >> 2) + 4 * h;
-    const float xr = __shfl(xs, R);
-    const uint32_t mi = (uint32_t)kk[0];
+    const int R = i32;
+    const float xr = xs;
+    const uint32_t mi = (uint32_t)mc;
     int32_t old = -1;
-    const bool mine = (l & 1) == 0 && r0 + R < n;
+    const bool mine = h == 0 && r0 + R < n;
     if (mine) {
       if (changed || inc) old = label[r0 + R];
       if (changed) nchg += old != (int32_t)mi;
       label[r0 + R] = (int32_t)mi;
-      const float dd = fmaxf(xr + km_unord((uint32_t)(kk[0] >> 32)), 0.f);
+      const float dd = fmaxf(xr + m, 0.f);
       part += (double)dd;
       if (dist) dist[r0 + R] = dd;
     }
