@@ -234,15 +234,19 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
                                                           uint16_t* __restrict__ o_flags,
                                                           int32_t* __restrict__ overflow,
                                                           uint32_t* __restrict__ n_overflow, int dbg) {
-  __shared__ uint32_t hk[WAVES][HC], hm[WAVES][HC], ho[WAVES][HC];
-  __shared__ uint64_t sk[WAVES][HC];
+  // OVL: the sort keys overlay the key / mask arrays once the table has been read into registers,
+  // which halves the wave's LDS (more waves per CU for this latency-bound kernel)
+  constexpr bool OVL = true;
+  __shared__ uint64_t hkm64[WAVES][HC];  // keys [0, HC) and masks [HC, 2 HC) as u32; sort keys (OVL)
+  __shared__ uint32_t ho[WAVES][HC];
+  __shared__ uint64_t sk[OVL ? 1 : WAVES][OVL ? 1 : HC];
   __shared__ uint32_t pre[WAVES][65], ka[WAVES][64], ki[WAVES][64], kl[WAVES][64];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int64_t gi = (int64_t)blockIdx.x * WAVES + w;
   if (gi >= n_sess) return;
   const int64_t s = sess ? sess[gi] : gi;
-  uint32_t* K = hk[w];
-  uint32_t* Mk = hm[w];
+  uint32_t* K = reinterpret_cast<uint32_t*>(hkm64[w]);
+  uint32_t* Mk = K + HC;
   uint32_t* Ord = ho[w];
   uint32_t* PRE = pre[w];
   for (int i = l; i < HC; i += 64) { K[i] = CS_EMPTY; Mk[i] = 0; Ord[i] = 0xFFFFFFFFu; }
@@ -332,12 +336,19 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
     return;
   }
   // compact (ts_order, aid_next, flags) sort keys
-  uint64_t* SK = sk[w];
+  uint64_t* SK = OVL ? hkm64[w] : sk[OVL ? 0 : w];
   int cnt = 0;
-  for (int i0 = 0; i0 < HC; i0 += 64) {
-    const int i = i0 + l;
+  constexpr int NR = OVL ? HC / 64 : 1;
+  uint64_t rk[NR];  // OVL: the lane's table entries (key or ~0), written after the whole table was read
+#pragma unroll
+  for (int c0 = 0; c0 < HC / 64; ++c0) {
+    const int i = c0 * 64 + l;
     const bool occ = K[i] != CS_EMPTY;
     const uint64_t b = __ballot(occ);
+    if (OVL) {
+#pragma unroll
+      for (int q = 0; q < NR; ++q) if (q == c0) rk[q] = ~0ull;
+    }
     if (occ && pass == 1) {
       const uint32_t mk_ = Mk[i];
       const uint32_t click = (mk_ >> 8) & 1u, cart = (mk_ >> 9) & 1u, order = (mk_ >> 10) & 1u;
@@ -350,9 +361,27 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
       f |= (((mk_ >> 5) & 1u) & order) << 5;
       f |= ((mk_ >> 6) & 3u) << 6;
       f |= ((mk_ >> 11) & 1u) << 8;
-      SK[cnt + (int)mbcnt(b)] = ((uint64_t)Ord[i] << 48) | ((uint64_t)K[i] << 16) | f;
+      const uint64_t key = ((uint64_t)Ord[i] << 48) | ((uint64_t)K[i] << 16) | f;
+      if (OVL) {
+#pragma unroll
+        for (int q = 0; q < NR; ++q) if (q == c0) rk[q] = key;
+      } else {
+        SK[cnt + (int)mbcnt(b)] = key;
+      }
     }
     cnt += (int)__popcll(b);
+  }
+  if (OVL && pass == 1) {  // every lane has read its entries: the table's memory becomes the key array
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    int c = 0;
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      const bool occ = rk[q] != ~0ull;
+      const uint64_t b = __ballot(occ);
+      if (occ) SK[c + (int)mbcnt(b)] = rk[q];
+      c += (int)__popcll(b);
+    }
   }
   if (pass == 0) {
     if (l == 0) n_cand[s] = (uint32_t)cnt;
