@@ -463,17 +463,24 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
 __global__ __launch_bounds__(256) void k_km_labelled(const float* __restrict__ X, int64_t n, int dim,
                                                      const float* __restrict__ C, const int32_t* __restrict__ label,
                                                      float* __restrict__ dist, double* __restrict__ inertia) {
+  // half a wave per row: lanes over the row's dims (coalesced), sum by a 32-lane butterfly
   double part = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+  const int hl = threadIdx.x & 31;
+  const int64_t nhalf = ((int64_t)gridDim.x * blockDim.x) >> 5;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 5; i < n; i += nhalf) {
     const float* x = X + i * dim;
     const float* c = C + (int64_t)label[i] * dim;
     float acc = 0.f;
-    for (int d = 0; d < dim; ++d) {
+    for (int d = hl; d < dim; d += 32) {
       const float t = x[d] - c[d];
-      acc += t * t;
+      acc = fmaf(t, t, acc);
     }
-    if (dist) dist[i] = acc;
-    part += (double)acc;
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+    if (hl == 0) {
+      if (dist) dist[i] = acc;
+      part += (double)acc;
+    }
   }
   for (int o = 32; o >= 1; o >>= 1) {
     const uint64_t b = __double_as_longlong(part);

@@ -3,7 +3,7 @@
 set -o pipefail
 O=gpurun_out/${1:-candab}; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_candidates_gpu.py tests/test_pipeline_gpu.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_candidates_gpu.py tests/test_pipeline_gpu.py tests/test_popularity_gpu.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 B=$GRAFT_REPO_ROOT/otto-recommender_amd/libottohip_ab.so
 for run in A1 B1; do
