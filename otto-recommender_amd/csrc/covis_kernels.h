@@ -291,8 +291,10 @@ __device__ __forceinline__ int lds_upper_ts(const uint64_t* tev, int a, int b, i
 constexpr int PB_CAP = 512;
 struct PrepLds {
   uint64_t key[PB_CAP];   // packed raw events, then the final (sorted, deduplicated) session layout
-  uint64_t srt[PB_CAP];   // sorted events before deduplication
-  uint16_t pref[3][PB_CAP + 1];
+  union {                 // srt is dead once the deduplicated layout is in key: pref reuses it
+    uint64_t srt[PB_CAP];   // sorted events before deduplication
+    uint16_t pref[3][PB_CAP + 1];
+  };
   uint16_t ss[65];        // session starts in the batch; ss[nsess] = batch size
   uint16_t pst[64], pen[64];
   uint8_t esid[PB_CAP];
