@@ -1143,13 +1143,13 @@ __device__ __forceinline__ uint32_t excl_at(const uint32_t (&x)[M], int m, uint3
 // through a per-wave LDS accumulator (one lane, after wave sums of packed 16-bit fields: a
 // task holds <= 1024 words), so no per-thread accumulator arrays take registers.
 template <int M>
-__global__ __launch_bounds__(256) void k_agg_sort(const Task* __restrict__ tasks, int64_t n_tasks,
+__global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task* __restrict__ tasks, int64_t n_tasks,
                                                   const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
                                                   const uint32_t* __restrict__ row_key, RulesDev R, Layout L,
                                                   int n_rules, OutRows O) {
   __shared__ unsigned long long sacc[4][MAX_RULES * 4];
   __shared__ RulesDev sR;
-  __shared__ uint32_t stg[4][3][64 * M];  // per wave: output rows of one task (key2, counts, file counts)
+  __shared__ uint32_t stg[4][2][64 * M];  // per wave: output rows of one task (key2, count | count_ge2 << 16)
   const uint32_t l = lane_id();
   const int wv = threadIdx.x >> 6;
   if (threadIdx.x == 0) sR = R;
@@ -1232,49 +1232,48 @@ __global__ __launch_bounds__(256) void k_agg_sort(const Task* __restrict__ tasks
     const uint32_t nmine = (uint32_t)__builtin_popcount(kend);
     const uint32_t incl = wave_incl_scan(nmine);
     const uint32_t nout = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    // the per-rule statistics come from the registers here (only key2 and the counts are staged)
+    const int nq = sR.n_of_type[type];
+    const int r0 = sR.rule_of_type[type][0], r1 = sR.rule_of_type[type][1];
+    uint32_t s0a = 0, s0b = 0, s1a = 0, s1b = 0;  // local rules 0 / 1: rows | nf1 << 16, pairs | nf2 << 16
     {
       uint32_t idx = incl - nmine;
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         if (kend & (1u << m)) {
-          stg[wv][0][idx] = v[m] >> F;
+          const uint32_t k2 = v[m] >> F, q = k2 >> A, cnt = b[m] & 0xFFFFu, cc = c[m];
+          stg[wv][0][idx] = k2;
           stg[wv][1][idx] = b[m];
-          stg[wv][2][idx] = c[m];
           ++idx;
+          const uint32_t ra = 1u | ((cc & 0xFFFFu) << 16), rb = cnt | (cc & 0xFFFF0000u);
+          if (q == 0) { s0a += ra; s0b += rb; }
+          else if (q == 1) { s1a += ra; s1b += rb; }
+          else {  // more than 2 rules of one type (not in the reference's five)
+            unsigned long long* acc = sacc[wv] + sR.rule_of_type[type][q] * 4;
+            atomicAdd(acc + 0, 1ull); atomicAdd(acc + 1, (unsigned long long)cnt);
+            atomicAdd(acc + 2, (unsigned long long)(cc & 0xFFFFu)); atomicAdd(acc + 3, (unsigned long long)(cc >> 16));
+          }
         }
       }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const int nq = sR.n_of_type[type];
-    const int r0 = sR.rule_of_type[type][0], r1 = sR.rule_of_type[type][1];
-    uint32_t s0a = 0, s0b = 0, s1a = 0, s1b = 0;  // local rules 0 / 1: rows | nf1 << 16, pairs | nf2 << 16
     const bool store = O.cap != 0;
     uint8_t* o_rule = O.rule + T.begin;
     int32_t* o_aid = O.aid + T.begin;
     int32_t* o_next = O.aid_next + T.begin;
     uint32_t* o_cnt = O.count + T.begin;
     uint32_t* o_c2 = O.count_ge2 + T.begin;
-    for (uint32_t i = l; i < nout; i += 64) {
-      const uint32_t k2 = stg[wv][0][i], bb = stg[wv][1][i], cc = stg[wv][2][i];
-      const uint32_t q = k2 >> A;
-      const uint32_t cnt = bb & 0xFFFFu;
-      if (store) {
+    if (store)
+      for (uint32_t i = l; i < nout; i += 64) {
+        const uint32_t k2 = stg[wv][0][i], bb = stg[wv][1][i];
+        const uint32_t q = k2 >> A;
         o_rule[i] = (uint8_t)(q == 0 ? r0 : (q == 1 ? r1 : sR.rule_of_type[type][q]));
         o_aid[i] = aid;
         o_next[i] = (int32_t)(k2 & L.amask);
-        o_cnt[i] = cnt;
+        o_cnt[i] = bb & 0xFFFFu;
         o_c2[i] = bb >> 16;
       }
-      const uint32_t ra = 1u | ((cc & 0xFFFFu) << 16), rb = cnt | (cc & 0xFFFF0000u);
-      if (q == 0) { s0a += ra; s0b += rb; }
-      else if (q == 1) { s1a += ra; s1b += rb; }
-      else {  // more than 2 rules of one type (not in the reference's five)
-        unsigned long long* acc = sacc[wv] + sR.rule_of_type[type][q] * 4;
-        atomicAdd(acc + 0, 1ull); atomicAdd(acc + 1, (unsigned long long)cnt);
-        atomicAdd(acc + 2, (unsigned long long)(cc & 0xFFFFu)); atomicAdd(acc + 3, (unsigned long long)(cc >> 16));
-      }
-    }
     if (store)  // the rest of the task's word range holds no row (marked here, no table-wide fill)
       for (uint32_t i = nout + l; i < len; i += 64) o_rule[i] = 0xFF;
     for (int q = 0; q < (nq < 2 ? nq : 2); ++q) {
