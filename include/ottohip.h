@@ -243,6 +243,14 @@ int ottohip_kmeans_update(ottohip_ctx* ctx, float* centroids, const int64_t* sum
  * counts, then update (sklearn relocates before the M-step). */
 int ottohip_kmeans_lloyd_iter(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* centroids, int k,
                               int32_t* labels, int64_t* sums, int64_t* counts, double* out, void* stream);
+/* Up to max_steps lloyd_iter steps with a single device->host copy: after each step the device
+ * applies sklearn's stop checks (no label changed; shift^2 <= tol; an empty cluster, which leaves
+ * the centroids untouched for the host's relocation) and the later steps do nothing. out (HOST
+ * double[6]) = out[0..3] of the last step run, steps run, stop reason (0 none, 1 no label changed,
+ * 2 shift^2 <= tol, 3 empty cluster). Shapes the MFMA E-step does not take run one step. */
+int ottohip_kmeans_lloyd_steps(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* centroids, int k,
+                               int32_t* labels, int64_t* sums, int64_t* counts, int max_steps, double tol,
+                               double* out, void* stream);
 int ottohip_kmeans_farthest(ottohip_ctx* ctx, const float* X, int64_t n, int dim, const float* centroids,
                             const int32_t* labels, int m, int64_t* rows, float* d2, void* stream);
 int ottohip_kmeans_relocate(ottohip_ctx* ctx, int64_t* sums, int64_t* counts, int k, int dim, const float* vecs,

@@ -223,7 +223,9 @@ __global__ __launch_bounds__(KM_MT, (NQ <= 13 ? 4 : 2)) void k_km_assign_mfma(co
                                                         unsigned long long* __restrict__ cnt,
                                                         double* __restrict__ inertia,
                                                         unsigned long long* __restrict__ changed,
-                                                        float* __restrict__ dist, int inc) {
+                                                        float* __restrict__ dist, int inc,
+                                                        const int* __restrict__ gate) {
+  if (gate && __builtin_amdgcn_readfirstlane(*gate)) return;  // batched Lloyd steps: converged earlier
   extern __shared__ unsigned long long smem64[];
   float4* Bl = reinterpret_cast<float4*>(smem64);                              // [NB][nq][64]
   int32_t* labl = reinterpret_cast<int32_t*>(Bl + NB * nq * 64);                // [waves][3][32]: row, new, old
@@ -242,7 +244,6 @@ __global__ __launch_bounds__(KM_MT, (NQ <= 13 ? 4 : 2)) void k_km_assign_mfma(co
   if (sums)
     for (int i = tid; i < k * dim + k; i += KM_MT) ls[i] = 0ull;
   __syncthreads();
-  const float cA = cnl[i32], cB = cnl[32 + i32];
   double part = 0.0;
   uint32_t nchg = 0;
   const int64_t ntile = (n + 31) >> 5;
@@ -415,9 +416,18 @@ __global__ __launch_bounds__(KM_MT, (NQ <= 13 ? 4 : 2)) void k_km_assign_mfma(co
 // inc: sums / cnt hold the exact sums / counts of the rows under `labels` (the previous labels) and
 // are updated by the rows whose label changes (MFMA kernel); otherwise they are accumulated from
 // scratch by every row (the caller zeroes them)
+// the MFMA E-step's operand conditions (the VALU kernel takes every other shape)
+static bool km_mfma_ok(int k, int dim, const float* X, const float* C) {
+  static const bool km_valu = getenv("OTTOHIP_KM_VALU") != nullptr;  // A/B switch
+  return !km_valu && k <= 64 && dim <= 8 * KM_NQ && (dim & 3) == 0 && ((uintptr_t)X & 15) == 0 &&
+         ((uintptr_t)C & 15) == 0;
+}
+
+// gate (MFMA kernel only): device flag, nonzero = skip (batched Lloyd steps after convergence)
 static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int64_t n, int dim, const float* C,
                             int32_t* labels, unsigned long long* sums, unsigned long long* cnt, double* inr,
-                            unsigned long long* changed = nullptr, float* dist = nullptr, int inc = 0) {
+                            unsigned long long* changed = nullptr, float* dist = nullptr, int inc = 0,
+                            const int* gate = nullptr) {
   const int KP = (k + 7) / 8 * 8;
   float *Ct, *cn;
   OH_TRY(ctx->ws.get("km_ct", (size_t)KP * dim, &Ct));
@@ -425,9 +435,7 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
   k_km_prep<<<grid_for(std::max<int64_t>((int64_t)KP * dim, KM_MAXK)), 256, 0, s>>>(C, k, dim, KP, Ct, cn);
   // the MFMA kernel measured 6.4 ms per Lloyd step at 12.9 M x 100, k = 50, against 5.1 ms for
   // the VALU kernel below (argmin butterflies and half the rows per wave): opt-in A/B switch only
-  static const bool km_valu = getenv("OTTOHIP_KM_VALU") != nullptr;  // A/B switch
-  if (!km_valu && k <= 64 && dim <= 8 * KM_NQ && (dim & 3) == 0 && ((uintptr_t)X & 15) == 0 &&
-      ((uintptr_t)C & 15) == 0) {
+  if (km_mfma_ok(k, dim, X, C)) {
     const int nq = (dim + 7) / 8, NB = k <= 32 ? 1 : 2;
     const size_t lds = (size_t)NB * nq * 64 * 16 + (KM_MT / 64) * 96 * 4 + 64 * 4 +
                        (sums ? ((size_t)k * dim + k) * 8 : 8);
@@ -438,10 +446,11 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
                          : (NB == 1 ? k_km_assign_mfma<1, KM_NQ> : k_km_assign_mfma<2, KM_NQ>);
     OH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)lds));
-    kern<<<grid, KM_MT, lds, s>>>(X, n, dim, nq, C, cn, k, labels, sums, cnt, inr, changed, dist, inc);
+    kern<<<grid, KM_MT, lds, s>>>(X, n, dim, nq, C, cn, k, labels, sums, cnt, inr, changed, dist, inc, gate);
     OH_HIP(hipGetLastError());
     return 0;
   }
+  if (gate) { set_error("kmeans: batched steps need the MFMA E-step"); return OTTOHIP_EINVAL; }
   if (inc && sums) {  // the VALU kernel accumulates from scratch
     OH_HIP(hipMemsetAsync(sums, 0, (size_t)k * dim * 8, s));
     OH_HIP(hipMemsetAsync(cnt, 0, (size_t)k * 8, s));
@@ -531,12 +540,19 @@ __global__ void k_km_relocate(unsigned long long* __restrict__ sums, unsigned lo
 // relocates (sklearn's order: relocation before the update) and calls the update again.
 // st: [0] shift^2 (double), [1] empty clusters (u64)
 constexpr int KM_UT = 256;
+// ctl (batched Lloyd steps, else nullptr): [0] stop reason (0 running, 1 no label changed, 2 shift^2 <=
+// tol, 3 empty cluster: centroids untouched, the host relocates), [1] steps run; a step after a
+// stop does nothing (its E-step was skipped too)
 __global__ __launch_bounds__(KM_UT) void k_km_update(float* __restrict__ C, const long long* __restrict__ sums,
                                                      const long long* __restrict__ cnt, int k, int dim,
-                                                     int commit_if_full, double* __restrict__ st) {
+                                                     int commit_if_full, double* __restrict__ st,
+                                                     int* __restrict__ ctl = nullptr,
+                                                     const unsigned long long* __restrict__ changed = nullptr,
+                                                     double tol = 0.0) {
   __shared__ double red[KM_UT];
   __shared__ int n_empty;
   const int tid = threadIdx.x;
+  if (ctl && __builtin_amdgcn_readfirstlane(ctl[0])) return;
   if (tid == 0) n_empty = 0;
   __syncthreads();
   for (int c = tid; c < k; c += KM_UT)
@@ -563,7 +579,15 @@ __global__ __launch_bounds__(KM_UT) void k_km_update(float* __restrict__ C, cons
   if (tid == 0) {
     st[0] = commit ? red[0] : -1.0;
     reinterpret_cast<unsigned long long*>(st)[1] = (unsigned long long)ne;
+    if (ctl) {  // sklearn 1.2 _kmeans_single_lloyd's checks after each step
+      ctl[1] += 1;
+      ctl[0] = !commit ? 3 : (*changed == 0 ? 1 : (red[0] <= tol ? 2 : 0));
+    }
   }
+}
+
+__global__ void k_km_gate_reset(const int* __restrict__ ctl, double* __restrict__ st) {
+  if (threadIdx.x < 4 && !ctl[0]) st[threadIdx.x] = 0.0;
 }
 
 // per column: sum of x and of (x - center)^2 in 2^-24 fixed point (exact, order-independent);
@@ -921,6 +945,57 @@ int ottohip_kmeans_lloyd_iter(ottohip_ctx* ctx, const float* X, int64_t n, int d
   out[1] = (double)c;
   out[2] = h[2];
   out[3] = (double)e;
+  return 0;
+}
+
+// Up to max_steps Lloyd iterations with one device->host copy: each step's update kernel checks
+// sklearn's stop conditions on the device and gates the later steps. out[0..3] as lloyd_iter for the
+// last step run, out[4] steps run, out[5] stop reason (0 none, 1 no label changed, 2 shift^2 <= tol,
+// 3 empty cluster: centroids untouched, relocate then ottohip_kmeans_update).
+int ottohip_kmeans_lloyd_steps(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* centroids, int k,
+                               int32_t* labels, int64_t* sums, int64_t* counts, int max_steps, double tol,
+                               double* out, void* stream) {
+  if (!ctx || !X || !centroids || !labels || !sums || !counts || !out || n < 1 || dim < 1 || dim > EMB_MAXD ||
+      k < 1 || k > KM_MAXK || max_steps < 1) {
+    set_error("kmeans_lloyd_steps: bad arguments (k <= %d, dim <= %d)", KM_MAXK, EMB_MAXD); return OTTOHIP_EINVAL;
+  }
+  if (((size_t)k * dim + k) * 8 > 65536) { set_error("kmeans_lloyd_steps: k * dim too large for LDS"); return OTTOHIP_ELIMIT; }
+  if (!km_mfma_ok(k, dim, X, centroids)) {  // VALU E-step: one step, stop reason from the host
+    OH_TRY(ottohip_kmeans_lloyd_iter(ctx, X, n, dim, centroids, k, labels, sums, counts, out, stream));
+    out[4] = 1;
+    out[5] = out[3] > 0 ? 3 : (out[1] == 0 ? 1 : (out[2] <= tol ? 2 : 0));
+    return 0;
+  }
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  double* st;  // [inertia, changed, shift, empty]
+  int* ctl;
+  OH_TRY(ctx->ws.get("km_stats", 4, &st));
+  OH_TRY(ctx->ws.get("km_ctl", 2, &ctl));
+  OH_HIP(hipMemsetAsync(ctl, 0, 2 * sizeof(int), s));
+  for (int i = 0; i < max_steps; ++i) {
+    k_km_gate_reset<<<1, 64, 0, s>>>(ctl, st);
+    OH_TRY(launch_km_assign(ctx, k, s, X, n, dim, centroids, labels, reinterpret_cast<unsigned long long*>(sums),
+                            reinterpret_cast<unsigned long long*>(counts), st,
+                            reinterpret_cast<unsigned long long*>(st + 1), nullptr, 1, ctl));
+    k_km_update<<<1, KM_UT, 0, s>>>(centroids, reinterpret_cast<const long long*>(sums),
+                                    reinterpret_cast<const long long*>(counts), k, dim, 1, st + 2, ctl,
+                                    reinterpret_cast<const unsigned long long*>(st + 1), tol);
+  }
+  OH_HIP(hipGetLastError());
+  double h[4];
+  int c2[2];
+  OH_TRY(d2h(h, st, 4, s));
+  OH_TRY(d2h(c2, ctl, 2, s));
+  unsigned long long c, e;
+  memcpy(&c, &h[1], 8);
+  memcpy(&e, &h[3], 8);
+  out[0] = h[0];
+  out[1] = (double)c;
+  out[2] = h[2];
+  out[3] = (double)e;
+  out[4] = c2[1];
+  out[5] = c2[0];
   return 0;
 }
 

@@ -57,6 +57,7 @@ def compute_sessions_embeddings(offsets, aid, ts, type_, words, embeddings, n_it
 
 
 FX = float(1 << 24)  # fixed-point scale of the device sums (csrc/popularity.hip KM_FX)
+LLOYD_BATCH = 10  # Lloyd steps per ottohip_kmeans_lloyd_steps call (the stop checks run on the device)
 
 
 def _allreduce(t, group):
@@ -159,7 +160,7 @@ class KMeans:
         labels = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
         best = None
         inr, chg, shift = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
-        st4 = (ctypes.c_double * 4)()
+        st6 = (ctypes.c_double * 6)()
         for run in range(self.n_init):
             seeds = next(seed_stream)
             C = self._gather_rows(Xc, seeds, grows, group)
@@ -167,20 +168,27 @@ class KMeans:
             sums.zero_()  # the one-GPU iteration keeps sums / counts of the current labels incrementally
             counts.zero_()
             strict, it = False, 0
-            for it in range(1, self.max_iter + 1):
-                if group is None:  # E-step + M-step, one device->host copy per iteration
-                    _lib.check(lib.ottohip_kmeans_lloyd_iter(ctx.h, _lib.ptr(Xc), n, dim, _lib.ptr(C), k,
-                                                             _lib.ptr(labels), _lib.ptr(sums), _lib.ptr(counts), st4,
-                                                             sh))
-                    n_changed = int(st4[1])
-                    shift.value = st4[2]
-                    if st4[3] > 0:  # empty clusters: relocate on a copy (sums / counts follow the labels), M-step
+            if group is None:  # batches of Lloyd steps, the stop checks on the device, one copy per batch
+                while it < self.max_iter:
+                    _lib.check(lib.ottohip_kmeans_lloyd_steps(ctx.h, _lib.ptr(Xc), n, dim, _lib.ptr(C), k,
+                                                              _lib.ptr(labels), _lib.ptr(sums), _lib.ptr(counts),
+                                                              min(LLOYD_BATCH, self.max_iter - it), tol_abs, st6, sh))
+                    it += int(st6[4])
+                    n_changed, reason = int(st6[1]), int(st6[5])
+                    shift.value = st6[2]
+                    if reason == 3:  # empty clusters: relocate on a copy (sums / counts follow the labels), M-step
                         rs_, rc_ = sums.clone(), counts.clone()
                         empty = np.flatnonzero(rc_.cpu().numpy() == 0)
                         self._relocate(Xc, C, labels, rs_, rc_, empty, grows, group, ctx, sh)
                         _lib.check(lib.ottohip_kmeans_update(ctx.h, _lib.ptr(C), _lib.ptr(rs_), _lib.ptr(rc_), k,
                                                              dim, ctypes.byref(shift), sh))
-                else:
+                        reason = 1 if n_changed == 0 else (2 if shift.value <= tol_abs else 0)
+                    if reason == 1:
+                        strict = True
+                    if reason in (1, 2):
+                        break
+            else:
+                for it in range(1, self.max_iter + 1):
                     _lib.check(lib.ottohip_kmeans_partial(ctx.h, _lib.ptr(Xc), n, dim, _lib.ptr(C), k,
                                                           _lib.ptr(labels), _lib.ptr(sums), _lib.ptr(counts),
                                                           ctypes.byref(inr), ctypes.byref(chg), sh))
@@ -192,11 +200,11 @@ class KMeans:
                         self._relocate(Xc, C, labels, sums, counts, empty, grows, group, ctx, sh)
                     _lib.check(lib.ottohip_kmeans_update(ctx.h, _lib.ptr(C), _lib.ptr(sums), _lib.ptr(counts), k,
                                                          dim, ctypes.byref(shift), sh))
-                if n_changed == 0:
-                    strict = True
-                    break
-                if shift.value <= tol_abs:
-                    break
+                    if n_changed == 0:
+                        strict = True
+                        break
+                    if shift.value <= tol_abs:
+                        break
             if not strict:  # E-step with the final centres (labels match cluster_centers_)
                 _lib.check(lib.ottohip_kmeans_partial(ctx.h, _lib.ptr(Xc), n, dim, _lib.ptr(C), k, _lib.ptr(labels),
                                                       _lib.ptr(sums), _lib.ptr(counts), ctypes.byref(inr),
