@@ -96,6 +96,9 @@ int exclusive_scan_u64(Ctx* ctx, const uint64_t* in, uint64_t* out, int64_t n, u
 
 // ------------------------------------------------------------------ radix sort
 constexpr int RS_T = 256, RS_WAVES = RS_T / 64, RS_R = 16, RS_TILE = RS_T * RS_R;  // 4096
+// a block sorts RS_SUB consecutive tiles in order, so the digit-count matrix (and its scan) has one
+// column per 4 tiles: the scan of every pass was larger than the scatter's own work
+constexpr int RS_SUB = 4, RS_BLOCK = RS_TILE * RS_SUB;
 
 __global__ __launch_bounds__(RS_T) void k_rs_hist(const uint32_t* __restrict__ keys, int64_t n, int shift,
                                                   uint32_t* __restrict__ hist, int nb) {
@@ -103,9 +106,9 @@ __global__ __launch_bounds__(RS_T) void k_rs_hist(const uint32_t* __restrict__ k
   for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_T) (&h[0][0])[i] = 0;
   __syncthreads();
   const int w = threadIdx.x >> 6;
-  const int64_t t0 = (int64_t)blockIdx.x * RS_TILE;
+  const int64_t t0 = (int64_t)blockIdx.x * RS_BLOCK;
 #pragma unroll 4
-  for (int r = 0; r < RS_R; ++r) {
+  for (int r = 0; r < RS_R * RS_SUB; ++r) {
     const int64_t idx = t0 + r * RS_T + threadIdx.x;
     if (idx < n) atomicAdd(&h[w][(keys[idx] >> shift) & 255u], 1u);
   }
@@ -124,69 +127,78 @@ __global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict_
                                                      const uint64_t* __restrict__ gofs, int nb, int iota) {
   __shared__ uint32_t wcnt[RS_WAVES][256];
   __shared__ uint32_t bstart[256];
+  __shared__ uint32_t tcnt[256];  // the sub-tile's count per digit
+  __shared__ uint32_t run[256];   // keys of each digit written by the block's earlier sub-tiles
   __shared__ uint32_t wsum[RS_WAVES];
   __shared__ uint32_t stage_k[RS_TILE];
   __shared__ uint32_t stage_v[RS_TILE];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
-  const int64_t t0 = (int64_t)blockIdx.x * RS_TILE;
-  for (int i = tid; i < RS_WAVES * 256; i += RS_T) (&wcnt[0][0])[i] = 0;
-  __syncthreads();
-  uint32_t key[RS_R], val[RS_R], rnk[RS_R];
-  // wave w owns the contiguous quarter [t0 + w*1024, t0 + (w+1)*1024): stable order
-#pragma unroll
-  for (int r = 0; r < RS_R; ++r) {
-    const int64_t idx = t0 + w * (RS_R * 64) + r * 64 + l;
-    const bool valid = idx < n;
-    key[r] = valid ? kin[idx] : 0u;
-    val[r] = valid ? (iota ? (uint32_t)idx : vin[idx]) : 0u;
-    const uint32_t d = (key[r] >> shift) & 255u;
-    uint64_t m = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      const bool bit = (d >> b) & 1u;
-      const uint64_t bb = __ballot(bit);
-      m &= bit ? bb : ~bb;
-    }
-    const uint32_t below = mbcnt(m);
-    const uint32_t old = wcnt[w][d];
-    __builtin_amdgcn_wave_barrier();
-    if (valid && below == 0) wcnt[w][d] = old + (uint32_t)__popcll(m);
-    __builtin_amdgcn_wave_barrier();
-    rnk[r] = old + below;
-  }
-  __syncthreads();
-  // per digit: wave offsets (exclusive over waves) and the tile-local digit start
-  {
-    const int d = tid;  // RS_T == 256 digits
-    uint32_t tot = 0;
-#pragma unroll
-    for (int k = 0; k < RS_WAVES; ++k) { uint32_t c = wcnt[k][d]; wcnt[k][d] = tot; tot += c; }
-    const uint32_t incl = wave_incl_scan(tot);
-    if (l == 63) wsum[w] = incl;
+  run[tid] = 0;  // RS_T == 256 digits
+  for (int sub = 0; sub < RS_SUB; ++sub) {
+    const int64_t t0 = (int64_t)blockIdx.x * RS_BLOCK + (int64_t)sub * RS_TILE;
+    if (t0 >= n) break;
+    for (int i = tid; i < RS_WAVES * 256; i += RS_T) (&wcnt[0][0])[i] = 0;
     __syncthreads();
-    uint32_t pre = 0;
-    for (int k = 0; k < w; ++k) pre += wsum[k];
-    bstart[d] = pre + incl - tot;
-  }
-  __syncthreads();
+    uint32_t key[RS_R], val[RS_R], rnk[RS_R];
+    // wave w owns the contiguous quarter [t0 + w*1024, t0 + (w+1)*1024): stable order
 #pragma unroll
-  for (int r = 0; r < RS_R; ++r) {
-    const int64_t idx = t0 + w * (RS_R * 64) + r * 64 + l;
-    if (idx < n) {
+    for (int r = 0; r < RS_R; ++r) {
+      const int64_t idx = t0 + w * (RS_R * 64) + r * 64 + l;
+      const bool valid = idx < n;
+      key[r] = valid ? kin[idx] : 0u;
+      val[r] = valid ? (iota ? (uint32_t)idx : vin[idx]) : 0u;
       const uint32_t d = (key[r] >> shift) & 255u;
-      const uint32_t p = bstart[d] + wcnt[w][d] + rnk[r];
-      stage_k[p] = key[r];
-      stage_v[p] = val[r];
+      uint64_t m = __ballot(valid);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        m &= bit ? bb : ~bb;
+      }
+      const uint32_t below = mbcnt(m);
+      const uint32_t old = wcnt[w][d];
+      __builtin_amdgcn_wave_barrier();
+      if (valid && below == 0) wcnt[w][d] = old + (uint32_t)__popcll(m);
+      __builtin_amdgcn_wave_barrier();
+      rnk[r] = old + below;
     }
-  }
-  __syncthreads();
-  const int64_t tn = n - t0 < RS_TILE ? n - t0 : RS_TILE;
-  for (int p = tid; p < tn; p += RS_T) {
-    const uint32_t k = stage_k[p];
-    const uint32_t d = (k >> shift) & 255u;
-    const uint64_t dst = gofs[(int64_t)d * nb + blockIdx.x] + (uint64_t)(p - bstart[d]);
-    kout[dst] = k;
-    vout[dst] = stage_v[p];
+    __syncthreads();
+    // per digit: wave offsets (exclusive over waves) and the tile-local digit start
+    {
+      const int d = tid;  // RS_T == 256 digits
+      uint32_t tot = 0;
+#pragma unroll
+      for (int k = 0; k < RS_WAVES; ++k) { uint32_t c = wcnt[k][d]; wcnt[k][d] = tot; tot += c; }
+      tcnt[d] = tot;
+      const uint32_t incl = wave_incl_scan(tot);
+      if (l == 63) wsum[w] = incl;
+      __syncthreads();
+      uint32_t pre = 0;
+      for (int k = 0; k < w; ++k) pre += wsum[k];
+      bstart[d] = pre + incl - tot;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RS_R; ++r) {
+      const int64_t idx = t0 + w * (RS_R * 64) + r * 64 + l;
+      if (idx < n) {
+        const uint32_t d = (key[r] >> shift) & 255u;
+        const uint32_t p = bstart[d] + wcnt[w][d] + rnk[r];
+        stage_k[p] = key[r];
+        stage_v[p] = val[r];
+      }
+    }
+    __syncthreads();
+    const int64_t tn = n - t0 < RS_TILE ? n - t0 : RS_TILE;
+    for (int p = tid; p < tn; p += RS_T) {
+      const uint32_t k = stage_k[p];
+      const uint32_t d = (k >> shift) & 255u;
+      const uint64_t dst = gofs[(int64_t)d * nb + blockIdx.x] + run[d] + (uint64_t)(p - bstart[d]);
+      kout[dst] = k;
+      vout[dst] = stage_v[p];
+    }
+    __syncthreads();  // run / stage / wcnt are rewritten by the next sub-tile
+    run[tid] += tcnt[tid];
   }
 }
 
@@ -198,7 +210,7 @@ int radix_sort_pairs(Ctx* ctx, uint32_t*& keys, uint32_t*& vals, uint32_t* keys_
     return 0;
   }
   if (n >= ((int64_t)1 << 32)) { set_error("radix_sort_pairs: n=%lld too large", (long long)n); return OTTOHIP_ELIMIT; }
-  const int nb = (int)ceil_div(n, RS_TILE);
+  const int nb = (int)ceil_div(n, RS_BLOCK);
   uint32_t* hist; uint64_t* gofs;
   OH_TRY(ctx->ws.get("rs_hist", (size_t)nb * 256, &hist));
   OH_TRY(ctx->ws.get("rs_gofs", (size_t)nb * 256, &gofs));
