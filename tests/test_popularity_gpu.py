@@ -53,6 +53,24 @@ def test_kmeans_matches_restatement(gpu):
     _check_kmeans(X, 10)
 
 
+def test_kmeans_lloyd_step_batches_equal_single_steps(gpu, monkeypatch):
+    """ottohip_kmeans_lloyd_steps: the device-side stop checks and gating of later steps give the
+    same clustering as one step per call (labels, centres, inertia, iterations bit-identical)."""
+    from otto_recommender_amd import popularity as gp
+    rng = np.random.default_rng(7)
+    centers = rng.normal(scale=2, size=(9, 100))
+    X = (centers[rng.integers(0, 9, 30000)] + rng.normal(size=(30000, 100))).astype(np.float32)
+    X[:4000] = X[0]  # duplicated rows: empty clusters on some seeds (relocation between batches)
+    fits = []
+    for batch in (1, 10):
+        monkeypatch.setattr(gp, "LLOYD_BATCH", batch)
+        km = gp.KMeans(n_clusters=9, random_state=42).fit(X)
+        fits.append((km.labels_.cpu().numpy(), km.cluster_centers_.cpu().numpy(), km.inertia_, km.n_iter_))
+    np.testing.assert_array_equal(fits[0][0], fits[1][0])
+    np.testing.assert_array_equal(fits[0][1], fits[1][1])
+    assert fits[0][2] == fits[1][2] and fits[0][3] == fits[1][3]
+
+
 def test_kmeans_empty_cluster_relocation(gpu):
     """a third of the rows identical: seeds collide, clusters empty out and are relocated to the
     farthest rows (_relocate_empty_clusters_dense)"""
