@@ -36,18 +36,31 @@ __global__ __launch_bounds__(64) void k_sess_emb(const int64_t* __restrict__ off
   for (int o = 32; o >= 1; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
   float acc0 = 0.f, acc1 = 0.f, wsum = 0.f;
   const float wt[3] = {0.1f, 0.3f, 0.6f};
-  for (int64_t e = e0; e < e1; ++e) {
-    double wtime = 1.0 - (double)(mx - ts[e]) / 259200.0;
-    if (wtime < 0.10) wtime = 0.10;
-    const int y = type[e];
-    const float w = (float)(wtime * (double)wt[y < 0 ? 0 : (y > 2 ? 2 : y)]);
-    const int32_t a = aid[e];
-    const int32_t r = (a >= 0 && a < n_aid_map) ? row_of_aid[a] : -1;
-    wsum += w;
-    if (r >= 0) {
-      const float* v = emb + (int64_t)r * dim;
-      if (l < dim) acc0 += v[l] * w;
-      if (l + 64 < dim) acc1 += v[l + 64] * w;
+  // lanes fetch 64 events' weights and embedding rows at once (independent loads); the sums then
+  // run over the events in order, exactly as one event at a time
+  for (int64_t b = e0; b < e1; b += 64) {
+    const int64_t e = b + l;
+    float w = 0.f;
+    int32_t r = -1;
+    if (e < e1) {
+      double wtime = 1.0 - (double)(mx - ts[e]) / 259200.0;
+      if (wtime < 0.10) wtime = 0.10;
+      const int y = type[e];
+      w = (float)(wtime * (double)wt[y < 0 ? 0 : (y > 2 ? 2 : y)]);
+      const int32_t a = aid[e];
+      r = (a >= 0 && a < n_aid_map) ? row_of_aid[a] : -1;
+    }
+    const int cnt = (int)(e1 - b < 64 ? e1 - b : 64);
+#pragma unroll 4
+    for (int j = 0; j < cnt; ++j) {
+      const float wj = __shfl(w, j);
+      const int32_t rj = __shfl(r, j);
+      wsum += wj;
+      if (rj >= 0) {
+        const float* v = emb + (int64_t)rj * dim;
+        if (l < dim) acc0 += v[l] * wj;
+        if (l + 64 < dim) acc1 += v[l + 64] * wj;
+      }
     }
   }
   float* o = out + s * dim;
