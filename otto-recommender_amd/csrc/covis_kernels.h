@@ -1097,7 +1097,33 @@ __device__ __forceinline__ void wave_bitonic_sort(uint32_t (&v)[M]) {
     for (int j = k >> 1; j > 0; j >>= 1) {
       // sentinels by arithmetic on the lane bits (no lane-mask registers): 0 = keep the min
       const int kb = __builtin_ctz(k), jb = __builtin_ctz(j);
-      if (j >= M) {  // partner in lane l ^ (j / M), same register; direction from lane bits only
+      if (j >= M && (j / M == 16 || j / M == 32) && M >= 2) {
+        // partner 16 / 32 lanes away: one v_permlane16/32_swap of two registers puts every pair's
+        // lower element in the first and its upper element in the second at the same lane, an
+        // in-lane compare-exchange (two med3) sorts both registers' pairs, a second swap puts
+        // them back: 2 VALU per register instead of a swap, a copy, a select and a med3
+        const uint32_t lo_lane = l & ~(uint32_t)(j / M);  // lane of the pair's lower element
+        const uint32_t smin = 0u - (((lo_lane * M) >> kb) & 1u);  // 0: the lower element takes the min
+#pragma unroll
+        for (int m = 0; m < M; m += 2) {
+          uint32_t x = v[m], y = v[m + 1];
+          if (j / M == 16) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+            x = sw[0]; y = sw[1];
+          } else {
+            const auto sw = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+            x = sw[0]; y = sw[1];
+          }
+          const uint32_t lo = umed3(x, y, smin), hi = umed3(x, y, ~smin);
+          if (j / M == 16) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(lo, hi, false, false);
+            v[m] = sw[0]; v[m + 1] = sw[1];
+          } else {
+            const auto sw = __builtin_amdgcn_permlane32_swap(lo, hi, false, false);
+            v[m] = sw[0]; v[m + 1] = sw[1];
+          }
+        }
+      } else if (j >= M) {  // partner in lane l ^ (j / M), same register; direction from lane bits only
         const uint32_t sent = 0u - ((((l * M) >> kb) ^ ((l * M) >> jb)) & 1u);
 #pragma unroll
         for (int m = 0; m < M; ++m) v[m] = umed3(v[m], xor_lane_n(v[m], j / M), sent);
