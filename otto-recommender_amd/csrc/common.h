@@ -143,10 +143,9 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t v) {  // value of lane (th
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
   } else if constexpr (J == 2) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
-  } else if constexpr (J == 4) {
-    const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x104, 0xF, 0xF, true);
-    const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x114, 0xF, 0xF, true);
-    return (lane_id() & 4u) ? dn : up;
+  } else if constexpr (J == 4) {  // ds_swizzle bitmask mode (xor 4, within 32 lanes): one LDS-crossbar
+                                   // instruction instead of two DPP moves and a select
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (4 << 10) | 0x1F);
   } else if constexpr (J == 8) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, true);  // row_ror:8
   } else if constexpr (J == 16) {
