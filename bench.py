@@ -70,6 +70,30 @@ def cpu_baseline(seed: int = 0, pandas_files: int = 10) -> dict:
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16, /opt/skills/guides/MI355X_MICROARCH.md
 
 
+def bench_a6(dev, tab, ctx) -> dict:
+    """A6 (model/count_co_events.py:103-181) on the counted 220 M-event table, per rule: the per-file
+    count >= 2 filter, the part-wise branch (2) where N > MAX_ROWS_POLARS_GROUPBY (its parts are
+    recounted from the resident events), MIN_COUNT_TO_SAVE, count-desc order and head. Timed after
+    the co-visitation steps and reported beside the line (the reference's ETAs cover count + merge,
+    :202, :210); not part of `value`."""
+    import torch
+    from otto_recommender_amd import covis as gc, config as cfg
+    per = {}
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for n in tab.names:
+        t1 = time.perf_counter()
+        a, _, _ = gc.concat_files_w_stats_fused(dev, n, table=tab, ctx=ctx)
+        torch.cuda.synchronize()
+        st = tab.stats(n)
+        use_ge2 = "click_to" in n and st["file_rows"] > cfg.CLICK_FILTER_ROWS
+        N = st["file_rows_ge2"] if use_ge2 else st["file_rows"]
+        per[n] = {"ms": round((time.perf_counter() - t1) * 1e3, 2), "rows_out": int(a.numel()),
+                  "file_rows_N": int(N), "part_wise": bool(N > cfg.MAX_ROWS_POLARS_GROUPBY)}
+        del a
+    return {"per_rule": per, "total_ms": round((time.perf_counter() - t0) * 1e3, 2)}
+
+
 def bench_knn(steps: int, warmup: int, n_items: int, n_q: int, with_cpu: bool, group=None) -> dict:
     """BASELINE configs[2]: exact top-20 kNN of the first n_q vocabulary rows. group: the queries
     are split in equal ranges over the ranks (the item matrix replicated on every GPU, SURVEY.md
@@ -213,6 +237,7 @@ def main():
     ap.add_argument("--events", type=int, default=220_000_000)
     ap.add_argument("--pandas-files", type=int, default=10, help="files of the pandas reference-algorithm baseline")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-a6", action="store_true", help="skip the A6 (concat_files_w_stats) timing beside the line")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--knn-steps", type=int, default=2, help="0 disables the configs[2] kNN measurement")
     ap.add_argument("--workload", choices=["covis", "knn", "candidates"], default="covis",
@@ -312,6 +337,13 @@ def main():
     tab = step()
     phases = ctx.timings()
     ctx.set_timing(False)
+    a6 = None
+    if world == 1 and not args.no_a6:
+        ctx.trim()  # the build's word buffers are not needed by A6
+        try:  # reported beside the line; it must not cost the main line
+            a6 = bench_a6(dev, tab, ctx)
+        except Exception as exc:  # noqa: BLE001
+            a6 = {"error": repr(exc)}
     tab.free()
 
     t_step = dt / args.steps
@@ -384,6 +416,10 @@ def main():
         "phases_ms": {p[0]: round(p[1], 3) for p in phases},
         "gen_s": round(gen_s, 1),
     }
+    if a6 is not None:
+        if "total_ms" in a6:
+            a6["count_plus_merge_ms"] = round(t_step * 1e3 + a6["total_ms"], 2)
+        out["a6"] = a6
     if not args.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(args.seed, args.pandas_files)
     if args.knn_steps > 0:

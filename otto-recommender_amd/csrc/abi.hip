@@ -835,14 +835,16 @@ int ottohip_table_copy(const ottohip_table* t, int rule, int32_t* aid, int32_t* 
   hipStream_t s = S(stream);
   Ctx* ctx = t->ctx;
   const int64_t n = t->n_slots;
-  uint32_t* flag;
-  uint64_t* idx;
-  OH_TRY(ctx->ws.get("copy_flag", (size_t)n, &flag));
-  OH_TRY(ctx->ws.get("copy_idx", (size_t)n, &idx));
-  k_select_rule<<<grid_for(n), 256, 0, s>>>(t->b.rule, n, rule, flag);
-  OH_TRY(exclusive_scan_u32(ctx, flag, idx, n, nullptr, s));
-  k_compact_rule<<<grid_for(n), 256, 0, s>>>(t->b.rule, n, rule, idx, t->b.aid, t->b.aid_next,
-                                                     t->b.count, t->b.count_ge2, aid, aid_next, count, count_ge2);
+  const int64_t nb = ceil_div(n, FIN_B);
+  uint32_t* bcnt;
+  uint64_t* boff;
+  OH_TRY(ctx->ws.get("blk_cnt", (size_t)nb, &bcnt));
+  OH_TRY(ctx->ws.get("blk_off", (size_t)nb, &boff));
+  k_blk_count<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.count, t->b.count_ge2, n, rule, 0, 0u, bcnt);
+  OH_TRY(exclusive_scan_u32(ctx, bcnt, boff, nb, nullptr, s));
+  k_blk_compact<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n,
+                                               rule, 0, 0u, boff, reinterpret_cast<uint32_t*>(aid),
+                                               reinterpret_cast<uint32_t*>(aid_next), count, count_ge2);
   OH_HIP(hipGetLastError());
   return 0;
 }
@@ -885,13 +887,15 @@ extern "C" int ottohip_table_finalize(ottohip_ctx* ctx, const ottohip_table* t, 
   const uint32_t thr = (uint32_t)std::max<int32_t>(mp->min_count, 1);
   Workspace& ws = ctx->ws;
   const int64_t n = t->n_slots;
-  uint32_t* flag;
-  uint64_t *idx, *tot;
-  OH_TRY(ws.get("fin_flag", (size_t)n, &flag));
-  OH_TRY(ws.get("fin_idx", (size_t)n, &idx));
+  const int64_t nb = ceil_div(n, FIN_B);
+  uint32_t* bcnt;
+  uint64_t *boff, *tot;
+  OH_TRY(ws.get("blk_cnt", (size_t)nb, &bcnt));
+  OH_TRY(ws.get("blk_off", (size_t)nb, &boff));
   OH_TRY(ws.get("fin_tot", 1, &tot));
-  k_fin_select<<<grid_for(n), 256, 0, s>>>(t->b.rule, t->b.count, t->b.count_ge2, n, rule, use_ge2 ? 1 : 0, thr, flag);
-  OH_TRY(exclusive_scan_u32(ctx, flag, idx, n, tot, s));
+  k_blk_count<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.count, t->b.count_ge2, n, rule, use_ge2 ? 1 : 0, thr,
+                                             bcnt);
+  OH_TRY(exclusive_scan_u32(ctx, bcnt, boff, nb, tot, s));
   uint64_t m = 0;
   OH_TRY(d2h(&m, tot, 1, s));
   if (m == 0) return 0;
@@ -903,8 +907,8 @@ extern "C" int ottohip_table_finalize(ottohip_ctx* ctx, const ottohip_table* t, 
   OH_TRY(ws.get("fin_v0", (size_t)m, &v0));
   OH_TRY(ws.get("fin_k1", (size_t)m, &k1));
   OH_TRY(ws.get("fin_v1", (size_t)m, &v1));
-  k_fin_compact<<<grid_for(n), 256, 0, s>>>(flag, idx, n, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2,
-                                            use_ge2 ? 1 : 0, sa, sb, sc);
+  k_blk_compact<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n,
+                                               rule, use_ge2 ? 1 : 0, thr, boff, sa, sb, sc, nullptr);
   // LSD: aid_next asc, then aid asc, then count desc (stable) -> (count desc, aid, aid_next);
   // aids are < n_items, so their passes cover bits_for(n_items) bits (3 x 8 at 1.86 M items)
   const int abits = std::max(1, bits_for((uint64_t)t->n_items));

@@ -1750,43 +1750,66 @@ __global__ void k_split_classify(const Task* __restrict__ tasks, int64_t n, cons
 }
 
 // ------------------------------------------------------------------ per-rule compaction
-__global__ void k_select_rule(const uint8_t* __restrict__ rule, int64_t n, int r, uint32_t* __restrict__ flag) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) flag[i] = rule[i] == (uint8_t)r;
+// One rule's rows of a table, compacted in slot order without per-slot flag / index arrays:
+// per 4096-slot block a count (k_blk_count), one scan over the blocks, and a compaction that
+// re-evaluates the predicate with wave ballots and block prefixes (k_blk_compact). The predicate is
+// rule == r and, with thr > 0, (use_ge2 ? count_ge2 : count) >= thr.
+constexpr int FIN_T = 256, FIN_PER = 16, FIN_B = FIN_T * FIN_PER;
+__device__ __forceinline__ bool blk_keep(const uint8_t* __restrict__ rule, const uint32_t* __restrict__ c,
+                                         const uint32_t* __restrict__ c2, int64_t i, int r, int use_ge2,
+                                         uint32_t thr) {
+  if (rule[i] != (uint8_t)r) return false;
+  return thr == 0 || (use_ge2 ? c2[i] : c[i]) >= thr;
 }
-__global__ void k_compact_rule(const uint8_t* __restrict__ rule, int64_t n, int r, const uint64_t* __restrict__ idx,
-                               const int32_t* __restrict__ a, const int32_t* __restrict__ b,
-                               const uint32_t* __restrict__ c, const uint32_t* __restrict__ c2,
-                               int32_t* __restrict__ oa, int32_t* __restrict__ ob, uint32_t* __restrict__ oc,
-                               uint32_t* __restrict__ oc2) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || rule[i] != (uint8_t)r) return;
-  const uint64_t p = idx[i];
-  if (oa) oa[p] = a[i];
-  if (ob) ob[p] = b[i];
-  if (oc) oc[p] = c[i];
-  if (oc2) oc2[p] = c2[i];
+__global__ __launch_bounds__(FIN_T) void k_blk_count(const uint8_t* __restrict__ rule, const uint32_t* __restrict__ c,
+                                                     const uint32_t* __restrict__ c2, int64_t n, int r, int use_ge2,
+                                                     uint32_t thr, uint32_t* __restrict__ bcnt) {
+  __shared__ uint32_t wt[FIN_T / 64];
+  const int64_t base = (int64_t)blockIdx.x * FIN_B;
+  uint32_t k = 0;
+#pragma unroll 4
+  for (int q = 0; q < FIN_PER; ++q) {
+    const int64_t i = base + q * FIN_T + threadIdx.x;
+    k += (i < n && blk_keep(rule, c, c2, i, r, use_ge2, thr)) ? 1u : 0u;
+  }
+  k = wave_sum(k);
+  if ((threadIdx.x & 63) == 0) wt[threadIdx.x >> 6] = k;
+  __syncthreads();
+  if (threadIdx.x == 0) bcnt[blockIdx.x] = wt[0] + wt[1] + wt[2] + wt[3];
+}
+// outputs (nullable): o0 = aid, o1 = aid_next, o2 = use_ge2 ? count_ge2 : count, o3 = count_ge2
+__global__ __launch_bounds__(FIN_T) void k_blk_compact(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
+                                                       const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
+                                                       const uint32_t* __restrict__ c2, int64_t n, int r, int use_ge2,
+                                                       uint32_t thr, const uint64_t* __restrict__ boff,
+                                                       uint32_t* __restrict__ o0, uint32_t* __restrict__ o1,
+                                                       uint32_t* __restrict__ o2, uint32_t* __restrict__ o3) {
+  __shared__ uint32_t wt[FIN_T / 64];
+  const int w = threadIdx.x >> 6;
+  const int64_t base = (int64_t)blockIdx.x * FIN_B;
+  uint64_t run = boff[blockIdx.x];
+  for (int q = 0; q < FIN_PER; ++q) {
+    const int64_t i = base + q * FIN_T + threadIdx.x;
+    const bool keep = i < n && blk_keep(rule, c, c2, i, r, use_ge2, thr);
+    const uint64_t bal = __ballot(keep);
+    if ((threadIdx.x & 63) == 0) wt[w] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < FIN_T / 64; ++k) { pre += k < w ? wt[k] : 0u; tot += wt[k]; }
+    if (keep) {
+      const uint64_t p = run + pre + mbcnt(bal);
+      if (o0) o0[p] = (uint32_t)a[i];
+      if (o1) o1[p] = (uint32_t)b[i];
+      if (o2) o2[p] = use_ge2 ? c2[i] : c[i];
+      if (o3) o3[p] = c2[i];
+    }
+    run += tot;
+    __syncthreads();  // wt is rewritten by the next chunk
+  }
 }
 
 // ------------------------------------------------------------------ finalize (merge A6)
-// flag rows of rule r whose selected count passes the threshold
-__global__ void k_fin_select(const uint8_t* __restrict__ rule, const uint32_t* __restrict__ c,
-                             const uint32_t* __restrict__ c2, int64_t n, int r, int use_ge2, uint32_t thr,
-                             uint32_t* __restrict__ flag) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t v = use_ge2 ? c2[i] : c[i];
-  flag[i] = rule[i] == (uint8_t)r && v >= thr;
-}
-__global__ void k_fin_compact(const uint32_t* __restrict__ flag, const uint64_t* __restrict__ idx, int64_t n,
-                              const int32_t* __restrict__ a, const int32_t* __restrict__ b,
-                              const uint32_t* __restrict__ c, const uint32_t* __restrict__ c2, int use_ge2,
-                              uint32_t* __restrict__ sa, uint32_t* __restrict__ sb, uint32_t* __restrict__ sc) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || !flag[i]) return;
-  const uint64_t p = idx[i];
-  sa[p] = (uint32_t)a[i]; sb[p] = (uint32_t)b[i]; sc[p] = use_ge2 ? c2[i] : c[i];
-}
 __global__ void k_iota_key(const uint32_t* __restrict__ src, int64_t n, uint32_t* __restrict__ key,
                            uint32_t* __restrict__ val) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
