@@ -1570,7 +1570,7 @@ constexpr int SPLIT_T = 256;
 
 // Digits of one split: ceil(len / SPLIT_MEAN), 2..SPLIT_DMAX (any count, not only powers of two), so
 // hashed buckets average <= SPLIT_MEAN words and almost all fit the 512-word register sort.
-constexpr int SPLIT_DMAX = 256;  // digits per split level (1024 measured slower: 47.6 vs 46.1 ms reduce)
+constexpr int SPLIT_DMAX = 512;  // digits per split level (512 vs 256: reduce -1 ms same-box; 1024 was slower)
 __device__ __forceinline__ uint32_t split_ndig(const Task& t) {
   const uint64_t d = ((uint64_t)t.len + c_split_mean - 1) / c_split_mean;
   return d < 2 ? 2u : (d > (uint64_t)SPLIT_DMAX ? (uint32_t)SPLIT_DMAX : (uint32_t)d);
