@@ -57,6 +57,19 @@ typedef struct {
   int32_t n_files;
 } ottohip_events;
 
+/* Reference-schema parquet rows -> the CSR above, on the device. Replaces the host-side read of
+ * model/count_co_events.py:81,91 (pl.read_parquet of a file written by etl/jsonl_to_parquet.py:59-84,
+ * schema :23-29); the caller decodes the parquet columns and uploads them raw (device, n_rows).
+ * Rows whose sessions form contiguous runs with distinct ids keep their order (the reference's files);
+ * otherwise the rows are stably sorted by session id (*reordered = 1). Writes session_offsets
+ * [n_sessions + 1] = offset_base + row start (so files can be appended into one CSR),
+ * session_ids [n_sessions] (may be NULL) and the aid / ts / type columns (may alias the inputs).
+ * Capacity: n_rows + 1 offsets, n_rows ids. OTTOHIP_ELIMIT if n_rows >= 2^32. */
+int ottohip_events_csr(ottohip_ctx* ctx, const int32_t* session, const int32_t* aid, const int32_t* ts,
+                       const int8_t* type, int64_t n_rows, int64_t offset_base, int64_t* session_offsets,
+                       int32_t* session_ids, int32_t* aid_out, int32_t* ts_out, int8_t* type_out,
+                       int64_t* n_sessions, int* reordered, void* stream);
+
 typedef struct {
   int32_t min_dt;   /* config.MIN_TIME_TO_NEXT (-86400), count_co_events.py:33-36 */
   int32_t max_dt;   /* config.MAX_TIME_TO_NEXT (+86400) */

@@ -21,7 +21,7 @@ import numpy as np
 
 from . import _lib
 from . import config
-from .synth import Events, events_from_columns, read_parquet_events
+from .synth import Events
 
 
 def reference_rules(names=None):
@@ -54,6 +54,62 @@ class DeviceEvents:
             file_bounds = np.array([0, ev.n_sessions], np.int64)
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=False)
         return DeviceEvents(t(off), t(ev.aid), t(ev.ts), t(ev.type), file_bounds, ev.n_sessions, ev.n_events)
+
+    @staticmethod
+    def from_columns(session, aid, ts, type_, file_rows=None, device=None, ctx=None, stream=None) -> "DeviceEvents":
+        """Raw event rows (session, aid, ts, type; numpy or device tensors) -> device CSR built by
+        ottohip_events_csr, file by file (file_rows: rows per file, the reference's 100k-session
+        files; None = one file). Each file's sessions must not continue in another file."""
+        import torch
+        _lib.require_gpu()
+        dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        ctx = ctx or _lib.context()
+        up = lambda a, dt: (a.to(dev) if torch.is_tensor(a) else
+                            torch.from_numpy(np.ascontiguousarray(a, dt)).to(dev))
+        sess, aid_d, ts_d, ty_d = (up(session, np.int32), up(aid, np.int32), up(ts, np.int32), up(type_, np.int8))
+        n = int(sess.numel())
+        if not (aid_d.numel() == ts_d.numel() == ty_d.numel() == n):
+            raise ValueError("events: columns of different lengths")
+        if (sess.dtype, aid_d.dtype, ts_d.dtype, ty_d.dtype) != (torch.int32, torch.int32, torch.int32, torch.int8):
+            raise TypeError("events: columns must be session:int32, aid:int32, ts:int32, type:int8")
+        file_rows = [n] if file_rows is None else [int(r) for r in file_rows]
+        if sum(file_rows) != n:
+            raise ValueError("events: file_rows do not add up to the rows")
+        off = torch.empty(n + len(file_rows), dtype=torch.int64, device=dev)
+        aid_o, ts_o, ty_o = torch.empty_like(aid_d), torch.empty_like(ts_d), torch.empty_like(ty_d)
+        bounds = np.zeros(len(file_rows) + 1, np.int64)
+        r0 = 0
+        ns = ctypes.c_int64()
+        lib = _lib.load()
+        for f, rows in enumerate(file_rows):
+            s0 = int(bounds[f])
+            sl = slice(r0, r0 + rows)
+            _lib.check(lib.ottohip_events_csr(ctx.h, _lib.ptr(sess[sl]), _lib.ptr(aid_d[sl]), _lib.ptr(ts_d[sl]),
+                                              _lib.ptr(ty_d[sl]), rows, r0, _lib.ptr(off[s0:]), None,
+                                              _lib.ptr(aid_o[sl]), _lib.ptr(ts_o[sl]), _lib.ptr(ty_o[sl]),
+                                              ctypes.byref(ns), None, _lib.stream_handle(stream)))
+            bounds[f + 1] = s0 + ns.value
+            r0 += rows
+        S = int(bounds[-1])
+        return DeviceEvents(off[:S + 1].contiguous(), aid_o, ts_o, ty_o, bounds, S, n)
+
+    @staticmethod
+    def from_parquet(paths, device=None, ctx=None, stream=None) -> "DeviceEvents":
+        """Reference-schema session files (etl/jsonl_to_parquet.py:23-29, one file = one
+        file_session_bounds entry, as read at model/count_co_events.py:81,91): columns decoded on
+        the host, uploaded raw, grouped into the CSR on the device."""
+        import pyarrow.parquet as pq
+        paths = [paths] if isinstance(paths, (str, os.PathLike)) else list(paths)
+        cols = {k: [] for k in ("session", "aid", "ts", "type")}
+        rows = []
+        for p in paths:
+            t = pq.read_table(p, columns=list(cols))
+            rows.append(t.num_rows)
+            for k, dt in (("session", np.int32), ("aid", np.int32), ("ts", np.int32), ("type", np.int8)):
+                cols[k].append(t.column(k).to_numpy().astype(dt, copy=False))
+        cat = {k: (np.concatenate(v) if v else np.zeros(0, np.int8 if k == "type" else np.int32)) for k, v in cols.items()}
+        return DeviceEvents.from_columns(cat["session"], cat["aid"], cat["ts"], cat["type"], rows or None,
+                                         device, ctx, stream)
 
     def subset_files(self, f0: int, f1: int) -> "DeviceEvents":
         """Files [f0, f1) as a device view (offsets rebased; event columns are views)."""
@@ -317,8 +373,8 @@ def merge_train_test(name: str, train, test, n_items: int = config.N_ITEMS_OTTO,
     return concat_tables_w_stats(name, [train, test], n_items=n_items, ctx=ctx, **kw)
 
 
-def _n_items_for(aid: np.ndarray) -> int:
-    return max(config.N_ITEMS_OTTO, int(aid.max()) + 1 if len(aid) else 1)
+def _n_items_for_device(aid) -> int:
+    return max(config.N_ITEMS_OTTO, int(aid.max().item()) + 1 if aid.numel() else 1)
 
 
 def count_co_events(df, names=None) -> Dict[str, "object"]:
@@ -331,10 +387,9 @@ def count_co_events(df, names=None) -> Dict[str, "object"]:
     if "aid_next" in df.columns:
         raise ValueError("count_co_events() takes raw events; the joined frame of self_merge() is not materialised "
                          "on the device path")
-    ev = events_from_columns(df["session"].to_numpy(), df["aid"].to_numpy(), df["ts"].to_numpy(),
-                             df["type"].to_numpy())
-    dev = DeviceEvents.from_host(ev)
-    tab = count_co_events_fused(dev, names, n_items=_n_items_for(ev.aid))
+    dev = DeviceEvents.from_columns(df["session"].to_numpy(), df["aid"].to_numpy(), df["ts"].to_numpy(),
+                                    df["type"].to_numpy())
+    tab = count_co_events_fused(dev, names, n_items=_n_items_for_device(dev.aid))
     out = {}
     for n in tab.names:
         a, b, c, _ = tab.to_numpy(n, sort=False)
@@ -359,8 +414,8 @@ def count_co_events_all_files(dir_sessions, dir_stats, skip_if_exists=True):
         outs = {n: f"{dir_stats}/{n}/{stem}.parquet" for n in config.CO_EVENTS_TO_COUNT}
         if skip_if_exists and all(os.path.exists(p) for p in outs.values()):
             continue
-        ev = read_parquet_events(f)
-        tab = count_co_events_fused(DeviceEvents.from_host(ev), n_items=_n_items_for(ev.aid))
+        dev = DeviceEvents.from_parquet(f)
+        tab = count_co_events_fused(dev, n_items=_n_items_for_device(dev.aid))
         for n, p in outs.items():
             a, b, c, _ = tab.to_numpy(n, sort=False)
             _write_table(p, a, b, c, np.uint32)
@@ -405,18 +460,8 @@ def count_co_events_build(dir_sessions, dir_stats, names=None):
     reads every session file once, counts all files in one device pass and writes the merged
     tables {dir_stats}/{name}.parquet (aid:int32, aid_next:int32, count:int32), count desc."""
     files = sorted(glob.glob(f"{dir_sessions}/*.parquet"))
-    parts = [read_parquet_events(f) for f in files]
-    bounds = np.zeros(len(parts) + 1, np.int64)
-    for i, p in enumerate(parts):
-        bounds[i + 1] = bounds[i] + p.n_sessions
-    off = np.zeros(int(bounds[-1]) + 1, np.int64)
-    cols = [np.concatenate([getattr(p, k) for p in parts]) for k in ("session", "aid", "ts", "type")]
-    pos = 0
-    for i, p in enumerate(parts):
-        off[bounds[i]:bounds[i + 1] + 1] = p.session_offsets - p.session_offsets[0] + pos
-        pos += p.n_events
-    ev = Events(off, *cols)
-    tab = count_co_events_fused(DeviceEvents.from_host(ev, bounds), names, n_items=_n_items_for(ev.aid))
+    dev = DeviceEvents.from_parquet(files)
+    tab = count_co_events_fused(dev, names, n_items=_n_items_for_device(dev.aid))
     for n in tab.names:
         a, b, c = (x.cpu().numpy() for x in tab.finalize(n))
         _write_table(f"{dir_stats}/{n}.parquet", a, b, c, np.int32)

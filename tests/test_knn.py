@@ -82,6 +82,28 @@ def test_get_top_k_similar_faiss_frame(gpu):
     assert np.array_equal(df["aid"].to_numpy().reshape(50, 20)[:, 0], words[:50])
 
 
+def test_retrieve_knns_parquet_cache(gpu, tmp_path):
+    """retrieve_w2vec_knns_via_faiss_index (w2vec_aids.py:176-206): neighbours of the first
+    first_n_aids words, written to the cache parquet (:191, :204) with the frame's dtypes and read
+    back instead of searching on the next call (:193-195)."""
+    import pandas as pd
+    import pyarrow.parquet as pq
+    from otto_recommender_amd import w2vec
+    emb = synth.embeddings(6000, seed=5)
+    words = synth.item_words(seed=0, n_items=6000)
+    cache = str(tmp_path / "w2v" / "model.top-20-nns-300-aids.parquet")
+    df = w2vec.retrieve_w2vec_knns_via_faiss_index(emb, words, k=20, first_n_aids=300, cache_file=cache)
+    schema = pq.read_schema(cache)
+    assert [(f.name, str(f.type)) for f in schema][:4] == [("aid", "int32"), ("aid_next", "int32"),
+                                                            ("dist_w2vec", "int32"), ("rank_w2vec", "int8")]
+    ri, rd = oracle.topk_exact(emb, np.arange(300), 20)
+    assert np.array_equal(df["aid"].to_numpy().reshape(300, 20)[:, 0], words[:300])
+    got = df["aid_next"].to_numpy().reshape(300, 20)
+    assert np.mean([set(a) == set(b) for a, b in zip(got, words[ri])]) >= 0.995
+    again = w2vec.retrieve_w2vec_knns_via_faiss_index(None, None, k=20, first_n_aids=300, cache_file=cache)
+    pd.testing.assert_frame_equal(again.reset_index(drop=True), df.reset_index(drop=True))
+
+
 def test_knn_rejects_out_of_range_rows(gpu):
     from otto_recommender_amd import _lib as L
     from otto_recommender_amd.w2vec import KnnIndex
