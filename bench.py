@@ -94,6 +94,34 @@ def bench_a6(dev, tab, ctx) -> dict:
     return {"per_rule": per, "total_ms": round((time.perf_counter() - t0) * 1e3, 2)}
 
 
+def bench_ingest(ev, fb, dev, ctx, reps: int = 3) -> dict:
+    """Event ingest: the raw rows of the 220 M-event workload, resident in HBM as
+    the reference's parquet columns (session, aid, ts, type) in file order, grouped into the session CSR
+    by ottohip_events_csr file by file (`DeviceEvents.from_columns`, the path of `from_parquet`).
+    Algorithmic bytes: read session 4E, write offsets 8S, copy aid/ts/type 9E + 9E. Checked against
+    the host-built CSR the co-visitation line counts on."""
+    import torch
+    from otto_recommender_amd import covis as gc
+    cols = [torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in (ev.session, ev.aid, ev.ts, ev.type)]
+    off = ev.session_offsets
+    file_rows = (off[fb[1:]] - off[fb[:-1]]).tolist()
+    gc.DeviceEvents.from_columns(*cols, file_rows=file_rows, ctx=ctx)  # warmup (workspace)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        d = gc.DeviceEvents.from_columns(*cols, file_rows=file_rows, ctx=ctx)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    ok = bool(torch.equal(d.offsets, dev.offsets) and torch.equal(d.aid, dev.aid) and torch.equal(d.ts, dev.ts)
+              and torch.equal(d.type, dev.type) and np.array_equal(d.file_bounds, dev.file_bounds))
+    E, S = ev.n_events, ev.n_sessions
+    alg = 4.0 * E + 8.0 * (S + 1) + 18.0 * E
+    return {"ms": round(dt * 1e3, 3), "events_per_s": E / dt, "files": len(file_rows), "matches_host_csr": ok,
+            "roofline": {"bound": "hbm", "achieved": alg / dt / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": alg / dt / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": alg,
+                         "note": "host-clock time of the per-file calls (two 8-byte device->host reads per file)"}}
+
+
 def bench_knn(steps: int, warmup: int, n_items: int, n_q: int, with_cpu: bool, group=None) -> dict:
     """BASELINE configs[2]: exact top-20 kNN of the first n_q vocabulary rows. group: the queries
     are split in equal ranges over the ranks (the item matrix replicated on every GPU, SURVEY.md
@@ -238,6 +266,7 @@ def main():
     ap.add_argument("--pandas-files", type=int, default=10, help="files of the pandas reference-algorithm baseline")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-a6", action="store_true", help="skip the A6 (concat_files_w_stats) timing beside the line")
+    ap.add_argument("--no-ingest", action="store_true", help="skip the event-ingest (device CSR build) timing")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--knn-steps", type=int, default=2, help="0 disables the configs[2] kNN measurement")
     ap.add_argument("--workload", choices=["covis", "knn", "candidates"], default="covis",
@@ -345,6 +374,15 @@ def main():
         except Exception as exc:  # noqa: BLE001
             a6 = {"error": repr(exc)}
     tab.free()
+    ingest = None
+    if world == 1 and not args.no_ingest:
+        ctx.trim()
+        try:  # reported beside the line
+            ingest = bench_ingest(ev, fb, dev, ctx)
+        except Exception as exc:  # noqa: BLE001
+            ingest = {"error": repr(exc)}
+        ctx.trim()
+        torch.cuda.empty_cache()
 
     t_step = dt / args.steps
     if world > 1:
@@ -420,6 +458,8 @@ def main():
         if "total_ms" in a6:
             a6["count_plus_merge_ms"] = round(t_step * 1e3 + a6["total_ms"], 2)
         out["a6"] = a6
+    if ingest is not None:
+        out["ingest"] = ingest
     if not args.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(args.seed, args.pandas_files)
     if args.knn_steps > 0:
