@@ -70,6 +70,16 @@ int ottohip_events_csr(ottohip_ctx* ctx, const int32_t* session, const int32_t* 
                        int32_t* session_ids, int32_t* aid_out, int32_t* ts_out, int8_t* type_out,
                        int64_t* n_sessions, int* reordered, void* stream);
 
+/* The same over n_files files appended in one table (file f = rows [file_row_starts[f],
+ * file_row_starts[f+1]), HOST array of n_files + 1 with file_row_starts[0] == 0): one pass when the
+ * run heads ascend strictly over all files (the reference's files), else file by file as above.
+ * file_session_bounds (HOST out, n_files + 1) = each file's first session, the last entry the
+ * session count: the ottohip_events.file_session_bounds of the result. */
+int ottohip_events_csr_files(ottohip_ctx* ctx, const int32_t* session, const int32_t* aid, const int32_t* ts,
+                             const int8_t* type, int n_files, const int64_t* file_row_starts,
+                             int64_t* session_offsets, int32_t* session_ids, int32_t* aid_out, int32_t* ts_out,
+                             int8_t* type_out, int64_t* file_session_bounds, int* reordered, void* stream);
+
 typedef struct {
   int32_t min_dt;   /* config.MIN_TIME_TO_NEXT (-86400), count_co_events.py:33-36 */
   int32_t max_dt;   /* config.MAX_TIME_TO_NEXT (+86400) */

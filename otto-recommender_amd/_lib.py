@@ -72,6 +72,8 @@ SIGNATURES = {
     "ottohip_run_hist": (ctypes.c_int, [_VP, _VP, _I64, _I64, ctypes.c_int, ctypes.c_uint32, _I64, _VP, _VP]),
     "ottohip_events_csr": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _I64, _I64, _VP, _VP, _VP, _VP, _VP,
                                           ctypes.POINTER(_I64), ctypes.POINTER(ctypes.c_int), _VP]),
+    "ottohip_events_csr_files": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, ctypes.c_int, _VP, _VP, _VP, _VP, _VP, _VP,
+                                                _VP, ctypes.POINTER(ctypes.c_int), _VP]),
     "ottohip_topk_per_aid": (ctypes.c_int, [_VP, _VP, _VP, _VP, _I64, _I32, ctypes.c_int] + [_VP] * 7 +
                              [ctypes.POINTER(_I64), _VP]),
     "ottohip_lists_build": (ctypes.c_int, [_VP, _VP, _VP, _VP, _I64, _I32, _VP, _VP, _VP, _VP]),

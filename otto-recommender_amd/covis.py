@@ -58,8 +58,8 @@ class DeviceEvents:
     @staticmethod
     def from_columns(session, aid, ts, type_, file_rows=None, device=None, ctx=None, stream=None) -> "DeviceEvents":
         """Raw event rows (session, aid, ts, type; numpy or device tensors) -> device CSR built by
-        ottohip_events_csr, file by file (file_rows: rows per file, the reference's 100k-session
-        files; None = one file). Each file's sessions must not continue in another file."""
+        ottohip_events_csr_files (file_rows: rows per file, the reference's 100k-session files;
+        None = one file). A file's first row always starts a session."""
         import torch
         _lib.require_gpu()
         dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
@@ -77,19 +77,13 @@ class DeviceEvents:
             raise ValueError("events: file_rows do not add up to the rows")
         off = torch.empty(n + len(file_rows), dtype=torch.int64, device=dev)
         aid_o, ts_o, ty_o = torch.empty_like(aid_d), torch.empty_like(ts_d), torch.empty_like(ty_d)
+        starts = np.zeros(len(file_rows) + 1, np.int64)
+        starts[1:] = np.cumsum(file_rows)
         bounds = np.zeros(len(file_rows) + 1, np.int64)
-        r0 = 0
-        ns = ctypes.c_int64()
-        lib = _lib.load()
-        for f, rows in enumerate(file_rows):
-            s0 = int(bounds[f])
-            sl = slice(r0, r0 + rows)
-            _lib.check(lib.ottohip_events_csr(ctx.h, _lib.ptr(sess[sl]), _lib.ptr(aid_d[sl]), _lib.ptr(ts_d[sl]),
-                                              _lib.ptr(ty_d[sl]), rows, r0, _lib.ptr(off[s0:]), None,
-                                              _lib.ptr(aid_o[sl]), _lib.ptr(ts_o[sl]), _lib.ptr(ty_o[sl]),
-                                              ctypes.byref(ns), None, _lib.stream_handle(stream)))
-            bounds[f + 1] = s0 + ns.value
-            r0 += rows
+        _lib.check(_lib.load().ottohip_events_csr_files(
+            ctx.h, _lib.ptr(sess), _lib.ptr(aid_d), _lib.ptr(ts_d), _lib.ptr(ty_d), len(file_rows),
+            starts.ctypes.data, _lib.ptr(off), None, _lib.ptr(aid_o), _lib.ptr(ts_o), _lib.ptr(ty_o),
+            bounds.ctypes.data, None, _lib.stream_handle(stream)))
         S = int(bounds[-1])
         return DeviceEvents(off[:S + 1].contiguous(), aid_o, ts_o, ty_o, bounds, S, n)
 

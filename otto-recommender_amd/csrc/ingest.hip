@@ -64,9 +64,23 @@ __global__ void k_csr_gather(const uint32_t* __restrict__ skey, const uint32_t* 
   type_out[i] = type[p];
 }
 
-// runs of sess[0..n) -> offsets / ids / head keys; returns R
+// every file's first row starts a run (a session id repeated in the next file is another session)
+__global__ void k_csr_mark(const int64_t* __restrict__ fstart, int nf, int64_t n, uint32_t* __restrict__ flag) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f < nf && fstart[f] < n) flag[fstart[f]] = 1u;
+}
+
+// run index of each file's first row -> file_session_bounds (the last entry is R)
+__global__ void k_csr_bounds(const int64_t* __restrict__ fstart, int nf, int64_t n, const uint64_t* __restrict__ idx,
+                             const uint64_t* __restrict__ tot, int64_t* __restrict__ bounds) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f <= nf) bounds[f] = (int64_t)(fstart[f] < n ? idx[fstart[f]] : *tot);
+}
+
+// runs of sess[0..n) -> offsets / ids / head keys; returns R. fstart (device, nf entries): rows
+// that start a run whatever their id
 static int csr_runs(Ctx* ctx, const int32_t* sess, int64_t n, int64_t base, int64_t* off, int32_t* ids,
-                    uint32_t* key, int64_t* R, hipStream_t s) {
+                    uint32_t* key, int64_t* R, hipStream_t s, const int64_t* fstart = nullptr, int nf = 0) {
   Workspace& ws = ctx->ws;
   uint32_t* flag;
   uint64_t *idx, *tot;
@@ -74,6 +88,7 @@ static int csr_runs(Ctx* ctx, const int32_t* sess, int64_t n, int64_t base, int6
   OH_TRY(ws.get("csr_idx", (size_t)n, &idx));
   OH_TRY(ws.get("csr_tot", 1, &tot));
   k_csr_flags<<<grid_for(n), 256, 0, s>>>(sess, n, flag);
+  if (nf > 0) k_csr_mark<<<grid_for(nf), 256, 0, s>>>(fstart, nf, n, flag);
   OH_TRY(exclusive_scan_u32(ctx, flag, idx, n, tot, s));
   k_csr_heads<<<grid_for(n), 256, 0, s>>>(sess, n, flag, idx, base, off, ids, key);
   OH_HIP(hipGetLastError());
@@ -170,5 +185,69 @@ extern "C" int ottohip_events_csr(ottohip_ctx* c, const int32_t* session, const 
   }
   OH_HIP(hipStreamSynchronize(s));
   *n_sessions = R;
+  return 0;
+}
+
+extern "C" int ottohip_events_csr_files(ottohip_ctx* c, const int32_t* session, const int32_t* aid, const int32_t* ts,
+                                        const int8_t* type, int n_files, const int64_t* file_row_starts,
+                                        int64_t* session_offsets, int32_t* session_ids, int32_t* aid_out,
+                                        int32_t* ts_out, int8_t* type_out, int64_t* file_session_bounds,
+                                        int* reordered, void* stream) {
+  if (!c || n_files < 1 || !file_row_starts || !file_session_bounds || !session_offsets || file_row_starts[0] != 0) {
+    set_error("events_csr_files: bad arguments");
+    return OTTOHIP_EINVAL;
+  }
+  for (int f = 0; f < n_files; ++f)
+    if (file_row_starts[f + 1] < file_row_starts[f]) { set_error("events_csr_files: file %d ends before it starts", f); return OTTOHIP_EINVAL; }
+  const int64_t n = file_row_starts[n_files];
+  if (n > 0 && (!session || !aid || !ts || !type || !aid_out || !ts_out || !type_out)) {
+    set_error("events_csr_files: bad arguments");
+    return OTTOHIP_EINVAL;
+  }
+  if (n >= ((int64_t)1 << 32)) { set_error("events_csr_files: %lld rows >= 2^32", (long long)n); return OTTOHIP_ELIMIT; }
+  ottohip_ctx* ctx = c;
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  if (reordered) *reordered = 0;
+  int64_t R = 0;
+  bool grouped = n == 0;
+  if (n > 0) {
+    // one pass over every file (runs forced at file starts); kept when the run heads ascend strictly
+    // over all files, which the reference's files do (session ids increase from file to file)
+    Workspace& ws = ctx->ws;
+    uint32_t* key;
+    int64_t *fs, *fb;
+    OH_TRY(ws.get("csr_key", (size_t)n, &key));
+    OH_TRY(ws.get("csr_fs", (size_t)n_files + 1, &fs));
+    OH_TRY(ws.get("csr_fb", (size_t)n_files + 1, &fb));
+    OH_HIP(hipMemcpyAsync(fs, file_row_starts, (size_t)(n_files + 1) * 8, hipMemcpyHostToDevice, s));
+    OH_TRY(csr_runs(ctx, session, n, 0, session_offsets, session_ids, key, &R, s, fs, n_files));
+    OH_TRY(strictly_ascending(ctx, key, R, &grouped, s));
+    if (grouped) {
+      uint64_t *idx, *tot;
+      OH_TRY(ws.get("csr_idx", (size_t)n, &idx));
+      OH_TRY(ws.get("csr_tot", 1, &tot));
+      k_csr_bounds<<<grid_for(n_files + 1), 256, 0, s>>>(fs, n_files, n, idx, tot, fb);
+      OH_HIP(hipGetLastError());
+      OH_TRY(d2h(file_session_bounds, fb, (size_t)n_files + 1, s));
+      if (aid_out != aid) OH_HIP(hipMemcpyAsync(aid_out, aid, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+      if (ts_out != ts) OH_HIP(hipMemcpyAsync(ts_out, ts, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+      if (type_out != type) OH_HIP(hipMemcpyAsync(type_out, type, (size_t)n, hipMemcpyDeviceToDevice, s));
+      OH_HIP(hipStreamSynchronize(s));
+      return 0;
+    }
+  }
+  // otherwise file by file (each file grouped on its own, appended at its row offset)
+  file_session_bounds[0] = 0;
+  for (int f = 0; f < n_files; ++f) {
+    const int64_t r0 = file_row_starts[f], rows = file_row_starts[f + 1] - r0, s0 = file_session_bounds[f];
+    int64_t ns = 0;
+    int re = 0;
+    OH_TRY(ottohip_events_csr(c, session + r0, aid + r0, ts + r0, type + r0, rows, r0, session_offsets + s0,
+                              session_ids ? session_ids + s0 : nullptr, aid_out + r0, ts_out + r0, type_out + r0,
+                              &ns, &re, stream));
+    file_session_bounds[f + 1] = s0 + ns;
+    if (reordered && re) *reordered = 1;
+  }
   return 0;
 }

@@ -124,3 +124,45 @@ def test_from_parquet_counts_like_host_csr(gpu, tmp_path):
         for x, y in zip(a.to_numpy(n), b.to_numpy(n)):
             np.testing.assert_array_equal(x, y, err_msg=n)
         assert a.stats(n) == b.stats(n)
+
+
+def _files_ref(sess, aid, ts, ty, file_rows):
+    """per-file restatement: each file grouped on its own, appended at its row offset"""
+    offs, cols, bounds, r0 = [np.zeros(1, np.int64)], [[], [], []], [0], 0
+    for rows in file_rows:
+        sl = slice(r0, r0 + rows)
+        off, _, a, t, y, _ = _csr_ref(sess[sl], aid[sl], ts[sl], ty[sl])
+        offs.append(off[1:] + r0)
+        for c, x in zip(cols, (a, t, y)):
+            c.append(x)
+        bounds.append(bounds[-1] + len(off) - 1)
+        r0 += rows
+    return np.concatenate(offs), [np.concatenate(c) if c else c for c in cols], np.array(bounds, np.int64)
+
+
+@pytest.mark.parametrize("case", ["reference", "id_continues", "split_in_file", "empty_files"])
+def test_csr_files(gpu, case):
+    """ottohip_events_csr_files (DeviceEvents.from_columns): one pass over the reference's files, file by
+    file when a session id continues into the next file or a file's sessions are split"""
+    from otto_recommender_amd import covis as gc
+    ev = synth.generate(9_000, first_session=10)
+    sess, aid, ts, ty = (np.array(x) for x in _rows(ev))
+    cut = [int(ev.session_offsets[i]) for i in (0, 3_000, 6_000, 9_000)]
+    file_rows = list(np.diff(cut))
+    if case == "id_continues":  # file 1 starts with file 0's last session id
+        sess[cut[1]:cut[1] + 5] = sess[cut[1] - 1]
+    elif case == "split_in_file":
+        rng = np.random.default_rng(4)
+        o = cut[2] + rng.permutation(cut[3] - cut[2])
+        sess[cut[2]:], aid[cut[2]:], ts[cut[2]:], ty[cut[2]:] = sess[o], aid[o], ts[o], ty[o]
+    elif case == "empty_files":
+        file_rows = [0, file_rows[0], 0, file_rows[1] + file_rows[2], 0]
+    d = gc.DeviceEvents.from_columns(sess, aid, ts, ty, file_rows=file_rows, ctx=gpu)
+    off, cols, bounds = _files_ref(sess, aid, ts, ty, file_rows)
+    np.testing.assert_array_equal(d.file_bounds, bounds)
+    np.testing.assert_array_equal(d.offsets.cpu().numpy(), off)
+    for g, r in zip((d.aid, d.ts, d.type), cols):
+        np.testing.assert_array_equal(g.cpu().numpy(), r)
+    assert d.n_sessions == bounds[-1] and d.n_events == len(sess)
+    if case == "reference":
+        np.testing.assert_array_equal(off, ev.session_offsets - ev.session_offsets[0])
