@@ -45,8 +45,8 @@ fetch, write = load(sys.argv[1]), load(sys.argv[2])
 bf, bw = phases(fetch), phases(write)
 n = min(len(bf), len(bw))
 out = {"note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes of bench.py --steps 1 --warmup 0 "
-               "--knn-steps 1 --cand-steps 0; FETCH_SIZE (KiB) doubled per MI355X_MICROARCH.md; bytes per "
-               f"build phase averaged over {n} builds; k_knn_main per launch; produced by tools/pmc_phases.py"}
+               "--knn-steps 1 --cand-steps 0 --no-cpu --no-a6 --no-ingest; FETCH_SIZE (KiB) doubled per MI355X_MICROARCH.md; bytes per "
+               f"build phase averaged over {n} full builds (run with --no-a6 --no-ingest, so no A6 part recounts or other kernels follow a build); k_knn_main per launch; produced by tools/pmc_phases.py"}
 for ph in ("prep_count", "rows", "emit", "reduce"):
     f = sum(b[ph] for b in bf[:n]) / n
     w = sum(b[ph] for b in bw[:n]) / n
