@@ -119,7 +119,7 @@ def bench_ingest(ev, fb, dev, ctx, reps: int = 3) -> dict:
     return {"ms": round(dt * 1e3, 3), "events_per_s": E / dt, "files": len(file_rows), "matches_host_csr": ok,
             "roofline": {"bound": "hbm", "achieved": alg / dt / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": alg / dt / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": alg,
-                         "note": "host-clock time of the per-file calls (two 8-byte device->host reads per file)"}}
+                         "note": "host-clock time of one ottohip_events_csr_files call over all files (three small device->host reads)"}}
 
 
 def bench_knn(steps: int, warmup: int, n_items: int, n_q: int, with_cpu: bool, group=None) -> dict:
