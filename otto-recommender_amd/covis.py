@@ -76,7 +76,10 @@ class DeviceEvents:
         if sum(file_rows) != n:
             raise ValueError("events: file_rows do not add up to the rows")
         off = torch.empty(n + len(file_rows), dtype=torch.int64, device=dev)
-        aid_o, ts_o, ty_o = torch.empty_like(aid_d), torch.empty_like(ts_d), torch.empty_like(ty_d)
+        # columns uploaded here are rewritten in place (no copy); a caller's device columns are kept
+        owned = not any(torch.is_tensor(x) for x in (aid, ts, type_))
+        aid_o, ts_o, ty_o = ((aid_d, ts_d, ty_d) if owned else
+                             (torch.empty_like(aid_d), torch.empty_like(ts_d), torch.empty_like(ty_d)))
         starts = np.zeros(len(file_rows) + 1, np.int64)
         starts[1:] = np.cumsum(file_rows)
         bounds = np.zeros(len(file_rows) + 1, np.int64)
