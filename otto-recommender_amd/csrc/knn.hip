@@ -93,7 +93,8 @@ constexpr int KN_GL = KN_IT * KN_CH / KN_T;  // glds per thread per tile (8)
 template <int ABL, int KS>
 __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ items, int64_t V,
                                                   const uint4* __restrict__ queries, int64_t nq,
-                                                  uint32_t* __restrict__ cand, float* __restrict__ thr_io) {
+                                                  uint32_t* __restrict__ cand, float* __restrict__ thr_io,
+                                                  int pre_stride) {
   __shared__ uint4 ring[KN_RING * KN_IT * KN_CH];  // 2 x 64 KiB, the only LDS object
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, r = l & 31, h = l >> 5;
   const int64_t qbase = (int64_t)blockIdx.x * KN_QB + w * 64;
@@ -119,7 +120,7 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
   float thr = -INFINITY;
   constexpr bool PRE = ABL == 2;
   const int64_t nTall = ceil_div(V, KN_IT);
-  const int64_t nT = PRE ? (nTall - 1 + PRE_STRIDE - 1) / PRE_STRIDE : nTall;  // tiles scanned
+  const int64_t nT = PRE ? (nTall - 1 + pre_stride - 1) / pre_stride : nTall;  // tiles scanned
   if (ABL == 0 && thr_io) {  // start the list at the pre-pass bound (placeholders with no index)
     const float b = q < nq ? thr_io[q] : -INFINITY;
 #pragma unroll
@@ -132,7 +133,7 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
   auto issue = [&](int64_t t) {
     if (ABL == 3 && t >= KN_RING) return;  // ablation: item stream off after the first tiles (timing only)
     uint4* dst = ring + (int)(t % KN_RING) * (KN_IT * KN_CH);
-    const int64_t tt = PRE ? t * PRE_STRIDE : t;
+    const int64_t tt = PRE ? t * pre_stride : t;
 #pragma unroll
     for (int u = 0; u < KN_GL; ++u) {
       const int p = u * KN_T + tid, row = p >> 4, c = p & 15;
@@ -400,23 +401,25 @@ int ottohip_knn_topk(ottohip_ctx* c, const ottohip_knn_index* ix, const int32_t*
   ctx->end(ph, s);
   static const int abl = getenv("OTTOHIP_KNN_ABLATE") ? atoi(getenv("OTTOHIP_KNN_ABLATE")) : 0;
   static const int nopre = getenv("OTTOHIP_KNN_NOPRE") ? atoi(getenv("OTTOHIP_KNN_NOPRE")) : 0;
+  // pre-pass sampling stride (A/B switch OTTOHIP_KNN_PRE_STRIDE; PRE_STRIDE by default)
+  static const int pst = getenv("OTTOHIP_KNN_PRE_STRIDE") ? std::max(2, atoi(getenv("OTTOHIP_KNN_PRE_STRIDE"))) : PRE_STRIDE;
   const unsigned grid = (unsigned)ceil_div(n_q, KN_QB);
   const int64_t nT = ceil_div(ix->n_items, KN_IT);
   float* thr = nullptr;
   const bool k8 = ix->dim + 2 > 7 * 16;
-  if (!abl && !nopre && (nT - 1) / PRE_STRIDE >= KN_C) {  // enough sampled tiles for KN_C groups
+  if (!abl && !nopre && (nT - 1) / pst >= KN_C) {  // enough sampled tiles for KN_C groups
     OH_TRY(ctx->ws.get("knn_thr", (size_t)n_q, &thr));
-    const int64_t nS = (nT - 1 + PRE_STRIDE - 1) / PRE_STRIDE;
+    const int64_t nS = (nT - 1 + pst - 1) / pst;
     ph = ctx->begin("knn_pre", s, 2.0 * (double)n_q * (double)(nS * KN_IT) * ix->dim);
     (k8 ? k_knn_main<2, 8> : k_knn_main<2, 7>)<<<grid, KN_T, 0, s>>>(reinterpret_cast<const uint4*>(ix->packed), ix->n_items,
-                                          reinterpret_cast<const uint4*>(qp), n_q, cand, thr);
+                                          reinterpret_cast<const uint4*>(qp), n_q, cand, thr, pst);
     ctx->end(ph, s);
   }
   ph = ctx->begin("knn_main", s, 2.0 * (double)n_q * (double)ix->n_items * ix->dim);
   auto kmain = k8 ? (abl == 3 ? k_knn_main<3, 8> : (abl ? k_knn_main<1, 8> : k_knn_main<0, 8>))
                   : (abl == 3 ? k_knn_main<3, 7> : (abl ? k_knn_main<1, 7> : k_knn_main<0, 7>));
   kmain<<<grid, KN_T, 0, s>>>(reinterpret_cast<const uint4*>(ix->packed), ix->n_items,
-                              reinterpret_cast<const uint4*>(qp), n_q, cand, thr);
+                              reinterpret_cast<const uint4*>(qp), n_q, cand, thr, pst);
   ctx->end(ph, s);
   ph = ctx->begin("knn_rerank", s, 0);
   k_knn_rerank<<<(unsigned)ceil_div(n_q * 64, 256), 256, 0, s>>>(ix->emb, ix->n_items, ix->dim, query_rows, n_q, cand,
