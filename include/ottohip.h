@@ -115,6 +115,33 @@ int ottohip_ctx_timing(ottohip_ctx* ctx, int idx, const char** name, float* ms, 
 int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip_rule* rules,
                         int n_rules, const ottohip_covis_params* params, ottohip_table** out,
                         void* stream);
+/* Per-file options of one rule, for concat_files_w_stats' part-wise branch by rows
+ * (model/count_co_events.py:136-158: part i = rows [i * rows_part, (i + 1) * rows_part) of the
+ * concatenation of the per-file tables, each file's table in (aid, aid_next) order here):
+ *   - a row slice of a boundary file is a key range of its ordered table, key = aid << 32 | aid_next:
+ *     the rule's pairs of file lo_file with key < lo_key and of file hi_file with key >= hi_key are
+ *     cut before they are counted (-1 = no cut; the file ids of the call: local index, or the
+ *     file_ids / global ids of the multi-GPU calls);
+ *   - file_rows / file_rows_ge2 (HOST out, n_files entries, n_files <= 1024, may be NULL): per file,
+ *     the rule's rows after the cuts and those with per-file count >= 2 (the N of :117 / :131 per file). */
+typedef struct {
+  int32_t rule;      /* index into the call's rules */
+  int32_t lo_file;
+  int32_t hi_file;
+  int32_t n_files;
+  uint64_t lo_key;
+  uint64_t hi_key;
+  int64_t* file_rows;
+  int64_t* file_rows_ge2;
+} ottohip_file_opts;
+int ottohip_covis_count_opts(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip_rule* rules, int n_rules,
+                             const ottohip_covis_params* params, const ottohip_file_opts* opts, ottohip_table** out,
+                             void* stream);
+/* keys (HOST out [n_idx]) = (aid << 32 | aid_next) of rows idx[i] (HOST) of one rule's rows in
+ * (aid, aid_next) order; use_ge2: only rows with per-file count >= 2 (count_ge2 > 0). With a one-file
+ * table these are the boundary keys of a row slice (ottohip_file_opts). OTTOHIP_ERANGE: idx >= rows. */
+int ottohip_table_keys_at(ottohip_ctx* ctx, const ottohip_table* t, int rule, int use_ge2, const int64_t* idx,
+                          int n_idx, uint64_t* keys, void* stream);
 int ottohip_table_stats(const ottohip_table* t, int rule, ottohip_rule_stats* st);
 /* copy one rule's rows (unordered) into caller device buffers of n_rows entries;
  * any output pointer may be NULL */
@@ -367,6 +394,12 @@ int ottohip_covis_reduce_received(ottohip_ctx* ctx, const ottohip_rule* rules, i
                                   const ottohip_covis_params* params, int32_t n_files_total, const uint32_t* words,
                                   int64_t n_words, const uint64_t* pieces, int64_t n_pieces, ottohip_table** out,
                                   void* stream);
+/* the same with per-file options (global file ids; the owner's histograms cover its own rows, the
+ * host all-reduces them) */
+int ottohip_covis_reduce_received_opts(ottohip_ctx* ctx, const ottohip_rule* rules, int n_rules,
+                                       const ottohip_covis_params* params, int32_t n_files_total, const uint32_t* words,
+                                       int64_t n_words, const uint64_t* pieces, int64_t n_pieces,
+                                       const ottohip_file_opts* opts, ottohip_table** out, void* stream);
 
 /* ---- Word2Vec top-K similarity (model/w2vec_aids.py:98-173) ------------------------------
  * Replaces load_index_faiss_ivff (:98-110) + get_top_k_similar_faiss (:125-173): exact L2

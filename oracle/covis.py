@@ -146,23 +146,23 @@ def concat_files_w_stats(name: str, parts: list, loaded_from_cache: bool = False
                          max_rows_groupby: int = MAX_ROWS_POLARS_GROUPBY,
                          optim_rows: int = OPTIM_ROWS_POLARS_GROUPBY,
                          max_pairs: int = MAX_CO_EVENT_PAIRS_TO_SAVE_DISK,
-                         click_filter_rows: int = 100_000_000, part_mode: str = "rows"):
+                         click_filter_rows: int = 100_000_000):
     """Restates model/count_co_events.py:103-181 on in-memory per-file tables
-    [(aid, aid_next, count)...] concatenated in the given order. Branch (2) slices in concat
-    order; the reference's nondeterminism there (polars groupby row order) is replaced by the
-    deterministic (count desc, aid, aid_next) order. part_mode="files" cuts branch (2)'s parts
-    at whole-file boundaries instead (file p*nf//n_parts starts part p), the device path's
-    definition (covis.concat_files_w_stats_fused). Returns (aid:int32, aid_next:int32, count:int32)."""
+    [(aid, aid_next, count)...] concatenated in the given order. Branch (2) slices ceil(N/n_parts)
+    consecutive rows of that concatenation (:136-153), so the row order inside each table decides
+    the slices: the reference's per-file tables come out of polars' groupby in an unspecified order,
+    which makes its branch (2) nondeterministic; the build fixes it as (aid, aid_next) ascending
+    (count_co_events_file's order) and every sort's ties as (count desc, aid, aid_next).
+    Returns (aid:int32, aid_next:int32, count:int32)."""
     nf = len(parts)
     cat = lambda k, dt, sel: (np.concatenate([parts[f][k] for f in sel]).astype(dt) if len(sel)
                               else np.zeros(0, dt))
     a, b, c = cat(0, np.int32, range(nf)), cat(1, np.int32, range(nf)), cat(2, np.int64, range(nf))
-    fid = np.concatenate([np.full(len(parts[f][0]), f, np.int64) for f in range(nf)]) if nf else np.zeros(0, np.int64)
     n = len(a)
     # :131-132 lossy per-part filter for click_to tables
     if "click_to" in name and n > click_filter_rows and not loaded_from_cache:
         keep = c >= MIN_COUNT_IN_PART.get(name, 1)
-        a, b, c, fid = a[keep], b[keep], c[keep], fid[keep]
+        a, b, c = a[keep], b[keep], c[keep]
         n = len(a)
     # :135-166 groupby by parts
     if n > max_rows_groupby and not loaded_from_cache:
@@ -170,11 +170,7 @@ def concat_files_w_stats(name: str, parts: list, loaded_from_cache: bool = False
         n_parts = math.ceil(n / rows_part)
         max_rows_part = int(max_rows_groupby / n * rows_part)
         rows_part = math.ceil(n / n_parts)
-        if part_mode == "files":
-            bnd = [(p * nf) // n_parts for p in range(n_parts + 1)]
-            sel = [(fid >= bnd[i]) & (fid < bnd[i + 1]) for i in range(n_parts)]
-        else:
-            sel = [slice(i * rows_part, (i + 1) * rows_part) for i in range(n_parts)]
+        sel = [slice(i * rows_part, (i + 1) * rows_part) for i in range(n_parts)]
         pa, pb, pc = [], [], []
         for m in sel:
             sa, sb, sc = _groupby_sum(a[m], b[m], c[m])
@@ -190,18 +186,16 @@ def concat_files_w_stats(name: str, parts: list, loaded_from_cache: bool = False
     return a, b, c.astype(np.int32)
 
 
-def merge_train_test(name: str, train_parts: list, test_parts: list, train_mode: str = "rows",
-                     test_mode: str = "rows", **kw):
+def merge_train_test(name: str, train_parts: list, test_parts: list, **kw):
     """Restates the stage orchestration of model/count_co_events.py:209-226 (A7) for one rule:
     concat_files_w_stats per folder (:214-215), each with its OWN N for the :131 and :135
     triggers and its own MIN_COUNT_TO_SAVE cut, then concat_files_w_stats on the concatenation
     [train table, test table] of the two thresholded folder tables (:218-226). Branch (2) of the
-    final merge slices rows of that concatenation (part_mode="rows"), which is deterministic
-    here: both inputs are in (count desc, aid, aid_next) order. *_mode: branch-(2) part
-    definition of each folder merge ("files" = the fused device path's whole-file parts)."""
-    t = concat_files_w_stats(name, train_parts, part_mode=train_mode, **kw)
-    s = concat_files_w_stats(name, test_parts, part_mode=test_mode, **kw)
-    return concat_files_w_stats(name, [t, s], part_mode="rows", **kw)
+    final merge slices rows of that concatenation, which is deterministic here: both inputs are
+    in (count desc, aid, aid_next) order."""
+    t = concat_files_w_stats(name, train_parts, **kw)
+    s = concat_files_w_stats(name, test_parts, **kw)
+    return concat_files_w_stats(name, [t, s], **kw)
 
 
 def files_digest(offsets, aid, ts, type_, file_bounds, threads: int = 0, rules=REFERENCE_RULES) -> dict:

@@ -43,6 +43,12 @@ class RuleStats(ctypes.Structure):
                 ("file_rows_ge2", ctypes.c_int64)]
 
 
+class FileOpts(ctypes.Structure):
+    _fields_ = [("rule", ctypes.c_int32), ("lo_file", ctypes.c_int32), ("hi_file", ctypes.c_int32),
+                ("n_files", ctypes.c_int32), ("lo_key", ctypes.c_uint64), ("hi_key", ctypes.c_uint64),
+                ("file_rows", ctypes.c_void_p), ("file_rows_ge2", ctypes.c_void_p)]
+
+
 class MergeParams(ctypes.Structure):
     _fields_ = [("click_rule", ctypes.c_int32), ("min_count_in_part", ctypes.c_int32), ("min_count", ctypes.c_int32),
                 ("max_rows", ctypes.c_int64), ("filter_rows", ctypes.c_int64), ("max_rows_groupby", ctypes.c_int64)]
@@ -60,6 +66,10 @@ SIGNATURES = {
                                           ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_double)]),
     "ottohip_covis_count": (ctypes.c_int, [_VP, ctypes.POINTER(Events), ctypes.POINTER(Rule), ctypes.c_int,
                                            ctypes.POINTER(CovisParams), ctypes.POINTER(_VP), _VP]),
+    "ottohip_covis_count_opts": (ctypes.c_int, [_VP, ctypes.POINTER(Events), ctypes.POINTER(Rule), ctypes.c_int,
+                                                ctypes.POINTER(CovisParams), ctypes.POINTER(FileOpts),
+                                                ctypes.POINTER(_VP), _VP]),
+    "ottohip_table_keys_at": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_int, _VP, ctypes.c_int, _VP, _VP]),
     "ottohip_table_stats": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.POINTER(RuleStats)]),
     "ottohip_table_copy": (ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, _VP, _VP]),
     "ottohip_table_free": (None, [_VP]),
@@ -125,6 +135,9 @@ SIGNATURES = {
     "ottohip_emit_free": (None, [_VP]),
     "ottohip_covis_reduce_received": (ctypes.c_int, [_VP, ctypes.POINTER(Rule), ctypes.c_int, ctypes.POINTER(CovisParams),
                                                      _I32, _VP, _I64, _VP, _I64, ctypes.POINTER(_VP), _VP]),
+    "ottohip_covis_reduce_received_opts": (ctypes.c_int, [_VP, ctypes.POINTER(Rule), ctypes.c_int,
+                                                          ctypes.POINTER(CovisParams), _I32, _VP, _I64, _VP, _I64,
+                                                          ctypes.POINTER(FileOpts), ctypes.POINTER(_VP), _VP]),
     "ottohip_knn_index_create": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, ctypes.POINTER(_VP), _VP]),
     "ottohip_knn_topk": (ctypes.c_int, [_VP, _VP, _VP, _I64, ctypes.c_int, _VP, _VP, _VP]),
     "ottohip_knn_index_free": (None, [_VP]),

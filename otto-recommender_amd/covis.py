@@ -64,7 +64,7 @@ class DeviceEvents:
         _lib.require_gpu()
         dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         ctx = ctx or _lib.context()
-        up = lambda a, dt: (a.to(dev) if torch.is_tensor(a) else
+        up = lambda a, dt: (a.to(dev).contiguous() if torch.is_tensor(a) else
                             torch.from_numpy(np.ascontiguousarray(a, dt)).to(dev))
         sess, aid_d, ts_d, ty_d = (up(session, np.int32), up(aid, np.int32), up(ts, np.int32), up(type_, np.int8))
         n = int(sess.numel())
@@ -225,42 +225,136 @@ def max_files_per_call(names=None, n_items: int = config.N_ITEMS_OTTO) -> int:
     bits (csrc/abi.hip setup_rules), so 2^(31 - rule bits - aid bits) files (512 at 1.86 M items)."""
     names, rules = reference_rules(names)
     per_type = max(sum(1 for r in rules if r.this_type == t) for t in range(3))
-    return 1 << (31 - _bits_for(per_type) - max(1, _bits_for(int(n_items))))
+    return min(1 << (31 - _bits_for(per_type) - max(1, _bits_for(int(n_items)))), 65535)
+
+
+class FileCuts:
+    """Per-file options of one rule for a count (ottohip_file_opts): `lo` = (file, key) drops the
+    rule's pairs of that file with key < key, `hi` = (file, key) those with key >= key (key =
+    aid << 32 | aid_next; file = index among the call's files, or global id in the sharded calls);
+    per_file=True reports every file's rows of the rule (file_rows / file_rows_ge2 per file)."""
+
+    def __init__(self, rule: str, lo=None, hi=None, per_file: bool = False):
+        self.rule, self.lo, self.hi, self.per_file = rule, lo, hi, per_file
+
+    def shifted(self, f0: int, f1: int) -> "FileCuts":
+        """The options of the files [f0, f1) renumbered from 0 (a batch of whole files)."""
+        mv = lambda c: (c[0] - f0, c[1]) if c is not None and f0 <= c[0] < f1 else None
+        return FileCuts(self.rule, mv(self.lo), mv(self.hi), self.per_file)
+
+    def abi(self, names, n_files: int):
+        o = _lib.FileOpts()
+        o.rule = list(names).index(self.rule)
+        o.lo_file, o.lo_key = (int(self.lo[0]), int(self.lo[1])) if self.lo is not None else (-1, 0)
+        o.hi_file, o.hi_key = (int(self.hi[0]), int(self.hi[1])) if self.hi is not None else (-1, 0)
+        o.n_files = int(n_files)
+        rows = rows2 = None
+        if self.per_file:
+            rows, rows2 = np.zeros(max(n_files, 1), np.int64), np.zeros(max(n_files, 1), np.int64)
+            o.file_rows, o.file_rows_ge2 = rows.ctypes.data, rows2.ctypes.data
+        return o, rows, rows2
 
 
 def count_co_events_fused(events: DeviceEvents, names=None, n_items: int = config.N_ITEMS_OTTO, dedup: bool = True,
-                          stream=None, ctx=None, max_files: int | None = None) -> CovisTable:
+                          stream=None, ctx=None, max_files: int | None = None, cuts: FileCuts | None = None) -> CovisTable:
     """All rules over all files of `events` in one device pass (per-file counts folded into
     count / count_ge2): count_co_events_all_files + the groupby of concat_files_w_stats.
     More files than one pass can tell apart (max_files_per_call) are counted in batches of
     whole files and the batch tables merge-summed: count, count_ge2 and the per-file row
-    statistics are sums over disjoint file sets."""
+    statistics are sums over disjoint file sets. cuts: per-file options of one rule (FileCuts);
+    with per_file=True the table carries file_rows_per_file / file_rows_ge2_per_file (numpy)."""
     ctx = ctx or _lib.context()
     cap = max_files or max_files_per_call(names, n_items)
     nf = len(events.file_bounds) - 1
     if nf > cap:
         import torch
         from . import dist as gd
-        recs, fs = [], None
+        recs, fs, pf, pf2 = [], None, [], []
         for f0 in range(0, nf, cap):
-            t = count_co_events_fused(events.subset_files(f0, min(nf, f0 + cap)), names, n_items, dedup, stream, ctx,
-                                      max_files=cap)
+            f1 = min(nf, f0 + cap)
+            t = count_co_events_fused(events.subset_files(f0, f1), names, n_items, dedup, stream, ctx,
+                                      max_files=cap, cuts=cuts.shifted(f0, f1) if cuts is not None else None)
             st = [(t.stats(r)["file_rows"], t.stats(r)["file_rows_ge2"]) for r in range(len(t.names))]
             fs = st if fs is None else [(a + c, b + d) for (a, b), (c, d) in zip(fs, st)]
+            if cuts is not None and cuts.per_file:
+                pf.append(t.file_rows_per_file); pf2.append(t.file_rows_ge2_per_file)
             r, _ = gd.pack_by_owner(t, 1, stream)
             recs.append(r.clone())
             names = t.names
             t.free()
         merged = gd.table_from_records(torch.cat(recs).contiguous(), names, n_items, fs, ctx=ctx, stream=stream)
+        if pf:
+            merged.file_rows_per_file, merged.file_rows_ge2_per_file = np.concatenate(pf), np.concatenate(pf2)
         return merged
     names, rules = reference_rules(names)
     p = _lib.CovisParams()
     p.min_dt, p.max_dt, p.n_items, p.dedup = config.MIN_TIME_TO_NEXT, config.MAX_TIME_TO_NEXT, int(n_items), int(dedup)
     ev = events.abi()
     h = ctypes.c_void_p()
-    _lib.check(_lib.load().ottohip_covis_count(ctx.h, ctypes.byref(ev), rules, len(names), ctypes.byref(p),
-                                               ctypes.byref(h), _lib.stream_handle(stream)))
-    return CovisTable(h, names, ctx)
+    lib = _lib.load()
+    if cuts is None:
+        _lib.check(lib.ottohip_covis_count(ctx.h, ctypes.byref(ev), rules, len(names), ctypes.byref(p),
+                                           ctypes.byref(h), _lib.stream_handle(stream)))
+        return CovisTable(h, names, ctx)
+    o, rows, rows2 = cuts.abi(names, nf)
+    _lib.check(lib.ottohip_covis_count_opts(ctx.h, ctypes.byref(ev), rules, len(names), ctypes.byref(p),
+                                            ctypes.byref(o), ctypes.byref(h), _lib.stream_handle(stream)))
+    tab = CovisTable(h, names, ctx)
+    if cuts.per_file:
+        tab.file_rows_per_file, tab.file_rows_ge2_per_file = rows[:nf], rows2[:nf]
+    return tab
+
+
+def part_plan(file_rows, n_parts: int):
+    """Row slices of concat_files_w_stats' branch (2) (model/count_co_events.py:136-153) over the
+    per-file row counts of the concatenation: part i = rows [i * rows_part, (i + 1) * rows_part),
+    rows_part = ceil(N / n_parts). Returns [(fa, lo, fb, hi)]: the part starts at row lo of file fa
+    and ends before row hi of file fb (fa <= fb; files strictly between are whole)."""
+    import math
+    R = np.asarray(file_rows, np.int64)
+    N = int(R.sum())
+    C = np.concatenate([[0], np.cumsum(R)])
+    rows_part = math.ceil(N / n_parts) if n_parts else 0
+    plan = []
+    for i in range(n_parts):
+        g0, g1 = i * rows_part, min((i + 1) * rows_part, N)
+        if g1 <= g0:
+            continue
+        fa = int(np.searchsorted(C, g0, side="right")) - 1
+        fb = int(np.searchsorted(C, g1 - 1, side="right")) - 1
+        plan.append((fa, int(g0 - C[fa]), fb, int(g1 - C[fb])))
+    return plan
+
+
+def table_keys_at(table: CovisTable, name, use_ge2: bool, idx, stream=None) -> np.ndarray:
+    """ottohip_table_keys_at: keys (aid << 32 | aid_next) of rows idx of one rule's rows in (aid,
+    aid_next) order (use_ge2: rows with count >= 2 only)."""
+    idx = np.ascontiguousarray(idx, np.int64)
+    keys = np.zeros(max(len(idx), 1), np.uint64)
+    _lib.check(_lib.load().ottohip_table_keys_at(table.ctx.h, table.h, table._rule(name), 1 if use_ge2 else 0,
+                                                 idx.ctypes.data, len(idx), keys.ctypes.data,
+                                                 _lib.stream_handle(stream)))
+    return keys[:len(idx)]
+
+
+def boundary_keys(events: DeviceEvents, name: str, plan, file_rows, use_ge2: bool, n_items: int, ctx=None) -> dict:
+    """{(file, row): key} for every part boundary of `plan` that falls inside a file: the file is
+    counted alone (its per-file table, as count_co_events.py:94 writes it) and the key of that row
+    of its (aid, aid_next)-ordered (use_ge2: count >= 2) rows is read."""
+    need = {}
+    for fa, lo, fb, hi in plan:
+        if lo > 0:
+            need.setdefault(fa, set()).add(lo)
+        if hi < int(file_rows[fb]):
+            need.setdefault(fb, set()).add(hi)
+    out = {}
+    for f, rows in sorted(need.items()):
+        rows = sorted(rows)
+        t = count_co_events_fused(events.subset_files(f, f + 1), [name], n_items=n_items, ctx=ctx)
+        for r, k in zip(rows, table_keys_at(t, name, use_ge2, rows)):
+            out[(f, r)] = int(k)
+        t.free()
+    return out
 
 
 def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTable | None = None,
@@ -272,10 +366,12 @@ def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTabl
     (1) per-file count >= 2 for click_to_* tables when N > 1e8 (count_ge2), (2) when still
     N > max_rows_groupby, part-wise groupby -> keep count >= MIN_COUNT_IN_PART -> count desc
     -> head(int(max_rows_groupby / N * optim_rows)) per part, (3) groupby, MIN_COUNT_TO_SAVE,
-    count desc, head(max_pairs). The reference slices parts by rows in polars' (unspecified)
-    row order, which makes branch (2) nondeterministic; here a part is a
-    run of consecutive whole files, ceil(N / optim_rows) parts of equal file counts. Returns
-    torch (aid, aid_next, count:int32) in (count desc, aid, aid_next) order."""
+    count desc, head(max_pairs). Branch (2) slices rows as the reference does (:136-153):
+    ceil(N / n_parts) consecutive rows of the files' concatenated per-file tables, each file's
+    table in (aid, aid_next) order (polars leaves it unspecified). One pass
+    gives every file's row count; a part is the count of its files with the boundary files cut
+    to the key range of their row slice (FileCuts). Returns torch (aid, aid_next, count:int32)
+    in (count desc, aid, aid_next) order."""
     import math
     import torch
     from . import dist as gd
@@ -295,15 +391,20 @@ def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTabl
         tab.free()
     n_parts = math.ceil(N / optim_rows)
     max_rows_part = int(max_rows_groupby / N * optim_rows)
-    nf = len(events.file_bounds) - 1
-    bounds = [(p * nf) // n_parts for p in range(n_parts + 1)]
+    t = count_co_events_fused(events, [name], n_items=n_items, ctx=ctx, cuts=FileCuts(name, per_file=True))
+    R = t.file_rows_ge2_per_file if use_ge2 else t.file_rows_per_file
+    t.free()
+    if int(R.sum()) != N:
+        raise RuntimeError(f"{name}: per-file rows sum to {int(R.sum())}, the table's N is {N}")
+    plan = part_plan(R, n_parts)
+    keys = boundary_keys(events, name, plan, R, use_ge2, n_items, ctx)
     part = {"click_rule": 1 if use_ge2 else 0, "filter_rows": -1, "max_rows_groupby": 1 << 62,
             "min_count": config.MIN_COUNT_IN_PART.get(name, 1)}
     recs = []
-    for f0, f1 in zip(bounds[:-1], bounds[1:]):
-        if f1 <= f0:
-            continue
-        t = count_co_events_fused(events.subset_files(f0, f1), [name], n_items=n_items, ctx=ctx)
+    for fa, lo, fb, hi in plan:
+        cuts = FileCuts(name, lo=(0, keys[(fa, lo)]) if lo > 0 else None,
+                        hi=(fb - fa, keys[(fb, hi)]) if hi < int(R[fb]) else None)
+        t = count_co_events_fused(events.subset_files(fa, fb + 1), [name], n_items=n_items, ctx=ctx, cuts=cuts)
         a, b, c = t.finalize(name, max_rows=max_rows_part, params=part)
         recs.append(torch.stack([a, b, c, torch.zeros_like(c)], 1))
         t.free()
@@ -452,14 +553,18 @@ def concat_files_w_stats(name, dir_stats, files_stats=None, n_items: int | None 
     _write_table(f"{dir_stats}/{name}.parquet", a.cpu().numpy(), b.cpu().numpy(), c.cpu().numpy(), np.int32)
 
 
-def count_co_events_build(dir_sessions, dir_stats, names=None):
+def count_co_events_build(dir_sessions, dir_stats, names=None, **kw):
     """Fused equivalent of `count_co_events_all_files` + `concat_files_w_stats` for one folder:
     reads every session file once, counts all files in one device pass and writes the merged
-    tables {dir_stats}/{name}.parquet (aid:int32, aid_next:int32, count:int32), count desc."""
+    tables {dir_stats}/{name}.parquet (aid:int32, aid_next:int32, count:int32), count desc. Every
+    branch of :131-175 applies (concat_files_w_stats_fused: the part-wise branch (2) by rows where
+    a rule's N exceeds MAX_ROWS_POLARS_GROUPBY, e.g. click_to_click at 220 M events). kw:
+    concat_files_w_stats_fused thresholds (max_rows_groupby, optim_rows, max_pairs, click_filter_rows)."""
     files = sorted(glob.glob(f"{dir_sessions}/*.parquet"))
     dev = DeviceEvents.from_parquet(files)
-    tab = count_co_events_fused(dev, names, n_items=_n_items_for_device(dev.aid))
+    n_items = _n_items_for_device(dev.aid)
+    tab = count_co_events_fused(dev, names, n_items=n_items)
     for n in tab.names:
-        a, b, c = (x.cpu().numpy() for x in tab.finalize(n))
+        a, b, c = (x.cpu().numpy() for x in concat_files_w_stats_fused(dev, n, table=tab, n_items=n_items, **kw))
         _write_table(f"{dir_stats}/{n}.parquet", a, b, c, np.int32)
     tab.free()

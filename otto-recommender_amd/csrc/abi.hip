@@ -362,13 +362,54 @@ static int covis_emit_words(ottohip_ctx* ctx, const Front& F, const ottohip_even
 }
 
 // S5: words grouped by row -> table rows (count, count_ge2) and per-rule statistics
+// ottohip_file_opts -> the kernels' FileOpts (device histogram / drop counter from the workspace)
+static int file_opts_setup(ottohip_ctx* ctx, const ottohip_file_opts* o, int n_rules, const RulesDev& R,
+                           FileOpts& fo, hipStream_t s) {
+  if (o->rule < 0 || o->rule >= n_rules) { set_error("file_opts: rule %d outside the call's rules", o->rule); return OTTOHIP_EINVAL; }
+  const bool want_hist = o->file_rows || o->file_rows_ge2;
+  if (want_hist && (o->n_files < 1 || o->n_files > FO_MAXF)) {
+    set_error("file_opts: n_files=%d outside [1, %d]", o->n_files, FO_MAXF); return OTTOHIP_ELIMIT;
+  }
+  memset(&fo, 0, sizeof fo);
+  for (int t = 0; t < 3; ++t)
+    for (int q = 0; q < R.n_of_type[t]; ++q)
+      if (R.rule_of_type[t][q] == o->rule) { fo.type = t; fo.q = (uint32_t)q; }
+  fo.lo_file = o->lo_file < 0 ? 0xFFFFFFFFu : (uint32_t)o->lo_file;
+  fo.hi_file = o->hi_file < 0 ? 0xFFFFFFFFu : (uint32_t)o->hi_file;
+  fo.lo_key = o->lo_key;
+  fo.hi_key = o->hi_key;
+  OH_TRY(ctx->ws.get("fo_dropped", 1, &fo.dropped));
+  OH_HIP(hipMemsetAsync(fo.dropped, 0, 8, s));
+  if (want_hist) {
+    fo.nf = (uint32_t)o->n_files;
+    OH_TRY(ctx->ws.get("fo_hist", (size_t)fo.nf, &fo.hist));
+    OH_HIP(hipMemsetAsync(fo.hist, 0, (size_t)fo.nf * 8, s));
+  }
+  return 0;
+}
+
+static int file_opts_finish(const ottohip_file_opts* o, const FileOpts& fo, hipStream_t s) {
+  if (!fo.hist) return 0;
+  std::vector<unsigned long long> h(fo.nf);
+  OH_TRY(d2h(h.data(), fo.hist, h.size(), s));
+  for (uint32_t f = 0; f < fo.nf; ++f) {
+    if (o->file_rows) o->file_rows[f] = (int64_t)(h[f] & 0xFFFFFFFFull);
+    if (o->file_rows_ge2) o->file_rows_ge2[f] = (int64_t)(h[f] >> 32);
+  }
+  return 0;
+}
+
 static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P, const uint64_t* row_begin,
                         const uint32_t* row_key, int64_t Rn, const RulesDev& R, const Layout& Lt, int n_rules,
-                        ottohip_table* T, hipStream_t s) {
+                        ottohip_table* T, hipStream_t s, const ottohip_file_opts* fopts = nullptr) {
   Workspace& ws = ctx->ws;
   int rc;
   int* err;
   OH_TRY(ws.get("err", 4, &err));
+  FileOpts fo;
+  memset(&fo, 0, sizeof fo);
+  if (fopts) OH_TRY(file_opts_setup(ctx, fopts, n_rules, R, fo, s));
+  const bool FOon = fopts != nullptr;
   if (ctx->spare.cap >= P) {
     T->b = ctx->spare;
     ctx->spare = TableBufs();
@@ -458,16 +499,27 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     // rewritten by the next level's classify, which waits for them (ev_join)
     hipStream_t ss = s2 ? s2 : s;
     if (s2) { OH_HIP(hipEventRecord(ctx->ev_fork, s)); OH_HIP(hipStreamWaitEvent(s2, ctx->ev_fork, 0)); }
-#define OH_SORT(c, M)                                                                                      \
-    if (nlist[c])                                                                                          \
-      k_agg_sort<M><<<(unsigned)std::min<uint64_t>(ceil_div((int64_t)nlist[c], 4), sgrid), 256, 0, ss>>>(  \
-          TL.sort[c], (int64_t)nlist[c], w0, w1, row_key, R, Lt, n_rules, Osort);
+#define OH_SORT(c, M)                                                                                        \
+    if (nlist[c]) {                                                                                          \
+      const unsigned g_ = (unsigned)std::min<uint64_t>(ceil_div((int64_t)nlist[c], 4), sgrid);              \
+      if (FOon)                                                                                              \
+        k_agg_sort<M, true><<<g_, 256, 0, ss>>>(TL.sort[c], (int64_t)nlist[c], w0, w1, row_key, R, Lt, n_rules, \
+                                                Osort, fo);                                                  \
+      else                                                                                                   \
+        k_agg_sort<M><<<g_, 256, 0, ss>>>(TL.sort[c], (int64_t)nlist[c], w0, w1, row_key, R, Lt, n_rules, Osort, \
+                                          fo);                                                               \
+    }
     OH_SORT(0, 1) OH_SORT(1, 2) OH_SORT(2, 4) OH_SORT(3, 8) OH_SORT(4, 16)
 #undef OH_SORT
     if (s2) OH_HIP(hipEventRecord(ctx->ev_join[level & 1], s2));
     if (nlist[N_SORT]) {  // tasks that overflow the LDS table are appended to the split list
-      k_agg_hash<<<(unsigned)std::min<uint64_t>(nlist[N_SORT], (uint64_t)agg_grid), AGG_T, 0, s>>>(
-          TL.hash, (int64_t)nlist[N_SORT], w0, w1, row_key, R, Lt, n_rules, O, TL.split, lcount + N_SORT + 1);
+      const unsigned hg = (unsigned)std::min<uint64_t>(nlist[N_SORT], (uint64_t)agg_grid);
+      if (FOon)
+        k_agg_hash<true><<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], w0, w1, row_key, R, Lt, n_rules, O,
+                                              TL.split, lcount + N_SORT + 1, fo);
+      else
+        k_agg_hash<<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], w0, w1, row_key, R, Lt, n_rules, O, TL.split,
+                                        lcount + N_SORT + 1, fo);
       if ((rc = d2h(nlist, lcount, N_SORT + 2, s))) return rc;
     }
     const int64_t ns = (int64_t)nlist[N_SORT + 1];
@@ -525,12 +577,17 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   for (int k = 0; k < STAT_STRIPES; ++k)
     for (int j = 0; j < MAX_RULES * 4; ++j) st[j] += stv[(size_t)k * STAT_STRIDE + j];
   if (hipGetLastError() != hipSuccess) { set_error("reduce failed"); return OTTOHIP_EHIP; }
-  unsigned long long sum_pairs = 0, U = 0;
+  unsigned long long sum_pairs = 0, U = 0, dropped = 0;
   for (int r = 0; r < n_rules; ++r) { sum_pairs += st[r * 4 + 1]; U += st[r * 4 + 0]; }
+  if (FOon) {
+    if ((rc = d2h(&dropped, fo.dropped, 1, s))) return rc;
+    if ((rc = file_opts_finish(fopts, fo, s))) return rc;
+  }
   T->n_rows = (int64_t)U;
   T->n_slots = (int64_t)P;
-  if (sum_pairs != P || U > P) {  // conservation: every emitted pair is counted exactly once
-    set_error("reduce: %llu pairs counted of %llu emitted (rows %llu)", sum_pairs, (unsigned long long)P, U);
+  if (sum_pairs + dropped != P || U > P) {  // conservation: every emitted pair is counted (or cut) exactly once
+    set_error("reduce: %llu pairs counted + %llu cut of %llu emitted (rows %llu)", sum_pairs, dropped,
+              (unsigned long long)P, U);
     return OTTOHIP_EHIP;
   }
   for (int r = 0; r < n_rules; ++r) {
@@ -653,8 +710,17 @@ int ottohip_test_radix_sort_pairs(ottohip_ctx* ctx, uint32_t* keys, uint32_t* va
   return 0;
 }
 
-int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip_rule* rules, int n_rules,
-                        const ottohip_covis_params* params, ottohip_table** out, void* stream) {
+static void file_opts_zero(const ottohip_file_opts* o) {
+  if (!o) return;
+  for (int f = 0; f < o->n_files; ++f) {
+    if (o->file_rows) o->file_rows[f] = 0;
+    if (o->file_rows_ge2) o->file_rows_ge2[f] = 0;
+  }
+}
+
+int ottohip_covis_count_opts(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip_rule* rules, int n_rules,
+                             const ottohip_covis_params* params, const ottohip_file_opts* opts, ottohip_table** out,
+                             void* stream) {
   if (!ctx || !ev || !rules || !params || !out) { set_error("ottohip_covis_count: NULL argument"); return OTTOHIP_EINVAL; }
   *out = nullptr;
   hipStream_t s = S(stream);
@@ -663,6 +729,10 @@ int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohi
   Front F;
   OH_TRY(check_events(ev));
   OH_TRY(setup_rules(rules, n_rules, params, ev->n_files, F.R, F.Lt));
+  if (opts && (opts->file_rows || opts->file_rows_ge2) && opts->n_files < ev->n_files) {
+    set_error("file_opts: n_files=%d < the call's %d files", opts->n_files, ev->n_files); return OTTOHIP_EINVAL;
+  }
+  file_opts_zero(opts);
   ottohip_table* T = new_table(ctx, n_rules, params->n_items);
   auto fail = [&](int rc) { ottohip_table_free(T); return rc; };
   int rc;
@@ -671,9 +741,15 @@ int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohi
   uint32_t *w0, *w1;
   if ((rc = ctx->ws.get("words0", (size_t)F.P, &w0)) || (rc = ctx->ws.get("words1", (size_t)F.P, &w1))) return fail(rc);
   if ((rc = covis_emit_words(ctx, F, ev, w0, s))) return fail(rc);
-  if ((rc = covis_reduce(ctx, w0, w1, F.P, F.row_begin, F.row_key, F.Rn, F.R, F.Lt, n_rules, T, s))) return fail(rc);
+  if ((rc = covis_reduce(ctx, w0, w1, F.P, F.row_begin, F.row_key, F.Rn, F.R, F.Lt, n_rules, T, s, opts)))
+    return fail(rc);
   *out = T;
   return 0;
+}
+
+int ottohip_covis_count(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip_rule* rules, int n_rules,
+                        const ottohip_covis_params* params, ottohip_table** out, void* stream) {
+  return ottohip_covis_count_opts(ctx, ev, rules, n_rules, params, nullptr, out, stream);
 }
 
 int ottohip_covis_emit(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip_rule* rules, int n_rules,
@@ -740,10 +816,22 @@ int ottohip_covis_reduce_received(ottohip_ctx* ctx, const ottohip_rule* rules, i
                                   const ottohip_covis_params* params, int32_t n_files_total, const uint32_t* words,
                                   int64_t n_words, const uint64_t* pieces, int64_t n_pieces, ottohip_table** out,
                                   void* stream) {
+  return ottohip_covis_reduce_received_opts(ctx, rules, n_rules, params, n_files_total, words, n_words, pieces,
+                                            n_pieces, nullptr, out, stream);
+}
+
+int ottohip_covis_reduce_received_opts(ottohip_ctx* ctx, const ottohip_rule* rules, int n_rules,
+                                       const ottohip_covis_params* params, int32_t n_files_total, const uint32_t* words,
+                                       int64_t n_words, const uint64_t* pieces, int64_t n_pieces,
+                                       const ottohip_file_opts* opts, ottohip_table** out, void* stream) {
   if (!ctx || !rules || !params || !out || n_words < 0 || n_pieces < 0 || (n_words > 0 && !words) ||
       (n_pieces > 0 && !pieces)) {
     set_error("ottohip_covis_reduce_received: bad arguments"); return OTTOHIP_EINVAL;
   }
+  if (opts && (opts->file_rows || opts->file_rows_ge2) && opts->n_files < n_files_total) {
+    set_error("file_opts: n_files=%d < n_files_total=%d", opts->n_files, n_files_total); return OTTOHIP_EINVAL;
+  }
+  file_opts_zero(opts);
   *out = nullptr;
   hipStream_t s = S(stream);
   OH_HIP(hipSetDevice(ctx->device));
@@ -808,7 +896,7 @@ int ottohip_covis_reduce_received(ottohip_ctx* ctx, const ottohip_rule* rules, i
   }
   if (hipGetLastError() != hipSuccess) { set_error("assemble launch failed"); return fail(OTTOHIP_EHIP); }
   ctx->end(ph, s);
-  if ((rc = covis_reduce(ctx, w0, w1, P, row_begin, row_key, Rn, R, Lt, n_rules, T, s))) return fail(rc);
+  if ((rc = covis_reduce(ctx, w0, w1, P, row_begin, row_key, Rn, R, Lt, n_rules, T, s, opts))) return fail(rc);
   *out = T;
   return 0;
 }
@@ -846,6 +934,73 @@ int ottohip_table_copy(const ottohip_table* t, int rule, int32_t* aid, int32_t* 
                                                rule, 0, 0u, boff, reinterpret_cast<uint32_t*>(aid),
                                                reinterpret_cast<uint32_t*>(aid_next), count, count_ge2);
   OH_HIP(hipGetLastError());
+  return 0;
+}
+
+__global__ void k_keys_at(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ sa,
+                          const uint32_t* __restrict__ sb, const int64_t* __restrict__ idx, int n,
+                          uint64_t* __restrict__ keys) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t j = perm[idx[i]];
+  keys[i] = ((uint64_t)sa[j] << 32) | sb[j];
+}
+
+int ottohip_table_keys_at(ottohip_ctx* ctx, const ottohip_table* t, int rule, int use_ge2, const int64_t* idx,
+                          int n_idx, uint64_t* keys, void* stream) {
+  if (!ctx || !t || rule < 0 || rule >= t->n_rules || n_idx < 0 || (n_idx > 0 && (!idx || !keys))) {
+    set_error("table_keys_at: bad args"); return OTTOHIP_EINVAL;
+  }
+  if (n_idx == 0) return 0;
+  hipStream_t s = S(stream);
+  Workspace& ws = ctx->ws;
+  const int64_t n = t->n_slots;
+  const int64_t nb = ceil_div(std::max<int64_t>(n, 1), FIN_B);
+  uint32_t* bcnt;
+  uint64_t *boff, *tot;
+  OH_TRY(ws.get("blk_cnt", (size_t)nb, &bcnt));
+  OH_TRY(ws.get("blk_off", (size_t)nb, &boff));
+  OH_TRY(ws.get("fin_tot", 1, &tot));
+  uint64_t m = 0;
+  if (t->n_rows > 0 && n > 0) {
+    // rows of the rule (use_ge2: per-file count >= 2, i.e. count_ge2 >= 1)
+    k_blk_count<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.count, t->b.count_ge2, n, rule, use_ge2 ? 1 : 0,
+                                               use_ge2 ? 1u : 0u, bcnt);
+    OH_TRY(exclusive_scan_u32(ctx, bcnt, boff, nb, tot, s));
+    OH_TRY(d2h(&m, tot, 1, s));
+  }
+  for (int i = 0; i < n_idx; ++i)
+    if (idx[i] < 0 || (uint64_t)idx[i] >= m) {
+      set_error("table_keys_at: index %lld outside the rule's %llu rows", (long long)idx[i], (unsigned long long)m);
+      return OTTOHIP_ERANGE;
+    }
+  uint32_t *sa, *sb, *k0, *v0, *k1, *v1;
+  int64_t* didx;
+  uint64_t* dkeys;
+  OH_TRY(ws.get("fin_sa", (size_t)m, &sa));
+  OH_TRY(ws.get("fin_sb", (size_t)m, &sb));
+  OH_TRY(ws.get("fin_k0", (size_t)m, &k0));
+  OH_TRY(ws.get("fin_v0", (size_t)m, &v0));
+  OH_TRY(ws.get("fin_k1", (size_t)m, &k1));
+  OH_TRY(ws.get("fin_v1", (size_t)m, &v1));
+  OH_TRY(ws.get("ka_idx", (size_t)n_idx, &didx));
+  OH_TRY(ws.get("ka_keys", (size_t)n_idx, &dkeys));
+  k_blk_compact<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n,
+                                               rule, use_ge2 ? 1 : 0, use_ge2 ? 1u : 0u, boff, sa, sb, nullptr,
+                                               nullptr);
+  // LSD: aid_next, then aid (stable) -> (aid, aid_next) ascending
+  const int abits = std::max(1, bits_for((uint64_t)t->n_items));
+  uint32_t *k = k0, *v = v0;
+  k_iota_key<<<grid_for((int64_t)m), 256, 0, s>>>(sb, (int64_t)m, k, v);
+  OH_TRY(radix_sort_pairs(ctx, k, v, k == k0 ? k1 : k0, v == v0 ? v1 : v0, (int64_t)m, abits, s));
+  uint32_t* kn = (k == k0) ? k1 : k0;
+  k_gather_key<<<grid_for((int64_t)m), 256, 0, s>>>(sa, v, (int64_t)m, 0, kn);
+  k = kn;
+  OH_TRY(radix_sort_pairs(ctx, k, v, k == k0 ? k1 : k0, v == v0 ? v1 : v0, (int64_t)m, abits, s));
+  OH_HIP(hipMemcpyAsync(didx, idx, (size_t)n_idx * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  k_keys_at<<<grid_for(n_idx), 256, 0, s>>>(v, sa, sb, didx, n_idx, dkeys);
+  OH_HIP(hipGetLastError());
+  OH_TRY(d2h(keys, dkeys, (size_t)n_idx, s));
   return 0;
 }
 

@@ -64,6 +64,28 @@ struct OutRows {
   unsigned long long* stats;  // [STAT_STRIPES][MAX_RULES][4]: rows, pairs, file_rows, file_rows_ge2
 };
 
+// Per-file options of one rule (ottohip_file_opts; A6 branch (2) by rows, count_co_events.py:136-158):
+// a row slice of a boundary file is a key range of its (aid, aid_next)-ordered table, so the words
+// of file lo_file with key < lo_key and of file hi_file with key >= hi_key are dropped by the leaf
+// tasks before they are counted; hist[f] accumulates file f's rows of the rule (low 32 bits) and
+// those with per-file count >= 2 (high 32 bits). Applied to the rule's words only.
+constexpr int FO_MAXF = 1024;
+struct FileOpts {
+  int type;              // row type of the rule
+  uint32_t q;            // the rule's index among the rules of its type (word bits above aid_next)
+  uint32_t lo_file, hi_file;  // 0xFFFFFFFF: no cut
+  uint64_t lo_key, hi_key;    // key = aid << 32 | aid_next
+  unsigned long long* hist;   // [nf] or null
+  uint32_t nf;
+  unsigned long long* dropped;  // words dropped by the cuts (the reduce's conservation check)
+};
+__device__ __forceinline__ bool fo_drop(const FileOpts& fo, uint32_t w, int32_t aid, const Layout& L) {
+  if (w == W_EMPTY || (w >> (L.A + L.F)) != fo.q) return false;
+  const uint32_t f = w & ((1u << L.F) - 1u);
+  const uint64_t key = ((uint64_t)(uint32_t)aid << 32) | ((w >> L.F) & L.amask);
+  return (f == fo.lo_file && key < fo.lo_key) || (f == fo.hi_file && key >= fo.hi_key);
+}
+
 // ------------------------------------------------------------------ block maps
 __global__ void k_block_first(const int64_t* __restrict__ off, int64_t S, int64_t NB,
                               int64_t* __restrict__ first, int32_t* __restrict__ long_list,
@@ -1168,26 +1190,29 @@ __device__ __forceinline__ uint32_t excl_at(const uint32_t (&x)[M], int m, uint3
 // The next task's words are loaded while the current one is folded. Per-rule statistics go
 // through a per-wave LDS accumulator (one lane, after wave sums of packed 16-bit fields: a
 // task holds <= 1024 words), so no per-thread accumulator arrays take registers.
-template <int M>
+template <int M, bool FO = false>
 __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task* __restrict__ tasks, int64_t n_tasks,
                                                   const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
                                                   const uint32_t* __restrict__ row_key, RulesDev R, Layout L,
-                                                  int n_rules, OutRows O) {
+                                                  int n_rules, OutRows O, FileOpts fo) {
   __shared__ unsigned long long sacc[4][MAX_RULES * 4];
   __shared__ RulesDev sR;
   __shared__ uint32_t stg[4][2][64 * M];  // per wave: output rows of one task (key2, count | count_ge2 << 16)
+  __shared__ unsigned long long fh[FO ? FO_MAXF : 1];  // per-file rows of the FileOpts rule
   const uint32_t l = lane_id();
   const int wv = threadIdx.x >> 6;
   if (threadIdx.x == 0) sR = R;
   for (int i = (int)l; i < MAX_RULES * 4; i += 64) sacc[wv][i] = 0;
+  if constexpr (FO)
+    for (uint32_t i = threadIdx.x; i < fo.nf; i += blockDim.x) fh[i] = 0;
   __syncthreads();
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   int64_t ti = __builtin_amdgcn_readfirstlane((int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   const int F = L.F, A = L.A;
   uint32_t v[M];
   Task T;
-  uint32_t rk = 0;
-  auto fetch = [&](int64_t t, Task& TT, uint32_t (&vv)[M], uint32_t& rkk) {
+  uint32_t rk = 0, nd = 0;
+  auto fetch = [&](int64_t t, Task& TT, uint32_t (&vv)[M], uint32_t& rkk, uint32_t& ndd) {
     TT = tasks[t];
     const uint32_t* W = (TT.buf ? w1 : w0) + TT.begin;
 #pragma unroll
@@ -1197,15 +1222,27 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
       vv[m] = i < TT.len ? x : W_EMPTY;
     }
     rkk = row_key[TT.row];
+    ndd = 0;
+    if constexpr (FO) {  // the cut words become W_EMPTY (sorted past the task's new end)
+      if ((int)(rkk >> A) == fo.type) {
+        const int32_t ad = (int32_t)(rkk & L.amask);
+        uint32_t k = 0;
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+          if (fo_drop(fo, vv[m], ad, L)) { vv[m] = W_EMPTY; ++k; }
+        ndd = wave_sum(k);
+      }
+    }
   };
-  if (ti < n_tasks) fetch(ti, T, v, rk);
+  if (ti < n_tasks) fetch(ti, T, v, rk, nd);
   while (ti < n_tasks) {
     const int64_t tn = ti + nw;
     Task Tn;
     uint32_t vn[M];
-    uint32_t rkn = 0;
-    if (tn < n_tasks) fetch(tn, Tn, vn, rkn);
-    const uint32_t len = T.len;
+    uint32_t rkn = 0, ndn = 0;
+    if (tn < n_tasks) fetch(tn, Tn, vn, rkn, ndn);
+    const uint32_t len = T.len - nd;
+    if (FO && nd && l == 0) atomicAdd(fo.dropped, (unsigned long long)nd);
     wave_bitonic_sort<M>(v);
     const uint32_t pl = lane_prev(v[M - 1]), nl = lane_next(v[0]);
     // (1) run flags from the neighbours (a w-run = one word = one (rule, aid_next, file)):
@@ -1220,6 +1257,14 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
       const bool we = valid && (e + 1 == len || nxt != v[m]);
       c[m] = (we ? 1u : 0u) | ((ws && we) ? (1u << 11) : 0u);
       b[m] = c[m];
+    }
+    if constexpr (FO) {  // one per-file row per w-run end of the rule; a singleton w-run has count 1
+      if (fo.hist && (int)(rk >> A) == fo.type) {
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+          if ((c[m] & 1u) && (v[m] >> (A + F)) == fo.q)
+            atomicAdd(&fh[v[m] & ((1u << F) - 1u)], (c[m] >> 11) ? 1ull : (1ull | (1ull << 32)));
+      }
     }
     wave_scan_elems<M, false>(b);
     // (2) at each k-run (rule, aid_next) start: its exclusive X << 10 | position, carried to the
@@ -1301,7 +1346,7 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
         o_c2[i] = bb >> 16;
       }
     if (store)  // the rest of the task's word range holds no row (marked here, no table-wide fill)
-      for (uint32_t i = nout + l; i < len; i += 64) o_rule[i] = 0xFF;
+      for (uint32_t i = nout + l; i < T.len; i += 64) o_rule[i] = 0xFF;
     for (int q = 0; q < (nq < 2 ? nq : 2); ++q) {
       const uint32_t sa = wave_sum(q == 0 ? s0a : s1a), sb = wave_sum(q == 0 ? s0b : s1b);
       if (l == 0 && sa) {
@@ -1313,6 +1358,7 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     T = Tn;
     rk = rkn;
+    nd = ndn;
 #pragma unroll
     for (int m = 0; m < M; ++m) v[m] = vn[m];
     ti = tn;
@@ -1323,6 +1369,13 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
   unsigned long long* stats = O.stats + (size_t)(gwave & (STAT_STRIPES - 1)) * STAT_STRIDE;
   for (int i = (int)l; i < n_rules * 4; i += 64)
     if (sacc[wv][i]) atomicAdd(&stats[i], sacc[wv][i]);
+  if constexpr (FO) {
+    if (fo.hist) {
+      __syncthreads();
+      for (uint32_t i = threadIdx.x; i < fo.nf; i += blockDim.x)
+        if (fh[i]) atomicAdd(&fo.hist[i], fh[i]);
+    }
+  }
 }
 
 // Task lists filled by classification kernels (wave-aggregated pushes)
@@ -1382,20 +1435,29 @@ struct TaskLists {
   uint64_t cap;           // capacity of every list
 };
 
+template <bool FO = false>
 __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tasks, int64_t n_tasks,
                                                     const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
                                                     const uint32_t* __restrict__ row_key, RulesDev R, Layout L,
                                                     int n_rules, OutRows O, Task* __restrict__ overflow,
-                                                    unsigned long long* __restrict__ n_overflow) {
+                                                    unsigned long long* __restrict__ n_overflow, FileOpts fo) {
   __shared__ unsigned long long lds[2 * HCAP];  // 64 KiB: phase A [0, cap), phase B [0, 2cap)
   __shared__ uint32_t wtot[AGG_T / 64];
   __shared__ uint32_t nocc;
+  __shared__ unsigned long long fh[FO ? FO_MAXF : 1];  // per-file rows of the FileOpts rule
   const int tid = threadIdx.x;
   RuleAcc acc;
   acc.zero();
+  if constexpr (FO) {
+    for (uint32_t i = tid; i < fo.nf; i += AGG_T) fh[i] = 0;
+    __syncthreads();
+  }
   for (int64_t ti = blockIdx.x; ti < n_tasks; ti += gridDim.x) {
     const Task T = tasks[ti];
     const uint32_t* W = (T.buf ? w1 : w0) + T.begin;
+    const RowInfo ri = row_info(row_key, T.row, L.A);
+    const bool fo_row = FO && ri.type == fo.type;
+    uint32_t ndrop = 0;
     const uint32_t dbound = T.len;
     // optimistic: more keys possible than fit; give up at 3/4 fill and send the task to a split
     const bool optimistic = 2 * dbound > (uint32_t)HCAP;
@@ -1414,6 +1476,7 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
       for (int j = 0; j < PF; ++j) {
         const uint32_t i = i0 + j * AGG_T + tid;
         wbuf[j] = i < T.len ? W[i] : W_EMPTY;
+        if (FO && fo_row && fo_drop(fo, wbuf[j], ri.aid, L)) { wbuf[j] = W_EMPTY; ++ndrop; }
       }
       // each thread adds at most PF keys after this check: 256 * 8 < HCAP / 4 keeps the table from filling
       if (optimistic && __hip_atomic_load(&nocc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > limit) {
@@ -1458,6 +1521,16 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
       kw[s] = (uint32_t)(v >> 32);
       kc[s] = (uint32_t)v;
     }
+    if constexpr (FO) {  // the task completed: its drops count, and every slot is one per-file row
+      const uint32_t nd = wave_sum(ndrop);
+      if (nd && (tid & 63) == 0) atomicAdd(fo.dropped, (unsigned long long)nd);
+      if (fo.hist && fo_row) {
+#pragma unroll
+        for (int s = 0; s < SL; ++s)
+          if (kw[s] != W_EMPTY && (kw[s] >> (L.A + L.F)) == fo.q)
+            atomicAdd(&fh[kw[s] & ((1u << L.F) - 1u)], kc[s] >= 2 ? (1ull | (1ull << 32)) : 1ull);
+      }
+    }
     __syncthreads();
     unsigned long long* B = lds;            // key2 << 32 | count
     unsigned long long* B2 = lds + cap;     // count_ge2 << 32 | nf2 << 16 | nf1
@@ -1482,7 +1555,6 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
     }
     __syncthreads();
     // compact into the task's own word range (outputs <= words)
-    const RowInfo ri = row_info(row_key, T.row, L.A);
     uint32_t mine = 0;
     for (uint32_t i = tid; i < cap; i += AGG_T) mine += (uint32_t)(B[i] >> 32) != W_EMPTY;
     const uint32_t incl = wave_incl_scan(mine);
@@ -1508,6 +1580,13 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
     __syncthreads();
   }
   acc.flush(O.stats, n_rules);
+  if constexpr (FO) {
+    if (fo.hist) {
+      __syncthreads();
+      for (uint32_t i = tid; i < fo.nf; i += AGG_T)
+        if (fh[i]) atomicAdd(&fo.hist[i], fh[i]);
+    }
+  }
 }
 
 // ---- classification of rows and split buckets into task lists

@@ -176,8 +176,10 @@ def emit_for_owners(events, n_parts: int, file_ids=None, n_files_total: int | No
 
 
 def reduce_received(words, pieces, names, n_files_total: int, n_items: int = config.N_ITEMS_OTTO, dedup: bool = True,
-                    stream=None, ctx=None):
-    """Assemble the received segments (one word range per row) and reduce them to a table."""
+                    stream=None, ctx=None, cuts=None):
+    """Assemble the received segments (one word range per row) and reduce them to a table.
+    cuts: covis.FileCuts in global file ids (per_file: this owner's rows per file, which the caller
+    all-reduces)."""
     from .covis import CovisTable, reference_rules
     ctx = ctx or _lib.context()
     names, rules = reference_rules(names)
@@ -185,11 +187,18 @@ def reduce_received(words, pieces, names, n_files_total: int, n_items: int = con
     p.min_dt, p.max_dt, p.n_items, p.dedup = config.MIN_TIME_TO_NEXT, config.MAX_TIME_TO_NEXT, int(n_items), int(dedup)
     h = ctypes.c_void_p()
     nw, npc = int(words.numel()), int(pieces.numel())
-    _lib.check(_lib.load().ottohip_covis_reduce_received(ctx.h, rules, len(names), ctypes.byref(p), int(n_files_total),
-                                                         _lib.ptr(words) if nw else None, nw,
-                                                         _lib.ptr(pieces) if npc else None, npc, ctypes.byref(h),
-                                                         _lib.stream_handle(stream)))
-    return CovisTable(h, names, ctx)
+    args = (ctx.h, rules, len(names), ctypes.byref(p), int(n_files_total), _lib.ptr(words) if nw else None, nw,
+            _lib.ptr(pieces) if npc else None, npc)
+    if cuts is None:
+        _lib.check(_lib.load().ottohip_covis_reduce_received(*args, ctypes.byref(h), _lib.stream_handle(stream)))
+        return CovisTable(h, names, ctx)
+    o, rows, rows2 = cuts.abi(names, int(n_files_total))
+    _lib.check(_lib.load().ottohip_covis_reduce_received_opts(*args, ctypes.byref(o), ctypes.byref(h),
+                                                              _lib.stream_handle(stream)))
+    tab = CovisTable(h, names, ctx)
+    if cuts.per_file:
+        tab.file_rows_per_file, tab.file_rows_ge2_per_file = rows[:int(n_files_total)], rows2[:int(n_files_total)]
+    return tab
 
 
 def set_file_stats(table, file_stats):
@@ -220,37 +229,54 @@ def _chunk_files(events, n_chunks: int) -> list:
 
 
 def _count_sharded_batches(events, file_ids, n_files_total: int, cap: int, group, names, n_items, dedup, stream, ctx,
-                           chunks):
+                           chunks, cuts=None):
     """More global files than a pair word can tell apart: batches of cap global file ids, each
     counted sharded (batch-local file ids), and every rank merge-sums its own shard tables (the
     owner partition is the same in every batch, so no exchange)."""
     import torch
     fids = np.asarray(file_ids if file_ids is not None else range(len(events.file_bounds) - 1), np.int64)
-    recs, fs, out_names = [], None, None
+    recs, fs, out_names, pf, pf2 = [], None, None, [], []
     for g0 in range(0, int(n_files_total), cap):
         g1 = min(int(n_files_total), g0 + cap)
         sel = np.nonzero((fids >= g0) & (fids < g1))[0]  # the rank's files are in ascending global order
         lo, hi = (int(sel[0]), int(sel[-1]) + 1) if len(sel) else (0, 0)
         sub = events.subset_files(lo, hi)
         t = count_co_events_sharded(sub, (fids[lo:hi] - g0).tolist(), g1 - g0, group, names, n_items, dedup, stream,
-                                    ctx, chunks, max_files=cap)
+                                    ctx, chunks, max_files=cap,
+                                    cuts=cuts.shifted(g0, g1) if cuts is not None else None)
         st = [(t.stats(r)["file_rows"], t.stats(r)["file_rows_ge2"]) for r in range(len(t.names))]
         fs = st if fs is None else [(a + c, b + d) for (a, b), (c, d) in zip(fs, st)]
+        if cuts is not None and cuts.per_file:
+            pf.append(t.file_rows_per_file); pf2.append(t.file_rows_ge2_per_file)
         r, _ = pack_by_owner(t, 1, stream)
         recs.append(r.clone())
         out_names = t.names
         t.free()
-    return table_from_records(torch.cat(recs).contiguous(), out_names, n_items, fs, ctx=ctx, stream=stream)
+    tab = table_from_records(torch.cat(recs).contiguous(), out_names, n_items, fs, ctx=ctx, stream=stream)
+    if pf:
+        tab.file_rows_per_file, tab.file_rows_ge2_per_file = np.concatenate(pf), np.concatenate(pf2)
+    return tab
+
+
+def allreduce_per_file(rows, rows2, group=None):
+    """Sum the owners' per-file row counts (each owner holds its aids' rows of every file)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(np.stack([rows, rows2]), dtype=torch.int64, device=_comm_device(group))
+    dist.all_reduce(t, group=group)
+    t = t.cpu().numpy()
+    return t[0].copy(), t[1].copy()
 
 
 def count_co_events_sharded(events, file_ids, n_files_total: int, group=None, names=None,
                             n_items: int = config.N_ITEMS_OTTO, dedup: bool = True, stream=None, ctx=None,
-                            chunks: int | None = None, max_files: int | None = None):
+                            chunks: int | None = None, max_files: int | None = None, cuts=None):
     """The N-GPU build: this rank's whole files (global ids file_ids) -> pair words laid out by
     owner -> all-to-all-v of words and row pieces (RCCL) -> assemble + reduce of the owner's
     rows. Returns this rank's shard (rows with owner(aid) == rank) of the single-GPU table;
     its file_rows / file_rows_ge2 are the GLOBAL per-file row counts (all-reduced), which is
-    what concat_files_w_stats compares against its thresholds (:131, :135)."""
+    what concat_files_w_stats compares against its thresholds (:131, :135). cuts: covis.FileCuts
+    in global file ids, applied by the owners; per_file statistics are all-reduced (global)."""
     import torch.distributed as dist
     import torch
     from .covis import reference_rules
@@ -258,9 +284,11 @@ def count_co_events_sharded(events, file_ids, n_files_total: int, group=None, na
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     cap = max_files or max_files_per_call(names, n_items)
+    if cuts is not None and cuts.per_file:
+        cap = min(cap, 1024)  # the per-file histogram's file range (ottohip_file_opts)
     if int(n_files_total) > cap:
         tab = _count_sharded_batches(events, file_ids, n_files_total, cap, group, names, n_items, dedup, stream,
-                                     ctx or _lib.context(), chunks)
+                                     ctx or _lib.context(), chunks, cuts)
         tab.rank, tab.world = rank, world
         return tab
     # the rank's files in n_chunks contiguous groups (balanced by events): chunk c's all-to-all
@@ -292,11 +320,18 @@ def count_co_events_sharded(events, file_ids, n_files_total: int, group=None, na
     rw = got[0][0] if len(got) == 1 else torch.cat([g[0] for g in got])
     rp = got[0][1] if len(got) == 1 else torch.cat([g[1] for g in got])
     del got
-    tab = reduce_received(rw, rp, names, n_files_total, n_items, dedup, stream, ctx)
+    if stream is not None and rw.is_cuda:
+        # work.wait() (RCCL) orders only torch's current stream after the transfer (and the cat ran
+        # there): the caller's stream, on which the reduce runs, waits for it
+        stream.wait_stream(torch.cuda.current_stream())
+    tab = reduce_received(rw, rp, names, n_files_total, n_items, dedup, stream, ctx, cuts)
     del rw, rp
     fs = allreduce_file_stats([(tab.stats(r)["file_rows"], tab.stats(r)["file_rows_ge2"]) for r in range(len(names))],
                               group)
     set_file_stats(tab, fs)
+    if cuts is not None and cuts.per_file:
+        tab.file_rows_per_file, tab.file_rows_ge2_per_file = allreduce_per_file(tab.file_rows_per_file,
+                                                                                tab.file_rows_ge2_per_file, group)
     tab.rank, tab.world = rank, world
     return tab
 
@@ -319,6 +354,9 @@ def merge_tables_by_owner(events, group=None, names=None, n_items: int = config.
         stream.synchronize()
     recv = exchange_records(recs, counts, group)
     del recs
+    if stream is not None and recv.is_cuda:  # the exchange is ordered on torch's current stream only
+        import torch
+        stream.wait_stream(torch.cuda.current_stream())
     tab = table_from_records(recv, names, n_items, fs, ctx=local.ctx, stream=stream)
     tab.rank, tab.world = rank, world
     return tab
@@ -465,13 +503,17 @@ def concat_files_w_stats_sharded(events, file_ids, n_files_total: int, name: str
     """concat_files_w_stats (model/count_co_events.py:103-181) for one rule over files dealt to
     ranks: the N-GPU form of covis.concat_files_w_stats_fused, same results on every rank.
     (1) per-file count >= 2 when the GLOBAL N > click_filter_rows; (2) when still > max_rows_groupby,
-    ceil(N / optim_rows) parts of whole global files (file p * nf // n_parts starts part p, as in
-    the fused path), each counted sharded (every rank counts its files of the part), thresholded
-    at MIN_COUNT_IN_PART and cut to its GLOBAL head(int(max_rows_groupby / N * optim_rows)); the
+    ceil(N / optim_rows) row slices of the concatenated per-file tables (each in (aid, aid_next)
+    order, as on one GPU): one sharded pass gives every global file's rows (the owners' per-file
+    counts, all-reduced), the holder of a file cut by a part boundary reads the boundary key from
+    its own count of that file, and each part is counted sharded (every rank counts its files of
+    the part, the owners cut the boundary files to the part's key range), thresholded at
+    MIN_COUNT_IN_PART and cut to its GLOBAL head(int(max_rows_groupby / N * optim_rows)); the
     owner-local part outputs are merge-summed locally (ownership is by aid, so no exchange); (3)
     MIN_COUNT_TO_SAVE and the global head(max_pairs) (finalize_sharded)."""
     import math
     import torch
+    from .covis import FileCuts, part_plan, count_co_events_fused, table_keys_at
     ctx = ctx or _lib.context()
     file_ids = [int(f) for f in file_ids]
     own = table is None
@@ -490,19 +532,41 @@ def concat_files_w_stats_sharded(events, file_ids, n_files_total: int, name: str
         tab.free()
     n_parts = math.ceil(N / optim_rows)
     max_rows_part = int(max_rows_groupby / N * optim_rows)
-    bounds = [(p * n_files_total) // n_parts for p in range(n_parts + 1)]
-    part = {"click_rule": 1 if use_ge2 else 0, "filter_rows": -1,
-            "min_count": config.MIN_COUNT_IN_PART.get(name, 1)}
     fid = np.asarray(file_ids, np.int64)
     if np.any(np.diff(fid) <= 0):
         raise ValueError("file_ids must be increasing (the rank's files in events order)")
-    pieces = []
-    for f0, f1 in zip(bounds[:-1], bounds[1:]):
-        if f1 <= f0:
+    t = count_co_events_sharded(events, file_ids, n_files_total, group, [name], n_items, stream=stream, ctx=ctx,
+                                cuts=FileCuts(name, per_file=True))
+    R = t.file_rows_ge2_per_file if use_ge2 else t.file_rows_per_file
+    t.free()
+    if int(R.sum()) != N:
+        raise RuntimeError(f"{name}: per-file rows sum to {int(R.sum())}, the global N is {N}")
+    plan = part_plan(R, n_parts)
+    # boundary keys: every rank walks the same list; the holder of the file fills its entries
+    need = sorted({(fa, lo) for fa, lo, _, _ in plan if lo > 0} |
+                  {(fb, hi) for _, _, fb, hi in plan if hi < int(R[fb])})
+    kv = np.zeros(max(len(need), 1), np.int64)
+    for f in sorted({f for f, _ in need}):
+        pos = np.flatnonzero(fid == f)
+        if len(pos) == 0:
             continue
-        l0, l1 = int(np.searchsorted(fid, f0)), int(np.searchsorted(fid, f1))
+        rows = [r for g, r in need if g == f]
+        t = count_co_events_fused(events.subset_files(int(pos[0]), int(pos[0]) + 1), [name], n_items=n_items, ctx=ctx,
+                                  stream=stream)
+        for r, k in zip(rows, table_keys_at(t, name, use_ge2, rows, stream)):
+            kv[need.index((f, r))] = int(k)
+        t.free()
+    kv = _allreduce_sum(torch.from_numpy(kv), group).numpy()
+    keys = {fr: int(kv[i]) for i, fr in enumerate(need)}
+    part = {"click_rule": 1 if use_ge2 else 0, "filter_rows": -1,
+            "min_count": config.MIN_COUNT_IN_PART.get(name, 1)}
+    pieces = []
+    for fa, lo, fb, hi in plan:
+        l0, l1 = int(np.searchsorted(fid, fa)), int(np.searchsorted(fid, fb + 1))
+        cuts = FileCuts(name, lo=(fa, keys[(fa, lo)]) if lo > 0 else None,
+                        hi=(fb, keys[(fb, hi)]) if hi < int(R[fb]) else None)
         t = count_co_events_sharded(events.subset_files(l0, l1), file_ids[l0:l1], n_files_total, group, [name],
-                                    n_items, stream=stream, ctx=ctx)
+                                    n_items, stream=stream, ctx=ctx, cuts=cuts)
         pieces.append(finalize_sharded(t, name, max_rows_part, part, False, n_items, group, stream))
         t.free()
     dev = torch.device("cuda", ctx.device)

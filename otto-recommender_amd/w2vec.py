@@ -68,6 +68,21 @@ def load_index_faiss_ivff(embeddings, model_name: str | None = None) -> KnnIndex
     return KnnIndex(embeddings)
 
 
+def word_rows(words, words_q) -> np.ndarray:
+    """Row of each query word in the vocabulary `words` (-1 = not in it): the index lookup of
+    w2vec_aids.py:156-163 as one sorted search (any vocabulary size, no per-word host loop)."""
+    words = np.asarray(words, np.int64)
+    wq = np.asarray(words_q, np.int64)
+    if len(words) == 0:
+        return np.full(len(wq), -1, np.int64)
+    order = np.argsort(words, kind="stable")
+    sw = words[order]
+    pos = np.searchsorted(sw, wq)
+    hit = pos < len(sw)
+    hit[hit] = sw[pos[hit]] == wq[hit]
+    return np.where(hit, order[np.minimum(pos, max(len(sw) - 1, 0))], -1).astype(np.int64)
+
+
 def get_top_k_similar_faiss(words_q, words, map_word_embedding=None, index_faiss_ivff=None, k: int = 20,
                             return_itself: bool = True):
     """w2vec_aids.py:125-173. words_q: query aids; words: the vocabulary (row order of the
@@ -82,9 +97,8 @@ def get_top_k_similar_faiss(words_q, words, map_word_embedding=None, index_faiss
     if index is None:
         raise ValueError("index_faiss_ivff (a KnnIndex) is required")
     words = np.asarray(words, np.int64)
-    word2idx = {int(w): i for i, w in enumerate(words)} if len(words) < 5_000_000 else None
     wq = np.asarray(words_q, np.int64)
-    rows = np.array([word2idx.get(int(w), -1) for w in wq], np.int64)
+    rows = word_rows(words, wq)
     found = rows >= 0
     rows, wq = rows[found], wq[found]
     if len(rows) == 0:

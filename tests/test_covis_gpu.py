@@ -303,23 +303,67 @@ def test_finalize_radix_parity_small_items(gpu, n_items):
     tab.free()
 
 
-def test_concat_files_w_stats_part_branch(gpu):
+@pytest.mark.parametrize("kw", [
+    # c2c: filter (1) + 7 parts; c2cob: 4 parts without (1); cart_to_cart: (3) only
+    dict(max_rows_groupby=300_000, optim_rows=250_000, max_pairs=200_000, click_filter_rows=1_000_000),
+    # parts far smaller than a file (several cuts inside one file, parts inside one file), no filter (1)
+    dict(max_rows_groupby=50_000, optim_rows=20_000, max_pairs=10**9, click_filter_rows=10**9),
+])
+def test_concat_files_w_stats_part_branch(gpu, kw):
     """A6 branch (2) (count_co_events.py:135-166) at test scale: thresholds scaled down so the
-    click filter (1) and the part-wise groupby (2) both trigger; parts are whole-file runs
-    (oracle part_mode="files"). Bit-exact against the restatement."""
+    click filter (1) and the part-wise groupby (2) trigger; parts are row slices of the
+    concatenated per-file tables (each in (aid, aid_next) order), so most part boundaries cut a
+    file. Bit-exact against the restatement."""
     from otto_recommender_amd import covis as gc
     ev = synth.generate(30_000, first_session=2024)
     fb = synth.file_session_bounds(ev.n_sessions, per_file=3_000)
     per_file = oracle.count_co_events_files(ev.session_offsets, ev.aid, ev.ts, ev.type, fb)
     dev = gc.DeviceEvents.from_host(ev, fb)
-    # c2c: filter (1) + 7 parts; c2cob: 4 parts without (1); cart_to_cart: (3) only
-    kw = dict(max_rows_groupby=300_000, optim_rows=250_000, max_pairs=200_000, click_filter_rows=1_000_000)
     for n in ("click_to_click", "click_to_cart_or_buy", "cart_to_cart"):
-        ra, rb, rc = oracle.concat_files_w_stats(n, [p[n] for p in per_file], part_mode="files", **kw)
+        ra, rb, rc = oracle.concat_files_w_stats(n, [p[n] for p in per_file], **kw)
         a, b, c = (x.cpu().numpy() for x in gc.concat_files_w_stats_fused(dev, n, **kw))
         np.testing.assert_array_equal(a, ra, err_msg=n)
         np.testing.assert_array_equal(b, rb, err_msg=n)
         np.testing.assert_array_equal(c, rc, err_msg=n)
+
+
+def test_file_cuts_per_file_rows_and_key_slices(gpu):
+    """ottohip_file_opts: per-file rows (and rows with count >= 2) of one rule equal every file's
+    own table; a lo / hi key cut on a file keeps exactly the rows of its (aid, aid_next)-ordered
+    table inside the key range; table_keys_at reads the rows' keys in that order."""
+    from otto_recommender_amd import covis as gc
+    ev = synth.generate(12_000, first_session=77)
+    fb = synth.file_session_bounds(ev.n_sessions, per_file=3_000)
+    per_file = oracle.count_co_events_files(ev.session_offsets, ev.aid, ev.ts, ev.type, fb)
+    dev = gc.DeviceEvents.from_host(ev, fb)
+    for n in NAMES:
+        t = gc.count_co_events_fused(dev, [n], cuts=gc.FileCuts(n, per_file=True))
+        np.testing.assert_array_equal(t.file_rows_per_file, [len(p[n][0]) for p in per_file], err_msg=n)
+        np.testing.assert_array_equal(t.file_rows_ge2_per_file, [int((p[n][2] >= 2).sum()) for p in per_file],
+                                      err_msg=n)
+        t.free()
+    n = "click_to_click"
+    a1, b1, c1 = per_file[1][n]
+    key = (a1.astype(np.uint64) << np.uint64(32)) | b1.astype(np.uint64)
+    for ge2 in (False, True):
+        sel = c1 >= 2 if ge2 else np.ones(len(c1), bool)
+        t1 = gc.count_co_events_fused(dev.subset_files(1, 2), [n])
+        idx = [0, 5, int(sel.sum()) // 2, int(sel.sum()) - 1]
+        np.testing.assert_array_equal(gc.table_keys_at(t1, n, ge2, idx), key[sel][idx])
+        t1.free()
+    lo, hi = int(key[len(key) // 3]), int(key[2 * len(key) // 3])
+    t = gc.count_co_events_fused(dev, [n], cuts=gc.FileCuts(n, lo=(1, lo), hi=(2, hi), per_file=True))
+    keep1, a2, b2, c2 = key >= lo, *per_file[2][n]
+    keep2 = ((a2.astype(np.uint64) << np.uint64(32)) | b2.astype(np.uint64)) < hi
+    parts = [per_file[0][n], tuple(x[keep1] for x in per_file[1][n]), tuple(x[keep2] for x in per_file[2][n]),
+             per_file[3][n]]
+    np.testing.assert_array_equal(t.file_rows_per_file, [len(p[0]) for p in parts])
+    ga, gb, gcnt = oracle._groupby_sum(*(np.concatenate([p[i] for p in parts]) for i in range(3)))
+    a, b, c, _ = t.to_numpy(n)
+    np.testing.assert_array_equal(a, ga)
+    np.testing.assert_array_equal(b, gb)
+    np.testing.assert_array_equal(c, gcnt)
+    t.free()
 
 
 @pytest.mark.slow

@@ -85,7 +85,7 @@ def test_covis_sharded_two_ranks(gpu, tmp_path):
             np.testing.assert_array_equal(got[f"stats/{n}"], [len(a), int((c >= 2).sum())])
         for tag, kw in cfg["merges"].items():
             ref = np.stack([np.asarray(x, np.int64) for x in
-                            oracle.concat_files_w_stats(n, [p[n] for p in per_file], part_mode="files", **kw)], 1)
+                            oracle.concat_files_w_stats(n, [p[n] for p in per_file], **kw)], 1)
             for r, got in enumerate(res):
                 np.testing.assert_array_equal(got[f"final/{tag}/{n}"], ref, err_msg=f"final {tag} rank {r} {n}")
             sl = np.concatenate([got[f"slice/{tag}/{n}"] for got in res])

@@ -50,7 +50,7 @@ def test_concat_tables_rows_branch(gpu, kw):
     per_file = oracle.count_co_events_files(ev.session_offsets, ev.aid, ev.ts, ev.type, fb)
     for n in ("click_to_click", "click_to_cart_or_buy", "cart_to_buy"):
         tabs = _shuffled_tables(per_file, n, seed=len(n))
-        ref = oracle.concat_files_w_stats(n, tabs, part_mode="rows", **kw)
+        ref = oracle.concat_files_w_stats(n, tabs, **kw)
         got = _np(gc.concat_tables_w_stats(n, [tuple(map(np.asarray, t)) for t in
                                                [(a, b, c.view(np.int32)) for a, b, c in tabs]], **kw))
         _assert_same(got, ref, n)
@@ -71,7 +71,7 @@ def test_concat_tables_edges(gpu):
     # cache: no (1) even above filter_rows -> the count-1 rows still sum
     kw = dict(click_filter_rows=1, max_rows_groupby=2, optim_rows=1)
     got = _np(gc.concat_tables_w_stats("click_to_click", [t1, t2], loaded_from_cache=True, **kw))
-    ref = oracle.concat_files_w_stats("click_to_click", [t1, t2], loaded_from_cache=True, part_mode="rows", **kw)
+    ref = oracle.concat_files_w_stats("click_to_click", [t1, t2], loaded_from_cache=True, **kw)
     _assert_same(got, ref, "cache")
 
 
@@ -97,13 +97,12 @@ def test_merge_train_test_a7(gpu):
     tte = gc.count_co_events_fused(dte)
     differs = 0
     for n in NAMES:
-        ref = oracle.merge_train_test(n, [p[n] for p in pf_tr], [p[n] for p in pf_te], train_mode="files",
-                                      test_mode="files", **kw)
+        ref = oracle.merge_train_test(n, [p[n] for p in pf_tr], [p[n] for p in pf_te], **kw)
         t = gc.concat_files_w_stats_fused(dtr, n, table=ttr, **kw)
         s = gc.concat_files_w_stats_fused(dte, n, table=tte, **kw)
         got = _np(gc.merge_train_test(n, t, s, **kw))
         _assert_same(got, ref, n)
-        fused = oracle.concat_files_w_stats(n, [p[n] for p in pf_tr + pf_te], part_mode="files", **kw)
+        fused = oracle.concat_files_w_stats(n, [p[n] for p in pf_tr + pf_te], **kw)
         differs += int(len(fused[0]) != len(ref[0]) or not np.array_equal(fused[2], ref[2]))
     assert differs > 0, "A7 test input does not separate per-folder thresholds from one fused merge"
 
@@ -138,7 +137,7 @@ def test_file_flow_reference_signatures(gpu, tmp_path):
                 _assert_same(tuple(x[o] for x in got), ref_tab, f"{folder}/{n}/{f}")
                 per.append(got)  # the oracle merges the files as written (row order included)
             gc.concat_files_w_stats(n, f"{dir_stats}/{folder}")
-            folder_ref[(folder, n)] = oracle.concat_files_w_stats(n, per, part_mode="rows")
+            folder_ref[(folder, n)] = oracle.concat_files_w_stats(n, per)
             t = pq.read_table(f"{dir_stats}/{folder}/{n}.parquet")
             assert [str(x) for x in t.schema.types] == ["int32", "int32", "int32"], t.schema
             _assert_same(tuple(t.column(k).to_numpy() for k in ("aid", "aid_next", "count")),
@@ -146,8 +145,7 @@ def test_file_flow_reference_signatures(gpu, tmp_path):
     for n in NAMES:
         gc.concat_files_w_stats(n, dir_stats, files_stats=[f"{dir_stats}/train_sessions/{n}.parquet",
                                                            f"{dir_stats}/test_sessions/{n}.parquet"])
-        ref = oracle.concat_files_w_stats(n, [folder_ref[("train_sessions", n)], folder_ref[("test_sessions", n)]],
-                                          part_mode="rows")
+        ref = oracle.concat_files_w_stats(n, [folder_ref[("train_sessions", n)], folder_ref[("test_sessions", n)]])
         t = pq.read_table(f"{dir_stats}/{n}.parquet")
         got = tuple(t.column(k).to_numpy() for k in ("aid", "aid_next", "count"))
         _assert_same(got, ref, f"train+test/{n}")
