@@ -60,8 +60,9 @@ typedef struct {
 /* Reference-schema parquet rows -> the CSR above, on the device. Replaces the host-side read of
  * model/count_co_events.py:81,91 (pl.read_parquet of a file written by etl/jsonl_to_parquet.py:59-84,
  * schema :23-29); the caller decodes the parquet columns and uploads them raw (device, n_rows).
- * Rows whose sessions form contiguous runs with distinct ids keep their order (the reference's files);
- * otherwise the rows are stably sorted by session id (*reordered = 1). Writes session_offsets
+ * Rows whose sessions form contiguous runs with distinct ids keep their order (the reference's files):
+ * the sessions, and session_ids, are then in FILE order, which need not be ascending (*reordered = 0);
+ * otherwise the rows are stably sorted by session id and session_ids ascend (*reordered = 1). Writes session_offsets
  * [n_sessions + 1] = offset_base + row start (so files can be appended into one CSR),
  * session_ids [n_sessions] (may be NULL) and the aid / ts / type columns (may alias the inputs).
  * Capacity: n_rows + 1 offsets, n_rows ids. OTTOHIP_ELIMIT if n_rows >= 2^32. */

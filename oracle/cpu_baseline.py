@@ -70,9 +70,9 @@ def port(n_files: int, threads: int, seed: int) -> dict:
         raise RuntimeError(f"oracle_count_files_omp failed ({rc})")
     pairs = int(tot[1::2].sum())
     return {"value": pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"first {len(fb) - 1} files ({ev.n_sessions} sessions, {ev.n_events} events, {pairs} pairs) "
-                      f"of the same stream; oracle/covis_oracle.c per-file count, files over {threads} OpenMP "
-                      f"threads, {dt:.1f} s", "seconds": dt, "pairs": pairs, "files": len(fb) - 1}
+            "sample": f"per-file counting only, no cross-file merge: first {len(fb) - 1} files ({ev.n_sessions} "
+                      f"sessions, {ev.n_events} events, {pairs} pairs) of the same stream; oracle/covis_oracle.c "
+                      f"per-file count, files over {threads} OpenMP threads, {dt:.1f} s", "seconds": dt, "pairs": pairs, "files": len(fb) - 1}
 
 
 def _pandas_file(args):
@@ -97,7 +97,8 @@ def pandas_pool(n_files: int, workers: int, seed: int) -> dict:
     pairs = sum(p for _, p in res)
     busy = sum(d for d, _ in res)
     return {"value": pairs / wall, "unit": "pairs/s", "cores": workers, "kind": "port",
-            "sample": f"first {n_files} files ({n_files * 100000} sessions, {pairs} pairs); oracle/covis_pandas.py "
+            "sample": f"per-file counting only, no cross-file merge: first {n_files} files ({n_files * 100000} "
+                      f"sessions, {pairs} pairs); oracle/covis_pandas.py "
                       f"op-for-op restatement of model/count_co_events.py:17-94 (unique, 10k-session parts, join, "
                       f"filters, groupby), process pool of {workers}; {wall:.1f} s wall (includes generating each "
                       f"file in its worker), {busy:.1f} s summed counting time",

@@ -9,6 +9,7 @@ Everything runs in libottohip.so (csrc/candidates.hip); pandas/pyarrow only at t
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -209,11 +210,12 @@ def labels_csr(labels, session_ids):
 
 
 def retrieve_candidates(df_sessions_aids_full, aid_pairs_co_events: dict, df_knns_w2vec_all, df_knns_w2vec_1_2,
-                        df_session_cl=None, df_pop_cl50=None, n_items: int | None = None):
+                        df_session_cl=None, df_pop_cl50=None, n_items: int | None = None, file_out: str | None = None):
     """Candidate-only variant of retrieve_and_gen_feats (model/retrieve.py:422-657), pandas in/out.
     df_sessions_aids_full [session, aid, ts, type]; aid_pairs_co_events {name: R1 frame}; kNN frames
     [aid, aid_next, dist_w2vec*, rank_w2vec*]; df_session_cl [session, cl50]; df_pop_cl50 [aid, cl50, rank_*_cl50].
-    Returns DataFrame[session, aid_next, ts_order_aid, src_*] sorted by (session, ts_order_aid, aid_next)."""
+    Returns DataFrame[session, aid_next, ts_order_aid, src_*] sorted by (session, ts_order_aid, aid_next);
+    file_out: also written in the retrieved schema (write_retrieved, :651-655)."""
     from .synth import events_from_columns
     d = df_sessions_aids_full
     ev = events_from_columns(d["session"].to_numpy(), d["aid"].to_numpy(), d["ts"].to_numpy(), d["type"].to_numpy())
@@ -239,11 +241,38 @@ def retrieve_candidates(df_sessions_aids_full, aid_pairs_co_events: dict, df_knn
         cmap = {int(c): i for i, c in enumerate(clusters)}
         pop = (p["cl50"].map(cmap).to_numpy(), p["aid"].to_numpy())
         ncl = len(clusters)
-        m = dict(zip(df_session_cl["session"].to_numpy().tolist(), df_session_cl["cl50"].to_numpy().tolist()))
-        scl = np.array([cmap.get(int(m[s]), -1) if s in m and m[s] == m[s] else -1 for s in sess_ids.tolist()],
-                       np.int32)
+        # session -> dense cluster index (-1: no cluster / null), one sorted search
+        sc = df_session_cl.dropna(subset=["cl50"])
+        ks = sc["session"].to_numpy().astype(np.int64)
+        kc = np.searchsorted(clusters, sc["cl50"].to_numpy())
+        o = np.argsort(ks, kind="stable")
+        ks, kc = ks[o], kc[o]
+        j = np.searchsorted(ks, sess_ids.astype(np.int64))
+        hit = j < len(ks)
+        hit[hit] = ks[j[hit]] == sess_ids[hit]
+        scl = np.where(hit, kc[np.minimum(j, max(len(ks) - 1, 0))] if len(ks) else -1, -1).astype(np.int32)
     src = CandidateSources(r1, ka, k12, pop, ncl, n_items)
     c = generate(ev.session_offsets, ev.aid, ev.ts, ev.type, src, scl)
     out = c.to_pandas(sess_ids)
     c.free()
+    if file_out is not None:
+        write_retrieved(out, file_out)
     return out
+
+
+def write_retrieved(df, file_out):
+    """The retrieved-candidates file of retrieve_and_gen_feats (model/retrieve.py:647-655):
+    rows sorted by (session, ts_order_aid) -- ties by aid_next here -- written to parquet with the
+    candidate columns [session:int32, aid_next:int32, ts_order_aid:int16, src_*:int8], the columns
+    model/eval_retrieved.py:45-53 reads (session, aid_next, src_*; rank = position in the session)."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    d = df.sort_values(["session", "ts_order_aid", "aid_next"], kind="stable")
+    cols = {"session": pa.array(d["session"].to_numpy().astype(np.int32)),
+            "aid_next": pa.array(d["aid_next"].to_numpy().astype(np.int32)),
+            "ts_order_aid": pa.array(d["ts_order_aid"].to_numpy().astype(np.int16))}
+    for n in SRC_NAMES:
+        if n in d.columns:
+            cols[n] = pa.array(d[n].to_numpy().astype(np.int8))
+    os.makedirs(os.path.dirname(os.path.abspath(file_out)), exist_ok=True)
+    pq.write_table(pa.table(cols), file_out)

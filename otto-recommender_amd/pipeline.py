@@ -83,13 +83,15 @@ def _knn_lists(words, emb, knn_queries, ctx, dev, group):
 def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int = config.N_ITEMS_OTTO,
         n_clusters: int = 50, kmeans_iter: int = 100, knn_queries: int = config.W2VEC_SEARCH_SIMILAR_FOR_FIRST_N_AIDS,
         ctx=None, timings: dict | None = None, keep_tables: bool = False, group=None, n_init="auto",
-        per_file: int | None = None) -> dict:
+        per_file: int | None = None, keep_candidates: bool = True) -> dict:
     """Config 5 end to end. group (torch.distributed, one process per GPU): train and test files
     are dealt whole to ranks (count + sharded A6 per folder, replicated A7 and R1), kNN queries are
     split over ranks and all-gathered, KMeans rows (every session) are sharded with all-reduced
     sums, C3 counters are all-reduced, and each rank generates the candidates of its own test
     files; recall sums are all-reduced. Every rank returns the global numbers; 'candidates' is the
-    whole job's candidate count and 'local_candidates' this rank's."""
+    whole job's candidate count and 'local_candidates' this rank's. keep_tables: host copies of every
+    stage's output in 'intermediates' (the candidates as a DataFrame, or with keep_candidates=False
+    as the device CSR 'candidates_csr' plus 'test_session_ids', for full-size runs)."""
     import torch
     from .synth import file_session_bounds
     from . import dist as gd
@@ -200,6 +202,10 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
             "r1": {n: tuple(h(x) for x in v) for n, v in r1.items()},
             "knn": [tuple(h(x) for x in v) for v in knn],
             "cluster_labels": h(labels_all), "cluster_rows": grows, "pop": p[["cl50", "aid"]].reset_index(drop=True),
-            "candidates": cands.to_pandas(sess)}
+            "n_clusters": n_clusters, "test_session_ids": sess}
+        if keep_candidates:
+            out["intermediates"]["candidates"] = cands.to_pandas(sess)
+        else:
+            out["intermediates"]["candidates_csr"] = cands.to_torch()
     cands.free()
     return out

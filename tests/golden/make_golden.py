@@ -8,6 +8,8 @@ covis_1k.npz         five per-rule tables of the first 1,000 otto-synth sessions
                      produced by the op-for-op pandas restatement of count_co_events.py:17-94
 digest_220m.json     (--full) BASELINE configs[1] at full size: per rule the order-independent
                      checksums of the merged table, from per-file oracle tables (linear sums)
+digest_config5.json  (--config5) BASELINE configs[4] at full size (12.9 M sessions): canonical digests of
+                     the A7 train+test tables of the rules without the part-wise branch
 digests.json         sha256 of canonical (aid, aid_next, count) streams:
                      config-1 slice (first 10,000 sessions, click_to_click) and a 3-file slice
                      (300,000 sessions, all five rules, per-file tables merged with c / c_ge2)
@@ -84,6 +86,15 @@ def main():
     dig["slice_300k_3files_file_rows_ge2"] = {k: int(sum(int((p[k][2] >= 2).sum()) for p in per_file)) for k in m}
     with open(os.path.join(HERE, "digests.json"), "w") as f:
         json.dump(dig, f, indent=1, sort_keys=True)
+    # the streamed A6 of config5_c2c equals the in-memory restatement (branches (1), (2), (3))
+    for n in ("click_to_click", "click_to_cart_or_buy"):
+        full = [p[n] for p in per_file]
+        ge2 = [tuple(x[t[2] >= 2] for x in t) for t in full]
+        kw = dict(max_rows_groupby=1_500_000, optim_rows=700_000, max_pairs=50_000, click_filter_rows=2_000_000)
+        want = covis.concat_files_w_stats(n, full, **kw)
+        got = concat_files_w_stats_streamed(n, full, ge2, sum(len(t[0]) for t in full), **kw)
+        for x, y in zip(want, got):
+            assert np.array_equal(x, y), n
 
 
 
@@ -101,8 +112,137 @@ def full_digest(target_events: int = 220_000_000, seed: int = 0, threads: int = 
                                  "(seed 1) / x count_ge2 (seed 2); pairs = sum count; file_rows = per-file rows"}
 
 
+def _count_file_worker(args):
+    """one 100k-session file of a folder, the non-click_to_click rules (C oracle, per-file table)"""
+    path, f, names = args
+    d = np.load(path)
+    off, aid, ts, ty, fb = d["off"], d["aid"], d["ts"], d["type"], d["fb"]
+    s0, s1 = int(fb[f]), int(fb[f + 1])
+    e0, e1 = int(off[s0]), int(off[s1])
+    rules = {n: covis.REFERENCE_RULES[n] for n in names}
+    return covis.count_co_events_file(off[s0:s1 + 1] - off[s0], aid[e0:e1], ts[e0:e1], ty[e0:e1], rules)
+
+
+def config5_a7(n_sessions: int = 12_900_000, workers: int = 8, names=None) -> dict:
+    """BASELINE configs[4] co-visitation stage at full size (the bench's 12.9 M sessions, seed 0):
+    train / truncated-test split (synth.split_test_labels), per-file tables of each folder's
+    100k-session files (C oracle), A6 per folder and the A7 train+test merge (oracle/covis.py
+    merge_train_test) for the rules whose A6 does not take the part-wise branch (2). Per rule the
+    canonical digest (rows, sum, sha256) of the final table, written to digest_config5.json."""
+    import multiprocessing as mp
+    import tempfile
+    names = names or ["click_to_cart_or_buy", "cart_to_cart", "cart_to_buy", "buy_to_buy"]
+    ev = synth.generate(n_sessions)
+    train, test, _ = synth.split_test_labels(ev)
+    del ev
+    per = {}
+    with tempfile.TemporaryDirectory() as tmp:
+        for tag, e in (("train", train), ("test", test)):
+            fb = synth.file_session_bounds(e.n_sessions)
+            path = os.path.join(tmp, f"{tag}.npz")
+            np.savez(path, off=e.session_offsets - e.session_offsets[0], aid=e.aid, ts=e.ts, type=e.type, fb=fb)
+            with mp.get_context("spawn").Pool(workers) as pool:
+                per[tag] = pool.map(_count_file_worker, [(path, f, names) for f in range(len(fb) - 1)], chunksize=1)
+    out = {"sessions": n_sessions, "train_sessions": int(train.n_sessions), "test_sessions": int(test.n_sessions),
+           "train_files": len(per["train"]), "test_files": len(per["test"]), "rules": {}}
+    for n in names:
+        tr, te = [p[n] for p in per["train"]], [p[n] for p in per["test"]]
+        n_tr = sum(len(t[0]) for t in tr)
+        assert n_tr <= covis.MAX_ROWS_POLARS_GROUPBY, (n, n_tr)  # (2) not taken: the digest is exact
+        out["rules"][n] = covis.canonical_digest({n: covis.merge_train_test(n, tr, te)})[n]
+        out["rules"][n]["folder_rows"] = [n_tr, sum(len(t[0]) for t in te)]
+    return out
+
+
+def _count_file_c2c_worker(args):
+    """one file's click_to_click table: (rows, rows with count >= 2, the table, its count >= 2 part)"""
+    t = _count_file_worker(args)["click_to_click"]
+    keep = t[2] >= 2
+    return len(t[0]), int(keep.sum()), None, tuple(x[keep] for x in t)  # (1) applies at this size: no full table
+
+
+def concat_files_w_stats_streamed(name, tables_full, tables_ge2, n_rows, max_rows_groupby=covis.MAX_ROWS_POLARS_GROUPBY,
+                                  optim_rows=covis.OPTIM_ROWS_POLARS_GROUPBY,
+                                  max_pairs=covis.MAX_CO_EVENT_PAIRS_TO_SAVE_DISK, click_filter_rows=100_000_000):
+    """oracle/covis.py concat_files_w_stats (model/count_co_events.py:103-181) without materialising
+    the concatenation: the per-file tables (each in (aid, aid_next) order) are consumed file by file
+    into the row slices of branch (2). Checked equal to the in-memory restatement in main()."""
+    import math
+    use_ge2 = "click_to" in name and n_rows > click_filter_rows
+    tabs = tables_ge2 if use_ge2 else tables_full
+    if tabs is None or any(t is None for t in tabs):
+        raise ValueError("the per-file tables this branch needs were not kept")
+    N = sum(len(t[0]) for t in tabs)
+    thr_part = covis.MIN_COUNT_IN_PART.get(name, 1)
+    if N > max_rows_groupby:
+        n_parts = math.ceil(N / optim_rows)
+        max_rows_part = int(max_rows_groupby / N * optim_rows)
+        rows_part = math.ceil(N / n_parts)
+        parts, cur, filled = [], [], 0
+
+        def close(chunks):
+            a, b, c = (np.concatenate([x[i] for x in chunks]) for i in range(3))
+            sa, sb, sc = covis._groupby_sum(a, b, c.astype(np.int64))
+            k = sc >= thr_part
+            sa, sb, sc = covis._sort_count_desc(sa[k], sb[k], sc[k])
+            parts.append((sa[:max_rows_part], sb[:max_rows_part], sc[:max_rows_part]))
+
+        for t in tabs:
+            pos = 0
+            while pos < len(t[0]):
+                take = min(rows_part - filled, len(t[0]) - pos)
+                cur.append(tuple(x[pos:pos + take] for x in t))
+                pos += take
+                filled += take
+                if filled == rows_part:
+                    close(cur)
+                    cur, filled = [], 0
+        if cur:
+            close(cur)
+        tabs = parts
+    a, b, c = (np.concatenate([x[i] for x in tabs]) for i in range(3))
+    a, b, c = covis._groupby_sum(a, b, c.astype(np.int64))
+    k = c >= covis.MIN_COUNT_TO_SAVE.get(name, 1)
+    a, b, c = covis._sort_count_desc(a[k], b[k], c[k])
+    return a[:max_pairs], b[:max_pairs], c[:max_pairs].astype(np.int32)
+
+
+def config5_c2c(n_sessions: int = 12_900_000, workers: int = 8) -> dict:
+    """click_to_click of config5_a7: the train folder takes A6 branches (1) and (2) (row slices of the
+    per-file tables in (aid, aid_next) order), so the folder merge is streamed
+    (concat_files_w_stats_streamed); the test folder and the A7 merge as in config5_a7."""
+    import multiprocessing as mp
+    import tempfile
+    ev = synth.generate(n_sessions)
+    train, test, _ = synth.split_test_labels(ev)
+    del ev
+    folders = []
+    out = {}
+    with tempfile.TemporaryDirectory() as tmp:
+        for tag, e in (("train", train), ("test", test)):
+            fb = synth.file_session_bounds(e.n_sessions)
+            path = os.path.join(tmp, f"{tag}.npz")
+            np.savez(path, off=e.session_offsets - e.session_offsets[0], aid=e.aid, ts=e.ts, type=e.type, fb=fb)
+            with mp.get_context("spawn").Pool(workers) as pool:
+                res = pool.map(_count_file_c2c_worker, [(path, f, ["click_to_click"]) for f in range(len(fb) - 1)],
+                               chunksize=1)
+            n_rows = sum(r[0] for r in res)
+            n_ge2 = sum(r[1] for r in res)
+            out[f"{tag}_rows"], out[f"{tag}_rows_ge2"] = n_rows, n_ge2
+            folders.append(concat_files_w_stats_streamed("click_to_click", [r[2] for r in res], [r[3] for r in res],
+                                                         n_rows))
+            del res
+    out.update(covis.canonical_digest({"click_to_click": covis.concat_files_w_stats("click_to_click", folders)})[
+        "click_to_click"])
+    return out
+
+
 if __name__ == "__main__":
     if "--full" in sys.argv:  # ~1 min on 8 cores: the 220M-event digest only
         json.dump(full_digest(), open(os.path.join(HERE, "digest_220m.json"), "w"), indent=1)
+    elif "--config5" in sys.argv:  # a few minutes on 8 cores (~40 GB): the config-5 A7 digests
+        d = config5_a7()
+        d["rules"]["click_to_click"] = config5_c2c()
+        json.dump(d, open(os.path.join(HERE, "digest_config5.json"), "w"), indent=1)
     else:
         main()

@@ -118,3 +118,38 @@ def test_candidates_edge_sessions(gpu):
     got = gcand.retrieve_candidates(df, empty, kn("all"), kn("1_2"))
     for col in ["session", "aid_next", "ts_order_aid"] + gcand.SRC_NAMES:
         np.testing.assert_array_equal(got[col].to_numpy().astype(np.int64), ref[col].to_numpy().astype(np.int64))
+
+
+def test_candidates_written_in_retrieved_schema(gpu, tmp_path):
+    """retrieve_candidates(..., file_out) writes the retrieved file of model/retrieve.py:651-655: rows
+    sorted by (session, ts_order_aid), columns session:int32, aid_next:int32, ts_order_aid:int16,
+    src_*:int8. model/eval_retrieved.py:45-118's recall over the file read back (rank = position
+    within the session) equals the device recall (k_cand_recall) of the same candidates."""
+    import pyarrow.parquet as pq
+    from otto_recommender_amd import candidates as gcand
+    ev, df, r1, ka, k12, cl, pop = _fixture(2500, seed=21, first=7000)
+    f = str(tmp_path / "test-retrieved" / "0000000_0002500.parquet")
+    got = gcand.retrieve_candidates(df, r1, ka, k12, file_out=f)
+    t = pq.read_table(f)
+    assert t.column_names == ["session", "aid_next", "ts_order_aid"] + gcand.SRC_NAMES
+    assert [str(x) for x in t.schema.types] == ["int32", "int32", "int16"] + ["int8"] * len(gcand.SRC_NAMES)
+    back = t.to_pandas()
+    key = back["session"].to_numpy().astype(np.int64) * 100_000 + back["ts_order_aid"].to_numpy()
+    assert (np.diff(key) >= 0).all()
+    for c in back.columns:
+        np.testing.assert_array_equal(back[c].to_numpy().astype(np.int64), got[c].to_numpy().astype(np.int64), err_msg=c)
+    labels = _labels(df, seed=9)
+    sess = ev.session[ev.session_offsets[:-1]]
+    lo, la = gcand.labels_csr(labels, sess)
+    src = gcand.CandidateSources({n: (x["aid"].to_numpy(), x["aid_next"].to_numpy(), x[f"{n}_rank"].to_numpy())
+                                  for n, x in r1.items()},
+                                 (ka["aid"].to_numpy(), ka["aid_next"].to_numpy(), ka["rank_w2vec_all"].to_numpy()),
+                                 (k12["aid"].to_numpy(), k12["aid_next"].to_numpy(), k12["rank_w2vec_1_2"].to_numpy()))
+    c = gcand.generate(ev.session_offsets, ev.aid, ev.ts, ev.type, src)
+    for s in (None, "src_w2vec_1_2", "src_cart_to_cart"):
+        e = oracle_retrieve.recall(back, labels, src=s)
+        r = c.recall(lo, la, src=s)
+        for tt in ("clicks", "carts", "orders", "total"):
+            for k in ("20", "100", "200", "all"):
+                assert abs(r[tt][f"top{k}"] - e[tt][f"top{k}"]) < 1e-12, (s, tt, k)
+    c.free()

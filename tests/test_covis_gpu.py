@@ -366,6 +366,47 @@ def test_file_cuts_per_file_rows_and_key_slices(gpu):
     t.free()
 
 
+@pytest.mark.parametrize("case", ["split_hash", "overflow"])
+def test_file_cuts_hot_rows(gpu, case):
+    """Key cuts and per-file rows through the split, LDS-hash and hash-overflow paths of the reduce
+    (a hot aid with many partners, as in test_heavy_rows_split_and_hash_paths /
+    test_hot_row_overflow_resplit), over 4 files with lo / hi cuts inside the hot row."""
+    from otto_recommender_amd import covis as gc
+    rng = np.random.default_rng(11 if case == "split_hash" else 12)
+    n_s, n = (4000, 40) if case == "split_hash" else (3000, 40)
+    rows = []
+    for s in range(n_s):
+        ts = np.sort(rng.integers(0, 3600, n))
+        if case == "split_hash":
+            aid = np.where(rng.random(n) < 0.5, 7, rng.integers(0, 200_000, n))
+        else:
+            aid = np.where(np.arange(n) % 2 == 0, 7, rng.integers(0, 1_800_000, n))
+        rows.append(np.stack([np.full(n, s), aid, ts, np.zeros(n, np.int64)], 1))
+    a = np.concatenate(rows)
+    ev = synth.events_from_columns(a[:, 0], a[:, 1], a[:, 2], a[:, 3])
+    fb = synth.file_session_bounds(ev.n_sessions, per_file=n_s // 4)
+    n = "click_to_click"
+    per_file = oracle.count_co_events_files(ev.session_offsets, ev.aid, ev.ts, ev.type, fb,
+                                            rules={n: oracle.REFERENCE_RULES[n]})
+    dev = gc.DeviceEvents.from_host(ev, fb)
+    key = lambda t: (t[0].astype(np.uint64) << np.uint64(32)) | t[1].astype(np.uint64)
+    k1, k2 = key(per_file[1][n]), key(per_file[2][n])
+    hot1 = np.flatnonzero(per_file[1][n][0] == 7)
+    hot2 = np.flatnonzero(per_file[2][n][0] == 7)
+    lo, hi = int(k1[hot1[len(hot1) // 3]]), int(k2[hot2[len(hot2) // 2]])
+    t = gc.count_co_events_fused(dev, [n], cuts=gc.FileCuts(n, lo=(1, lo), hi=(2, hi), per_file=True))
+    parts = [per_file[0][n], tuple(x[k1 >= lo] for x in per_file[1][n]), tuple(x[k2 < hi] for x in per_file[2][n]),
+             per_file[3][n]]
+    np.testing.assert_array_equal(t.file_rows_per_file, [len(p[0]) for p in parts])
+    np.testing.assert_array_equal(t.file_rows_ge2_per_file, [int((p[2] >= 2).sum()) for p in parts])
+    ga, gb, gcnt = oracle._groupby_sum(*(np.concatenate([p[i] for p in parts]) for i in range(3)))
+    a_, b_, c_, _ = t.to_numpy(n)
+    np.testing.assert_array_equal(a_, ga)
+    np.testing.assert_array_equal(b_, gb)
+    np.testing.assert_array_equal(c_, gcnt)
+    t.free()
+
+
 @pytest.mark.slow
 def test_full_220m_digest(gpu):
     """BASELINE configs[1] at full size (220M events, 135 files of 100k sessions, all five rules):

@@ -59,14 +59,44 @@ def _owner(aid, world):
 
 
 def test_covis_sharded_two_ranks(gpu, tmp_path):
-    import otto_recommender_amd.synth as synth
     cfg = {"sessions": 18_000, "per_file": 1_500, "first_session": 5150,
            "merges": {
                "reference": {},
                # (1) + (2) for click_to_click, global head cut with ties for every rule
                "scaled": {"click_filter_rows": 200_000, "max_rows_groupby": 250_000, "optim_rows": 150_000,
                           "max_pairs": 700}}}
-    res = _launch("covis", cfg, tmp_path)
+    _check_covis_sharded(cfg, tmp_path, world=2)
+
+
+def test_covis_sharded_four_ranks(gpu, tmp_path):
+    """The same at world 4 (SURVEY.md §8(e) runs 1/2/4/8): 16 files dealt by weight, branch (2)
+    parts of two to three files (ranks hold no file of some parts; the boundary keys come from
+    the file's holder), the global head cut on a count whose ties live on >= 3 owners, and the
+    exchange in 1 / 3 chunks and in global file batches of 2 (_count_sharded_batches)."""
+    from otto_recommender_amd.covis import part_plan
+    cfg = {"sessions": 24_000, "per_file": 1_500, "first_session": 31337,
+           "merges": {
+               "scaled": {"click_filter_rows": 10**9, "max_rows_groupby": 1_500_000, "optim_rows": 600_000,
+                          "max_pairs": 2_000},
+               "filtered": {"click_filter_rows": 100_000, "max_rows_groupby": 300_000, "optim_rows": 120_000,
+                            "max_pairs": 5_000}}}
+    res, per_file = _check_covis_sharded(cfg, tmp_path, world=4)
+    files_of = [set(r["files"].tolist()) for r in res]
+    kw = cfg["merges"]["scaled"]
+    n = "click_to_click"
+    R = np.array([len(p[n][0]) for p in per_file])
+    plan = part_plan(R, -(-int(R.sum()) // kw["optim_rows"]))
+    idle = sum(1 for fa, _, fb, _ in plan for f in files_of if not f & set(range(fa, fb + 1)))
+    assert len(plan) > 1 and idle > 0, "no rank without files of a part"
+    # ties at the global cut spread over >= 3 owners
+    full = oracle.concat_files_w_stats(n, [p[n] for p in per_file], **dict(kw, max_pairs=10**9))
+    cstar = int(full[2][kw["max_pairs"] - 1])
+    assert len(set(_owner(full[0][full[2] == cstar], 4).tolist())) >= 3
+
+
+def _check_covis_sharded(cfg, tmp_path, world):
+    import otto_recommender_amd.synth as synth
+    res = _launch("covis", cfg, tmp_path, world=world)
     ev = synth.generate(cfg["sessions"], first_session=cfg["first_session"])
     fb = synth.file_session_bounds(ev.n_sessions, per_file=cfg["per_file"])
     per_file = oracle.count_co_events_files(ev.session_offsets, ev.aid, ev.ts, ev.type, fb)
@@ -77,7 +107,7 @@ def test_covis_sharded_two_ranks(gpu, tmp_path):
         c = np.concatenate([p[n][2] for p in per_file]).astype(np.int64)
         ra, rb, rc = oracle._groupby_sum(a, b, c)
         _, _, rg = oracle._groupby_sum(a, b, np.where(c >= 2, c, 0))
-        own = _owner(ra, 2)
+        own = _owner(ra, world)
         for r, got in enumerate(res):
             m = own == r
             np.testing.assert_array_equal(got[f"shard/{n}"], np.stack([ra[m], rb[m], rc[m], rg[m]], 1).astype(np.int64),
@@ -93,6 +123,7 @@ def test_covis_sharded_two_ranks(gpu, tmp_path):
             np.testing.assert_array_equal(sl[o], ref, err_msg=f"slices {tag} {n}")
             if tag == "scaled" and n in ("click_to_click", "click_to_cart_or_buy"):
                 assert len(ref) == kw["max_pairs"], (n, len(ref))  # the global cut is active
+    return res, per_file
 
 
 def test_pipeline_two_ranks_equals_one_gpu(gpu, tmp_path):

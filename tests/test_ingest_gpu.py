@@ -79,6 +79,10 @@ def test_csr_distinct_runs_in_any_order_keep_order(gpu):
     parts = [ev.slice_sessions(int(i), int(i) + 1) for i in order]
     cols = [np.concatenate([getattr(p, k) for p in parts]) for k in ("session", "aid", "ts", "type")]
     _check(gpu, *cols, expect_reordered=False)
+    # the session ids come back in file order, not ascending (documented in ottohip.h)
+    _, ids, _, _, _, re = _csr_dev(gpu, *cols)
+    assert not re
+    np.testing.assert_array_equal(ids, order.astype(np.int32))
 
 
 @pytest.mark.parametrize("n,seed", [(37, 0), (5_000, 1), (2_000_003, 2)])

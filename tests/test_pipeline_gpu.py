@@ -86,3 +86,80 @@ def test_pipeline_recall_parity(gpu):
     for t in ("clicks", "carts", "orders", "total"):
         for k in ("top20", "top100", "top200", "topall"):
             assert abs(res["recall"][t][k] - rec[t][k]) < 1e-12, (t, k)
+
+
+@pytest.mark.slow
+def test_pipeline_config5_full_size(gpu):
+    """BASELINE configs[4] at the bench's size (12.9 M sessions, 100k-session files, seed 0):
+    - the A7 train+test tables of all five rules equal the C oracle's (tests/golden/digest_config5.json,
+      make_golden.py --config5): click_to_click's train folder takes A6 branches (1) and (2) by rows
+      (N = 500 M rows with count >= 2), the others (1) / (3);
+    - the candidates of 20,000 sampled test sessions equal oracle/retrieve.candidates given the
+      device's own R1 / kNN / pop lists and clustering (model/retrieve.py:477-595);
+    - device recall sums (k_cand_recall) of those sessions equal model/eval_retrieved.py:45-118's."""
+    import json
+    import os
+    import pandas as pd
+    import torch
+    import covis as oracle
+    import retrieve as oracle_retrieve
+    import otto_recommender_amd.synth as synth
+    from otto_recommender_amd import pipeline, candidates as gcand, config
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "digest_config5.json")))
+    ev = synth.generate(g["sessions"])
+    train, test, labels = synth.split_test_labels(ev)
+    del ev
+    assert (train.n_sessions, test.n_sessions) == (g["train_sessions"], g["test_sessions"])
+    words = synth.item_words()
+    emb = synth.embeddings(len(words), seed=1)
+    emb2 = synth.embeddings(len(words), seed=3)
+    res = pipeline.run(train, test, labels, words, emb, words, emb2, keep_tables=True, keep_candidates=False)
+    im = res["intermediates"]
+    for n in config.CO_EVENTS_TO_COUNT:
+        d = oracle.canonical_digest({n: im["tables"][n]})[n]
+        ref = g["rules"][n]
+        assert (d["rows"], d["sum"], d["sha256"]) == (ref["rows"], ref["sum"], ref["sha256"]), n
+    # 20k sampled test sessions: candidates from the device run vs the oracle on the same sources
+    rng = np.random.default_rng(55)
+    S = test.n_sessions
+    pick = np.sort(rng.choice(S, size=20_000, replace=False))
+    csr = im["candidates_csr"]
+    off = csr["off"].cpu().numpy()
+    lens = off[pick + 1] - off[pick]
+    rows = torch.from_numpy(np.repeat(off[pick] - np.cumsum(lens) + lens, lens) + np.arange(lens.sum())).to(
+        csr["aid_next"].device)
+    sess_ids = im["test_session_ids"]
+    got = pd.DataFrame({"session": np.repeat(sess_ids[pick], lens),
+                        "aid_next": csr["aid_next"][rows].cpu().numpy(),
+                        "ts_order_aid": csr["ts_order_aid"][rows].cpu().numpy()})
+    fl = csr["flags"][rows].cpu().numpy().view(np.uint16)
+    for i, c in enumerate(gcand.SRC_NAMES):
+        got[c] = ((fl >> i) & 1).astype(np.int8)
+    parts = [test.slice_sessions(int(s), int(s) + 1) for s in pick]
+    sub = pipeline._concat(parts)
+    df = sub.to_pandas()
+    aids = np.unique(df["aid"].to_numpy())
+    f = lambda a, b, r, col: (lambda m: pd.DataFrame({"aid": a[m], "aid_next": b[m], col: r[m]}))(np.isin(a, aids))
+    r1 = {n: f(*im["r1"][n], f"{n}_rank") for n in config.CO_EVENTS_TO_COUNT}
+    knn = [f(*k, "rank") for k in im["knn"]]
+    cl = im["cluster_labels"][train.n_sessions:][pick]
+    scl = pd.DataFrame({"session": sess_ids[pick], "cl50": cl})
+    ref = oracle_retrieve.candidates(df, r1, knn[0], knn[1], scl, im["pop"])
+    assert len(got) == len(ref) > 20 * 20_000
+    for c in ["session", "aid_next", "ts_order_aid"] + gcand.SRC_NAMES:
+        np.testing.assert_array_equal(got[c].to_numpy().astype(np.int64), ref[c].to_numpy().astype(np.int64),
+                                      err_msg=c)
+    # recall sums of the sample: the device kernel on the sampled sessions vs the restatement
+    p = im["pop"]
+    src = gcand.CandidateSources(im["r1"], im["knn"][0], im["knn"][1], (p["cl50"].to_numpy(), p["aid"].to_numpy()),
+                                 im["n_clusters"], config.N_ITEMS_OTTO)
+    c = gcand.generate(sub.session_offsets, sub.aid, sub.ts, sub.type, src, cl.astype(np.int32))
+    lab = labels[labels["session"].isin(sess_ids[pick])]
+    lo, la = gcand.labels_csr(lab, sess_ids[pick])
+    r = c.recall(lo, la)
+    e = oracle_retrieve.recall(ref, lab)
+    for t in ("clicks", "carts", "orders", "total"):
+        for k in ("top20", "top100", "top200", "topall"):
+            assert abs(r[t][k] - e[t][k]) < 1e-12, (t, k)
+    assert c.n_cand == len(ref)
+    c.free()
