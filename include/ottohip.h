@@ -251,6 +251,14 @@ void ottohip_candidates_free(ottohip_candidates* c);
  * labels per type t as CSR lab_off[t * (n_sessions + 1) + s] into lab_aid (unique per session/type).
  * sums_out[t * 5 + {0..4}] = sum over sessions of min(hit@20, max_k), min(hit@100, max_k),
  * min(hit@200, max_k), min(hit@all, max_k), min(true, max_k). */
+/* The label CSR ottohip_candidates_recall reads, built on the device from the label rows (session, aid,
+ * type; device, n rows; the test labels model/eval_retrieved.py:59-64 joins): per type t and session
+ * s (the index of its id in session_ids, device [n_sessions], any order) the unique aids, ascending.
+ * lab_off (device, 3 * (n_sessions + 1)) = global positions in lab_aid (device, capacity n); rows of
+ * unknown sessions or types outside {0, 1, 2} are dropped; *n_out = labels kept. */
+int ottohip_labels_csr(ottohip_ctx* ctx, const int32_t* session_ids, int64_t n_sessions, const int32_t* session,
+                       const int32_t* aid, const int8_t* type, int64_t n, int64_t* lab_off, int32_t* lab_aid,
+                       int64_t* n_out, void* stream);
 int ottohip_candidates_recall(ottohip_ctx* ctx, const ottohip_candidates* c, const int64_t* lab_off,
                               const int32_t* lab_aid, uint32_t src_mask, int max_k, int64_t* sums_out, void* stream);
 

@@ -91,6 +91,7 @@ SIGNATURES = {
     "ottohip_candidates_info": (ctypes.c_int, [_VP, ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
     "ottohip_candidates_copy": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
     "ottohip_candidates_free": (None, [_VP]),
+    "ottohip_labels_csr": (ctypes.c_int, [_VP, _VP, _I64, _VP, _VP, _VP, _I64, _VP, _VP, ctypes.POINTER(_I64), _VP]),
     "ottohip_candidates_recall": (ctypes.c_int, [_VP, _VP, _VP, _VP, ctypes.c_uint32, ctypes.c_int,
                                                  ctypes.POINTER(_I64), _VP]),
     "ottohip_session_embeddings": (ctypes.c_int, [_VP, _VP, _I64, _VP, _VP, _VP, _VP, _I32, _VP, ctypes.c_int, _VP, _VP]),

@@ -183,6 +183,26 @@ def generate(offsets, aid, ts, type_, sources: CandidateSources, session_cl=None
     return Candidates(h, ctx)
 
 
+def labels_csr_device(session, aid, type_, session_ids, ctx=None, stream=None):
+    """ottohip_labels_csr: label rows (session, aid, type; device tensors or host arrays) -> the
+    device CSR (off int64 [3*(S+1)], aid int32) that Candidates.recall reads, sessions in the order
+    of session_ids; unique per (session, type), aids ascending."""
+    import torch
+    ctx = ctx or _lib.context()
+    dev = _dev(ctx)
+    t = lambda x, d: (x if isinstance(x, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(x))).to(dev, d).contiguous()
+    se, ai, ty, sid = t(session, torch.int32), t(aid, torch.int32), t(type_, torch.int8), t(session_ids, torch.int32)
+    n, S = int(se.numel()), int(sid.numel())
+    off = torch.empty(3 * (S + 1), dtype=torch.int64, device=dev)
+    out = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    m = ctypes.c_int64()
+    _lib.check(_lib.load().ottohip_labels_csr(ctx.h, _lib.ptr(sid) if S else None, S, _lib.ptr(se) if n else None,
+                                              _lib.ptr(ai) if n else None, _lib.ptr(ty) if n else None, n,
+                                              _lib.ptr(off), _lib.ptr(out) if n else None, ctypes.byref(m),
+                                              _lib.stream_handle(stream)))
+    return off, out[:int(m.value)]
+
+
 def labels_csr(labels, session_ids):
     """labels DataFrame[session, aid, type] -> (off [3*(S+1)] int64, aid int32), unique per (session, type),
     sessions in the order of session_ids."""

@@ -548,7 +548,8 @@ def concat_files_w_stats(name, dir_stats, files_stats=None, n_items: int | None 
         n_items = max([config.N_ITEMS_OTTO] + [int(max(t[0].max(), t[1].max())) + 1 for t in tabs if len(t[0])])
     if any(len(t[2]) and int(t[2].max()) > 0x7FFFFFFF for t in tabs):
         raise ValueError("concat_files_w_stats: a per-file count exceeds int32")
-    dev_tabs = [tuple(torch.from_numpy(x.view(np.int32)) for x in t) for t in tabs]
+    dev_tabs = [tuple(torch.from_numpy(x.view(np.int32) if x.flags.writeable else x.view(np.int32).copy()) for x in t)
+                for t in tabs]
     a, b, c = concat_tables_w_stats(name, dev_tabs, n_items=n_items, loaded_from_cache=cached, **kw)
     _write_table(f"{dir_stats}/{name}.parquet", a.cpu().numpy(), b.cpu().numpy(), c.cpu().numpy(), np.int32)
 

@@ -380,6 +380,10 @@ static int file_opts_setup(ottohip_ctx* ctx, const ottohip_file_opts* o, int n_r
   fo.hi_key = o->hi_key;
   OH_TRY(ctx->ws.get("fo_dropped", 1, &fo.dropped));
   OH_HIP(hipMemsetAsync(fo.dropped, 0, 8, s));
+  if (getenv("OTTOHIP_DEBUG")) {
+    OH_TRY(ctx->ws.get("fo_dbg", 8, &fo.dbg));
+    OH_HIP(hipMemsetAsync(fo.dbg, 0, 64, s));
+  }
   if (want_hist) {
     fo.nf = (uint32_t)o->n_files;
     OH_TRY(ctx->ws.get("fo_hist", (size_t)fo.nf, &fo.hist));
@@ -581,6 +585,12 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   for (int r = 0; r < n_rules; ++r) { sum_pairs += st[r * 4 + 1]; U += st[r * 4 + 0]; }
   if (FOon) {
     if ((rc = d2h(&dropped, fo.dropped, 1, s))) return rc;
+    if (fo.dbg) {
+      unsigned long long dv[8];
+      if ((rc = d2h(dv, fo.dbg, 8, s))) return rc;
+      fprintf(stderr, "[ottohip] file opts: hash dropped %llu kept %llu (loaded %llu inserted %llu), sort dropped %llu kept %llu\n",
+              dv[0], dv[1], dv[4], dv[5], dv[2], dv[3]);
+    }
     if ((rc = file_opts_finish(fopts, fo, s))) return rc;
   }
   T->n_rows = (int64_t)U;

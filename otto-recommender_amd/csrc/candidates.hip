@@ -545,9 +545,125 @@ __global__ void k_u64_to_u32(const uint64_t* __restrict__ a, int64_t n, uint32_t
 
 }  // namespace ottohip
 
+namespace ottohip {
+// ---- label CSR for R9 (model/eval_retrieved.py:45-118): (type, session index, aid) unique
+// session ids sorted with their positions; each label row finds its session by binary search
+__global__ void k_lab_sid_keys(const int32_t* __restrict__ sid, int64_t S, uint32_t* __restrict__ k,
+                               uint32_t* __restrict__ v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= S) return;
+  k[i] = (uint32_t)sid[i] ^ 0x80000000u;  // signed order
+  v[i] = (uint32_t)i;
+}
+// key of a label row after its aid pass: type << sb | session index, or all ones (dropped)
+__global__ void k_lab_group(const uint32_t* __restrict__ perm, int64_t n, const int32_t* __restrict__ sess,
+                            const int8_t* __restrict__ type, const uint32_t* __restrict__ sk,
+                            const uint32_t* __restrict__ sv, int64_t S, int sb, uint32_t* __restrict__ key) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t j = perm[i];
+  const int t = type[j];
+  const uint32_t x = (uint32_t)sess[j] ^ 0x80000000u;
+  int64_t lo = 0, hi = S;  // first sorted id >= x
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (sk[m] < x) lo = m + 1; else hi = m;
+  }
+  const bool ok = t >= 0 && t <= 2 && lo < S && sk[lo] == x;
+  key[i] = ok ? (((uint32_t)t << sb) | sv[lo]) : 0xFFFFFFFFu;
+}
+// kept = valid and not an equal (group, aid) duplicate of its predecessor
+__global__ void k_lab_keep(const uint32_t* __restrict__ g, const uint32_t* __restrict__ perm, int64_t n,
+                           const int32_t* __restrict__ aid, uint32_t* __restrict__ keep) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bool valid = g[i] != 0xFFFFFFFFu;
+  keep[i] = valid && (i == 0 || g[i - 1] != g[i] || aid[perm[i - 1]] != aid[perm[i]]) ? 1u : 0u;
+}
+__global__ void k_lab_compact(const uint32_t* __restrict__ g, const uint32_t* __restrict__ perm,
+                              const uint32_t* __restrict__ keep, const uint64_t* __restrict__ pos, int64_t n,
+                              const int32_t* __restrict__ aid, int sb, int64_t S, int32_t* __restrict__ out_aid,
+                              uint64_t* __restrict__ out_grp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !keep[i]) return;
+  out_aid[pos[i]] = aid[perm[i]];
+  out_grp[pos[i]] = (uint64_t)(g[i] >> sb) * (uint64_t)S + (g[i] & ((1u << sb) - 1u));
+}
+// lab_off[t * (S + 1) + s] = first kept label of group >= t * S + s
+__global__ void k_lab_off(const uint64_t* __restrict__ grp, int64_t m, int64_t S, int64_t* __restrict__ off) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 3 * (S + 1)) return;
+  const int64_t t = i / (S + 1), s = i % (S + 1);
+  const uint64_t x = (uint64_t)t * (uint64_t)S + (uint64_t)s;
+  int64_t lo = 0, hi = m;
+  while (lo < hi) {
+    const int64_t md = (lo + hi) >> 1;
+    if (grp[md] < x) lo = md + 1; else hi = md;
+  }
+  off[i] = lo;
+}
+}  // namespace ottohip
+
 using namespace ottohip;
 
 extern "C" {
+
+int ottohip_labels_csr(ottohip_ctx* ctx, const int32_t* session_ids, int64_t n_sessions, const int32_t* session,
+                       const int32_t* aid, const int8_t* type, int64_t n, int64_t* lab_off, int32_t* lab_aid,
+                       int64_t* n_out, void* stream) {
+  if (!ctx || n_sessions < 0 || n < 0 || !lab_off || !n_out || (n_sessions > 0 && !session_ids) ||
+      (n > 0 && (!session || !aid || !type || !lab_aid))) {
+    set_error("labels_csr: bad args"); return OTTOHIP_EINVAL;
+  }
+  if (n_sessions >= ((int64_t)1 << 29) || n >= ((int64_t)1 << 32)) { set_error("labels_csr: input too large"); return OTTOHIP_ELIMIT; }
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  *n_out = 0;
+  const int64_t S_ = n_sessions;
+  Workspace& ws = ctx->ws;
+  uint32_t *sk, *sv, *sk2, *sv2, *k, *v, *k2, *v2, *keep;
+  uint64_t *pos, *grp, *tot;
+  OH_TRY(ws.get("lab_sk", (size_t)std::max<int64_t>(S_, 1), &sk));
+  OH_TRY(ws.get("lab_sv", (size_t)std::max<int64_t>(S_, 1), &sv));
+  OH_TRY(ws.get("lab_sk2", (size_t)std::max<int64_t>(S_, 1), &sk2));
+  OH_TRY(ws.get("lab_sv2", (size_t)std::max<int64_t>(S_, 1), &sv2));
+  OH_TRY(ws.get("lab_k", (size_t)std::max<int64_t>(n, 1), &k));
+  OH_TRY(ws.get("lab_v", (size_t)std::max<int64_t>(n, 1), &v));
+  OH_TRY(ws.get("lab_k2", (size_t)std::max<int64_t>(n, 1), &k2));
+  OH_TRY(ws.get("lab_v2", (size_t)std::max<int64_t>(n, 1), &v2));
+  OH_TRY(ws.get("lab_keep", (size_t)std::max<int64_t>(n, 1), &keep));
+  OH_TRY(ws.get("lab_pos", (size_t)std::max<int64_t>(n, 1), &pos));
+  OH_TRY(ws.get("lab_grp", (size_t)std::max<int64_t>(n, 1), &grp));
+  OH_TRY(ws.get("lab_tot", 1, &tot));
+  uint32_t *ks = sk, *vs = sv;
+  if (S_ > 0) {
+    k_lab_sid_keys<<<grid_for(S_), 256, 0, s>>>(session_ids, S_, ks, vs);
+    OH_TRY(radix_sort_pairs(ctx, ks, vs, sk2, sv2, S_, 32, s));
+  }
+  uint64_t m = 0;
+  if (n > 0 && S_ > 0) {
+    // stable LSD: aid, then (type, session index) -> (type, session index, aid)
+    uint32_t *kk = k, *vv = v;
+    OH_HIP(hipMemcpyAsync(kk, aid, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+    OH_TRY(radix_sort_pairs(ctx, kk, vv, k2, v2, n, 32, s, true));
+    const int sb = std::max(1, bits_for((uint64_t)S_));
+    uint32_t* kn = kk == k ? k2 : k;
+    k_lab_group<<<grid_for(n), 256, 0, s>>>(vv, n, session, type, ks, vs, S_, sb, kn);
+    kk = kn;
+    uint32_t* vn_alt = vv == v ? v2 : v;
+    uint32_t* kn_alt = kk == k ? k2 : k;
+    OH_TRY(radix_sort_pairs(ctx, kk, vv, kn_alt, vn_alt, n, 32, s));
+    k_lab_keep<<<grid_for(n), 256, 0, s>>>(kk, vv, n, aid, keep);
+    OH_TRY(exclusive_scan_u32(ctx, keep, pos, n, tot, s));
+    OH_TRY(d2h(&m, tot, 1, s));
+    k_lab_compact<<<grid_for(n), 256, 0, s>>>(kk, vv, keep, pos, n, aid, sb, S_, lab_aid, grp);
+  }
+  k_lab_off<<<grid_for(3 * (S_ + 1)), 256, 0, s>>>(grp, (int64_t)m, S_, lab_off);
+  OH_HIP(hipGetLastError());
+  *n_out = (int64_t)m;
+  return 0;
+}
+
 
 // rows (key, nxt[, rank]) -> CSR: out_off [n_keys + 1] (u32), out_nxt / out_rank [n] in key order
 int ottohip_lists_build(ottohip_ctx* ctx, const int32_t* key, const int32_t* nxt, const int16_t* rank, int64_t n,

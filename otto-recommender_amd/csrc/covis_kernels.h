@@ -78,6 +78,7 @@ struct FileOpts {
   unsigned long long* hist;   // [nf] or null
   uint32_t nf;
   unsigned long long* dropped;  // words dropped by the cuts (the reduce's conservation check)
+  unsigned long long* dbg;      // OTTOHIP_DEBUG: [hash dropped, hash kept, sort dropped, sort kept] or null
 };
 __device__ __forceinline__ bool fo_drop(const FileOpts& fo, uint32_t w, int32_t aid, const Layout& L) {
   if (w == W_EMPTY || (w >> (L.A + L.F)) != fo.q) return false;
@@ -1228,8 +1229,11 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
         const int32_t ad = (int32_t)(rkk & L.amask);
         uint32_t k = 0;
 #pragma unroll
-        for (int m = 0; m < M; ++m)
-          if (fo_drop(fo, vv[m], ad, L)) { vv[m] = W_EMPTY; ++k; }
+        for (int m = 0; m < M; ++m) {  // branch-free (a conditional register write here was miscompiled
+          const bool dr = fo_drop(fo, vv[m], ad, L);  // in the hash kernel's load loop: see k_agg_hash)
+          k += dr ? 1u : 0u;
+          vv[m] = dr ? W_EMPTY : vv[m];
+        }
         ndd = wave_sum(k);
       }
     }
@@ -1243,6 +1247,7 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
     if (tn < n_tasks) fetch(tn, Tn, vn, rkn, ndn);
     const uint32_t len = T.len - nd;
     if (FO && nd && l == 0) atomicAdd(fo.dropped, (unsigned long long)nd);
+    if (FO && fo.dbg && l == 0) { atomicAdd(fo.dbg + 2, (unsigned long long)nd); atomicAdd(fo.dbg + 3, (unsigned long long)len); }
     wave_bitonic_sort<M>(v);
     const uint32_t pl = lane_prev(v[M - 1]), nl = lane_next(v[0]);
     // (1) run flags from the neighbours (a w-run = one word = one (rule, aid_next, file)):
@@ -1457,7 +1462,7 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
     const uint32_t* W = (T.buf ? w1 : w0) + T.begin;
     const RowInfo ri = row_info(row_key, T.row, L.A);
     const bool fo_row = FO && ri.type == fo.type;
-    uint32_t ndrop = 0;
+    uint32_t ndrop = 0, dbg_loaded = 0, dbg_ins = 0;
     const uint32_t dbound = T.len;
     // optimistic: more keys possible than fit; give up at 3/4 fill and send the task to a split
     const bool optimistic = 2 * dbound > (uint32_t)HCAP;
@@ -1476,7 +1481,14 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
       for (int j = 0; j < PF; ++j) {
         const uint32_t i = i0 + j * AGG_T + tid;
         wbuf[j] = i < T.len ? W[i] : W_EMPTY;
-        if (FO && fo_row && fo_drop(fo, wbuf[j], ri.aid, L)) { wbuf[j] = W_EMPTY; ++ndrop; }
+        if (FO && fo.dbg && wbuf[j] != W_EMPTY) ++dbg_loaded;
+        if constexpr (FO) {  // branch-free: the cut word becomes W_EMPTY (the if-form lost ~15% of the
+                             // W_EMPTY writes under hipcc 7.2 -O3: counted and cut at once, found by the
+                             // reduce's conservation check, tests/test_covis_gpu.py::test_file_cuts_hot_rows)
+          const bool dr = fo_row && fo_drop(fo, wbuf[j], ri.aid, L);
+          ndrop += dr ? 1u : 0u;
+          wbuf[j] = dr ? W_EMPTY : wbuf[j];
+        }
       }
       // each thread adds at most PF keys after this check: 256 * 8 < HCAP / 4 keeps the table from filling
       if (optimistic && __hip_atomic_load(&nocc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > limit) {
@@ -1496,6 +1508,10 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
         }
       }
       const uint32_t created = hash_insert_batch<PF>(A, wbuf, inc, cm, slot);
+      if (FO && fo.dbg) {
+#pragma unroll
+        for (int j = 0; j < PF; ++j) dbg_ins += (wbuf[j] != W_EMPTY && slot[j] != HASH_FULL) ? inc[j] : 0u;
+      }
 #pragma unroll
       for (int j = 0; j < PF; ++j) full |= wbuf[j] != W_EMPTY && slot[j] == HASH_FULL;
       if (optimistic) {
@@ -1524,6 +1540,17 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
     if constexpr (FO) {  // the task completed: its drops count, and every slot is one per-file row
       const uint32_t nd = wave_sum(ndrop);
       if (nd && (tid & 63) == 0) atomicAdd(fo.dropped, (unsigned long long)nd);
+      if (fo.dbg) {
+        uint32_t kept = 0;
+#pragma unroll
+        for (int s = 0; s < SL; ++s) kept += kw[s] != W_EMPTY ? kc[s] : 0u;
+        kept = wave_sum(kept);
+        const uint32_t ld = wave_sum(dbg_loaded), ins = wave_sum(dbg_ins);
+        if ((tid & 63) == 0) {
+          atomicAdd(fo.dbg + 0, (unsigned long long)nd); atomicAdd(fo.dbg + 1, (unsigned long long)kept);
+          atomicAdd(fo.dbg + 4, (unsigned long long)ld); atomicAdd(fo.dbg + 5, (unsigned long long)ins);
+        }
+      }
       if (fo.hist && fo_row) {
 #pragma unroll
         for (int s = 0; s < SL; ++s)

@@ -123,6 +123,11 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
     fb = np.concatenate([b_tr, b_te[1:] + b_tr[-1]])
     n_tr_files = len(b_tr) - 1
     dev_all = gc.DeviceEvents.from_host(allev, fb)
+    # the label rows of this rank's test sessions (input, resident like the events)
+    sess = ev_te.session[ev_te.session_offsets[:-1] - ev_te.session_offsets[0]]
+    lab_cols = [torch.from_numpy(np.ascontiguousarray(labels[k].to_numpy(), dt)).to(dev)
+                for k, dt in (("session", np.int32), ("aid", np.int32), ("type", np.int8))]
+    sess_dev = torch.from_numpy(np.ascontiguousarray(sess, np.int32)).to(dev)
     t = mark("upload", t)
     folders = [(dev_all.subset_files(0, n_tr_files), my_tr, len(fb_tr) - 1),
                (dev_all.subset_files(n_tr_files, len(fb) - 1), my_te, len(fb_te) - 1)]
@@ -182,8 +187,7 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
     dev_test = folders[1][0]
     cands = gcand.generate(dev_test.offsets, dev_test.aid, dev_test.ts, dev_test.type, src, test_cl)
     t = mark("candidates", t)
-    sess = ev_te.session[ev_te.session_offsets[:-1] - ev_te.session_offsets[0]]
-    lo, la = gcand.labels_csr(labels, sess)
+    lo, la = gcand.labels_csr_device(*lab_cols, sess_dev, ctx=ctx)
     t = mark("labels_csr", t)
     sums = cands.recall_sums(lo, la)
     n_cand = cands.n_cand

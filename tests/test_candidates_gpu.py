@@ -153,3 +153,22 @@ def test_candidates_written_in_retrieved_schema(gpu, tmp_path):
             for k in ("20", "100", "200", "all"):
                 assert abs(r[tt][f"top{k}"] - e[tt][f"top{k}"]) < 1e-12, (s, tt, k)
     c.free()
+
+
+def test_labels_csr_device_matches_host(gpu):
+    """ottohip_labels_csr (device) == candidates.labels_csr (host restatement of the label join of
+    model/eval_retrieved.py:59-64): unique aids per (type, session) in session_ids order, rows of
+    unknown sessions and types outside {0, 1, 2} dropped, duplicates removed; negative ids."""
+    from otto_recommender_amd import candidates as gcand
+    rng = np.random.default_rng(17)
+    sess_ids = rng.permutation(np.arange(-50, 30_000, 3, dtype=np.int32))[:9000]
+    n = 60_000
+    lab = pd.DataFrame({"session": np.concatenate([rng.choice(sess_ids, n - 100), rng.integers(-99, -60, 100)]),
+                        "aid": rng.integers(0, 500, n), "type": rng.integers(-1, 4, n).astype(np.int8)})
+    lo_h, la_h = gcand.labels_csr(lab, sess_ids)
+    lo_d, la_d = gcand.labels_csr_device(lab["session"].to_numpy(), lab["aid"].to_numpy(), lab["type"].to_numpy(),
+                                         sess_ids)
+    np.testing.assert_array_equal(lo_d.cpu().numpy(), lo_h)
+    np.testing.assert_array_equal(la_d.cpu().numpy(), la_h)
+    lo_e, la_e = gcand.labels_csr_device(np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0, np.int8), sess_ids)
+    assert int(lo_e.abs().sum().item()) == 0 and la_e.numel() == 0

@@ -27,7 +27,9 @@ hot2 = np.flatnonzero(per_file[2][nm][0] == 7)
 lo, hi = int(k1[hot1[len(hot1) // 3]]), int(k2[hot2[len(hot2) // 2]])
 exp_lo = int(per_file[1][nm][2][k1 < lo].sum()); exp_hi = int(per_file[2][nm][2][k2 >= hi].sum())
 print("expected cut lo", exp_lo, "hi", exp_hi, "total pairs", sum(int(p[nm][2].sum()) for p in per_file), flush=True)
-for env in ("1", "0"):
+if "diff" in sys.argv:
+    os.environ["OTTOHIP_CONSERVATION_WARN"] = "1"
+for env in (() if ("diff" in sys.argv or "levels" in sys.argv) else ("1",)):
     os.environ["OTTOHIP_REDUCE_OVERLAP"] = env
     for tag, cuts in (("none+pf", gc.FileCuts(nm, per_file=True)), ("lo", gc.FileCuts(nm, lo=(1, lo))),
                       ("hi", gc.FileCuts(nm, hi=(2, hi))), ("lo+hi", gc.FileCuts(nm, lo=(1, lo), hi=(2, hi))),
@@ -39,11 +41,15 @@ for env in ("1", "0"):
         except Exception as e:
             print(env, tag, "FAIL", e, flush=True)
     break
-os.environ["OTTOHIP_DEBUG"] = "1"
-try:
-    t = gc.count_co_events_fused(dev, [nm], cuts=gc.FileCuts(nm, lo=(1, lo)))
-except Exception as e:
-    print("dbg", e, flush=True)
+if "levels" in sys.argv:
+    os.environ["OTTOHIP_DEBUG"] = "1"
+    os.environ["OTTOHIP_CONSERVATION_WARN"] = "1"
+    for tag, cuts in (("hi", gc.FileCuts(nm, hi=(2, hi))), ("lo", gc.FileCuts(nm, lo=(1, lo)))):
+        print("=== levels", tag, flush=True)
+        t = gc.count_co_events_fused(dev, [nm], cuts=cuts)
+        t.free()
+if "diff" not in sys.argv:
+    sys.exit(0)
 
 # the hi-cut table against the oracle: which keys differ
 os.environ.pop("OTTOHIP_DEBUG", None)
@@ -62,3 +68,20 @@ common, i1, i2 = np.intersect1d(kd, ko, return_indices=True)
 diff = np.flatnonzero(c_[i1].astype(np.int64) != gcnt[i2])
 print("count diffs", len(diff), [(int(common[j] >> 32), int(common[j] & 0xFFFFFFFF), int(c_[i1][j]), int(gcnt[i2][j])) for j in diff[:20]], flush=True)
 print("hi key", hi >> 32, hi & 0xFFFFFFFF, flush=True)
+# expected split of the hi cut between the level-1 hash task (level-0 digit of (7, 7)) and the rest
+def _mix(x, level):
+    x = (x ^ ((level * 0x9E3779B9) & 0xFFFFFFFF)) & 0xFFFFFFFF
+    x ^= x >> 16; x = (x * 0x7feb352d) & 0xFFFFFFFF; x ^= x >> 15; x = (x * 0x846ca68b) & 0xFFFFFFFF; x ^= x >> 16
+    return x
+if "levels" in sys.argv:
+    dig = lambda k: (_mix(int(k), 0) * 512) >> 32
+    d7 = dig(7)
+    tot_h = drop_h = 0
+    for f, p in enumerate(per_file):
+        a_, b_, c_ = p[nm]
+        m = (a_ == 7) & np.array([dig(x) == d7 for x in b_])
+        tot_h += int(c_[m].sum())
+        if f == 2:
+            kk = (a_.astype(np.uint64) << np.uint64(32)) | b_.astype(np.uint64)
+            drop_h += int(c_[m & (kk >= hi)].sum())
+    print("expected hash task words", tot_h, "dropped there", drop_h, "kept", tot_h - drop_h, flush=True)
