@@ -154,8 +154,10 @@ static int check_events(const ottohip_events* ev) {
   return 0;
 }
 
+// allow_sym: emit a symmetric rule's pairs once (aid_j >= aid_i) and mirror its rows (RulesDev::sym_mask);
+// OTTOHIP_SYMMETRIC=0 turns it off (A/B switch)
 static int setup_rules(const ottohip_rule* rules, int n_rules, const ottohip_covis_params* params, int n_files_total,
-                       RulesDev& R, Layout& Lt) {
+                       RulesDev& R, Layout& Lt, bool allow_sym = false) {
   if (n_rules < 1 || n_rules > MAX_RULES) { set_error("n_rules=%d outside [1, %d]", n_rules, MAX_RULES); return OTTOHIP_EINVAL; }
   if (params->n_items < 1 || params->n_items > (1 << 30)) { set_error("n_items=%d outside [1, 2^30]", params->n_items); return OTTOHIP_ERANGE; }
   if (n_files_total > 65535) { set_error("n_files > 65535"); return OTTOHIP_ELIMIT; }
@@ -175,6 +177,10 @@ static int setup_rules(const ottohip_rule* rules, int n_rules, const ottohip_cov
   }
   for (int r = 0; r < n_rules; ++r)
     if (R.lo[r] > R.hi[r]) R.mask[r] = 0;  // empty window: never matches (count stays 0)
+  static const bool sym_env = !(getenv("OTTOHIP_SYMMETRIC") && !strcmp(getenv("OTTOHIP_SYMMETRIC"), "0"));
+  if (allow_sym && sym_env)
+    for (int r = 0; r < n_rules; ++r)  // next types == {this type}, dt window symmetric: (i, j) qualifies iff (j, i) does
+      if (R.mask[r] == (1u << rules[r].this_type) && R.lo[r] == -R.hi[r]) R.sym_mask |= 1u << r;
   Lt.A = std::max(1, bits_for((uint64_t)params->n_items));
   Lt.F = bits_for((uint64_t)n_files_total);
   Lt.BR = bits_for((uint64_t)max_per_type);
@@ -414,15 +420,17 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   memset(&fo, 0, sizeof fo);
   if (fopts) OH_TRY(file_opts_setup(ctx, fopts, n_rules, R, fo, s));
   const bool FOon = fopts != nullptr;
-  if (ctx->spare.cap >= P) {
+  // symmetric rules: slots [P, 2P) hold the mirror (aid_next, aid) of the row at slot - P, or a hole
+  const uint64_t n_slots = R.sym_mask ? 2 * P : P;
+  if (ctx->spare.cap >= n_slots) {
     T->b = ctx->spare;
     ctx->spare = TableBufs();
   } else {
     const double t0 = alloc_log_begin();
     (void)hipDeviceSynchronize();
     ctx->spare.release();
-    OH_TRY(T->b.alloc(P));
-    alloc_log_end(t0, "table", "slots", (size_t)P * 17);
+    OH_TRY(T->b.alloc(n_slots));
+    alloc_log_end(t0, "table", "slots", (size_t)n_slots * 17);
   }
   unsigned long long *stats, *lcount;
   OH_TRY(ws.get("stats", (size_t)STAT_STRIPES * STAT_STRIDE, &stats));
@@ -431,10 +439,10 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   hipMemsetAsync(err, 0, sizeof(int), s);
   // rows are written at their task's word offsets; each leaf task marks the rest of its range
   // (rule 0xFF), so the slots need no fill (a debug ablation drops the sort kernels' stores)
-  if (getenv("OTTOHIP_REDUCE_DBG")) hipMemsetAsync(T->b.rule, 0xFF, P, s);
+  if (getenv("OTTOHIP_REDUCE_DBG")) hipMemsetAsync(T->b.rule, 0xFF, n_slots, s);
   OutRows O;
   O.rule = T->b.rule; O.aid = T->b.aid; O.aid_next = T->b.aid_next; O.count = T->b.count; O.count_ge2 = T->b.count_ge2;
-  O.cap = P; O.stats = stats;
+  O.cap = P; O.stats = stats; O.mirror = R.sym_mask ? P : 0;
   // profiling ablation: OTTOHIP_REDUCE_DBG=1 drops the register-sort kernels' row stores
   static const int rdbg = getenv("OTTOHIP_REDUCE_DBG") ? atoi(getenv("OTTOHIP_REDUCE_DBG")) : 0;
   OutRows Osort = O;
@@ -577,12 +585,13 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   if (!drained) { set_error("reduce: split levels did not converge"); return OTTOHIP_ELIMIT; }
   std::vector<unsigned long long> stv((size_t)STAT_STRIPES * STAT_STRIDE);
   if ((rc = d2h(stv.data(), stats, stv.size(), s))) return rc;
-  unsigned long long st[MAX_RULES * 4] = {};
+  unsigned long long st[STAT_STRIDE] = {};
   for (int k = 0; k < STAT_STRIPES; ++k)
-    for (int j = 0; j < MAX_RULES * 4; ++j) st[j] += stv[(size_t)k * STAT_STRIDE + j];
+    for (int j = 0; j < STAT_STRIDE; ++j) st[j] += stv[(size_t)k * STAT_STRIDE + j];
   if (hipGetLastError() != hipSuccess) { set_error("reduce failed"); return OTTOHIP_EHIP; }
-  unsigned long long sum_pairs = 0, U = 0, dropped = 0;
-  for (int r = 0; r < n_rules; ++r) { sum_pairs += st[r * 4 + 1]; U += st[r * 4 + 0]; }
+  unsigned long long U = 0, dropped = 0;
+  for (int r = 0; r < n_rules; ++r) U += st[r * 4 + 0];
+  const unsigned long long sum_pairs = st[STAT_RAW + 1], raw_rows = st[STAT_RAW];  // stored rows / pairs
   if (FOon) {
     if ((rc = d2h(&dropped, fo.dropped, 1, s))) return rc;
     if (fo.dbg) {
@@ -594,10 +603,10 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     if ((rc = file_opts_finish(fopts, fo, s))) return rc;
   }
   T->n_rows = (int64_t)U;
-  T->n_slots = (int64_t)P;
-  if (sum_pairs + dropped != P || U > P) {  // conservation: every emitted pair is counted (or cut) exactly once
+  T->n_slots = (int64_t)n_slots;
+  if (sum_pairs + dropped != P || raw_rows > P) {  // conservation: every emitted pair is counted (or cut) exactly once
     set_error("reduce: %llu pairs counted + %llu cut of %llu emitted (rows %llu)", sum_pairs, dropped,
-              (unsigned long long)P, U);
+              (unsigned long long)P, raw_rows);
     static const bool warn_only = getenv("OTTOHIP_CONSERVATION_WARN") != nullptr;  // debugging aid
     if (!warn_only) return OTTOHIP_EHIP;
     fprintf(stderr, "[ottohip] WARNING %s\n", ottohip_last_error());
@@ -740,7 +749,7 @@ int ottohip_covis_count_opts(ottohip_ctx* ctx, const ottohip_events* ev, const o
   ctx->reset_timing();
   Front F;
   OH_TRY(check_events(ev));
-  OH_TRY(setup_rules(rules, n_rules, params, ev->n_files, F.R, F.Lt));
+  OH_TRY(setup_rules(rules, n_rules, params, ev->n_files, F.R, F.Lt, /*allow_sym=*/opts == nullptr));
   if (opts && (opts->file_rows || opts->file_rows_ge2) && opts->n_files < ev->n_files) {
     set_error("file_opts: n_files=%d < the call's %d files", opts->n_files, ev->n_files); return OTTOHIP_EINVAL;
   }

@@ -29,14 +29,36 @@ constexpr int SPLIT_MEAN = 420;   // hashed split buckets average at most this m
 __constant__ uint32_t c_split_mean = SPLIT_MEAN;  // OTTOHIP_SPLIT_MEAN overrides it (A/B switch, abi.hip)
 constexpr uint32_t W_EMPTY = 0xFFFFFFFFu;
 constexpr int STAT_STRIPES = 256;            // copies of the per-rule statistics
-constexpr int STAT_STRIDE = MAX_RULES * 4;   // u64 per copy (256 B: one L2 line pair per stripe)
+// u64 per copy: [rule * 4 + {rows, pairs, file_rows, file_rows_ge2}] (a symmetric rule's rows with
+// aid != aid_next count twice: the row and its mirror), then STAT_RAW + {0: stored rows, 1: stored
+// pairs} over all rules (the reduce's conservation check against the emitted words)
+constexpr int STAT_RAW = MAX_RULES * 4;
+constexpr int STAT_STRIDE = STAT_RAW + 8;
 
 struct RulesDev {
   int32_t lo[MAX_RULES], hi[MAX_RULES];    // window on dt = ts_j - ts_i, inclusive
   uint32_t mask[MAX_RULES];                // allowed next types
   int32_t n_of_type[4];                    // rules whose this_type == t
   int32_t rule_of_type[4][MAX_RULES];      // global rule id per (t, local index)
+  // Symmetric rules (next types == {this type}, window symmetric in dt: click_to_click, cart_to_cart,
+  // buy_to_buy): every qualifying ordered pair (i, j) has its mirror (j, i), so count(a, b) ==
+  // count(b, a) per session, per file and in total. Only pairs with aid_j >= aid_i are emitted
+  // (both orders of equal aids); each leaf writes the mirror (b, a) of every row with a < b.
+  uint32_t sym_mask;
 };
+
+__device__ __forceinline__ bool rule_sym(const RulesDev& R, int r) { return (R.sym_mask >> r) & 1u; }
+
+// partners j in [jb, je) of the same type t with aid_j >= aid (packed low word aid << 2 | type)
+__device__ __forceinline__ uint32_t count_sym_partners(const uint64_t* ev, int jb, int je, uint32_t aid, int t) {
+  const uint32_t lo = (aid << 2) | (uint32_t)t;
+  uint32_t m = 0;
+  for (int j = jb; j < je; ++j) {
+    const uint32_t w = (uint32_t)ev[j];
+    m += ((w & 3u) == (uint32_t)t && w >= lo) ? 1u : 0u;
+  }
+  return m;
+}
 
 struct Layout {
   int A;      // aid bits
@@ -61,7 +83,8 @@ struct OutRows {
   uint32_t* count;
   uint32_t* count_ge2;
   uint64_t cap;
-  unsigned long long* stats;  // [STAT_STRIPES][MAX_RULES][4]: rows, pairs, file_rows, file_rows_ge2
+  unsigned long long* stats;  // [STAT_STRIPES][STAT_STRIDE]
+  uint64_t mirror;            // symmetric rules: the mirror (b, a) of the row at slot p goes to slot mirror + p
 };
 
 // Per-file options of one rule (ottohip_file_opts; A6 branch (2) by rows, count_co_events.py:136-158):
@@ -236,8 +259,12 @@ __device__ __forceinline__ uint32_t count_event(const SessView& S, int i, const 
     const int je = upper_ts(S.ev, S.nv, tsi + R.hi[r]);
     if (je <= jb) continue;
     uint32_t m = 0;
-    for (int tt = 0; tt < 3; ++tt)
-      if ((R.mask[r] >> tt) & 1u) m += S.pref[tt * S.pstride + je] - S.pref[tt * S.pstride + jb];
+    if (rule_sym(R, r)) {
+      m = count_sym_partners(S.ev, jb, je, (uint32_t)ev_aid(e), t);
+    } else {
+      for (int tt = 0; tt < 3; ++tt)
+        if ((R.mask[r] >> tt) & 1u) m += S.pref[tt * S.pstride + je] - S.pref[tt * S.pstride + jb];
+    }
     if (((R.mask[r] >> t) & 1u) && R.lo[r] <= 0 && R.hi[r] >= 0) {
       if (run < 0) run = equal_run(S.ev, S.nv, i);
       m -= (uint32_t)run;  // the identity row of :23-27 (and exact twins when dedup is off)
@@ -474,9 +501,13 @@ __global__ __launch_bounds__(64) void k_prep_count(const int64_t* __restrict__ o
           const int je = lds_upper_ts(S.key, jb, hi, tsi + sR.hi[r]);
           if (je <= jb) continue;
           uint32_t m = 0;
+          if (rule_sym(sR, r)) {
+            m = count_sym_partners(S.key, jb, je, (uint32_t)ev_aid(e), t);
+          } else {
 #pragma unroll
-          for (int tt = 0; tt < 3; ++tt)
-            if ((sR.mask[r] >> tt) & 1u) m += (uint32_t)S.pref[tt][je] - (uint32_t)S.pref[tt][jb];
+            for (int tt = 0; tt < 3; ++tt)
+              if ((sR.mask[r] >> tt) & 1u) m += (uint32_t)S.pref[tt][je] - (uint32_t)S.pref[tt][jb];
+          }
           if (((sR.mask[r] >> t) & 1u) && sR.lo[r] <= 0 && sR.hi[r] >= 0) {
             if (run < 0) {  // the identity row of :23-27 (and exact twins when dedup is off)
               int a = idx, z = idx + 1;
@@ -739,7 +770,7 @@ __device__ __forceinline__ void emit_session(const SessView& S, int64_t e0, cons
         uint32_t word = 0;
         if (j < je) {
           const uint64_t ej = S.ev[j];
-          match = ej != e && ((R.mask[r] >> ev_type(ej)) & 1u);
+          match = ej != e && ((R.mask[r] >> ev_type(ej)) & 1u) && (!rule_sym(R, r) || ev_aid(ej) >= ev_aid(e));
           word = hi | ((uint32_t)ev_aid(ej) << L.F);
         }
         const uint32_t bal = (uint32_t)(__ballot(match) >> (sg * 16)) & 0xFFFFu;
@@ -770,6 +801,8 @@ constexpr uint32_t EB_NONE = 1023u;
 struct EmitLds {
   uint64_t tev[EB_CAP];                 // type-partitioned events of the batch
   uint32_t rpre[EB_RCAP], rhi[EB_RCAP], rj[EB_RCAP];
+  uint32_t rmin[EB_RCAP];               // smallest partner aid written (symmetric rules: the event's aid)
+  uint32_t rcar[EB_RCAP];               // words of the record written in earlier rounds
   uint64_t rout[EB_RCAP];
   uint16_t ss[65];                      // session start (batch-relative); ss[f] = batch size
   uint16_t sb[4][64];                   // per session: start of the type-t list; sb[3] = end of valid
@@ -785,11 +818,15 @@ struct EmitLds {
 // l + 64 in registers and marks the window position of a start that falls in the round, so a
 // lane's record is the last one of earlier rounds plus the marks at or below the lane: one LDS
 // write and read per round instead of a binary search per pair.
+// A record of a symmetric rule writes only the partners with aid >= rmin (the event's aid): a
+// lane's word goes to the record's output at its rank among the record's written words, i.e. the
+// record's words of earlier rounds (rcar) plus those of the record's lanes below it in this round.
 __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, int F, uint32_t* __restrict__ words,
                                            int dbg, uint32_t& rid) {
   const uint32_t l = lane_id();
   const uint32_t sa = (int)l < nrec ? S.rpre[l] : 0xFFFFFFFFu;
   const uint32_t sb = (int)l + 64 < nrec ? S.rpre[l + 64] : 0xFFFFFFFFu;
+  const uint64_t below = (1ull << l) - 1ull;  // lanes < l
   int ob = -1;  // last record starting before the round's window
   for (uint32_t c = 0; c < tot; c += 64) {
     ++rid;
@@ -801,13 +838,25 @@ __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, i
     const int o = ob + (int)__popcll(mm & (~0ull >> (63u - l)));
     ob += (int)__popcll(mm);
     const uint32_t p = c + l;
+    bool qual = false;
+    uint32_t word = 0, start = 0, car = 0;
     if (p < tot) {
-      const uint32_t off = p - S.rpre[o];
+      start = S.rpre[o];
       const uint32_t jj = S.rj[o];
-      uint32_t j = (jj & 1023u) + off;
+      uint32_t j = (jj & 1023u) + (p - start);
       if (j >= ((jj >> 10) & 1023u)) j += jj >> 21;
-      const uint32_t word = S.rhi[o] | ((uint32_t)ev_aid(S.tev[j]) << F);
-      if (!(dbg & 1)) words[S.rout[o] + off] = word;
+      const uint32_t a = (uint32_t)ev_aid(S.tev[j]);
+      qual = a >= S.rmin[o];
+      word = S.rhi[o] | (a << F);
+      car = S.rcar[o];
+    }
+    const uint64_t Q = __ballot(qual);
+    const uint32_t first = start > c ? start - c : 0u;  // the record's first lane in this round
+    const uint64_t mine = Q & ~((1ull << first) - 1ull);
+    if (qual && !(dbg & 1)) words[S.rout[o] + car + (uint32_t)__popcll(mine & below)] = word;
+    if (p < tot) {  // the record's last lane of the round carries its written words forward
+      const uint32_t nxt = o + 1 < nrec ? S.rpre[o + 1] : tot;
+      if (p + 1 == nxt || l == 63) S.rcar[o] = car + (uint32_t)__popcll(mine & (below | (1ull << l)));
     }
   }
 }
@@ -954,11 +1003,16 @@ __global__ __launch_bounds__(64) void k_emit(const int64_t* __restrict__ off, co
       }
       const int nq = valid ? sR.n_of_type[t] : 0;
       uint32_t eo = 0;
+      bool has_sym = false;
+      // the event's symmetric-rule record comes last: its written length is only known to S2's count
 #pragma unroll 1
-      for (int q = 0; q < maxq; ++q) {
+      for (int qq = 0; qq < 2 * maxq; ++qq) {
+        const int q = qq % maxq, pass = qq / maxq;
         const int r = q < nq ? sR.rule_of_type[t][q] : 0;
-        const uint32_t msk = q < nq ? sR.mask[r] : 0u;
+        const bool sym = q < nq && rule_sym(sR, r);
+        const uint32_t msk = (q < nq && sym == (pass == 1)) ? sR.mask[r] : 0u;
         const int32_t lo = sR.lo[r], hi = sR.hi[r];
+        has_sym |= msk != 0u && sym;
 #pragma unroll 1
         for (int tt = 0; tt < 3; ++tt) {
           const bool act = (msk >> tt) & 1u;
@@ -989,13 +1043,15 @@ __global__ __launch_bounds__(64) void k_emit(const int64_t* __restrict__ off, co
             S.rhi[ri] = ((uint32_t)q << shiftR) | file;
             S.rj[ri] = jb | (xlo << 10) | (xlen << 21);
             S.rout[ri] = eout + eo;
+            S.rmin[ri] = sym ? (uint32_t)ev_aid(v) : 0u;
+            S.rcar[ri] = 0u;
           }
-          eo += len;
+          if (!sym) eo += len;
           nrec += nn;
           tot += __shfl(incl, 63);
         }
       }
-      if (valid && eo != ecnt) atomicOr(err, 4);
+      if (valid && (has_sym ? eo > ecnt : eo != ecnt)) atomicOr(err, 4);
     }
     if (nrec > 0) {
       __builtin_amdgcn_wave_barrier();
@@ -1040,9 +1096,14 @@ __device__ __forceinline__ RowInfo row_info(const uint32_t* row_key, uint32_t ro
 }
 
 __device__ __forceinline__ void put_row(const OutRows& O, uint64_t p, int rule, int32_t aid, int32_t next,
-                                        uint32_t c, uint32_t c2) {
+                                        uint32_t c, uint32_t c2, bool mirror) {
   if (p < O.cap) {
     O.rule[p] = (uint8_t)rule; O.aid[p] = aid; O.aid_next[p] = next; O.count[p] = c; O.count_ge2[p] = c2;
+  }
+  if (O.mirror) {  // the mirror region of a symmetric table: (aid_next, aid) or a hole
+    const uint64_t m = O.mirror + p;
+    O.rule[m] = mirror ? (uint8_t)rule : (uint8_t)0xFF;
+    if (mirror) { O.aid[m] = next; O.aid_next[m] = aid; O.count[m] = c; O.count_ge2[m] = c2; }
   }
 }
 
@@ -1050,14 +1111,22 @@ __device__ __forceinline__ void put_row(const OutRows& O, uint64_t p, int rule, 
 struct RuleAcc {
   uint32_t rows[MAX_RULES], nf1[MAX_RULES], nf2[MAX_RULES];
   unsigned long long pairs[MAX_RULES];
+  uint32_t raw_rows;
+  unsigned long long raw_pairs;
   __device__ void zero() {
 #pragma unroll
     for (int r = 0; r < MAX_RULES; ++r) { rows[r] = nf1[r] = nf2[r] = 0; pairs[r] = 0; }
+    raw_rows = 0; raw_pairs = 0;
   }
-  __device__ void add(int rule, uint32_t c, uint32_t nf) {
+  // mult 2: a symmetric rule's row with aid != aid_next (its mirror row counts too)
+  __device__ void add(int rule, uint32_t c, uint32_t nf, uint32_t mult) {
 #pragma unroll
     for (int r = 0; r < MAX_RULES; ++r)
-      if (r == rule) { rows[r] += 1; pairs[r] += c; nf1[r] += nf & 0xFFFFu; nf2[r] += nf >> 16; }
+      if (r == rule) {
+        rows[r] += mult; pairs[r] += (unsigned long long)c * mult; nf1[r] += (nf & 0xFFFFu) * mult;
+        nf2[r] += (nf >> 16) * mult;
+      }
+    raw_rows += 1; raw_pairs += c;
   }
   // wave reduction, then one device atomic per nonzero statistic into this wave's stripe of
   // the striped statistics array (STAT_STRIPES copies: same-address atomics serialise in L2)
@@ -1079,6 +1148,16 @@ struct RuleAcc {
         }
         if (lane_id() == 0 && x) atomicAdd(&stats[r * 4 + k], x);
       }
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      unsigned long long x = k == 0 ? (unsigned long long)raw_rows : raw_pairs;
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t lo = __shfl_xor((uint32_t)x, d), hi = __shfl_xor((uint32_t)(x >> 32), d);
+        x += ((unsigned long long)hi << 32) | lo;
+      }
+      if (lane_id() == 0 && x) atomicAdd(&stats[STAT_RAW + k], x);
     }
   }
 };
@@ -1196,14 +1275,14 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
                                                   const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
                                                   const uint32_t* __restrict__ row_key, RulesDev R, Layout L,
                                                   int n_rules, OutRows O, FileOpts fo) {
-  __shared__ unsigned long long sacc[4][MAX_RULES * 4];
+  __shared__ unsigned long long sacc[4][STAT_STRIDE];
   __shared__ RulesDev sR;
   __shared__ uint32_t stg[4][2][64 * M];  // per wave: output rows of one task (key2, count | count_ge2 << 16)
   __shared__ unsigned long long fh[FO ? FO_MAXF : 1];  // per-file rows of the FileOpts rule
   const uint32_t l = lane_id();
   const int wv = threadIdx.x >> 6;
   if (threadIdx.x == 0) sR = R;
-  for (int i = (int)l; i < MAX_RULES * 4; i += 64) sacc[wv][i] = 0;
+  for (int i = (int)l; i < STAT_STRIDE; i += 64) sacc[wv][i] = 0;
   if constexpr (FO)
     for (uint32_t i = threadIdx.x; i < fo.nf; i += blockDim.x) fh[i] = 0;
   __syncthreads();
@@ -1311,7 +1390,10 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
     // the per-rule statistics come from the registers here (only key2 and the counts are staged)
     const int nq = sR.n_of_type[type];
     const int r0 = sR.rule_of_type[type][0], r1 = sR.rule_of_type[type][1];
-    uint32_t s0a = 0, s0b = 0, s1a = 0, s1b = 0;  // local rules 0 / 1: rows | nf1 << 16, pairs | nf2 << 16
+    // local rules 0 / 1: rows | nf1 << 16, pairs | nf2 << 16 (a symmetric rule's off-diagonal rows twice);
+    // sraw: stored rows | stored pairs << 16
+    uint32_t s0a = 0, s0b = 0, s1a = 0, s1b = 0, sraw = 0;
+    const bool sym0 = rule_sym(sR, r0), sym1 = nq > 1 && rule_sym(sR, r1);
     {
       uint32_t idx = incl - nmine;
 #pragma unroll
@@ -1321,13 +1403,18 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
           stg[wv][0][idx] = k2;
           stg[wv][1][idx] = b[m];
           ++idx;
-          const uint32_t ra = 1u | ((cc & 0xFFFFu) << 16), rb = cnt | (cc & 0xFFFF0000u);
+          const bool offd = (k2 & L.amask) != (uint32_t)aid;
+          const uint32_t mult = ((q == 0 ? sym0 : (q == 1 ? sym1 : rule_sym(sR, sR.rule_of_type[type][q]))) && offd)
+                                    ? 2u : 1u;
+          const uint32_t ra = (1u | ((cc & 0xFFFFu) << 16)) * mult, rb = (cnt | (cc & 0xFFFF0000u)) * mult;
+          sraw += 1u | (cnt << 16);
           if (q == 0) { s0a += ra; s0b += rb; }
           else if (q == 1) { s1a += ra; s1b += rb; }
           else {  // more than 2 rules of one type (not in the reference's five)
             unsigned long long* acc = sacc[wv] + sR.rule_of_type[type][q] * 4;
-            atomicAdd(acc + 0, 1ull); atomicAdd(acc + 1, (unsigned long long)cnt);
-            atomicAdd(acc + 2, (unsigned long long)(cc & 0xFFFFu)); atomicAdd(acc + 3, (unsigned long long)(cc >> 16));
+            atomicAdd(acc + 0, (unsigned long long)mult); atomicAdd(acc + 1, (unsigned long long)cnt * mult);
+            atomicAdd(acc + 2, (unsigned long long)(cc & 0xFFFFu) * mult);
+            atomicAdd(acc + 3, (unsigned long long)(cc >> 16) * mult);
           }
         }
       }
@@ -1344,20 +1431,35 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
       for (uint32_t i = l; i < nout; i += 64) {
         const uint32_t k2 = stg[wv][0][i], bb = stg[wv][1][i];
         const uint32_t q = k2 >> A;
-        o_rule[i] = (uint8_t)(q == 0 ? r0 : (q == 1 ? r1 : sR.rule_of_type[type][q]));
+        const int rule = q == 0 ? r0 : (q == 1 ? r1 : sR.rule_of_type[type][q]);
+        const int32_t next = (int32_t)(k2 & L.amask);
+        o_rule[i] = (uint8_t)rule;
         o_aid[i] = aid;
-        o_next[i] = (int32_t)(k2 & L.amask);
+        o_next[i] = next;
         o_cnt[i] = bb & 0xFFFFu;
         o_c2[i] = bb >> 16;
+        if (O.mirror) {  // the mirror region: (aid_next, aid) of a symmetric rule's off-diagonal row, else a hole
+          const uint64_t mi = O.mirror + T.begin + i;
+          const bool mr = rule_sym(sR, rule) && next != aid;
+          O.rule[mi] = mr ? (uint8_t)rule : (uint8_t)0xFF;
+          if (mr) { O.aid[mi] = next; O.aid_next[mi] = aid; O.count[mi] = bb & 0xFFFFu; O.count_ge2[mi] = bb >> 16; }
+        }
       }
     if (store)  // the rest of the task's word range holds no row (marked here, no table-wide fill)
-      for (uint32_t i = nout + l; i < T.len; i += 64) o_rule[i] = 0xFF;
+      for (uint32_t i = nout + l; i < T.len; i += 64) {
+        o_rule[i] = 0xFF;
+        if (O.mirror) O.rule[O.mirror + T.begin + i] = 0xFF;
+      }
     for (int q = 0; q < (nq < 2 ? nq : 2); ++q) {
       const uint32_t sa = wave_sum(q == 0 ? s0a : s1a), sb = wave_sum(q == 0 ? s0b : s1b);
       if (l == 0 && sa) {
         unsigned long long* acc = sacc[wv] + (q == 0 ? r0 : r1) * 4;
         acc[0] += sa & 0xFFFFu; acc[1] += sb & 0xFFFFu; acc[2] += sa >> 16; acc[3] += sb >> 16;
       }
+    }
+    {
+      const uint32_t sr = wave_sum(sraw);
+      if (l == 0) { sacc[wv][STAT_RAW] += sr & 0xFFFFu; sacc[wv][STAT_RAW + 1] += sr >> 16; }
     }
     __builtin_amdgcn_wave_barrier();  // the staging rows are rewritten by the next task
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1372,7 +1474,7 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const uint32_t gwave = blockIdx.x * (blockDim.x >> 6) + wv;
   unsigned long long* stats = O.stats + (size_t)(gwave & (STAT_STRIPES - 1)) * STAT_STRIDE;
-  for (int i = (int)l; i < n_rules * 4; i += 64)
+  for (int i = (int)l; i < STAT_STRIDE; i += 64)
     if (sacc[wv][i]) atomicAdd(&stats[i], sacc[wv][i]);
   if constexpr (FO) {
     if (fo.hist) {
@@ -1597,13 +1699,18 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
       const unsigned long long v2 = B2[i];
       const int rule = R.rule_of_type[ri.type][k2 >> L.A];
       const uint32_t c = (uint32_t)v, c2 = (uint32_t)(v2 >> 32), nf = (uint32_t)v2;
-      put_row(O, p++, rule, ri.aid, (int32_t)(k2 & L.amask), c, c2);
-      acc.add(rule, c, nf);
+      const int32_t next = (int32_t)(k2 & L.amask);
+      const bool mr = rule_sym(R, rule) && next != ri.aid;
+      put_row(O, p++, rule, ri.aid, next, c, c2, mr);
+      acc.add(rule, c, nf, mr ? 2u : 1u);
     }
     // the rest of the task's word range holds no row (no table-wide fill: every word position
     // belongs to exactly one leaf task, sort or hash)
     const uint32_t nout = wtot[0] + wtot[1] + wtot[2] + wtot[3];
-    for (uint32_t i = nout + tid; i < T.len; i += AGG_T) O.rule[T.begin + i] = 0xFF;
+    for (uint32_t i = nout + tid; i < T.len; i += AGG_T) {
+      O.rule[T.begin + i] = 0xFF;
+      if (O.mirror) O.rule[O.mirror + T.begin + i] = 0xFF;
+    }
     __syncthreads();
   }
   acc.flush(O.stats, n_rules);
