@@ -800,9 +800,9 @@ constexpr uint32_t EB_NONE = 1023u;
 
 struct EmitLds {
   uint64_t tev[EB_CAP];                 // type-partitioned events of the batch
-  uint32_t rpre[EB_RCAP], rhi[EB_RCAP], rj[EB_RCAP];
-  uint32_t rmin[EB_RCAP];               // smallest partner aid written (symmetric rules: the event's aid)
-  uint32_t rcar[EB_RCAP];               // words of the record written in earlier rounds
+  uint32_t rpre[EB_RCAP];               // record start in the flattened pair order
+  uint4 rec[EB_RCAP];                   // per record: start, list position | exclusion, word high bits,
+                                        // smallest partner aid written (symmetric rules: the event's aid)
   uint64_t rout[EB_RCAP];
   uint16_t ss[65];                      // session start (batch-relative); ss[f] = batch size
   uint16_t sb[4][64];                   // per session: start of the type-t list; sb[3] = end of valid
@@ -818,16 +818,18 @@ struct EmitLds {
 // l + 64 in registers and marks the window position of a start that falls in the round, so a
 // lane's record is the last one of earlier rounds plus the marks at or below the lane: one LDS
 // write and read per round instead of a binary search per pair.
-// A record of a symmetric rule writes only the partners with aid >= rmin (the event's aid): a
-// lane's word goes to the record's output at its rank among the record's written words, i.e. the
-// record's words of earlier rounds (rcar) plus those of the record's lanes below it in this round.
+// A record of a symmetric rule writes only the partners with aid >= its smallest aid (rec.w, the event's
+// aid; 0 for other rules): a lane's word goes to the record's output at its rank among the record's
+// written words -- those of earlier rounds (only the record spanning the round boundary has any: a
+// wave-uniform carry) plus those of the record's lanes below it in this round (one ballot).
 __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, int F, uint32_t* __restrict__ words,
                                            int dbg, uint32_t& rid) {
   const uint32_t l = lane_id();
   const uint32_t sa = (int)l < nrec ? S.rpre[l] : 0xFFFFFFFFu;
   const uint32_t sb = (int)l + 64 < nrec ? S.rpre[l + 64] : 0xFFFFFFFFu;
-  const uint64_t below = (1ull << l) - 1ull;  // lanes < l
-  int ob = -1;  // last record starting before the round's window
+  const uint64_t below = (1ull << l) - 1ull, upto = below | (1ull << l);  // lanes < l, <= l
+  int ob = -1;        // last record starting before the round's window
+  uint32_t cc = 0;    // words written in earlier rounds by the record spanning into this round
   for (uint32_t c = 0; c < tot; c += 64) {
     ++rid;
     if (sa - c < 64u) S.mark[sa - c] = rid;
@@ -835,29 +837,27 @@ __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, i
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     const uint64_t mm = __ballot(S.mark[l] == rid);
-    const int o = ob + (int)__popcll(mm & (~0ull >> (63u - l)));
+    const uint64_t mle = mm & upto;
+    const int o = ob + (int)__popcll(mle);
     ob += (int)__popcll(mm);
     const uint32_t p = c + l;
     bool qual = false;
-    uint32_t word = 0, start = 0, car = 0;
+    uint32_t word = 0;
     if (p < tot) {
-      start = S.rpre[o];
-      const uint32_t jj = S.rj[o];
-      uint32_t j = (jj & 1023u) + (p - start);
-      if (j >= ((jj >> 10) & 1023u)) j += jj >> 21;
+      const uint4 rc = S.rec[o];
+      uint32_t j = (rc.y & 1023u) + (p - rc.x);
+      if (j >= ((rc.y >> 10) & 1023u)) j += rc.y >> 21;
       const uint32_t a = (uint32_t)ev_aid(S.tev[j]);
-      qual = a >= S.rmin[o];
-      word = S.rhi[o] | (a << F);
-      car = S.rcar[o];
+      qual = a >= rc.w;
+      word = rc.z | (a << F);
     }
     const uint64_t Q = __ballot(qual);
-    const uint32_t first = start > c ? start - c : 0u;  // the record's first lane in this round
+    // the record's lanes in this round start at its mark, or at lane 0 for the spanning record
+    const uint32_t first = mle ? 63u - (uint32_t)__builtin_clzll(mle) : 0u;
     const uint64_t mine = Q & ~((1ull << first) - 1ull);
+    const uint32_t car = mle ? 0u : cc;
     if (qual && !(dbg & 1)) words[S.rout[o] + car + (uint32_t)__popcll(mine & below)] = word;
-    if (p < tot) {  // the record's last lane of the round carries its written words forward
-      const uint32_t nxt = o + 1 < nrec ? S.rpre[o + 1] : tot;
-      if (p + 1 == nxt || l == 63) S.rcar[o] = car + (uint32_t)__popcll(mine & (below | (1ull << l)));
-    }
+    cc = (uint32_t)__builtin_amdgcn_readlane((int)(car + (uint32_t)__popcll(mine)), 63);
   }
 }
 
@@ -1005,8 +1005,11 @@ __global__ __launch_bounds__(64) void k_emit(const int64_t* __restrict__ off, co
       uint32_t eo = 0;
       bool has_sym = false;
       // the event's symmetric-rule record comes last: its written length is only known to S2's count
+      bool lane_sym = false;
+      for (int q = 0; q < nq; ++q) lane_sym |= rule_sym(sR, sR.rule_of_type[t][q]);
+      const int nqq = __ballot(lane_sym) ? 2 * maxq : maxq;
 #pragma unroll 1
-      for (int qq = 0; qq < 2 * maxq; ++qq) {
+      for (int qq = 0; qq < nqq; ++qq) {
         const int q = qq % maxq, pass = qq / maxq;
         const int r = q < nq ? sR.rule_of_type[t][q] : 0;
         const bool sym = q < nq && rule_sym(sR, r);
@@ -1040,11 +1043,9 @@ __global__ __launch_bounds__(64) void k_emit(const int64_t* __restrict__ off, co
           if (len > 0) {
             const int ri = nrec + (int)mbcnt(m);
             S.rpre[ri] = tot + incl - len;
-            S.rhi[ri] = ((uint32_t)q << shiftR) | file;
-            S.rj[ri] = jb | (xlo << 10) | (xlen << 21);
+            S.rec[ri] = make_uint4(tot + incl - len, jb | (xlo << 10) | (xlen << 21), ((uint32_t)q << shiftR) | file,
+                                   sym ? (uint32_t)ev_aid(v) : 0u);
             S.rout[ri] = eout + eo;
-            S.rmin[ri] = sym ? (uint32_t)ev_aid(v) : 0u;
-            S.rcar[ri] = 0u;
           }
           if (!sym) eo += len;
           nrec += nn;

@@ -23,9 +23,11 @@ def topk_per_aid(aid, aid_next, count, first_n: int, n_items: int = config.N_ITE
     import torch
     ctx = ctx or _lib.context()
     dev = torch.device("cuda", ctx.device)
-    a = torch.as_tensor(aid).to(dev, torch.int32).contiguous()
-    b = torch.as_tensor(aid_next).to(dev, torch.int32).contiguous()
-    c = torch.as_tensor(count).to(dev, torch.int32).contiguous()
+    # (numpy columns read from parquet are read-only: torch wants a writable buffer to wrap)
+    w = lambda x: x.copy() if isinstance(x, np.ndarray) and not x.flags.writeable else x
+    a = torch.as_tensor(w(aid)).to(dev, torch.int32).contiguous()
+    b = torch.as_tensor(w(aid_next)).to(dev, torch.int32).contiguous()
+    c = torch.as_tensor(w(count)).to(dev, torch.int32).contiguous()
     n = int(a.numel())
     if not (b.numel() == n == c.numel()):
         raise ValueError("aid, aid_next and count must have the same length")
