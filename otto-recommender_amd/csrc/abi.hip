@@ -123,6 +123,7 @@ struct Front {
   uint32_t* lpscr = nullptr;
   uint32_t* cnt = nullptr;
   uint64_t* poff = nullptr;
+  uint32_t* poff32 = nullptr;  // instead of poff when every word offset < 2^32 (one-GPU fused layout)
   uint64_t P = 0;
   int64_t Rn = 0;
   uint32_t* row_key = nullptr;
@@ -314,11 +315,21 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
     if (herr) { set_error("input out of range: aid outside [0, n_items) or type outside {0,1,2}"); return OTTOHIP_ERANGE; }
     F.P = X >> 24;
     F.Rn = (int64_t)(X & 0xFFFFFFull);
-    OH_TRY(ws.get("poff", (size_t)E, &F.poff));
     OH_TRY(ws.get("row_key", (size_t)std::max<int64_t>(F.Rn, 1), &F.row_key));
     OH_TRY(ws.get("row_begin", (size_t)std::max<int64_t>(F.Rn, 1), &F.row_begin));
-    k_rows_tile<<<(unsigned)nb, RT_T, 0, s>>>(rks, poss, F.cnt, E, kmask, INV, cshift, boff, F.poff, F.row_key,
-                                              F.row_begin);
+    // word offsets below 2^32: u32 per event (the random scatter of one offset per event and the
+    // emit's reads move half the bytes; measured rows 12.3 -> 11.1 ms at 220 M events)
+    static const char* p32env = getenv("OTTOHIP_POFF32");  // A/B switch: 0 = u64 offsets
+    F.poff = nullptr; F.poff32 = nullptr;
+    if (F.P < (1ull << 32) && !(p32env && !strcmp(p32env, "0"))) {
+      OH_TRY(ws.get("poff32", (size_t)E, &F.poff32));
+      k_rows_tile<<<(unsigned)nb, RT_T, 0, s>>>(rks, poss, F.cnt, E, kmask, INV, cshift, boff, nullptr, F.poff32, 0u,
+                                                0xFFFFFFFFu, 1, F.row_key, F.row_begin);
+    } else {
+      OH_TRY(ws.get("poff", (size_t)E, &F.poff));
+      k_rows_tile<<<(unsigned)nb, RT_T, 0, s>>>(rks, poss, F.cnt, E, kmask, INV, cshift, boff, F.poff, nullptr, 0u, 0u,
+                                                1, F.row_key, F.row_begin);
+    }
     OH_HIP(hipGetLastError());
     ctx->end(ph, s);
     return 0;
@@ -338,6 +349,7 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
   F.P = PR[0];
   F.Rn = (int64_t)PR[1];
   OH_TRY(ws.get("poff", (size_t)E, &F.poff));
+  F.poff32 = nullptr;
   OH_TRY(ws.get("row_key", (size_t)std::max<int64_t>(F.Rn, 1), &F.row_key));
   OH_TRY(ws.get("row_begin", (size_t)std::max<int64_t>(F.Rn, 1), &F.row_begin));
   k_rows<<<grid_for(E), 256, 0, s>>>(rks, poss, E, INV, kmask, woff, row_flag, row_idx, F.poff, F.row_key,
@@ -355,10 +367,10 @@ static int covis_emit_words(ottohip_ctx* ctx, const Front& F, const ottohip_even
   OH_HIP(hipMemsetAsync(eerr, 0, sizeof(int), s));
   if (F.NB > 0)
     k_emit<<<(unsigned)F.NB, 64, 0, s>>>(F.off, F.first, F.NB, F.evp, F.R, F.Lt, F.fb, ev->n_files, F.fid, F.cnt,
-                                         F.poff, w0, eerr, dbg);
+                                         EvOff{F.poff, F.poff32}, w0, eerr, dbg);
   if (F.nl > 0)
     k_emit_long<<<F.nl, 64, 0, s>>>(F.off, F.long_list, F.d_loff, F.lscr, F.lpscr, F.evp, F.R, F.Lt, F.fb,
-                                     ev->n_files, F.fid, F.cnt, F.poff, w0);
+                                     ev->n_files, F.fid, F.cnt, EvOff{F.poff, F.poff32}, w0);
   if (hipGetLastError() != hipSuccess) { set_error("k_emit launch failed"); return OTTOHIP_EHIP; }
   ctx->end(ph, s);
   int herr = 0;
@@ -455,6 +467,12 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     OH_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_split_mean), &v, sizeof v, 0, hipMemcpyHostToDevice, s));
     OH_HIP(hipStreamSynchronize(s));
   }
+  static const int hash_prio = getenv("OTTOHIP_HASH_PRIO") ? atoi(getenv("OTTOHIP_HASH_PRIO")) : 0;  // A/B switch
+  if (hash_prio) {
+    const uint32_t v = (uint32_t)hash_prio;
+    OH_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_hash_prio), &v, sizeof v, 0, hipMemcpyHostToDevice, s));
+    OH_HIP(hipStreamSynchronize(s));
+  }
   int ph = ctx->begin("reduce", s, 4.0 * (double)P);
   // level 0 task lists come from the rows
   uint64_t cap0 = (uint64_t)std::max<int64_t>(Rn, 1);
@@ -526,12 +544,34 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     if (s2) OH_HIP(hipEventRecord(ctx->ev_join[level & 1], s2));
     if (nlist[N_SORT]) {  // tasks that overflow the LDS table are appended to the split list
       const unsigned hg = (unsigned)std::min<uint64_t>(nlist[N_SORT], (uint64_t)agg_grid);
+      static const bool hprof = getenv("OTTOHIP_HASH_PROF") != nullptr;  // per-task profile (debugging aid)
+      if (hprof) {
+        if ((rc = ws.get("hash_prof", (size_t)(2 * nlist[N_SORT]), &fo.prof))) return rc;
+        OH_HIP(hipMemsetAsync(fo.prof, 0, 16 * nlist[N_SORT], s));
+      }
       if (FOon)
         k_agg_hash<true><<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], w0, w1, row_key, R, Lt, n_rules, O,
                                               TL.split, lcount + N_SORT + 1, fo);
       else
         k_agg_hash<<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], w0, w1, row_key, R, Lt, n_rules, O, TL.split,
                                         lcount + N_SORT + 1, fo);
+      if (hprof) {
+        std::vector<unsigned long long> pv(2 * nlist[N_SORT]);
+        if ((rc = d2h(pv.data(), fo.prof, pv.size(), s))) return rc;
+        std::vector<size_t> ord(nlist[N_SORT]);
+        for (size_t i = 0; i < ord.size(); ++i) ord[i] = i;
+        auto tk = [&](size_t i) { return pv[2 * i + 1] & ~(1ull << 63); };
+        std::sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return tk(a) > tk(b); });
+        unsigned long long tsum = 0, wsum = 0;
+        for (size_t i = 0; i < ord.size(); ++i) { tsum += tk(i); wsum += (uint32_t)pv[2 * i]; }
+        fprintf(stderr, "[ottohip] hash level %d: %zu tasks, %llu words, %.3f ms summed task time; slowest:", level,
+                ord.size(), wsum, tsum / 1e5);
+        for (size_t i = 0; i < ord.size() && i < 10; ++i)
+          fprintf(stderr, " [len %u rows %u %.3f ms%s]", (uint32_t)pv[2 * ord[i]], (uint32_t)(pv[2 * ord[i]] >> 32),
+                  tk(ord[i]) / 1e5, (pv[2 * ord[i] + 1] >> 63) ? " full" : "");
+        fprintf(stderr, "\n");
+        fo.prof = nullptr;
+      }
       if ((rc = d2h(nlist, lcount, N_SORT + 2, s))) return rc;
     }
     const int64_t ns = (int64_t)nlist[N_SORT + 1];

@@ -27,6 +27,7 @@ constexpr int EV_BLOCK = 256;     // events per wave block (sessions starting in
 constexpr int LCAP = 512;         // sessions up to LCAP events run from LDS
 constexpr int SPLIT_MEAN = 420;   // hashed split buckets average at most this many words (default)
 __constant__ uint32_t c_split_mean = SPLIT_MEAN;  // OTTOHIP_SPLIT_MEAN overrides it (A/B switch, abi.hip)
+__constant__ uint32_t c_hash_prio = 0;  // OTTOHIP_HASH_PRIO: wave priority of the LDS-hash leaves (A/B switch)
 constexpr uint32_t W_EMPTY = 0xFFFFFFFFu;
 constexpr int STAT_STRIPES = 256;            // copies of the per-rule statistics
 // u64 per copy: [rule * 4 + {rows, pairs, file_rows, file_rows_ge2}] (a symmetric rule's rows with
@@ -102,6 +103,7 @@ struct FileOpts {
   uint32_t nf;
   unsigned long long* dropped;  // words dropped by the cuts (the reduce's conservation check)
   unsigned long long* dbg;      // OTTOHIP_DEBUG: [hash dropped, hash kept, sort dropped, sort kept] or null
+  unsigned long long* prof;     // OTTOHIP_HASH_PROF: per hash task {len | rows << 32, wall-clock ticks | full << 63} or null
 };
 __device__ __forceinline__ bool fo_drop(const FileOpts& fo, uint32_t w, int32_t aid, const Layout& L) {
   if (w == W_EMPTY || (w >> (L.A + L.F)) != fo.q) return false;
@@ -532,6 +534,14 @@ __global__ __launch_bounds__(64) void k_prep_count(const int64_t* __restrict__ o
 }
 
 // ------------------------------------------------------------------ S3 rows
+// Per event: the first word of its run (row-major word order). u64, or u32 when every word offset
+// fits 32 bits (the one-GPU fused layout).
+struct EvOff {
+  const uint64_t* p64;
+  const uint32_t* p32;
+  __device__ __forceinline__ uint64_t at(int64_t e) const { return p32 ? (uint64_t)p32[e] : p64[e]; }
+};
+
 __global__ void k_gather_counts(const uint32_t* __restrict__ rk, const uint32_t* __restrict__ pos,
                                 const uint32_t* __restrict__ cnt, int64_t n, uint32_t INV,
                                 uint32_t* __restrict__ c_sorted, uint32_t* __restrict__ row_flag) {
@@ -598,11 +608,14 @@ __global__ __launch_bounds__(RT_T) void k_rows_sums(const uint32_t* __restrict__
   if (threadIdx.x == 0) sums[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
+// poff32 != null: u32 offsets, only for events with position in [plo, plo + pw) (windows of the event
+// range, one launch each, measured slower than one pass: plo = 0, pw = ~0); rows only when write_rows.
 __global__ __launch_bounds__(RT_T) void k_rows_tile(const uint32_t* __restrict__ rks, const uint32_t* __restrict__ poss,
                                                     const uint32_t* __restrict__ cnt, int64_t n, uint32_t kmask,
                                                     uint32_t INV, int shift, const uint64_t* __restrict__ offs,
-                                                    uint64_t* __restrict__ poff, uint32_t* __restrict__ row_key,
-                                                    uint64_t* __restrict__ row_begin) {
+                                                    uint64_t* __restrict__ poff, uint32_t* __restrict__ poff32,
+                                                    uint32_t plo, uint32_t pw, int write_rows,
+                                                    uint32_t* __restrict__ row_key, uint64_t* __restrict__ row_begin) {
   const int64_t base = (int64_t)blockIdx.x * RT_TILE + (int64_t)threadIdx.x * RT_I;
   uint64_t x[RT_I];
   uint32_t key[RT_I];
@@ -625,8 +638,13 @@ __global__ __launch_bounds__(RT_T) void k_rows_tile(const uint32_t* __restrict__
   for (int i = 0; i < RT_I; ++i) {
     if (key[i] != INV) {
       const uint64_t woff = run >> 24;
-      poff[poss[base + i]] = woff;
-      if (st[i]) {
+      const uint32_t ps = poss[base + i];
+      if (poff32) {
+        if (ps - plo < pw) poff32[ps] = (uint32_t)woff;
+      } else {
+        poff[ps] = woff;
+      }
+      if (st[i] && write_rows) {
         const uint64_t r = run & 0xFFFFFFull;
         row_key[r] = key[i];
         row_begin[r] = woff;
@@ -746,7 +764,7 @@ __global__ __launch_bounds__(256) void k_piece_copy(const uint32_t* __restrict__
 // block's LDS copies with e0 = the session's offset inside the block
 __device__ __forceinline__ void emit_session(const SessView& S, int64_t e0, const RulesDev& R, const Layout& L,
                                              uint32_t file, const uint32_t* __restrict__ cnt,
-                                             const uint64_t* __restrict__ poff, uint32_t* __restrict__ words,
+                                             EvOff poff, uint32_t* __restrict__ words,
                                              int dbg = 0) {
   const int l = lane_id();
   const int sg = l >> 4, sl = l & 15;
@@ -754,7 +772,7 @@ __device__ __forceinline__ void emit_session(const SessView& S, int64_t e0, cons
   for (int i0 = 0; i0 < S.nv; i0 += 4) {
     const int i = i0 + sg;
     bool active = i < S.nv && cnt[e0 + i] != 0u;
-    uint64_t out = active ? poff[e0 + i] : 0;
+    uint64_t out = active ? poff.at(e0 + i) : 0;
     const uint64_t e = active ? S.ev[i] : 0;
     const int t = ev_type(e);
     const int64_t tsi = ev_ts(e);
@@ -864,7 +882,7 @@ __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, i
 __global__ __launch_bounds__(64) void k_emit(const int64_t* __restrict__ off, const int64_t* __restrict__ first,
                                              int64_t NB, const uint64_t* __restrict__ ev, RulesDev R, Layout L,
                                              const int64_t* __restrict__ fb, int nf, const uint32_t* __restrict__ fid,
-                                             const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ poff,
+                                             const uint32_t* __restrict__ cnt, EvOff poff,
                                              uint32_t* __restrict__ words, int* __restrict__ err, int dbg) {
   __shared__ EmitLds S;
   __shared__ RulesDev sR;
@@ -990,7 +1008,7 @@ __global__ __launch_bounds__(64) void k_emit(const int64_t* __restrict__ off, co
       const uint64_t v = valid ? S.tev[sp] : EV_INVALID;
       const int t = ev_type(v);
       const uint32_t k = in ? S.esid[idx] : 0u;
-      const uint64_t eout = valid ? poff[E0 + idx] : 0;
+      const uint64_t eout = valid ? poff.at(E0 + idx) : 0;
       const uint32_t ecnt = valid ? cnt[E0 + idx] : 0;
       const int64_t tsi = ev_ts(v);
       const uint32_t file = S.sfile[k];
@@ -1071,7 +1089,7 @@ __global__ __launch_bounds__(64) void k_emit_long(const int64_t* __restrict__ of
                                                   const uint64_t* __restrict__ ev, RulesDev R, Layout L,
                                                   const int64_t* __restrict__ fb, int nf,
                                                   const uint32_t* __restrict__ fid,
-                                                  const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ poff,
+                                                  const uint32_t* __restrict__ cnt, EvOff poff,
                                                   uint32_t* __restrict__ words) {
   const int64_t s = list[blockIdx.x];
   const int64_t e0 = off[s];
@@ -1554,6 +1572,10 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
   __shared__ uint32_t nocc;
   __shared__ unsigned long long fh[FO ? FO_MAXF : 1];  // per-file rows of the FileOpts rule
   const int tid = threadIdx.x;
+  // the hash leaves share CUs with the register sorts of the same level (aux stream): a raised wave
+  // priority lets their LDS-latency-bound loop issue ahead of the VALU-bound sorts
+  if (c_hash_prio == 1) __builtin_amdgcn_s_setprio(1);
+  else if (c_hash_prio >= 2) __builtin_amdgcn_s_setprio(3);
   RuleAcc acc;
   acc.zero();
   if constexpr (FO) {
@@ -1562,6 +1584,7 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
   }
   for (int64_t ti = blockIdx.x; ti < n_tasks; ti += gridDim.x) {
     const Task T = tasks[ti];
+    const uint64_t t_start = fo.prof ? wall_clock64() : 0;
     const uint32_t* W = (T.buf ? w1 : w0) + T.begin;
     const RowInfo ri = row_info(row_key, T.row, L.A);
     const bool fo_row = FO && ri.type == fo.type;
@@ -1578,12 +1601,23 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
     __syncthreads();
     bool full = false;
     constexpr int PF = 8;  // words per thread loaded ahead of their inserts
-    uint32_t wbuf[PF];
+    uint32_t wbuf[PF], nbuf[PF];
+    const uint32_t l64 = (uint32_t)tid & 63u;
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const uint32_t i = j * AGG_T + tid;
+      nbuf[j] = i < T.len ? W[i] : W_EMPTY;
+    }
     for (uint32_t i0 = 0; i0 < T.len && !full; i0 += AGG_T * PF) {
+      // the next batch's loads are in flight while this batch is inserted
 #pragma unroll
       for (int j = 0; j < PF; ++j) {
-        const uint32_t i = i0 + j * AGG_T + tid;
-        wbuf[j] = i < T.len ? W[i] : W_EMPTY;
+        wbuf[j] = nbuf[j];
+        const uint32_t i = i0 + (uint32_t)(AGG_T * PF) + j * AGG_T + tid;
+        nbuf[j] = i < T.len ? W[i] : W_EMPTY;
+      }
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
         if (FO && fo.dbg && wbuf[j] != W_EMPTY) ++dbg_loaded;
         if constexpr (FO) {  // branch-free: the cut word becomes W_EMPTY (the if-form lost ~15% of the
                              // W_EMPTY writes under hipcc 7.2 -O3: counted and cut at once, found by the
@@ -1600,15 +1634,17 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
       }
       uint32_t inc[PF], slot[PF];
 #pragma unroll
-      for (int j = 0; j < PF; ++j) {  // a wave-uniform word becomes one add of the wave's count
-        const bool act = wbuf[j] != W_EMPTY;
-        const uint32_t wu = __builtin_amdgcn_readfirstlane(wbuf[j]);
-        const uint64_t am = __ballot(act);
-        inc[j] = 1u;
-        if (am && __ballot(act && wbuf[j] == wu) == am) {
-          inc[j] = (uint32_t)__popcll(am);
-          if ((tid & 63) != 0) wbuf[j] = W_EMPTY;
-        }
+      for (int j = 0; j < PF; ++j) {
+        // runs of equal words over the wave's 64 consecutive words (hot keys arrive in long runs:
+        // words keep their event order through the splits) become one insert of the run length.
+        // Branch-free: a lane that is not a run head carries W_EMPTY.
+        const uint32_t w = wbuf[j];
+        const bool head = l64 == 0u || lane_prev(w) != w;
+        const uint64_t hm = __ballot(head);
+        const uint64_t after = l64 == 63u ? 0ull : hm & (~0ull << (l64 + 1u));
+        const uint32_t end = after ? (uint32_t)__builtin_ctzll(after) : 64u;
+        inc[j] = end - l64;
+        wbuf[j] = head ? w : W_EMPTY;
       }
       const uint32_t created = hash_insert_batch<PF>(A, wbuf, inc, cm, slot);
       if (FO && fo.dbg) {
@@ -1627,6 +1663,10 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
       if (tid == 0) {
         const unsigned long long k = atomicAdd(n_overflow, 1ull);
         overflow[k] = T;  // capacity = number of hash tasks
+        if (fo.prof) {
+          fo.prof[2 * ti] = T.len;
+          fo.prof[2 * ti + 1] = (wall_clock64() - t_start) | (1ull << 63);
+        }
       }
       __syncthreads();
       continue;
@@ -1713,6 +1753,10 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
       if (O.mirror) O.rule[O.mirror + T.begin + i] = 0xFF;
     }
     __syncthreads();
+    if (fo.prof && tid == 0) {
+      fo.prof[2 * ti] = T.len | ((unsigned long long)nout << 32);
+      fo.prof[2 * ti + 1] = wall_clock64() - t_start;
+    }
   }
   acc.flush(O.stats, n_rules);
   if constexpr (FO) {
