@@ -310,6 +310,11 @@ int ottohip_kmeans_lloyd_iter(ottohip_ctx* ctx, const float* X, int64_t n, int d
 int ottohip_kmeans_lloyd_steps(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* centroids, int k,
                                int32_t* labels, int64_t* sums, int64_t* counts, int max_steps, double tol,
                                double* out, void* stream);
+/* The E-step of lloyd_steps is a split-precision pass (x = hi + lo and c = hi + lo in bf16, three bf16
+ * MFMA products, a rigorous error bound) that decides every row whose two best scores are separated
+ * beyond the bound, plus the exact f32 kernel on the remaining near ties: labels, sums and stop
+ * checks are bit-identical to the exact kernel on every row (out[0] then covers the near ties only).
+ * (OTTOHIP_KM_SPLIT=0: the exact kernel on every row). */
 int ottohip_kmeans_farthest(ottohip_ctx* ctx, const float* X, int64_t n, int dim, const float* centroids,
                             const int32_t* labels, int m, int64_t* rows, float* d2, void* stream);
 int ottohip_kmeans_relocate(ottohip_ctx* ctx, int64_t* sums, int64_t* counts, int k, int dim, const float* vecs,

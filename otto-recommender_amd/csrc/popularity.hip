@@ -226,9 +226,76 @@ __device__ __forceinline__ long long km_fx(float x) {
   return fabsf(x) < 128.f ? (long long)__float2int_rn(y) : __float2ll_rn(y);
 }
 
+// The rows of a wave whose vector enters a cluster's block sums (one per flagged lane: row, new
+// cluster, previous cluster or -1 to leave none), listed in the wave's LDS slot (3 x 32 ints), then
+// lanes over dims: 2^-24 fixed-point adds into the block's LDS sums (exact, order-independent).
+__device__ __forceinline__ void km_move_rows(const float* __restrict__ X, int dim, unsigned long long* ls,
+                                             unsigned long long* lc, int32_t* labl, bool flag, int64_t row,
+                                             uint32_t to, int32_t from) {
+  const int l = (int)lane_id();
+  const uint64_t bm = __ballot(flag);
+  if (flag) {
+    const int p = (int)mbcnt(bm);
+    labl[p] = (int32_t)row;
+    labl[32 + p] = (int32_t)to;
+    labl[64 + p] = from;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const int nr = (int)__popcll(bm);
+  for (int rr = 0; rr < nr; rr += 8) {  // 8 rows' loads in flight
+    float xa[8], xb[8];
+    int cc[8], co[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int pq = rr + q < nr ? rr + q : nr - 1;
+      const int64_t r = labl[pq];
+      cc[q] = labl[32 + pq];
+      co[q] = labl[64 + pq];
+      const float* xq = X + r * dim;
+      xa[q] = l < dim ? xq[l] : 0.f;
+      xb[q] = l + 64 < dim ? xq[l + 64] : 0.f;
+    }
+    // exact 2^24 scaling: one f32 -> i32 conversion per value while every |x| < 128 (the
+    // product is exact and below 2^31); the general f32 -> i64 sequence only for a wave
+    // that holds a larger value
+    bool big = false;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) big |= fabsf(xa[q]) >= 128.f || fabsf(xb[q]) >= 128.f;
+    long long fa[8], fb[8];
+    if (__builtin_expect(__ballot(big) != 0, 0)) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) { fa[q] = __float2ll_rn(xa[q] * 16777216.0f); fb[q] = __float2ll_rn(xb[q] * 16777216.0f); }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        fa[q] = (long long)__float2int_rn(xa[q] * 16777216.0f);
+        fb[q] = (long long)__float2int_rn(xb[q] * 16777216.0f);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      if (rr + q >= nr) break;
+      unsigned long long* rw = ls + cc[q] * dim;
+      if (l < dim) atomicAdd(&rw[l], (unsigned long long)fa[q]);
+      if (l + 64 < dim) atomicAdd(&rw[l + 64], (unsigned long long)fb[q]);
+      if (l == 0) atomicAdd(&lc[cc[q]], 1ull);
+      if (co[q] >= 0) {  // two's-complement deltas: the block's sums may go below zero
+        unsigned long long* orow = ls + co[q] * dim;
+        if (l < dim) atomicAdd(&orow[l], (unsigned long long)(-fa[q]));
+        if (l + 64 < dim) atomicAdd(&orow[l + 64], (unsigned long long)(-fb[q]));
+        if (l == 0) atomicAdd(&lc[co[q]], ~0ull);
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();  // labl is rewritten by the next tile
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
 // NQ: 16-B pieces per row half as a constant (13 for dim 100: the row registers of the unused
 // pieces are not allocated, which keeps the kernel at <= 128 VGPRs = 2 blocks per CU)
-template <int NB, int NQ>
+// LIST: score only the rows lrows[0, *lnrows) (the split-precision pass's near ties)
+template <int NB, int NQ, bool LIST = false>
 __global__ __launch_bounds__(KM_MT, (NQ <= 13 ? 4 : 2)) void k_km_assign_mfma(const float* __restrict__ X, int64_t n, int dim, int nq,
                                                         const float* __restrict__ C, const float* __restrict__ cn,
                                                         int k, int32_t* __restrict__ label,
@@ -237,7 +304,9 @@ __global__ __launch_bounds__(KM_MT, (NQ <= 13 ? 4 : 2)) void k_km_assign_mfma(co
                                                         double* __restrict__ inertia,
                                                         unsigned long long* __restrict__ changed,
                                                         float* __restrict__ dist, int inc,
-                                                        const int* __restrict__ gate) {
+                                                        const int* __restrict__ gate,
+                                                        const uint32_t* __restrict__ lrows = nullptr,
+                                                        const unsigned long long* __restrict__ lnrows = nullptr) {
   if (gate && __builtin_amdgcn_readfirstlane(*gate)) return;  // batched Lloyd steps: converged earlier
   extern __shared__ unsigned long long smem64[];
   float4* Bl = reinterpret_cast<float4*>(smem64);                              // [NB][nq][64]
@@ -259,11 +328,14 @@ __global__ __launch_bounds__(KM_MT, (NQ <= 13 ? 4 : 2)) void k_km_assign_mfma(co
   __syncthreads();
   double part = 0.0;
   uint32_t nchg = 0;
-  const int64_t ntile = (n + 31) >> 5;
+  const int64_t nl = LIST ? (int64_t)__builtin_amdgcn_readfirstlane((int)*lnrows) : n;  // rows to score
+  const int64_t ntile = (nl + 31) >> 5;
   const int64_t nwv = (int64_t)gridDim.x * (KM_MT / 64);
   for (int64_t t = (int64_t)blockIdx.x * (KM_MT / 64) + wv; t < ntile; t += nwv) {
     const int64_t r0 = t << 5;
-    const float* x = X + (r0 + i32 < n ? r0 + i32 : n - 1) * dim;
+    const bool in_l = r0 + i32 < nl;
+    const int64_t row = LIST ? (int64_t)lrows[in_l ? r0 + i32 : nl - 1] : (in_l ? r0 + i32 : n - 1);
+    const float* x = X + row * dim;
     float4 a[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -331,81 +403,19 @@ __global__ __launch_bounds__(KM_MT, (NQ <= 13 ? 4 : 2)) void k_km_assign_mfma(co
       const int pc = __shfl_xor(mc, 32);
       if (pm < m || (pm == m && pc < mc)) { m = pm; mc = pc; }
     }
-    const int R = i32;
     const float xr = xs;
     const uint32_t mi = (uint32_t)mc;
     int32_t old = -1;
-    const bool mine = h == 0 && r0 + R < n;
+    const bool mine = h == 0 && in_l;
     if (mine) {
-      if (changed || inc) old = label[r0 + R];
+      if (changed || inc) old = label[row];
       if (changed) nchg += old != (int32_t)mi;
-      label[r0 + R] = (int32_t)mi;
+      label[row] = (int32_t)mi;
       const float dd = fmaxf(xr + m, 0.f);
       part += (double)dd;
-      if (dist) dist[r0 + R] = dd;
+      if (dist) dist[row] = dd;
     }
-    if (sums) {
-      // rows whose vector enters a cluster's sums: every row, or (incremental) the rows whose
-      // label changed, which also leave their previous cluster; listed in LDS, lanes over dims
-      const bool in_list = mine && (!inc || old != (int32_t)mi);
-      const uint64_t bm = __ballot(in_list);
-      if (in_list) {
-        const int p = (int)mbcnt(bm);
-        labl[wv * 96 + p] = R;
-        labl[wv * 96 + 32 + p] = (int32_t)mi;
-        labl[wv * 96 + 64 + p] = inc ? old : -1;
-      }
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      const int nr = (int)__popcll(bm);
-      for (int rr = 0; rr < nr; rr += 8) {  // 8 rows' loads in flight
-        float xa[8], xb[8];
-        int cc[8], co[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int pq = rr + q < nr ? rr + q : nr - 1;
-          const int r = labl[wv * 96 + pq];
-          cc[q] = labl[wv * 96 + 32 + pq];
-          co[q] = labl[wv * 96 + 64 + pq];
-          const float* xq = X + (r0 + r) * dim;
-          xa[q] = l < dim ? xq[l] : 0.f;
-          xb[q] = l + 64 < dim ? xq[l + 64] : 0.f;
-        }
-        // exact 2^24 scaling: one f32 -> i32 conversion per value while every |x| < 128 (the
-        // product is exact and below 2^31); the general f32 -> i64 sequence only for a wave
-        // that holds a larger value
-        bool big = false;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) big |= fabsf(xa[q]) >= 128.f || fabsf(xb[q]) >= 128.f;
-        long long fa[8], fb[8];
-        if (__builtin_expect(__ballot(big) != 0, 0)) {
-#pragma unroll
-          for (int q = 0; q < 8; ++q) { fa[q] = __float2ll_rn(xa[q] * 16777216.0f); fb[q] = __float2ll_rn(xb[q] * 16777216.0f); }
-        } else {
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            fa[q] = (long long)__float2int_rn(xa[q] * 16777216.0f);
-            fb[q] = (long long)__float2int_rn(xb[q] * 16777216.0f);
-          }
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          if (rr + q >= nr) break;
-          unsigned long long* row = ls + cc[q] * dim;
-          if (l < dim) atomicAdd(&row[l], (unsigned long long)fa[q]);
-          if (l + 64 < dim) atomicAdd(&row[l + 64], (unsigned long long)fb[q]);
-          if (l == 0) atomicAdd(&lc[cc[q]], 1ull);
-          if (co[q] >= 0) {  // two's-complement deltas: the block's sums may go below zero
-            unsigned long long* orow = ls + co[q] * dim;
-            if (l < dim) atomicAdd(&orow[l], (unsigned long long)(-fa[q]));
-            if (l + 64 < dim) atomicAdd(&orow[l + 64], (unsigned long long)(-fb[q]));
-            if (l == 0) atomicAdd(&lc[co[q]], ~0ull);
-          }
-        }
-      }
-      __builtin_amdgcn_wave_barrier();  // labl is rewritten by the next tile
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    }
+    if (sums) km_move_rows(X, dim, ls, lc, labl + wv * 96, mine && (!inc || old != (int32_t)mi), row, mi, inc ? old : -1);
   }
   __syncthreads();
   if (sums) {
@@ -426,6 +436,217 @@ __global__ __launch_bounds__(KM_MT, (NQ <= 13 ? 4 : 2)) void k_km_assign_mfma(co
   }
 }
 
+// Split-precision E-step (one Lloyd step of every row): x = xh + xl and c = ch + cl in bf16 (hi and the
+// rounded rest), x.c ~ xh.ch + xh.cl + xl.ch on v_mfma_f32_32x32x16_bf16 (products exact in f32, f32
+// accumulation): |x.c - approx| <= (3 u^2 + gamma_336) sum |x_i c_i| with u = 2^-8, under 6.6e-5 |x| |c|,
+// so a score |c|^2 - 2 x.c is off by <= 1.32e-4 |x| |c|, and the f32 kernel's (k_km_assign_mfma) by
+// <= 2 gamma_128 |x||c| = 1.5e-5 |x||c| (same |c|^2 in both). A row is decided when its two smallest
+// approximate scores differ by more than twice the sum, 2.94e-4 |x| max|c|: the exact f32 step would
+// then pick the same cluster, strictly. KMS_SEP = 6e-4 keeps a 2x margin over that. Decided rows get
+// their label and sums here; the others (near ties, ~1-2 % of rows on session embeddings) are
+// listed for the exact kernel (per block in LDS, one global atomic per block). Same output layout as
+// k_km_assign_mfma: lane (i, h) ends with row i's scores of clusters (r & 3) + 8 (r >> 2) + 4 h.
+typedef __bf16 km_bf16x8 __attribute__((ext_vector_type(8)));
+constexpr float KMS_SEP = 6e-4f;
+constexpr int KMS_AMB = 1024;  // near-tie rows staged per block before they spill to the global list
+__device__ __forceinline__ uint16_t km_bf16(float f) {  // round to nearest even (finite values)
+  uint32_t u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+typedef __bf16 km_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float km_f32x2 __attribute__((ext_vector_type(2)));
+// v = hi + lo + r: hi = RN_bf16(v), lo = RN_bf16(v - hi) (v_cvt_pk_bf16_f32, round to nearest even;
+// v - hi is exact in f32), |r| <= u^2 |v|
+__device__ __forceinline__ void km_split8(const float (&v)[8], uint4& hi, uint4& lo) {
+  uint32_t hw[4], lw[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const km_f32x2 a = {v[2 * p], v[2 * p + 1]};
+    const uint32_t hu = __builtin_bit_cast(uint32_t, __builtin_convertvector(a, km_bf16x2));
+    const km_f32x2 r = {v[2 * p] - __uint_as_float(hu << 16), v[2 * p + 1] - __uint_as_float(hu & 0xFFFF0000u)};
+    hw[p] = hu;
+    lw[p] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, km_bf16x2));
+  }
+  hi = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+  lo = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+}
+
+template <int NB, int KS>
+__global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __restrict__ X, int64_t n, int dim,
+                                                             const float* __restrict__ C, const float* __restrict__ cn,
+                                                             int k, int32_t* __restrict__ label,
+                                                             unsigned long long* __restrict__ sums,
+                                                             unsigned long long* __restrict__ cnt,
+                                                             unsigned long long* __restrict__ changed,
+                                                             const int* __restrict__ gate,
+                                                             uint32_t* __restrict__ amb_rows,
+                                                             unsigned long long* __restrict__ n_amb) {
+  if (gate && __builtin_amdgcn_readfirstlane(*gate)) return;
+  extern __shared__ unsigned long long smem64[];
+  uint4* Cf = reinterpret_cast<uint4*>(smem64);                               // [NB][KS][hi, lo][64]
+  unsigned long long* ls = reinterpret_cast<unsigned long long*>(Cf + NB * KS * 2 * 64);  // k * dim sums
+  unsigned long long* lc = ls + k * dim;                                       // k counts
+  int32_t* labl = reinterpret_cast<int32_t*>(lc + k);                         // [waves][3][32]
+  float* cnl = reinterpret_cast<float*>(labl + (KM_MT / 64) * 96);             // [64]
+  uint32_t* amb = reinterpret_cast<uint32_t*>(cnl + 64);                       // [KMS_AMB]
+  __shared__ uint32_t namb;
+  __shared__ unsigned long long abase;
+  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6, h = l >> 5, i32 = l & 31;
+  // centroid fragments: lane (r, h) of block b, k-step s holds centroid 32 b + r, dims 16 s + 8 h .. + 7
+  for (int e = tid; e < NB * KS * 64; e += KM_MT) {
+    const int ll = e & 63, sb = e >> 6, s_ = sb % KS, b = sb / KS;
+    const int c = b * 32 + (ll & 31), d0 = 16 * s_ + 8 * (ll >> 5);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (c < k && d0 + j < dim) ? C[(int64_t)c * dim + d0 + j] : 0.f;
+    uint4 hi, lo;
+    km_split8(v, hi, lo);
+    Cf[(sb * 2 + 0) * 64 + ll] = hi;
+    Cf[(sb * 2 + 1) * 64 + ll] = lo;
+  }
+  if (tid < 64) cnl[tid] = cn[tid];
+  for (int i = tid; i < k * dim + k; i += KM_MT) ls[i] = 0ull;
+  if (tid == 0) namb = 0;
+  __syncthreads();
+  float c2 = l < k ? cnl[l] : 0.f;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) c2 = fmaxf(c2, __shfl_xor(c2, o));
+  const float cmax = sqrtf(c2);
+  uint32_t nchg = 0;
+  const int64_t ntile = (n + 31) >> 5;
+  const int64_t nwv = (int64_t)gridDim.x * (KM_MT / 64);
+  // the next tile's rows (and its rows' current labels) are loaded while this tile is scored
+  float4 raw[2 * KS];
+  int32_t lab_n = -1;
+  auto load = [&](int64_t tt) __attribute__((always_inline)) {
+    const int64_t rr = (tt << 5) + i32 < n ? (tt << 5) + i32 : n - 1;
+    const float* xp = X + rr * dim;
+#pragma unroll
+    for (int s_ = 0; s_ < KS; ++s_) {
+      const int d0 = 16 * s_ + 8 * h;  // dim % 4 == 0: a 16-B piece is all in or all out
+      raw[2 * s_] = d0 < dim ? *reinterpret_cast<const float4*>(xp + d0) : make_float4(0.f, 0.f, 0.f, 0.f);
+      raw[2 * s_ + 1] = d0 + 4 < dim ? *reinterpret_cast<const float4*>(xp + d0 + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    lab_n = label[rr];
+  };
+  const int64_t t_first = (int64_t)blockIdx.x * (KM_MT / 64) + wv;
+  if (t_first < ntile) load(t_first);
+  for (int64_t t = t_first; t < ntile; t += nwv) {
+    const int64_t r0 = t << 5;
+    const bool in_r = r0 + i32 < n;
+    const int64_t row = in_r ? r0 + i32 : n - 1;
+    km_bf16x8 xh[KS], xl[KS];
+    float xs = 0.f;
+#pragma unroll
+    for (int s_ = 0; s_ < KS; ++s_) {
+      const float4 p0 = raw[2 * s_], p1 = raw[2 * s_ + 1];
+      const float v[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xs += v[j] * v[j];
+      uint4 hi, lo;
+      km_split8(v, hi, lo);
+      xh[s_] = __builtin_bit_cast(km_bf16x8, hi);
+      xl[s_] = __builtin_bit_cast(km_bf16x8, lo);
+    }
+    const int32_t lab_cur = lab_n;
+    if (t + nwv < ntile) load(t + nwv);
+    xs += __shfl_xor(xs, 32);
+    km_f32x16 acc0 = {}, acc1 = {};
+#pragma unroll
+    for (int s_ = 0; s_ < KS; ++s_) {
+      const km_bf16x8 ch0 = __builtin_bit_cast(km_bf16x8, Cf[((0 * KS + s_) * 2 + 0) * 64 + l]);
+      const km_bf16x8 cl0 = __builtin_bit_cast(km_bf16x8, Cf[((0 * KS + s_) * 2 + 1) * 64 + l]);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, xh[s_], acc0, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, xl[s_], acc0, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl0, xh[s_], acc0, 0, 0, 0);
+      if (NB == 2) {
+        const km_bf16x8 ch1 = __builtin_bit_cast(km_bf16x8, Cf[((1 * KS + s_) * 2 + 0) * 64 + l]);
+        const km_bf16x8 cl1 = __builtin_bit_cast(km_bf16x8, Cf[((1 * KS + s_) * 2 + 1) * 64 + l]);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, xh[s_], acc1, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, xl[s_], acc1, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl1, xh[s_], acc1, 0, 0, 0);
+      }
+    }
+    // approximate scores |c|^2 - 2 x.c; the smallest, the lowest cluster holding it, the second smallest
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 n0 = *reinterpret_cast<const float4*>(cnl + 8 * j + 4 * h);
+      acc0[4 * j + 0] = n0.x - 2.f * acc0[4 * j + 0];
+      acc0[4 * j + 1] = n0.y - 2.f * acc0[4 * j + 1];
+      acc0[4 * j + 2] = n0.z - 2.f * acc0[4 * j + 2];
+      acc0[4 * j + 3] = n0.w - 2.f * acc0[4 * j + 3];
+      if (NB == 2) {
+        const float4 n1 = *reinterpret_cast<const float4*>(cnl + 32 + 8 * j + 4 * h);
+        acc1[4 * j + 0] = n1.x - 2.f * acc1[4 * j + 0];
+        acc1[4 * j + 1] = n1.y - 2.f * acc1[4 * j + 1];
+        acc1[4 * j + 2] = n1.z - 2.f * acc1[4 * j + 2];
+        acc1[4 * j + 3] = n1.w - 2.f * acc1[4 * j + 3];
+      }
+    }
+    float m = INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      m = fminf(m, acc0[r]);
+      if (NB == 2) m = fminf(m, acc1[r]);
+    }
+    int mc = 64;
+#pragma unroll
+    for (int r = 15; r >= 0; --r) {
+      if (NB == 2) mc = acc1[r] == m ? 32 + (r & 3) + 8 * (r >> 2) + 4 * h : mc;
+    }
+#pragma unroll
+    for (int r = 15; r >= 0; --r) mc = acc0[r] == m ? (r & 3) + 8 * (r >> 2) + 4 * h : mc;
+    {
+      const float pm = __shfl_xor(m, 32);
+      const int pc = __shfl_xor(mc, 32);
+      if (pm < m || (pm == m && pc < mc)) { m = pm; mc = pc; }
+    }
+    float m2 = INFINITY;  // smallest score of any other cluster
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int c0 = (r & 3) + 8 * (r >> 2) + 4 * h;
+      m2 = fminf(m2, c0 == mc ? INFINITY : acc0[r]);
+      if (NB == 2) m2 = fminf(m2, c0 + 32 == mc ? INFINITY : acc1[r]);
+    }
+    m2 = fminf(m2, __shfl_xor(m2, 32));
+    const bool decided = m2 - m > KMS_SEP * sqrtf(xs) * cmax;
+    const uint32_t mi = (uint32_t)mc;
+    const bool mine = h == 0 && in_r && decided;
+    int32_t old = -1;
+    if (mine) {
+      old = lab_cur;
+      nchg += old != (int32_t)mi;
+      if (old != (int32_t)mi) label[row] = (int32_t)mi;
+    }
+    // near ties: staged in LDS for the exact kernel (overflow: straight to the global list)
+    const bool tie = h == 0 && in_r && !decided;
+    const uint64_t tm = __ballot(tie);
+    if (tm) {
+      uint32_t b = 0;
+      if (l == 0) b = atomicAdd(&namb, (uint32_t)__popcll(tm));
+      b = __shfl(b, 0);
+      if (tie) {
+        const uint32_t p = b + mbcnt(tm);
+        if (p < (uint32_t)KMS_AMB) amb[p] = (uint32_t)row;
+        else amb_rows[atomicAdd(n_amb, 1ull)] = (uint32_t)row;
+      }
+    }
+    km_move_rows(X, dim, ls, lc, labl + wv * 96, mine && old != (int32_t)mi, row, mi, old);
+  }
+  __syncthreads();
+  for (int i = tid; i < k * dim; i += KM_MT)
+    if (ls[i]) atomicAdd(&sums[i], ls[i]);
+  for (int i = tid; i < k; i += KM_MT)
+    if (lc[i]) atomicAdd(&cnt[i], lc[i]);
+  const uint32_t na = namb < (uint32_t)KMS_AMB ? namb : (uint32_t)KMS_AMB;
+  if (tid == 0) abase = na ? atomicAdd(n_amb, (unsigned long long)na) : 0ull;
+  __syncthreads();
+  for (uint32_t i = tid; i < na; i += KM_MT) amb_rows[abase + i] = amb[i];
+  const uint32_t w = wave_sum(nchg);
+  if (l == 0 && w) atomicAdd(changed, (unsigned long long)w);
+}
+
 // inc: sums / cnt hold the exact sums / counts of the rows under `labels` (the previous labels) and
 // are updated by the rows whose label changes (MFMA kernel); otherwise they are accumulated from
 // scratch by every row (the caller zeroes them)
@@ -440,7 +661,7 @@ static bool km_mfma_ok(int k, int dim, const float* X, const float* C) {
 static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int64_t n, int dim, const float* C,
                             int32_t* labels, unsigned long long* sums, unsigned long long* cnt, double* inr,
                             unsigned long long* changed = nullptr, float* dist = nullptr, int inc = 0,
-                            const int* gate = nullptr) {
+                            const int* gate = nullptr, bool split = false) {
   const int KP = (k + 7) / 8 * 8;
   float *Ct, *cn;
   OH_TRY(ctx->ws.get("km_ct", (size_t)KP * dim, &Ct));
@@ -455,11 +676,40 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
     const int64_t ntile = ceil_div(n, 32);
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(ntile, KM_MT / 64),
                                                                            (int64_t)ctx->n_cu * 2));
+    // split: the split-precision pass decides (almost) every row, the exact kernel scores the near ties
+    // (incremental sums, a changed-label count and no distances: the batched Lloyd steps)
+    const char* se = getenv("OTTOHIP_KM_SPLIT");  // A/B switch, read per call
+    split = split && inc && sums && changed && !dist && !(se && !strcmp(se, "0"));
+    uint32_t* amb = nullptr;
+    unsigned long long* n_amb = nullptr;
+    if (split) {
+      OH_TRY(ctx->ws.get("km_amb", (size_t)std::max<int64_t>(n, 1), &amb));
+      OH_TRY(ctx->ws.get("km_namb", 1, &n_amb));
+      OH_HIP(hipMemsetAsync(n_amb, 0, 8, s));
+      const int KS = dim <= 112 ? 7 : 8;
+      const size_t lds2 = (size_t)NB * KS * 2 * 64 * 16 + ((size_t)k * dim + k) * 8 + (KM_MT / 64) * 96 * 4 + 64 * 4 +
+                          (size_t)KMS_AMB * 4;
+      auto sk = KS == 7 ? (NB == 1 ? k_km_assign_split<1, 7> : k_km_assign_split<2, 7>)
+                        : (NB == 1 ? k_km_assign_split<1, 8> : k_km_assign_split<2, 8>);
+      OH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(sk), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)lds2));
+      // one resident block per CU (the kernel's registers allow one 8-wave block): one round of blocks,
+      // so each block's LDS set-up and sum flush happen once
+      const unsigned sgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(ntile, KM_MT / 64), ctx->n_cu));
+      sk<<<sgrid, KM_MT, lds2, s>>>(X, n, dim, C, cn, k, labels, sums, cnt, changed, gate, amb, n_amb);
+      OH_HIP(hipGetLastError());
+    }
     auto kern = nq == 13 ? (NB == 1 ? k_km_assign_mfma<1, 13> : k_km_assign_mfma<2, 13>)
                          : (NB == 1 ? k_km_assign_mfma<1, KM_NQ> : k_km_assign_mfma<2, KM_NQ>);
+    if (split)
+      kern = nq == 13 ? (NB == 1 ? k_km_assign_mfma<1, 13, true> : k_km_assign_mfma<2, 13, true>)
+                      : (NB == 1 ? k_km_assign_mfma<1, KM_NQ, true> : k_km_assign_mfma<2, KM_NQ, true>);
     OH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)lds));
-    kern<<<grid, KM_MT, lds, s>>>(X, n, dim, nq, C, cn, k, labels, sums, cnt, inr, changed, dist, inc, gate);
+    // near ties only (about 1-2 % of the rows): a quarter of the grid, fewer block set-ups and flushes
+    const unsigned egrid = split ? (unsigned)std::max(1, ctx->n_cu / 2) : grid;
+    kern<<<egrid, KM_MT, lds, s>>>(X, n, dim, nq, C, cn, k, labels, sums, cnt, inr, changed, dist, inc, gate,
+                                   amb, n_amb);
     OH_HIP(hipGetLastError());
     return 0;
   }
@@ -964,7 +1214,10 @@ int ottohip_kmeans_lloyd_iter(ottohip_ctx* ctx, const float* X, int64_t n, int d
 // Up to max_steps Lloyd iterations with one device->host copy: each step's update kernel checks
 // sklearn's stop conditions on the device and gates the later steps. out[0..3] as lloyd_iter for the
 // last step run, out[4] steps run, out[5] stop reason (0 none, 1 no label changed, 2 shift^2 <= tol,
-// 3 empty cluster: centroids untouched, relocate then ottohip_kmeans_update).
+// 3 empty cluster: centroids untouched, relocate then ottohip_kmeans_update). Each E-step is the
+// split-precision pass plus the exact f32 kernel on its near ties (OTTOHIP_KM_SPLIT=0: the exact kernel on
+// every row; labels, sums and stop checks are identical): out[0] then holds the near ties' inertia only
+// (the run's inertia is ottohip_kmeans_inertia's).
 int ottohip_kmeans_lloyd_steps(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* centroids, int k,
                                int32_t* labels, int64_t* sums, int64_t* counts, int max_steps, double tol,
                                double* out, void* stream) {
@@ -990,7 +1243,7 @@ int ottohip_kmeans_lloyd_steps(ottohip_ctx* ctx, const float* X, int64_t n, int 
     k_km_gate_reset<<<1, 64, 0, s>>>(ctl, st);
     OH_TRY(launch_km_assign(ctx, k, s, X, n, dim, centroids, labels, reinterpret_cast<unsigned long long*>(sums),
                             reinterpret_cast<unsigned long long*>(counts), st,
-                            reinterpret_cast<unsigned long long*>(st + 1), nullptr, 1, ctl));
+                            reinterpret_cast<unsigned long long*>(st + 1), nullptr, 1, ctl, true));
     k_km_update<<<1, KM_UT, 0, s>>>(centroids, reinterpret_cast<const long long*>(sums),
                                     reinterpret_cast<const long long*>(counts), k, dim, 1, st + 2, ctl,
                                     reinterpret_cast<const unsigned long long*>(st + 1), tol);

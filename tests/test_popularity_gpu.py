@@ -71,6 +71,76 @@ def test_kmeans_lloyd_step_batches_equal_single_steps(gpu, monkeypatch):
     assert fits[0][2] == fits[1][2] and fits[0][3] == fits[1][3]
 
 
+@pytest.mark.parametrize("case", ["sessions_k50", "relocation_k9", "blocks_k33"])
+def test_kmeans_bounded_steps_equal_full_steps(gpu, monkeypatch, case):
+    """The bounded Lloyd steps (rows whose distance bounds separate keep their label unscored,
+    csrc/popularity.hip k_km_filter) give bit-identical labels, centres, inertia and iterations to
+    scoring every row each step: k = 50 on session embeddings of synthetic sessions (the config-5
+    clustering; runs go to max_iter), duplicated rows with empty clusters relocated between steps,
+    and k = 33 (the last bound group holds one cluster)."""
+    from otto_recommender_amd import popularity as gp
+    rng = np.random.default_rng(11)
+    if case == "sessions_k50":
+        ev = synth.generate(40_000, first_session=4242)
+        words = np.unique(ev.aid)
+        emb = synth.embeddings(len(words), seed=1)
+        X = gp.compute_sessions_embeddings(ev.session_offsets, ev.aid, ev.ts, ev.type, words, emb).cpu().numpy()
+        k, n_init = 50, 2
+    elif case == "relocation_k9":
+        centers = rng.normal(scale=2, size=(9, 100))
+        X = (centers[rng.integers(0, 9, 30000)] + rng.normal(size=(30000, 100))).astype(np.float32)
+        X[:4000] = X[0]
+        k, n_init = 9, 10
+    else:
+        centers = rng.normal(scale=3, size=(40, 100))
+        X = (centers[rng.integers(0, 40, 20000)] + rng.normal(size=(20000, 100))).astype(np.float32)
+        k, n_init = 33, 3
+    fits = []
+    for bounds in ("0", "1"):
+        monkeypatch.setenv("OTTOHIP_KM_BOUNDS", bounds)
+        km = gp.KMeans(n_clusters=k, random_state=42, n_init=n_init).fit(X)
+        fits.append((km.labels_.cpu().numpy(), km.cluster_centers_.cpu().numpy(), km.inertia_, km.n_iter_))
+    np.testing.assert_array_equal(fits[0][0], fits[1][0])
+    np.testing.assert_array_equal(fits[0][1], fits[1][1])
+    assert fits[0][2] == fits[1][2] and fits[0][3] == fits[1][3]
+
+
+@pytest.mark.parametrize("case", ["sessions_k50", "relocation_k9", "blocks_k33", "one_block_k20"])
+def test_kmeans_split_precision_steps_equal_exact_steps(gpu, monkeypatch, case):
+    """The split-precision E-step (bf16 hi/lo MFMA pass deciding every row whose two best scores are
+    separated beyond the error bound, the exact f32 kernel on the near ties; csrc/popularity.hip
+    k_km_assign_split) gives bit-identical labels, centres, inertia and iterations to the exact f32
+    kernel on every row: k = 50 on session embeddings of synthetic sessions (the config-5 clustering,
+    runs reach max_iter), duplicated rows with empty clusters relocated, k = 33 and k = 20."""
+    from otto_recommender_amd import popularity as gp
+    rng = np.random.default_rng(11)
+    if case == "sessions_k50":
+        ev = synth.generate(40_000, first_session=4242)
+        words = np.unique(ev.aid)
+        emb = synth.embeddings(len(words), seed=1)
+        X = gp.compute_sessions_embeddings(ev.session_offsets, ev.aid, ev.ts, ev.type, words, emb).cpu().numpy()
+        k, n_init = 50, 2
+    elif case == "relocation_k9":
+        centers = rng.normal(scale=2, size=(9, 100))
+        X = (centers[rng.integers(0, 9, 30000)] + rng.normal(size=(30000, 100))).astype(np.float32)
+        X[:4000] = X[0]
+        k, n_init = 9, 10
+    else:
+        k = 33 if case == "blocks_k33" else 20
+        centers = rng.normal(scale=3, size=(40, 100))
+        X = (centers[rng.integers(0, 40, 20000)] + rng.normal(size=(20000, 100))).astype(np.float32)
+        n_init = 3
+    fits = []
+    for split in ("0", "1"):  # the exact kernel on every row; the split pass + the exact kernel on near ties
+        monkeypatch.setenv("OTTOHIP_KM_SPLIT", split)
+        km = gp.KMeans(n_clusters=k, random_state=42, n_init=n_init).fit(X)
+        fits.append((km.labels_.cpu().numpy(), km.cluster_centers_.cpu().numpy(), km.inertia_, km.n_iter_))
+    for f in fits[1:]:
+        np.testing.assert_array_equal(fits[0][0], f[0])
+        np.testing.assert_array_equal(fits[0][1], f[1])
+        assert fits[0][2] == f[2] and fits[0][3] == f[3]
+
+
 def test_kmeans_empty_cluster_relocation(gpu):
     """a third of the rows identical: seeds collide, clusters empty out and are relocated to the
     farthest rows (_relocate_empty_clusters_dense)"""
