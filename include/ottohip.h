@@ -314,7 +314,14 @@ int ottohip_kmeans_lloyd_steps(ottohip_ctx* ctx, const float* X, int64_t n, int 
  * MFMA products, a rigorous error bound) that decides every row whose two best scores are separated
  * beyond the bound, plus the exact f32 kernel on the remaining near ties: labels, sums and stop
  * checks are bit-identical to the exact kernel on every row (out[0] then covers the near ties only).
- * (OTTOHIP_KM_SPLIT=0: the exact kernel on every row). */
+ * (OTTOHIP_KM_SPLIT=0: the exact kernel on every row).
+ * Rows are skipped by distance bounds carried across steps and calls (Hamerly's upper bound to the
+ * own centre and one lower bound to all others, moved by each centre's shift since the bounds were
+ * set): a row whose bounds separate beyond the exact kernel's error keeps its label unscored, the
+ * same label the exact kernel gives it. The bounds belong to (X, labels, n, dim, k) of the previous
+ * lloyd_steps call on the context; a row with label -1 (a new run) is always scored, and every other
+ * kmeans entry point that writes labels discards them. Between calls, change labels only through the
+ * library or by resetting them to -1. (OTTOHIP_KM_BOUNDS=0: every row scored each step.) */
 int ottohip_kmeans_farthest(ottohip_ctx* ctx, const float* X, int64_t n, int dim, const float* centroids,
                             const int32_t* labels, int m, int64_t* rows, float* d2, void* stream);
 int ottohip_kmeans_relocate(ottohip_ctx* ctx, int64_t* sums, int64_t* counts, int k, int dim, const float* vecs,

@@ -520,6 +520,14 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
         unsigned long long sw = 0, mx = 0;
         for (auto& t : tv) { sw += t.len; mx = std::max<unsigned long long>(mx, t.len); }
         fprintf(stderr, " %llu(max %llu)", sw, mx);
+        if (c == N_SORT + 1 && !tv.empty()) {  // split tasks: words by log2(len) class
+          unsigned long long hw[40] = {}, hn[40] = {};
+          for (auto& t : tv) { const int b = 63 - __builtin_clzll((unsigned long long)t.len | 1ull); hw[b] += t.len; ++hn[b]; }
+          fprintf(stderr, " [split by log2 len:");
+          for (int b = 0; b < 40; ++b)
+            if (hn[b]) fprintf(stderr, " 2^%d:%llu tasks/%llu words", b, hn[b], hw[b]);
+          fprintf(stderr, "]");
+        }
       }
       fprintf(stderr, "\n");
     }

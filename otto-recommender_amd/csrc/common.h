@@ -116,6 +116,13 @@ struct Ctx {
     return (int)phases.size() - 1;
   }
   void end(int id, hipStream_t s) { if (id >= 0) hipEventRecord(phases[id].b, s); }
+  // KMeans distance bounds (batched Lloyd steps): valid for the rows of (X, labels, n, dim, k) of the
+  // last ottohip_kmeans_lloyd_steps call; every other entry point that writes labels clears km_bvalid
+  const void* km_bX = nullptr;
+  const void* km_bL = nullptr;
+  int64_t km_bn = -1;
+  int km_bdim = 0, km_bk = 0;
+  bool km_bvalid = false;
 };
 
 inline int bits_for(uint64_t n_values) {  // bits needed to store values in [0, n_values)

@@ -472,7 +472,126 @@ __device__ __forceinline__ void km_split8(const float (&v)[8], uint4& hi, uint4&
   lo = make_uint4(lw[0], lw[1], lw[2], lw[3]);
 }
 
-template <int NB, int KS>
+// Distance bounds across Lloyd steps (Hamerly's single lower bound), so a step scores only the rows
+// whose label could change. Per row: ub >= |x - c_a| (a = its label) and lb <= min_{j != a} |x - c_j|,
+// both for the centres Cp the bounds were last made valid for. A step first takes
+// delta_j >= |C_j - Cp_j| (k_km_delta, then Cp = C), so by the triangle inequality u = ub + delta_a and
+// l = lb - max_{j != a} delta_j bound the distances to the new centres C. The exact f32 kernel
+// (k_km_assign_mfma) scores s_j = |c_j|^2 - 2 x.c_j within 2e-5 cmax (|x| + cmax) (its MFMA dot,
+// the stored |c|^2 and two roundings; cmax = max |c_j|), so it keeps label a whenever
+// l^2 - u^2 > 4e-5 cmax (|x| + cmax); with |x| <= u + cmax the filter asks for
+// (l - u)(l + u) > KMB_SKIP cmax (u + 2 cmax), KMB_SKIP = 2e-4 (5x margin). Such rows keep their
+// label and sums (nothing to move); the others are listed for the split-precision pass, which
+// rebuilds their bounds from its approximate scores (error within 2e-4 cmax (|x| + cmax) there, so
+// u^2 <= m + |x|^2 + e and l^2 >= m2 + |x|^2 - e with m, m2 the two smallest scores), and near ties
+// get lb = 0 (scored again next step). Every bound is rounded outwards (relative 2^-20 / 1e-6).
+constexpr float KMB_SKIP = 2e-4f;
+constexpr float KMB_ERR = 2e-4f;
+// dl: [0, 64) delta_j, [64] largest delta, [65] second largest, [66] its cluster (as float), [67] cmax
+__global__ void k_km_delta(const float* __restrict__ C, float* __restrict__ Cp, const float* __restrict__ cn,
+                           int k, int dim, int force, float* __restrict__ dl, const int* __restrict__ gate,
+                           unsigned long long* __restrict__ n_eval) {
+  if (gate && __builtin_amdgcn_readfirstlane(*gate)) return;  // stopped: Cp stays the bounds' centres
+  const int j = threadIdx.x;  // one block of 64 threads
+  float d = 0.f;
+  if (j < k) {
+    double s = 0.0;
+    for (int i = 0; i < dim; ++i) {
+      const double t = (double)C[(int64_t)j * dim + i] - (double)Cp[(int64_t)j * dim + i];
+      s += t * t;
+    }
+    d = force ? INFINITY : (float)(sqrt(s) * (1.0 + 1e-6));
+  }
+  __syncthreads();  // every read of Cp before it is overwritten
+  if (j < k)
+    for (int i = 0; i < dim; ++i) Cp[(int64_t)j * dim + i] = C[(int64_t)j * dim + i];
+  // largest and second largest delta (ties: any cluster holding the largest, the second equals it)
+  float m1 = d;
+  int a1 = j;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float pm = __shfl_xor(m1, o);
+    const int pa = __shfl_xor(a1, o);
+    if (pm > m1 || (pm == m1 && pa < a1)) { m1 = pm; a1 = pa; }
+  }
+  float m2 = j == a1 ? 0.f : d;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m2 = fmaxf(m2, __shfl_xor(m2, o));
+  float c2 = j < k ? cn[j] : 0.f;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) c2 = fmaxf(c2, __shfl_xor(c2, o));
+  dl[j] = d;
+  if (j == 0) {
+    dl[64] = m1;
+    dl[65] = m2;
+    dl[66] = (float)a1;
+    dl[67] = sqrtf(c2) * 1.000001f;
+    *n_eval = 0;
+  }
+}
+
+// rows whose bounds leave their label certain keep it (bounds moved to the new centres); the
+// others are listed in row order: a block takes KMF_PER * 256 consecutive rows, one device atomic
+// per block reserves its list range
+constexpr int KMF_PER = 16;
+__global__ __launch_bounds__(256) void k_km_filter(int64_t n, int k, const int32_t* __restrict__ label,
+                                                   float* __restrict__ ub, float* __restrict__ lb,
+                                                   const float* __restrict__ dl, uint32_t* __restrict__ erows,
+                                                   unsigned long long* __restrict__ n_eval,
+                                                   const int* __restrict__ gate) {
+  if (gate && __builtin_amdgcn_readfirstlane(*gate)) return;
+  __shared__ float sd[68];
+  __shared__ uint32_t wc[KMF_PER * 4];
+  __shared__ unsigned long long base;
+  if (threadIdx.x < 68) sd[threadIdx.x] = dl[threadIdx.x];
+  __syncthreads();
+  const float d1 = sd[64], d2 = sd[65], cmax = sd[67];
+  const int a1 = (int)sd[66];
+  const int wv = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * (KMF_PER * 256);
+  uint32_t evm = 0;  // bit j: row r0 + j * 256 + tid is scored
+#pragma unroll 4
+  for (int j = 0; j < KMF_PER; ++j) {
+    const int64_t i = r0 + j * 256 + threadIdx.x;
+    bool ev = false;
+    if (i < n) {
+      const int32_t a = label[i];
+      if (a < 0 || a >= k) {
+        ev = true;
+      } else {
+        const float u = (ub[i] + sd[a]) * (1.f + 0x1p-20f);
+        const float l = (lb[i] - (a == a1 ? d2 : d1)) * (1.f - 0x1p-20f);
+        if (l > u && (l - u) * (l + u) > KMB_SKIP * cmax * (u + 2.f * cmax)) {
+          ub[i] = u;
+          lb[i] = l;
+        } else {
+          ev = true;
+        }
+      }
+    }
+    evm |= ev ? (1u << j) : 0u;
+    const uint64_t m = __ballot(ev);
+    if (lane_id() == 0) wc[j * 4 + wv] = (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {  // exclusive scan of the (row step, wave) counts, one reservation
+    const uint32_t c = wc[threadIdx.x];
+    const uint32_t incl = wave_incl_scan(c);
+    wc[threadIdx.x] = incl - c;
+    if (threadIdx.x == 63) base = incl ? atomicAdd(n_eval, (unsigned long long)incl) : 0ull;
+  }
+  __syncthreads();
+  const unsigned long long b0 = base;
+#pragma unroll 4
+  for (int j = 0; j < KMF_PER; ++j) {
+    const bool ev = (evm >> j) & 1u;
+    const uint64_t m = __ballot(ev);
+    if (ev) erows[b0 + wc[j * 4 + wv] + mbcnt(m)] = (uint32_t)(r0 + j * 256 + threadIdx.x);
+  }
+}
+
+// BL: score the rows erows[0, *n_eval) (k_km_filter's list) and rebuild their bounds
+template <int NB, int KS, bool BL = false>
 __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __restrict__ X, int64_t n, int dim,
                                                              const float* __restrict__ C, const float* __restrict__ cn,
                                                              int k, int32_t* __restrict__ label,
@@ -481,7 +600,11 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
                                                              unsigned long long* __restrict__ changed,
                                                              const int* __restrict__ gate,
                                                              uint32_t* __restrict__ amb_rows,
-                                                             unsigned long long* __restrict__ n_amb) {
+                                                             unsigned long long* __restrict__ n_amb,
+                                                             const uint32_t* __restrict__ erows = nullptr,
+                                                             const unsigned long long* __restrict__ n_eval = nullptr,
+                                                             float* __restrict__ ub = nullptr,
+                                                             float* __restrict__ lb = nullptr) {
   if (gate && __builtin_amdgcn_readfirstlane(*gate)) return;
   extern __shared__ unsigned long long smem64[];
   uint4* Cf = reinterpret_cast<uint4*>(smem64);                               // [NB][KS][hi, lo][64]
@@ -514,13 +637,17 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
   for (int o = 32; o >= 1; o >>= 1) c2 = fmaxf(c2, __shfl_xor(c2, o));
   const float cmax = sqrtf(c2);
   uint32_t nchg = 0;
-  const int64_t ntile = (n + 31) >> 5;
+  const int64_t nl = BL ? (int64_t)__builtin_amdgcn_readfirstlane((int)*n_eval) : n;  // rows to score
+  const int64_t ntile = (nl + 31) >> 5;
   const int64_t nwv = (int64_t)gridDim.x * (KM_MT / 64);
   // the next tile's rows (and its rows' current labels) are loaded while this tile is scored
   float4 raw[2 * KS];
   int32_t lab_n = -1;
+  int64_t row_n = 0;
   auto load = [&](int64_t tt) __attribute__((always_inline)) {
-    const int64_t rr = (tt << 5) + i32 < n ? (tt << 5) + i32 : n - 1;
+    const int64_t ri = (tt << 5) + i32 < nl ? (tt << 5) + i32 : nl - 1;
+    const int64_t rr = BL ? (int64_t)erows[ri] : ri;
+    row_n = rr;
     const float* xp = X + rr * dim;
 #pragma unroll
     for (int s_ = 0; s_ < KS; ++s_) {
@@ -534,8 +661,8 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
   if (t_first < ntile) load(t_first);
   for (int64_t t = t_first; t < ntile; t += nwv) {
     const int64_t r0 = t << 5;
-    const bool in_r = r0 + i32 < n;
-    const int64_t row = in_r ? r0 + i32 : n - 1;
+    const bool in_r = r0 + i32 < nl;
+    const int64_t row = row_n;
     km_bf16x8 xh[KS], xl[KS];
     float xs = 0.f;
 #pragma unroll
@@ -611,6 +738,12 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
     }
     m2 = fminf(m2, __shfl_xor(m2, 32));
     const bool decided = m2 - m > KMS_SEP * sqrtf(xs) * cmax;
+    if (BL && h == 0 && in_r) {  // the row's bounds for these centres (near ties: none, lb = 0)
+      const float cm = cmax * 1.000001f;
+      const float e = KMB_ERR * cm * (sqrtf(xs) * 1.0001f + cm);
+      ub[row] = decided ? sqrtf(fmaxf(m + xs * 1.00001f + e, 0.f)) * 1.000001f : 0.f;
+      lb[row] = decided ? sqrtf(fmaxf(m2 + xs * 0.99999f - e, 0.f)) * 0.999999f : 0.f;
+    }
     const uint32_t mi = (uint32_t)mc;
     const bool mine = h == 0 && in_r && decided;
     int32_t old = -1;
@@ -657,11 +790,18 @@ static bool km_mfma_ok(int k, int dim, const float* X, const float* C) {
          ((uintptr_t)C & 15) == 0;
 }
 
+// distance bounds in the batched Lloyd steps (OTTOHIP_KM_BOUNDS=0 / OTTOHIP_KM_SPLIT=0: A/B switches, read per call)
+static bool km_bounds_on(int64_t n) {
+  const char* be = getenv("OTTOHIP_KM_BOUNDS");
+  const char* se = getenv("OTTOHIP_KM_SPLIT");
+  return n <= 0xFFFFFFFFll && !(be && !strcmp(be, "0")) && !(se && !strcmp(se, "0"));
+}
+
 // gate (MFMA kernel only): device flag, nonzero = skip (batched Lloyd steps after convergence)
 static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int64_t n, int dim, const float* C,
                             int32_t* labels, unsigned long long* sums, unsigned long long* cnt, double* inr,
                             unsigned long long* changed = nullptr, float* dist = nullptr, int inc = 0,
-                            const int* gate = nullptr, bool split = false) {
+                            const int* gate = nullptr, bool split = false, int bounds = -1) {
   const int KP = (k + 7) / 8 * 8;
   float *Ct, *cn;
   OH_TRY(ctx->ws.get("km_ct", (size_t)KP * dim, &Ct));
@@ -689,14 +829,47 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
       const int KS = dim <= 112 ? 7 : 8;
       const size_t lds2 = (size_t)NB * KS * 2 * 64 * 16 + ((size_t)k * dim + k) * 8 + (KM_MT / 64) * 96 * 4 + 64 * 4 +
                           (size_t)KMS_AMB * 4;
+      // bounds >= 0 (batched steps): skip the rows whose distance bounds keep their label; 1 = the
+      // bounds are not valid for these rows (every row scored, bounds rebuilt)
+      const bool bl = bounds >= 0 && km_bounds_on(n);
       auto sk = KS == 7 ? (NB == 1 ? k_km_assign_split<1, 7> : k_km_assign_split<2, 7>)
                         : (NB == 1 ? k_km_assign_split<1, 8> : k_km_assign_split<2, 8>);
+      if (bl)
+        sk = KS == 7 ? (NB == 1 ? k_km_assign_split<1, 7, true> : k_km_assign_split<2, 7, true>)
+                     : (NB == 1 ? k_km_assign_split<1, 8, true> : k_km_assign_split<2, 8, true>);
       OH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(sk), hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)lds2));
       // one resident block per CU (the kernel's registers allow one 8-wave block): one round of blocks,
       // so each block's LDS set-up and sum flush happen once
       const unsigned sgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(ntile, KM_MT / 64), ctx->n_cu));
-      sk<<<sgrid, KM_MT, lds2, s>>>(X, n, dim, C, cn, k, labels, sums, cnt, changed, gate, amb, n_amb);
+      if (bl) {
+        float *ub, *lb, *cp, *dl;
+        uint32_t* erows;
+        unsigned long long* n_eval;
+        OH_TRY(ctx->ws.get("km_ub", (size_t)n, &ub));
+        OH_TRY(ctx->ws.get("km_lb", (size_t)n, &lb));
+        OH_TRY(ctx->ws.get("km_cp", (size_t)k * dim, &cp));
+        OH_TRY(ctx->ws.get("km_dl", 68, &dl));
+        OH_TRY(ctx->ws.get("km_erows", (size_t)n, &erows));
+        OH_TRY(ctx->ws.get("km_neval", 1, &n_eval));
+        k_km_delta<<<1, 64, 0, s>>>(C, cp, cn, k, dim, bounds, dl, gate, n_eval);
+        const unsigned fgrid = (unsigned)std::max<int64_t>(1, ceil_div(n, KMF_PER * 256));
+        k_km_filter<<<fgrid, 256, 0, s>>>(n, k, labels, ub, lb, dl, erows, n_eval, gate);
+        static const bool bdbg = getenv("OTTOHIP_KM_BDBG") != nullptr;  // rows scored per step (debugging aid)
+        if (bdbg) {
+          unsigned long long ne = 0;
+          float dh[68];
+          OH_TRY(d2h(&ne, n_eval, 1, s));
+          OH_TRY(d2h(dh, dl, 68, s));
+          fprintf(stderr, "[ottohip] kmeans bounds: %llu of %lld rows scored (force %d, delta max %.4g / %.4g, cmax %.4g)\n",
+                  ne, (long long)n, bounds, dh[64], dh[65], dh[67]);
+        }
+        sk<<<(unsigned)ctx->n_cu, KM_MT, lds2, s>>>(X, n, dim, C, cn, k, labels, sums, cnt, changed, gate, amb, n_amb,
+                                                    erows, n_eval, ub, lb);
+      } else {
+        sk<<<sgrid, KM_MT, lds2, s>>>(X, n, dim, C, cn, k, labels, sums, cnt, changed, gate, amb, n_amb, nullptr, nullptr,
+                                     nullptr, nullptr);
+      }
       OH_HIP(hipGetLastError());
     }
     auto kern = nq == 13 ? (NB == 1 ? k_km_assign_mfma<1, 13> : k_km_assign_mfma<2, 13>)
@@ -1094,6 +1267,7 @@ int ottohip_kmeans_step(ottohip_ctx* ctx, const float* X, int64_t n, int dim, fl
     set_error("kmeans_step: k * dim too large for LDS"); return OTTOHIP_ELIMIT;
   }
   hipStream_t s = S(stream);
+  ctx->km_bvalid = false;  // labels written outside the batched steps: their distance bounds are stale
   OH_HIP(hipSetDevice(ctx->device));
   unsigned long long* sums;
   unsigned long long* cnt;
@@ -1141,6 +1315,7 @@ int ottohip_kmeans_partial(ottohip_ctx* ctx, const float* X, int64_t n, int dim,
   }
   if (((size_t)k * dim + k) * 8 > 65536) { set_error("kmeans_partial: k * dim too large for LDS"); return OTTOHIP_ELIMIT; }
   hipStream_t s = S(stream);
+  ctx->km_bvalid = false;  // labels written outside the batched steps: their distance bounds are stale
   OH_HIP(hipSetDevice(ctx->device));
   double* st;  // [inertia, changed]
   OH_TRY(ctx->ws.get("km_stats", 4, &st));
@@ -1189,6 +1364,7 @@ int ottohip_kmeans_lloyd_iter(ottohip_ctx* ctx, const float* X, int64_t n, int d
   }
   if (((size_t)k * dim + k) * 8 > 65536) { set_error("kmeans_lloyd_iter: k * dim too large for LDS"); return OTTOHIP_ELIMIT; }
   hipStream_t s = S(stream);
+  ctx->km_bvalid = false;  // labels written outside the batched steps: their distance bounds are stale
   OH_HIP(hipSetDevice(ctx->device));
   double* st;  // [inertia, changed, shift, empty]
   OH_TRY(ctx->ws.get("km_stats", 4, &st));
@@ -1239,11 +1415,17 @@ int ottohip_kmeans_lloyd_steps(ottohip_ctx* ctx, const float* X, int64_t n, int 
   OH_TRY(ctx->ws.get("km_stats", 4, &st));
   OH_TRY(ctx->ws.get("km_ctl", 2, &ctl));
   OH_HIP(hipMemsetAsync(ctl, 0, 2 * sizeof(int), s));
+  // the distance bounds carry over from the previous call on the same rows and labels (a new run
+  // resets its labels to -1, which scores those rows); otherwise the first step rebuilds them
+  const bool bvalid = ctx->km_bvalid && ctx->km_bX == X && ctx->km_bL == labels && ctx->km_bn == n &&
+                      ctx->km_bdim == dim && ctx->km_bk == k;
+  ctx->km_bvalid = false;
   for (int i = 0; i < max_steps; ++i) {
     k_km_gate_reset<<<1, 64, 0, s>>>(ctl, st);
     OH_TRY(launch_km_assign(ctx, k, s, X, n, dim, centroids, labels, reinterpret_cast<unsigned long long*>(sums),
                             reinterpret_cast<unsigned long long*>(counts), st,
-                            reinterpret_cast<unsigned long long*>(st + 1), nullptr, 1, ctl, true));
+                            reinterpret_cast<unsigned long long*>(st + 1), nullptr, 1, ctl, true,
+                            (i == 0 && !bvalid) ? 1 : 0));
     k_km_update<<<1, KM_UT, 0, s>>>(centroids, reinterpret_cast<const long long*>(sums),
                                     reinterpret_cast<const long long*>(counts), k, dim, 1, st + 2, ctl,
                                     reinterpret_cast<const unsigned long long*>(st + 1), tol);
@@ -1253,6 +1435,8 @@ int ottohip_kmeans_lloyd_steps(ottohip_ctx* ctx, const float* X, int64_t n, int 
   int c2[2];
   OH_TRY(d2h(h, st, 4, s));
   OH_TRY(d2h(c2, ctl, 2, s));
+  ctx->km_bX = X; ctx->km_bL = labels; ctx->km_bn = n; ctx->km_bdim = dim; ctx->km_bk = k;
+  ctx->km_bvalid = km_bounds_on(n);
   unsigned long long c, e;
   memcpy(&c, &h[1], 8);
   memcpy(&e, &h[3], 8);
@@ -1373,6 +1557,7 @@ int ottohip_kmeans_assign(ottohip_ctx* ctx, const float* X, int64_t n, int dim, 
   }
 
   hipStream_t s = S(stream);
+  ctx->km_bvalid = false;  // labels written outside the batched steps: their distance bounds are stale
   double* inr;
   OH_TRY(ctx->ws.get("km_inertia", 1, &inr));
   OH_HIP(hipMemsetAsync(inr, 0, 8, s));
