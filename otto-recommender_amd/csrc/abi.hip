@@ -323,8 +323,21 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
     F.poff = nullptr; F.poff32 = nullptr;
     if (F.P < (1ull << 32) && !(p32env && !strcmp(p32env, "0"))) {
       OH_TRY(ws.get("poff32", (size_t)E, &F.poff32));
-      k_rows_tile<<<(unsigned)nb, RT_T, 0, s>>>(rks, poss, F.cnt, E, kmask, INV, cshift, boff, nullptr, F.poff32, 0u,
-                                                0xFFFFFFFFu, 1, F.row_key, F.row_begin);
+      // the offsets leave the tile pass in sorted order (coalesced), one radix pass partitions the
+      // (position, offset) pairs by the positions' top 8 bits, and the final scatter writes one
+      // 1/256 slice of poff32 at a time (OTTOHIP_POFF_PART=0: the tile pass scatters directly)
+      static const char* ppenv = getenv("OTTOHIP_POFF_PART");  // A/B switch
+      if (!(ppenv && !strcmp(ppenv, "0")) && E > 4096) {
+        uint32_t* rkA = rks == rk ? rk2 : rk;  // the sort's idle pair
+        uint32_t* posA = poss == pos ? pos2 : pos;
+        k_rows_tile<<<(unsigned)nb, RT_T, 0, s>>>(rks, poss, F.cnt, E, kmask, INV, cshift, boff, nullptr, F.poff32, 0u,
+                                                  0xFFFFFFFFu, 1, F.row_key, F.row_begin, rkA);
+        OH_TRY(radix_pass(ctx, poss, rkA, posA, rks, E, std::max(0, bits_for((uint64_t)E) - 8), s));
+        k_poff_scatter<<<grid_for(E), 256, 0, s>>>(posA, rks, E, F.poff32);
+      } else {
+        k_rows_tile<<<(unsigned)nb, RT_T, 0, s>>>(rks, poss, F.cnt, E, kmask, INV, cshift, boff, nullptr, F.poff32, 0u,
+                                                  0xFFFFFFFFu, 1, F.row_key, F.row_begin);
+      }
     } else {
       OH_TRY(ws.get("poff", (size_t)E, &F.poff));
       k_rows_tile<<<(unsigned)nb, RT_T, 0, s>>>(rks, poss, F.cnt, E, kmask, INV, cshift, boff, F.poff, nullptr, 0u, 0u,

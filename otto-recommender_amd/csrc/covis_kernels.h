@@ -615,7 +615,8 @@ __global__ __launch_bounds__(RT_T) void k_rows_tile(const uint32_t* __restrict__
                                                     uint32_t INV, int shift, const uint64_t* __restrict__ offs,
                                                     uint64_t* __restrict__ poff, uint32_t* __restrict__ poff32,
                                                     uint32_t plo, uint32_t pw, int write_rows,
-                                                    uint32_t* __restrict__ row_key, uint64_t* __restrict__ row_begin) {
+                                                    uint32_t* __restrict__ row_key, uint64_t* __restrict__ row_begin,
+                                                    uint32_t* __restrict__ wsorted = nullptr) {
   const int64_t base = (int64_t)blockIdx.x * RT_TILE + (int64_t)threadIdx.x * RT_I;
   uint64_t x[RT_I];
   uint32_t key[RT_I];
@@ -636,10 +637,12 @@ __global__ __launch_bounds__(RT_T) void k_rows_tile(const uint32_t* __restrict__
   for (int k = 0; k < w; ++k) run += ws[k];
 #pragma unroll
   for (int i = 0; i < RT_I; ++i) {
+    if (wsorted && base + i < n) wsorted[base + i] = key[i] != INV ? (uint32_t)(run >> 24) : 0u;  // sorted order
     if (key[i] != INV) {
       const uint64_t woff = run >> 24;
       const uint32_t ps = poss[base + i];
-      if (poff32) {
+      if (wsorted) {
+      } else if (poff32) {
         if (ps - plo < pw) poff32[ps] = (uint32_t)woff;
       } else {
         poff[ps] = woff;
@@ -652,6 +655,15 @@ __global__ __launch_bounds__(RT_T) void k_rows_tile(const uint32_t* __restrict__
     }
     run += x[i];
   }
+}
+
+// the word offsets in event order from (position, offset) pairs already partitioned by the positions'
+// high bits (k_rows_tile's wsorted + one radix pass): each pass of the grid writes into a few MB of
+// the destination at a time, so the 4-B writes merge in the caches instead of one random line each
+__global__ void k_poff_scatter(const uint32_t* __restrict__ pos, const uint32_t* __restrict__ woff, int64_t n,
+                               uint32_t* __restrict__ poff32) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) poff32[pos[k]] = woff[k];
 }
 
 // multi-GPU layout: row keys become (owner(aid), type, aid) so every owner's rows and words

@@ -13,4 +13,7 @@ int exclusive_scan_u64(Ctx* ctx, const uint64_t* in, uint64_t* out, int64_t n, u
 // instead of reading vals (vals still provides the buffer)
 int radix_sort_pairs(Ctx* ctx, uint32_t*& keys, uint32_t*& vals, uint32_t* keys_alt, uint32_t* vals_alt,
                      int64_t n, int bits, hipStream_t s, bool iota_vals = false);
+// one stable 8-bit pass on digit (key >> shift) & 255
+int radix_pass(Ctx* ctx, const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout, int64_t n,
+               int shift, hipStream_t s);
 }  // namespace ottohip

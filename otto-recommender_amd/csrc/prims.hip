@@ -202,6 +202,23 @@ __global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict_
   }
 }
 
+// one stable 8-bit pass on digit (key >> shift) & 255: (kin, vin) -> (kout, vout)
+int radix_pass(Ctx* ctx, const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout, int64_t n,
+               int shift, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (n >= ((int64_t)1 << 32)) { set_error("radix_pass: n=%lld too large", (long long)n); return OTTOHIP_ELIMIT; }
+  const int nb = (int)ceil_div(n, RS_BLOCK);
+  uint32_t* hist; uint64_t* gofs;
+  OH_TRY(ctx->ws.get("rs_hist", (size_t)nb * 256, &hist));
+  OH_TRY(ctx->ws.get("rs_gofs", (size_t)nb * 256, &gofs));
+  k_rs_hist<<<nb, RS_T, 0, s>>>(kin, n, shift, hist, nb);
+  OH_HIP(hipGetLastError());
+  OH_TRY(exclusive_scan_u32(ctx, hist, gofs, (int64_t)nb * 256, nullptr, s));
+  k_rs_scatter<<<nb, RS_T, 0, s>>>(kin, vin, kout, vout, n, shift, gofs, nb, 0);
+  OH_HIP(hipGetLastError());
+  return 0;
+}
+
 int radix_sort_pairs(Ctx* ctx, uint32_t*& keys, uint32_t*& vals, uint32_t* keys_alt, uint32_t* vals_alt,
                      int64_t n, int bits, hipStream_t s, bool iota_vals) {
   if (n <= 1 || bits <= 0) {  // nothing to sort; generated values still have to be written
