@@ -550,6 +550,20 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     // rewritten by the next level's classify, which waits for them (ev_join)
     hipStream_t ss = s2 ? s2 : s;
     if (s2) { OH_HIP(hipEventRecord(ctx->ev_fork, s)); OH_HIP(hipStreamWaitEvent(s2, ctx->ev_fork, 0)); }
+    // OTTOHIP_HASH_FIRST=1 (A/B switch): the level's LDS-hash leaves are queued before its register
+    // sorts, so their few long-running blocks take CU slots before the sorts' many short ones
+    static const bool hash_first = getenv("OTTOHIP_HASH_FIRST") && !strcmp(getenv("OTTOHIP_HASH_FIRST"), "1");
+    const bool hf = hash_first && nlist[N_SORT] != 0;
+    auto launch_hash = [&]() {
+      const unsigned hg = (unsigned)std::min<uint64_t>(nlist[N_SORT], (uint64_t)agg_grid);
+      if (FOon)
+        k_agg_hash<true><<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], w0, w1, row_key, R, Lt, n_rules, O,
+                                              TL.split, lcount + N_SORT + 1, fo);
+      else
+        k_agg_hash<<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], w0, w1, row_key, R, Lt, n_rules, O, TL.split,
+                                        lcount + N_SORT + 1, fo);
+    };
+    if (hf) launch_hash();
 #define OH_SORT(c, M)                                                                                        \
     if (nlist[c]) {                                                                                          \
       const unsigned g_ = (unsigned)std::min<uint64_t>(ceil_div((int64_t)nlist[c], 4), sgrid);              \
@@ -564,18 +578,12 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
 #undef OH_SORT
     if (s2) OH_HIP(hipEventRecord(ctx->ev_join[level & 1], s2));
     if (nlist[N_SORT]) {  // tasks that overflow the LDS table are appended to the split list
-      const unsigned hg = (unsigned)std::min<uint64_t>(nlist[N_SORT], (uint64_t)agg_grid);
-      static const bool hprof = getenv("OTTOHIP_HASH_PROF") != nullptr;  // per-task profile (debugging aid)
+      static const bool hprof = getenv("OTTOHIP_HASH_PROF") != nullptr && !hash_first;  // per-task profile (debugging aid)
       if (hprof) {
         if ((rc = ws.get("hash_prof", (size_t)(2 * nlist[N_SORT]), &fo.prof))) return rc;
         OH_HIP(hipMemsetAsync(fo.prof, 0, 16 * nlist[N_SORT], s));
       }
-      if (FOon)
-        k_agg_hash<true><<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], w0, w1, row_key, R, Lt, n_rules, O,
-                                              TL.split, lcount + N_SORT + 1, fo);
-      else
-        k_agg_hash<<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], w0, w1, row_key, R, Lt, n_rules, O, TL.split,
-                                        lcount + N_SORT + 1, fo);
+      if (!hf) launch_hash();
       if (hprof) {
         std::vector<unsigned long long> pv(2 * nlist[N_SORT]);
         if ((rc = d2h(pv.data(), fo.prof, pv.size(), s))) return rc;

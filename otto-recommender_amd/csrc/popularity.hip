@@ -861,8 +861,11 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
           float dh[68];
           OH_TRY(d2h(&ne, n_eval, 1, s));
           OH_TRY(d2h(dh, dl, 68, s));
-          fprintf(stderr, "[ottohip] kmeans bounds: %llu of %lld rows scored (force %d, delta max %.4g / %.4g, cmax %.4g)\n",
-                  ne, (long long)n, bounds, dh[64], dh[65], dh[67]);
+          std::vector<float> ds(dh, dh + k);
+          std::sort(ds.begin(), ds.end());
+          fprintf(stderr, "[ottohip] kmeans bounds: %llu of %lld rows scored (force %d, delta max %.4g / %.4g, "
+                  "median %.4g, p10 %.4g, cmax %.4g)\n", ne, (long long)n, bounds, dh[64], dh[65], ds[k / 2],
+                  ds[k / 10], dh[67]);
         }
         sk<<<(unsigned)ctx->n_cu, KM_MT, lds2, s>>>(X, n, dim, C, cn, k, labels, sums, cnt, changed, gate, amb, n_amb,
                                                     erows, n_eval, ub, lb);
