@@ -254,6 +254,7 @@ def bench_candidates(n_sessions: int, steps: int, kmeans_iter: int, group=None, 
             "recall@20": {k: round(v["top20"], 6) for k, v in res["recall"].items()},
             "recall_topall": {k: round(v["topall"], 6) for k, v in res["recall"].items()},
             "stages_s": {k: round(v, 4) for k, v in res["timings_s"].items()},
+            "outside_stages_s": round(min(dts) - sum(res["timings_s"].values()), 4),
             "data": "synthetic (otto-synth seed 0, embeddings seeds 1/3, labels by the OTTO protocol)"}
 
 

@@ -480,6 +480,12 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     OH_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_split_mean), &v, sizeof v, 0, hipMemcpyHostToDevice, s));
     OH_HIP(hipStreamSynchronize(s));
   }
+  static const char* fuse_env = getenv("OTTOHIP_SPLIT_FUSE");  // A/B switch
+  if (fuse_env && !strcmp(fuse_env, "0")) {
+    const uint32_t v = 0;
+    OH_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_split_fuse), &v, sizeof v, 0, hipMemcpyHostToDevice, s));
+    OH_HIP(hipStreamSynchronize(s));
+  }
   static const int hash_prio = getenv("OTTOHIP_HASH_PRIO") ? atoi(getenv("OTTOHIP_HASH_PRIO")) : 0;  // A/B switch
   if (hash_prio) {
     const uint32_t v = (uint32_t)hash_prio;
@@ -550,9 +556,10 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     // rewritten by the next level's classify, which waits for them (ev_join)
     hipStream_t ss = s2 ? s2 : s;
     if (s2) { OH_HIP(hipEventRecord(ctx->ev_fork, s)); OH_HIP(hipStreamWaitEvent(s2, ctx->ev_fork, 0)); }
-    // OTTOHIP_HASH_FIRST=1 (A/B switch): the level's LDS-hash leaves are queued before its register
-    // sorts, so their few long-running blocks take CU slots before the sorts' many short ones
-    static const bool hash_first = getenv("OTTOHIP_HASH_FIRST") && !strcmp(getenv("OTTOHIP_HASH_FIRST"), "1");
+    // the level's LDS-hash leaves are queued before its register sorts, so their few long-running
+    // blocks take CU slots before the sorts' many short ones (step -0.5 ms same box; OTTOHIP_HASH_FIRST=0:
+    // sorts first)
+    static const bool hash_first = !(getenv("OTTOHIP_HASH_FIRST") && !strcmp(getenv("OTTOHIP_HASH_FIRST"), "0"));
     const bool hf = hash_first && nlist[N_SORT] != 0;
     auto launch_hash = [&]() {
       const unsigned hg = (unsigned)std::min<uint64_t>(nlist[N_SORT], (uint64_t)agg_grid);
@@ -637,16 +644,16 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     if ((rc = exclusive_scan_u32(ctx, hmat, hoff, nent, hoff + nent, s))) return rc;
     static const int sub = getenv("OTTOHIP_SPLIT_SUB") ? atoi(getenv("OTTOHIP_SPLIT_SUB")) : 4096;  // A/B switch
     if (sub == 8192)
-      k_split_scatter<8192><<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, hoff, w0, w1, Lt.F);
+      k_split_scatter<8192><<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, hoff, w0, w1, Lt.F, hmat);
     else
-      k_split_scatter<4096><<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, hoff, w0, w1, Lt.F);
+      k_split_scatter<4096><<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, hoff, w0, w1, Lt.F, hmat);
     // next lists (a sub-bucket is one task in exactly one list: ndig bounds every list): the other
     // parity's set, last read by the sorts of level - 1
     if (s2 && level >= 1) OH_HIP(hipStreamWaitEvent(s, ctx->ev_join[(level + 1) & 1], 0));
     const uint64_t capn = (uint64_t)ndig;
     if ((rc = get_lists(std::max(cap0, capn), srcA ? "t_splitB" : "t_splitA", (level + 1) & 1))) return rc;
     hipMemsetAsync(lcount, 0, 8 * 8, s);
-    k_split_classify<<<grid_for(ndig), 256, 0, s>>>(cur_split, ns, dgb, mtb, hoff, ndig, TL, err);
+    k_split_classify<<<grid_for(ndig), 256, 0, s>>>(cur_split, ns, dgb, mtb, hoff, ndig, TL, err, hmat);
     srcA = !srcA;
     if (hipGetLastError() != hipSuccess) { set_error("split launch failed"); return OTTOHIP_EHIP; }
   }

@@ -27,6 +27,7 @@ constexpr int EV_BLOCK = 256;     // events per wave block (sessions starting in
 constexpr int LCAP = 512;         // sessions up to LCAP events run from LDS
 constexpr int SPLIT_MEAN = 420;   // hashed split buckets average at most this many words (default)
 __constant__ uint32_t c_split_mean = SPLIT_MEAN;  // OTTOHIP_SPLIT_MEAN overrides it (A/B switch, abi.hip)
+__constant__ uint32_t c_split_fuse = 1;  // one-chunk split tasks counted inside k_split_scatter (OTTOHIP_SPLIT_FUSE=0: off)
 __constant__ uint32_t c_hash_prio = 0;  // OTTOHIP_HASH_PRIO: wave priority of the LDS-hash leaves (A/B switch)
 constexpr uint32_t W_EMPTY = 0xFFFFFFFFu;
 constexpr int STAT_STRIPES = 256;            // copies of the per-rule statistics
@@ -825,7 +826,13 @@ __device__ __forceinline__ void emit_session(const SessView& S, int64_t e0, cons
 //           independent of session length or of how selective a rule's type mask is.
 // Sessions of more than LCAP events take k_emit_long.
 constexpr int EB_CAP = 512;    // events per batch (positions fit 10 bits)
-constexpr int EB_RCAP = 128;   // segment records per flush
+#ifndef OH_EB_RCAP
+#define OH_EB_RCAP 64
+#endif
+#ifndef OH_EMIT_WPE
+#define OH_EMIT_WPE
+#endif
+constexpr int EB_RCAP = OH_EB_RCAP;  // segment records per flush (<= 128: two record starts per lane)
 constexpr uint32_t EB_NONE = 1023u;
 
 struct EmitLds {
@@ -891,7 +898,7 @@ __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, i
   }
 }
 
-__global__ __launch_bounds__(64) void k_emit(const int64_t* __restrict__ off, const int64_t* __restrict__ first,
+__global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restrict__ off, const int64_t* __restrict__ first,
                                              int64_t NB, const uint64_t* __restrict__ ev, RulesDev R, Layout L,
                                              const int64_t* __restrict__ fb, int nf, const uint32_t* __restrict__ fid,
                                              const uint32_t* __restrict__ cnt, EvOff poff,
@@ -1897,6 +1904,10 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_hist(const Task* __restrict__
   const Task T = tasks[t];
   const uint32_t nd = split_ndig(T), nch = (uint32_t)ceil_div((int64_t)T.len, SPLIT_CH);
   const uint32_t c = (uint32_t)(blockIdx.x - chunk_base[t]);
+  if (nch == 1 && c_split_fuse) {  // one-chunk task: k_split_scatter counts it itself (zeros keep the scan exact)
+    for (uint32_t d = threadIdx.x; d < nd; d += SPLIT_T) hmat[mat_base[t] + d] = 0u;
+    return;
+  }
   const uint64_t c0 = (uint64_t)c * SPLIT_CH;
   const uint64_t c1 = c0 + SPLIT_CH < T.len ? c0 + SPLIT_CH : T.len;
   const uint32_t* W = (T.buf ? w1 : w0) + T.begin;
@@ -1924,7 +1935,8 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
                                                            const uint32_t* __restrict__ chunk_task,
                                                            const uint64_t* __restrict__ mat_base,
                                                            const uint64_t* __restrict__ hoff,
-                                                           uint32_t* __restrict__ w0, uint32_t* __restrict__ w1, int F) {
+                                                           uint32_t* __restrict__ w0, uint32_t* __restrict__ w1, int F,
+                                                           uint32_t* __restrict__ hmat) {
   constexpr int DPT = SPLIT_DMAX / SPLIT_T;  // digits per thread in the scans
   __shared__ uint32_t h[SPLIT_DMAX], st[SPLIT_DMAX];
   __shared__ uint64_t gb[SPLIT_DMAX];
@@ -1941,7 +1953,47 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
   constexpr int SUB_PER_T = SUB / SPLIT_T;
   const int tid = threadIdx.x;
   const uint64_t mb = mat_base[t];
-  for (uint32_t d = tid; d < nd; d += SPLIT_T) gb[d] = T.begin + (hoff[mb + (uint64_t)d * nch + c] - hoff[mb]);
+  if (nch == 1 && c_split_fuse) {
+    // one-chunk task (<= SPLIT_CH words): its digit counts come from this block (the words are read
+    // twice here, the second time from the caches, instead of once by k_split_hist and once here from
+    // HBM); they go to hmat for k_split_classify, and the bucket starts are a scan of them
+    for (uint32_t d = tid; d < nd; d += SPLIT_T) h[d] = 0;
+    __syncthreads();
+    for (uint64_t i0 = c0; i0 < c1; i0 += 8 * SPLIT_T) {
+      uint32_t wr[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint64_t i = i0 + tid + j * SPLIT_T;
+        wr[j] = i < c1 ? Win[i] : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (i0 + tid + j * SPLIT_T < c1) atomicAdd(&h[split_digit(wr[j], F, T.rem, nd)], 1u);
+    }
+    __syncthreads();
+    uint32_t v[DPT], tsum = 0;
+#pragma unroll
+    for (int q = 0; q < DPT; ++q) {
+      const uint32_t d = (uint32_t)(tid * DPT + q);
+      v[q] = d < nd ? h[d] : 0u;
+      tsum += v[q];
+    }
+    const uint32_t incl = wave_incl_scan(tsum);
+    if ((tid & 63) == 63) wsum[tid >> 6] = incl;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (int q = 0; q < (tid >> 6); ++q) pre += wsum[q];
+    uint32_t run = pre + incl - tsum;
+#pragma unroll
+    for (int q = 0; q < DPT; ++q) {
+      const uint32_t d = (uint32_t)(tid * DPT + q);
+      if (d < nd) { gb[d] = T.begin + run; hmat[mb + d] = v[q]; }
+      run += v[q];
+    }
+    __syncthreads();  // h / wsum are reused by the sub-tile loop
+  } else {
+    for (uint32_t d = tid; d < nd; d += SPLIT_T) gb[d] = T.begin + (hoff[mb + (uint64_t)d * nch + c] - hoff[mb]);
+  }
   for (uint64_t s0 = c0; s0 < c1; s0 += SUB) {
     const int m = (int)((c1 - s0) < (uint64_t)SUB ? (c1 - s0) : (uint64_t)SUB);
     uint32_t wr[SUB_PER_T], dg[SUB_PER_T];
@@ -1999,7 +2051,7 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
 // one thread per (split task, digit): push the non-empty sub-buckets as next-level tasks
 __global__ void k_split_classify(const Task* __restrict__ tasks, int64_t n, const uint64_t* __restrict__ digit_base,
                                  const uint64_t* __restrict__ mat_base, const uint64_t* __restrict__ hoff,
-                                 int64_t n_digits_total, TaskLists TL, int* err) {
+                                 int64_t n_digits_total, TaskLists TL, int* err, const uint32_t* __restrict__ hmat) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   Task T;
   T.begin = 0; T.rem = 0; T.row = 0; T.buf = 0; T.len = 0;
@@ -2009,9 +2061,16 @@ __global__ void k_split_classify(const Task* __restrict__ tasks, int64_t n, cons
     T = tasks[t];
     const uint64_t d = (uint64_t)i - digit_base[t], nch = (uint64_t)ceil_div((int64_t)T.len, SPLIT_CH);
     const uint64_t mb = mat_base[t];
-    const uint64_t lo = hoff[mb + d * nch], hi = hoff[mb + (d + 1) * nch];
-    c = hi - lo;
-    b = T.begin + (lo - hoff[mb]);
+    if (nch == 1 && c_split_fuse) {  // counted by k_split_scatter: hoff holds zeros for this task
+      uint64_t lo = 0;
+      for (uint64_t e = 0; e < d; ++e) lo += hmat[mb + e];
+      c = hmat[mb + d];
+      b = T.begin + lo;
+    } else {
+      const uint64_t lo = hoff[mb + d * nch], hi = hoff[mb + (d + 1) * nch];
+      c = hi - lo;
+      b = T.begin + (lo - hoff[mb]);
+    }
   }
   // a bucket within 4x of its expected size is split again (its parent was too large for one
   // split's 8 bits); one far above it holds a few hot keys and goes to the hash path

@@ -92,6 +92,7 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
     whole job's candidate count and 'local_candidates' this rank's. keep_tables: host copies of every
     stage's output in 'intermediates' (the candidates as a DataFrame, or with keep_candidates=False
     as the device CSR 'candidates_csr' plus 'test_session_ids', for full-size runs)."""
+    t_entry = time.perf_counter()
     import torch
     from .synth import file_session_bounds
     from . import dist as gd
@@ -110,6 +111,7 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
         return time.perf_counter()
 
     t = time.perf_counter()
+    T["prelude"] = T.get("prelude", 0.0) + t - t_entry
     # ---- co-visitation (model/count_co_events.py:201-226): count each folder (:204-205), A6 per
     # folder with its own file statistics (:212-216), then A6 on [train, test] (A7, :218-226)
     from .synth import SESSIONS_PER_FILE
@@ -212,4 +214,5 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
         else:
             out["intermediates"]["candidates_csr"] = cands.to_torch()
     cands.free()
+    mark("finish", t)
     return out
