@@ -832,7 +832,10 @@ constexpr int EB_CAP = 512;    // events per batch (positions fit 10 bits)
 #ifndef OH_EMIT_WPE
 #define OH_EMIT_WPE
 #endif
-constexpr int EB_RCAP = OH_EB_RCAP;  // segment records per flush (<= 128: two record starts per lane)
+constexpr int EB_RCAP = OH_EB_RCAP;  // segment records per flush
+// 64 <= EB_RCAP: one round of record building adds up to 64 records after a flush;
+// EB_RCAP <= 128: the flush keeps two record starts per lane (32 overflowed the record arrays: LDS corruption)
+static_assert(EB_RCAP >= 64 && EB_RCAP <= 128, "records per emit flush");
 constexpr uint32_t EB_NONE = 1023u;
 
 struct EmitLds {
