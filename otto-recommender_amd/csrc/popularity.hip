@@ -472,28 +472,22 @@ __device__ __forceinline__ void km_split8(const float (&v)[8], uint4& hi, uint4&
   lo = make_uint4(lw[0], lw[1], lw[2], lw[3]);
 }
 
-// Distance bounds across Lloyd steps (Yinyang-style: one upper bound, one lower bound per group of 8
-// consecutive clusters), so a step scores only the rows whose label could change. Per row:
-// ub >= |x - c_a| (a = its label) and lb_g <= min_{j in group g, j != a} |x - c_j|, all for the centres
-// Cp the bounds were last made valid for. A step first takes delta_j >= |C_j - Cp_j| (k_km_delta, then
-// Cp = C), so by the triangle inequality u = ub + delta_a and l = min_g (lb_g - max_{j in g} delta_j)
-// bound the distances to the new centres C (on session embeddings a few centres move far more than
-// the rest: the largest shift is 10-100x the median, so per-group maxima keep most groups' bounds
-// where one global maximum would drop them all). The exact f32 kernel
+// Distance bounds across Lloyd steps (Hamerly's single lower bound), so a step scores only the rows
+// whose label could change. Per row: ub >= |x - c_a| (a = its label) and lb <= min_{j != a} |x - c_j|,
+// both for the centres Cp the bounds were last made valid for. A step first takes
+// delta_j >= |C_j - Cp_j| (k_km_delta, then Cp = C), so by the triangle inequality u = ub + delta_a and
+// l = lb - max_{j != a} delta_j bound the distances to the new centres C. The exact f32 kernel
 // (k_km_assign_mfma) scores s_j = |c_j|^2 - 2 x.c_j within 2e-5 cmax (|x| + cmax) (its MFMA dot,
 // the stored |c|^2 and two roundings; cmax = max |c_j|), so it keeps label a whenever
 // l^2 - u^2 > 4e-5 cmax (|x| + cmax); with |x| <= u + cmax the filter asks for
 // (l - u)(l + u) > KMB_SKIP cmax (u + 2 cmax), KMB_SKIP = 2e-4 (5x margin). Such rows keep their
 // label and sums (nothing to move); the others are listed for the split-precision pass, which
 // rebuilds their bounds from its approximate scores (error within 2e-4 cmax (|x| + cmax) there, so
-// u^2 <= m + |x|^2 + e and lb_g^2 >= m_g + |x|^2 - e with m the smallest score and m_g the smallest
-// of group g's other clusters), and near ties get lb = 0 (scored again next step). Every bound is
-// rounded outwards (relative 2^-20 / 1e-6).
+// u^2 <= m + |x|^2 + e and l^2 >= m2 + |x|^2 - e with m, m2 the two smallest scores), and near ties
+// get lb = 0 (scored again next step). Every bound is rounded outwards (relative 2^-20 / 1e-6).
 constexpr float KMB_SKIP = 2e-4f;
 constexpr float KMB_ERR = 2e-4f;
-constexpr int KMB_G = 8;  // lower bounds per row (groups of 8 clusters, k <= 64)
-constexpr int KMB_DL = 80;
-// dl: [0, 64) delta_j, [64, 72) per-group largest delta, [72] cmax
+// dl: [0, 64) delta_j, [64] largest delta, [65] second largest, [66] its cluster (as float), [67] cmax
 __global__ void k_km_delta(const float* __restrict__ C, float* __restrict__ Cp, const float* __restrict__ cn,
                            int k, int dim, int force, float* __restrict__ dl, const int* __restrict__ gate,
                            unsigned long long* __restrict__ n_eval) {
@@ -511,17 +505,27 @@ __global__ void k_km_delta(const float* __restrict__ C, float* __restrict__ Cp, 
   __syncthreads();  // every read of Cp before it is overwritten
   if (j < k)
     for (int i = 0; i < dim; ++i) Cp[(int64_t)j * dim + i] = C[(int64_t)j * dim + i];
-  // largest delta of each group of 8 clusters
-  float gm = d;
+  // largest and second largest delta (ties: any cluster holding the largest, the second equals it)
+  float m1 = d;
+  int a1 = j;
 #pragma unroll
-  for (int o = 1; o < 8; o <<= 1) gm = fmaxf(gm, __shfl_xor(gm, o));
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float pm = __shfl_xor(m1, o);
+    const int pa = __shfl_xor(a1, o);
+    if (pm > m1 || (pm == m1 && pa < a1)) { m1 = pm; a1 = pa; }
+  }
+  float m2 = j == a1 ? 0.f : d;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m2 = fmaxf(m2, __shfl_xor(m2, o));
   float c2 = j < k ? cn[j] : 0.f;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) c2 = fmaxf(c2, __shfl_xor(c2, o));
   dl[j] = d;
-  if ((j & 7) == 0) dl[64 + (j >> 3)] = gm;
   if (j == 0) {
-    dl[72] = sqrtf(c2) * 1.000001f;
+    dl[64] = m1;
+    dl[65] = m2;
+    dl[66] = (float)a1;
+    dl[67] = sqrtf(c2) * 1.000001f;
     *n_eval = 0;
   }
 }
@@ -536,15 +540,13 @@ __global__ __launch_bounds__(256) void k_km_filter(int64_t n, int k, const int32
                                                    unsigned long long* __restrict__ n_eval,
                                                    const int* __restrict__ gate) {
   if (gate && __builtin_amdgcn_readfirstlane(*gate)) return;
-  __shared__ float sd[KMB_DL];
+  __shared__ float sd[68];
   __shared__ uint32_t wc[KMF_PER * 4];
   __shared__ unsigned long long base;
-  if (threadIdx.x < KMB_DL) sd[threadIdx.x] = dl[threadIdx.x];
+  if (threadIdx.x < 68) sd[threadIdx.x] = dl[threadIdx.x];
   __syncthreads();
-  const float cmax = sd[72];
-  float dg[KMB_G];
-#pragma unroll
-  for (int g = 0; g < KMB_G; ++g) dg[g] = sd[64 + g];
+  const float d1 = sd[64], d2 = sd[65], cmax = sd[67];
+  const int a1 = (int)sd[66];
   const int wv = threadIdx.x >> 6;
   const int64_t r0 = (int64_t)blockIdx.x * (KMF_PER * 256);
   uint32_t evm = 0;  // bit j: row r0 + j * 256 + tid is scored
@@ -558,18 +560,10 @@ __global__ __launch_bounds__(256) void k_km_filter(int64_t n, int k, const int32
         ev = true;
       } else {
         const float u = (ub[i] + sd[a]) * (1.f + 0x1p-20f);
-        float4* lp = reinterpret_cast<float4*>(lb + i * KMB_G);
-        float4 q0 = lp[0], q1 = lp[1];
-        // a negative bound stays a (useless) lower bound: bounds only decrease until the row is scored
-        q0.x = (q0.x - dg[0]) * (1.f - 0x1p-20f); q0.y = (q0.y - dg[1]) * (1.f - 0x1p-20f);
-        q0.z = (q0.z - dg[2]) * (1.f - 0x1p-20f); q0.w = (q0.w - dg[3]) * (1.f - 0x1p-20f);
-        q1.x = (q1.x - dg[4]) * (1.f - 0x1p-20f); q1.y = (q1.y - dg[5]) * (1.f - 0x1p-20f);
-        q1.z = (q1.z - dg[6]) * (1.f - 0x1p-20f); q1.w = (q1.w - dg[7]) * (1.f - 0x1p-20f);
-        const float l = fminf(fminf(fminf(q0.x, q0.y), fminf(q0.z, q0.w)), fminf(fminf(q1.x, q1.y), fminf(q1.z, q1.w)));
+        const float l = (lb[i] - (a == a1 ? d2 : d1)) * (1.f - 0x1p-20f);
         if (l > u && (l - u) * (l + u) > KMB_SKIP * cmax * (u + 2.f * cmax)) {
           ub[i] = u;
-          lp[0] = q0;
-          lp[1] = q1;
+          lb[i] = l;
         } else {
           ev = true;
         }
@@ -744,34 +738,11 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
     }
     m2 = fminf(m2, __shfl_xor(m2, 32));
     const bool decided = m2 - m > KMS_SEP * sqrtf(xs) * cmax;
-    if constexpr (BL) {  // the row's bounds for these centres (near ties: none, lb = 0)
-      // smallest score of each group of 8 clusters without the row's own: lane half h holds clusters
-      // 8q + 4h + (0..3) of group q in registers 4q .. 4q + 3 (acc1: group 4 + q); this lane keeps
-      // groups 4h .. 4h + 3
-      float g4[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float a0 = INFINITY, a1 = INFINITY;
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int c0 = rr + 8 * q + 4 * h;
-          a0 = fminf(a0, c0 == mc ? INFINITY : acc0[4 * q + rr]);
-          if (NB == 2) a1 = fminf(a1, c0 + 32 == mc ? INFINITY : acc1[4 * q + rr]);
-        }
-        const float f0 = fminf(a0, __shfl_xor(a0, 32)), f1 = fminf(a1, __shfl_xor(a1, 32));
-        g4[q] = h == 0 ? f0 : f1;
-      }
-      if (in_r) {
-        const float cm = cmax * 1.000001f;
-        const float e = KMB_ERR * cm * (sqrtf(xs) * 1.0001f + cm);
-        if (h == 0) ub[row] = decided ? sqrtf(fmaxf(m + xs * 1.00001f + e, 0.f)) * 1.000001f : 0.f;
-        float4 o;
-        o.x = decided ? sqrtf(fmaxf(g4[0] + xs * 0.99999f - e, 0.f)) * 0.999999f : 0.f;
-        o.y = decided ? sqrtf(fmaxf(g4[1] + xs * 0.99999f - e, 0.f)) * 0.999999f : 0.f;
-        o.z = decided ? sqrtf(fmaxf(g4[2] + xs * 0.99999f - e, 0.f)) * 0.999999f : 0.f;
-        o.w = decided ? sqrtf(fmaxf(g4[3] + xs * 0.99999f - e, 0.f)) * 0.999999f : 0.f;
-        reinterpret_cast<float4*>(lb + row * KMB_G)[h] = o;
-      }
+    if (BL && h == 0 && in_r) {  // the row's bounds for these centres (near ties: none, lb = 0)
+      const float cm = cmax * 1.000001f;
+      const float e = KMB_ERR * cm * (sqrtf(xs) * 1.0001f + cm);
+      ub[row] = decided ? sqrtf(fmaxf(m + xs * 1.00001f + e, 0.f)) * 1.000001f : 0.f;
+      lb[row] = decided ? sqrtf(fmaxf(m2 + xs * 0.99999f - e, 0.f)) * 0.999999f : 0.f;
     }
     const uint32_t mi = (uint32_t)mc;
     const bool mine = h == 0 && in_r && decided;
@@ -876,9 +847,9 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
         uint32_t* erows;
         unsigned long long* n_eval;
         OH_TRY(ctx->ws.get("km_ub", (size_t)n, &ub));
-        OH_TRY(ctx->ws.get("km_lb", (size_t)n * KMB_G, &lb));
+        OH_TRY(ctx->ws.get("km_lb", (size_t)n, &lb));
         OH_TRY(ctx->ws.get("km_cp", (size_t)k * dim, &cp));
-        OH_TRY(ctx->ws.get("km_dl", KMB_DL, &dl));
+        OH_TRY(ctx->ws.get("km_dl", 68, &dl));
         OH_TRY(ctx->ws.get("km_erows", (size_t)n, &erows));
         OH_TRY(ctx->ws.get("km_neval", 1, &n_eval));
         k_km_delta<<<1, 64, 0, s>>>(C, cp, cn, k, dim, bounds, dl, gate, n_eval);
@@ -887,14 +858,14 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
         static const bool bdbg = getenv("OTTOHIP_KM_BDBG") != nullptr;  // rows scored per step (debugging aid)
         if (bdbg) {
           unsigned long long ne = 0;
-          float dh[KMB_DL];
+          float dh[68];
           OH_TRY(d2h(&ne, n_eval, 1, s));
-          OH_TRY(d2h(dh, dl, KMB_DL, s));
+          OH_TRY(d2h(dh, dl, 68, s));
           std::vector<float> ds(dh, dh + k);
           std::sort(ds.begin(), ds.end());
-          fprintf(stderr, "[ottohip] kmeans bounds: %llu of %lld rows scored (force %d, delta max %.4g, "
-                  "median %.4g, p10 %.4g, cmax %.4g)\n", ne, (long long)n, bounds, ds[k - 1], ds[k / 2],
-                  ds[k / 10], dh[72]);
+          fprintf(stderr, "[ottohip] kmeans bounds: %llu of %lld rows scored (force %d, delta max %.4g / %.4g, "
+                  "median %.4g, p10 %.4g, cmax %.4g)\n", ne, (long long)n, bounds, dh[64], dh[65], ds[k / 2],
+                  ds[k / 10], dh[67]);
         }
         sk<<<(unsigned)ctx->n_cu, KM_MT, lds2, s>>>(X, n, dim, C, cn, k, labels, sums, cnt, changed, gate, amb, n_amb,
                                                     erows, n_eval, ub, lb);
