@@ -838,15 +838,25 @@ constexpr int EB_RCAP = OH_EB_RCAP;  // segment records per flush
 static_assert(EB_RCAP >= 64 && EB_RCAP <= 128, "records per emit flush");
 constexpr uint32_t EB_NONE = 1023u;
 
-struct EmitLds {
-  uint64_t tev[EB_CAP];                 // type-partitioned events of the batch
-  uint32_t rpre[EB_RCAP];               // record start in the flattened pair order
+struct EmitRecs {
   uint4 rec[EB_RCAP];                   // per record: start, list position | exclusion, word high bits,
                                         // smallest partner aid written (symmetric rules: the event's aid)
   uint64_t rout[EB_RCAP];
+  uint32_t rpre[EB_RCAP];               // record start in the flattened pair order
+};
+struct EmitPre {
+  uint16_t pst[3][64], pen[3][64];      // per-type prefix counts at session start / end
+};
+struct EmitLds {
+  uint64_t tev[EB_CAP];                 // type-partitioned events of the batch
+  // passes 1-2 use the prefix counts, pass 3 and the flushes the records: one LDS range for both
+  // (the batch's last flush ends before the next batch's pass 1, behind a wave barrier)
+  union {
+    EmitRecs r;
+    EmitPre p;
+  } u;
   uint16_t ss[65];                      // session start (batch-relative); ss[f] = batch size
   uint16_t sb[4][64];                   // per session: start of the type-t list; sb[3] = end of valid
-  uint16_t pst[3][64], pen[3][64];      // per-type prefix counts at session start / end
   uint32_t sfile[64];
   uint16_t espos[EB_CAP];               // per batch event: position in tev (EB_NONE: invalid)
   uint8_t esid[EB_CAP];                 // per batch event: session index in the batch
@@ -865,8 +875,8 @@ struct EmitLds {
 __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, int F, uint32_t* __restrict__ words,
                                            int dbg, uint32_t& rid) {
   const uint32_t l = lane_id();
-  const uint32_t sa = (int)l < nrec ? S.rpre[l] : 0xFFFFFFFFu;
-  const uint32_t sb = (int)l + 64 < nrec ? S.rpre[l + 64] : 0xFFFFFFFFu;
+  const uint32_t sa = (int)l < nrec ? S.u.r.rpre[l] : 0xFFFFFFFFu;
+  const uint32_t sb = (int)l + 64 < nrec ? S.u.r.rpre[l + 64] : 0xFFFFFFFFu;
   const uint64_t below = (1ull << l) - 1ull, upto = below | (1ull << l);  // lanes < l, <= l
   int ob = -1;        // last record starting before the round's window
   uint32_t cc = 0;    // words written in earlier rounds by the record spanning into this round
@@ -884,7 +894,7 @@ __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, i
     bool qual = false;
     uint32_t word = 0;
     if (p < tot) {
-      const uint4 rc = S.rec[o];
+      const uint4 rc = S.u.r.rec[o];
       uint32_t j = (rc.y & 1023u) + (p - rc.x);
       if (j >= ((rc.y >> 10) & 1023u)) j += rc.y >> 21;
       const uint32_t a = (uint32_t)ev_aid(S.tev[j]);
@@ -896,7 +906,7 @@ __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, i
     const uint32_t first = mle ? 63u - (uint32_t)__builtin_clzll(mle) : 0u;
     const uint64_t mine = Q & ~((1ull << first) - 1ull);
     const uint32_t car = mle ? 0u : cc;
-    if (qual && !(dbg & 1)) words[S.rout[o] + car + (uint32_t)__popcll(mine & below)] = word;
+    if (qual && !(dbg & 1)) words[S.u.r.rout[o] + car + (uint32_t)__popcll(mine & below)] = word;
     cc = (uint32_t)__builtin_amdgcn_readlane((int)(car + (uint32_t)__popcll(mine)), 63);
   }
 }
@@ -980,9 +990,9 @@ __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restri
         if (k + st < nsess && (int)S.ss[k + st] <= idx) k += st;
       const uint64_t m0 = __ballot(t == 0), m1 = __ballot(t == 1), m2 = __ballot(t == 2);
       const uint32_t P0 = base0 + mbcnt(m0), P1 = base1 + mbcnt(m1), P2 = base2 + mbcnt(m2);
-      if (in && idx == (int)S.ss[k]) { S.pst[0][k] = P0; S.pst[1][k] = P1; S.pst[2][k] = P2; }
+      if (in && idx == (int)S.ss[k]) { S.u.p.pst[0][k] = P0; S.u.p.pst[1][k] = P1; S.u.p.pst[2][k] = P2; }
       if (in && idx == (int)S.ss[k + 1] - 1) {
-        S.pen[0][k] = P0 + (t == 0); S.pen[1][k] = P1 + (t == 1); S.pen[2][k] = P2 + (t == 2);
+        S.u.p.pen[0][k] = P0 + (t == 0); S.u.p.pen[1][k] = P1 + (t == 1); S.u.p.pen[2][k] = P2 + (t == 2);
       }
       base0 += (uint32_t)__popcll(m0); base1 += (uint32_t)__popcll(m1); base2 += (uint32_t)__popcll(m2);
       sid[c] = (uint32_t)k;
@@ -993,7 +1003,7 @@ __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restri
     if (l < nsess) {
       const uint32_t a = S.ss[l];
       if (S.ss[l + 1] > a) {
-        const uint32_t c0 = S.pen[0][l] - S.pst[0][l], c1 = S.pen[1][l] - S.pst[1][l], c2 = S.pen[2][l] - S.pst[2][l];
+        const uint32_t c0 = S.u.p.pen[0][l] - S.u.p.pst[0][l], c1 = S.u.p.pen[1][l] - S.u.p.pst[1][l], c2 = S.u.p.pen[2][l] - S.u.p.pst[2][l];
         S.sb[0][l] = a; S.sb[1][l] = a + c0; S.sb[2][l] = a + c0 + c1; S.sb[3][l] = a + c0 + c1 + c2;
       }
     }
@@ -1009,7 +1019,7 @@ __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restri
         uint32_t pos = EB_NONE;
         if (t < 3) {
           const uint32_t k = sid[c];
-          pos = S.sb[t][k] + pr[c] - S.pst[t][k];
+          pos = S.sb[t][k] + pr[c] - S.u.p.pst[t][k];
           S.tev[pos] = vv[c];
         }
         S.espos[idx] = (uint16_t)pos;
@@ -1082,10 +1092,10 @@ __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restri
           const uint32_t incl = wave_incl_scan(len);
           if (len > 0) {
             const int ri = nrec + (int)mbcnt(m);
-            S.rpre[ri] = tot + incl - len;
-            S.rec[ri] = make_uint4(tot + incl - len, jb | (xlo << 10) | (xlen << 21), ((uint32_t)q << shiftR) | file,
+            S.u.r.rpre[ri] = tot + incl - len;
+            S.u.r.rec[ri] = make_uint4(tot + incl - len, jb | (xlo << 10) | (xlen << 21), ((uint32_t)q << shiftR) | file,
                                    sym ? (uint32_t)ev_aid(v) : 0u);
-            S.rout[ri] = eout + eo;
+            S.u.r.rout[ri] = eout + eo;
           }
           if (!sym) eo += len;
           nrec += nn;
