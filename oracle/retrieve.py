@@ -8,6 +8,10 @@ R1  get_df_count_for_co_event_type  (model/retrieve.py:18-63), restated on numpy
       * rank('ordinal', reverse=True).over('aid') after sort(['aid']): ties in count are broken
         by row order within the aid, taken here as FILE order (the build's deterministic
         choice; polars' unstable sort leaves it unspecified).
+R5  trim rule's horizontal minima (model/retrieve.py:498, 502, 505: pl.min([col, ...])) are taken as
+    polars' horizontal min with nulls SKIPPED (a row's min over its non-null sources; null only when
+    every source is null), restated as pandas DataFrame.min(axis=1) (skipna=True). The installed
+    polars version is unpinned; this is the assumed semantics, parity unpinned.
 Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
 """
 from __future__ import annotations
