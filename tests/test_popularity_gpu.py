@@ -197,3 +197,46 @@ def test_session_item_similarity(gpu):
     np.testing.assert_allclose(cos[ok], rc[ok], rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(eu[ok], re[ok], rtol=1e-5)
     assert np.all(cos[~ok] == 0) and np.all(eu[~ok] == -1)
+
+
+def test_kmeans_bounds_invalidated_by_other_label_writers(gpu, monkeypatch):
+    """The distance bounds carried between ottohip_kmeans_lloyd_steps calls (csrc/popularity.hip
+    k_km_filter) are dropped when another entry point writes the labels (ottohip_kmeans_partial here)
+    and when the centroids move outside the batched steps (ottohip_kmeans_update): the same call
+    sequence gives bit-identical labels, centroids and stop reasons with and without the bounds."""
+    import ctypes
+    import torch
+    from otto_recommender_amd import _lib
+    rng = np.random.default_rng(21)
+    centers = rng.normal(scale=2, size=(20, 64))
+    X = torch.from_numpy((centers[rng.integers(0, 20, 50_000)] + rng.normal(size=(50_000, 64))).astype(np.float32)).cuda()
+    n, dim, k = X.shape[0], X.shape[1], 20
+    lib, ctx = _lib.load(), _lib.context()
+    sh = _lib.stream_handle()
+    runs = []
+    for bounds in ("0", "1"):
+        monkeypatch.setenv("OTTOHIP_KM_BOUNDS", bounds)
+        perm = np.random.default_rng(5).permutation(n)[:k]
+        C = X[torch.from_numpy(perm).cuda()].clone()
+        labels = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        sums = torch.zeros(k * dim, dtype=torch.int64, device="cuda")
+        counts = torch.zeros(k, dtype=torch.int64, device="cuda")
+        out = (ctypes.c_double * 6)()
+        trace = []
+        for phase in range(4):
+            _lib.check(lib.ottohip_kmeans_lloyd_steps(ctx.h, _lib.ptr(X), n, dim, _lib.ptr(C), k, _lib.ptr(labels),
+                                                      _lib.ptr(sums), _lib.ptr(counts), 3, 0.0, out, sh))
+            trace.append((int(out[4]), int(out[5]), int(out[1])))
+            if phase == 1:  # an outside label writer, then an outside centroid update
+                inr, chg = ctypes.c_double(), ctypes.c_int64()
+                _lib.check(lib.ottohip_kmeans_partial(ctx.h, _lib.ptr(X), n, dim, _lib.ptr(C), k, _lib.ptr(labels),
+                                                      _lib.ptr(sums), _lib.ptr(counts), ctypes.byref(inr),
+                                                      ctypes.byref(chg), sh))
+                shift = ctypes.c_double()
+                _lib.check(lib.ottohip_kmeans_update(ctx.h, _lib.ptr(C), _lib.ptr(sums), _lib.ptr(counts), k, dim,
+                                                     ctypes.byref(shift), sh))
+        torch.cuda.synchronize()
+        runs.append((labels.cpu().numpy(), C.cpu().numpy(), trace))
+    np.testing.assert_array_equal(runs[0][0], runs[1][0])
+    np.testing.assert_array_equal(runs[0][1], runs[1][1])
+    assert runs[0][2] == runs[1][2]
