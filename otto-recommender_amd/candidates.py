@@ -261,16 +261,7 @@ def retrieve_candidates(df_sessions_aids_full, aid_pairs_co_events: dict, df_knn
         cmap = {int(c): i for i, c in enumerate(clusters)}
         pop = (p["cl50"].map(cmap).to_numpy(), p["aid"].to_numpy())
         ncl = len(clusters)
-        # session -> dense cluster index (-1: no cluster / null), one sorted search
-        sc = df_session_cl.dropna(subset=["cl50"])
-        ks = sc["session"].to_numpy().astype(np.int64)
-        kc = np.searchsorted(clusters, sc["cl50"].to_numpy())
-        o = np.argsort(ks, kind="stable")
-        ks, kc = ks[o], kc[o]
-        j = np.searchsorted(ks, sess_ids.astype(np.int64))
-        hit = j < len(ks)
-        hit[hit] = ks[j[hit]] == sess_ids[hit]
-        scl = np.where(hit, kc[np.minimum(j, max(len(ks) - 1, 0))] if len(ks) else -1, -1).astype(np.int32)
+        scl = session_cluster_index(df_session_cl, clusters, sess_ids)
     src = CandidateSources(r1, ka, k12, pop, ncl, n_items)
     c = generate(ev.session_offsets, ev.aid, ev.ts, ev.type, src, scl)
     out = c.to_pandas(sess_ids)
@@ -278,6 +269,22 @@ def retrieve_candidates(df_sessions_aids_full, aid_pairs_co_events: dict, df_knn
     if file_out is not None:
         write_retrieved(out, file_out)
     return out
+
+
+def session_cluster_index(df_session_cl, clusters, sess_ids) -> np.ndarray:
+    """Dense cluster index (position in the sorted `clusters`) of every session in sess_ids, -1 for a
+    session without a row or with a null cl50: one sorted search. A session listed more than once
+    takes its LAST row (the dict lookup this replaced kept the last value of a duplicated key)."""
+    sc = df_session_cl.dropna(subset=["cl50"])
+    ks = sc["session"].to_numpy().astype(np.int64)
+    kc = np.searchsorted(clusters, sc["cl50"].to_numpy())
+    o = np.argsort(ks, kind="stable")
+    ks, kc = ks[o], kc[o]
+    q = np.asarray(sess_ids, np.int64)
+    j = np.searchsorted(ks, q, side="right") - 1  # the last of equal sessions (stable order)
+    hit = j >= 0
+    hit[hit] = ks[j[hit]] == q[hit]
+    return np.where(hit, kc[np.maximum(j, 0)] if len(ks) else -1, -1).astype(np.int32)
 
 
 def write_retrieved(df, file_out):

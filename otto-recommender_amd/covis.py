@@ -265,6 +265,8 @@ def count_co_events_fused(events: DeviceEvents, names=None, n_items: int = confi
     with per_file=True the table carries file_rows_per_file / file_rows_ge2_per_file (numpy)."""
     ctx = ctx or _lib.context()
     cap = max_files or max_files_per_call(names, n_items)
+    if cuts is not None and cuts.per_file:
+        cap = min(cap, 1024)  # the per-file histogram's file range (ottohip_file_opts), as in dist.py
     nf = len(events.file_bounds) - 1
     if nf > cap:
         import torch

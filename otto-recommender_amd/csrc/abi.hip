@@ -179,9 +179,16 @@ static int setup_rules(const ottohip_rule* rules, int n_rules, const ottohip_cov
   for (int r = 0; r < n_rules; ++r)
     if (R.lo[r] > R.hi[r]) R.mask[r] = 0;  // empty window: never matches (count stays 0)
   static const bool sym_env = !(getenv("OTTOHIP_SYMMETRIC") && !strcmp(getenv("OTTOHIP_SYMMETRIC"), "0"));
+  // next types == {this type}, dt window symmetric: (i, j) qualifies iff (j, i) does. At most one such
+  // rule per event type is stored once: k_emit places an event's symmetric record after all of its
+  // other records (its written length is known only to S2's count), so a second one would overwrite it
   if (allow_sym && sym_env)
-    for (int r = 0; r < n_rules; ++r)  // next types == {this type}, dt window symmetric: (i, j) qualifies iff (j, i) does
-      if (R.mask[r] == (1u << rules[r].this_type) && R.lo[r] == -R.hi[r]) R.sym_mask |= 1u << r;
+    for (int r = 0; r < n_rules; ++r) {
+      const int t = rules[r].this_type;
+      bool taken = false;
+      for (int q = 0; q < r; ++q) taken |= ((R.sym_mask >> q) & 1u) && rules[q].this_type == t;
+      if (!taken && R.mask[r] == (1u << t) && R.lo[r] == -R.hi[r]) R.sym_mask |= 1u << r;
+    }
   Lt.A = std::max(1, bits_for((uint64_t)params->n_items));
   Lt.F = bits_for((uint64_t)n_files_total);
   Lt.BR = bits_for((uint64_t)max_per_type);
@@ -374,7 +381,8 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
 // S4: words of every qualifying pair at its row's offsets
 static int covis_emit_words(ottohip_ctx* ctx, const Front& F, const ottohip_events* ev, uint32_t* w0, hipStream_t s) {
   int ph = ctx->begin("emit", s, 8.0 * F.E + 12.0 * F.E + 4.0 * (double)F.P);
-  static const int dbg = getenv("OTTOHIP_EMIT_DBG") ? atoi(getenv("OTTOHIP_EMIT_DBG")) : 0;  // profiling ablations
+  static const int dbg0 = getenv("OTTOHIP_EMIT_DBG") ? atoi(getenv("OTTOHIP_EMIT_DBG")) : 0;  // profiling ablations
+  const int dbg = dbg0 | (getenv("OTTOHIP_DEBUG") ? 4 : 0);  // 4: bounds checks of the emit record arrays
   int* eerr;
   OH_TRY(ctx->ws.get("emit_err", 4, &eerr));
   OH_HIP(hipMemsetAsync(eerr, 0, sizeof(int), s));
@@ -388,6 +396,7 @@ static int covis_emit_words(ottohip_ctx* ctx, const Front& F, const ottohip_even
   ctx->end(ph, s);
   int herr = 0;
   OH_TRY(d2h(&herr, eerr, 1, s));
+  if (herr & 8) { set_error("emit: record index outside the flush's records (err=%d)", herr); return OTTOHIP_EHIP; }
   if (herr) { set_error("emit: pairs written per event disagree with the count stage (err=%d)", herr); return OTTOHIP_EHIP; }
   return 0;
 }
@@ -737,6 +746,7 @@ int ottohip_ctx_trim(ottohip_ctx* ctx) {
   ctx->ws.release();
   ctx->spare.release();
   dev_trim();
+  ctx->km_bvalid = false;  // the KMeans distance bounds lived in the released workspace
   return 0;
 }
 

@@ -872,8 +872,10 @@ struct EmitLds {
 // aid; 0 for other rules): a lane's word goes to the record's output at its rank among the record's
 // written words -- those of earlier rounds (only the record spanning the round boundary has any: a
 // wave-uniform carry) plus those of the record's lanes below it in this round (one ballot).
+// dbg & 4 (OTTOHIP_DEBUG): a lane whose record index falls outside [0, nrec) sets err bit 8 and writes
+// nothing (the record arrays hold EB_RCAP entries; an out-of-range index would read stale LDS)
 __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, int F, uint32_t* __restrict__ words,
-                                           int dbg, uint32_t& rid) {
+                                           int dbg, uint32_t& rid, int* __restrict__ err) {
   const uint32_t l = lane_id();
   const uint32_t sa = (int)l < nrec ? S.u.r.rpre[l] : 0xFFFFFFFFu;
   const uint32_t sb = (int)l + 64 < nrec ? S.u.r.rpre[l + 64] : 0xFFFFFFFFu;
@@ -893,7 +895,9 @@ __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, i
     const uint32_t p = c + l;
     bool qual = false;
     uint32_t word = 0;
-    if (p < tot) {
+    const bool bad = (dbg & 4) && p < tot && (o < 0 || o >= nrec);
+    if (bad) atomicOr(err, 8);
+    if (p < tot && !bad) {
       const uint4 rc = S.u.r.rec[o];
       uint32_t j = (rc.y & 1023u) + (p - rc.x);
       if (j >= ((rc.y >> 10) & 1023u)) j += rc.y >> 21;
@@ -906,7 +910,7 @@ __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, i
     const uint32_t first = mle ? 63u - (uint32_t)__builtin_clzll(mle) : 0u;
     const uint64_t mine = Q & ~((1ull << first) - 1ull);
     const uint32_t car = mle ? 0u : cc;
-    if (qual && !(dbg & 1)) words[S.u.r.rout[o] + car + (uint32_t)__popcll(mine & below)] = word;
+    if (qual && !(dbg & 1) && !bad) words[S.u.r.rout[o] + car + (uint32_t)__popcll(mine & below)] = word;
     cc = (uint32_t)__builtin_amdgcn_readlane((int)(car + (uint32_t)__popcll(mine)), 63);
   }
 }
@@ -1084,13 +1088,14 @@ __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restri
           if (nrec + nn > EB_RCAP) {
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            emit_flush(S, nrec, tot, L.F, words, dbg, rid);
+            emit_flush(S, nrec, tot, L.F, words, dbg, rid, err);
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             nrec = 0; tot = 0;
           }
           const uint32_t incl = wave_incl_scan(len);
-          if (len > 0) {
+          if ((dbg & 4) && nrec + nn > EB_RCAP) atomicOr(err, 8);  // the record arrays would overflow
+          if (len > 0 && !((dbg & 4) && nrec + (int)mbcnt(m) >= EB_RCAP)) {
             const int ri = nrec + (int)mbcnt(m);
             S.u.r.rpre[ri] = tot + incl - len;
             S.u.r.rec[ri] = make_uint4(tot + incl - len, jb | (xlo << 10) | (xlen << 21), ((uint32_t)q << shiftR) | file,
@@ -1107,7 +1112,7 @@ __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restri
     if (nrec > 0) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      emit_flush(S, nrec, tot, L.F, words, dbg, rid);
+      emit_flush(S, nrec, tot, L.F, words, dbg, rid, err);
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

@@ -74,18 +74,39 @@ def exchange(send, send_counts, group=None, return_counts=False):
     return (recv, recv_counts) if return_counts else recv
 
 
-def exchange_async(send, send_counts, group=None):
-    """exchange() with the payload all-to-all left in flight: the entry counts are exchanged at
-    once (the receive size), the payload returns a handle. finish_exchange(handle) waits and
-    returns the received tensor; meanwhile the current stream keeps computing (RCCL runs on its
-    own stream)."""
+def start_count_exchange(counts_per_peer, group=None):
+    """Non-blocking all-to-all of k entry counts per peer (counts_per_peer: [world][k] ints): returns
+    a handle for finish_count_exchange, so the small exchange runs while the caller launches more
+    device work (the payload sizes are needed only when the payload exchange is posted)."""
     import torch
     import torch.distributed as dist
     dev = _comm_device(group)
-    sc = torch.tensor([int(c) for c in send_counts], dtype=torch.int64, device=dev)
+    sc = torch.tensor([[int(x) for x in row] for row in counts_per_peer], dtype=torch.int64, device=dev)
     rc = torch.empty_like(sc)
-    dist.all_to_all_single(rc, sc, group=group)
-    recv_counts = [int(x) for x in rc.tolist()]
+    work = dist.all_to_all_single(rc, sc, group=group, async_op=True)
+    return work, rc, sc
+
+
+def finish_count_exchange(handle):
+    """[world][k] counts received from every peer (host ints)."""
+    work, rc, _sc = handle
+    work.wait()
+    return [[int(x) for x in row] for row in rc.cpu().tolist()]
+
+
+def exchange_async(send, send_counts, group=None, recv_counts=None):
+    """exchange() with the payload all-to-all left in flight: without recv_counts the entry counts
+    are exchanged first (the receive size); the payload returns a handle. finish_exchange(handle)
+    waits and returns the received tensor; meanwhile the current stream keeps computing (RCCL runs
+    on its own stream, ordered after torch's current stream)."""
+    import torch
+    import torch.distributed as dist
+    dev = _comm_device(group)
+    if recv_counts is None:
+        sc = torch.tensor([int(c) for c in send_counts], dtype=torch.int64, device=dev)
+        rc = torch.empty_like(sc)
+        dist.all_to_all_single(rc, sc, group=group)
+        recv_counts = [int(x) for x in rc.tolist()]
     src = send if send.device == dev else send.to(dev)
     recv = torch.empty((sum(recv_counts),) + tuple(send.shape[1:]), dtype=send.dtype, device=dev)
     work = dist.all_to_all_single(recv, src.contiguous(), recv_counts, [int(c) for c in send_counts], group=group,
@@ -143,36 +164,55 @@ def table_from_records(recs, names, n_items: int, file_stats=None, ctx=None, str
     return CovisTable(h, names, ctx)
 
 
+class OwnerEmit:
+    """S1-S3 of this rank's files with owner-major rows (ottohip_covis_emit): words_per_owner and
+    pieces_per_owner are known when the constructor returns; write() runs S4 into fresh device
+    buffers (ottohip_emit_write) and returns (words int32 [P], pieces int64 [rows])."""
+
+    def __init__(self, events, n_parts: int, file_ids=None, n_files_total: int | None = None, names=None,
+                 n_items: int = config.N_ITEMS_OTTO, dedup: bool = True, stream=None, ctx=None):
+        from .covis import reference_rules
+        self.ctx = ctx or _lib.context()
+        self.names, rules = reference_rules(names)
+        p = _lib.CovisParams()
+        p.min_dt, p.max_dt, p.n_items, p.dedup = (config.MIN_TIME_TO_NEXT, config.MAX_TIME_TO_NEXT, int(n_items),
+                                                  int(dedup))
+        ev = events.abi()
+        nf = ev.n_files
+        fids = (ctypes.c_int32 * nf)(*(range(nf) if file_ids is None else [int(f) for f in file_ids]))
+        n_tot = nf if n_files_total is None else int(n_files_total)
+        self.h = ctypes.c_void_p()
+        wpp = (ctypes.c_int64 * n_parts)()
+        rpp = (ctypes.c_int64 * n_parts)()
+        self.sh = _lib.stream_handle(stream)
+        _lib.check(_lib.load().ottohip_covis_emit(self.ctx.h, ctypes.byref(ev), rules, len(self.names), ctypes.byref(p),
+                                                  fids, n_tot, n_parts, ctypes.byref(self.h), wpp, rpp, self.sh))
+        self._events = events  # the event buffers stay referenced until write()
+        self.words_per_owner, self.pieces_per_owner = list(wpp), list(rpp)
+
+    def write(self):
+        import torch
+        lib = _lib.load()
+        try:
+            dev = torch.device("cuda", self.ctx.device)
+            words = torch.empty(sum(self.words_per_owner), dtype=torch.int32, device=dev)
+            pieces = torch.empty(sum(self.pieces_per_owner), dtype=torch.int64, device=dev)
+            _lib.check(lib.ottohip_emit_write(self.h, _lib.ptr(words) if words.numel() else None,
+                                              _lib.ptr(pieces) if pieces.numel() else None, self.sh))
+        finally:
+            lib.ottohip_emit_free(self.h)
+            self.h = None
+            self._events = None
+        return words, pieces
+
+
 def emit_for_owners(events, n_parts: int, file_ids=None, n_files_total: int | None = None, names=None,
                     n_items: int = config.N_ITEMS_OTTO, dedup: bool = True, stream=None, ctx=None):
     """Pair words of this rank's files, laid out owner-major (ottohip_covis_emit + emit_write).
     Returns (words int32 [P], words_per_owner, pieces int64 [rows], pieces_per_owner, names)."""
-    import torch
-    from .covis import reference_rules
-    ctx = ctx or _lib.context()
-    names, rules = reference_rules(names)
-    p = _lib.CovisParams()
-    p.min_dt, p.max_dt, p.n_items, p.dedup = config.MIN_TIME_TO_NEXT, config.MAX_TIME_TO_NEXT, int(n_items), int(dedup)
-    ev = events.abi()
-    nf = ev.n_files
-    fids = (ctypes.c_int32 * nf)(*(range(nf) if file_ids is None else [int(f) for f in file_ids]))
-    n_tot = nf if n_files_total is None else int(n_files_total)
-    em = ctypes.c_void_p()
-    wpp = (ctypes.c_int64 * n_parts)()
-    rpp = (ctypes.c_int64 * n_parts)()
-    lib = _lib.load()
-    sh = _lib.stream_handle(stream)
-    _lib.check(lib.ottohip_covis_emit(ctx.h, ctypes.byref(ev), rules, len(names), ctypes.byref(p), fids, n_tot, n_parts,
-                                      ctypes.byref(em), wpp, rpp, sh))
-    try:
-        dev = torch.device("cuda", ctx.device)
-        words = torch.empty(sum(wpp), dtype=torch.int32, device=dev)
-        pieces = torch.empty(sum(rpp), dtype=torch.int64, device=dev)
-        _lib.check(lib.ottohip_emit_write(em, _lib.ptr(words) if words.numel() else None,
-                                          _lib.ptr(pieces) if pieces.numel() else None, sh))
-    finally:
-        lib.ottohip_emit_free(em)
-    return words, list(wpp), pieces, list(rpp), names
+    em = OwnerEmit(events, n_parts, file_ids, n_files_total, names, n_items, dedup, stream, ctx)
+    words, pieces = em.write()
+    return words, em.words_per_owner, pieces, em.pieces_per_owner, em.names
 
 
 def reduce_received(words, pieces, names, n_files_total: int, n_items: int = config.N_ITEMS_OTTO, dedup: bool = True,
@@ -304,16 +344,27 @@ def count_co_events_sharded(events, file_ids, n_files_total: int, group=None, na
     pending = []
     for c in range(len(bounds) - 1):
         f0, f1 = bounds[c], bounds[c + 1]
+        em = None
         if f1 > f0:
             sub = events if (f0, f1) == (0, nf) else events.subset_files(f0, f1)
-            words, wpp, pieces, ppp, names = emit_for_owners(sub, world, fids[f0:f1], n_files_total, names, n_items,
-                                                              dedup, stream, ctx)
+            em = OwnerEmit(sub, world, fids[f0:f1], n_files_total, names, n_items, dedup, stream, ctx)
+            wpp, ppp = em.words_per_owner, em.pieces_per_owner
         else:  # no files in this chunk (e.g. a rank without files of one part): it still joins the exchange
-            words, pieces = torch.empty(0, dtype=torch.int32, device=dev), torch.empty(0, dtype=torch.int64, device=dev)
             wpp, ppp = [0] * world, [0] * world
-        if stream is not None:
-            stream.synchronize()  # RCCL orders after the current stream, not a side stream
-        pending.append((exchange_async(words, wpp, group), exchange_async(pieces, ppp, group)))
+        # the receive sizes travel while S4 writes the words (no host wait on the exchange path
+        # beyond the library's own end-of-emit check)
+        cnt = start_count_exchange([[w, p] for w, p in zip(wpp, ppp)], group)
+        if em is not None:
+            words, pieces = em.write()
+        else:
+            words, pieces = torch.empty(0, dtype=torch.int32, device=dev), torch.empty(0, dtype=torch.int64, device=dev)
+        rc = finish_count_exchange(cnt)
+        if stream is not None and words.is_cuda:
+            # RCCL orders its work after torch's current stream: make that stream wait for the
+            # caller's stream (an event wait on the device, not a host synchronize)
+            torch.cuda.current_stream().wait_stream(stream)
+        pending.append((exchange_async(words, wpp, group, recv_counts=[r[0] for r in rc]),
+                        exchange_async(pieces, ppp, group, recv_counts=[r[1] for r in rc])))
         del words, pieces
     got = [(finish_exchange(hw), finish_exchange(hp)) for hw, hp in pending]
     del pending
@@ -350,8 +401,9 @@ def merge_tables_by_owner(events, group=None, names=None, n_items: int = config.
                                for r in range(len(names))], group)
     recs, counts = pack_by_owner(local, world, stream)
     local.free()
-    if stream is not None:
-        stream.synchronize()
+    if stream is not None and recs.is_cuda:
+        import torch
+        torch.cuda.current_stream().wait_stream(stream)  # RCCL orders after torch's current stream
     recv = exchange_records(recs, counts, group)
     del recs
     if stream is not None and recv.is_cuda:  # the exchange is ordered on torch's current stream only

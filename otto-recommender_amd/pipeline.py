@@ -203,6 +203,7 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
     rec = gcand.recall_from_sums(sums)
     t = mark("recall", t)
     out = {"pairs": int(pairs), "candidates": int(n_cand), "local_candidates": cands.n_cand,
+           "local_test_files": len(my_te),
            "test_sessions": int(test.n_sessions), "kmeans_iter": km.n_iter_, "kmeans_inertia": km.inertia_,
            "recall": rec, "timings_s": T}
     if keep_tables:  # host copies of every stage's output, for the parity tests

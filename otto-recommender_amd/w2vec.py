@@ -70,17 +70,19 @@ def load_index_faiss_ivff(embeddings, model_name: str | None = None) -> KnnIndex
 
 def word_rows(words, words_q) -> np.ndarray:
     """Row of each query word in the vocabulary `words` (-1 = not in it): the index lookup of
-    w2vec_aids.py:156-163 as one sorted search (any vocabulary size, no per-word host loop)."""
+    w2vec_aids.py:156-163 as one sorted search (any vocabulary size, no per-word host loop).
+    A word listed more than once maps to its LAST row, as the reference's dict(zip(words, ...))
+    keeps the last value of a duplicated key."""
     words = np.asarray(words, np.int64)
     wq = np.asarray(words_q, np.int64)
     if len(words) == 0:
         return np.full(len(wq), -1, np.int64)
     order = np.argsort(words, kind="stable")
     sw = words[order]
-    pos = np.searchsorted(sw, wq)
-    hit = pos < len(sw)
+    pos = np.searchsorted(sw, wq, side="right") - 1  # the last of equal words (stable order)
+    hit = pos >= 0
     hit[hit] = sw[pos[hit]] == wq[hit]
-    return np.where(hit, order[np.minimum(pos, max(len(sw) - 1, 0))], -1).astype(np.int64)
+    return np.where(hit, order[np.maximum(pos, 0)], -1).astype(np.int64)
 
 
 def get_top_k_similar_faiss(words_q, words, map_word_embedding=None, index_faiss_ivff=None, k: int = 20,

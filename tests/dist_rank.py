@@ -85,6 +85,7 @@ def pipeline(out, cfg):
                  per_file=cfg["per_file"])
     im = res["intermediates"]
     o = {"candidates_total": np.array([res["candidates"], res["local_candidates"]], np.int64),
+         "n_test_files": np.array([res.get("local_test_files", -1)], np.int64),
          "recall": np.array([res["recall"][t][k] for t in ("clicks", "carts", "orders", "total")
                              for k in ("top20", "top100", "top200", "topall")]),
          "cluster_labels": im["cluster_labels"], "cluster_rows": im["cluster_rows"],

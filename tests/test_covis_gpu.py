@@ -268,6 +268,77 @@ def test_click_to_click_symmetry_and_determinism(gpu):
             np.testing.assert_array_equal(x, y)
 
 
+def test_two_symmetric_rules_of_one_type(gpu, monkeypatch):
+    """Two click->click windows (12 h and 1 h) in one call: both are symmetric (next types == {click},
+    dt window symmetric), but only one rule per event type may be stored once (k_emit places the
+    symmetric record after the event's other records). Every table must equal the oracle's."""
+    from otto_recommender_amd import config as cfg
+    monkeypatch.setitem(cfg.MAP_NAME_COUNT_TYPE, "click_to_click_1h", (0, [0]))
+    monkeypatch.setitem(cfg.MAP_MAX_TIME_TO_NEXT, "click_to_click_1h", 3600)
+    names = ["click_to_click", "click_to_click_1h", "click_to_cart_or_buy"]
+    ev = synth.generate(20_000, first_session=777)
+    fb = synth.file_session_bounds(ev.n_sessions, per_file=5_000)
+    tab = _gpu_tables(ev, fb, names=names)
+    rules = {"click_to_click": oracle.REFERENCE_RULES["click_to_click"], "click_to_click_1h": (0, (0,), 3600),
+             "click_to_cart_or_buy": oracle.REFERENCE_RULES["click_to_cart_or_buy"]}
+    per_file = oracle.count_co_events_files(ev.session_offsets, ev.aid, ev.ts, ev.type, fb, rules=rules)
+    for n in names:
+        a = np.concatenate([p[n][0] for p in per_file]); b = np.concatenate([p[n][1] for p in per_file])
+        c = np.concatenate([p[n][2] for p in per_file]).astype(np.int64)
+        ra, rb, rc = oracle._groupby_sum(a, b, c)
+        _, _, rg = oracle._groupby_sum(a, b, np.where(c >= 2, c, 0))
+        ga, gb, gc_, g2 = tab.to_numpy(n)
+        for x, y in ((ga, ra), (gb, rb), (gc_, rc), (g2, rg)):
+            np.testing.assert_array_equal(x.astype(np.int64), y, err_msg=n)
+        st = tab.stats(n)
+        assert (st["n_rows"], st["n_pairs"], st["file_rows"]) == (len(ra), int(rc.sum()), len(a)), n
+    assert len(per_file[0]["click_to_click_1h"][0]) < len(per_file[0]["click_to_click"][0])
+    tab.free()
+
+
+def test_emit_record_guard_dense_sessions(gpu, monkeypatch):
+    """Sessions built so that every event of a batch opens a record in every (rule, next type) round
+    (62 clicks + a cart + a buy within an hour: each click has a click_to_click and two
+    click_to_cart_or_buy windows), so the emit flushes its record arrays as often as it can. With
+    OTTOHIP_DEBUG the emit checks every record index against the flush's records (err bit 8); the
+    tables must equal the oracle's."""
+    monkeypatch.setenv("OTTOHIP_DEBUG", "1")
+    rng = np.random.default_rng(3)
+    rows = []
+    for s_ in range(600):
+        ty = np.zeros(64, np.int64); ty[rng.choice(64, 2, replace=False)] = [1, 2]
+        aid = rng.choice(50_000, 64, replace=False)
+        ts = np.sort(rng.integers(0, 3600, 64))
+        rows.append(np.stack([np.full(64, s_), aid, ts, ty], 1))
+    a = np.concatenate(rows)
+    ev = synth.events_from_columns(a[:, 0], a[:, 1], a[:, 2], a[:, 3])
+    _assert_single_file(ev)
+
+
+def test_per_file_rows_beyond_1024_files(gpu):
+    """count_co_events_fused with per-file statistics over more files than the per-file histogram
+    holds (1024), on a small item vocabulary (a pair word could tell 2^21 files apart): the call runs
+    in batches of <= 1024 files and reports every file's rows."""
+    from otto_recommender_amd import covis as gc
+    rng = np.random.default_rng(11)
+    n_s = 1100 * 4
+    lens = rng.integers(2, 9, n_s)
+    sess = np.repeat(np.arange(n_s), lens)
+    aid = rng.integers(0, 900, len(sess))
+    ts = np.concatenate([np.sort(rng.integers(0, 40_000, k)) for k in lens])
+    ev = synth.events_from_columns(sess, aid, ts, np.zeros(len(sess), np.int64))
+    fb = synth.file_session_bounds(ev.n_sessions, per_file=4)
+    assert len(fb) - 1 == 1100
+    n = "click_to_click"
+    dev = gc.DeviceEvents.from_host(ev, fb)
+    t = gc.count_co_events_fused(dev, [n], n_items=1000, cuts=gc.FileCuts(n, per_file=True))
+    per_file = oracle.count_co_events_files(ev.session_offsets, ev.aid, ev.ts, ev.type, fb,
+                                            rules={n: oracle.REFERENCE_RULES[n]})
+    np.testing.assert_array_equal(t.file_rows_per_file, [len(p[n][0]) for p in per_file])
+    np.testing.assert_array_equal(t.file_rows_ge2_per_file, [int((p[n][2] >= 2).sum()) for p in per_file])
+    t.free()
+
+
 def test_finalize_matches_merge_restatement(gpu):
     ev = synth.generate(300_000)
     fb = synth.file_session_bounds(ev.n_sessions)

@@ -94,9 +94,40 @@ def test_covis_sharded_four_ranks(gpu, tmp_path):
     assert len(set(_owner(full[0][full[2] == cstar], 4).tolist())) >= 3
 
 
-def _check_covis_sharded(cfg, tmp_path, world):
+def test_covis_sharded_eight_ranks(gpu, tmp_path):
+    """BASELINE configs[3] at world 8 (8 fresh rank processes on cuda:0, gloo): the G = 8 owner hash,
+    an 8-way all-to-all-v of pair words and row pieces, branch (2) parts of a few files each (most
+    ranks hold no file of a given part; the boundary keys come from the file's holder), and the global
+    head cut on a count whose ties live on >= 5 of the 8 owners; every shard, final table and slice
+    set against the oracle (model/count_co_events.py:103-181)."""
+    from otto_recommender_amd.covis import part_plan
+    cfg = {"sessions": 32_000, "per_file": 1_000, "first_session": 424_242,
+           "merges": {
+               "scaled": {"click_filter_rows": 10**9, "max_rows_groupby": 1_500_000, "optim_rows": 700_000,
+                          "max_pairs": 3_000},
+               "filtered": {"click_filter_rows": 100_000, "max_rows_groupby": 250_000, "optim_rows": 120_000,
+                            "max_pairs": 8_000}}}
+    res, per_file = _check_covis_sharded(cfg, tmp_path, world=8, timeout=420)
+    files_of = [set(r["files"].tolist()) for r in res]
+    n = "click_to_click"
+    for tag in ("scaled", "filtered"):
+        kw = cfg["merges"][tag]
+        use_ge2 = sum(len(p[n][0]) for p in per_file) > kw["click_filter_rows"]
+        R = np.array([int((p[n][2] >= 2).sum()) if use_ge2 else len(p[n][0]) for p in per_file])
+        assert R.sum() > kw["max_rows_groupby"], tag  # branch (2) is taken
+        plan = part_plan(R, -(-int(R.sum()) // kw["optim_rows"]))
+        idle = sum(1 for fa, _, fb, _ in plan for f in files_of if not f & set(range(fa, fb + 1)))
+        assert len(plan) > 2 and idle > len(plan), tag
+    # ties at the global cut spread over >= 5 owners
+    kw = cfg["merges"]["scaled"]
+    full = oracle.concat_files_w_stats(n, [p[n] for p in per_file], **dict(kw, max_pairs=10**9))
+    cstar = int(full[2][kw["max_pairs"] - 1])
+    assert len(set(_owner(full[0][full[2] == cstar], 8).tolist())) >= 5
+
+
+def _check_covis_sharded(cfg, tmp_path, world, timeout=240):
     import otto_recommender_amd.synth as synth
-    res = _launch("covis", cfg, tmp_path, world=world)
+    res = _launch("covis", cfg, tmp_path, world=world, timeout=timeout)
     ev = synth.generate(cfg["sessions"], first_session=cfg["first_session"])
     fb = synth.file_session_bounds(ev.n_sessions, per_file=cfg["per_file"])
     per_file = oracle.count_co_events_files(ev.session_offsets, ev.aid, ev.ts, ev.type, fb)
@@ -132,11 +163,25 @@ def test_pipeline_two_ranks_equals_one_gpu(gpu, tmp_path):
     sums, C3 counters all-reduced, candidates per rank. Every shard-level output must equal the
     1-GPU run on the same input: A7 tables, kNN lists, cluster labels, pop lists, the union of
     the per-rank candidates, and recall."""
-    import otto_recommender_amd.synth as synth
-    from otto_recommender_amd import pipeline as pl
     cfg = {"sessions": 30_000, "first_session": 808, "clusters": 6, "iters": 15, "queries": 20_000, "n_init": 2,
            "per_file": 2_500}
-    res = _launch("pipeline", cfg, tmp_path, timeout=400)
+    _check_pipeline_ranks(cfg, tmp_path, world=2)
+
+
+def test_pipeline_eight_ranks_equals_one_gpu(gpu, tmp_path):
+    """BASELINE configs[4] at world 8 (8 fresh rank processes on cuda:0): the same checks as the
+    2-rank test, with files small enough that every rank holds train files and some rank holds no
+    test file (no candidate sessions of its own)."""
+    cfg = {"sessions": 24_000, "first_session": 9090, "clusters": 6, "iters": 12, "queries": 16_000, "n_init": 2,
+           "per_file": 1_000}
+    res = _check_pipeline_ranks(cfg, tmp_path, world=8)
+    assert min(int(r["n_test_files"][0]) for r in res) == 0  # a rank without test files (no candidates of its own)
+
+
+def _check_pipeline_ranks(cfg, tmp_path, world):
+    import otto_recommender_amd.synth as synth
+    from otto_recommender_amd import pipeline as pl
+    res = _launch("pipeline", cfg, tmp_path, world=world, timeout=400)
     ev = synth.generate(cfg["sessions"], first_session=cfg["first_session"])
     train, test, labels = synth.split_test_labels(ev)
     words = synth.item_words()
@@ -166,3 +211,4 @@ def test_pipeline_two_ranks_equals_one_gpu(gpu, tmp_path):
     ref = ref[np.lexsort((ref[:, 1], ref[:, cols.index("ts_order_aid")], ref[:, 0]))]
     np.testing.assert_array_equal(got, ref)
     assert sum(int(r["candidates_total"][1]) for r in res) == one["candidates"]
+    return res

@@ -34,3 +34,18 @@ def test_word_rows_lookup():
     np.testing.assert_array_equal(words[got[6:]], q[6:])
     assert want[int(words[3])] == 3
     assert (word_rows(np.zeros(0, np.int64), q[:4]) == -1).all()
+
+
+def test_duplicate_keys_take_the_last_row():
+    """Duplicated vocabulary words / session rows resolve to their LAST row, as the reference's
+    dict lookups do (w2vec.word_rows, candidates.session_cluster_index)."""
+    import pandas as pd
+    from otto_recommender_amd.w2vec import word_rows
+    from otto_recommender_amd.candidates import session_cluster_index
+    words = np.array([40, 10, 40, 30, 10, 10], np.int64)
+    np.testing.assert_array_equal(word_rows(words, [10, 40, 30, 20]), [5, 2, 3, -1])
+    df = pd.DataFrame({"session": [7, 3, 7, 9, 5], "cl50": [1.0, 4.0, 2.0, np.nan, 1.0]})
+    clusters = np.array([1.0, 2.0, 4.0])
+    np.testing.assert_array_equal(session_cluster_index(df, clusters, np.array([7, 3, 9, 5, 8])), [1, 2, -1, 0, -1])
+    empty = df.iloc[:0]
+    np.testing.assert_array_equal(session_cluster_index(empty, clusters, np.array([7])), [-1])
