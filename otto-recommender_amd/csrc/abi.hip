@@ -454,8 +454,8 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   memset(&fo, 0, sizeof fo);
   if (fopts) OH_TRY(file_opts_setup(ctx, fopts, n_rules, R, fo, s));
   const bool FOon = fopts != nullptr;
-  // symmetric rules: slots [P, 2P) hold the mirror (aid_next, aid) of the row at slot - P, or a hole
-  const uint64_t n_slots = R.sym_mask ? 2 * P : P;
+  // symmetric rules store one row per unordered pair; the readers produce the mirrors (T->sym_mask)
+  const uint64_t n_slots = P;
   if (ctx->spare.cap >= n_slots) {
     T->b = ctx->spare;
     ctx->spare = TableBufs();
@@ -476,7 +476,8 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   if (getenv("OTTOHIP_REDUCE_DBG")) hipMemsetAsync(T->b.rule, 0xFF, n_slots, s);
   OutRows O;
   O.rule = T->b.rule; O.aid = T->b.aid; O.aid_next = T->b.aid_next; O.count = T->b.count; O.count_ge2 = T->b.count_ge2;
-  O.cap = P; O.stats = stats; O.mirror = R.sym_mask ? P : 0;
+  O.cap = P; O.stats = stats;
+  T->sym_mask = R.sym_mask;
   // profiling ablation: OTTOHIP_REDUCE_DBG=1 drops the register-sort kernels' row stores
   static const int rdbg = getenv("OTTOHIP_REDUCE_DBG") ? atoi(getenv("OTTOHIP_REDUCE_DBG")) : 0;
   OutRows Osort = O;
@@ -1035,10 +1036,11 @@ int ottohip_table_copy(const ottohip_table* t, int rule, int32_t* aid, int32_t* 
   uint64_t* boff;
   OH_TRY(ctx->ws.get("blk_cnt", (size_t)nb, &bcnt));
   OH_TRY(ctx->ws.get("blk_off", (size_t)nb, &boff));
-  k_blk_count<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.count, t->b.count_ge2, n, rule, 0, 0u, bcnt);
+  k_blk_count<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n, rule, 0, 0u,
+                                             t->sym(rule), bcnt);
   OH_TRY(exclusive_scan_u32(ctx, bcnt, boff, nb, nullptr, s));
   k_blk_compact<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n,
-                                               rule, 0, 0u, boff, reinterpret_cast<uint32_t*>(aid),
+                                               rule, 0, 0u, t->sym(rule), boff, reinterpret_cast<uint32_t*>(aid),
                                                reinterpret_cast<uint32_t*>(aid_next), count, count_ge2);
   OH_HIP(hipGetLastError());
   return 0;
@@ -1071,8 +1073,8 @@ int ottohip_table_keys_at(ottohip_ctx* ctx, const ottohip_table* t, int rule, in
   uint64_t m = 0;
   if (t->n_rows > 0 && n > 0) {
     // rows of the rule (use_ge2: per-file count >= 2, i.e. count_ge2 >= 1)
-    k_blk_count<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.count, t->b.count_ge2, n, rule, use_ge2 ? 1 : 0,
-                                               use_ge2 ? 1u : 0u, bcnt);
+    k_blk_count<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n, rule,
+                                               use_ge2 ? 1 : 0, use_ge2 ? 1u : 0u, t->sym(rule), bcnt);
     OH_TRY(exclusive_scan_u32(ctx, bcnt, boff, nb, tot, s));
     OH_TRY(d2h(&m, tot, 1, s));
   }
@@ -1093,8 +1095,8 @@ int ottohip_table_keys_at(ottohip_ctx* ctx, const ottohip_table* t, int rule, in
   OH_TRY(ws.get("ka_idx", (size_t)n_idx, &didx));
   OH_TRY(ws.get("ka_keys", (size_t)n_idx, &dkeys));
   k_blk_compact<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n,
-                                               rule, use_ge2 ? 1 : 0, use_ge2 ? 1u : 0u, boff, sa, sb, nullptr,
-                                               nullptr);
+                                               rule, use_ge2 ? 1 : 0, use_ge2 ? 1u : 0u, t->sym(rule), boff, sa, sb,
+                                               nullptr, nullptr);
   // LSD: aid_next, then aid (stable) -> (aid, aid_next) ascending
   const int abits = std::max(1, bits_for((uint64_t)t->n_items));
   uint32_t *k = k0, *v = v0;
@@ -1155,8 +1157,8 @@ extern "C" int ottohip_table_finalize(ottohip_ctx* ctx, const ottohip_table* t, 
   OH_TRY(ws.get("blk_cnt", (size_t)nb, &bcnt));
   OH_TRY(ws.get("blk_off", (size_t)nb, &boff));
   OH_TRY(ws.get("fin_tot", 1, &tot));
-  k_blk_count<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.count, t->b.count_ge2, n, rule, use_ge2 ? 1 : 0, thr,
-                                             bcnt);
+  k_blk_count<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n, rule,
+                                             use_ge2 ? 1 : 0, thr, t->sym(rule), bcnt);
   OH_TRY(exclusive_scan_u32(ctx, bcnt, boff, nb, tot, s));
   uint64_t m = 0;
   OH_TRY(d2h(&m, tot, 1, s));
@@ -1170,7 +1172,7 @@ extern "C" int ottohip_table_finalize(ottohip_ctx* ctx, const ottohip_table* t, 
   OH_TRY(ws.get("fin_k1", (size_t)m, &k1));
   OH_TRY(ws.get("fin_v1", (size_t)m, &v1));
   k_blk_compact<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n,
-                                               rule, use_ge2 ? 1 : 0, thr, boff, sa, sb, sc, nullptr);
+                                               rule, use_ge2 ? 1 : 0, thr, t->sym(rule), boff, sa, sb, sc, nullptr);
   // LSD: aid_next asc, then aid asc, then count desc (stable) -> (count desc, aid, aid_next);
   // aids are < n_items, so their passes cover bits_for(n_items) bits (3 x 8 at 1.86 M items)
   const int abits = std::max(1, bits_for((uint64_t)t->n_items));

@@ -45,7 +45,9 @@ struct RulesDev {
   // Symmetric rules (next types == {this type}, window symmetric in dt: click_to_click, cart_to_cart,
   // buy_to_buy): every qualifying ordered pair (i, j) has its mirror (j, i), so count(a, b) ==
   // count(b, a) per session, per file and in total. Only pairs with aid_j >= aid_i are emitted
-  // (both orders of equal aids); each leaf writes the mirror (b, a) of every row with a < b.
+  // (both orders of equal aids) and only the row (a, b), a <= b, is stored: the table's readers
+  // (compaction, digest, owner packing) produce the mirror (b, a) of every stored row with a < b
+  // (ottohip_table::sym_mask).
   uint32_t sym_mask;
 };
 
@@ -86,7 +88,6 @@ struct OutRows {
   uint32_t* count_ge2;
   uint64_t cap;
   unsigned long long* stats;  // [STAT_STRIPES][STAT_STRIDE]
-  uint64_t mirror;            // symmetric rules: the mirror (b, a) of the row at slot p goes to slot mirror + p
 };
 
 // Per-file options of one rule (ottohip_file_opts; A6 branch (2) by rows, count_co_events.py:136-158):
@@ -1152,14 +1153,9 @@ __device__ __forceinline__ RowInfo row_info(const uint32_t* row_key, uint32_t ro
 }
 
 __device__ __forceinline__ void put_row(const OutRows& O, uint64_t p, int rule, int32_t aid, int32_t next,
-                                        uint32_t c, uint32_t c2, bool mirror) {
+                                        uint32_t c, uint32_t c2) {
   if (p < O.cap) {
     O.rule[p] = (uint8_t)rule; O.aid[p] = aid; O.aid_next[p] = next; O.count[p] = c; O.count_ge2[p] = c2;
-  }
-  if (O.mirror) {  // the mirror region of a symmetric table: (aid_next, aid) or a hole
-    const uint64_t m = O.mirror + p;
-    O.rule[m] = mirror ? (uint8_t)rule : (uint8_t)0xFF;
-    if (mirror) { O.aid[m] = next; O.aid_next[m] = aid; O.count[m] = c; O.count_ge2[m] = c2; }
   }
 }
 
@@ -1494,18 +1490,9 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
         o_next[i] = next;
         o_cnt[i] = bb & 0xFFFFu;
         o_c2[i] = bb >> 16;
-        if (O.mirror) {  // the mirror region: (aid_next, aid) of a symmetric rule's off-diagonal row, else a hole
-          const uint64_t mi = O.mirror + T.begin + i;
-          const bool mr = rule_sym(sR, rule) && next != aid;
-          O.rule[mi] = mr ? (uint8_t)rule : (uint8_t)0xFF;
-          if (mr) { O.aid[mi] = next; O.aid_next[mi] = aid; O.count[mi] = bb & 0xFFFFu; O.count_ge2[mi] = bb >> 16; }
-        }
       }
     if (store)  // the rest of the task's word range holds no row (marked here, no table-wide fill)
-      for (uint32_t i = nout + l; i < T.len; i += 64) {
-        o_rule[i] = 0xFF;
-        if (O.mirror) O.rule[O.mirror + T.begin + i] = 0xFF;
-      }
+      for (uint32_t i = nout + l; i < T.len; i += 64) o_rule[i] = 0xFF;
     for (int q = 0; q < (nq < 2 ? nq : 2); ++q) {
       const uint32_t sa = wave_sum(q == 0 ? s0a : s1a), sb = wave_sum(q == 0 ? s0b : s1b);
       if (l == 0 && sa) {
@@ -1779,16 +1766,13 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
       const uint32_t c = (uint32_t)v, c2 = (uint32_t)(v2 >> 32), nf = (uint32_t)v2;
       const int32_t next = (int32_t)(k2 & L.amask);
       const bool mr = rule_sym(R, rule) && next != ri.aid;
-      put_row(O, p++, rule, ri.aid, next, c, c2, mr);
+      put_row(O, p++, rule, ri.aid, next, c, c2);
       acc.add(rule, c, nf, mr ? 2u : 1u);
     }
     // the rest of the task's word range holds no row (no table-wide fill: every word position
     // belongs to exactly one leaf task, sort or hash)
     const uint32_t nout = wtot[0] + wtot[1] + wtot[2] + wtot[3];
-    for (uint32_t i = nout + tid; i < T.len; i += AGG_T) {
-      O.rule[T.begin + i] = 0xFF;
-      if (O.mirror) O.rule[O.mirror + T.begin + i] = 0xFF;
-    }
+    for (uint32_t i = nout + tid; i < T.len; i += AGG_T) O.rule[T.begin + i] = 0xFF;
     __syncthreads();
     if (fo.prof && tid == 0) {
       fo.prof[2 * ti] = T.len | ((unsigned long long)nout << 32);
@@ -2100,7 +2084,9 @@ __global__ void k_split_classify(const Task* __restrict__ tasks, int64_t n, cons
 // One rule's rows of a table, compacted in slot order without per-slot flag / index arrays:
 // per 4096-slot block a count (k_blk_count), one scan over the blocks, and a compaction that
 // re-evaluates the predicate with wave ballots and block prefixes (k_blk_compact). The predicate is
-// rule == r and, with thr > 0, (use_ge2 ? count_ge2 : count) >= thr.
+// rule == r and, with thr > 0, (use_ge2 ? count_ge2 : count) >= thr. sym: the rule's rows are stored
+// once (aid <= aid_next); a kept row with aid != aid_next stands for itself and its mirror
+// (aid_next, aid), written right after it.
 constexpr int FIN_T = 256, FIN_PER = 16, FIN_B = FIN_T * FIN_PER;
 __device__ __forceinline__ bool blk_keep(const uint8_t* __restrict__ rule, const uint32_t* __restrict__ c,
                                          const uint32_t* __restrict__ c2, int64_t i, int r, int use_ge2,
@@ -2108,16 +2094,17 @@ __device__ __forceinline__ bool blk_keep(const uint8_t* __restrict__ rule, const
   if (rule[i] != (uint8_t)r) return false;
   return thr == 0 || (use_ge2 ? c2[i] : c[i]) >= thr;
 }
-__global__ __launch_bounds__(FIN_T) void k_blk_count(const uint8_t* __restrict__ rule, const uint32_t* __restrict__ c,
+__global__ __launch_bounds__(FIN_T) void k_blk_count(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
+                                                     const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
                                                      const uint32_t* __restrict__ c2, int64_t n, int r, int use_ge2,
-                                                     uint32_t thr, uint32_t* __restrict__ bcnt) {
+                                                     uint32_t thr, int sym, uint32_t* __restrict__ bcnt) {
   __shared__ uint32_t wt[FIN_T / 64];
   const int64_t base = (int64_t)blockIdx.x * FIN_B;
   uint32_t k = 0;
 #pragma unroll 4
   for (int q = 0; q < FIN_PER; ++q) {
     const int64_t i = base + q * FIN_T + threadIdx.x;
-    k += (i < n && blk_keep(rule, c, c2, i, r, use_ge2, thr)) ? 1u : 0u;
+    if (i < n && blk_keep(rule, c, c2, i, r, use_ge2, thr)) k += (sym && a[i] != b[i]) ? 2u : 1u;
   }
   k = wave_sum(k);
   if ((threadIdx.x & 63) == 0) wt[threadIdx.x >> 6] = k;
@@ -2128,7 +2115,7 @@ __global__ __launch_bounds__(FIN_T) void k_blk_count(const uint8_t* __restrict__
 __global__ __launch_bounds__(FIN_T) void k_blk_compact(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
                                                        const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
                                                        const uint32_t* __restrict__ c2, int64_t n, int r, int use_ge2,
-                                                       uint32_t thr, const uint64_t* __restrict__ boff,
+                                                       uint32_t thr, int sym, const uint64_t* __restrict__ boff,
                                                        uint32_t* __restrict__ o0, uint32_t* __restrict__ o1,
                                                        uint32_t* __restrict__ o2, uint32_t* __restrict__ o3) {
   __shared__ uint32_t wt[FIN_T / 64];
@@ -2138,18 +2125,27 @@ __global__ __launch_bounds__(FIN_T) void k_blk_compact(const uint8_t* __restrict
   for (int q = 0; q < FIN_PER; ++q) {
     const int64_t i = base + q * FIN_T + threadIdx.x;
     const bool keep = i < n && blk_keep(rule, c, c2, i, r, use_ge2, thr);
-    const uint64_t bal = __ballot(keep);
-    if ((threadIdx.x & 63) == 0) wt[w] = (uint32_t)__popcll(bal);
+    const uint32_t ai = keep ? (uint32_t)a[i] : 0u, bi = keep ? (uint32_t)b[i] : 0u;
+    const bool mir = keep && sym && ai != bi;
+    const uint64_t bal = __ballot(keep), bm = __ballot(mir);
+    if ((threadIdx.x & 63) == 0) wt[w] = (uint32_t)(__popcll(bal) + __popcll(bm));
     __syncthreads();
     uint32_t pre = 0, tot = 0;
 #pragma unroll
     for (int k = 0; k < FIN_T / 64; ++k) { pre += k < w ? wt[k] : 0u; tot += wt[k]; }
     if (keep) {
-      const uint64_t p = run + pre + mbcnt(bal);
-      if (o0) o0[p] = (uint32_t)a[i];
-      if (o1) o1[p] = (uint32_t)b[i];
-      if (o2) o2[p] = use_ge2 ? c2[i] : c[i];
-      if (o3) o3[p] = c2[i];
+      const uint64_t p = run + pre + mbcnt(bal) + mbcnt(bm);
+      const uint32_t cv = use_ge2 ? c2[i] : c[i], gv = o3 ? c2[i] : 0u;
+      if (o0) o0[p] = ai;
+      if (o1) o1[p] = bi;
+      if (o2) o2[p] = cv;
+      if (o3) o3[p] = gv;
+      if (mir) {
+        if (o0) o0[p + 1] = bi;
+        if (o1) o1[p + 1] = ai;
+        if (o2) o2[p + 1] = cv;
+        if (o3) o3[p + 1] = gv;
+      }
     }
     run += tot;
     __syncthreads();  // wt is rewritten by the next chunk

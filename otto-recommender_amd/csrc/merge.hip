@@ -63,14 +63,20 @@ __global__ __launch_bounds__(256) void k_table_digest(const uint8_t* __restrict_
                                                       const int32_t* __restrict__ aid_next,
                                                       const uint32_t* __restrict__ count,
                                                       const uint32_t* __restrict__ count_ge2, int64_t n, int r,
-                                                      unsigned long long* __restrict__ out) {
+                                                      int sym, unsigned long long* __restrict__ out) {
   uint64_t d[5] = {0, 0, 0, 0, 0};
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     if (rule[i] != (uint8_t)r) continue;
     const uint64_t c = count[i], g = count_ge2[i];
-    d[0] += row_mix((uint64_t)r, (uint32_t)aid[i], (uint32_t)aid_next[i], 1) * c;
-    d[1] += row_mix((uint64_t)r, (uint32_t)aid[i], (uint32_t)aid_next[i], 2) * g;
+    const uint32_t a = (uint32_t)aid[i], b = (uint32_t)aid_next[i];
+    d[0] += row_mix((uint64_t)r, a, b, 1) * c;
+    d[1] += row_mix((uint64_t)r, a, b, 2) * g;
     d[2] += c; d[3] += g; d[4] += 1;
+    if (sym && a != b) {  // the mirror (b, a) of a row stored once
+      d[0] += row_mix((uint64_t)r, b, a, 1) * c;
+      d[1] += row_mix((uint64_t)r, b, a, 2) * g;
+      d[2] += c; d[3] += g; d[4] += 1;
+    }
   }
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
@@ -230,7 +236,7 @@ extern "C" int ottohip_table_digest(ottohip_ctx* ctx, const ottohip_table* t, in
   OH_HIP(hipMemsetAsync(d, 0, 5 * 8, s));
   if (t->n_slots > 0)
     k_table_digest<<<(unsigned)std::min<int64_t>(ceil_div(t->n_slots, 256), (int64_t)ctx->n_cu * 8), 256, 0, s>>>(
-        t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, t->n_slots, rule, d);
+        t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, t->n_slots, rule, t->sym(rule), d);
   OH_HIP(hipGetLastError());
   OH_TRY(d2h(reinterpret_cast<unsigned long long*>(out), d, 5, s));
   return 0;

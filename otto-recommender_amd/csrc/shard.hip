@@ -23,7 +23,10 @@ constexpr uint32_t REC_AID_MASK = (1u << 29) - 1u;
 
 // per block, rows per owner -> cnt[owner * nblk + block] (owner-major, so one exclusive scan
 // gives every block's base offset inside every owner's segment)
+// sym_mask: rules whose rows are stored once (aid <= aid_next); a stored row with aid != aid_next
+// also yields its mirror record (aid_next, aid), which goes to owner(aid_next)
 __global__ __launch_bounds__(PK_T) void k_own_hist(const uint8_t* __restrict__ rule, const int32_t* __restrict__ aid,
+                                                   const int32_t* __restrict__ aid_next, uint32_t sym_mask,
                                                    int64_t n, uint32_t P, uint32_t* __restrict__ cnt, int64_t nblk) {
   __shared__ uint32_t h[PK_MAXP];
   for (int i = threadIdx.x; i < (int)P; i += PK_T) h[i] = 0;
@@ -32,7 +35,14 @@ __global__ __launch_bounds__(PK_T) void k_own_hist(const uint8_t* __restrict__ r
 #pragma unroll 4
   for (int j = 0; j < PK_PER; ++j) {
     const int64_t i = base + j * PK_T + threadIdx.x;
-    if (i < n && rule[i] != 0xFF) atomicAdd(&h[owner_dev((uint32_t)aid[i], P)], 1u);
+    if (i < n && rule[i] != 0xFF) {
+      const uint32_t a = (uint32_t)aid[i];
+      atomicAdd(&h[owner_dev(a, P)], 1u);
+      if ((sym_mask >> rule[i]) & 1u) {
+        const uint32_t b = (uint32_t)aid_next[i];
+        if (a != b) atomicAdd(&h[owner_dev(b, P)], 1u);
+      }
+    }
   }
   __syncthreads();
   for (int o = threadIdx.x; o < (int)P; o += PK_T) cnt[(int64_t)o * nblk + blockIdx.x] = h[o];
@@ -41,7 +51,8 @@ __global__ __launch_bounds__(PK_T) void k_own_hist(const uint8_t* __restrict__ r
 __global__ __launch_bounds__(PK_T) void k_own_scatter(const uint8_t* __restrict__ rule, const int32_t* __restrict__ aid,
                                                       const int32_t* __restrict__ aid_next,
                                                       const uint32_t* __restrict__ count,
-                                                      const uint32_t* __restrict__ count_ge2, int64_t n, uint32_t P,
+                                                      const uint32_t* __restrict__ count_ge2, uint32_t sym_mask,
+                                                      int64_t n, uint32_t P,
                                                       const uint64_t* __restrict__ off, int64_t nblk,
                                                       uint4* __restrict__ out) {
   __shared__ uint32_t cur[PK_MAXP];
@@ -52,9 +63,14 @@ __global__ __launch_bounds__(PK_T) void k_own_scatter(const uint8_t* __restrict_
   for (int j = 0; j < PK_PER; ++j) {
     const int64_t i = base + j * PK_T + threadIdx.x;
     if (i < n && rule[i] != 0xFF) {
-      const uint32_t a = (uint32_t)aid[i], o = owner_dev(a, P);
+      const uint32_t a = (uint32_t)aid[i], o = owner_dev(a, P), b = (uint32_t)aid_next[i], r = rule[i];
+      const uint32_t c = count[i], g = count_ge2[i];
       const uint64_t pos = off[(int64_t)o * nblk + blockIdx.x] + atomicAdd(&cur[o], 1u);
-      out[pos] = make_uint4(((uint32_t)rule[i] << 29) | a, (uint32_t)aid_next[i], count[i], count_ge2[i]);
+      out[pos] = make_uint4((r << 29) | a, b, c, g);
+      if (((sym_mask >> r) & 1u) && a != b) {
+        const uint32_t ob = owner_dev(b, P);
+        out[off[(int64_t)ob * nblk + blockIdx.x] + atomicAdd(&cur[ob], 1u)] = make_uint4((r << 29) | b, a, c, g);
+      }
     }
   }
 }
@@ -179,9 +195,11 @@ int ottohip_table_pack_by_owner(ottohip_ctx* ctx, const ottohip_table* t, int n_
   OH_TRY(ws.get("pk_tot", 1, &tot));
   OH_TRY(ws.get("pk_starts", (size_t)n_parts + 1, &starts));
   int ph = ctx->begin("pack", s, 17.0 * n + 16.0 * t->n_rows);
-  k_own_hist<<<(unsigned)nblk, PK_T, 0, s>>>(t->b.rule, t->b.aid, n, (uint32_t)n_parts, cnt, nblk);
+  k_own_hist<<<(unsigned)nblk, PK_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->sym_mask, n, (uint32_t)n_parts, cnt,
+                                             nblk);
   OH_TRY(exclusive_scan_u32(ctx, cnt, off, nblk * n_parts, tot, s));
-  k_own_scatter<<<(unsigned)nblk, PK_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n,
+  k_own_scatter<<<(unsigned)nblk, PK_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2,
+                                                 t->sym_mask, n,
                                                  (uint32_t)n_parts, off, nblk, reinterpret_cast<uint4*>(out_records));
   k_part_starts<<<grid_for(n_parts + 1), 256, 0, s>>>(off, nblk, (uint32_t)n_parts, tot, starts);
   OH_HIP(hipGetLastError());

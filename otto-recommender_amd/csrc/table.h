@@ -48,6 +48,8 @@ struct ottohip_table {
   int64_t n_rows = 0;   // valid rows (sum over rules)
   int64_t n_slots = 0;  // entries of the row arrays; holes carry rule = 0xFF
   TableBufs b;
+  uint32_t sym_mask = 0;  // rules stored once per unordered pair (aid <= aid_next): readers add the mirrors
+  int sym(int rule) const { return (int)((sym_mask >> rule) & 1u); }
   ottohip_rule_stats stats[MAX_RULES];
   ottohip_ctx* ctx = nullptr;
 };

@@ -7,7 +7,9 @@ kat_appendix_a.json  SURVEY.md Appendix A known-answer test (hand-derived, check
 covis_1k.npz         five per-rule tables of the first 1,000 otto-synth sessions (seed 0),
                      produced by the op-for-op pandas restatement of count_co_events.py:17-94
 digest_220m.json     (--full) BASELINE configs[1] at full size: per rule the order-independent
-                     checksums of the merged table, from per-file oracle tables (linear sums)
+                     checksums of the merged table, from per-file oracle tables (linear sums);
+                     (--full-a6) under "a6" the canonical digests of every rule's A6 output
+                     (concat_files_w_stats incl. branch (2) for click_to_click), streamed
 digest_config5.json  (--config5) BASELINE configs[4] at full size (12.9 M sessions): canonical digests of
                      the A7 train+test tables of the rules without the part-wise branch
 digests.json         sha256 of canonical (aid, aid_next, count) streams:
@@ -121,6 +123,57 @@ def _count_file_worker(args):
     e0, e1 = int(off[s0]), int(off[s1])
     rules = {n: covis.REFERENCE_RULES[n] for n in names}
     return covis.count_co_events_file(off[s0:s1 + 1] - off[s0], aid[e0:e1], ts[e0:e1], ty[e0:e1], rules)
+
+
+def _count_file_a6_worker(args):
+    """one 100k-session file, all five rules (C oracle): per rule (rows, rows with count >= 2, the
+    table or None, its count >= 2 part or None). click_to_* rules keep only the count >= 2 part
+    (branch (1) of A6 applies to them at 220 M events; the caller asserts it), the others keep
+    the whole table."""
+    t = _count_file_worker(args)
+    out = {}
+    for n, (a, b, c) in t.items():
+        keep = c >= 2
+        if n.startswith("click_to"):
+            out[n] = (len(a), int(keep.sum()), None, (a[keep], b[keep], c[keep]))
+        else:
+            out[n] = (len(a), int(keep.sum()), (a, b, c), None)
+    return out
+
+
+def full_a6(target_events: int = 220_000_000, seed: int = 0, workers: int = 8) -> dict:
+    """BASELINE configs[1] A6 (concat_files_w_stats, model/count_co_events.py:103-181) of every rule at
+    full size: per-file tables of the 135 files (C oracle, a process pool), then the streamed restatement
+    (concat_files_w_stats_streamed: branch (1) for click_to_* rules, branch (2) by row slices for
+    click_to_click, MIN_COUNT_TO_SAVE, count desc, head). Per rule the canonical digest (rows, sum,
+    sha256 of the (aid, aid_next, count) rows) of the final table, written under "a6" in
+    digest_220m.json."""
+    import multiprocessing as mp
+    import tempfile
+    n_sess, _ = synth.sessions_for_events(target_events, 0, seed)
+    ev = synth.generate(n_sess, 0, seed)
+    fb = synth.file_session_bounds(n_sess)
+    names = list(covis.REFERENCE_RULES)
+    with tempfile.TemporaryDirectory() as tmp:
+        path = os.path.join(tmp, "events.npz")
+        np.savez(path, off=ev.session_offsets - ev.session_offsets[0], aid=ev.aid, ts=ev.ts, type=ev.type, fb=fb)
+        del ev
+        with mp.get_context("spawn").Pool(workers) as pool:
+            res = pool.map(_count_file_a6_worker, [(path, f, names) for f in range(len(fb) - 1)], chunksize=1)
+    out = {}
+    for n in names:
+        rows = sum(r[n][0] for r in res)
+        if n.startswith("click_to"):
+            assert rows > 100_000_000, (n, rows)  # branch (1): the per-file count >= 2 parts suffice
+        tabs_full = [r[n][2] for r in res]
+        tabs_ge2 = [r[n][3] for r in res]
+        a, b, c = concat_files_w_stats_streamed(n, tabs_full, tabs_ge2, rows)
+        d = covis.canonical_digest({n: (a, b, c)})[n]
+        d["file_rows"], d["file_rows_ge2"] = rows, sum(r[n][1] for r in res)
+        out[n] = d
+        for r in res:
+            r[n] = None
+    return out
 
 
 def config5_a7(n_sessions: int = 12_900_000, workers: int = 8, names=None) -> dict:
@@ -239,7 +292,16 @@ def config5_c2c(n_sessions: int = 12_900_000, workers: int = 8) -> dict:
 
 if __name__ == "__main__":
     if "--full" in sys.argv:  # ~1 min on 8 cores: the 220M-event digest only
-        json.dump(full_digest(), open(os.path.join(HERE, "digest_220m.json"), "w"), indent=1)
+        g = full_digest()
+        old = os.path.join(HERE, "digest_220m.json")
+        if os.path.exists(old) and "a6" in json.load(open(old)):
+            g["a6"] = json.load(open(old))["a6"]
+        json.dump(g, open(old, "w"), indent=1)
+    elif "--full-a6" in sys.argv:  # a few minutes on 8 cores (~30 GB): the 220M-event A6 digests
+        path = os.path.join(HERE, "digest_220m.json")
+        g = json.load(open(path))
+        g["a6"] = full_a6(seed=g["seed"])
+        json.dump(g, open(path, "w"), indent=1)
     elif "--config5" in sys.argv:  # a few minutes on 8 cores (~40 GB): the config-5 A7 digests
         d = config5_a7()
         d["rules"]["click_to_click"] = config5_c2c()

@@ -489,7 +489,10 @@ def test_full_220m_digest(gpu):
     n_sess, n_ev = synth.sessions_for_events(220_000_000, 0, g["seed"])
     assert (n_sess, n_ev) == (g["sessions"], g["events"])
     ev = synth.generate(n_sess, 0, g["seed"])
-    tab = _gpu_tables(ev, synth.file_session_bounds(n_sess))
+    from otto_recommender_amd import covis as gc
+    dev = gc.DeviceEvents.from_host(ev, synth.file_session_bounds(n_sess))
+    del ev
+    tab = gc.count_co_events_fused(dev)
     for n in NAMES:
         d, st, ref = tab.digest(n), tab.stats(n), g["rules"][n]
         for k in ("d_count", "d_count_ge2", "pairs", "pairs_ge2"):
@@ -513,4 +516,13 @@ def test_full_220m_digest(gpu):
             assert fa.numel() == expect, n
             assert bool((fc[1:] <= fc[:-1]).all()), n  # count desc
         del a, b, c, c2
+    # A6 (concat_files_w_stats, model/count_co_events.py:103-181) of every rule at full size, incl. the
+    # part-wise branch (2) of click_to_click (N = 694 M > 3e8 per-file rows with count >= 2), against
+    # the streamed restatement over the C oracle's 135 per-file tables (make_golden.py --full-a6)
+    for n in NAMES:
+        fa, fb_, fc = gc.concat_files_w_stats_fused(dev, n, table=tab)
+        got = oracle.canonical_digest({n: tuple(x.cpu().numpy() for x in (fa, fb_, fc))})[n]
+        ref = g["a6"][n]
+        assert (got["rows"], got["sum"], got["sha256"]) == (ref["rows"], ref["sum"], ref["sha256"]), n
+        assert bool((fc[1:] <= fc[:-1]).all()), n
     tab.free()
