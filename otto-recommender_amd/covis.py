@@ -363,7 +363,7 @@ def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTabl
                                n_items: int = config.N_ITEMS_OTTO, max_rows_groupby: int = config.MAX_ROWS_POLARS_GROUPBY,
                                optim_rows: int = config.OPTIM_ROWS_POLARS_GROUPBY,
                                max_pairs: int = config.MAX_CO_EVENT_PAIRS_TO_SAVE_DISK,
-                               click_filter_rows: int = config.CLICK_FILTER_ROWS, ctx=None):
+                               click_filter_rows: int = config.CLICK_FILTER_ROWS, ctx=None, timings: dict | None = None):
     """model/count_co_events.py:103-181 for one rule over the files of `events`, all branches:
     (1) per-file count >= 2 for click_to_* tables when N > 1e8 (count_ge2), (2) when still
     N > max_rows_groupby, part-wise groupby -> keep count >= MIN_COUNT_IN_PART -> count desc
@@ -373,11 +373,21 @@ def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTabl
     table in (aid, aid_next) order (polars leaves it unspecified). One pass
     gives every file's row count; a part is the count of its files with the boundary files cut
     to the key range of their row slice (FileCuts). Returns torch (aid, aid_next, count:int32)
-    in (count desc, aid, aid_next) order."""
+    in (count desc, aid, aid_next) order. timings: per-stage seconds are added to this dict
+    (device-synchronised; a profiling aid)."""
     import math
+    import time
     import torch
     from . import dist as gd
     ctx = ctx or _lib.context()
+    t_last = [time.perf_counter()]
+
+    def mark(stage):
+        if timings is not None:
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            timings[stage] = timings.get(stage, 0.0) + t - t_last[0]
+            t_last[0] = t
     own = table is None
     tab = table if table is not None else count_co_events_fused(events, [name], n_items=n_items, ctx=ctx)
     st = tab.stats(name)
@@ -393,13 +403,16 @@ def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTabl
         tab.free()
     n_parts = math.ceil(N / optim_rows)
     max_rows_part = int(max_rows_groupby / N * optim_rows)
+    mark("prelude")
     t = count_co_events_fused(events, [name], n_items=n_items, ctx=ctx, cuts=FileCuts(name, per_file=True))
     R = t.file_rows_ge2_per_file if use_ge2 else t.file_rows_per_file
     t.free()
     if int(R.sum()) != N:
         raise RuntimeError(f"{name}: per-file rows sum to {int(R.sum())}, the table's N is {N}")
+    mark("file_rows")
     plan = part_plan(R, n_parts)
     keys = boundary_keys(events, name, plan, R, use_ge2, n_items, ctx)
+    mark("boundary_keys")
     part = {"click_rule": 1 if use_ge2 else 0, "filter_rows": -1, "max_rows_groupby": 1 << 62,
             "min_count": config.MIN_COUNT_IN_PART.get(name, 1)}
     recs = []
@@ -407,15 +420,19 @@ def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTabl
         cuts = FileCuts(name, lo=(0, keys[(fa, lo)]) if lo > 0 else None,
                         hi=(fb - fa, keys[(fb, hi)]) if hi < int(R[fb]) else None)
         t = count_co_events_fused(events.subset_files(fa, fb + 1), [name], n_items=n_items, ctx=ctx, cuts=cuts)
+        mark("part_count")
         a, b, c = t.finalize(name, max_rows=max_rows_part, params=part)
         recs.append(torch.stack([a, b, c, torch.zeros_like(c)], 1))
         t.free()
+        mark("part_finalize")
     r = torch.cat(recs) if recs else torch.zeros((0, 4), dtype=torch.int32, device=events.aid.device)
     merged = gd.table_from_records(r.contiguous(), [name], n_items, ctx=ctx)
+    mark("merge_parts")
     out = merged.finalize(name, max_rows=max_pairs,
                           params={"click_rule": 0, "filter_rows": -1, "max_rows_groupby": 1 << 62,
                                   "min_count": config.MIN_COUNT_TO_SAVE.get(name, 1)})
     merged.free()
+    mark("final")
     return out
 
 

@@ -414,6 +414,8 @@ static int file_opts_setup(ottohip_ctx* ctx, const ottohip_file_opts* o, int n_r
   for (int t = 0; t < 3; ++t)
     for (int q = 0; q < R.n_of_type[t]; ++q)
       if (R.rule_of_type[t][q] == o->rule) { fo.type = t; fo.q = (uint32_t)q; }
+  fo.sym = (uint32_t)((R.sym_mask >> o->rule) & 1u);
+  if (fo.sym && (o->lo_file >= 0 || o->hi_file >= 0)) { set_error("file_opts: key cuts on a symmetric table"); return OTTOHIP_EINVAL; }
   fo.lo_file = o->lo_file < 0 ? 0xFFFFFFFFu : (uint32_t)o->lo_file;
   fo.hi_file = o->hi_file < 0 ? 0xFFFFFFFFu : (uint32_t)o->hi_file;
   fo.lo_key = o->lo_key;
@@ -836,7 +838,9 @@ int ottohip_covis_count_opts(ottohip_ctx* ctx, const ottohip_events* ev, const o
   ctx->reset_timing();
   Front F;
   OH_TRY(check_events(ev));
-  OH_TRY(setup_rules(rules, n_rules, params, ev->n_files, F.R, F.Lt, /*allow_sym=*/opts == nullptr));
+  // symmetric storage stays on with per-file statistics only; key cuts need both orders of a pair stored
+  const bool sym_ok = opts == nullptr || (opts->lo_file < 0 && opts->hi_file < 0);
+  OH_TRY(setup_rules(rules, n_rules, params, ev->n_files, F.R, F.Lt, /*allow_sym=*/sym_ok));
   if (opts && (opts->file_rows || opts->file_rows_ge2) && opts->n_files < ev->n_files) {
     set_error("file_opts: n_files=%d < the call's %d files", opts->n_files, ev->n_files); return OTTOHIP_EINVAL;
   }

@@ -103,6 +103,7 @@ struct FileOpts {
   uint64_t lo_key, hi_key;    // key = aid << 32 | aid_next
   unsigned long long* hist;   // [nf] or null
   uint32_t nf;
+  uint32_t sym;               // the rule is stored once per unordered pair (no key cuts): hist counts mirrors
   unsigned long long* dropped;  // words dropped by the cuts (the reduce's conservation check)
   unsigned long long* dbg;      // OTTOHIP_DEBUG: [hash dropped, hash kept, sort dropped, sort kept] or null
   unsigned long long* prof;     // OTTOHIP_HASH_PROF: per hash task {len | rows << 32, wall-clock ticks | full << 63} or null
@@ -1329,7 +1330,8 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
                                                   int n_rules, OutRows O, FileOpts fo) {
   __shared__ unsigned long long sacc[4][STAT_STRIDE];
   __shared__ RulesDev sR;
-  __shared__ uint32_t stg[4][2][64 * M];  // per wave: output rows of one task (key2, count | count_ge2 << 16)
+  __shared__ uint32_t stg[4][2][64 * M + 64];  // per wave: output rows of one task (key2, count | count_ge2 << 16),
+                                              // + one dummy slot per lane
   __shared__ unsigned long long fh[FO ? FO_MAXF : 1];  // per-file rows of the FileOpts rule
   const uint32_t l = lane_id();
   const int wv = threadIdx.x >> 6;
@@ -1380,37 +1382,46 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
     if (FO && nd && l == 0) atomicAdd(fo.dropped, (unsigned long long)nd);
     if (FO && fo.dbg && l == 0) { atomicAdd(fo.dbg + 2, (unsigned long long)nd); atomicAdd(fo.dbg + 3, (unsigned long long)len); }
     wave_bitonic_sort<M>(v);
-    const uint32_t pl = lane_prev(v[M - 1]), nl = lane_next(v[0]);
+    // neighbours across lanes; lane 0's predecessor and lane 63's successor are sentinels that differ
+    // from the element in every field (so no element needs an index test: words are < W_EMPTY, and the
+    // invalid tail is W_EMPTY, sorted last). All flags below are branch-free selects: the former
+    // short-circuit tests (e < len && (e == 0 || ...)) compiled to exec-mask branches per element.
+    const uint32_t pl0 = lane_prev(v[M - 1]), nl0 = lane_next(v[0]);
+    const uint32_t pl = l == 0u ? ~v[0] : pl0, nl = l == 63u ? W_EMPTY : nl0;
     // (1) run flags from the neighbours (a w-run = one word = one (rule, aid_next, file)):
-    //     X = [w-run end] | [singleton w-run] << 11, summed by one scan (fields <= 1024)
+    //     X = [w-run end] | [singleton w-run] << 11, summed by one scan (fields <= 1024);
+    //     k-run (rule, aid_next) starts and ends as bit masks over the lane's elements
     uint32_t a[M], b[M], c[M];
+    uint32_t kst = 0, kend = 0;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      const uint32_t e = l * M + m;
       const uint32_t prv = m > 0 ? v[m - 1] : pl, nxt = m < M - 1 ? v[m + 1] : nl;
-      const bool valid = e < len;
-      const bool ws = valid && (e == 0 || prv != v[m]);
-      const bool we = valid && (e + 1 == len || nxt != v[m]);
-      c[m] = (we ? 1u : 0u) | ((ws && we) ? (1u << 11) : 0u);
+      const uint32_t valid = v[m] != W_EMPTY ? 1u : 0u;
+      const uint32_t ws = valid & (prv != v[m] ? 1u : 0u);
+      const uint32_t we = valid & (nxt != v[m] ? 1u : 0u);
+      c[m] = we | ((ws & we) << 11);
       b[m] = c[m];
+      kst |= (valid & ((prv >> F) != (v[m] >> F) ? 1u : 0u)) << m;
+      kend |= (valid & ((nxt >> F) != (v[m] >> F) ? 1u : 0u)) << m;
     }
     if constexpr (FO) {  // one per-file row per w-run end of the rule; a singleton w-run has count 1
       if (fo.hist && (int)(rk >> A) == fo.type) {
 #pragma unroll
         for (int m = 0; m < M; ++m)
-          if ((c[m] & 1u) && (v[m] >> (A + F)) == fo.q)
-            atomicAdd(&fh[v[m] & ((1u << F) - 1u)], (c[m] >> 11) ? 1ull : (1ull | (1ull << 32)));
+          if ((c[m] & 1u) && (v[m] >> (A + F)) == fo.q) {  // a symmetric rule's stored row (a, b), a < b, is
+            const unsigned long long mult =                // also the row (b, a) of the file's table
+                (fo.sym && ((v[m] >> F) & L.amask) != (rk & L.amask)) ? 2ull : 1ull;
+            atomicAdd(&fh[v[m] & ((1u << F) - 1u)], mult * ((c[m] >> 11) ? 1ull : (1ull | (1ull << 32))));
+          }
       }
     }
     wave_scan_elems<M, false>(b);
-    // (2) at each k-run (rule, aid_next) start: its exclusive X << 10 | position, carried to the
-    //     k-run's end by one max scan (strictly increasing over the starts)
+    // (2) at each k-run start: its exclusive X << 10 | position, carried to the k-run's end by one
+    //     max scan (strictly increasing over the starts)
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       const uint32_t e = l * M + m;
-      const uint32_t prv = m > 0 ? v[m - 1] : pl;
-      const bool ks = e < len && (e == 0 || (prv >> F) != (v[m] >> F));
-      a[m] = ks ? (((b[m] - c[m]) << 10) | e) : 0u;
+      a[m] = ((kst >> m) & 1u) ? (((b[m] - c[m]) << 10) | e) : 0u;
     }
     wave_scan_elems<M, true>(a);
     // (3) at k-run ends: count = its words, S = its files with one word, nf1 = its files;
@@ -1424,18 +1435,11 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
       b[m] = cnt | ((cnt - s1) << 16);
       c[m] = nf1 | ((nf1 - s1) << 16);
     }
-    // (4) one output row per k-run end: (key2, count | count_ge2 << 16, nf1 | nf2 << 16) staged in
-    //     this wave's LDS rows at its rank among the k-run ends, then written out linearly into the
-    //     task's own word range (coalesced stores on a task-uniform base)
+    // (4) one output row per k-run end: (key2, count | count_ge2 << 16) staged in this wave's LDS
+    //     rows at its rank among the k-run ends (other elements write a per-lane dummy slot), then
+    //     written out linearly into the task's own word range (coalesced stores on a task-uniform base)
     const int type = (int)(rk >> A);
     const int32_t aid = (int32_t)(rk & ((1u << A) - 1u));
-    uint32_t kend = 0;
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const uint32_t e = l * M + m;
-      const uint32_t nxt = m < M - 1 ? v[m + 1] : nl;
-      kend |= (e < len && (e + 1 == len || (nxt >> F) != (v[m] >> F))) ? (1u << m) : 0u;
-    }
     const uint32_t nmine = (uint32_t)__builtin_popcount(kend);
     const uint32_t incl = wave_incl_scan(nmine);
     const uint32_t nout = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
@@ -1444,30 +1448,38 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
     const int r0 = sR.rule_of_type[type][0], r1 = sR.rule_of_type[type][1];
     // local rules 0 / 1: rows | nf1 << 16, pairs | nf2 << 16 (a symmetric rule's off-diagonal rows twice);
     // sraw: stored rows | stored pairs << 16
-    uint32_t s0a = 0, s0b = 0, s1a = 0, s1b = 0, sraw = 0;
-    const bool sym0 = rule_sym(sR, r0), sym1 = nq > 1 && rule_sym(sR, r1);
+    uint32_t s0a = 0, s0b = 0, s1a = 0, s1b = 0, sraw = 0, q2 = 0;
+    const uint32_t sym0 = rule_sym(sR, r0) ? 1u : 0u, sym1 = (nq > 1 && rule_sym(sR, r1)) ? 1u : 0u;
     {
       uint32_t idx = incl - nmine;
 #pragma unroll
       for (int m = 0; m < M; ++m) {
-        if (kend & (1u << m)) {
-          const uint32_t k2 = v[m] >> F, q = k2 >> A, cnt = b[m] & 0xFFFFu, cc = c[m];
-          stg[wv][0][idx] = k2;
-          stg[wv][1][idx] = b[m];
-          ++idx;
-          const bool offd = (k2 & L.amask) != (uint32_t)aid;
-          const uint32_t mult = ((q == 0 ? sym0 : (q == 1 ? sym1 : rule_sym(sR, sR.rule_of_type[type][q]))) && offd)
-                                    ? 2u : 1u;
-          const uint32_t ra = (1u | ((cc & 0xFFFFu) << 16)) * mult, rb = (cnt | (cc & 0xFFFF0000u)) * mult;
-          sraw += 1u | (cnt << 16);
-          if (q == 0) { s0a += ra; s0b += rb; }
-          else if (q == 1) { s1a += ra; s1b += rb; }
-          else {  // more than 2 rules of one type (not in the reference's five)
-            unsigned long long* acc = sacc[wv] + sR.rule_of_type[type][q] * 4;
-            atomicAdd(acc + 0, (unsigned long long)mult); atomicAdd(acc + 1, (unsigned long long)cnt * mult);
-            atomicAdd(acc + 2, (unsigned long long)(cc & 0xFFFFu) * mult);
-            atomicAdd(acc + 3, (unsigned long long)(cc >> 16) * mult);
-          }
+        const uint32_t ke = (kend >> m) & 1u;
+        const uint32_t k2 = v[m] >> F, q = k2 >> A, cnt = b[m] & 0xFFFFu, cc = c[m];
+        const uint32_t slot = ke ? idx : (uint32_t)(64 * M) + l;
+        stg[wv][0][slot] = k2;
+        stg[wv][1][slot] = b[m];
+        idx += ke;
+        const uint32_t offd = (k2 & L.amask) != (uint32_t)aid ? 1u : 0u;
+        const uint32_t mult = 1u + (offd & (q == 0 ? sym0 : (q == 1 ? sym1 : 0u)));
+        const uint32_t ra = (1u | ((cc & 0xFFFFu) << 16)) * mult, rb = (cnt | (cc & 0xFFFF0000u)) * mult;
+        sraw += ke ? (1u | (cnt << 16)) : 0u;
+        s0a += (ke && q == 0) ? ra : 0u; s0b += (ke && q == 0) ? rb : 0u;
+        s1a += (ke && q == 1) ? ra : 0u; s1b += (ke && q == 1) ? rb : 0u;
+        q2 |= (ke && q >= 2) ? 1u : 0u;
+      }
+    }
+    if (__ballot(q2 != 0u)) {  // more than 2 rules of one type (not in the reference's five)
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const uint32_t k2 = v[m] >> F, q = k2 >> A;
+        if (((kend >> m) & 1u) && q >= 2) {
+          const uint32_t cnt = b[m] & 0xFFFFu, cc = c[m];
+          const uint32_t mult = (rule_sym(sR, sR.rule_of_type[type][q]) && (k2 & L.amask) != (uint32_t)aid) ? 2u : 1u;
+          unsigned long long* acc = sacc[wv] + sR.rule_of_type[type][q] * 4;
+          atomicAdd(acc + 0, (unsigned long long)mult); atomicAdd(acc + 1, (unsigned long long)cnt * mult);
+          atomicAdd(acc + 2, (unsigned long long)(cc & 0xFFFFu) * mult);
+          atomicAdd(acc + 3, (unsigned long long)(cc >> 16) * mult);
         }
       }
     }
@@ -1721,8 +1733,10 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
       if (fo.hist && fo_row) {
 #pragma unroll
         for (int s = 0; s < SL; ++s)
-          if (kw[s] != W_EMPTY && (kw[s] >> (L.A + L.F)) == fo.q)
-            atomicAdd(&fh[kw[s] & ((1u << L.F) - 1u)], kc[s] >= 2 ? (1ull | (1ull << 32)) : 1ull);
+          if (kw[s] != W_EMPTY && (kw[s] >> (L.A + L.F)) == fo.q) {
+            const unsigned long long mult = (fo.sym && ((kw[s] >> L.F) & L.amask) != (uint32_t)ri.aid) ? 2ull : 1ull;
+            atomicAdd(&fh[kw[s] & ((1u << L.F) - 1u)], mult * (kc[s] >= 2 ? (1ull | (1ull << 32)) : 1ull));
+          }
       }
     }
     __syncthreads();
