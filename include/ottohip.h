@@ -138,6 +138,26 @@ typedef struct {
 int ottohip_covis_count_opts(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip_rule* rules, int n_rules,
                              const ottohip_covis_params* params, const ottohip_file_opts* opts, ottohip_table** out,
                              void* stream);
+/* All parts of concat_files_w_stats' branch (2) (model/count_co_events.py:136-166) for ONE rule from
+ * ONE count (replaces a count per part with ottohip_file_opts key cuts). Part i is rows
+ * [i * rows_part, (i + 1) * rows_part) of the concatenation of the per-file tables, each in (aid,
+ * aid_next) order, so a pair of file f with key k = aid << 32 | aid_next belongs to part
+ * first_part[f], or first_part[f] + 1 when f holds a cut (cut_file[c] == f) and k >= cut_key[c] (one
+ * cut per file; the host falls back to per-part counts otherwise). The table's rows are (part, aid,
+ * aid_next) with count / count_ge2 summed over the part's files only; a row's rule index IS its part
+ * (ottohip_table_finalize(t, part, ...) orders one part; ottohip_table_stats(t, part) holds the part's
+ * rows and pairs). n_rules == 1, n_files <= 1024, n_parts <= 254, n_cuts <= 64, n_items <= 2^24. */
+typedef struct {
+  int32_t n_files;           /* the call's files */
+  int32_t n_parts;
+  const int32_t* first_part; /* HOST [n_files] */
+  int32_t n_cuts;
+  const int32_t* cut_file;   /* HOST [n_cuts] */
+  const uint64_t* cut_key;   /* HOST [n_cuts] */
+} ottohip_part_opts;
+int ottohip_covis_count_parts(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip_rule* rules, int n_rules,
+                              const ottohip_covis_params* params, const ottohip_part_opts* parts, ottohip_table** out,
+                              void* stream);
 /* keys (HOST out [n_idx]) = (aid << 32 | aid_next) of rows idx[i] (HOST) of one rule's rows in
  * (aid, aid_next) order; use_ge2: only rows with per-file count >= 2 (count_ge2 > 0). With a one-file
  * table these are the boundary keys of a row slice (ottohip_file_opts). OTTOHIP_ERANGE: idx >= rows. */

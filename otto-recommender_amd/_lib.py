@@ -49,6 +49,11 @@ class FileOpts(ctypes.Structure):
                 ("file_rows", ctypes.c_void_p), ("file_rows_ge2", ctypes.c_void_p)]
 
 
+class PartOpts(ctypes.Structure):
+    _fields_ = [("n_files", ctypes.c_int32), ("n_parts", ctypes.c_int32), ("first_part", ctypes.c_void_p),
+                ("n_cuts", ctypes.c_int32), ("cut_file", ctypes.c_void_p), ("cut_key", ctypes.c_void_p)]
+
+
 class MergeParams(ctypes.Structure):
     _fields_ = [("click_rule", ctypes.c_int32), ("min_count_in_part", ctypes.c_int32), ("min_count", ctypes.c_int32),
                 ("max_rows", ctypes.c_int64), ("filter_rows", ctypes.c_int64), ("max_rows_groupby", ctypes.c_int64)]
@@ -69,6 +74,8 @@ SIGNATURES = {
     "ottohip_covis_count_opts": (ctypes.c_int, [_VP, ctypes.POINTER(Events), ctypes.POINTER(Rule), ctypes.c_int,
                                                 ctypes.POINTER(CovisParams), ctypes.POINTER(FileOpts),
                                                 ctypes.POINTER(_VP), _VP]),
+    "ottohip_covis_count_parts": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int, ctypes.POINTER(CovisParams),
+                                                 ctypes.POINTER(PartOpts), ctypes.POINTER(_VP), _VP]),
     "ottohip_table_keys_at": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_int, _VP, ctypes.c_int, _VP, _VP]),
     "ottohip_table_stats": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.POINTER(RuleStats)]),
     "ottohip_table_copy": (ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, _VP, _VP]),

@@ -328,6 +328,54 @@ def part_plan(file_rows, n_parts: int):
     return plan
 
 
+def part_assignment(plan, file_rows, keys):
+    """Per-file part map of one ottohip_covis_count_parts call for the row slices `plan`: the first part
+    of every file and the cuts (file, key): a pair of file f with key >= key belongs to the next part.
+    None when some file holds two cuts (a file longer than a part) or the map does not fit the call."""
+    nf = len(file_rows)
+    first = np.full(nf, -1, np.int64)
+    cuts = {}
+    for p, (fa, lo, fb, hi) in enumerate(plan):
+        for f in range(fa, fb + 1):
+            if first[f] < 0:
+                first[f] = p
+        if hi < int(file_rows[fb]):
+            if fb in cuts:
+                return None
+            cuts[fb] = int(keys[(fb, hi)])
+    # files without rows between parts: any part (they hold no row of the sliced column)
+    last = 0
+    for f in range(nf):
+        if first[f] < 0:
+            first[f] = last
+        last = first[f]
+    if len(plan) > 254 or len(cuts) > 64 or nf > 1024:
+        return None
+    return first.astype(np.int32), sorted(cuts.items())
+
+
+def count_co_events_parts(events: DeviceEvents, name: str, first_part, cuts, n_parts: int,
+                          n_items: int = config.N_ITEMS_OTTO, dedup: bool = True, stream=None, ctx=None) -> CovisTable:
+    """ottohip_covis_count_parts: one count of rule `name` whose rows are (part, aid, aid_next), every
+    pair in the part of its file (first_part[f], or the next part from the file's cut key on). The
+    returned table's rule index is the part (names = [name] * n_parts)."""
+    ctx = ctx or _lib.context()
+    names, rules = reference_rules([name])
+    p = _lib.CovisParams()
+    p.min_dt, p.max_dt, p.n_items, p.dedup = config.MIN_TIME_TO_NEXT, config.MAX_TIME_TO_NEXT, int(n_items), int(dedup)
+    fp = np.ascontiguousarray(first_part, np.int32)
+    cf = np.ascontiguousarray([f for f, _ in cuts] or [0], np.int32)
+    ck = np.ascontiguousarray([k for _, k in cuts] or [0], np.uint64)
+    po = _lib.PartOpts()
+    po.n_files, po.n_parts, po.first_part = len(fp), int(n_parts), fp.ctypes.data
+    po.n_cuts, po.cut_file, po.cut_key = len(cuts), cf.ctypes.data, ck.ctypes.data
+    ev = events.abi()
+    h = ctypes.c_void_p()
+    _lib.check(_lib.load().ottohip_covis_count_parts(ctx.h, ctypes.byref(ev), rules, 1, ctypes.byref(p), ctypes.byref(po),
+                                                     ctypes.byref(h), _lib.stream_handle(stream)))
+    return CovisTable(h, [name] * int(n_parts), ctx)
+
+
 def table_keys_at(table: CovisTable, name, use_ge2: bool, idx, stream=None) -> np.ndarray:
     """ottohip_table_keys_at: keys (aid << 32 | aid_next) of rows idx of one rule's rows in (aid,
     aid_next) order (use_ge2: rows with count >= 2 only)."""
@@ -363,7 +411,8 @@ def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTabl
                                n_items: int = config.N_ITEMS_OTTO, max_rows_groupby: int = config.MAX_ROWS_POLARS_GROUPBY,
                                optim_rows: int = config.OPTIM_ROWS_POLARS_GROUPBY,
                                max_pairs: int = config.MAX_CO_EVENT_PAIRS_TO_SAVE_DISK,
-                               click_filter_rows: int = config.CLICK_FILTER_ROWS, ctx=None, timings: dict | None = None):
+                               click_filter_rows: int = config.CLICK_FILTER_ROWS, ctx=None, timings: dict | None = None,
+                               one_count: bool = True):
     """model/count_co_events.py:103-181 for one rule over the files of `events`, all branches:
     (1) per-file count >= 2 for click_to_* tables when N > 1e8 (count_ge2), (2) when still
     N > max_rows_groupby, part-wise groupby -> keep count >= MIN_COUNT_IN_PART -> count desc
@@ -372,8 +421,9 @@ def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTabl
     ceil(N / n_parts) consecutive rows of the files' concatenated per-file tables, each file's
     table in (aid, aid_next) order (polars leaves it unspecified). One pass
     gives every file's row count; a part is the count of its files with the boundary files cut
-    to the key range of their row slice (FileCuts). Returns torch (aid, aid_next, count:int32)
-    in (count desc, aid, aid_next) order. timings: per-stage seconds are added to this dict
+    to the key range of their row slice; with one_count (default) all parts come from ONE count whose
+    rows carry their part (ottohip_covis_count_parts), else one count per part (FileCuts). Returns torch
+    (aid, aid_next, count:int32) in (count desc, aid, aid_next) order. timings: per-stage seconds are added to this dict
     (device-synchronised; a profiling aid)."""
     import math
     import time
@@ -416,6 +466,18 @@ def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTabl
     part = {"click_rule": 1 if use_ge2 else 0, "filter_rows": -1, "max_rows_groupby": 1 << 62,
             "min_count": config.MIN_COUNT_IN_PART.get(name, 1)}
     recs = []
+    nf = len(events.file_bounds) - 1
+    fits = one_count and n_items <= (1 << 24) and nf <= max_files_per_call([name], n_items)
+    assign = part_assignment(plan, R, keys) if fits else None
+    if assign is not None:  # every part from ONE count (its rows carry their part)
+        t = count_co_events_parts(events, name, assign[0], assign[1], len(plan), n_items, ctx=ctx)
+        mark("part_count")
+        for p_ in range(len(plan)):
+            a, b, c = t.finalize(p_, max_rows=max_rows_part, params=part)
+            recs.append(torch.stack([a, b, c, torch.zeros_like(c)], 1))
+        t.free()
+        mark("part_finalize")
+        plan = []
     for fa, lo, fb, hi in plan:
         cuts = FileCuts(name, lo=(0, keys[(fa, lo)]) if lo > 0 else None,
                         hi=(fb - fa, keys[(fb, hi)]) if hi < int(R[fb]) else None)

@@ -447,7 +447,8 @@ static int file_opts_finish(const ottohip_file_opts* o, const FileOpts& fo, hipS
 
 static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P, const uint64_t* row_begin,
                         const uint32_t* row_key, int64_t Rn, const RulesDev& R, const Layout& Lt, int n_rules,
-                        ottohip_table* T, hipStream_t s, const ottohip_file_opts* fopts = nullptr) {
+                        ottohip_table* T, hipStream_t s, const ottohip_file_opts* fopts = nullptr,
+                        const FileOpts* fo_parts = nullptr) {
   Workspace& ws = ctx->ws;
   int rc;
   int* err;
@@ -455,7 +456,12 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   FileOpts fo;
   memset(&fo, 0, sizeof fo);
   if (fopts) OH_TRY(file_opts_setup(ctx, fopts, n_rules, R, fo, s));
-  const bool FOon = fopts != nullptr;
+  if (fo_parts) {  // part mode: tables already on the device; a drop counter for the conservation check
+    fo = *fo_parts;
+    OH_TRY(ctx->ws.get("fo_dropped", 1, &fo.dropped));
+    OH_HIP(hipMemsetAsync(fo.dropped, 0, 8, s));
+  }
+  const bool FOon = fopts != nullptr || fo_parts != nullptr;
   // symmetric rules store one row per unordered pair; the readers produce the mirrors (T->sym_mask)
   const uint64_t n_slots = P;
   if (ctx->spare.cap >= n_slots) {
@@ -855,6 +861,86 @@ int ottohip_covis_count_opts(ottohip_ctx* ctx, const ottohip_events* ev, const o
   if ((rc = covis_emit_words(ctx, F, ev, w0, s))) return fail(rc);
   if ((rc = covis_reduce(ctx, w0, w1, F.P, F.row_begin, F.row_key, F.Rn, F.R, F.Lt, n_rules, T, s, opts)))
     return fail(rc);
+  *out = T;
+  return 0;
+}
+
+int ottohip_covis_count_parts(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip_rule* rules, int n_rules,
+                              const ottohip_covis_params* params, const ottohip_part_opts* po, ottohip_table** out,
+                              void* stream) {
+  if (!ctx || !ev || !rules || !params || !po || !out || !po->first_part || (po->n_cuts > 0 && (!po->cut_file || !po->cut_key))) {
+    set_error("ottohip_covis_count_parts: NULL argument"); return OTTOHIP_EINVAL;
+  }
+  *out = nullptr;
+  if (n_rules != 1) { set_error("count_parts: one rule per call (got %d)", n_rules); return OTTOHIP_EINVAL; }
+  OH_TRY(check_events(ev));
+  const int nf = ev->n_files;
+  if (po->n_files != nf) { set_error("count_parts: n_files=%d, the call has %d files", po->n_files, nf); return OTTOHIP_EINVAL; }
+  if (nf > FO_MAXF) { set_error("count_parts: %d files > %d per call", nf, FO_MAXF); return OTTOHIP_ELIMIT; }
+  if (po->n_parts < 1 || po->n_parts > 254 || po->n_parts > TABLE_MAX_IDS) {
+    set_error("count_parts: n_parts=%d outside [1, 254]", po->n_parts); return OTTOHIP_ELIMIT;
+  }
+  if (po->n_cuts < 0 || po->n_cuts > FO_MAXCUT) { set_error("count_parts: n_cuts=%d outside [0, %d]", po->n_cuts, FO_MAXCUT); return OTTOHIP_ELIMIT; }
+  if (params->n_items > (1 << 24)) { set_error("count_parts: n_items > 2^24"); return OTTOHIP_ELIMIT; }
+  std::vector<uint8_t> part_of(nf), cut_of(nf, FO_NOCUT);
+  for (int f = 0; f < nf; ++f) {
+    if (po->first_part[f] < 0 || po->first_part[f] >= po->n_parts) { set_error("count_parts: first_part[%d] out of range", f); return OTTOHIP_EINVAL; }
+    part_of[f] = (uint8_t)po->first_part[f];
+  }
+  for (int c = 0; c < po->n_cuts; ++c) {
+    const int f = po->cut_file[c];
+    if (f < 0 || f >= nf || cut_of[f] != FO_NOCUT || part_of[f] + 1 >= po->n_parts) {
+      set_error("count_parts: cut %d (file %d) invalid: one cut per file, inside the parts", c, f); return OTTOHIP_EINVAL;
+    }
+    cut_of[f] = (uint8_t)c;
+  }
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  ctx->reset_timing();
+  Front F;
+  OH_TRY(setup_rules(rules, n_rules, params, nf, F.R, F.Lt, /*allow_sym=*/false));
+  ottohip_table* T = new_table(ctx, n_rules, params->n_items);
+  auto fail = [&](int rc) { ottohip_table_free(T); return rc; };
+  int rc;
+  if ((rc = covis_front(ctx, ev, params, nullptr, 1, F, s))) return fail(rc);
+  T->n_rules = po->n_parts;
+  if (F.P == 0) { *out = T; return 0; }
+  uint32_t *w0, *w1;
+  if ((rc = ctx->ws.get("words0", (size_t)F.P, &w0)) || (rc = ctx->ws.get("words1", (size_t)F.P, &w1))) return fail(rc);
+  if ((rc = covis_emit_words(ctx, F, ev, w0, s))) return fail(rc);
+  FileOpts fo;
+  memset(&fo, 0, sizeof fo);
+  fo.type = rules[0].this_type;
+  fo.q = 0;
+  fo.lo_file = fo.hi_file = 0xFFFFFFFFu;
+  fo.nf = (uint32_t)nf;
+  fo.parts = 1;
+  fo.ncut = (uint32_t)po->n_cuts;
+  for (int c = 0; c < po->n_cuts; ++c) fo.cut_key[c] = po->cut_key[c];
+  uint8_t *d_part, *d_cut;
+  if ((rc = ctx->ws.get("fo_part_of", (size_t)nf, &d_part)) || (rc = ctx->ws.get("fo_cut_of", (size_t)nf, &d_cut))) return fail(rc);
+  OH_HIP(hipMemcpyAsync(d_part, part_of.data(), nf, hipMemcpyHostToDevice, s));
+  OH_HIP(hipMemcpyAsync(d_cut, cut_of.data(), nf, hipMemcpyHostToDevice, s));
+  OH_HIP(hipStreamSynchronize(s));  // host vectors
+  fo.part_of = d_part;
+  fo.cut_of = d_cut;
+  if ((rc = covis_reduce(ctx, w0, w1, F.P, F.row_begin, F.row_key, F.Rn, F.R, F.Lt, n_rules, T, s, nullptr, &fo)))
+    return fail(rc);
+  // per part: rows and pairs (file statistics stay 0: the part-wise finalize is told which column to use)
+  T->n_rules = po->n_parts;
+  unsigned long long* ph;
+  if ((rc = ctx->ws.get("part_hist", 512, &ph))) return fail(rc);
+  OH_HIP(hipMemsetAsync(ph, 0, 512 * 8, s));
+  k_rule_hist<<<(unsigned)std::min<int64_t>(ceil_div((int64_t)T->n_slots, 256), (int64_t)ctx->n_cu * 8), 256, 0, s>>>(
+      T->b.rule, T->b.count, T->n_slots, ph, ph + 256);
+  OH_HIP(hipGetLastError());
+  std::vector<unsigned long long> hh(512);
+  if ((rc = d2h(hh.data(), ph, hh.size(), s))) return fail(rc);
+  for (int p = 0; p < po->n_parts; ++p) {
+    T->stats[p] = ottohip_rule_stats{};
+    T->stats[p].n_rows = (int64_t)hh[p];
+    T->stats[p].n_pairs = (int64_t)hh[256 + p];
+  }
   *out = T;
   return 0;
 }

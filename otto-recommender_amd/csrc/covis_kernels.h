@@ -96,6 +96,8 @@ struct OutRows {
 // tasks before they are counted; hist[f] accumulates file f's rows of the rule (low 32 bits) and
 // those with per-file count >= 2 (high 32 bits). Applied to the rule's words only.
 constexpr int FO_MAXF = 1024;
+constexpr int FO_MAXCUT = 64;
+constexpr uint8_t FO_NOCUT = 0xFF;
 struct FileOpts {
   int type;              // row type of the rule
   uint32_t q;            // the rule's index among the rules of its type (word bits above aid_next)
@@ -104,10 +106,36 @@ struct FileOpts {
   unsigned long long* hist;   // [nf] or null
   uint32_t nf;
   uint32_t sym;               // the rule is stored once per unordered pair (no key cuts): hist counts mirrors
+  // part mode (ottohip_covis_count_parts, A6 branch (2) from one count): a word of file f with key k belongs
+  // to part part_of[f] + (cut_of[f] != NONE && k >= cut_key[cut_of[f]]); k-runs break where the part
+  // changes and a row's output "rule" byte is its part (single-rule counts, aid_next < 2^24)
+  uint32_t parts;             // 0: off
+  const uint8_t* part_of;     // device [nf]
+  const uint8_t* cut_of;      // device [nf]: index into cut_key, FO_NOCUT = none
+  uint32_t ncut;
+  uint64_t cut_key[FO_MAXCUT];
   unsigned long long* dropped;  // words dropped by the cuts (the reduce's conservation check)
   unsigned long long* dbg;      // OTTOHIP_DEBUG: [hash dropped, hash kept, sort dropped, sort kept] or null
   unsigned long long* prof;     // OTTOHIP_HASH_PROF: per hash task {len | rows << 32, wall-clock ticks | full << 63} or null
 };
+// LDS copy of the part-mode tables (FO kernels)
+struct PartLds {
+  uint8_t part_of[FO_MAXF];
+  uint8_t cut_of[FO_MAXF];
+  uint64_t cut_key[FO_MAXCUT];
+};
+__device__ __forceinline__ void part_lds_load(const FileOpts& fo, PartLds& P) {
+  if (!fo.parts) return;
+  for (uint32_t i = threadIdx.x; i < fo.nf; i += blockDim.x) { P.part_of[i] = fo.part_of[i]; P.cut_of[i] = fo.cut_of[i]; }
+  for (uint32_t i = threadIdx.x; i < fo.ncut; i += blockDim.x) P.cut_key[i] = fo.cut_key[i];
+}
+// part of word w (valid) of row aid
+__device__ __forceinline__ uint32_t word_part(const PartLds& P, uint32_t w, uint32_t aid, const Layout& L) {
+  const uint32_t f = w & ((1u << L.F) - 1u);
+  const uint32_t ci = P.cut_of[f];
+  const uint64_t key = ((uint64_t)aid << 32) | ((w >> L.F) & L.amask);
+  return (uint32_t)P.part_of[f] + ((ci != FO_NOCUT && key >= P.cut_key[ci & (FO_MAXCUT - 1)]) ? 1u : 0u);
+}
 __device__ __forceinline__ bool fo_drop(const FileOpts& fo, uint32_t w, int32_t aid, const Layout& L) {
   if (w == W_EMPTY || (w >> (L.A + L.F)) != fo.q) return false;
   const uint32_t f = w & ((1u << L.F) - 1u);
@@ -1333,12 +1361,15 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
   __shared__ uint32_t stg[4][2][64 * M + 64];  // per wave: output rows of one task (key2, count | count_ge2 << 16),
                                               // + one dummy slot per lane
   __shared__ unsigned long long fh[FO ? FO_MAXF : 1];  // per-file rows of the FileOpts rule
+  __shared__ std::conditional_t<FO, PartLds, char> sP[1];  // part-mode tables (FO kernels only)
   const uint32_t l = lane_id();
   const int wv = threadIdx.x >> 6;
   if (threadIdx.x == 0) sR = R;
   for (int i = (int)l; i < STAT_STRIDE; i += 64) sacc[wv][i] = 0;
-  if constexpr (FO)
+  if constexpr (FO) {
     for (uint32_t i = threadIdx.x; i < fo.nf; i += blockDim.x) fh[i] = 0;
+    part_lds_load(fo, sP[0]);
+  }
   __syncthreads();
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   int64_t ti = __builtin_amdgcn_readfirstlane((int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6));
@@ -1388,6 +1419,19 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
     // short-circuit tests (e < len && (e == 0 || ...)) compiled to exec-mask branches per element.
     const uint32_t pl0 = lane_prev(v[M - 1]), nl0 = lane_next(v[0]);
     const uint32_t pl = l == 0u ? ~v[0] : pl0, nl = l == 63u ? W_EMPTY : nl0;
+    // part mode: parts of the elements and of the cross-lane neighbours (words of one key are in file
+    // order, and the part is non-decreasing in the file for a fixed key, so a part's words stay adjacent)
+    uint32_t pt[FO ? M : 1];
+    uint32_t ppl = 0, pnl = 0;
+    const bool pmode = FO && fo.parts;
+    if constexpr (FO) {
+      if (pmode) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) pt[m] = v[m] != W_EMPTY ? word_part(sP[0], v[m], rk & L.amask, L) : 0xFFu;
+        ppl = lane_prev(pt[M - 1]);
+        pnl = lane_next(pt[0]);
+      }
+    }
     // (1) run flags from the neighbours (a w-run = one word = one (rule, aid_next, file)):
     //     X = [w-run end] | [singleton w-run] << 11, summed by one scan (fields <= 1024);
     //     k-run (rule, aid_next) starts and ends as bit masks over the lane's elements
@@ -1401,8 +1445,16 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
       const uint32_t we = valid & (nxt != v[m] ? 1u : 0u);
       c[m] = we | ((ws & we) << 11);
       b[m] = c[m];
-      kst |= (valid & ((prv >> F) != (v[m] >> F) ? 1u : 0u)) << m;
-      kend |= (valid & ((nxt >> F) != (v[m] >> F) ? 1u : 0u)) << m;
+      uint32_t kbs = (prv >> F) != (v[m] >> F) ? 1u : 0u, kbe = (nxt >> F) != (v[m] >> F) ? 1u : 0u;
+      if constexpr (FO) {
+        if (pmode) {  // a k-run is one (key, part)
+          const uint32_t pp = m > 0 ? pt[m - 1] : ppl, pn = m < M - 1 ? pt[m + 1] : pnl;
+          kbs |= pp != pt[m] ? 1u : 0u;
+          kbe |= pn != pt[m] ? 1u : 0u;
+        }
+      }
+      kst |= (valid & kbs) << m;
+      kend |= (valid & kbe) << m;
     }
     if constexpr (FO) {  // one per-file row per w-run end of the rule; a singleton w-run has count 1
       if (fo.hist && (int)(rk >> A) == fo.type) {
@@ -1457,7 +1509,11 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
         const uint32_t ke = (kend >> m) & 1u;
         const uint32_t k2 = v[m] >> F, q = k2 >> A, cnt = b[m] & 0xFFFFu, cc = c[m];
         const uint32_t slot = ke ? idx : (uint32_t)(64 * M) + l;
-        stg[wv][0][slot] = k2;
+        uint32_t k2s = k2;
+        if constexpr (FO) {
+          if (pmode) k2s = k2 | (pt[m] << 24);  // the part rides above aid_next (< 2^24 in part mode)
+        }
+        stg[wv][0][slot] = k2s;
         stg[wv][1][slot] = b[m];
         idx += ke;
         const uint32_t offd = (k2 & L.amask) != (uint32_t)aid ? 1u : 0u;
@@ -1495,7 +1551,7 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
       for (uint32_t i = l; i < nout; i += 64) {
         const uint32_t k2 = stg[wv][0][i], bb = stg[wv][1][i];
         const uint32_t q = k2 >> A;
-        const int rule = q == 0 ? r0 : (q == 1 ? r1 : sR.rule_of_type[type][q]);
+        const int rule = pmode ? (int)(k2 >> 24) : (q == 0 ? r0 : (q == 1 ? r1 : sR.rule_of_type[type][q]));
         const int32_t next = (int32_t)(k2 & L.amask);
         o_rule[i] = (uint8_t)rule;
         o_aid[i] = aid;
@@ -1607,6 +1663,7 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
   __shared__ uint32_t wtot[AGG_T / 64];
   __shared__ uint32_t nocc;
   __shared__ unsigned long long fh[FO ? FO_MAXF : 1];  // per-file rows of the FileOpts rule
+  __shared__ std::conditional_t<FO, PartLds, char> sP[1];  // part-mode tables (FO kernels only)
   const int tid = threadIdx.x;
   // the hash leaves share CUs with the register sorts of the same level (aux stream): a raised wave
   // priority lets their LDS-latency-bound loop issue ahead of the VALU-bound sorts
@@ -1616,8 +1673,10 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
   acc.zero();
   if constexpr (FO) {
     for (uint32_t i = tid; i < fo.nf; i += AGG_T) fh[i] = 0;
+    part_lds_load(fo, sP[0]);
     __syncthreads();
   }
+  const bool pmode = FO && fo.parts;
   for (int64_t ti = blockIdx.x; ti < n_tasks; ti += gridDim.x) {
     const Task T = tasks[ti];
     const uint64_t t_start = fo.prof ? wall_clock64() : 0;
@@ -1751,6 +1810,9 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         k2[j] = kw[s0 + j] == W_EMPTY ? W_EMPTY : kw[s0 + j] >> L.F;
+        if constexpr (FO) {  // part mode: the folded key is (part, aid_next)
+          if (pmode && kw[s0 + j] != W_EMPTY) k2[j] |= word_part(sP[0], kw[s0 + j], (uint32_t)ri.aid, L) << 24;
+        }
         c8[j] = kc[s0 + j];
       }
       hash_insert_batch<8>(B, k2, c8, cm, slot);
@@ -1776,11 +1838,11 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
       const uint32_t k2 = (uint32_t)(v >> 32);
       if (k2 == W_EMPTY) continue;
       const unsigned long long v2 = B2[i];
-      const int rule = R.rule_of_type[ri.type][k2 >> L.A];
+      const int rule = pmode ? 0 : R.rule_of_type[ri.type][k2 >> L.A];
       const uint32_t c = (uint32_t)v, c2 = (uint32_t)(v2 >> 32), nf = (uint32_t)v2;
       const int32_t next = (int32_t)(k2 & L.amask);
       const bool mr = rule_sym(R, rule) && next != ri.aid;
-      put_row(O, p++, rule, ri.aid, next, c, c2);
+      put_row(O, p++, pmode ? (int)(k2 >> 24) : rule, ri.aid, next, c, c2);  // part mode: the part as "rule"
       acc.add(rule, c, nf, mr ? 2u : 1u);
     }
     // the rest of the task's word range holds no row (no table-wide fill: every word position
@@ -2164,6 +2226,21 @@ __global__ __launch_bounds__(FIN_T) void k_blk_compact(const uint8_t* __restrict
     run += tot;
     __syncthreads();  // wt is rewritten by the next chunk
   }
+}
+
+// rows and pairs per rule byte (part-mode tables: per part), block histograms in LDS
+__global__ __launch_bounds__(256) void k_rule_hist(const uint8_t* __restrict__ rule, const uint32_t* __restrict__ count,
+                                                   int64_t n, unsigned long long* __restrict__ rows,
+                                                   unsigned long long* __restrict__ pairs) {
+  __shared__ unsigned long long hr[256], hp[256];
+  hr[threadIdx.x] = 0; hp[threadIdx.x] = 0;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t r = rule[i];
+    if (r != 0xFFu) { atomicAdd(&hr[r], 1ull); atomicAdd(&hp[r], (unsigned long long)count[i]); }
+  }
+  __syncthreads();
+  if (hr[threadIdx.x]) { atomicAdd(&rows[threadIdx.x], hr[threadIdx.x]); atomicAdd(&pairs[threadIdx.x], hp[threadIdx.x]); }
 }
 
 // ------------------------------------------------------------------ finalize (merge A6)

@@ -41,6 +41,7 @@ struct ottohip_ctx : public Ctx {
   uint64_t gen = 0;  // count calls so far (emit handles refer to the workspace of one call)
 };
 
+constexpr int TABLE_MAX_IDS = 256;  // rule ids of a table's rows (part ids: ottohip_covis_count_parts)
 struct ottohip_table {
   int device = 0;
   int n_rules = 0;
@@ -50,7 +51,7 @@ struct ottohip_table {
   TableBufs b;
   uint32_t sym_mask = 0;  // rules stored once per unordered pair (aid <= aid_next): readers add the mirrors
   int sym(int rule) const { return (int)((sym_mask >> rule) & 1u); }
-  ottohip_rule_stats stats[MAX_RULES];
+  ottohip_rule_stats stats[TABLE_MAX_IDS];  // per rule (or per part of a ottohip_covis_count_parts table)
   ottohip_ctx* ctx = nullptr;
 };
 

@@ -465,6 +465,21 @@ def test_file_cuts_hot_rows(gpu, case):
     hot1 = np.flatnonzero(per_file[1][n][0] == 7)
     hot2 = np.flatnonzero(per_file[2][n][0] == 7)
     lo, hi = int(k1[hot1[len(hot1) // 3]]), int(k2[hot2[len(hot2) // 2]])
+    # ONE count with every row tagged by its part (ottohip_covis_count_parts): part 0 = file 0 + file 1 below
+    # lo, part 1 = file 1 from lo + file 2 below hi, part 2 = file 2 from hi + file 3
+    tp = gc.count_co_events_parts(dev, n, [0, 0, 1, 2], [(1, lo), (2, hi)], 3)
+    ref_parts = [[per_file[0][n], tuple(x[k1 < lo] for x in per_file[1][n])],
+                 [tuple(x[k1 >= lo] for x in per_file[1][n]), tuple(x[k2 < hi] for x in per_file[2][n])],
+                 [tuple(x[k2 >= hi] for x in per_file[2][n]), per_file[3][n]]]
+    for p_, fs in enumerate(ref_parts):
+        ca, cb, cc = (np.concatenate([f[i] for f in fs]) for i in range(3))
+        ga, gb, gcnt = oracle._groupby_sum(ca, cb, cc.astype(np.int64))
+        _, _, gg2 = oracle._groupby_sum(ca, cb, np.where(cc >= 2, cc, 0).astype(np.int64))
+        a_, b_, c_, g_ = tp.to_numpy(p_)
+        for x, y in ((a_, ga), (b_, gb), (c_, gcnt), (g_, gg2)):
+            np.testing.assert_array_equal(x.astype(np.int64), y, err_msg=f"part {p_}")
+    assert sum(tp.stats(p_)["n_pairs"] for p_ in range(3)) == sum(int(p[n][2].sum()) for p in per_file)
+    tp.free()
     t = gc.count_co_events_fused(dev, [n], cuts=gc.FileCuts(n, lo=(1, lo), hi=(2, hi), per_file=True))
     parts = [per_file[0][n], tuple(x[k1 >= lo] for x in per_file[1][n]), tuple(x[k2 < hi] for x in per_file[2][n]),
              per_file[3][n]]
