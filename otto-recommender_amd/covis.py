@@ -608,13 +608,45 @@ def _read_table(path):
                  for k, dt in (("aid", np.int32), ("aid_next", np.int32), ("count", np.uint32)))
 
 
-def concat_files_w_stats(name, dir_stats, files_stats=None, n_items: int | None = None, **kw):
+def _part_heads(name, tabs, n_items, max_rows_groupby, optim_rows, ctx=None):
+    """Branch (2) of :135-166 on host tables (already through the :131-132 filter): per row slice of
+    the concatenation, groupby-sum (device merge of records), count >= MIN_COUNT_IN_PART, count desc,
+    head(int(max_rows_groupby / N * optim_rows)); returns the concatenation of the part heads (host)."""
+    import math
+    import torch
+    from . import dist as gd
+    ctx = ctx or _lib.context()
+    cat = [np.concatenate([t[i] for t in tabs]) for i in range(3)]
+    N = len(cat[0])
+    n_parts = math.ceil(N / optim_rows)
+    max_rows_part = int(max_rows_groupby / N * optim_rows)
+    rows_part = math.ceil(N / n_parts)
+    dev = torch.device("cuda", ctx.device)
+    out = []
+    for i in range(n_parts):
+        sl = slice(i * rows_part, (i + 1) * rows_part)
+        rec = torch.from_numpy(np.stack([cat[0][sl].astype(np.int32), cat[1][sl].astype(np.int32),
+                                         cat[2][sl].view(np.int32), np.zeros(len(cat[0][sl]), np.int32)], 1)).to(dev)
+        t = gd.table_from_records(rec.contiguous(), [name], n_items, ctx=ctx)
+        a, b, c = t.finalize(name, max_rows=max_rows_part,
+                             params={"click_rule": 0, "filter_rows": -1, "max_rows_groupby": 1 << 62,
+                                     "min_count": config.MIN_COUNT_IN_PART.get(name, 1)})
+        out.append((a.cpu().numpy(), b.cpu().numpy(), c.cpu().numpy().view(np.uint32)))
+        t.free()
+    return tuple(np.concatenate([o[i] for o in out]) if out else np.zeros(0, np.int32) for i in range(3))
+
+
+def concat_files_w_stats(name, dir_stats, files_stats=None, n_items: int | None = None,
+                         max_rows_groupby: int = config.MAX_ROWS_POLARS_GROUPBY,
+                         optim_rows: int = config.OPTIM_ROWS_POLARS_GROUPBY,
+                         click_filter_rows: int = config.CLICK_FILTER_ROWS, **kw):
     """model/count_co_events.py:103-181 with the reference's signature and files: reads
     {dir_stats}/tmp/{name}.parquet if present (loaded_from_cache, :106-110), else the tables listed
     in files_stats (:111-112), else every {dir_stats}/{name}/*.parquet in sorted order (:113-114);
-    runs A6 on the device (ottohip_concat_tables) and writes {dir_stats}/{name}.parquet
-    [aid:int32, aid_next:int32, count:int32] in count-desc order (:179). The build needs no
-    out-of-memory retry, so it never writes the tmp cache itself."""
+    runs A6 on the device and writes {dir_stats}/{name}.parquet [aid:int32, aid_next:int32,
+    count:int32] in count-desc order (:179). When the part-wise branch (2) runs, the concatenated
+    part heads are written to {dir_stats}/tmp/{name}.parquet first (:164-166), as the reference does,
+    so a second call takes the loaded_from_cache path on the same file."""
     import torch
     file_tmp = f"{dir_stats}/tmp/{name}.parquet"
     cached = os.path.exists(file_tmp)
@@ -629,9 +661,23 @@ def concat_files_w_stats(name, dir_stats, files_stats=None, n_items: int | None 
         n_items = max([config.N_ITEMS_OTTO] + [int(max(t[0].max(), t[1].max())) + 1 for t in tabs if len(t[0])])
     if any(len(t[2]) and int(t[2].max()) > 0x7FFFFFFF for t in tabs):
         raise ValueError("concat_files_w_stats: a per-file count exceeds int32")
+    if not cached:
+        n_rows = sum(len(t[0]) for t in tabs)
+        if "click_to" in name and n_rows > click_filter_rows:  # :131-132, then :135's test on the filtered rows
+            thr = config.MIN_COUNT_IN_PART.get(name, 1)
+            tabs_f = [tuple(x[t[2] >= thr] for x in t) for t in tabs]
+        else:
+            tabs_f = tabs
+        if sum(len(t[0]) for t in tabs_f) > max_rows_groupby:  # :135-166, the parts written to tmp (:164-166)
+            parts = _part_heads(name, tabs_f, n_items, max_rows_groupby, optim_rows)
+            os.makedirs(f"{dir_stats}/tmp", exist_ok=True)
+            _write_table(file_tmp, *parts, np.uint32)
+            tabs, cached = [parts], True
     dev_tabs = [tuple(torch.from_numpy(x.view(np.int32) if x.flags.writeable else x.view(np.int32).copy()) for x in t)
                 for t in tabs]
-    a, b, c = concat_tables_w_stats(name, dev_tabs, n_items=n_items, loaded_from_cache=cached, **kw)
+    a, b, c = concat_tables_w_stats(name, dev_tabs, n_items=n_items, loaded_from_cache=cached,
+                                    max_rows_groupby=max_rows_groupby, optim_rows=optim_rows,
+                                    click_filter_rows=click_filter_rows, **kw)
     _write_table(f"{dir_stats}/{name}.parquet", a.cpu().numpy(), b.cpu().numpy(), c.cpu().numpy(), np.int32)
 
 

@@ -3,7 +3,7 @@
   co-visitation per folder (count_co_events_fused) -> A6 per folder -> A7 train+test merge -> R1
   Word2Vec kNN of both models (first 600k vocabulary rows)   -> B3 lists
   session embeddings (C1) -> KMeans k=50 (C2) -> popularity ranks cl50 / cl1 (C3)
-  candidates for the test sessions (R3-R6) -> recall@20 (R9)
+  candidates for the test sessions (R3-R6) -> session-item similarity (R7) -> recall@20 (R9)
 
 Mirrors the order of the reference's scripts (model/count_co_events.py, model/w2vec_aids.py,
 model/kmeans_sessions.py, model/count_popularity.py, model/retrieve.py, model/eval_retrieved.py)
@@ -193,6 +193,12 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
     dev_test = folders[1][0]
     cands = gcand.generate(dev_test.offsets, dev_test.aid, dev_test.ts, dev_test.type, src, test_cl)
     t = mark("candidates", t)
+    # ---- R7: cosine similarity / Euclidean distance between each candidate and its session's C1
+    # embedding (model/retrieve.py:604-625; candidates without an aid embedding: 0 / -1)
+    csr = cands.to_torch()
+    se_test = se[n_tr_sessions:]
+    sim = gp.session_item_similarity(csr["off"], csr["aid_next"], se_test, words_all, emb_all, None, n_items, ctx)
+    t = mark("R7_similarity", t)
     lo, la = gcand.labels_csr_device(*lab_cols, sess_dev, ctx=ctx)
     t = mark("labels_csr", t)
     sums = cands.recall_sums(lo, la)
@@ -214,10 +220,16 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
             "knn": [tuple(h(x) for x in v) for v in knn],
             "cluster_labels": h(labels_all), "cluster_rows": grows, "pop": p[["cl50", "aid"]].reset_index(drop=True),
             "n_clusters": n_clusters, "test_session_ids": sess}
+        if keep_candidates:  # R7 of every candidate and the test sessions' C1 embeddings (small runs)
+            out["intermediates"]["similarity"] = tuple(h(x) for x in sim)
+            out["intermediates"]["test_session_embeddings"] = h(se_test)
+        else:
+            out["intermediates"]["similarity"] = sim
         if keep_candidates:
             out["intermediates"]["candidates"] = cands.to_pandas(sess)
         else:
             out["intermediates"]["candidates_csr"] = cands.to_torch()
     cands.free()
+    del csr, sim, se_test
     mark("finish", t)
     return out

@@ -25,7 +25,8 @@ def test_pipeline_small(gpu):
             assert 0.0 <= res["recall"][t][k] <= 1.0
         assert res["recall"][t]["top20"] <= res["recall"][t]["top100"] <= res["recall"][t]["topall"]
     assert res["recall"]["total"]["topall"] > 0.1  # self + co-visit candidates recover revisits
-    for stage in ("covis_count", "R1", "knn", "C1_embeddings", "C2_kmeans", "C3_popularity", "candidates", "recall"):
+    for stage in ("covis_count", "R1", "knn", "C1_embeddings", "C2_kmeans", "C3_popularity", "candidates",
+                  "R7_similarity", "recall"):
         assert stage in T, stage
 
 
@@ -82,6 +83,19 @@ def test_pipeline_recall_parity(gpu):
     for c in ["session", "aid_next", "ts_order_aid"] + [c for c in ref_c.columns if c.startswith("src_")]:
         np.testing.assert_array_equal(got_c[c].to_numpy().astype(np.int64), ref_c[c].to_numpy().astype(np.int64),
                                       err_msg=c)
+    # R7 (model/retrieve.py:604-625) of every candidate: cos / Euclidean to the session's C1 embedding in
+    # f64 (candidates without an aid embedding: 0 / -1); fp32 on the device, rtol 1e-5
+    cos, eu = im["similarity"]
+    se = im["test_session_embeddings"]
+    from otto_recommender_amd.w2vec import word_rows
+    o_ = np.argsort(sess_te, kind="stable")
+    sidx = o_[np.searchsorted(sess_te[o_], got_c["session"].to_numpy())]
+    r_ = word_rows(words, got_c["aid_next"].to_numpy())
+    ok = r_ >= 0
+    rc, re = oracle_pop.similarity(se[sidx[ok]].astype(np.float64), emb[r_[ok]].astype(np.float64))
+    np.testing.assert_allclose(cos[ok], rc, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(eu[ok], re, rtol=1e-5)
+    assert np.all(cos[~ok] == 0) and np.all(eu[~ok] == -1)
     rec = oracle_retrieve.recall(ref_c, labels)
     for t in ("clicks", "carts", "orders", "total"):
         for k in ("top20", "top100", "top200", "topall"):
