@@ -292,6 +292,37 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
 
   // ---- S3 rows (aid-major transpose; owner-major first when n_parts > 1)
   ph = ctx->begin("rows", s, 0);
+  static const bool rows_atomic = getenv("OTTOHIP_ROWS") && !strcmp(getenv("OTTOHIP_ROWS"), "atomic");
+  if (rows_atomic && fused) {  // no sort: dense rows, per-event ranks by returning atomics (k_rows_atomic)
+    const uint32_t INVa = 3u << Lt.A;
+    const uint32_t kmask_a = Lt.A + 2 >= 32 ? ~0u : (1u << (Lt.A + 2)) - 1u;
+    const int64_t nk = (int64_t)3 << Lt.A;  // dense (type, aid) keys
+    uint32_t* dcnt;
+    uint64_t *doff, *tot;
+    OH_TRY(ws.get("ra_cnt", (size_t)(nk * RA_SUB), &dcnt));
+    OH_TRY(ws.get("ra_off", (size_t)(nk * RA_SUB), &doff));
+    OH_TRY(ws.get("tot", 4, &tot));
+    OH_HIP(hipMemsetAsync(dcnt, 0, (size_t)(nk * RA_SUB) * 4, s));
+    k_rows_atomic<<<grid_for(E), 256, 0, s>>>(rk, F.cnt, E, kmask_a, INVa, dcnt, pos);
+    OH_TRY(exclusive_scan_u32(ctx, dcnt, doff, nk * RA_SUB, tot, s));
+    uint64_t PP = 0;
+    OH_TRY(d2h(&PP, tot, 1, s));
+    int herr = 0;
+    OH_TRY(d2h(&herr, err, 1, s));
+    if (herr) { set_error("input out of range: aid outside [0, n_items) or type outside {0,1,2}"); return OTTOHIP_ERANGE; }
+    F.P = PP;
+    F.Rn = nk;
+    OH_TRY(ws.get("row_key", (size_t)nk, &F.row_key));
+    OH_TRY(ws.get("row_begin", (size_t)nk, &F.row_begin));
+    k_rows_dense<<<grid_for(nk), 256, 0, s>>>(doff, nk, F.row_key, F.row_begin);
+    F.poff = nullptr; F.poff32 = nullptr;
+    if (F.P < (1ull << 32)) OH_TRY(ws.get("poff32", (size_t)E, &F.poff32));
+    else OH_TRY(ws.get("poff", (size_t)E, &F.poff));
+    k_rows_atomic_off<<<grid_for(E), 256, 0, s>>>(rk, E, kmask_a, INVa, doff, pos, F.poff32, F.poff);
+    OH_HIP(hipGetLastError());
+    ctx->end(ph, s);
+    return 0;
+  }
   uint32_t INV = 3u << Lt.A;
   int kbits = Lt.A + 2;
   if (n_parts > 1) {
@@ -382,12 +413,13 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
 static int covis_emit_words(ottohip_ctx* ctx, const Front& F, const ottohip_events* ev, uint32_t* w0, hipStream_t s) {
   int ph = ctx->begin("emit", s, 8.0 * F.E + 12.0 * F.E + 4.0 * (double)F.P);
   static const int dbg0 = getenv("OTTOHIP_EMIT_DBG") ? atoi(getenv("OTTOHIP_EMIT_DBG")) : 0;  // profiling ablations
-  const int dbg = dbg0 | (getenv("OTTOHIP_DEBUG") ? 4 : 0);  // 4: bounds checks of the emit record arrays
+  const int dbg = dbg0;
+  const bool guard = getenv("OTTOHIP_DEBUG") != nullptr;  // bounds checks of the emit record arrays
   int* eerr;
   OH_TRY(ctx->ws.get("emit_err", 4, &eerr));
   OH_HIP(hipMemsetAsync(eerr, 0, sizeof(int), s));
   if (F.NB > 0)
-    k_emit<<<(unsigned)F.NB, 64, 0, s>>>(F.off, F.first, F.NB, F.evp, F.R, F.Lt, F.fb, ev->n_files, F.fid, F.cnt,
+    (guard ? k_emit<true> : k_emit<false>)<<<(unsigned)F.NB, 64, 0, s>>>(F.off, F.first, F.NB, F.evp, F.R, F.Lt, F.fb, ev->n_files, F.fid, F.cnt,
                                          EvOff{F.poff, F.poff32}, w0, eerr, dbg);
   if (F.nl > 0)
     k_emit_long<<<F.nl, 64, 0, s>>>(F.off, F.long_list, F.d_loff, F.lscr, F.lpscr, F.evp, F.R, F.Lt, F.fb,

@@ -697,6 +697,44 @@ __global__ void k_poff_scatter(const uint32_t* __restrict__ pos, const uint32_t*
   if (k < n) poff32[pos[k]] = woff[k];
 }
 
+// ---- rows without a sort (OTTOHIP_ROWS=atomic, one GPU): the row of key k is the dense index k of
+// (type << A | aid); its words are cut into RA_SUB sub-ranges, one per counter, so the atomics of a hot
+// row spread over RA_SUB addresses. Each event takes its run inside its sub-range with one returning
+// atomic (word order inside a row is free: the reduce sorts it), one scan over the dense counters gives
+// every sub-range its first word, and the event's word offset is that start plus its rank.
+constexpr int RA_SUB = 8;
+__device__ __forceinline__ uint32_t ra_sub(int64_t e) { return (uint32_t)(e >> 8) & (RA_SUB - 1); }
+__global__ void k_rows_atomic(const uint32_t* __restrict__ rk, const uint32_t* __restrict__ cnt, int64_t n,
+                              uint32_t kmask, uint32_t INV, uint32_t* __restrict__ dcnt, uint32_t* __restrict__ rank) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const uint32_t key = rk[e] & kmask;
+  uint32_t r = 0;
+  if (key != INV) {
+    const uint32_t c = cnt[e];
+    if (c) r = atomicAdd(&dcnt[(uint64_t)key * RA_SUB + ra_sub(e)], c);
+  }
+  rank[e] = r;
+}
+// word offset of every event (u32 when P < 2^32, else u64) from its sub-range start and rank
+__global__ void k_rows_atomic_off(const uint32_t* __restrict__ rk, int64_t n, uint32_t kmask, uint32_t INV,
+                                  const uint64_t* __restrict__ doff, const uint32_t* __restrict__ rank,
+                                  uint32_t* __restrict__ poff32, uint64_t* __restrict__ poff) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const uint32_t key = rk[e] & kmask;
+  const uint64_t o = key != INV ? doff[(uint64_t)key * RA_SUB + ra_sub(e)] + rank[e] : 0;
+  if (poff32) poff32[e] = (uint32_t)o; else poff[e] = o;
+}
+// dense rows: row r = key r, first word = its first sub-range's start
+__global__ void k_rows_dense(const uint64_t* __restrict__ doff, int64_t nk, uint32_t* __restrict__ row_key,
+                             uint64_t* __restrict__ row_begin) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nk) return;
+  row_key[r] = (uint32_t)r;
+  row_begin[r] = doff[(uint64_t)r * RA_SUB];
+}
+
 // multi-GPU layout: row keys become (owner(aid), type, aid) so every owner's rows and words
 // are contiguous (the all-to-all send segments); invalid events sort after every owner
 __global__ void k_owner_key(uint32_t* __restrict__ rk, int64_t n, uint32_t INV, int A, uint32_t G, uint32_t INV2) {
@@ -902,8 +940,9 @@ struct EmitLds {
 // aid; 0 for other rules): a lane's word goes to the record's output at its rank among the record's
 // written words -- those of earlier rounds (only the record spanning the round boundary has any: a
 // wave-uniform carry) plus those of the record's lanes below it in this round (one ballot).
-// dbg & 4 (OTTOHIP_DEBUG): a lane whose record index falls outside [0, nrec) sets err bit 8 and writes
+// GUARD (OTTOHIP_DEBUG): a lane whose record index falls outside [0, nrec) sets err bit 8 and writes
 // nothing (the record arrays hold EB_RCAP entries; an out-of-range index would read stale LDS)
+template <bool GUARD>
 __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, int F, uint32_t* __restrict__ words,
                                            int dbg, uint32_t& rid, int* __restrict__ err) {
   const uint32_t l = lane_id();
@@ -925,7 +964,7 @@ __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, i
     const uint32_t p = c + l;
     bool qual = false;
     uint32_t word = 0;
-    const bool bad = (dbg & 4) && p < tot && (o < 0 || o >= nrec);
+    const bool bad = GUARD && p < tot && (o < 0 || o >= nrec);
     if (bad) atomicOr(err, 8);
     if (p < tot && !bad) {
       const uint4 rc = S.u.r.rec[o];
@@ -945,6 +984,7 @@ __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, i
   }
 }
 
+template <bool GUARD>  // GUARD (OTTOHIP_DEBUG): bounds checks of the record arrays (err bit 8)
 __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restrict__ off, const int64_t* __restrict__ first,
                                              int64_t NB, const uint64_t* __restrict__ ev, RulesDev R, Layout L,
                                              const int64_t* __restrict__ fb, int nf, const uint32_t* __restrict__ fid,
@@ -1118,14 +1158,14 @@ __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restri
           if (nrec + nn > EB_RCAP) {
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            emit_flush(S, nrec, tot, L.F, words, dbg, rid, err);
+            emit_flush<GUARD>(S, nrec, tot, L.F, words, dbg, rid, err);
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             nrec = 0; tot = 0;
           }
           const uint32_t incl = wave_incl_scan(len);
-          if ((dbg & 4) && nrec + nn > EB_RCAP) atomicOr(err, 8);  // the record arrays would overflow
-          if (len > 0 && !((dbg & 4) && nrec + (int)mbcnt(m) >= EB_RCAP)) {
+          if (GUARD && nrec + nn > EB_RCAP) atomicOr(err, 8);  // the record arrays would overflow
+          if (len > 0 && !(GUARD && nrec + (int)mbcnt(m) >= EB_RCAP)) {
             const int ri = nrec + (int)mbcnt(m);
             S.u.r.rpre[ri] = tot + incl - len;
             S.u.r.rec[ri] = make_uint4(tot + incl - len, jb | (xlo << 10) | (xlen << 21), ((uint32_t)q << shiftR) | file,
@@ -1142,7 +1182,7 @@ __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restri
     if (nrec > 0) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      emit_flush(S, nrec, tot, L.F, words, dbg, rid, err);
+      emit_flush<GUARD>(S, nrec, tot, L.F, words, dbg, rid, err);
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

@@ -18,4 +18,4 @@ for run in A1 B1 A2 B2; do
 done
 unset OTTOHIP_LIB
 OTTOHIP_ALLOC_LOG=1 timeout -k 10 300 python3 -u bench.py --no-cpu --no-ingest --steps 3 --warmup 1 --knn-steps 0 --cand-steps 0 > "$O/b_a6.log" 2>&1 || { tail -20 "$O/b_a6.log"; exit 1; }
-python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); a=d['a6']; print(a["total_ms_runs"], a.get("warmup_ms"), a["per_rule"]["click_to_click"])" "$O/b_a6.log"
+python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); a=d['a6']; print(a['total_ms_runs'], a.get('warmup_ms'), a['per_rule']['click_to_click'])" "$O/b_a6.log"
