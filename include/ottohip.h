@@ -158,6 +158,14 @@ typedef struct {
 int ottohip_covis_count_parts(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip_rule* rules, int n_rules,
                               const ottohip_covis_params* params, const ottohip_part_opts* parts, ottohip_table** out,
                               void* stream);
+/* Heads of every part of a ottohip_covis_count_parts table (:155-162 for all parts at once): per part p,
+ * among its rows with v >= min_count (v = count_ge2 if use_ge2 else count), the first max_rows_part in
+ * (v desc, aid asc, aid_next asc) order, selected by histograms (no sort). Written to out_records
+ * (device, cap records of 16 B: {aid, aid_next, v, 0}, the ottohip_table_from_records layout, rule 0) in
+ * no particular order; *n_out = records. n_parts <= 32. OTTOHIP_ELIMIT: a part's cut falls on a count
+ * >= 65535 (the host orders that part with ottohip_table_finalize instead) or cap is too small. */
+int ottohip_table_part_heads(ottohip_ctx* ctx, const ottohip_table* t, int n_parts, int use_ge2, int32_t min_count,
+                             int64_t max_rows_part, void* out_records, int64_t cap, int64_t* n_out, void* stream);
 /* keys (HOST out [n_idx]) = (aid << 32 | aid_next) of rows idx[i] (HOST) of one rule's rows in
  * (aid, aid_next) order; use_ge2: only rows with per-file count >= 2 (count_ge2 > 0). With a one-file
  * table these are the boundary keys of a row slice (ottohip_file_opts). OTTOHIP_ERANGE: idx >= rows. */

@@ -376,6 +376,23 @@ def count_co_events_parts(events: DeviceEvents, name: str, first_part, cuts, n_p
     return CovisTable(h, [name] * int(n_parts), ctx)
 
 
+def part_heads(table: CovisTable, n_parts: int, use_ge2: bool, min_count: int, max_rows_part: int, stream=None):
+    """ottohip_table_part_heads: the head(max_rows_part) of every part of a count_co_events_parts table as
+    int32 records [m, 4] (aid, aid_next, count, 0), or None where the device selection does not apply (a
+    part's cut count >= 65535): the caller then finalizes part by part."""
+    import torch
+    cap = max(1, int(n_parts) * int(max_rows_part))
+    rec = torch.empty((cap, 4), dtype=torch.int32, device=torch.device("cuda", table.ctx.device))
+    n = ctypes.c_int64(0)
+    rc = _lib.load().ottohip_table_part_heads(table.ctx.h, table.h, int(n_parts), 1 if use_ge2 else 0, int(min_count),
+                                              int(max_rows_part), _lib.ptr(rec), cap, ctypes.byref(n),
+                                              _lib.stream_handle(stream))
+    if rc == _lib.OTTOHIP_ELIMIT:
+        return None
+    _lib.check(rc)
+    return rec[:int(n.value)]
+
+
 def table_keys_at(table: CovisTable, name, use_ge2: bool, idx, stream=None) -> np.ndarray:
     """ottohip_table_keys_at: keys (aid << 32 | aid_next) of rows idx of one rule's rows in (aid,
     aid_next) order (use_ge2: rows with count >= 2 only)."""
@@ -472,9 +489,13 @@ def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTabl
     if assign is not None:  # every part from ONE count (its rows carry their part)
         t = count_co_events_parts(events, name, assign[0], assign[1], len(plan), n_items, ctx=ctx)
         mark("part_count")
-        for p_ in range(len(plan)):
-            a, b, c = t.finalize(p_, max_rows=max_rows_part, params=part)
-            recs.append(torch.stack([a, b, c, torch.zeros_like(c)], 1))
+        heads = part_heads(t, len(plan), use_ge2, part["min_count"], max_rows_part) if len(plan) <= 32 else None
+        if heads is not None:  # every part's head at once (histogram cuts, no per-part sort)
+            recs.append(heads)
+        else:
+            for p_ in range(len(plan)):
+                a, b, c = t.finalize(p_, max_rows=max_rows_part, params=part)
+                recs.append(torch.stack([a, b, c, torch.zeros_like(c)], 1))
         t.free()
         mark("part_finalize")
         plan = []

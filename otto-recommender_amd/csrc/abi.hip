@@ -303,7 +303,7 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
     OH_TRY(ws.get("ra_off", (size_t)(nk * RA_SUB), &doff));
     OH_TRY(ws.get("tot", 4, &tot));
     OH_HIP(hipMemsetAsync(dcnt, 0, (size_t)(nk * RA_SUB) * 4, s));
-    k_rows_atomic<<<grid_for(E), 256, 0, s>>>(rk, F.cnt, E, kmask_a, INVa, dcnt, pos);
+    k_rows_atomic<<<grid_for(E, 256 * RA_PER), 256, 0, s>>>(rk, F.cnt, E, kmask_a, INVa, dcnt, pos);
     OH_TRY(exclusive_scan_u32(ctx, dcnt, doff, nk * RA_SUB, tot, s));
     uint64_t PP = 0;
     OH_TRY(d2h(&PP, tot, 1, s));
@@ -318,7 +318,7 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
     F.poff = nullptr; F.poff32 = nullptr;
     if (F.P < (1ull << 32)) OH_TRY(ws.get("poff32", (size_t)E, &F.poff32));
     else OH_TRY(ws.get("poff", (size_t)E, &F.poff));
-    k_rows_atomic_off<<<grid_for(E), 256, 0, s>>>(rk, E, kmask_a, INVa, doff, pos, F.poff32, F.poff);
+    k_rows_atomic_off<<<grid_for(E, 256 * RA_PER), 256, 0, s>>>(rk, E, kmask_a, INVa, doff, pos, F.poff32, F.poff);
     OH_HIP(hipGetLastError());
     ctx->end(ph, s);
     return 0;
@@ -1249,6 +1249,91 @@ void ottohip_table_free(ottohip_table* t) {
 }
 
 }  // extern "C"
+
+extern "C" int ottohip_table_part_heads(ottohip_ctx* ctx, const ottohip_table* t, int n_parts, int use_ge2,
+                                        int32_t min_count, int64_t max_rows_part, void* out_records, int64_t cap,
+                                        int64_t* n_out, void* stream) {
+  if (!ctx || !t || !n_out || n_parts < 1 || n_parts > PH_MAXP || n_parts > t->n_rules || max_rows_part < 0 ||
+      (cap > 0 && !out_records) || t->sym_mask) {
+    set_error("table_part_heads: bad arguments (n_parts in [1, %d], a part-mode table)", PH_MAXP); return OTTOHIP_EINVAL;
+  }
+  *n_out = 0;
+  if (t->n_rows == 0 || t->n_slots == 0 || max_rows_part == 0) return 0;
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  Workspace& ws = ctx->ws;
+  const int64_t n = t->n_slots;
+  const uint32_t thr = (uint32_t)std::max<int32_t>(min_count, 1);
+  const unsigned sgrid = (unsigned)std::min<int64_t>(ceil_div(n, 256), (int64_t)ctx->n_cu * 16);
+  // (1) v histogram per part
+  unsigned long long* hist;
+  OH_TRY(ws.get("ph_hist", (size_t)n_parts * PH_VBINS, &hist));
+  OH_HIP(hipMemsetAsync(hist, 0, (size_t)n_parts * PH_VBINS * 8, s));
+  k_ph_hist<<<sgrid, 256, 0, s>>>(t->b.rule, t->b.count, t->b.count_ge2, n, n_parts, use_ge2, thr, hist);
+  std::vector<unsigned long long> hh((size_t)n_parts * PH_VBINS);
+  OH_TRY(d2h(hh.data(), hist, hh.size(), s));
+  PartCut pc;
+  memset(&pc, 0, sizeof pc);
+  std::vector<uint64_t> need(n_parts, 0);
+  int n_tie = 0;
+  for (int p = 0; p < n_parts; ++p) {
+    const unsigned long long* h = hh.data() + (size_t)p * PH_VBINS;
+    unsigned long long above = 0;
+    pc.cstar[p] = 0; pc.astar[p] = 0xFFFFFFFFu; pc.stage[p] = 0;
+    int64_t v = PH_VBINS - 1;
+    for (; v >= (int64_t)thr; --v) {
+      if (above + h[v] >= (unsigned long long)max_rows_part) break;
+      above += h[v];
+    }
+    if (v < (int64_t)thr) continue;  // the part has at most max_rows_part rows: all kept
+    if (v == PH_VBINS - 1) { set_error("table_part_heads: a part's cut count >= %u", PH_VBINS - 1); return OTTOHIP_ELIMIT; }
+    pc.cstar[p] = (uint32_t)v;
+    need[p] = (uint64_t)max_rows_part - above;  // 1 <= need <= h[v]
+    if (need[p] < h[v]) { pc.stage[p] = 1; ++n_tie; }  // ties at c*: cut by (aid, aid_next)
+  }
+  const int64_t ni = t->n_items;
+  if (n_tie) {
+    uint32_t *th, *found;
+    uint64_t* ex;
+    OH_TRY(ws.get("ph_tie", (size_t)n_parts * ni, &th));
+    OH_TRY(ws.get("ph_tie_ex", (size_t)ni, &ex));
+    OH_TRY(ws.get("ph_found", 2, &found));
+    for (int st = 1; st <= 2; ++st) {
+      OH_HIP(hipMemsetAsync(th, 0, (size_t)n_parts * ni * 4, s));
+      k_ph_tie_hist<<<sgrid, 256, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n, n_parts,
+                                          use_ge2, pc, st, ni, th);
+      for (int p = 0; p < n_parts; ++p) {
+        if (pc.stage[p] != (uint32_t)st) continue;
+        OH_TRY(exclusive_scan_u32(ctx, th + (size_t)p * ni, ex, ni, nullptr, s));
+        OH_HIP(hipMemsetAsync(found, 0xFF, 8, s));
+        k_ph_find<<<grid_for(ni), 256, 0, s>>>(ex, th + (size_t)p * ni, ni, need[p], found);
+        uint32_t fr[2];
+        OH_TRY(d2h(fr, found, 2, s));
+        if (fr[0] == 0xFFFFFFFFu) { set_error("table_part_heads: tie cut not found (part %d)", p); return OTTOHIP_EHIP; }
+        if (st == 1) { pc.astar[p] = fr[0]; need[p] = fr[1]; pc.stage[p] = 2; }
+        else { pc.nstar[p] = fr[0]; pc.stage[p] = 3; }
+      }
+    }
+  }
+  // (2) kept rows of every part -> records
+  const int64_t nb = ceil_div(n, FIN_B);
+  uint32_t* bcnt;
+  uint64_t *boff, *tot;
+  OH_TRY(ws.get("blk_cnt", (size_t)nb, &bcnt));
+  OH_TRY(ws.get("blk_off", (size_t)nb, &boff));
+  OH_TRY(ws.get("fin_tot", 1, &tot));
+  k_ph_count<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n, n_parts,
+                                            use_ge2, thr, pc, bcnt);
+  OH_TRY(exclusive_scan_u32(ctx, bcnt, boff, nb, tot, s));
+  uint64_t m = 0;
+  OH_TRY(d2h(&m, tot, 1, s));
+  if ((int64_t)m > cap) { set_error("table_part_heads: %llu rows > capacity %lld", (unsigned long long)m, (long long)cap); return OTTOHIP_ELIMIT; }
+  if (m) k_ph_compact<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n,
+                                                      n_parts, use_ge2, thr, pc, boff, reinterpret_cast<uint4*>(out_records));
+  OH_HIP(hipGetLastError());
+  *n_out = (int64_t)m;
+  return 0;
+}
 
 extern "C" int ottohip_table_finalize(ottohip_ctx* ctx, const ottohip_table* t, int rule,
                                       const ottohip_merge_params* mp, int32_t* aid, int32_t* aid_next,

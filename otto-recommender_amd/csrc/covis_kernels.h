@@ -704,27 +704,45 @@ __global__ void k_poff_scatter(const uint32_t* __restrict__ pos, const uint32_t*
 // every sub-range its first word, and the event's word offset is that start plus its rank.
 constexpr int RA_SUB = 8;
 __device__ __forceinline__ uint32_t ra_sub(int64_t e) { return (uint32_t)(e >> 8) & (RA_SUB - 1); }
-__global__ void k_rows_atomic(const uint32_t* __restrict__ rk, const uint32_t* __restrict__ cnt, int64_t n,
-                              uint32_t kmask, uint32_t INV, uint32_t* __restrict__ dcnt, uint32_t* __restrict__ rank) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  const uint32_t key = rk[e] & kmask;
-  uint32_t r = 0;
-  if (key != INV) {
-    const uint32_t c = cnt[e];
-    if (c) r = atomicAdd(&dcnt[(uint64_t)key * RA_SUB + ra_sub(e)], c);
+// RA_PER events per thread (coalesced, stride blockDim): their returning atomics are in flight together
+// (one at a time leaves the kernel bound by the atomics' round-trip latency)
+constexpr int RA_PER = 8;
+__global__ __launch_bounds__(256) void k_rows_atomic(const uint32_t* __restrict__ rk, const uint32_t* __restrict__ cnt,
+                                                     int64_t n, uint32_t kmask, uint32_t INV, uint32_t* __restrict__ dcnt,
+                                                     uint32_t* __restrict__ rank) {
+  const int64_t e0 = (int64_t)blockIdx.x * (256 * RA_PER) + threadIdx.x;
+  uint32_t key[RA_PER], c[RA_PER], r[RA_PER];
+#pragma unroll
+  for (int j = 0; j < RA_PER; ++j) {
+    const int64_t e = e0 + j * 256;
+    key[j] = e < n ? rk[e] & kmask : INV;
+    c[j] = key[j] != INV ? cnt[e] : 0u;
   }
-  rank[e] = r;
+#pragma unroll
+  for (int j = 0; j < RA_PER; ++j)
+    r[j] = c[j] ? atomicAdd(&dcnt[(uint64_t)key[j] * RA_SUB + ra_sub(e0 + j * 256)], c[j]) : 0u;
+#pragma unroll
+  for (int j = 0; j < RA_PER; ++j)
+    if (e0 + j * 256 < n) rank[e0 + j * 256] = r[j];
 }
 // word offset of every event (u32 when P < 2^32, else u64) from its sub-range start and rank
-__global__ void k_rows_atomic_off(const uint32_t* __restrict__ rk, int64_t n, uint32_t kmask, uint32_t INV,
-                                  const uint64_t* __restrict__ doff, const uint32_t* __restrict__ rank,
-                                  uint32_t* __restrict__ poff32, uint64_t* __restrict__ poff) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  const uint32_t key = rk[e] & kmask;
-  const uint64_t o = key != INV ? doff[(uint64_t)key * RA_SUB + ra_sub(e)] + rank[e] : 0;
-  if (poff32) poff32[e] = (uint32_t)o; else poff[e] = o;
+__global__ __launch_bounds__(256) void k_rows_atomic_off(const uint32_t* __restrict__ rk, int64_t n, uint32_t kmask,
+                                                         uint32_t INV, const uint64_t* __restrict__ doff,
+                                                         const uint32_t* __restrict__ rank,
+                                                         uint32_t* __restrict__ poff32, uint64_t* __restrict__ poff) {
+  const int64_t e0 = (int64_t)blockIdx.x * (256 * RA_PER) + threadIdx.x;
+  uint64_t o[RA_PER];
+#pragma unroll
+  for (int j = 0; j < RA_PER; ++j) {
+    const int64_t e = e0 + j * 256;
+    const uint32_t key = e < n ? rk[e] & kmask : INV;
+    o[j] = key != INV ? doff[(uint64_t)key * RA_SUB + ra_sub(e)] + rank[e] : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < RA_PER; ++j) {
+    const int64_t e = e0 + j * 256;
+    if (e < n) { if (poff32) poff32[e] = (uint32_t)o[j]; else poff[e] = o[j]; }
+  }
 }
 // dense rows: row r = key r, first word = its first sub-range's start
 __global__ void k_rows_dense(const uint64_t* __restrict__ doff, int64_t nk, uint32_t* __restrict__ row_key,
@@ -2281,6 +2299,116 @@ __global__ __launch_bounds__(256) void k_rule_hist(const uint8_t* __restrict__ r
   }
   __syncthreads();
   if (hr[threadIdx.x]) { atomicAdd(&rows[threadIdx.x], hr[threadIdx.x]); atomicAdd(&pairs[threadIdx.x], hp[threadIdx.x]); }
+}
+
+// ---- heads of every part of a part-mode table (ottohip_table_part_heads): per part p the first K rows of
+// (v desc, aid asc, aid_next asc) among rows with v >= thr (v = count_ge2 or count) are exactly the rows
+// with v > c*_p, or v == c*_p and (aid, aid_next) <= (a*_p, n*_p) -- the cut found by histograms over v,
+// then over the aids of the tie rows, then over the aid_next of the cut aid (no sort of the part).
+constexpr int PH_MAXP = 32;        // parts per call
+constexpr uint32_t PH_VBINS = 65536;  // v histogram bins (v >= 65535 share the last: the host falls back)
+struct PartCut {
+  uint32_t cstar[PH_MAXP];  // 0: keep every row with v >= thr
+  uint32_t astar[PH_MAXP];  // 0xFFFFFFFF: no tie cut on aid (every tie row kept)
+  uint32_t nstar[PH_MAXP];
+  uint32_t stage[PH_MAXP];  // tie histograms: 1 = aids of the v == c* rows, 2 = aid_next of the (c*, a*) rows
+};
+__device__ __forceinline__ uint32_t ph_val(const uint32_t* c, const uint32_t* c2, int64_t i, int use_ge2) {
+  return use_ge2 ? c2[i] : c[i];
+}
+__global__ __launch_bounds__(256) void k_ph_hist(const uint8_t* __restrict__ rule, const uint32_t* __restrict__ c,
+                                                 const uint32_t* __restrict__ c2, int64_t n, int n_parts, int use_ge2,
+                                                 uint32_t thr, unsigned long long* __restrict__ hist) {
+  __shared__ uint32_t hs[PH_MAXP][256];
+  for (int i = threadIdx.x; i < PH_MAXP * 256; i += 256) (&hs[0][0])[i] = 0;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t p = rule[i];
+    if (p >= (uint32_t)n_parts) continue;
+    const uint32_t v = ph_val(c, c2, i, use_ge2);
+    if (v < thr) continue;
+    if (v < 256u) atomicAdd(&hs[p][v], 1u);
+    else atomicAdd(&hist[(uint64_t)p * PH_VBINS + (v < PH_VBINS ? v : PH_VBINS - 1)], 1ull);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n_parts * 256; i += 256) {
+    const uint32_t x = (&hs[0][0])[i];
+    if (x) atomicAdd(&hist[(uint64_t)(i >> 8) * PH_VBINS + (i & 255)], (unsigned long long)x);
+  }
+}
+// tie histograms of stage `st` (1: aid of the v == c* rows, 2: aid_next of the v == c*, aid == a* rows)
+__global__ void k_ph_tie_hist(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a, const int32_t* __restrict__ b,
+                              const uint32_t* __restrict__ c, const uint32_t* __restrict__ c2, int64_t n, int n_parts,
+                              int use_ge2, PartCut pc, int st, int64_t n_items, uint32_t* __restrict__ h) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t p = rule[i];
+    if (p >= (uint32_t)n_parts || pc.stage[p] != (uint32_t)st) continue;
+    if (ph_val(c, c2, i, use_ge2) != pc.cstar[p]) continue;
+    const uint32_t ai = (uint32_t)a[i];
+    if (st == 1) atomicAdd(&h[(uint64_t)p * n_items + ai], 1u);
+    else if (ai == pc.astar[p]) atomicAdd(&h[(uint64_t)p * n_items + (uint32_t)b[i]], 1u);
+  }
+}
+// smallest index j with incl[j] >= need (incl = inclusive prefix of one part's histogram)
+__global__ void k_ph_find(const uint64_t* __restrict__ excl, const uint32_t* __restrict__ h, int64_t n, uint64_t need,
+                          uint32_t* __restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint64_t lo = excl[j], hi = lo + h[j];
+  if (h[j] && lo < need && need <= hi) { out[0] = (uint32_t)j; out[1] = (uint32_t)(need - lo); }
+}
+__device__ __forceinline__ bool ph_keep(const uint8_t* rule, const int32_t* a, const int32_t* b, const uint32_t* c,
+                                        const uint32_t* c2, int64_t i, int n_parts, int use_ge2, uint32_t thr,
+                                        const PartCut& pc) {
+  const uint32_t p = rule[i];
+  if (p >= (uint32_t)n_parts) return false;
+  const uint32_t v = ph_val(c, c2, i, use_ge2);
+  if (v < thr) return false;
+  const uint32_t cs = pc.cstar[p];
+  if (v != cs) return v > cs;
+  if (pc.astar[p] == 0xFFFFFFFFu) return true;
+  const uint32_t ai = (uint32_t)a[i];
+  return ai < pc.astar[p] || (ai == pc.astar[p] && (uint32_t)b[i] <= pc.nstar[p]);
+}
+__global__ __launch_bounds__(FIN_T) void k_ph_count(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
+                                                    const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
+                                                    const uint32_t* __restrict__ c2, int64_t n, int n_parts, int use_ge2,
+                                                    uint32_t thr, PartCut pc, uint32_t* __restrict__ bcnt) {
+  __shared__ uint32_t wt[FIN_T / 64];
+  const int64_t base = (int64_t)blockIdx.x * FIN_B;
+  uint32_t k = 0;
+  for (int q = 0; q < FIN_PER; ++q) {
+    const int64_t i = base + q * FIN_T + threadIdx.x;
+    k += (i < n && ph_keep(rule, a, b, c, c2, i, n_parts, use_ge2, thr, pc)) ? 1u : 0u;
+  }
+  k = wave_sum(k);
+  if ((threadIdx.x & 63) == 0) wt[threadIdx.x >> 6] = k;
+  __syncthreads();
+  if (threadIdx.x == 0) bcnt[blockIdx.x] = wt[0] + wt[1] + wt[2] + wt[3];
+}
+// kept rows -> records {aid, aid_next, v, 0} (rule 0) at block offsets boff
+__global__ __launch_bounds__(FIN_T) void k_ph_compact(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
+                                                      const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
+                                                      const uint32_t* __restrict__ c2, int64_t n, int n_parts,
+                                                      int use_ge2, uint32_t thr, PartCut pc,
+                                                      const uint64_t* __restrict__ boff, uint4* __restrict__ out) {
+  __shared__ uint32_t wt[FIN_T / 64];
+  const int w = threadIdx.x >> 6;
+  const int64_t base = (int64_t)blockIdx.x * FIN_B;
+  uint64_t run = boff[blockIdx.x];
+  for (int q = 0; q < FIN_PER; ++q) {
+    const int64_t i = base + q * FIN_T + threadIdx.x;
+    const bool keep = i < n && ph_keep(rule, a, b, c, c2, i, n_parts, use_ge2, thr, pc);
+    const uint64_t bal = __ballot(keep);
+    if ((threadIdx.x & 63) == 0) wt[w] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < FIN_T / 64; ++k) { pre += k < w ? wt[k] : 0u; tot += wt[k]; }
+    if (keep) out[run + pre + mbcnt(bal)] = make_uint4((uint32_t)a[i], (uint32_t)b[i], ph_val(c, c2, i, use_ge2), 0u);
+    run += tot;
+    __syncthreads();
+  }
 }
 
 // ------------------------------------------------------------------ finalize (merge A6)
