@@ -338,6 +338,16 @@ int ottohip_kmeans_lloyd_iter(ottohip_ctx* ctx, const float* X, int64_t n, int d
 int ottohip_kmeans_lloyd_steps(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* centroids, int k,
                                int32_t* labels, int64_t* sums, int64_t* counts, int max_steps, double tol,
                                double* out, void* stream);
+/* lloyd_steps for TWO independent runs (two n_init runs of :152-159) in lockstep: one read of X per step
+ * scores both (the step is bound by the X stream). centroids / labels / sums / counts are HOST arrays
+ * of the two runs' device pointers, max_steps (HOST int[2]) the step budget of each run (0: the run sits
+ * out); out (HOST double[12]) = the 6 values of lloyd_steps per run. Each
+ * run's labels, centres, stop step and reason equal lloyd_steps on that run alone (no distance bounds
+ * here). OTTOHIP_ELIMIT for shapes outside the pair kernel (32 < k <= 64, dim <= 112): run them one
+ * at a time. */
+int ottohip_kmeans_lloyd_steps_pair(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* const* centroids,
+                                    int k, int32_t* const* labels, int64_t* const* sums, int64_t* const* counts,
+                                    const int* max_steps, double tol, double* out, void* stream);
 /* The E-step of lloyd_steps is a split-precision pass (x = hi + lo and c = hi + lo in bf16, three bf16
  * MFMA products, a rigorous error bound) that decides every row whose two best scores are separated
  * beyond the bound, plus the exact f32 kernel on the remaining near ties: labels, sums and stop

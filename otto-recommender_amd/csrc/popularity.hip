@@ -780,6 +780,209 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
   if (l == 0 && w) atomicAdd(changed, (unsigned long long)w);
 }
 
+// Two n_init runs in lockstep over ONE read of X (C2, the reference's 10 independent runs): the
+// split-precision E-step of k_km_assign_split for run 0 and run 1 of a pair, each with its own
+// centroid fragments, LDS sums, labels, near-tie list and stop gate. The step is bound by the X stream
+// (5.2 GB at 12.9 M x 100): one pass instead of two halves it, and the two runs' MFMA chains fill the
+// time the single-run kernel spent waiting on memory. Every run sees exactly the arithmetic of
+// k_km_assign_split (same scores, same near-tie test, same fixed-point sums), so its labels, centres
+// and stopping step are those of the run alone. No distance bounds (every row is scored).
+struct KmPair {
+  const float* C[2];
+  const float* cn[2];
+  int32_t* label[2];
+  unsigned long long* sums[2];
+  unsigned long long* cnt[2];
+  unsigned long long* changed[2];
+  const int* gate[2];
+  uint32_t* amb_rows[2];
+  unsigned long long* n_amb[2];
+};
+constexpr int KMP_AMB = 1024;  // near-tie rows staged per block and run
+template <int NB, int KS>
+__global__ __launch_bounds__(KM_MT, 1) void k_km_assign_split_pair(const float* __restrict__ X, int64_t n, int dim,
+                                                                   int k, KmPair P) {
+  bool act[2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) act[g] = !(P.gate[g] && __builtin_amdgcn_readfirstlane(*P.gate[g]));
+  if (!act[0] && !act[1]) return;
+  extern __shared__ unsigned long long smem64[];
+  uint4* Cf = reinterpret_cast<uint4*>(smem64);                                   // [2][NB][KS][hi, lo][64]
+  unsigned long long* ls = reinterpret_cast<unsigned long long*>(Cf + 2 * NB * KS * 2 * 64);  // [2][k * dim]
+  unsigned long long* lc = ls + 2 * k * dim;                                      // [2][k]
+  int32_t* labl = reinterpret_cast<int32_t*>(lc + 2 * k);                         // [waves][3][32]
+  float* cnl = reinterpret_cast<float*>(labl + (KM_MT / 64) * 96);                // [2][64]
+  uint32_t* amb = reinterpret_cast<uint32_t*>(cnl + 128);                         // [2][KMP_AMB]
+  __shared__ uint32_t namb[2];
+  __shared__ unsigned long long abase[2];
+  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6, h = l >> 5, i32 = l & 31;
+  for (int e = tid; e < 2 * NB * KS * 64; e += KM_MT) {
+    const int ll = e & 63, gsb = e >> 6, g = gsb / (NB * KS), sb = gsb % (NB * KS), s_ = sb % KS, b = sb / KS;
+    const int c = b * 32 + (ll & 31), d0 = 16 * s_ + 8 * (ll >> 5);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (act[g] && c < k && d0 + j < dim) ? P.C[g][(int64_t)c * dim + d0 + j] : 0.f;
+    uint4 hi, lo;
+    km_split8(v, hi, lo);
+    Cf[((g * NB * KS + sb) * 2 + 0) * 64 + ll] = hi;
+    Cf[((g * NB * KS + sb) * 2 + 1) * 64 + ll] = lo;
+  }
+  if (tid < 128) cnl[tid] = act[tid >> 6] ? P.cn[tid >> 6][tid & 63] : 0.f;
+  for (int i = tid; i < 2 * (k * dim + k); i += KM_MT) ls[i] = 0ull;  // ls and lc are adjacent
+  if (tid < 2) namb[tid] = 0;
+  __syncthreads();
+  float cmax[2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    float c2 = l < k ? cnl[g * 64 + l] : 0.f;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) c2 = fmaxf(c2, __shfl_xor(c2, o));
+    cmax[g] = sqrtf(c2);
+  }
+  uint32_t nchg[2] = {0, 0};
+  const int64_t ntile = (n + 31) >> 5;
+  const int64_t nwv = (int64_t)gridDim.x * (KM_MT / 64);
+  float4 raw[2 * KS];
+  int32_t lab_n[2] = {-1, -1};
+  int64_t row_n = 0;
+  auto load = [&](int64_t tt) __attribute__((always_inline)) {
+    const int64_t rr = (tt << 5) + i32 < n ? (tt << 5) + i32 : n - 1;
+    row_n = rr;
+    const float* xp = X + rr * dim;
+#pragma unroll
+    for (int s_ = 0; s_ < KS; ++s_) {
+      const int d0 = 16 * s_ + 8 * h;
+      raw[2 * s_] = d0 < dim ? *reinterpret_cast<const float4*>(xp + d0) : make_float4(0.f, 0.f, 0.f, 0.f);
+      raw[2 * s_ + 1] = d0 + 4 < dim ? *reinterpret_cast<const float4*>(xp + d0 + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int g = 0; g < 2; ++g) lab_n[g] = act[g] ? P.label[g][rr] : -1;
+  };
+  const int64_t t_first = (int64_t)blockIdx.x * (KM_MT / 64) + wv;
+  if (t_first < ntile) load(t_first);
+  for (int64_t t = t_first; t < ntile; t += nwv) {
+    const int64_t r0 = t << 5;
+    const bool in_r = r0 + i32 < n;
+    const int64_t row = row_n;
+    km_bf16x8 xh[KS], xl[KS];
+    float xs = 0.f;
+#pragma unroll
+    for (int s_ = 0; s_ < KS; ++s_) {
+      const float4 p0 = raw[2 * s_], p1 = raw[2 * s_ + 1];
+      const float v[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xs += v[j] * v[j];
+      uint4 hi, lo;
+      km_split8(v, hi, lo);
+      xh[s_] = __builtin_bit_cast(km_bf16x8, hi);
+      xl[s_] = __builtin_bit_cast(km_bf16x8, lo);
+    }
+    const int32_t lab_cur[2] = {lab_n[0], lab_n[1]};
+    if (t + nwv < ntile) load(t + nwv);
+    xs += __shfl_xor(xs, 32);
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      if (!act[g]) continue;  // wave-uniform
+      const uint4* Cg = Cf + g * NB * KS * 2 * 64;
+      const float* cng = cnl + g * 64;
+      km_f32x16 acc0 = {}, acc1 = {};
+#pragma unroll
+      for (int s_ = 0; s_ < KS; ++s_) {
+        const km_bf16x8 ch0 = __builtin_bit_cast(km_bf16x8, Cg[((0 * KS + s_) * 2 + 0) * 64 + l]);
+        const km_bf16x8 cl0 = __builtin_bit_cast(km_bf16x8, Cg[((0 * KS + s_) * 2 + 1) * 64 + l]);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, xh[s_], acc0, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, xl[s_], acc0, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl0, xh[s_], acc0, 0, 0, 0);
+        if (NB == 2) {
+          const km_bf16x8 ch1 = __builtin_bit_cast(km_bf16x8, Cg[((1 * KS + s_) * 2 + 0) * 64 + l]);
+          const km_bf16x8 cl1 = __builtin_bit_cast(km_bf16x8, Cg[((1 * KS + s_) * 2 + 1) * 64 + l]);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, xh[s_], acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, xl[s_], acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl1, xh[s_], acc1, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 n0 = *reinterpret_cast<const float4*>(cng + 8 * j + 4 * h);
+        acc0[4 * j + 0] = n0.x - 2.f * acc0[4 * j + 0];
+        acc0[4 * j + 1] = n0.y - 2.f * acc0[4 * j + 1];
+        acc0[4 * j + 2] = n0.z - 2.f * acc0[4 * j + 2];
+        acc0[4 * j + 3] = n0.w - 2.f * acc0[4 * j + 3];
+        if (NB == 2) {
+          const float4 n1 = *reinterpret_cast<const float4*>(cng + 32 + 8 * j + 4 * h);
+          acc1[4 * j + 0] = n1.x - 2.f * acc1[4 * j + 0];
+          acc1[4 * j + 1] = n1.y - 2.f * acc1[4 * j + 1];
+          acc1[4 * j + 2] = n1.z - 2.f * acc1[4 * j + 2];
+          acc1[4 * j + 3] = n1.w - 2.f * acc1[4 * j + 3];
+        }
+      }
+      float m = INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        m = fminf(m, acc0[r]);
+        if (NB == 2) m = fminf(m, acc1[r]);
+      }
+      int mc = 64;
+#pragma unroll
+      for (int r = 15; r >= 0; --r) {
+        if (NB == 2) mc = acc1[r] == m ? 32 + (r & 3) + 8 * (r >> 2) + 4 * h : mc;
+      }
+#pragma unroll
+      for (int r = 15; r >= 0; --r) mc = acc0[r] == m ? (r & 3) + 8 * (r >> 2) + 4 * h : mc;
+      {
+        const float pm = __shfl_xor(m, 32);
+        const int pc = __shfl_xor(mc, 32);
+        if (pm < m || (pm == m && pc < mc)) { m = pm; mc = pc; }
+      }
+      float m2 = INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int c0 = (r & 3) + 8 * (r >> 2) + 4 * h;
+        m2 = fminf(m2, c0 == mc ? INFINITY : acc0[r]);
+        if (NB == 2) m2 = fminf(m2, c0 + 32 == mc ? INFINITY : acc1[r]);
+      }
+      m2 = fminf(m2, __shfl_xor(m2, 32));
+      const bool decided = m2 - m > KMS_SEP * sqrtf(xs) * cmax[g];
+      const uint32_t mi = (uint32_t)mc;
+      const bool mine = h == 0 && in_r && decided;
+      int32_t old = -1;
+      if (mine) {
+        old = lab_cur[g];
+        nchg[g] += old != (int32_t)mi;
+        if (old != (int32_t)mi) P.label[g][row] = (int32_t)mi;
+      }
+      const bool tie = h == 0 && in_r && !decided;
+      const uint64_t tm = __ballot(tie);
+      if (tm) {
+        uint32_t b = 0;
+        if (l == 0) b = atomicAdd(&namb[g], (uint32_t)__popcll(tm));
+        b = __shfl(b, 0);
+        if (tie) {
+          const uint32_t p = b + mbcnt(tm);
+          if (p < (uint32_t)KMP_AMB) amb[g * KMP_AMB + p] = (uint32_t)row;
+          else P.amb_rows[g][atomicAdd(P.n_amb[g], 1ull)] = (uint32_t)row;
+        }
+      }
+      km_move_rows(X, dim, ls + g * k * dim, lc + g * k, labl + wv * 96, mine && old != (int32_t)mi, row, mi, old);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    if (!act[g]) continue;
+    for (int i = tid; i < k * dim; i += KM_MT)
+      if (ls[g * k * dim + i]) atomicAdd(&P.sums[g][i], ls[g * k * dim + i]);
+    for (int i = tid; i < k; i += KM_MT)
+      if (lc[g * k + i]) atomicAdd(&P.cnt[g][i], lc[g * k + i]);
+    const uint32_t na = namb[g] < (uint32_t)KMP_AMB ? namb[g] : (uint32_t)KMP_AMB;
+    if (tid == 0) abase[g] = na ? atomicAdd(P.n_amb[g], (unsigned long long)na) : 0ull;
+    __syncthreads();
+    for (uint32_t i = tid; i < na; i += KM_MT) P.amb_rows[g][abase[g] + i] = amb[g * KMP_AMB + i];
+    const uint32_t w = wave_sum(nchg[g]);
+    if (l == 0 && w) atomicAdd(P.changed[g], (unsigned long long)w);
+  }
+}
+
 // inc: sums / cnt hold the exact sums / counts of the rows under `labels` (the previous labels) and
 // are updated by the rows whose label changes (MFMA kernel); otherwise they are accumulated from
 // scratch by every row (the caller zeroes them)
@@ -1449,6 +1652,103 @@ int ottohip_kmeans_lloyd_steps(ottohip_ctx* ctx, const float* X, int64_t n, int 
   out[3] = (double)e;
   out[4] = c2[1];
   out[5] = c2[0];
+  return 0;
+}
+
+// ottohip_kmeans_lloyd_steps for two runs in lockstep (k_km_assign_split_pair: one read of X per step
+// for both runs). Per run the same steps, stop checks and outputs as ottohip_kmeans_lloyd_steps; a
+// run that stops (its gate) costs nothing in the other run's later steps.
+__global__ void k_km_gate_set(int* __restrict__ ctl, int reason) {
+  if (threadIdx.x == 0 && ctl[0] == 0) ctl[0] = reason;
+}
+
+int ottohip_kmeans_lloyd_steps_pair(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* const* centroids,
+                                    int k, int32_t* const* labels, int64_t* const* sums, int64_t* const* counts,
+                                    const int* max_steps, double tol, double* out, void* stream) {
+  if (!ctx || !X || !centroids || !labels || !sums || !counts || !out || !max_steps || n < 1 || dim < 1 ||
+      dim > EMB_MAXD || k < 1 || k > KM_MAXK || max_steps[0] < 0 || max_steps[1] < 0) {
+    set_error("kmeans_lloyd_steps_pair: bad arguments (k <= %d, dim <= %d)", KM_MAXK, EMB_MAXD); return OTTOHIP_EINVAL;
+  }
+  for (int g = 0; g < 2; ++g)
+    if (!centroids[g] || !labels[g] || !sums[g] || !counts[g] || !km_mfma_ok(k, dim, X, centroids[g]) || k <= 32 ||
+        dim > 112 || n > 0xFFFFFFFFll) {
+      set_error("kmeans_lloyd_steps_pair: needs the MFMA E-step (32 < k <= 64, dim <= 112, aligned operands)");
+      return OTTOHIP_ELIMIT;
+    }
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  ctx->km_bvalid = false;  // no distance bounds in lockstep steps
+  constexpr int NB = 2, KS = 7;
+  const int KP = (k + 7) / 8 * 8, nq = (dim + 7) / 8;
+  double* st;  // [2][inertia, changed, shift, empty]
+  int* ctl;    // [2][reason, steps]
+  OH_TRY(ctx->ws.get("kmp_stats", 8, &st));
+  OH_TRY(ctx->ws.get("kmp_ctl", 4, &ctl));
+  OH_HIP(hipMemsetAsync(ctl, 0, 4 * sizeof(int), s));
+  KmPair P;
+  float* Ct[2];
+  float* cn[2];
+  const char* ctn[2] = {"kmp_ct0", "kmp_ct1"};
+  const char* cnn[2] = {"kmp_cn0", "kmp_cn1"};
+  const char* abn[2] = {"kmp_amb0", "kmp_amb1"};
+  const char* nan_[2] = {"kmp_namb0", "kmp_namb1"};
+  for (int g = 0; g < 2; ++g) {
+    OH_TRY(ctx->ws.get(ctn[g], (size_t)KP * dim, &Ct[g]));
+    OH_TRY(ctx->ws.get(cnn[g], (size_t)KM_MAXK, &cn[g]));
+    OH_TRY(ctx->ws.get(abn[g], (size_t)n, &P.amb_rows[g]));
+    OH_TRY(ctx->ws.get(nan_[g], 1, &P.n_amb[g]));
+    P.C[g] = centroids[g];
+    P.cn[g] = cn[g];
+    P.label[g] = labels[g];
+    P.sums[g] = reinterpret_cast<unsigned long long*>(sums[g]);
+    P.cnt[g] = reinterpret_cast<unsigned long long*>(counts[g]);
+    P.changed[g] = reinterpret_cast<unsigned long long*>(st + 4 * g + 1);
+    P.gate[g] = ctl + 2 * g;
+  }
+  const size_t lds2 = (size_t)2 * NB * KS * 2 * 64 * 16 + (size_t)2 * ((size_t)k * dim + k) * 8 + (KM_MT / 64) * 96 * 4 +
+                      128 * 4 + (size_t)2 * KMP_AMB * 4;
+  OH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_km_assign_split_pair<NB, KS>),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
+  auto ek = nq == 13 ? k_km_assign_mfma<NB, 13, true> : k_km_assign_mfma<NB, KM_NQ, true>;
+  const size_t lds = (size_t)NB * nq * 64 * 16 + (KM_MT / 64) * 96 * 4 + 64 * 4 + ((size_t)k * dim + k) * 8;
+  OH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(ek), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const int64_t ntile = ceil_div(n, 32);
+  const unsigned pgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(ntile, KM_MT / 64), ctx->n_cu));
+  const unsigned egrid = (unsigned)std::max(1, ctx->n_cu / 2);
+  const int steps = std::max(max_steps[0], max_steps[1]);
+  for (int i = 0; i < steps; ++i) {
+    for (int g = 0; g < 2; ++g) {
+      if (i == max_steps[g]) k_km_gate_set<<<1, 64, 0, s>>>(ctl + 2 * g, 4);  // this run's step budget is spent
+      k_km_gate_reset<<<1, 64, 0, s>>>(ctl + 2 * g, st + 4 * g);
+      k_km_prep<<<grid_for(std::max<int64_t>((int64_t)KP * dim, KM_MAXK)), 256, 0, s>>>(centroids[g], k, dim, KP, Ct[g],
+                                                                                       cn[g]);
+      OH_HIP(hipMemsetAsync(P.n_amb[g], 0, 8, s));
+    }
+    k_km_assign_split_pair<NB, KS><<<pgrid, KM_MT, lds2, s>>>(X, n, dim, k, P);
+    for (int g = 0; g < 2; ++g)  // the near ties of each run, exact f32 scores
+      ek<<<egrid, KM_MT, lds, s>>>(X, n, dim, nq, centroids[g], cn[g], k, labels[g], P.sums[g], P.cnt[g], st + 4 * g,
+                                   P.changed[g], nullptr, 1, P.gate[g], P.amb_rows[g], P.n_amb[g]);
+    for (int g = 0; g < 2; ++g)
+      k_km_update<<<1, KM_UT, 0, s>>>(centroids[g], reinterpret_cast<const long long*>(sums[g]),
+                                      reinterpret_cast<const long long*>(counts[g]), k, dim, 1, st + 4 * g + 2,
+                                      ctl + 2 * g, reinterpret_cast<const unsigned long long*>(st + 4 * g + 1), tol);
+  }
+  OH_HIP(hipGetLastError());
+  double h[8];
+  int c2[4];
+  OH_TRY(d2h(h, st, 8, s));
+  OH_TRY(d2h(c2, ctl, 4, s));
+  for (int g = 0; g < 2; ++g) {
+    unsigned long long c, e;
+    memcpy(&c, &h[4 * g + 1], 8);
+    memcpy(&e, &h[4 * g + 3], 8);
+    out[6 * g + 0] = h[4 * g];
+    out[6 * g + 1] = (double)c;
+    out[6 * g + 2] = h[4 * g + 2];
+    out[6 * g + 3] = (double)e;
+    out[6 * g + 4] = c2[2 * g + 1];
+    out[6 * g + 5] = c2[2 * g] == 4 ? 0 : c2[2 * g];  // 4: stopped by its step budget, not a stop check
+  }
   return 0;
 }
 

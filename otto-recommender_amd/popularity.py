@@ -12,6 +12,7 @@ All compute runs in libottohip.so (csrc/popularity.hip).
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -161,7 +162,25 @@ class KMeans:
         best = None
         inr, chg, shift = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
         st6 = (ctypes.c_double * 6)()
+        # two runs in lockstep over one read of X per Lloyd step (ottohip_kmeans_lloyd_steps_pair) on one
+        # GPU; OTTOHIP_KM_PAIR=0 runs them one at a time (A/B switch)
+        pair_ok = (group is None and 32 < k <= 64 and dim <= 112 and dim % 4 == 0
+                   and os.environ.get("OTTOHIP_KM_PAIR", "1") != "0")
+        pending = None  # the second run of a pair, finished in lockstep with the first
         for run in range(self.n_init):
+            if pending is not None:
+                inertia, Cp, labp, itp = pending
+                pending = None
+                if best is None or inertia < best[0]:
+                    best = (inertia, Cp, labp, itp)
+                continue
+            if pair_ok and run + 1 < self.n_init:
+                res = self._fit_pair(Xc, [next(seed_stream), next(seed_stream)], grows, tol_abs, ctx, sh)
+                pending = res[1]
+                inertia, Cp, labp, itp = res[0]
+                if best is None or inertia < best[0]:
+                    best = (inertia, Cp, labp, itp)
+                continue
             seeds = next(seed_stream)
             C = self._gather_rows(Xc, seeds, grows, group)
             labels.fill_(-1)
@@ -218,6 +237,58 @@ class KMeans:
         self.inertia_, C, self.labels_, self.n_iter_ = best
         self.cluster_centers_ = C + mean_d
         return self
+
+    def _fit_pair(self, Xc, seeds2, grows, tol_abs, ctx, sh):
+        """Two runs of fit's single-GPU loop in lockstep: the same batches of device Lloyd steps, stop
+        checks and empty-cluster relocations per run, each run's E-step sharing one read of X with the
+        other's. Returns [(inertia, C, labels, n_iter)] for the two runs, in run order."""
+        import torch
+        lib = _lib.load()
+        n, dim = (int(v) for v in Xc.shape)
+        k = self.n_clusters
+        dev = Xc.device
+        C = [self._gather_rows(Xc, sd, grows, None) for sd in seeds2]
+        lab = [torch.full((max(n, 1),), -1, dtype=torch.int32, device=dev) for _ in range(2)]
+        sums = [torch.zeros(k * dim, dtype=torch.int64, device=dev) for _ in range(2)]
+        counts = [torch.zeros(k, dtype=torch.int64, device=dev) for _ in range(2)]
+        P = ctypes.c_void_p * 2
+        pc, pl = P(*[_lib.ptr(x) for x in C]), P(*[_lib.ptr(x) for x in lab])
+        ps, pn = P(*[_lib.ptr(x) for x in sums]), P(*[_lib.ptr(x) for x in counts])
+        it, done, strict = [0, 0], [False, False], [False, False]
+        st12 = (ctypes.c_double * 12)()
+        shift = ctypes.c_double()
+        while not all(done):
+            steps = (ctypes.c_int * 2)(*[0 if done[g] else min(LLOYD_BATCH, self.max_iter - it[g]) for g in range(2)])
+            _lib.check(lib.ottohip_kmeans_lloyd_steps_pair(ctx.h, _lib.ptr(Xc), n, dim, pc, k, pl, ps, pn, steps,
+                                                           tol_abs, st12, sh))
+            for g in range(2):
+                if done[g]:
+                    continue
+                it[g] += int(st12[6 * g + 4])
+                n_changed, reason = int(st12[6 * g + 1]), int(st12[6 * g + 5])
+                shift.value = st12[6 * g + 2]
+                if reason == 3:  # empty clusters: relocate on a copy (sums / counts follow the labels), M-step
+                    rs_, rc_ = sums[g].clone(), counts[g].clone()
+                    empty = np.flatnonzero(rc_.cpu().numpy() == 0)
+                    self._relocate(Xc, C[g], lab[g], rs_, rc_, empty, grows, None, ctx, sh)
+                    _lib.check(lib.ottohip_kmeans_update(ctx.h, _lib.ptr(C[g]), _lib.ptr(rs_), _lib.ptr(rc_), k, dim,
+                                                         ctypes.byref(shift), sh))
+                    reason = 1 if n_changed == 0 else (2 if shift.value <= tol_abs else 0)
+                if reason == 1:
+                    strict[g] = True
+                if reason in (1, 2) or it[g] >= self.max_iter:
+                    done[g] = True
+        out = []
+        inr, chg = ctypes.c_double(), ctypes.c_int64()
+        for g in range(2):
+            if not strict[g]:  # E-step with the final centres (labels match cluster_centers_)
+                _lib.check(lib.ottohip_kmeans_partial(ctx.h, _lib.ptr(Xc), n, dim, _lib.ptr(C[g]), k, _lib.ptr(lab[g]),
+                                                      _lib.ptr(sums[g]), _lib.ptr(counts[g]), ctypes.byref(inr),
+                                                      ctypes.byref(chg), sh))
+            _lib.check(lib.ottohip_kmeans_inertia(ctx.h, _lib.ptr(Xc), n, dim, _lib.ptr(C[g]), _lib.ptr(lab[g]),
+                                                  ctypes.byref(inr), sh))
+            out.append((float(inr.value), C[g], lab[g][:n], it[g]))
+        return out
 
     @staticmethod
     def _gather_rows(Xc, rows, grows, group):
