@@ -90,11 +90,18 @@ constexpr int KN_GL = KN_IT * KN_CH / KN_T;  // glds per thread per tile (8)
 //   bound of the query's KN_C-th best score -> thr_io[q]. MODE 0 then inserts only items above it.
 // KS = k-steps of 16 over the packed row: ceil((dim + 2) / 16) rounded up to 7 or 8 (dim 100 -> 7,
 // so the zero padding of columns 112..127 is neither streamed nor multiplied).
-template <int ABL, int KS>
+// BUF (MODE 0): the register list keeps scores only (one v_med3 per slot per insert instead of a
+//   compare, a med3 and two index selects); every inserted (score, item) is appended to the query's
+//   buffer cbuf[q * KN_BCAP ..] in insertion order and ncand[q] counts them. The final list is the
+//   first KN_C of the inserted candidates by (score desc, insertion order) -- exactly the candidates the
+//   index list would hold -- which k_knn_rerank_buf selects before the exact rerank.
+constexpr int KN_BCAP = 512;  // inserted candidates kept per query (overflow: the search reruns with index lists)
+template <int ABL, int KS, bool BUF = false>
 __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ items, int64_t V,
                                                   const uint4* __restrict__ queries, int64_t nq,
                                                   uint32_t* __restrict__ cand, float* __restrict__ thr_io,
-                                                  int pre_stride) {
+                                                  int pre_stride, uint2* __restrict__ cbuf = nullptr,
+                                                  uint32_t* __restrict__ ncand = nullptr) {
   __shared__ uint4 ring[KN_RING * KN_IT * KN_CH];  // 2 x 64 KiB, the only LDS object
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, r = l & 31, h = l >> 5;
   const int64_t qbase = (int64_t)blockIdx.x * KN_QB + w * 64;
@@ -147,7 +154,23 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
   // branch-free shift: slot j takes slot j-1 if s beats it, else s if s beats slot j (score: one
   // v_med3 of (sc[j-1], s, sc[j]); index: two selects). A lane-dependent "replace the minimum"
   // slot becomes a compare/select chain over every slot instead.
+  uint32_t nbuf = 0;
   auto insert = [&](float s_, uint32_t item) __attribute__((always_inline)) {
+    if constexpr (BUF) {
+      if (!PRE) {
+        if (q < nq && nbuf < (uint32_t)KN_BCAP)  // padding lanes past nq keep no buffer
+          cbuf[(size_t)q * KN_BCAP + nbuf] = make_uint2(__float_as_uint(s_), item);
+        ++nbuf;
+#pragma unroll
+        for (int jj = 0; jj < KN_C - 1; ++jj) {  // scores only: slot j takes max(slot j-1 clipped by s, ...)
+          const int j = KN_C - 1 - jj;
+          sc[j] = __builtin_amdgcn_fmed3f(sc[j - 1], s_, sc[j]);
+        }
+        sc[0] = fmaxf(sc[0], s_);
+        thr = sc[KN_C - 1];
+        return;
+      }
+    }
     bool cj = s_ > sc[KN_C - 1];
 #pragma unroll
     for (int jj = 0; jj < KN_C - 1; ++jj) {  // downwards: slot j - 1 still holds its old value
@@ -274,9 +297,44 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
     if (q < nq) thr_io[q] = nextafterf(sc[KN_C - 1], -INFINITY);  // items tying the bound are still inserted
     return;
   }
+  if constexpr (BUF) {
+    if (q < nq) ncand[q] = nbuf;
+    return;
+  }
   if (q < nq) {
 #pragma unroll
     for (int j = 0; j < KN_CAND; ++j) cand[q * KN_CAND + j] = j < KN_C ? ix[j] : 0xFFFFFFFFu;
+  }
+}
+
+// BUF search: per query (one wave) the first KN_C inserted candidates by (score desc, insertion order):
+// each lane ranks its buffer entries against all of them (keys unique by position), the entries of rank
+// < KN_C go to cand[] in rank order; a query with more than KN_BCAP inserts sets *overflow
+__global__ __launch_bounds__(256) void k_knn_select_buf(const uint2* __restrict__ cbuf,
+                                                        const uint32_t* __restrict__ ncand, int64_t nq,
+                                                        uint32_t* __restrict__ cand, int* __restrict__ overflow) {
+  __shared__ uint64_t keys[4][KN_BCAP];
+  const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int w = threadIdx.x >> 6;
+  const uint32_t l = lane_id();
+  if (q >= nq) return;
+  const uint32_t nc = ncand[q];
+  if (nc > (uint32_t)KN_BCAP) { if (l == 0) atomicOr(overflow, 1); return; }
+  const uint2* b = cbuf + (size_t)q * KN_BCAP;
+  for (uint32_t i = l; i < nc; i += 64) {  // ascending key = (score desc, position asc)
+    const uint32_t sb = b[i].x;
+    const uint32_t ord = (sb & 0x80000000u) ? ~sb : (sb | 0x80000000u);
+    keys[w][i] = ((uint64_t)~ord << 32) | i;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  for (uint32_t i = l; i < KN_CAND; i += 64) cand[q * KN_CAND + i] = 0xFFFFFFFFu;
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t i = l; i < nc; i += 64) {
+    const uint64_t ki = keys[w][i];
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < nc; ++j) r += keys[w][j] < ki ? 1u : 0u;
+    if (r < (uint32_t)KN_C) cand[q * KN_CAND + r] = b[i].y;
   }
 }
 
@@ -412,15 +470,41 @@ int ottohip_knn_topk(ottohip_ctx* c, const ottohip_knn_index* ix, const int32_t*
     const int64_t nS = (nT - 1 + pst - 1) / pst;
     ph = ctx->begin("knn_pre", s, 2.0 * (double)n_q * (double)(nS * KN_IT) * ix->dim);
     (k8 ? k_knn_main<2, 8> : k_knn_main<2, 7>)<<<grid, KN_T, 0, s>>>(reinterpret_cast<const uint4*>(ix->packed), ix->n_items,
-                                          reinterpret_cast<const uint4*>(qp), n_q, cand, thr, pst);
+                                          reinterpret_cast<const uint4*>(qp), n_q, cand, thr, pst, nullptr, nullptr);
     ctx->end(ph, s);
   }
   ph = ctx->begin("knn_main", s, 2.0 * (double)n_q * (double)ix->n_items * ix->dim);
-  auto kmain = k8 ? (abl == 3 ? k_knn_main<3, 8> : (abl ? k_knn_main<1, 8> : k_knn_main<0, 8>))
-                  : (abl == 3 ? k_knn_main<3, 7> : (abl ? k_knn_main<1, 7> : k_knn_main<0, 7>));
-  kmain<<<grid, KN_T, 0, s>>>(reinterpret_cast<const uint4*>(ix->packed), ix->n_items,
-                              reinterpret_cast<const uint4*>(qp), n_q, cand, thr, pst);
-  ctx->end(ph, s);
+  // candidate buffers instead of index lists (OTTOHIP_KNN_BUF=0: index lists; A/B switch)
+  static const bool use_buf = !(getenv("OTTOHIP_KNN_BUF") && !strcmp(getenv("OTTOHIP_KNN_BUF"), "0"));
+  bool done = false;
+  if (use_buf && !abl) {
+    uint2* cbuf;
+    uint32_t* ncand;
+    int* ovf;
+    OH_TRY(ctx->ws.get("knn_cbuf", (size_t)n_q * KN_BCAP, &cbuf));
+    OH_TRY(ctx->ws.get("knn_ncand", (size_t)n_q, &ncand));
+    OH_TRY(ctx->ws.get("knn_ovf", 1, &ovf));
+    OH_HIP(hipMemsetAsync(ovf, 0, sizeof(int), s));
+    (k8 ? k_knn_main<0, 8, true> : k_knn_main<0, 7, true>)<<<grid, KN_T, 0, s>>>(
+        reinterpret_cast<const uint4*>(ix->packed), ix->n_items, reinterpret_cast<const uint4*>(qp), n_q, cand, thr, pst,
+        cbuf, ncand);
+    ctx->end(ph, s);
+    ph = ctx->begin("knn_select", s, 0);
+    k_knn_select_buf<<<(unsigned)ceil_div(n_q * 64, 256), 256, 0, s>>>(cbuf, ncand, n_q, cand, ovf);
+    ctx->end(ph, s);
+    int hov = 0;
+    OH_HIP(hipMemcpyAsync(&hov, ovf, sizeof(int), hipMemcpyDeviceToHost, s));
+    OH_HIP(hipStreamSynchronize(s));
+    done = hov == 0;  // else: some query inserted more than KN_BCAP candidates -> index lists
+    if (!done) ph = ctx->begin("knn_main_lists", s, 2.0 * (double)n_q * (double)ix->n_items * ix->dim);
+  }
+  if (!done) {
+    auto kmain = k8 ? (abl == 3 ? k_knn_main<3, 8> : (abl ? k_knn_main<1, 8> : k_knn_main<0, 8>))
+                    : (abl == 3 ? k_knn_main<3, 7> : (abl ? k_knn_main<1, 7> : k_knn_main<0, 7>));
+    kmain<<<grid, KN_T, 0, s>>>(reinterpret_cast<const uint4*>(ix->packed), ix->n_items,
+                                reinterpret_cast<const uint4*>(qp), n_q, cand, thr, pst, nullptr, nullptr);
+    ctx->end(ph, s);
+  }
   ph = ctx->begin("knn_rerank", s, 0);
   k_knn_rerank<<<(unsigned)ceil_div(n_q * 64, 256), 256, 0, s>>>(ix->emb, ix->n_items, ix->dim, query_rows, n_q, cand,
                                                                  k, out_idx, out_d2);
