@@ -475,7 +475,7 @@ int ottohip_knn_topk(ottohip_ctx* c, const ottohip_knn_index* ix, const int32_t*
   }
   ph = ctx->begin("knn_main", s, 2.0 * (double)n_q * (double)ix->n_items * ix->dim);
   // candidate buffers instead of index lists (OTTOHIP_KNN_BUF=0: index lists; A/B switch)
-  static const bool use_buf = !(getenv("OTTOHIP_KNN_BUF") && !strcmp(getenv("OTTOHIP_KNN_BUF"), "0"));
+  const bool use_buf = !(getenv("OTTOHIP_KNN_BUF") && !strcmp(getenv("OTTOHIP_KNN_BUF"), "0"));  // read per call
   bool done = false;
   if (use_buf && !abl) {
     uint2* cbuf;

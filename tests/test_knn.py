@@ -33,6 +33,25 @@ def test_knn_small_exact(gpu):
     _check(emb, rows, 20, gi, gd)
 
 
+def test_knn_candidate_buffers_equal_index_lists(gpu, monkeypatch):
+    """The main pass with per-query candidate buffers (scores-only register lists, the first KN_C inserts
+    by score and insertion order selected before the rerank) returns exactly the indices and distances
+    of the index-list pass (OTTOHIP_KNN_BUF=0), on clustered embeddings with many near-equal scores."""
+    from otto_recommender_amd.w2vec import KnnIndex
+    emb = synth.embeddings(120_000, seed=9)
+    emb[1000:1100] = emb[5]  # exact duplicates: equal scores inserted in order
+    rows = np.concatenate([np.arange(0, 3000), np.arange(1000, 1100)])
+    out = []
+    for buf in ("0", "1"):
+        monkeypatch.setenv("OTTOHIP_KNN_BUF", buf)
+        ix = KnnIndex(emb)
+        i, d = ix.search(rows, k=20)
+        out.append((i.cpu().numpy(), d.cpu().numpy()))
+        ix.free()
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+
+
 def test_knn_arbitrary_rows_tiny_index_and_ties(gpu):
     from otto_recommender_amd.w2vec import KnnIndex
     rng = np.random.default_rng(1)
