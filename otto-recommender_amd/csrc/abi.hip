@@ -536,6 +536,24 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     OH_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_split_fuse), &v, sizeof v, 0, hipMemcpyHostToDevice, s));
     OH_HIP(hipStreamSynchronize(s));
   }
+  // LDS leaf (k_agg_lds) for rows and split buckets of (SORT_MAX, LDS_CAP] words, fed by splits of
+  // LDS_SPLIT_MEAN-word buckets (OTTOHIP_LDS_LEAF=1, read per call; default: register sorts of
+  // SPLIT_MEAN-word buckets only)
+  const bool lds_leaf = getenv("OTTOHIP_LDS_LEAF") && !strcmp(getenv("OTTOHIP_LDS_LEAF"), "1");
+  {
+    static int8_t lds_state[64] = {};  // per device (the constants live in each device's code object): 0 unset, 1 off, 2 on
+    int8_t& st = lds_state[ctx->device & 63];
+    if (st != (lds_leaf ? 2 : 1)) {
+      const uint32_t on = lds_leaf ? 1u : 0u;
+      OH_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_lds_leaf), &on, sizeof on, 0, hipMemcpyHostToDevice, s));
+      if (split_mean == SPLIT_MEAN) {
+        const uint32_t v = lds_leaf ? (uint32_t)LDS_SPLIT_MEAN : (uint32_t)SPLIT_MEAN;
+        OH_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_split_mean), &v, sizeof v, 0, hipMemcpyHostToDevice, s));
+      }
+      OH_HIP(hipStreamSynchronize(s));
+      st = lds_leaf ? 2 : 1;
+    }
+  }
   static const int hash_prio = getenv("OTTOHIP_HASH_PRIO") ? atoi(getenv("OTTOHIP_HASH_PRIO")) : 0;  // A/B switch
   if (hash_prio) {
     const uint32_t v = (uint32_t)hash_prio;
@@ -549,13 +567,16 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   TL.n = lcount;
   // task lists double-buffered by level parity: level l's sorts (aux stream) may still read theirs
   // while level l + 1's classify fills the other set
+  const uint64_t split_extra = P / 512 + 64;
   auto get_lists = [&](uint64_t capl, const char* split_name, int parity) -> int {
     static const char* names[2][N_SORT] = {{"t_sort0", "t_sort1", "t_sort2", "t_sort3", "t_sort4"},
                                            {"t_sort0b", "t_sort1b", "t_sort2b", "t_sort3b", "t_sort4b"}};
     for (int c = 0; c < N_SORT; ++c)
       if (int r = ws.get(names[parity][c], capl * sizeof(Task), reinterpret_cast<void**>(&TL.sort[c]))) return r;
     if (int r = ws.get(parity ? "t_hashb" : "t_hash", capl * sizeof(Task), reinterpret_cast<void**>(&TL.hash))) return r;
-    if (int r = ws.get(split_name, capl * sizeof(Task), reinterpret_cast<void**>(&TL.split))) return r;
+    if (int r = ws.get(parity ? "t_ldsb" : "t_lds", capl * sizeof(Task), reinterpret_cast<void**>(&TL.lds))) return r;
+    // the split list also takes the LDS leaf's hot segments (> 512 words each)
+    if (int r = ws.get(split_name, (capl + split_extra) * sizeof(Task), reinterpret_cast<void**>(&TL.split))) return r;
     TL.cap = capl;
     return 0;
   };
@@ -574,16 +595,16 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   const bool dbg = getenv("OTTOHIP_DEBUG") != nullptr;
   if (dbg) fprintf(stderr, "[ottohip] P=%llu rows=%lld\n", (unsigned long long)P, (long long)Rn);
   for (int level = 0; level < 40; ++level) {
-    unsigned long long nlist[N_SORT + 2];
-    if ((rc = d2h(nlist, lcount, N_SORT + 2, s))) return rc;
+    unsigned long long nlist[N_LISTS];
+    if ((rc = d2h(nlist, lcount, N_LISTS, s))) return rc;
     if ((rc = d2h(&herr, err, 1, s))) return rc;
     if (herr) { set_error("task list overflow / row too large (err=%d)", herr); return OTTOHIP_ELIMIT; }
     if (dbg) {
-      fprintf(stderr, "[ottohip] level %d: sort %llu/%llu/%llu/%llu/%llu hash %llu split %llu\n", level, nlist[0],
-              nlist[1], nlist[2], nlist[3], nlist[4], nlist[N_SORT], nlist[N_SORT + 1]);
-      Task* lists[N_SORT + 2] = {TL.sort[0], TL.sort[1], TL.sort[2], TL.sort[3], TL.sort[4], TL.hash, TL.split};
+      fprintf(stderr, "[ottohip] level %d: sort %llu/%llu/%llu/%llu/%llu hash %llu split %llu lds %llu\n", level, nlist[0],
+              nlist[1], nlist[2], nlist[3], nlist[4], nlist[N_SORT], nlist[N_SORT + 1], nlist[N_SORT + 2]);
+      Task* lists[N_LISTS] = {TL.sort[0], TL.sort[1], TL.sort[2], TL.sort[3], TL.sort[4], TL.hash, TL.split, TL.lds};
       fprintf(stderr, "[ottohip] level %d words:", level);
-      for (int c = 0; c < N_SORT + 2; ++c) {
+      for (int c = 0; c < N_LISTS; ++c) {
         std::vector<Task> tv(nlist[c]);
         if (nlist[c]) (void)d2h(tv.data(), lists[c], nlist[c], s);
         unsigned long long sw = 0, mx = 0;
@@ -634,6 +655,15 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     OH_SORT(0, 1) OH_SORT(1, 2) OH_SORT(2, 4) OH_SORT(3, 8) OH_SORT(4, 16)
 #undef OH_SORT
     if (s2) OH_HIP(hipEventRecord(ctx->ev_join[level & 1], s2));
+    if (nlist[N_SORT + 2]) {  // LDS leaves (hot segments are appended to the split list)
+      const unsigned lg = (unsigned)std::min<uint64_t>(nlist[N_SORT + 2], (uint64_t)ctx->n_cu * 4);
+      if (FOon)
+        k_agg_lds<true><<<lg, LDS_T, 0, s>>>(TL.lds, (int64_t)nlist[N_SORT + 2], w0, w1, row_key, R, Lt, O, TL.split,
+                                             lcount + N_SORT + 1, TL.cap + split_extra, err, fo);
+      else
+        k_agg_lds<<<lg, LDS_T, 0, s>>>(TL.lds, (int64_t)nlist[N_SORT + 2], w0, w1, row_key, R, Lt, O, TL.split,
+                                       lcount + N_SORT + 1, TL.cap + split_extra, err, fo);
+    }
     if (nlist[N_SORT]) {  // tasks that overflow the LDS table are appended to the split list
       static const bool hprof = getenv("OTTOHIP_HASH_PROF") != nullptr && !hash_first;  // per-task profile (debugging aid)
       if (hprof) {
@@ -658,8 +688,9 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
         fprintf(stderr, "\n");
         fo.prof = nullptr;
       }
-      if ((rc = d2h(nlist, lcount, N_SORT + 2, s))) return rc;
     }
+    if (nlist[N_SORT] || nlist[N_SORT + 2])
+      if ((rc = d2h(nlist, lcount, N_LISTS, s))) return rc;
     const int64_t ns = (int64_t)nlist[N_SORT + 1];
     if (dbg) fprintf(stderr, "[ottohip] level %d: split after hash overflow %lld\n", level, (long long)ns);
     if (ns == 0) {

@@ -25,10 +25,12 @@ namespace ottohip {
 
 constexpr int EV_BLOCK = 256;     // events per wave block (sessions starting in it)
 constexpr int LCAP = 512;         // sessions up to LCAP events run from LDS
-constexpr int SPLIT_MEAN = 420;   // hashed split buckets average at most this many words (default)
+constexpr int SPLIT_MEAN = 420;   // hashed split buckets average at most this many words (register sorts only)
+constexpr int LDS_SPLIT_MEAN = 2560;  // the same with the LDS leaf (k_agg_lds takes buckets of <= 4096 words)
 __constant__ uint32_t c_split_mean = SPLIT_MEAN;  // OTTOHIP_SPLIT_MEAN overrides it (A/B switch, abi.hip)
 __constant__ uint32_t c_split_fuse = 1;  // one-chunk split tasks counted inside k_split_scatter (OTTOHIP_SPLIT_FUSE=0: off)
 __constant__ uint32_t c_hash_prio = 0;  // OTTOHIP_HASH_PRIO: wave priority of the LDS-hash leaves (A/B switch)
+__constant__ uint32_t c_lds_leaf = 0;   // rows / split buckets of (SORT_MAX, LDS_CAP] words go to k_agg_lds (abi.hip)
 constexpr uint32_t W_EMPTY = 0xFFFFFFFFu;
 constexpr int STAT_STRIPES = 256;            // copies of the per-rule statistics
 // u64 per copy: [rule * 4 + {rows, pairs, file_rows, file_rows_ge2}] (a symmetric rule's rows with
@@ -1401,6 +1403,181 @@ __device__ __forceinline__ uint32_t excl_at(const uint32_t (&x)[M], int m, uint3
   return m > 0 ? x[m - 1] : lane_prev_tot;
 }
 
+// The fold of one sorted task (k_agg_sort, k_agg_lds): v holds its <= 64*M words (W_EMPTY past the
+// end), unsorted; rows go to the slots [obegin, obegin + olen) of the table (the task's own word range),
+// the rest of that range is marked empty. stgk / stgb: this wave's staging rows (64*M + 64 each),
+// sacc: this wave's statistics accumulator, P / fh: the FO kernels' part tables and per-file rows.
+template <int M, bool FO>
+__device__ __forceinline__ void agg_fold(uint32_t (&v)[M], uint64_t obegin, uint32_t olen, uint32_t rk,
+                                         const RulesDev& sR, const Layout& L, const OutRows& O, const FileOpts& fo,
+                                         const PartLds* P, unsigned long long* fh, uint32_t* stgk, uint32_t* stgb,
+                                         unsigned long long* sacc) {
+  const uint32_t l = lane_id();
+  const int F = L.F, A = L.A;
+  wave_bitonic_sort<M>(v);
+  // neighbours across lanes; lane 0's predecessor and lane 63's successor are sentinels that differ
+  // from the element in every field (so no element needs an index test: words are < W_EMPTY, and the
+  // invalid tail is W_EMPTY, sorted last). All flags below are branch-free selects: the former
+  // short-circuit tests (e < len && (e == 0 || ...)) compiled to exec-mask branches per element.
+  const uint32_t pl0 = lane_prev(v[M - 1]), nl0 = lane_next(v[0]);
+  const uint32_t pl = l == 0u ? ~v[0] : pl0, nl = l == 63u ? W_EMPTY : nl0;
+  // part mode: parts of the elements and of the cross-lane neighbours (words of one key are in file
+  // order, and the part is non-decreasing in the file for a fixed key, so a part's words stay adjacent)
+  uint32_t pt[FO ? M : 1];
+  uint32_t ppl = 0, pnl = 0;
+  const bool pmode = FO && fo.parts;
+  if constexpr (FO) {
+    if (pmode) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) pt[m] = v[m] != W_EMPTY ? word_part(*P, v[m], rk & L.amask, L) : 0xFFu;
+      ppl = lane_prev(pt[M - 1]);
+      pnl = lane_next(pt[0]);
+    }
+  }
+  // (1) run flags from the neighbours (a w-run = one word = one (rule, aid_next, file)):
+  //     X = [w-run end] | [singleton w-run] << 11, summed by one scan (fields <= 1024);
+  //     k-run (rule, aid_next) starts and ends as bit masks over the lane's elements
+  uint32_t a[M], b[M], c[M];
+  uint32_t kst = 0, kend = 0;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const uint32_t prv = m > 0 ? v[m - 1] : pl, nxt = m < M - 1 ? v[m + 1] : nl;
+    const uint32_t valid = v[m] != W_EMPTY ? 1u : 0u;
+    const uint32_t ws = valid & (prv != v[m] ? 1u : 0u);
+    const uint32_t we = valid & (nxt != v[m] ? 1u : 0u);
+    c[m] = we | ((ws & we) << 11);
+    b[m] = c[m];
+    uint32_t kbs = (prv >> F) != (v[m] >> F) ? 1u : 0u, kbe = (nxt >> F) != (v[m] >> F) ? 1u : 0u;
+    if constexpr (FO) {
+      if (pmode) {  // a k-run is one (key, part)
+        const uint32_t pp = m > 0 ? pt[m - 1] : ppl, pn = m < M - 1 ? pt[m + 1] : pnl;
+        kbs |= pp != pt[m] ? 1u : 0u;
+        kbe |= pn != pt[m] ? 1u : 0u;
+      }
+    }
+    kst |= (valid & kbs) << m;
+    kend |= (valid & kbe) << m;
+  }
+  if constexpr (FO) {  // one per-file row per w-run end of the rule; a singleton w-run has count 1
+    if (fo.hist && (int)(rk >> A) == fo.type) {
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        if ((c[m] & 1u) && (v[m] >> (A + F)) == fo.q) {  // a symmetric rule's stored row (a, b), a < b, is
+          const unsigned long long mult =                // also the row (b, a) of the file's table
+              (fo.sym && ((v[m] >> F) & L.amask) != (rk & L.amask)) ? 2ull : 1ull;
+          atomicAdd(&fh[v[m] & ((1u << F) - 1u)], mult * ((c[m] >> 11) ? 1ull : (1ull | (1ull << 32))));
+        }
+    }
+  }
+  wave_scan_elems<M, false>(b);
+  // (2) at each k-run start: its exclusive X << 10 | position, carried to the k-run's end by one
+  //     max scan (strictly increasing over the starts)
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const uint32_t e = l * M + m;
+    a[m] = ((kst >> m) & 1u) ? (((b[m] - c[m]) << 10) | e) : 0u;
+  }
+  wave_scan_elems<M, true>(a);
+  // (3) at k-run ends: count = its words, S = its files with one word, nf1 = its files;
+  //     count_ge2 = count - S, nf2 = nf1 - S. b = count | count_ge2 << 16, c = nf1 | nf2 << 16
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const uint32_t e = l * M + m;
+    const uint32_t d = b[m] - (a[m] >> 10);
+    const uint32_t nf1 = d & 2047u, s1 = (d >> 11) & 2047u;
+    const uint32_t cnt = e + 1 - (a[m] & 1023u);
+    b[m] = cnt | ((cnt - s1) << 16);
+    c[m] = nf1 | ((nf1 - s1) << 16);
+  }
+  // (4) one output row per k-run end: (key2, count | count_ge2 << 16) staged in this wave's LDS
+  //     rows at its rank among the k-run ends (other elements write a per-lane dummy slot), then
+  //     written out linearly into the task's own word range (coalesced stores on a task-uniform base)
+  const int type = (int)(rk >> A);
+  const int32_t aid = (int32_t)(rk & ((1u << A) - 1u));
+  const uint32_t nmine = (uint32_t)__builtin_popcount(kend);
+  const uint32_t incl = wave_incl_scan(nmine);
+  const uint32_t nout = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  // the per-rule statistics come from the registers here (only key2 and the counts are staged)
+  const int nq = sR.n_of_type[type];
+  const int r0 = sR.rule_of_type[type][0], r1 = sR.rule_of_type[type][1];
+  // local rules 0 / 1: rows | nf1 << 16, pairs | nf2 << 16 (a symmetric rule's off-diagonal rows twice);
+  // sraw: stored rows | stored pairs << 16
+  uint32_t s0a = 0, s0b = 0, s1a = 0, s1b = 0, sraw = 0, q2 = 0;
+  const uint32_t sym0 = rule_sym(sR, r0) ? 1u : 0u, sym1 = (nq > 1 && rule_sym(sR, r1)) ? 1u : 0u;
+  {
+    uint32_t idx = incl - nmine;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const uint32_t ke = (kend >> m) & 1u;
+      const uint32_t k2 = v[m] >> F, q = k2 >> A, cnt = b[m] & 0xFFFFu, cc = c[m];
+      const uint32_t slot = ke ? idx : (uint32_t)(64 * M) + l;
+      uint32_t k2s = k2;
+      if constexpr (FO) {
+        if (pmode) k2s = k2 | (pt[m] << 24);  // the part rides above aid_next (< 2^24 in part mode)
+      }
+      stgk[slot] = k2s;
+      stgb[slot] = b[m];
+      idx += ke;
+      const uint32_t offd = (k2 & L.amask) != (uint32_t)aid ? 1u : 0u;
+      const uint32_t mult = 1u + (offd & (q == 0 ? sym0 : (q == 1 ? sym1 : 0u)));
+      const uint32_t ra = (1u | ((cc & 0xFFFFu) << 16)) * mult, rb = (cnt | (cc & 0xFFFF0000u)) * mult;
+      sraw += ke ? (1u | (cnt << 16)) : 0u;
+      s0a += (ke && q == 0) ? ra : 0u; s0b += (ke && q == 0) ? rb : 0u;
+      s1a += (ke && q == 1) ? ra : 0u; s1b += (ke && q == 1) ? rb : 0u;
+      q2 |= (ke && q >= 2) ? 1u : 0u;
+    }
+  }
+  if (__ballot(q2 != 0u)) {  // more than 2 rules of one type (not in the reference's five)
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const uint32_t k2 = v[m] >> F, q = k2 >> A;
+      if (((kend >> m) & 1u) && q >= 2) {
+        const uint32_t cnt = b[m] & 0xFFFFu, cc = c[m];
+        const uint32_t mult = (rule_sym(sR, sR.rule_of_type[type][q]) && (k2 & L.amask) != (uint32_t)aid) ? 2u : 1u;
+        unsigned long long* acc = sacc + sR.rule_of_type[type][q] * 4;
+        atomicAdd(acc + 0, (unsigned long long)mult); atomicAdd(acc + 1, (unsigned long long)cnt * mult);
+        atomicAdd(acc + 2, (unsigned long long)(cc & 0xFFFFu) * mult);
+        atomicAdd(acc + 3, (unsigned long long)(cc >> 16) * mult);
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const bool store = O.cap != 0;
+  uint8_t* o_rule = O.rule + obegin;
+  int32_t* o_aid = O.aid + obegin;
+  int32_t* o_next = O.aid_next + obegin;
+  uint32_t* o_cnt = O.count + obegin;
+  uint32_t* o_c2 = O.count_ge2 + obegin;
+  if (store)
+    for (uint32_t i = l; i < nout; i += 64) {
+      const uint32_t k2 = stgk[i], bb = stgb[i];
+      const uint32_t q = k2 >> A;
+      const int rule = pmode ? (int)(k2 >> 24) : (q == 0 ? r0 : (q == 1 ? r1 : sR.rule_of_type[type][q]));
+      const int32_t next = (int32_t)(k2 & L.amask);
+      o_rule[i] = (uint8_t)rule;
+      o_aid[i] = aid;
+      o_next[i] = next;
+      o_cnt[i] = bb & 0xFFFFu;
+      o_c2[i] = bb >> 16;
+    }
+  if (store)  // the rest of the task's word range holds no row (marked here, no table-wide fill)
+    for (uint32_t i = nout + l; i < olen; i += 64) o_rule[i] = 0xFF;
+  for (int q = 0; q < (nq < 2 ? nq : 2); ++q) {
+    const uint32_t sa = wave_sum(q == 0 ? s0a : s1a), sb = wave_sum(q == 0 ? s0b : s1b);
+    if (l == 0 && sa) {
+      unsigned long long* acc = sacc + (q == 0 ? r0 : r1) * 4;
+      acc[0] += sa & 0xFFFFu; acc[1] += sb & 0xFFFFu; acc[2] += sa >> 16; acc[3] += sb >> 16;
+    }
+  }
+  {
+    const uint32_t sr = wave_sum(sraw);
+    if (l == 0) { sacc[STAT_RAW] += sr & 0xFFFFu; sacc[STAT_RAW + 1] += sr >> 16; }
+  }
+  __builtin_amdgcn_wave_barrier();  // the staging rows are rewritten by the next task
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
 // One wave per task of <= 64*M words (rows and split buckets): bitonic sort in registers, then
 // run-length folding with prefix / max scans only (no LDS, no atomics on the data path).
 //   w-runs (equal words = one (rule, aid_next, file)): per-file count cf
@@ -1431,7 +1608,7 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
   __syncthreads();
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   int64_t ti = __builtin_amdgcn_readfirstlane((int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6));
-  const int F = L.F, A = L.A;
+  const int A = L.A;
   uint32_t v[M];
   Task T;
   uint32_t rk = 0, nd = 0;
@@ -1470,168 +1647,8 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
     const uint32_t len = T.len - nd;
     if (FO && nd && l == 0) atomicAdd(fo.dropped, (unsigned long long)nd);
     if (FO && fo.dbg && l == 0) { atomicAdd(fo.dbg + 2, (unsigned long long)nd); atomicAdd(fo.dbg + 3, (unsigned long long)len); }
-    wave_bitonic_sort<M>(v);
-    // neighbours across lanes; lane 0's predecessor and lane 63's successor are sentinels that differ
-    // from the element in every field (so no element needs an index test: words are < W_EMPTY, and the
-    // invalid tail is W_EMPTY, sorted last). All flags below are branch-free selects: the former
-    // short-circuit tests (e < len && (e == 0 || ...)) compiled to exec-mask branches per element.
-    const uint32_t pl0 = lane_prev(v[M - 1]), nl0 = lane_next(v[0]);
-    const uint32_t pl = l == 0u ? ~v[0] : pl0, nl = l == 63u ? W_EMPTY : nl0;
-    // part mode: parts of the elements and of the cross-lane neighbours (words of one key are in file
-    // order, and the part is non-decreasing in the file for a fixed key, so a part's words stay adjacent)
-    uint32_t pt[FO ? M : 1];
-    uint32_t ppl = 0, pnl = 0;
-    const bool pmode = FO && fo.parts;
-    if constexpr (FO) {
-      if (pmode) {
-#pragma unroll
-        for (int m = 0; m < M; ++m) pt[m] = v[m] != W_EMPTY ? word_part(sP[0], v[m], rk & L.amask, L) : 0xFFu;
-        ppl = lane_prev(pt[M - 1]);
-        pnl = lane_next(pt[0]);
-      }
-    }
-    // (1) run flags from the neighbours (a w-run = one word = one (rule, aid_next, file)):
-    //     X = [w-run end] | [singleton w-run] << 11, summed by one scan (fields <= 1024);
-    //     k-run (rule, aid_next) starts and ends as bit masks over the lane's elements
-    uint32_t a[M], b[M], c[M];
-    uint32_t kst = 0, kend = 0;
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const uint32_t prv = m > 0 ? v[m - 1] : pl, nxt = m < M - 1 ? v[m + 1] : nl;
-      const uint32_t valid = v[m] != W_EMPTY ? 1u : 0u;
-      const uint32_t ws = valid & (prv != v[m] ? 1u : 0u);
-      const uint32_t we = valid & (nxt != v[m] ? 1u : 0u);
-      c[m] = we | ((ws & we) << 11);
-      b[m] = c[m];
-      uint32_t kbs = (prv >> F) != (v[m] >> F) ? 1u : 0u, kbe = (nxt >> F) != (v[m] >> F) ? 1u : 0u;
-      if constexpr (FO) {
-        if (pmode) {  // a k-run is one (key, part)
-          const uint32_t pp = m > 0 ? pt[m - 1] : ppl, pn = m < M - 1 ? pt[m + 1] : pnl;
-          kbs |= pp != pt[m] ? 1u : 0u;
-          kbe |= pn != pt[m] ? 1u : 0u;
-        }
-      }
-      kst |= (valid & kbs) << m;
-      kend |= (valid & kbe) << m;
-    }
-    if constexpr (FO) {  // one per-file row per w-run end of the rule; a singleton w-run has count 1
-      if (fo.hist && (int)(rk >> A) == fo.type) {
-#pragma unroll
-        for (int m = 0; m < M; ++m)
-          if ((c[m] & 1u) && (v[m] >> (A + F)) == fo.q) {  // a symmetric rule's stored row (a, b), a < b, is
-            const unsigned long long mult =                // also the row (b, a) of the file's table
-                (fo.sym && ((v[m] >> F) & L.amask) != (rk & L.amask)) ? 2ull : 1ull;
-            atomicAdd(&fh[v[m] & ((1u << F) - 1u)], mult * ((c[m] >> 11) ? 1ull : (1ull | (1ull << 32))));
-          }
-      }
-    }
-    wave_scan_elems<M, false>(b);
-    // (2) at each k-run start: its exclusive X << 10 | position, carried to the k-run's end by one
-    //     max scan (strictly increasing over the starts)
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const uint32_t e = l * M + m;
-      a[m] = ((kst >> m) & 1u) ? (((b[m] - c[m]) << 10) | e) : 0u;
-    }
-    wave_scan_elems<M, true>(a);
-    // (3) at k-run ends: count = its words, S = its files with one word, nf1 = its files;
-    //     count_ge2 = count - S, nf2 = nf1 - S. b = count | count_ge2 << 16, c = nf1 | nf2 << 16
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const uint32_t e = l * M + m;
-      const uint32_t d = b[m] - (a[m] >> 10);
-      const uint32_t nf1 = d & 2047u, s1 = (d >> 11) & 2047u;
-      const uint32_t cnt = e + 1 - (a[m] & 1023u);
-      b[m] = cnt | ((cnt - s1) << 16);
-      c[m] = nf1 | ((nf1 - s1) << 16);
-    }
-    // (4) one output row per k-run end: (key2, count | count_ge2 << 16) staged in this wave's LDS
-    //     rows at its rank among the k-run ends (other elements write a per-lane dummy slot), then
-    //     written out linearly into the task's own word range (coalesced stores on a task-uniform base)
-    const int type = (int)(rk >> A);
-    const int32_t aid = (int32_t)(rk & ((1u << A) - 1u));
-    const uint32_t nmine = (uint32_t)__builtin_popcount(kend);
-    const uint32_t incl = wave_incl_scan(nmine);
-    const uint32_t nout = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    // the per-rule statistics come from the registers here (only key2 and the counts are staged)
-    const int nq = sR.n_of_type[type];
-    const int r0 = sR.rule_of_type[type][0], r1 = sR.rule_of_type[type][1];
-    // local rules 0 / 1: rows | nf1 << 16, pairs | nf2 << 16 (a symmetric rule's off-diagonal rows twice);
-    // sraw: stored rows | stored pairs << 16
-    uint32_t s0a = 0, s0b = 0, s1a = 0, s1b = 0, sraw = 0, q2 = 0;
-    const uint32_t sym0 = rule_sym(sR, r0) ? 1u : 0u, sym1 = (nq > 1 && rule_sym(sR, r1)) ? 1u : 0u;
-    {
-      uint32_t idx = incl - nmine;
-#pragma unroll
-      for (int m = 0; m < M; ++m) {
-        const uint32_t ke = (kend >> m) & 1u;
-        const uint32_t k2 = v[m] >> F, q = k2 >> A, cnt = b[m] & 0xFFFFu, cc = c[m];
-        const uint32_t slot = ke ? idx : (uint32_t)(64 * M) + l;
-        uint32_t k2s = k2;
-        if constexpr (FO) {
-          if (pmode) k2s = k2 | (pt[m] << 24);  // the part rides above aid_next (< 2^24 in part mode)
-        }
-        stg[wv][0][slot] = k2s;
-        stg[wv][1][slot] = b[m];
-        idx += ke;
-        const uint32_t offd = (k2 & L.amask) != (uint32_t)aid ? 1u : 0u;
-        const uint32_t mult = 1u + (offd & (q == 0 ? sym0 : (q == 1 ? sym1 : 0u)));
-        const uint32_t ra = (1u | ((cc & 0xFFFFu) << 16)) * mult, rb = (cnt | (cc & 0xFFFF0000u)) * mult;
-        sraw += ke ? (1u | (cnt << 16)) : 0u;
-        s0a += (ke && q == 0) ? ra : 0u; s0b += (ke && q == 0) ? rb : 0u;
-        s1a += (ke && q == 1) ? ra : 0u; s1b += (ke && q == 1) ? rb : 0u;
-        q2 |= (ke && q >= 2) ? 1u : 0u;
-      }
-    }
-    if (__ballot(q2 != 0u)) {  // more than 2 rules of one type (not in the reference's five)
-#pragma unroll
-      for (int m = 0; m < M; ++m) {
-        const uint32_t k2 = v[m] >> F, q = k2 >> A;
-        if (((kend >> m) & 1u) && q >= 2) {
-          const uint32_t cnt = b[m] & 0xFFFFu, cc = c[m];
-          const uint32_t mult = (rule_sym(sR, sR.rule_of_type[type][q]) && (k2 & L.amask) != (uint32_t)aid) ? 2u : 1u;
-          unsigned long long* acc = sacc[wv] + sR.rule_of_type[type][q] * 4;
-          atomicAdd(acc + 0, (unsigned long long)mult); atomicAdd(acc + 1, (unsigned long long)cnt * mult);
-          atomicAdd(acc + 2, (unsigned long long)(cc & 0xFFFFu) * mult);
-          atomicAdd(acc + 3, (unsigned long long)(cc >> 16) * mult);
-        }
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const bool store = O.cap != 0;
-    uint8_t* o_rule = O.rule + T.begin;
-    int32_t* o_aid = O.aid + T.begin;
-    int32_t* o_next = O.aid_next + T.begin;
-    uint32_t* o_cnt = O.count + T.begin;
-    uint32_t* o_c2 = O.count_ge2 + T.begin;
-    if (store)
-      for (uint32_t i = l; i < nout; i += 64) {
-        const uint32_t k2 = stg[wv][0][i], bb = stg[wv][1][i];
-        const uint32_t q = k2 >> A;
-        const int rule = pmode ? (int)(k2 >> 24) : (q == 0 ? r0 : (q == 1 ? r1 : sR.rule_of_type[type][q]));
-        const int32_t next = (int32_t)(k2 & L.amask);
-        o_rule[i] = (uint8_t)rule;
-        o_aid[i] = aid;
-        o_next[i] = next;
-        o_cnt[i] = bb & 0xFFFFu;
-        o_c2[i] = bb >> 16;
-      }
-    if (store)  // the rest of the task's word range holds no row (marked here, no table-wide fill)
-      for (uint32_t i = nout + l; i < T.len; i += 64) o_rule[i] = 0xFF;
-    for (int q = 0; q < (nq < 2 ? nq : 2); ++q) {
-      const uint32_t sa = wave_sum(q == 0 ? s0a : s1a), sb = wave_sum(q == 0 ? s0b : s1b);
-      if (l == 0 && sa) {
-        unsigned long long* acc = sacc[wv] + (q == 0 ? r0 : r1) * 4;
-        acc[0] += sa & 0xFFFFu; acc[1] += sb & 0xFFFFu; acc[2] += sa >> 16; acc[3] += sb >> 16;
-      }
-    }
-    {
-      const uint32_t sr = wave_sum(sraw);
-      if (l == 0) { sacc[wv][STAT_RAW] += sr & 0xFFFFu; sacc[wv][STAT_RAW + 1] += sr >> 16; }
-    }
-    __builtin_amdgcn_wave_barrier();  // the staging rows are rewritten by the next task
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    agg_fold<M, FO>(v, T.begin, T.len, rk, sR, L, O, fo, reinterpret_cast<const PartLds*>(sP), fh, stg[wv][0], stg[wv][1],
+                    sacc[wv]);
     T = Tn;
     rk = rkn;
     nd = ndn;
@@ -1703,11 +1720,13 @@ __device__ __forceinline__ uint32_t hash_insert_batch(unsigned long long* slots,
 
 constexpr int N_SORT = 5;  // register-sort classes: 64, 128, 256, 512, 1024 words
 constexpr int SORT_MAX = 64 << (N_SORT - 1);
+constexpr int LDS_CAP = 4096;  // largest task of the LDS leaf (k_agg_lds)
 struct TaskLists {
   Task* sort[N_SORT];     // register sort by size class
   Task* hash;             // workgroup LDS hash (heavy buckets)
   Task* split;            // MSD split
-  unsigned long long* n;  // [N_SORT + 2]: sort classes..., hash, split
+  Task* lds;              // LDS leaf (k_agg_lds)
+  unsigned long long* n;  // [N_SORT + 3]: sort classes..., hash, split, lds
   uint64_t cap;           // capacity of every list
 };
 
@@ -1928,16 +1947,18 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
 // class of a task: [0, N_SORT) register sort of <= 64 << c words; N_SORT workgroup hash
 // (a split bucket that stayed far above its expected size: skewed towards a few hot keys,
 // hashed optimistically and sent back to a split on overflow); N_SORT + 1 split (rows, and
-// buckets that are large only because the parent needed more than one split's digits).
+// buckets that are large only because the parent needed more than one split's digits);
+// N_SORT + 2 the LDS leaf (rows and ordinary buckets of up to LDS_CAP words, when c_lds_leaf).
 constexpr int SPLIT_LEVELS = 4;
 __device__ __forceinline__ int task_class(uint64_t len, uint32_t level, bool split) {
   for (int c = 0; c < N_SORT; ++c)
     if (len <= (uint64_t)(64 << c)) return c;
+  if (split && c_lds_leaf && len <= (uint64_t)LDS_CAP) return N_SORT + 2;
   return (split && level < (uint32_t)SPLIT_LEVELS) ? N_SORT + 1 : N_SORT;
 }
 // Block-aggregated push: every thread of the (256-thread) block must call it once. Per list:
 // LDS counter per block, then one device atomic per list per block.
-constexpr int N_LISTS = N_SORT + 2;
+constexpr int N_LISTS = N_SORT + 3;
 __device__ __forceinline__ void push_task_block(const TaskLists& TL, bool valid, uint64_t begin, uint64_t len,
                                                 uint32_t row, uint32_t rem, uint32_t buf, bool split, int* err) {
   __shared__ uint32_t bcnt[N_LISTS];
@@ -1963,7 +1984,7 @@ __device__ __forceinline__ void push_task_block(const TaskLists& TL, bool valid,
   if (c >= 0) {
     const unsigned long long k = bbase[c] + my;
     Task t; t.begin = begin; t.len = (uint32_t)len; t.row = row; t.rem = rem; t.buf = buf;
-    Task* list = c < N_SORT ? TL.sort[c] : (c == N_SORT ? TL.hash : TL.split);
+    Task* list = c < N_SORT ? TL.sort[c] : (c == N_SORT ? TL.hash : (c == N_SORT + 1 ? TL.split : TL.lds));
     if (k < TL.cap) list[k] = t; else atomicOr(err, 4);
   }
 }
@@ -2212,6 +2233,166 @@ __global__ void k_split_classify(const Task* __restrict__ tasks, int64_t n, cons
   // split's 8 bits); one far above it holds a few hot keys and goes to the hash path
   const bool again = c != 0 && (uint64_t)c <= 4 * ((uint64_t)T.len / split_ndig(T) + 1);
   push_task_block(TL, c != 0, b, c, T.row, T.rem + 1u, T.buf ^ 1u, again, err);
+}
+
+// ---- LDS leaf: one workgroup per task of (SORT_MAX, LDS_CAP] words (rows, and split buckets of an ordinary
+// size). The task is read from HBM once and partitioned in LDS by a second hash of (rule, aid_next) into
+// sub-buckets of ~LDS_SUBW words (one LDS atomic per word gives its rank); the sub-buckets starting in one
+// LDS_SEG-word window form a segment (a sub-bucket above LDS_BIG words is a segment of its own), so a
+// segment holds whole keys and <= 512 words, and each wave sorts and folds segments straight from LDS
+// (agg_fold<4 | 8>). A segment above 512 words (hot keys) is written back to its place in the word buffer
+// and pushed to this level's split list. Against a split of the bucket in HBM followed by register sorts
+// of the sub-buckets, the words are read once instead of three times and written not at all, and the split
+// that feeds these tasks needs ~6x fewer digits (longer scatter runs).
+constexpr int LDS_T = 256;
+constexpr int LDS_WPT = LDS_CAP / LDS_T;           // words per thread
+constexpr int LDS_SUBW = 32;                       // mean words per sub-bucket
+constexpr int LDS_NSUB = LDS_CAP / LDS_SUBW;       // <= 128 sub-buckets
+constexpr int LDS_SEG = 384;
+constexpr int LDS_BIG = 128;
+static_assert(LDS_SEG + LDS_BIG <= 512, "a grouped segment fits the 512-word fold");
+static_assert(LDS_NSUB <= 128, "sub-bucket scan over waves 0 and 1");
+template <bool FO = false>
+__global__ __launch_bounds__(LDS_T) void k_agg_lds(const Task* __restrict__ tasks, int64_t n_tasks,
+                                                   uint32_t* __restrict__ w0, uint32_t* __restrict__ w1,
+                                                   const uint32_t* __restrict__ row_key, RulesDev R, Layout L,
+                                                   OutRows O, Task* __restrict__ overflow,
+                                                   unsigned long long* __restrict__ n_overflow, uint64_t ov_cap,
+                                                   int* __restrict__ err, FileOpts fo) {
+  __shared__ uint32_t words[LDS_CAP];
+  __shared__ uint32_t sh[LDS_NSUB], ss[LDS_NSUB + 1], seg[LDS_NSUB + 1];
+  __shared__ uint32_t wtot[LDS_T / 64], nseg;
+  __shared__ unsigned long long sacc[LDS_T / 64][STAT_STRIDE];
+  __shared__ RulesDev sR;
+  __shared__ uint32_t stg[LDS_T / 64][2][64 * 8 + 64];  // per wave: staged output rows (agg_fold)
+  __shared__ unsigned long long fh[FO ? FO_MAXF : 1];
+  __shared__ std::conditional_t<FO, PartLds, char> sP[1];
+  const int tid = threadIdx.x, wv = tid >> 6;
+  const uint32_t l = lane_id();
+  if (tid == 0) sR = R;
+  for (int i = (int)l; i < STAT_STRIDE; i += 64) sacc[wv][i] = 0;
+  if constexpr (FO) {
+    for (uint32_t i = tid; i < fo.nf; i += LDS_T) fh[i] = 0;
+    part_lds_load(fo, sP[0]);
+  }
+  __syncthreads();
+  const PartLds* P = reinterpret_cast<const PartLds*>(sP);
+  for (int64_t ti = blockIdx.x; ti < n_tasks; ti += gridDim.x) {
+    const Task T = tasks[ti];
+    uint32_t* W = (T.buf ? w1 : w0) + T.begin;
+    const uint32_t rk = row_key[T.row];
+    const uint32_t len = T.len;  // (SORT_MAX, LDS_CAP] by classification
+    const uint32_t nsub = (len + LDS_SUBW - 1) / LDS_SUBW;
+    uint32_t wr[LDS_WPT];
+#pragma unroll
+    for (int j = 0; j < LDS_WPT; ++j) {
+      const uint32_t i = (uint32_t)(j * LDS_T + tid);
+      wr[j] = i < len ? W[i] : W_EMPTY;
+    }
+    uint32_t ndrop = 0;
+    if constexpr (FO) {  // the cut words are dropped before the partition (branch-free, as in k_agg_sort)
+      if ((int)(rk >> L.A) == fo.type) {
+        const int32_t ad = (int32_t)(rk & L.amask);
+#pragma unroll
+        for (int j = 0; j < LDS_WPT; ++j) {
+          const bool dr = fo_drop(fo, wr[j], ad, L);
+          ndrop += dr ? 1u : 0u;
+          wr[j] = dr ? W_EMPTY : wr[j];
+        }
+      }
+    }
+    if (tid < LDS_NSUB) sh[tid] = 0;
+    __syncthreads();
+    uint32_t dr[LDS_WPT];
+#pragma unroll
+    for (int j = 0; j < LDS_WPT; ++j) {  // sub-bucket << 16 | the word's rank in it
+      const uint32_t d = split_digit(wr[j], L.F, T.rem + 64u, nsub);
+      dr[j] = (d << 16) | (wr[j] != W_EMPTY ? atomicAdd(&sh[d], 1u) : 0u);
+    }
+    __syncthreads();
+    {  // sub-bucket starts ss[0..LDS_NSUB] (exclusive scan over threads 0..127; ss[d >= nsub] = kept words)
+      const uint32_t c = tid < (int)nsub ? sh[tid] : 0u;
+      const uint32_t incl = wave_incl_scan(c);
+      if (l == 63u) wtot[wv] = incl;
+      __syncthreads();
+      const uint32_t pre = wv == 1 ? wtot[0] : 0u;
+      if (tid < LDS_NSUB) ss[tid] = pre + incl - c;
+      if (tid == LDS_NSUB - 1) ss[LDS_NSUB] = pre + incl;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < LDS_WPT; ++j)
+      if (wr[j] != W_EMPTY) words[ss[dr[j] >> 16] + (dr[j] & 0xFFFFu)] = wr[j];
+    // segments: sub-bucket d starts one when its key differs from that of d - 1 (key: the LDS_SEG window
+    // of its start, or its own id above LDS_BIG words)
+    bool st = false;
+    uint64_t sm = 0;
+    if (tid < LDS_NSUB) {
+      const uint32_t d = (uint32_t)tid;
+      auto key = [&](uint32_t e) {
+        return ss[e + 1] - ss[e] > (uint32_t)LDS_BIG ? (0x80000000u | e) : ss[e] / (uint32_t)LDS_SEG;
+      };
+      st = d < nsub && (d == 0 || key(d) != key(d - 1));
+      sm = __ballot(st);
+      if (l == 0u) wtot[wv] = (uint32_t)__popcll(sm);  // wtot's scan values were read before the last barrier
+    }
+    __syncthreads();
+    if (tid < LDS_NSUB) {
+      const uint32_t n0 = wtot[0], n1 = wtot[1];
+      if (st) seg[(wv == 1 ? n0 : 0u) + mbcnt(sm)] = (uint32_t)tid;
+      if (tid == 0) { nseg = n0 + n1; seg[n0 + n1] = nsub; }
+    }
+    __syncthreads();
+    const uint32_t ns = nseg;
+    for (uint32_t j = (uint32_t)wv; j < ns; j += LDS_T / 64) {
+      const uint32_t b = __builtin_amdgcn_readfirstlane(ss[seg[j]]), e = __builtin_amdgcn_readfirstlane(ss[seg[j + 1]]);
+      const uint32_t n = e - b;
+      if (n > 512u) {  // hot keys: back to the word buffer, split at this level (then hashed)
+        for (uint32_t i = l; i < n; i += 64) W[b + i] = words[b + i];
+        if (l == 0u) {
+          const unsigned long long k = atomicAdd(n_overflow, 1ull);
+          Task t2;
+          t2.begin = T.begin + b; t2.len = n; t2.row = T.row; t2.rem = T.rem; t2.buf = T.buf;
+          if (k < ov_cap) overflow[k] = t2; else atomicOr(err, 4);
+        }
+      } else if (n > 256u) {
+        uint32_t v[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          const uint32_t i = (uint32_t)(m * 64) + l;
+          v[m] = i < n ? words[b + i] : W_EMPTY;
+        }
+        agg_fold<8, FO>(v, T.begin + b, n, rk, sR, L, O, fo, P, fh, stg[wv][0], stg[wv][1], sacc[wv]);
+      } else if (n > 0u) {
+        uint32_t v[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const uint32_t i = (uint32_t)(m * 64) + l;
+          v[m] = i < n ? words[b + i] : W_EMPTY;
+        }
+        agg_fold<4, FO>(v, T.begin + b, n, rk, sR, L, O, fo, P, fh, stg[wv][0], stg[wv][1], sacc[wv]);
+      }
+    }
+    const uint32_t kept = ss[LDS_NSUB];  // the words cut by the file options leave [kept, len) without rows
+    if (O.cap)
+      for (uint32_t i = kept + (uint32_t)tid; i < len; i += LDS_T) O.rule[T.begin + i] = 0xFF;
+    if constexpr (FO) {
+      const uint32_t nd = wave_sum(ndrop);
+      if (nd && l == 0u) atomicAdd(fo.dropped, (unsigned long long)nd);
+    }
+    __syncthreads();  // words / sh / ss / seg are rewritten by the next task
+  }
+  const uint32_t gwave = blockIdx.x * (LDS_T / 64) + wv;
+  unsigned long long* stats = O.stats + (size_t)(gwave & (STAT_STRIPES - 1)) * STAT_STRIDE;
+  for (int i = (int)l; i < STAT_STRIDE; i += 64)
+    if (sacc[wv][i]) atomicAdd(&stats[i], sacc[wv][i]);
+  if constexpr (FO) {
+    if (fo.hist) {
+      __syncthreads();
+      for (uint32_t i = tid; i < fo.nf; i += LDS_T)
+        if (fh[i]) atomicAdd(&fo.hist[i], fh[i]);
+    }
+  }
 }
 
 // ------------------------------------------------------------------ per-rule compaction

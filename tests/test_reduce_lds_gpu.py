@@ -1,0 +1,68 @@
+"""The reduce's LDS leaf (k_agg_lds, OTTOHIP_LDS_LEAF=1): rows and split buckets of 1-4 k words read once,
+partitioned in LDS by a second hash of (rule, aid_next) and folded segment by segment, the splits feeding it
+cut to ~2.5 k-word buckets. The bit-exact checks of tests/test_covis_gpu.py with the leaf on (golden 3-file
+digests, random slices, hot rows through the split / hash / overflow paths, key cuts and per-file rows,
+part mode, A6 branch (2)), plus a row whose hot key overflows a segment (written back and re-split)."""
+import numpy as np
+import pytest
+
+import covis as oracle
+import otto_recommender_amd.synth as synth
+import test_covis_gpu as base
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def lds_leaf(monkeypatch):
+    monkeypatch.setenv("OTTOHIP_LDS_LEAF", "1")
+
+
+def test_lds_three_files_digests(gpu):
+    base.test_three_files_digests(gpu)
+
+
+def test_lds_random_slices(gpu):
+    base.test_random_slices_vs_oracle(gpu)
+
+
+def test_lds_heavy_rows(gpu):
+    base.test_heavy_rows_split_and_hash_paths(gpu)
+
+
+def test_lds_hot_row_overflow(gpu):
+    base.test_hot_row_overflow_resplit(gpu)
+
+
+@pytest.mark.parametrize("case", ["split_hash", "overflow"])
+def test_lds_file_cuts_hot_rows(gpu, case):
+    base.test_file_cuts_hot_rows(gpu, case)
+
+
+def test_lds_part_branch(gpu):
+    base.test_concat_files_w_stats_part_branch(
+        gpu, dict(max_rows_groupby=300_000, optim_rows=250_000, max_pairs=200_000, click_filter_rows=1_000_000))
+
+
+def test_lds_segment_overflow(gpu, monkeypatch, capfd):
+    """Row (click, 7) holds ~2.7 k words (an LDS task at level 0) of which 600 are one key (7, 8) of one
+    file: its sub-bucket is a segment above 512 words, written back to the word buffer and split again
+    (then hashed). Row (click, 8) (~4.8 k words) takes a split first. Exact against the oracle; the
+    debug listing shows LDS tasks."""
+    monkeypatch.setenv("OTTOHIP_DEBUG", "1")
+    rng = np.random.default_rng(21)
+    rows = []
+    for s in range(300):
+        aid = np.concatenate([[7, 8, 8], rng.integers(1000, 1_800_000, 7)])
+        ts = np.sort(rng.integers(0, 3600, len(aid)))
+        rows.append(np.stack([np.full(len(aid), s), aid, ts, np.zeros(len(aid), np.int64)], 1))
+    a = np.concatenate(rows)
+    ev = synth.events_from_columns(a[:, 0], a[:, 1], a[:, 2], a[:, 3])
+    base._assert_single_file(ev, names=["click_to_click"])
+    err = capfd.readouterr().err
+    lds = [int(line.split(" lds ")[1].split()[0]) for line in err.splitlines() if " lds " in line and "level 0:" in line]
+    assert lds and lds[0] >= 1, err[-2000:]
+    ref = oracle.count_co_events_file(ev.session_offsets, ev.aid, ev.ts, ev.type,
+                                      {"click_to_click": oracle.REFERENCE_RULES["click_to_click"]})["click_to_click"]
+    hot = (ref[0] == 7) & (ref[1] == 8)
+    assert int(ref[2][hot][0]) == 600
