@@ -1953,7 +1953,8 @@ constexpr int SPLIT_LEVELS = 4;
 __device__ __forceinline__ int task_class(uint64_t len, uint32_t level, bool split) {
   for (int c = 0; c < N_SORT; ++c)
     if (len <= (uint64_t)(64 << c)) return c;
-  if (split && c_lds_leaf && len <= (uint64_t)LDS_CAP) return N_SORT + 2;
+  // (the LDS leaf only below SPLIT_LEVELS: its hot-key overflow re-enters the split list, see k_agg_lds)
+  if (split && c_lds_leaf && len <= (uint64_t)LDS_CAP && level < (uint32_t)SPLIT_LEVELS) return N_SORT + 2;
   return (split && level < (uint32_t)SPLIT_LEVELS) ? N_SORT + 1 : N_SORT;
 }
 // Block-aggregated push: every thread of the (256-thread) block must call it once. Per list:
@@ -2352,7 +2353,10 @@ __global__ __launch_bounds__(LDS_T) void k_agg_lds(const Task* __restrict__ task
         if (l == 0u) {
           const unsigned long long k = atomicAdd(n_overflow, 1ull);
           Task t2;
-          t2.begin = T.begin + b; t2.len = n; t2.row = T.row; t2.rem = T.rem; t2.buf = T.buf;
+          // split at the last level that may still split: its sub-buckets (rem SPLIT_LEVELS) are hashed or
+          // register-sorted, never sent to an LDS leaf again (a hot key would cycle leaf -> split -> leaf)
+          t2.begin = T.begin + b; t2.len = n; t2.row = T.row; t2.buf = T.buf;
+          t2.rem = T.rem < (uint32_t)(SPLIT_LEVELS - 1) ? (uint32_t)(SPLIT_LEVELS - 1) : T.rem;
           if (k < ov_cap) overflow[k] = t2; else atomicOr(err, 4);
         }
       } else if (n > 256u) {

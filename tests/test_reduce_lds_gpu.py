@@ -45,7 +45,7 @@ def test_lds_part_branch(gpu):
 
 
 def test_lds_segment_overflow(gpu, monkeypatch, capfd):
-    """Row (click, 7) holds ~2.7 k words (an LDS task at level 0) of which 600 are one key (7, 8) of one
+    """Row (click, 7) holds ~2.7 k words (an LDS task at level 0) of which ~600 are one key (7, 8) of one
     file: its sub-bucket is a segment above 512 words, written back to the word buffer and split again
     (then hashed). Row (click, 8) (~4.8 k words) takes a split first. Exact against the oracle; the
     debug listing shows LDS tasks."""
@@ -65,4 +65,4 @@ def test_lds_segment_overflow(gpu, monkeypatch, capfd):
     ref = oracle.count_co_events_file(ev.session_offsets, ev.aid, ev.ts, ev.type,
                                       {"click_to_click": oracle.REFERENCE_RULES["click_to_click"]})["click_to_click"]
     hot = (ref[0] == 7) & (ref[1] == 8)
-    assert int(ref[2][hot][0]) == 600
+    assert int(ref[2][hot][0]) > 512  # one key above a segment (~600: twin events at equal ts dedup)
