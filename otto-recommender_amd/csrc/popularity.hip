@@ -1378,6 +1378,72 @@ __global__ __launch_bounds__(256) void k_sim(const int64_t* __restrict__ cand_of
   }
 }
 
+// R7, coalesced: 16 lanes per candidate, each lane holding 4 + 4 of the session's (<= 128, dim % 4 == 0)
+// dimensions and reading the item row as two float4 (one 400-B row = 25 float4 in one load instruction per
+// group), 4 candidates per wave per round, two rounds in flight; dot / |v|^2 / |q - v|^2 by 4 xor-shuffle
+// steps. k_sim above (one lane per candidate, dimension by dimension) read each row 4 B at a time, 64 rows
+// per load instruction.
+constexpr int SIM_U = 2;  // rounds of 4 candidates in flight per wave
+__global__ __launch_bounds__(256) void k_sim16(const int64_t* __restrict__ cand_off, int64_t S,
+                                               const int32_t* __restrict__ cnext, const float* __restrict__ sess_emb,
+                                               const uint8_t* __restrict__ sess_has, const int32_t* __restrict__ row_of_aid,
+                                               int32_t n_aid_map, const float* __restrict__ emb, int dim,
+                                               float* __restrict__ cos_out, float* __restrict__ eucl_out) {
+  const int l = threadIdx.x & 63, g = l >> 4, j = l & 15;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int d0 = 4 * j, d1 = 64 + 4 * j;
+  const bool h0 = d0 < dim, h1 = d1 < dim;
+  for (int64_t s = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); s < S; s += nw) {
+    const float* q = sess_emb + s * dim;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 q0 = h0 ? *reinterpret_cast<const float4*>(q + d0) : z4;
+    const float4 q1 = h1 ? *reinterpret_cast<const float4*>(q + d1) : z4;
+    float nq = q0.x * q0.x + q0.y * q0.y + q0.z * q0.z + q0.w * q0.w + q1.x * q1.x + q1.y * q1.y + q1.z * q1.z +
+               q1.w * q1.w;
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) nq += __shfl_xor(nq, m);
+    const float sq = sqrtf(nq);
+    const bool hs = sess_has == nullptr || sess_has[s];
+    const int64_t b = cand_off[s], e = cand_off[s + 1];
+    for (int64_t i0 = b; i0 < e; i0 += 4 * SIM_U) {
+      int32_t r[SIM_U];
+      float4 v0[SIM_U], v1[SIM_U];
+#pragma unroll
+      for (int u = 0; u < SIM_U; ++u) {
+        const int64_t i = i0 + 4 * u + g;
+        const int32_t a = i < e ? cnext[i] : -1;
+        r[u] = (hs && a >= 0 && a < n_aid_map) ? row_of_aid[a] : -1;
+        const float* v = emb + (int64_t)(r[u] < 0 ? 0 : r[u]) * dim;
+        v0[u] = (r[u] >= 0 && h0) ? *reinterpret_cast<const float4*>(v + d0) : z4;
+        v1[u] = (r[u] >= 0 && h1) ? *reinterpret_cast<const float4*>(v + d1) : z4;
+      }
+#pragma unroll
+      for (int u = 0; u < SIM_U; ++u) {
+        const float4 a0 = v0[u], a1 = v1[u];
+        float dot = q0.x * a0.x + q0.y * a0.y + q0.z * a0.z + q0.w * a0.w + q1.x * a1.x + q1.y * a1.y + q1.z * a1.z +
+                    q1.w * a1.w;
+        float nv = a0.x * a0.x + a0.y * a0.y + a0.z * a0.z + a0.w * a0.w + a1.x * a1.x + a1.y * a1.y + a1.z * a1.z +
+                   a1.w * a1.w;
+        float x, d2 = 0.f;
+        x = q0.x - a0.x; d2 += x * x; x = q0.y - a0.y; d2 += x * x; x = q0.z - a0.z; d2 += x * x; x = q0.w - a0.w; d2 += x * x;
+        x = q1.x - a1.x; d2 += x * x; x = q1.y - a1.y; d2 += x * x; x = q1.z - a1.z; d2 += x * x; x = q1.w - a1.w; d2 += x * x;
+#pragma unroll
+        for (int m = 1; m < 16; m <<= 1) {
+          dot += __shfl_xor(dot, m);
+          nv += __shfl_xor(nv, m);
+          d2 += __shfl_xor(d2, m);
+        }
+        const int64_t i = i0 + 4 * u + g;
+        if (j == 0 && i < e) {
+          const bool hit = r[u] >= 0;  // inner joins miss: 0 / -1
+          cos_out[i] = hit ? dot / (sq * sqrtf(nv)) : 0.f;
+          eucl_out[i] = hit ? sqrtf(d2) : -1.f;
+        }
+      }
+    }
+  }
+}
+
 
 // ---------------------------------------------------------------- KMeans init seeds (host)
 // sklearn 1.2 KMeans(init='random') draws the initial centres of run r as
@@ -2021,8 +2087,14 @@ int ottohip_session_item_similarity(ottohip_ctx* ctx, const int64_t* cand_off, i
   hipStream_t s = S(stream);
   OH_HIP(hipSetDevice(ctx->device));
   int ph = ctx->begin("r7_sim", s, 0);
-  k_sim<<<(unsigned)ceil_div(n_sessions, 4), 256, 0, s>>>(cand_off, n_sessions, aid_next, sess_emb, sess_has,
-                                                          row_of_aid, n_aid_map, emb, dim, cos_out, eucl_out);
+  const bool vec = dim <= 128 && dim % 4 == 0 && (reinterpret_cast<uintptr_t>(emb) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(sess_emb) & 15) == 0;
+  if (vec)
+    k_sim16<<<(unsigned)std::min<int64_t>(ceil_div(n_sessions, 4), (int64_t)ctx->n_cu * 16), 256, 0, s>>>(
+        cand_off, n_sessions, aid_next, sess_emb, sess_has, row_of_aid, n_aid_map, emb, dim, cos_out, eucl_out);
+  else
+    k_sim<<<(unsigned)ceil_div(n_sessions, 4), 256, 0, s>>>(cand_off, n_sessions, aid_next, sess_emb, sess_has,
+                                                            row_of_aid, n_aid_map, emb, dim, cos_out, eucl_out);
   OH_HIP(hipGetLastError());
   ctx->end(ph, s);
   return 0;

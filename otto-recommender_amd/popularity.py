@@ -162,10 +162,11 @@ class KMeans:
         best = None
         inr, chg, shift = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
         st6 = (ctypes.c_double * 6)()
-        # two runs in lockstep over one read of X per Lloyd step (ottohip_kmeans_lloyd_steps_pair) on one
-        # GPU; OTTOHIP_KM_PAIR=0 runs them one at a time (A/B switch)
+        # OTTOHIP_KM_PAIR=1: two runs in lockstep over one read of X per Lloyd step
+        # (ottohip_kmeans_lloyd_steps_pair). Off by default: the lockstep steps carry no distance bounds and
+        # measured slower than one bounded run at a time (config 5 C2 2.36 s vs 1.31 s, same box)
         pair_ok = (group is None and 32 < k <= 64 and dim <= 112 and dim % 4 == 0
-                   and os.environ.get("OTTOHIP_KM_PAIR", "1") != "0")
+                   and os.environ.get("OTTOHIP_KM_PAIR", "0") == "1")
         pending = None  # the second run of a pair, finished in lockstep with the first
         for run in range(self.n_init):
             if pending is not None:

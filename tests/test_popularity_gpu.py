@@ -214,15 +214,16 @@ def test_popularity_ranks_exact(gpu):
     np.testing.assert_array_equal(g1["aid"].to_numpy(), r1["aid"].to_numpy())
 
 
-def test_session_item_similarity(gpu):
+@pytest.mark.parametrize("dim", [100, 128, 64, 30])  # 16-lane float4 kernel; 30: the one-lane kernel
+def test_session_item_similarity(gpu, dim):
     from otto_recommender_amd import popularity as gp
     rng = np.random.default_rng(4)
     words = np.arange(0, 5000, 2, dtype=np.int32)
-    emb = rng.normal(size=(len(words), 100)).astype(np.float32)
+    emb = rng.normal(size=(len(words), dim)).astype(np.float32)
     S = 300
     off = np.concatenate([[0], np.cumsum(rng.integers(0, 40, S))]).astype(np.int64)
     nxt = rng.integers(0, 5000, off[-1]).astype(np.int32)
-    se = rng.normal(size=(S, 100)).astype(np.float32)
+    se = rng.normal(size=(S, dim)).astype(np.float32)
     has = (rng.random(S) < 0.9).astype(np.uint8)
     cos, eu = (x.cpu().numpy() for x in gp.session_item_similarity(off, nxt, se, words, emb, has))
     sidx = np.repeat(np.arange(S), np.diff(off))
