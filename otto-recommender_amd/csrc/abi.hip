@@ -418,8 +418,10 @@ static int covis_emit_words(ottohip_ctx* ctx, const Front& F, const ottohip_even
   int* eerr;
   OH_TRY(ctx->ws.get("emit_err", 4, &eerr));
   OH_HIP(hipMemsetAsync(eerr, 0, sizeof(int), s));
+  // per-type task lists in pass 3 (OTTOHIP_EMIT_TASKS=0: every (rule, next type) of the wave in turn; read per call)
+  const bool tasks = !(getenv("OTTOHIP_EMIT_TASKS") && !strcmp(getenv("OTTOHIP_EMIT_TASKS"), "0"));
   if (F.NB > 0)
-    (guard ? k_emit<true> : k_emit<false>)<<<(unsigned)F.NB, 64, 0, s>>>(F.off, F.first, F.NB, F.evp, F.R, F.Lt, F.fb, ev->n_files, F.fid, F.cnt,
+    (guard ? (tasks ? k_emit<true, true> : k_emit<true, false>) : (tasks ? k_emit<false, true> : k_emit<false, false>))<<<(unsigned)F.NB, 64, 0, s>>>(F.off, F.first, F.NB, F.evp, F.R, F.Lt, F.fb, ev->n_files, F.fid, F.cnt,
                                          EvOff{F.poff, F.poff32}, w0, eerr, dbg);
   if (F.nl > 0)
     k_emit_long<<<F.nl, 64, 0, s>>>(F.off, F.long_list, F.d_loff, F.lscr, F.lpscr, F.evp, F.R, F.Lt, F.fb,

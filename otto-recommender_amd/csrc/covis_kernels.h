@@ -1004,7 +1004,32 @@ __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, i
   }
 }
 
-template <bool GUARD>  // GUARD (OTTOHIP_DEBUG): bounds checks of the record arrays (err bit 8)
+// Per event type, the (rule, next type) windows an event of that type writes, as pass 3's task list: entry
+// q | tt << 4 | sym << 6, the non-symmetric rules first (a symmetric record's written length is only known to
+// S2's count, so it goes last in the event's run)
+struct EmitTasks {
+  uint8_t e[3][3 * MAX_RULES];
+  uint8_t n[4];
+};
+__device__ inline void emit_tasks_build(const RulesDev& R, EmitTasks& T) {
+  for (int t = 0; t < 3; ++t) {
+    int n = 0;
+    for (int pass = 0; pass < 2; ++pass)
+      for (int q = 0; q < R.n_of_type[t]; ++q) {
+        const int r = R.rule_of_type[t][q];
+        if (rule_sym(R, r) != (pass == 1)) continue;
+        for (int tt = 0; tt < 3; ++tt)
+          if ((R.mask[r] >> tt) & 1u) T.e[t][n++] = (uint8_t)(q | (tt << 4) | (pass << 6));
+      }
+    T.n[t] = (uint8_t)n;
+  }
+  T.n[3] = 0;
+}
+
+// GUARD (OTTOHIP_DEBUG): bounds checks of the record arrays (err bit 8). TASKS: pass 3 iterates the per-type
+// task lists (lanes of different types search their own lists together); else (OTTOHIP_EMIT_TASKS=0) every
+// (rule, next type) of the wave's types in turn
+template <bool GUARD, bool TASKS>
 __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restrict__ off, const int64_t* __restrict__ first,
                                              int64_t NB, const uint64_t* __restrict__ ev, RulesDev R, Layout L,
                                              const int64_t* __restrict__ fb, int nf, const uint32_t* __restrict__ fid,
@@ -1012,8 +1037,10 @@ __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restri
                                              uint32_t* __restrict__ words, int* __restrict__ err, int dbg) {
   __shared__ EmitLds S;
   __shared__ RulesDev sR;
+  __shared__ EmitTasks sT;
   const int l = threadIdx.x;
   if (l == 0) sR = R;
+  if (TASKS && l == 0) emit_tasks_build(R, sT);
   const int64_t g = blockIdx.x;
   if (g >= NB) return;
   const int64_t s0 = first[g], s1 = first[g + 1];
@@ -1028,6 +1055,7 @@ __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restri
   int64_t next_b = fcur + 1 < nf ? fb[fcur + 1] : INT64_MAX;
   uint32_t fid_cur = fid[fcur];
   __syncthreads();
+  const int maxtask = TASKS ? max((int)sT.n[0], max((int)sT.n[1], (int)sT.n[2])) : 0;
 
   int64_t b = s0;
   while (b < s1) {
@@ -1145,25 +1173,22 @@ __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restri
         while (rlo > lb && S.tev[rlo - 1] == v) --rlo;
         while (rhi < ub && S.tev[rhi] == v) ++rhi;
       }
-      const int nq = valid ? sR.n_of_type[t] : 0;
       uint32_t eo = 0;
       bool has_sym = false;
-      // the event's symmetric-rule record comes last: its written length is only known to S2's count
-      bool lane_sym = false;
-      for (int q = 0; q < nq; ++q) lane_sym |= rule_sym(sR, sR.rule_of_type[t][q]);
-      const int nqq = __ballot(lane_sym) ? 2 * maxq : maxq;
+      if constexpr (TASKS) {
+        // task kk of the lane's event: the (rule, next type) list window of the kk-th entry of its type's task
+        // table (symmetric rules last): lanes of different types search their own lists in one iteration
+        const int ntk = valid ? (int)sT.n[t] : 0;
 #pragma unroll 1
-      for (int qq = 0; qq < nqq; ++qq) {
-        const int q = qq % maxq, pass = qq / maxq;
-        const int r = q < nq ? sR.rule_of_type[t][q] : 0;
-        const bool sym = q < nq && rule_sym(sR, r);
-        const uint32_t msk = (q < nq && sym == (pass == 1)) ? sR.mask[r] : 0u;
-        const int32_t lo = sR.lo[r], hi = sR.hi[r];
-        has_sym |= msk != 0u && sym;
-#pragma unroll 1
-        for (int tt = 0; tt < 3; ++tt) {
-          const bool act = (msk >> tt) & 1u;
-          if (!__ballot(act)) continue;
+        for (int kk = 0; kk < maxtask; ++kk) {
+          const bool act = kk < ntk;
+          if (!__ballot(act)) break;
+          const uint32_t te = act ? (uint32_t)sT.e[t][kk] : 0u;
+          const int q = (int)(te & 15u), tt = (int)((te >> 4) & 3u);
+          const bool sym = act && ((te >> 6) & 1u);
+          const int r = act ? sR.rule_of_type[t][q] : 0;
+          const int32_t lo = sR.lo[r], hi = sR.hi[r];
+          has_sym |= sym;
           uint32_t len = 0, jb = 0, xlo = EB_NONE, xlen = 0;
           if (act) {
             const int a = S.sb[tt][k], e = S.sb[tt + 1][k];
@@ -1195,6 +1220,57 @@ __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restri
           if (!sym) eo += len;
           nrec += nn;
           tot += __shfl(incl, 63);
+        }
+      } else {
+        const int nq = valid ? sR.n_of_type[t] : 0;
+        // the event's symmetric-rule record comes last: its written length is only known to S2's count
+        bool lane_sym = false;
+        for (int q = 0; q < nq; ++q) lane_sym |= rule_sym(sR, sR.rule_of_type[t][q]);
+        const int nqq = __ballot(lane_sym) ? 2 * maxq : maxq;
+#pragma unroll 1
+        for (int qq = 0; qq < nqq; ++qq) {
+          const int q = qq % maxq, pass = qq / maxq;
+          const int r = q < nq ? sR.rule_of_type[t][q] : 0;
+          const bool sym = q < nq && rule_sym(sR, r);
+          const uint32_t msk = (q < nq && sym == (pass == 1)) ? sR.mask[r] : 0u;
+          const int32_t lo = sR.lo[r], hi = sR.hi[r];
+          has_sym |= msk != 0u && sym;
+#pragma unroll 1
+          for (int tt = 0; tt < 3; ++tt) {
+            const bool act = (msk >> tt) & 1u;
+            if (!__ballot(act)) continue;
+            uint32_t len = 0, jb = 0, xlo = EB_NONE, xlen = 0;
+            if (act) {
+              const int a = S.sb[tt][k], e = S.sb[tt + 1][k];
+              jb = (uint32_t)lds_lower_ts(S.tev, a, e, tsi + lo);
+              const uint32_t je = (uint32_t)lds_upper_ts(S.tev, (int)jb, e, tsi + hi);
+              len = je - jb;
+              if (tt == t && lo <= 0 && hi >= 0) { xlo = rlo; xlen = rhi - rlo; len -= xlen; }
+            }
+            const uint64_t m = __ballot(len > 0);
+            const int nn = (int)__popcll(m);
+            if (nn == 0) continue;
+            if (nrec + nn > EB_RCAP) {
+              __builtin_amdgcn_wave_barrier();
+              __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+              emit_flush<GUARD>(S, nrec, tot, L.F, words, dbg, rid, err);
+              __builtin_amdgcn_wave_barrier();
+              __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+              nrec = 0; tot = 0;
+            }
+            const uint32_t incl = wave_incl_scan(len);
+            if (GUARD && nrec + nn > EB_RCAP) atomicOr(err, 8);  // the record arrays would overflow
+            if (len > 0 && !(GUARD && nrec + (int)mbcnt(m) >= EB_RCAP)) {
+              const int ri = nrec + (int)mbcnt(m);
+              S.u.r.rpre[ri] = tot + incl - len;
+              S.u.r.rec[ri] = make_uint4(tot + incl - len, jb | (xlo << 10) | (xlen << 21), ((uint32_t)q << shiftR) | file,
+                                     sym ? (uint32_t)ev_aid(v) : 0u);
+              S.u.r.rout[ri] = eout + eo;
+            }
+            if (!sym) eo += len;
+            nrec += nn;
+            tot += __shfl(incl, 63);
+          }
         }
       }
       if (valid && (has_sym ? eo > ecnt : eo != ecnt)) atomicOr(err, 4);
@@ -2413,6 +2489,55 @@ __device__ __forceinline__ bool blk_keep(const uint8_t* __restrict__ rule, const
   if (rule[i] != (uint8_t)r) return false;
   return thr == 0 || (use_ge2 ? c2[i] : c[i]) >= thr;
 }
+// Slot scans read 4 consecutive slots per thread (slot arrays are 16-B aligned and i % 4 == 0): the rule
+// bytes as one u32, a u32 column as one uint4 (one-byte / one-word loads per slot ran at a third of HBM
+// bandwidth). Past n: rule 0xFF (no row). A block's FIN_B slots are FIN_PER / 4 rounds of 4 * FIN_T.
+__device__ __forceinline__ uint32_t ld_rule4(const uint8_t* __restrict__ rule, int64_t i, int64_t n) {
+  if (i + 4 <= n) return *reinterpret_cast<const uint32_t*>(rule + i);
+  uint32_t r = 0xFFFFFFFFu;
+  for (int j = 0; j < 4; ++j)
+    if (i + j < n) r = (r & ~(0xFFu << (8 * j))) | ((uint32_t)rule[i + j] << (8 * j));
+  return r;
+}
+__device__ __forceinline__ uint4 ld_u4(const uint32_t* __restrict__ p, int64_t i, int64_t n) {
+  if (i + 4 <= n) return *reinterpret_cast<const uint4*>(p + i);
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if (i < n) v.x = p[i];
+  if (i + 1 < n) v.y = p[i + 1];
+  if (i + 2 < n) v.z = p[i + 2];
+  return v;
+}
+__device__ __forceinline__ uint32_t u4_at(const uint4& v, int j) { return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w)); }
+// bit j: byte j of r4 equals r
+__device__ __forceinline__ uint32_t rule4_match(uint32_t r4, uint32_t r) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) m |= (((r4 >> (8 * j)) & 0xFFu) == r ? 1u : 0u) << j;
+  return m;
+}
+// kept slots of the 4 at i (bit mask) and their mirrored rows (bit mask), per blk_keep
+__device__ __forceinline__ void blk_keep4(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
+                                          const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
+                                          const uint32_t* __restrict__ c2, int64_t i, int64_t n, int r, int use_ge2,
+                                          uint32_t thr, int sym, uint32_t& keep, uint32_t& mir, uint4& A, uint4& B,
+                                          uint4& V, uint4& G, bool want_g) {
+  keep = rule4_match(ld_rule4(rule, i, n), (uint32_t)r);
+  mir = 0;
+  if (!keep) return;
+  V = ld_u4(use_ge2 ? c2 : c, i, n);
+  if (want_g) G = use_ge2 ? V : ld_u4(c2, i, n);
+  if (thr) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) keep &= ~((u4_at(V, j) < thr ? 1u : 0u) << j);
+  }
+  if (!keep) return;
+  A = ld_u4(reinterpret_cast<const uint32_t*>(a), i, n);
+  B = ld_u4(reinterpret_cast<const uint32_t*>(b), i, n);
+  if (sym) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) mir |= (((keep >> j) & 1u) && u4_at(A, j) != u4_at(B, j) ? 1u : 0u) << j;
+  }
+}
 __global__ __launch_bounds__(FIN_T) void k_blk_count(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
                                                      const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
                                                      const uint32_t* __restrict__ c2, int64_t n, int r, int use_ge2,
@@ -2420,10 +2545,14 @@ __global__ __launch_bounds__(FIN_T) void k_blk_count(const uint8_t* __restrict__
   __shared__ uint32_t wt[FIN_T / 64];
   const int64_t base = (int64_t)blockIdx.x * FIN_B;
   uint32_t k = 0;
-#pragma unroll 4
-  for (int q = 0; q < FIN_PER; ++q) {
-    const int64_t i = base + q * FIN_T + threadIdx.x;
-    if (i < n && blk_keep(rule, c, c2, i, r, use_ge2, thr)) k += (sym && a[i] != b[i]) ? 2u : 1u;
+#pragma unroll
+  for (int q = 0; q < FIN_PER / 4; ++q) {
+    const int64_t i = base + ((int64_t)q * FIN_T + threadIdx.x) * 4;
+    if (i >= n) break;
+    uint32_t keep, mir;
+    uint4 A, B, V, G;
+    blk_keep4(rule, a, b, c, c2, i, n, r, use_ge2, thr, sym, keep, mir, A, B, V, G, false);
+    k += (uint32_t)__popc(keep) + (uint32_t)__popc(mir);
   }
   k = wave_sum(k);
   if ((threadIdx.x & 63) == 0) wt[threadIdx.x >> 6] = k;
@@ -2441,33 +2570,40 @@ __global__ __launch_bounds__(FIN_T) void k_blk_compact(const uint8_t* __restrict
   const int w = threadIdx.x >> 6;
   const int64_t base = (int64_t)blockIdx.x * FIN_B;
   uint64_t run = boff[blockIdx.x];
-  for (int q = 0; q < FIN_PER; ++q) {
-    const int64_t i = base + q * FIN_T + threadIdx.x;
-    const bool keep = i < n && blk_keep(rule, c, c2, i, r, use_ge2, thr);
-    const uint32_t ai = keep ? (uint32_t)a[i] : 0u, bi = keep ? (uint32_t)b[i] : 0u;
-    const bool mir = keep && sym && ai != bi;
-    const uint64_t bal = __ballot(keep), bm = __ballot(mir);
-    if ((threadIdx.x & 63) == 0) wt[w] = (uint32_t)(__popcll(bal) + __popcll(bm));
+  for (int q = 0; q < FIN_PER / 4; ++q) {
+    const int64_t i = base + ((int64_t)q * FIN_T + threadIdx.x) * 4;
+    uint32_t keep = 0, mir = 0;
+    uint4 A, B, V, G;
+    if (i < n) blk_keep4(rule, a, b, c, c2, i, n, r, use_ge2, thr, sym, keep, mir, A, B, V, G, o3 != nullptr);
+    const uint32_t kc = (uint32_t)__popc(keep) + (uint32_t)__popc(mir);
+    const uint32_t incl = wave_incl_scan(kc);
+    if ((threadIdx.x & 63) == 63) wt[w] = incl;
     __syncthreads();
     uint32_t pre = 0, tot = 0;
 #pragma unroll
     for (int k = 0; k < FIN_T / 64; ++k) { pre += k < w ? wt[k] : 0u; tot += wt[k]; }
     if (keep) {
-      const uint64_t p = run + pre + mbcnt(bal) + mbcnt(bm);
-      const uint32_t cv = use_ge2 ? c2[i] : c[i], gv = o3 ? c2[i] : 0u;
-      if (o0) o0[p] = ai;
-      if (o1) o1[p] = bi;
-      if (o2) o2[p] = cv;
-      if (o3) o3[p] = gv;
-      if (mir) {
-        if (o0) o0[p + 1] = bi;
-        if (o1) o1[p + 1] = ai;
-        if (o2) o2[p + 1] = cv;
-        if (o3) o3[p + 1] = gv;
+      uint64_t p = run + pre + incl - kc;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (!((keep >> j) & 1u)) continue;
+        const uint32_t ai = u4_at(A, j), bi = u4_at(B, j), cv = u4_at(V, j), gv = o3 ? u4_at(G, j) : 0u;
+        if (o0) o0[p] = ai;
+        if (o1) o1[p] = bi;
+        if (o2) o2[p] = cv;
+        if (o3) o3[p] = gv;
+        ++p;
+        if ((mir >> j) & 1u) {
+          if (o0) o0[p] = bi;
+          if (o1) o1[p] = ai;
+          if (o2) o2[p] = cv;
+          if (o3) o3[p] = gv;
+          ++p;
+        }
       }
     }
     run += tot;
-    __syncthreads();  // wt is rewritten by the next chunk
+    __syncthreads();  // wt is rewritten by the next round
   }
 }
 
@@ -2478,9 +2614,24 @@ __global__ __launch_bounds__(256) void k_rule_hist(const uint8_t* __restrict__ r
   __shared__ unsigned long long hr[256], hp[256];
   hr[threadIdx.x] = 0; hp[threadIdx.x] = 0;
   __syncthreads();
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t r = rule[i];
-    if (r != 0xFFu) { atomicAdd(&hr[r], 1ull); atomicAdd(&hp[r], (unsigned long long)count[i]); }
+  // 4 consecutive slots per thread; equal rule bytes among them (the common case: one row's slots) take one
+  // pair of LDS atomics
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += (int64_t)gridDim.x * blockDim.x * 4) {
+    const uint32_t r4 = ld_rule4(rule, i, n);
+    if (r4 == 0xFFFFFFFFu) continue;
+    const uint4 c4 = ld_u4(count, i, n);
+    uint32_t cur = 0xFFu, nr = 0;
+    unsigned long long np = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t r = (r4 >> (8 * j)) & 0xFFu;
+      if (r != cur) {
+        if (cur != 0xFFu) { atomicAdd(&hr[cur], (unsigned long long)nr); atomicAdd(&hp[cur], np); }
+        cur = r; nr = 0; np = 0;
+      }
+      if (r != 0xFFu) { ++nr; np += u4_at(c4, j); }
+    }
+    if (cur != 0xFFu) { atomicAdd(&hr[cur], (unsigned long long)nr); atomicAdd(&hp[cur], np); }
   }
   __syncthreads();
   if (hr[threadIdx.x]) { atomicAdd(&rows[threadIdx.x], hr[threadIdx.x]); atomicAdd(&pairs[threadIdx.x], hp[threadIdx.x]); }
@@ -2507,13 +2658,17 @@ __global__ __launch_bounds__(256) void k_ph_hist(const uint8_t* __restrict__ rul
   __shared__ uint32_t hs[PH_MAXP][256];
   for (int i = threadIdx.x; i < PH_MAXP * 256; i += 256) (&hs[0][0])[i] = 0;
   __syncthreads();
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t p = rule[i];
-    if (p >= (uint32_t)n_parts) continue;
-    const uint32_t v = ph_val(c, c2, i, use_ge2);
-    if (v < thr) continue;
-    if (v < 256u) atomicAdd(&hs[p][v], 1u);
-    else atomicAdd(&hist[(uint64_t)p * PH_VBINS + (v < PH_VBINS ? v : PH_VBINS - 1)], 1ull);
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += (int64_t)gridDim.x * blockDim.x * 4) {
+    const uint32_t r4 = ld_rule4(rule, i, n);
+    if (r4 == 0xFFFFFFFFu) continue;
+    const uint4 v4 = ld_u4(use_ge2 ? c2 : c, i, n);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t p = (r4 >> (8 * j)) & 0xFFu, v = u4_at(v4, j);
+      if (p >= (uint32_t)n_parts || v < thr) continue;
+      if (v < 256u) atomicAdd(&hs[p][v], 1u);
+      else atomicAdd(&hist[(uint64_t)p * PH_VBINS + (v < PH_VBINS ? v : PH_VBINS - 1)], 1ull);
+    }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < n_parts * 256; i += 256) {
@@ -2521,17 +2676,46 @@ __global__ __launch_bounds__(256) void k_ph_hist(const uint8_t* __restrict__ rul
     if (x) atomicAdd(&hist[(uint64_t)(i >> 8) * PH_VBINS + (i & 255)], (unsigned long long)x);
   }
 }
-// tie histograms of stage `st` (1: aid of the v == c* rows, 2: aid_next of the v == c*, aid == a* rows)
+// tie histograms of stage `st` (1: aid of the v == c* rows, 2: aid_next of the v == c*, aid == a* rows). One
+// atomic per run of equal (part, key) among a wave's 64 consecutive slots (slots are in aid order, so the
+// tie rows of one part mostly share an aid): per part present in the wave, the run heads add their run length.
 __global__ void k_ph_tie_hist(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a, const int32_t* __restrict__ b,
                               const uint32_t* __restrict__ c, const uint32_t* __restrict__ c2, int64_t n, int n_parts,
                               int use_ge2, PartCut pc, int st, int64_t n_items, uint32_t* __restrict__ h) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t p = rule[i];
-    if (p >= (uint32_t)n_parts || pc.stage[p] != (uint32_t)st) continue;
-    if (ph_val(c, c2, i, use_ge2) != pc.cstar[p]) continue;
-    const uint32_t ai = (uint32_t)a[i];
-    if (st == 1) atomicAdd(&h[(uint64_t)p * n_items + ai], 1u);
-    else if (ai == pc.astar[p]) atomicAdd(&h[(uint64_t)p * n_items + (uint32_t)b[i]], 1u);
+  const int l = (int)lane_id();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~(int64_t)63; i0 < n; i0 += stride) {
+    const int64_t i = i0 + l;
+    uint32_t p = 0xFFFFFFFFu, key = 0;
+    bool tie = false;
+    if (i < n) {
+      p = rule[i];
+      if (p < (uint32_t)n_parts && pc.stage[p] == (uint32_t)st && ph_val(c, c2, i, use_ge2) == pc.cstar[p]) {
+        const uint32_t ai = (uint32_t)a[i];
+        if (st == 1) { tie = true; key = ai; }
+        else if (ai == pc.astar[p]) { tie = true; key = (uint32_t)b[i]; }
+      }
+    }
+    uint64_t pend = __ballot(tie);
+    while (pend) {
+      const int f = __ffsll((long long)pend) - 1;
+      const uint32_t pf = (uint32_t)__shfl((int)p, f);
+      const uint64_t mp = __ballot(tie && p == pf);
+      pend &= ~mp;
+      const bool in = (mp >> l) & 1ull;
+      const uint64_t below = mp & ((1ull << l) - 1ull);
+      const int prv = below ? 63 - __clzll((long long)below) : l;
+      const uint32_t kprev = (uint32_t)__shfl((int)key, prv);
+      const bool head = in && (!below || kprev != key);
+      const uint64_t hm = __ballot(head);
+      if (head) {
+        const uint64_t above = hm & ~((2ull << l) - 1ull);
+        const int nh = above ? __ffsll((long long)above) - 1 : 64;
+        const uint64_t upto = nh == 64 ? ~0ull : ((1ull << nh) - 1ull);
+        const uint32_t cnt = (uint32_t)__popcll(mp & upto & ~((1ull << l) - 1ull));
+        atomicAdd(&h[(uint64_t)pf * n_items + key], cnt);
+      }
+    }
   }
 }
 // smallest index j with incl[j] >= need (incl = inclusive prefix of one part's histogram)
@@ -2542,18 +2726,36 @@ __global__ void k_ph_find(const uint64_t* __restrict__ excl, const uint32_t* __r
   const uint64_t lo = excl[j], hi = lo + h[j];
   if (h[j] && lo < need && need <= hi) { out[0] = (uint32_t)j; out[1] = (uint32_t)(need - lo); }
 }
-__device__ __forceinline__ bool ph_keep(const uint8_t* rule, const int32_t* a, const int32_t* b, const uint32_t* c,
-                                        const uint32_t* c2, int64_t i, int n_parts, int use_ge2, uint32_t thr,
-                                        const PartCut& pc) {
-  const uint32_t p = rule[i];
-  if (p >= (uint32_t)n_parts) return false;
-  const uint32_t v = ph_val(c, c2, i, use_ge2);
-  if (v < thr) return false;
-  const uint32_t cs = pc.cstar[p];
-  if (v != cs) return v > cs;
-  if (pc.astar[p] == 0xFFFFFFFFu) return true;
-  const uint32_t ai = (uint32_t)a[i];
-  return ai < pc.astar[p] || (ai == pc.astar[p] && (uint32_t)b[i] <= pc.nstar[p]);
+// kept slots (bit mask) of the 4 at i; A / B / V loaded for the kept ones
+__device__ __forceinline__ uint32_t ph_keep4(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
+                                             const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
+                                             const uint32_t* __restrict__ c2, int64_t i, int64_t n, int n_parts,
+                                             int use_ge2, uint32_t thr, const PartCut& pc, bool want_ab, uint4& A,
+                                             uint4& B, uint4& V) {
+  const uint32_t r4 = ld_rule4(rule, i, n);
+  if (r4 == 0xFFFFFFFFu) return 0u;
+  V = ld_u4(use_ge2 ? c2 : c, i, n);
+  uint32_t keep = 0, tie = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t p = (r4 >> (8 * j)) & 0xFFu, v = u4_at(V, j);
+    if (p >= (uint32_t)n_parts || v < thr) continue;
+    const uint32_t cs = pc.cstar[p];
+    if (v != cs) keep |= (v > cs ? 1u : 0u) << j;
+    else if (pc.astar[p] == 0xFFFFFFFFu) keep |= 1u << j;
+    else tie |= 1u << j;
+  }
+  if (tie || (want_ab && keep)) {
+    A = ld_u4(reinterpret_cast<const uint32_t*>(a), i, n);
+    B = ld_u4(reinterpret_cast<const uint32_t*>(b), i, n);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (!((tie >> j) & 1u)) continue;
+    const uint32_t p = (r4 >> (8 * j)) & 0xFFu, ai = u4_at(A, j);
+    keep |= (ai < pc.astar[p] || (ai == pc.astar[p] && u4_at(B, j) <= pc.nstar[p]) ? 1u : 0u) << j;
+  }
+  return keep;
 }
 __global__ __launch_bounds__(FIN_T) void k_ph_count(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
                                                     const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
@@ -2562,16 +2764,19 @@ __global__ __launch_bounds__(FIN_T) void k_ph_count(const uint8_t* __restrict__ 
   __shared__ uint32_t wt[FIN_T / 64];
   const int64_t base = (int64_t)blockIdx.x * FIN_B;
   uint32_t k = 0;
-  for (int q = 0; q < FIN_PER; ++q) {
-    const int64_t i = base + q * FIN_T + threadIdx.x;
-    k += (i < n && ph_keep(rule, a, b, c, c2, i, n_parts, use_ge2, thr, pc)) ? 1u : 0u;
+#pragma unroll
+  for (int q = 0; q < FIN_PER / 4; ++q) {
+    const int64_t i = base + ((int64_t)q * FIN_T + threadIdx.x) * 4;
+    if (i >= n) break;
+    uint4 A, B, V;
+    k += (uint32_t)__popc(ph_keep4(rule, a, b, c, c2, i, n, n_parts, use_ge2, thr, pc, false, A, B, V));
   }
   k = wave_sum(k);
   if ((threadIdx.x & 63) == 0) wt[threadIdx.x >> 6] = k;
   __syncthreads();
   if (threadIdx.x == 0) bcnt[blockIdx.x] = wt[0] + wt[1] + wt[2] + wt[3];
 }
-// kept rows -> records {aid, aid_next, v, 0} (rule 0) at block offsets boff
+// kept rows -> records {aid, aid_next, v, 0} (rule 0) at block offsets boff, in slot order
 __global__ __launch_bounds__(FIN_T) void k_ph_compact(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
                                                       const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
                                                       const uint32_t* __restrict__ c2, int64_t n, int n_parts,
@@ -2581,16 +2786,21 @@ __global__ __launch_bounds__(FIN_T) void k_ph_compact(const uint8_t* __restrict_
   const int w = threadIdx.x >> 6;
   const int64_t base = (int64_t)blockIdx.x * FIN_B;
   uint64_t run = boff[blockIdx.x];
-  for (int q = 0; q < FIN_PER; ++q) {
-    const int64_t i = base + q * FIN_T + threadIdx.x;
-    const bool keep = i < n && ph_keep(rule, a, b, c, c2, i, n_parts, use_ge2, thr, pc);
-    const uint64_t bal = __ballot(keep);
-    if ((threadIdx.x & 63) == 0) wt[w] = (uint32_t)__popcll(bal);
+  for (int q = 0; q < FIN_PER / 4; ++q) {
+    const int64_t i = base + ((int64_t)q * FIN_T + threadIdx.x) * 4;
+    uint4 A, B, V;
+    const uint32_t keep = i < n ? ph_keep4(rule, a, b, c, c2, i, n, n_parts, use_ge2, thr, pc, true, A, B, V) : 0u;
+    const uint32_t kc = (uint32_t)__popc(keep);
+    const uint32_t incl = wave_incl_scan(kc);
+    if ((threadIdx.x & 63) == 63) wt[w] = incl;
     __syncthreads();
     uint32_t pre = 0, tot = 0;
 #pragma unroll
     for (int k = 0; k < FIN_T / 64; ++k) { pre += k < w ? wt[k] : 0u; tot += wt[k]; }
-    if (keep) out[run + pre + mbcnt(bal)] = make_uint4((uint32_t)a[i], (uint32_t)b[i], ph_val(c, c2, i, use_ge2), 0u);
+    uint64_t p = run + pre + incl - kc;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if ((keep >> j) & 1u) out[p++] = make_uint4(u4_at(A, j), u4_at(B, j), u4_at(V, j), 0u);
     run += tot;
     __syncthreads();
   }
