@@ -348,6 +348,14 @@ int ottohip_kmeans_lloyd_steps(ottohip_ctx* ctx, const float* X, int64_t n, int 
 int ottohip_kmeans_lloyd_steps_pair(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* const* centroids,
                                     int k, int32_t* const* labels, int64_t* const* sums, int64_t* const* counts,
                                     const int* max_steps, double tol, double* out, void* stream);
+/* lloyd_steps for n_runs (1..4) independent runs in lockstep (the n_init runs of :152-159, 4 at a time):
+ * one read of X per step scores all of them; a decided row whose label changes is applied to its run's
+ * fixed-point sums by a move list. Arrays as in lloyd_steps_pair with n_runs entries; out (HOST
+ * double[6 * n_runs]). Each run's labels, centres, stop step and reason equal lloyd_steps on that run
+ * alone (no distance bounds in lockstep). OTTOHIP_ELIMIT outside 32 < k <= 64, dim <= 112. */
+int ottohip_kmeans_lloyd_steps_multi(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* const* centroids,
+                                     int k, int32_t* const* labels, int64_t* const* sums, int64_t* const* counts,
+                                     const int* max_steps, int n_runs, double tol, double* out, void* stream);
 /* The E-step of lloyd_steps is a split-precision pass (x = hi + lo and c = hi + lo in bf16, three bf16
  * MFMA products, a rigorous error bound) that decides every row whose two best scores are separated
  * beyond the bound, plus the exact f32 kernel on the remaining near ties: labels, sums and stop

@@ -122,6 +122,9 @@ SIGNATURES = {
     "ottohip_kmeans_lloyd_steps_pair": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP, ctypes.c_int, _VP, _VP,
                                                        _VP, _VP, ctypes.c_double, ctypes.POINTER(ctypes.c_double),
                                                        _VP]),
+    "ottohip_kmeans_lloyd_steps_multi": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP, ctypes.c_int, _VP, _VP,
+                                                        _VP, _VP, ctypes.c_int, ctypes.c_double,
+                                                        ctypes.POINTER(ctypes.c_double), _VP]),
     "ottohip_kmeans_farthest": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP, _VP, ctypes.c_int, _VP, _VP, _VP]),
     "ottohip_kmeans_relocate": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int, ctypes.c_int, _VP, _VP, ctypes.c_int, _VP]),
     "ottohip_kmeans_inertia": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP, _VP, ctypes.POINTER(ctypes.c_double),

@@ -965,6 +965,7 @@ struct EmitLds {
 template <bool GUARD>
 __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, int F, uint32_t* __restrict__ words,
                                            int dbg, uint32_t& rid, int* __restrict__ err) {
+  if (dbg & 2) return;  // profiling ablation: records are built, never expanded
   const uint32_t l = lane_id();
   const uint32_t sa = (int)l < nrec ? S.u.r.rpre[l] : 0xFFFFFFFFu;
   const uint32_t sb = (int)l + 64 < nrec ? S.u.r.rpre[l + 64] : 0xFFFFFFFFu;
@@ -2676,46 +2677,48 @@ __global__ __launch_bounds__(256) void k_ph_hist(const uint8_t* __restrict__ rul
     if (x) atomicAdd(&hist[(uint64_t)(i >> 8) * PH_VBINS + (i & 255)], (unsigned long long)x);
   }
 }
-// tie histograms of stage `st` (1: aid of the v == c* rows, 2: aid_next of the v == c*, aid == a* rows). One
-// atomic per run of equal (part, key) among a wave's 64 consecutive slots (slots are in aid order, so the
-// tie rows of one part mostly share an aid): per part present in the wave, the run heads add their run length.
+// tie histograms of stage `st` (1: aid of the v == c* rows, 2: aid_next of the v == c*, aid == a* rows). Four
+// consecutive slots per thread (vector loads: one-byte loads per slot left the kernel address-bound); equal
+// (part, key) among a thread's slots (one row's slots are in aid order) take one atomic.
 __global__ void k_ph_tie_hist(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a, const int32_t* __restrict__ b,
                               const uint32_t* __restrict__ c, const uint32_t* __restrict__ c2, int64_t n, int n_parts,
-                              int use_ge2, PartCut pc, int st, int64_t n_items, uint32_t* __restrict__ h) {
-  const int l = (int)lane_id();
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~(int64_t)63; i0 < n; i0 += stride) {
-    const int64_t i = i0 + l;
-    uint32_t p = 0xFFFFFFFFu, key = 0;
-    bool tie = false;
-    if (i < n) {
-      p = rule[i];
-      if (p < (uint32_t)n_parts && pc.stage[p] == (uint32_t)st && ph_val(c, c2, i, use_ge2) == pc.cstar[p]) {
-        const uint32_t ai = (uint32_t)a[i];
-        if (st == 1) { tie = true; key = ai; }
-        else if (ai == pc.astar[p]) { tie = true; key = (uint32_t)b[i]; }
-      }
+                              int use_ge2, PartCut pc_arg, int st, int64_t n_items, uint32_t* __restrict__ h) {
+  // the cut tables in LDS: indexing the kernel-argument copy by a lane's part went through scratch memory
+  __shared__ PartCut pc;
+  if (threadIdx.x == 0) pc = pc_arg;
+  __syncthreads();
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += (int64_t)gridDim.x * blockDim.x * 4) {
+    const uint32_t r4 = ld_rule4(rule, i, n);
+    if (r4 == 0xFFFFFFFFu) continue;
+    const uint4 v4 = ld_u4(use_ge2 ? c2 : c, i, n);
+    uint32_t tie = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t p = (r4 >> (8 * j)) & 0xFFu;
+      tie |= (p < (uint32_t)n_parts && pc.stage[p] == (uint32_t)st && u4_at(v4, j) == pc.cstar[p] ? 1u : 0u) << j;
     }
-    uint64_t pend = __ballot(tie);
-    while (pend) {
-      const int f = __ffsll((long long)pend) - 1;
-      const uint32_t pf = (uint32_t)__shfl((int)p, f);
-      const uint64_t mp = __ballot(tie && p == pf);
-      pend &= ~mp;
-      const bool in = (mp >> l) & 1ull;
-      const uint64_t below = mp & ((1ull << l) - 1ull);
-      const int prv = below ? 63 - __clzll((long long)below) : l;
-      const uint32_t kprev = (uint32_t)__shfl((int)key, prv);
-      const bool head = in && (!below || kprev != key);
-      const uint64_t hm = __ballot(head);
-      if (head) {
-        const uint64_t above = hm & ~((2ull << l) - 1ull);
-        const int nh = above ? __ffsll((long long)above) - 1 : 64;
-        const uint64_t upto = nh == 64 ? ~0ull : ((1ull << nh) - 1ull);
-        const uint32_t cnt = (uint32_t)__popcll(mp & upto & ~((1ull << l) - 1ull));
-        atomicAdd(&h[(uint64_t)pf * n_items + key], cnt);
+    if (!tie) continue;
+    const uint4 a4 = ld_u4(reinterpret_cast<const uint32_t*>(a), i, n);
+    uint4 b4 = make_uint4(0u, 0u, 0u, 0u);
+    if (st == 2) b4 = ld_u4(reinterpret_cast<const uint32_t*>(b), i, n);
+    uint64_t cur = ~0ull;
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint64_t key = ~0ull;
+      if ((tie >> j) & 1u) {
+        const uint32_t p = (r4 >> (8 * j)) & 0xFFu, ai = u4_at(a4, j);
+        if (st == 1) key = (uint64_t)p * n_items + ai;
+        else if (ai == pc.astar[p]) key = (uint64_t)p * n_items + u4_at(b4, j);
       }
+      if (key == ~0ull) continue;
+      if (key != cur) {
+        if (cnt) atomicAdd(&h[cur], cnt);
+        cur = key; cnt = 0;
+      }
+      ++cnt;
     }
+    if (cnt) atomicAdd(&h[cur], cnt);
   }
 }
 // smallest index j with incl[j] >= need (incl = inclusive prefix of one part's histogram)
@@ -2760,8 +2763,11 @@ __device__ __forceinline__ uint32_t ph_keep4(const uint8_t* __restrict__ rule, c
 __global__ __launch_bounds__(FIN_T) void k_ph_count(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
                                                     const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
                                                     const uint32_t* __restrict__ c2, int64_t n, int n_parts, int use_ge2,
-                                                    uint32_t thr, PartCut pc, uint32_t* __restrict__ bcnt) {
+                                                    uint32_t thr, PartCut pc_arg, uint32_t* __restrict__ bcnt) {
   __shared__ uint32_t wt[FIN_T / 64];
+  __shared__ PartCut pc;  // LDS copy (lane-indexed)
+  if (threadIdx.x == 0) pc = pc_arg;
+  __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * FIN_B;
   uint32_t k = 0;
 #pragma unroll
@@ -2780,9 +2786,12 @@ __global__ __launch_bounds__(FIN_T) void k_ph_count(const uint8_t* __restrict__ 
 __global__ __launch_bounds__(FIN_T) void k_ph_compact(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
                                                       const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
                                                       const uint32_t* __restrict__ c2, int64_t n, int n_parts,
-                                                      int use_ge2, uint32_t thr, PartCut pc,
+                                                      int use_ge2, uint32_t thr, PartCut pc_arg,
                                                       const uint64_t* __restrict__ boff, uint4* __restrict__ out) {
   __shared__ uint32_t wt[FIN_T / 64];
+  __shared__ PartCut pc;  // LDS copy (lane-indexed)
+  if (threadIdx.x == 0) pc = pc_arg;
+  __syncthreads();
   const int w = threadIdx.x >> 6;
   const int64_t base = (int64_t)blockIdx.x * FIN_B;
   uint64_t run = boff[blockIdx.x];

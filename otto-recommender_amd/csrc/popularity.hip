@@ -77,7 +77,7 @@ constexpr double KM_FX = 16777216.0;  // 2^24 fixed point for the cluster sums
 __global__ void k_km_prep(const float* __restrict__ C, int k, int dim, int KP, float* __restrict__ Ct,
                           float* __restrict__ cn) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < KP * dim) {
+  if (Ct && i < KP * dim) {  // (the MFMA kernels read C itself: Ct may be null)
     const int d = i / KP, c = i % KP;
     Ct[i] = c < k ? C[c * dim + d] : 0.f;
   }
@@ -780,71 +780,74 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
   if (l == 0 && w) atomicAdd(changed, (unsigned long long)w);
 }
 
-// Two n_init runs in lockstep over ONE read of X (C2, the reference's 10 independent runs): the
-// split-precision E-step of k_km_assign_split for run 0 and run 1 of a pair, each with its own
-// centroid fragments, LDS sums, labels, near-tie list and stop gate. The step is bound by the X stream
-// (5.2 GB at 12.9 M x 100): one pass instead of two halves it, and the two runs' MFMA chains fill the
-// time the single-run kernel spent waiting on memory. Every run sees exactly the arithmetic of
-// k_km_assign_split (same scores, same near-tie test, same fixed-point sums), so its labels, centres
-// and stopping step are those of the run alone. No distance bounds (every row is scored).
-struct KmPair {
-  const float* C[2];
-  const float* cn[2];
-  int32_t* label[2];
-  unsigned long long* sums[2];
-  unsigned long long* cnt[2];
-  unsigned long long* changed[2];
-  const int* gate[2];
-  uint32_t* amb_rows[2];
-  unsigned long long* n_amb[2];
+// n_init runs in lockstep over ONE read of X (C2, the reference's 10 independent runs): the split-precision
+// E-step of k_km_assign_split for G runs, each with its own centroid fragments (LDS), labels, near-tie list
+// and stop gate. One pass reads X for G runs (5.2 GB per pass at 12.9 M x 100) and gives the MFMA units G
+// runs' products per row tile. The per-cluster sums are not kept in LDS here (G x 40 KB would not fit beside
+// the fragments): every decided row whose label changes is appended to its run's move list (row, old, new),
+// which k_km_apply_moves folds into the run's fixed-point sums afterwards (the same exact integer adds as
+// km_move_rows). Every run sees exactly the arithmetic of k_km_assign_split (same scores, same near-tie
+// test, same sums), so its labels, centres and stopping step are those of the run alone (no distance bounds).
+constexpr int KMM_MAXG = 4;  // runs per pass over X
+struct KmMulti {
+  const float* C[KMM_MAXG];
+  const float* cn[KMM_MAXG];
+  int32_t* label[KMM_MAXG];
+  unsigned long long* changed[KMM_MAXG];
+  const int* gate[KMM_MAXG];
+  uint32_t* amb_rows[KMM_MAXG];
+  unsigned long long* n_amb[KMM_MAXG];
+  uint2* moves[KMM_MAXG];                // {row, old | new << 16} (old 0xFFFF: none)
+  unsigned long long* n_moves[KMM_MAXG];
 };
-constexpr int KMP_AMB = 1024;  // near-tie rows staged per block and run
-template <int NB, int KS>
-__global__ __launch_bounds__(KM_MT, 1) void k_km_assign_split_pair(const float* __restrict__ X, int64_t n, int dim,
-                                                                   int k, KmPair P) {
-  bool act[2];
-#pragma unroll
-  for (int g = 0; g < 2; ++g) act[g] = !(P.gate[g] && __builtin_amdgcn_readfirstlane(*P.gate[g]));
-  if (!act[0] && !act[1]) return;
+template <int G, int NB, int KS>
+__global__ __launch_bounds__(KM_MT, 1) void k_km_assign_split_multi(const float* __restrict__ X, int64_t n, int dim,
+                                                                    int k, KmMulti P) {
+  // per-run state lives in LDS (the run loop is not unrolled: one copy of the MFMA chain, no spills)
+  __shared__ float s_cmax[KMM_MAXG];
+  __shared__ int s_act[KMM_MAXG];
+  __shared__ uint32_t s_nchg[KMM_MAXG];
+  // the tile's current labels of every run (loaded with the tile's rows one tile ahead: a label load inside
+  // the run loop waited for the next tile's row loads as well, vmcnt counting in order)
+  __shared__ int32_t s_lab[KM_MT / 64][KMM_MAXG][64];
+  bool any = false;
+  for (int g = 0; g < G; ++g) any |= !(P.gate[g] && __builtin_amdgcn_readfirstlane(*P.gate[g]));
+  if (!any) return;
   extern __shared__ unsigned long long smem64[];
-  uint4* Cf = reinterpret_cast<uint4*>(smem64);                                   // [2][NB][KS][hi, lo][64]
-  unsigned long long* ls = reinterpret_cast<unsigned long long*>(Cf + 2 * NB * KS * 2 * 64);  // [2][k * dim]
-  unsigned long long* lc = ls + 2 * k * dim;                                      // [2][k]
-  int32_t* labl = reinterpret_cast<int32_t*>(lc + 2 * k);                         // [waves][3][32]
-  float* cnl = reinterpret_cast<float*>(labl + (KM_MT / 64) * 96);                // [2][64]
-  uint32_t* amb = reinterpret_cast<uint32_t*>(cnl + 128);                         // [2][KMP_AMB]
-  __shared__ uint32_t namb[2];
-  __shared__ unsigned long long abase[2];
-  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6, h = l >> 5, i32 = l & 31;
-  for (int e = tid; e < 2 * NB * KS * 64; e += KM_MT) {
+  uint4* Cf = reinterpret_cast<uint4*>(smem64);                       // [G][NB][KS][hi, lo][64]
+  float* cnl = reinterpret_cast<float*>(Cf + G * NB * KS * 2 * 64);   // [G][64]
+  const int tid = threadIdx.x, l = tid & 63, h = l >> 5, i32 = l & 31;
+  for (int e = tid; e < G * NB * KS * 64; e += KM_MT) {
     const int ll = e & 63, gsb = e >> 6, g = gsb / (NB * KS), sb = gsb % (NB * KS), s_ = sb % KS, b = sb / KS;
     const int c = b * 32 + (ll & 31), d0 = 16 * s_ + 8 * (ll >> 5);
     float v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (act[g] && c < k && d0 + j < dim) ? P.C[g][(int64_t)c * dim + d0 + j] : 0.f;
+    for (int j = 0; j < 8; ++j) v[j] = (c < k && d0 + j < dim) ? P.C[g][(int64_t)c * dim + d0 + j] : 0.f;
     uint4 hi, lo;
     km_split8(v, hi, lo);
     Cf[((g * NB * KS + sb) * 2 + 0) * 64 + ll] = hi;
     Cf[((g * NB * KS + sb) * 2 + 1) * 64 + ll] = lo;
   }
-  if (tid < 128) cnl[tid] = act[tid >> 6] ? P.cn[tid >> 6][tid & 63] : 0.f;
-  for (int i = tid; i < 2 * (k * dim + k); i += KM_MT) ls[i] = 0ull;  // ls and lc are adjacent
-  if (tid < 2) namb[tid] = 0;
+  for (int i = tid; i < G * 64; i += KM_MT) cnl[i] = P.cn[i >> 6][i & 63];
+  if (tid < G) {
+    s_act[tid] = !(P.gate[tid] && *P.gate[tid]);
+    s_nchg[tid] = 0;
+  }
   __syncthreads();
-  float cmax[2];
-#pragma unroll
-  for (int g = 0; g < 2; ++g) {
+  if (tid < 64 * G) {  // wave g: the run's largest centroid norm
+    const int g = tid >> 6;
     float c2 = l < k ? cnl[g * 64 + l] : 0.f;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) c2 = fmaxf(c2, __shfl_xor(c2, o));
-    cmax[g] = sqrtf(c2);
+    if (l == 0) s_cmax[g] = sqrtf(c2);
   }
-  uint32_t nchg[2] = {0, 0};
+  __syncthreads();
   const int64_t ntile = (n + 31) >> 5;
   const int64_t nwv = (int64_t)gridDim.x * (KM_MT / 64);
   float4 raw[2 * KS];
-  int32_t lab_n[2] = {-1, -1};
+  int32_t lab_n[G];
   int64_t row_n = 0;
+  const int wv = tid >> 6;
   auto load = [&](int64_t tt) __attribute__((always_inline)) {
     const int64_t rr = (tt << 5) + i32 < n ? (tt << 5) + i32 : n - 1;
     row_n = rr;
@@ -856,9 +859,9 @@ __global__ __launch_bounds__(KM_MT, 1) void k_km_assign_split_pair(const float* 
       raw[2 * s_ + 1] = d0 + 4 < dim ? *reinterpret_cast<const float4*>(xp + d0 + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int g = 0; g < 2; ++g) lab_n[g] = act[g] ? P.label[g][rr] : -1;
+    for (int g = 0; g < G; ++g) lab_n[g] = s_act[g] ? P.label[g][rr] : -1;
   };
-  const int64_t t_first = (int64_t)blockIdx.x * (KM_MT / 64) + wv;
+  const int64_t t_first = (int64_t)blockIdx.x * (KM_MT / 64) + (tid >> 6);
   if (t_first < ntile) load(t_first);
   for (int64_t t = t_first; t < ntile; t += nwv) {
     const int64_t r0 = t << 5;
@@ -877,12 +880,15 @@ __global__ __launch_bounds__(KM_MT, 1) void k_km_assign_split_pair(const float* 
       xh[s_] = __builtin_bit_cast(km_bf16x8, hi);
       xl[s_] = __builtin_bit_cast(km_bf16x8, lo);
     }
-    const int32_t lab_cur[2] = {lab_n[0], lab_n[1]};
+#pragma unroll
+    for (int g = 0; g < G; ++g) s_lab[wv][g][l] = lab_n[g];
     if (t + nwv < ntile) load(t + nwv);
     xs += __shfl_xor(xs, 32);
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      if (!act[g]) continue;  // wave-uniform
+    const float xn = sqrtf(xs);
+#pragma unroll 1
+    for (int g = 0; g < G; ++g) {
+      if (!s_act[g]) continue;  // block-uniform
+      const int32_t lab_cur = s_lab[wv][g][l];
       const uint4* Cg = Cf + g * NB * KS * 2 * 64;
       const float* cng = cnl + g * 64;
       km_f32x16 acc0 = {}, acc1 = {};
@@ -942,45 +948,69 @@ __global__ __launch_bounds__(KM_MT, 1) void k_km_assign_split_pair(const float* 
         if (NB == 2) m2 = fminf(m2, c0 + 32 == mc ? INFINITY : acc1[r]);
       }
       m2 = fminf(m2, __shfl_xor(m2, 32));
-      const bool decided = m2 - m > KMS_SEP * sqrtf(xs) * cmax[g];
+      const bool decided = m2 - m > KMS_SEP * xn * s_cmax[g];
       const uint32_t mi = (uint32_t)mc;
       const bool mine = h == 0 && in_r && decided;
-      int32_t old = -1;
-      if (mine) {
-        old = lab_cur[g];
-        nchg[g] += old != (int32_t)mi;
-        if (old != (int32_t)mi) P.label[g][row] = (int32_t)mi;
+      const bool mv = mine && lab_cur != (int32_t)mi;
+      if (mv) P.label[g][row] = (int32_t)mi;
+      // moves and near ties: one list reservation per wave each
+      const uint64_t mm = __ballot(mv);
+      if (mm) {
+        unsigned long long b = 0;
+        if (l == 0) {
+          b = atomicAdd(P.n_moves[g], (unsigned long long)__popcll(mm));
+          atomicAdd(&s_nchg[g], (uint32_t)__popcll(mm));
+        }
+        b = __shfl(b, 0);
+        if (mv)
+          P.moves[g][b + mbcnt(mm)] = make_uint2((uint32_t)row, (lab_cur < 0 ? 0xFFFFu : (uint32_t)lab_cur) | (mi << 16));
       }
       const bool tie = h == 0 && in_r && !decided;
       const uint64_t tm = __ballot(tie);
       if (tm) {
-        uint32_t b = 0;
-        if (l == 0) b = atomicAdd(&namb[g], (uint32_t)__popcll(tm));
+        unsigned long long b = 0;
+        if (l == 0) b = atomicAdd(P.n_amb[g], (unsigned long long)__popcll(tm));
         b = __shfl(b, 0);
-        if (tie) {
-          const uint32_t p = b + mbcnt(tm);
-          if (p < (uint32_t)KMP_AMB) amb[g * KMP_AMB + p] = (uint32_t)row;
-          else P.amb_rows[g][atomicAdd(P.n_amb[g], 1ull)] = (uint32_t)row;
-        }
+        if (tie) P.amb_rows[g][b + mbcnt(tm)] = (uint32_t)row;
       }
-      km_move_rows(X, dim, ls + g * k * dim, lc + g * k, labl + wv * 96, mine && old != (int32_t)mi, row, mi, old);
     }
   }
   __syncthreads();
-#pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    if (!act[g]) continue;
-    for (int i = tid; i < k * dim; i += KM_MT)
-      if (ls[g * k * dim + i]) atomicAdd(&P.sums[g][i], ls[g * k * dim + i]);
-    for (int i = tid; i < k; i += KM_MT)
-      if (lc[g * k + i]) atomicAdd(&P.cnt[g][i], lc[g * k + i]);
-    const uint32_t na = namb[g] < (uint32_t)KMP_AMB ? namb[g] : (uint32_t)KMP_AMB;
-    if (tid == 0) abase[g] = na ? atomicAdd(P.n_amb[g], (unsigned long long)na) : 0ull;
-    __syncthreads();
-    for (uint32_t i = tid; i < na; i += KM_MT) P.amb_rows[g][abase[g] + i] = amb[g * KMP_AMB + i];
-    const uint32_t w = wave_sum(nchg[g]);
-    if (l == 0 && w) atomicAdd(P.changed[g], (unsigned long long)w);
+  if (tid < G && s_nchg[tid]) atomicAdd(P.changed[tid], (unsigned long long)s_nchg[tid]);
+}
+
+// the move list of one run (k_km_assign_split_multi) into its fixed-point sums / counts: 32 moves per wave
+// round through km_move_rows (the rows' vectors added to the new cluster and subtracted from the old one in
+// the block's LDS sums, then one atomic per nonzero sum)
+__global__ __launch_bounds__(KM_MT) void k_km_apply_moves(const float* __restrict__ X, int dim, int k,
+                                                          const uint2* __restrict__ moves,
+                                                          const unsigned long long* __restrict__ n_moves,
+                                                          unsigned long long* __restrict__ sums,
+                                                          unsigned long long* __restrict__ cnt, const int* __restrict__ gate) {
+  if (gate && __builtin_amdgcn_readfirstlane(*gate)) return;
+  const int64_t nm = (int64_t)*n_moves;
+  if ((int64_t)blockIdx.x * 32 * (KM_MT / 64) >= nm) return;
+  extern __shared__ unsigned long long smem64[];
+  unsigned long long* ls = smem64;   // k * dim
+  unsigned long long* lc = ls + k * dim;
+  int32_t* labl = reinterpret_cast<int32_t*>(lc + k);  // [waves][3][32]
+  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
+  for (int i = tid; i < k * dim + k; i += KM_MT) ls[i] = 0ull;
+  __syncthreads();
+  const int64_t nwv = (int64_t)gridDim.x * (KM_MT / 64);
+  for (int64_t b = ((int64_t)blockIdx.x * (KM_MT / 64) + wv) * 32; b < nm; b += nwv * 32) {
+    const int64_t i = b + l;
+    const bool f = l < 32 && i < nm;
+    uint2 m = make_uint2(0u, 0u);
+    if (f) m = moves[i];
+    const uint32_t from = m.y & 0xFFFFu;
+    km_move_rows(X, dim, ls, lc, labl + wv * 96, f, (int64_t)m.x, m.y >> 16, from == 0xFFFFu ? -1 : (int32_t)from);
   }
+  __syncthreads();
+  for (int i = tid; i < k * dim; i += KM_MT)
+    if (ls[i]) atomicAdd(&sums[i], ls[i]);
+  for (int i = tid; i < k; i += KM_MT)
+    if (lc[i]) atomicAdd(&cnt[i], lc[i]);
 }
 
 // inc: sums / cnt hold the exact sums / counts of the rows under `labels` (the previous labels) and
@@ -1721,90 +1751,112 @@ int ottohip_kmeans_lloyd_steps(ottohip_ctx* ctx, const float* X, int64_t n, int 
   return 0;
 }
 
-// ottohip_kmeans_lloyd_steps for two runs in lockstep (k_km_assign_split_pair: one read of X per step
-// for both runs). Per run the same steps, stop checks and outputs as ottohip_kmeans_lloyd_steps; a
-// run that stops (its gate) costs nothing in the other run's later steps.
+// ottohip_kmeans_lloyd_steps for up to KMM_MAXG runs in lockstep (k_km_assign_split_multi: one read of X per
+// step for all of them). Per run the same steps, stop checks and outputs as ottohip_kmeans_lloyd_steps; a run
+// that stops (its gate) costs nothing in the other runs' later steps.
 __global__ void k_km_gate_set(int* __restrict__ ctl, int reason) {
   if (threadIdx.x == 0 && ctl[0] == 0) ctl[0] = reason;
 }
 
-int ottohip_kmeans_lloyd_steps_pair(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* const* centroids,
-                                    int k, int32_t* const* labels, int64_t* const* sums, int64_t* const* counts,
-                                    const int* max_steps, double tol, double* out, void* stream) {
+int ottohip_kmeans_lloyd_steps_multi(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* const* centroids,
+                                     int k, int32_t* const* labels, int64_t* const* sums, int64_t* const* counts,
+                                     const int* max_steps, int n_runs, double tol, double* out, void* stream) {
   if (!ctx || !X || !centroids || !labels || !sums || !counts || !out || !max_steps || n < 1 || dim < 1 ||
-      dim > EMB_MAXD || k < 1 || k > KM_MAXK || max_steps[0] < 0 || max_steps[1] < 0) {
-    set_error("kmeans_lloyd_steps_pair: bad arguments (k <= %d, dim <= %d)", KM_MAXK, EMB_MAXD); return OTTOHIP_EINVAL;
+      dim > EMB_MAXD || k < 1 || k > KM_MAXK || n_runs < 1 || n_runs > KMM_MAXG) {
+    set_error("kmeans_lloyd_steps_multi: bad arguments (k <= %d, dim <= %d, 1 <= n_runs <= %d)", KM_MAXK, EMB_MAXD,
+              KMM_MAXG);
+    return OTTOHIP_EINVAL;
   }
-  for (int g = 0; g < 2; ++g)
-    if (!centroids[g] || !labels[g] || !sums[g] || !counts[g] || !km_mfma_ok(k, dim, X, centroids[g]) || k <= 32 ||
-        dim > 112 || n > 0xFFFFFFFFll) {
-      set_error("kmeans_lloyd_steps_pair: needs the MFMA E-step (32 < k <= 64, dim <= 112, aligned operands)");
+  for (int g = 0; g < n_runs; ++g)
+    if (max_steps[g] < 0 || !centroids[g] || !labels[g] || !sums[g] || !counts[g] || !km_mfma_ok(k, dim, X, centroids[g]) ||
+        k <= 32 || dim > 112 || n > 0xFFFFFFFFll) {
+      set_error("kmeans_lloyd_steps_multi: needs the MFMA E-step (32 < k <= 64, dim <= 112, aligned operands)");
       return OTTOHIP_ELIMIT;
     }
   hipStream_t s = S(stream);
   OH_HIP(hipSetDevice(ctx->device));
   ctx->km_bvalid = false;  // no distance bounds in lockstep steps
   constexpr int NB = 2, KS = 7;
+  const int G = n_runs;
   const int KP = (k + 7) / 8 * 8, nq = (dim + 7) / 8;
-  double* st;  // [2][inertia, changed, shift, empty]
-  int* ctl;    // [2][reason, steps]
-  OH_TRY(ctx->ws.get("kmp_stats", 8, &st));
-  OH_TRY(ctx->ws.get("kmp_ctl", 4, &ctl));
-  OH_HIP(hipMemsetAsync(ctl, 0, 4 * sizeof(int), s));
-  KmPair P;
-  float* Ct[2];
-  float* cn[2];
-  const char* ctn[2] = {"kmp_ct0", "kmp_ct1"};
-  const char* cnn[2] = {"kmp_cn0", "kmp_cn1"};
-  const char* abn[2] = {"kmp_amb0", "kmp_amb1"};
-  const char* nan_[2] = {"kmp_namb0", "kmp_namb1"};
-  for (int g = 0; g < 2; ++g) {
-    OH_TRY(ctx->ws.get(ctn[g], (size_t)KP * dim, &Ct[g]));
-    OH_TRY(ctx->ws.get(cnn[g], (size_t)KM_MAXK, &cn[g]));
-    OH_TRY(ctx->ws.get(abn[g], (size_t)n, &P.amb_rows[g]));
-    OH_TRY(ctx->ws.get(nan_[g], 1, &P.n_amb[g]));
+  double* st;  // [G][inertia, changed, shift, empty]
+  int* ctl;    // [G][reason, steps]
+  OH_TRY(ctx->ws.get("kmm_stats", (size_t)4 * KMM_MAXG, &st));
+  OH_TRY(ctx->ws.get("kmm_ctl", (size_t)2 * KMM_MAXG, &ctl));
+  OH_HIP(hipMemsetAsync(ctl, 0, (size_t)2 * KMM_MAXG * sizeof(int), s));
+  KmMulti P;
+  memset(&P, 0, sizeof P);
+  float* cn[KMM_MAXG] = {};
+  for (int g = 0; g < G; ++g) {
+    char nm[32];
+    snprintf(nm, sizeof nm, "kmm_cn%d", g);
+    OH_TRY(ctx->ws.get(nm, (size_t)KM_MAXK, &cn[g]));
+    snprintf(nm, sizeof nm, "kmm_amb%d", g);
+    OH_TRY(ctx->ws.get(nm, (size_t)n, &P.amb_rows[g]));
+    snprintf(nm, sizeof nm, "kmm_namb%d", g);
+    OH_TRY(ctx->ws.get(nm, 2, &P.n_amb[g]));  // [near ties, moves]
+    P.n_moves[g] = P.n_amb[g] + 1;
+    snprintf(nm, sizeof nm, "kmm_mv%d", g);
+    OH_TRY(ctx->ws.get(nm, (size_t)n, &P.moves[g]));
     P.C[g] = centroids[g];
     P.cn[g] = cn[g];
     P.label[g] = labels[g];
-    P.sums[g] = reinterpret_cast<unsigned long long*>(sums[g]);
-    P.cnt[g] = reinterpret_cast<unsigned long long*>(counts[g]);
     P.changed[g] = reinterpret_cast<unsigned long long*>(st + 4 * g + 1);
     P.gate[g] = ctl + 2 * g;
   }
-  const size_t lds2 = (size_t)2 * NB * KS * 2 * 64 * 16 + (size_t)2 * ((size_t)k * dim + k) * 8 + (KM_MT / 64) * 96 * 4 +
-                      128 * 4 + (size_t)2 * KMP_AMB * 4;
-  OH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_km_assign_split_pair<NB, KS>),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
+  const size_t ldsm = (size_t)G * NB * KS * 2 * 64 * 16 + (size_t)G * 64 * 4;
+  const void* mk = nullptr;
+  switch (G) {
+    case 1: mk = reinterpret_cast<const void*>(k_km_assign_split_multi<1, NB, KS>); break;
+    case 2: mk = reinterpret_cast<const void*>(k_km_assign_split_multi<2, NB, KS>); break;
+    case 3: mk = reinterpret_cast<const void*>(k_km_assign_split_multi<3, NB, KS>); break;
+    default: mk = reinterpret_cast<const void*>(k_km_assign_split_multi<4, NB, KS>); break;
+  }
+  OH_HIP(hipFuncSetAttribute(mk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsm));
+  const size_t ldsa = ((size_t)k * dim + k) * 8 + (KM_MT / 64) * 96 * 4;
+  OH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_km_apply_moves), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)ldsa));
   auto ek = nq == 13 ? k_km_assign_mfma<NB, 13, true> : k_km_assign_mfma<NB, KM_NQ, true>;
   const size_t lds = (size_t)NB * nq * 64 * 16 + (KM_MT / 64) * 96 * 4 + 64 * 4 + ((size_t)k * dim + k) * 8;
   OH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(ek), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const int64_t ntile = ceil_div(n, 32);
   const unsigned pgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(ntile, KM_MT / 64), ctx->n_cu));
   const unsigned egrid = (unsigned)std::max(1, ctx->n_cu / 2);
-  const int steps = std::max(max_steps[0], max_steps[1]);
+  const unsigned agrid = (unsigned)std::max(1, ctx->n_cu);
+  int steps = 0;
+  for (int g = 0; g < G; ++g) steps = std::max(steps, max_steps[g]);
   for (int i = 0; i < steps; ++i) {
-    for (int g = 0; g < 2; ++g) {
+    for (int g = 0; g < G; ++g) {
       if (i == max_steps[g]) k_km_gate_set<<<1, 64, 0, s>>>(ctl + 2 * g, 4);  // this run's step budget is spent
       k_km_gate_reset<<<1, 64, 0, s>>>(ctl + 2 * g, st + 4 * g);
-      k_km_prep<<<grid_for(std::max<int64_t>((int64_t)KP * dim, KM_MAXK)), 256, 0, s>>>(centroids[g], k, dim, KP, Ct[g],
-                                                                                       cn[g]);
-      OH_HIP(hipMemsetAsync(P.n_amb[g], 0, 8, s));
+      k_km_prep<<<grid_for(std::max<int64_t>((int64_t)KP * dim, KM_MAXK)), 256, 0, s>>>(centroids[g], k, dim, KP,
+                                                                                       nullptr, cn[g]);
+      OH_HIP(hipMemsetAsync(P.n_amb[g], 0, 16, s));
     }
-    k_km_assign_split_pair<NB, KS><<<pgrid, KM_MT, lds2, s>>>(X, n, dim, k, P);
-    for (int g = 0; g < 2; ++g)  // the near ties of each run, exact f32 scores
-      ek<<<egrid, KM_MT, lds, s>>>(X, n, dim, nq, centroids[g], cn[g], k, labels[g], P.sums[g], P.cnt[g], st + 4 * g,
-                                   P.changed[g], nullptr, 1, P.gate[g], P.amb_rows[g], P.n_amb[g]);
-    for (int g = 0; g < 2; ++g)
+    switch (G) {
+      case 1: k_km_assign_split_multi<1, NB, KS><<<pgrid, KM_MT, ldsm, s>>>(X, n, dim, k, P); break;
+      case 2: k_km_assign_split_multi<2, NB, KS><<<pgrid, KM_MT, ldsm, s>>>(X, n, dim, k, P); break;
+      case 3: k_km_assign_split_multi<3, NB, KS><<<pgrid, KM_MT, ldsm, s>>>(X, n, dim, k, P); break;
+      default: k_km_assign_split_multi<4, NB, KS><<<pgrid, KM_MT, ldsm, s>>>(X, n, dim, k, P); break;
+    }
+    for (int g = 0; g < G; ++g) {
+      unsigned long long* sg = reinterpret_cast<unsigned long long*>(sums[g]);
+      unsigned long long* cg = reinterpret_cast<unsigned long long*>(counts[g]);
+      k_km_apply_moves<<<agrid, KM_MT, ldsa, s>>>(X, dim, k, P.moves[g], P.n_moves[g], sg, cg, P.gate[g]);
+      // the near ties of the run, exact f32 scores
+      ek<<<egrid, KM_MT, lds, s>>>(X, n, dim, nq, centroids[g], cn[g], k, labels[g], sg, cg, st + 4 * g, P.changed[g],
+                                   nullptr, 1, P.gate[g], P.amb_rows[g], P.n_amb[g]);
       k_km_update<<<1, KM_UT, 0, s>>>(centroids[g], reinterpret_cast<const long long*>(sums[g]),
                                       reinterpret_cast<const long long*>(counts[g]), k, dim, 1, st + 4 * g + 2,
                                       ctl + 2 * g, reinterpret_cast<const unsigned long long*>(st + 4 * g + 1), tol);
+    }
   }
   OH_HIP(hipGetLastError());
-  double h[8];
-  int c2[4];
-  OH_TRY(d2h(h, st, 8, s));
-  OH_TRY(d2h(c2, ctl, 4, s));
-  for (int g = 0; g < 2; ++g) {
+  double h[4 * KMM_MAXG];
+  int c2[2 * KMM_MAXG];
+  OH_TRY(d2h(h, st, (size_t)4 * KMM_MAXG, s));
+  OH_TRY(d2h(c2, ctl, (size_t)2 * KMM_MAXG, s));
+  for (int g = 0; g < G; ++g) {
     unsigned long long c, e;
     memcpy(&c, &h[4 * g + 1], 8);
     memcpy(&e, &h[4 * g + 3], 8);
@@ -1816,6 +1868,13 @@ int ottohip_kmeans_lloyd_steps_pair(ottohip_ctx* ctx, const float* X, int64_t n,
     out[6 * g + 5] = c2[2 * g] == 4 ? 0 : c2[2 * g];  // 4: stopped by its step budget, not a stop check
   }
   return 0;
+}
+
+int ottohip_kmeans_lloyd_steps_pair(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* const* centroids,
+                                    int k, int32_t* const* labels, int64_t* const* sums, int64_t* const* counts,
+                                    const int* max_steps, double tol, double* out, void* stream) {
+  return ottohip_kmeans_lloyd_steps_multi(ctx, X, n, dim, centroids, k, labels, sums, counts, max_steps, 2, tol, out,
+                                          stream);
 }
 
 // the m rows farthest from their labelled centroid, (distance desc, row asc)

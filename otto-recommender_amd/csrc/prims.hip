@@ -95,7 +95,10 @@ int exclusive_scan_u64(Ctx* ctx, const uint64_t* in, uint64_t* out, int64_t n, u
 }
 
 // ------------------------------------------------------------------ radix sort
-constexpr int RS_T = 256, RS_WAVES = RS_T / 64, RS_R = 16, RS_TILE = RS_T * RS_R;  // 4096
+#ifndef OH_RS_R
+#define OH_RS_R 16
+#endif
+constexpr int RS_T = 256, RS_WAVES = RS_T / 64, RS_R = OH_RS_R, RS_TILE = RS_T * RS_R;  // 4096 (keys per thread: A/B build flag)
 // a block sorts RS_SUB consecutive tiles in order, so the digit-count matrix (and its scan) has one
 // column per 4 tiles: the scan of every pass was larger than the scatter's own work
 constexpr int RS_SUB = 4, RS_BLOCK = RS_TILE * RS_SUB;

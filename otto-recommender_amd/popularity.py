@@ -59,6 +59,7 @@ def compute_sessions_embeddings(offsets, aid, ts, type_, words, embeddings, n_it
 
 FX = float(1 << 24)  # fixed-point scale of the device sums (csrc/popularity.hip KM_FX)
 LLOYD_BATCH = 10  # Lloyd steps per ottohip_kmeans_lloyd_steps call (the stop checks run on the device)
+KM_GROUP = 1  # n_init runs in lockstep per read of X (ottohip_kmeans_lloyd_steps_multi); 1: one bounded run at a time
 
 
 def _allreduce(t, group):
@@ -162,25 +163,23 @@ class KMeans:
         best = None
         inr, chg, shift = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
         st6 = (ctypes.c_double * 6)()
-        # OTTOHIP_KM_PAIR=1: two runs in lockstep over one read of X per Lloyd step
-        # (ottohip_kmeans_lloyd_steps_pair). Off by default: the lockstep steps carry no distance bounds and
-        # measured slower than one bounded run at a time (config 5 C2 2.36 s vs 1.31 s, same box)
-        pair_ok = (group is None and 32 < k <= 64 and dim <= 112 and dim % 4 == 0
-                   and os.environ.get("OTTOHIP_KM_PAIR", "0") == "1")
-        pending = None  # the second run of a pair, finished in lockstep with the first
+        # one GPU: up to KM_GROUP runs in lockstep over one read of X per Lloyd step
+        # (ottohip_kmeans_lloyd_steps_multi); OTTOHIP_KM_GROUP=1 runs them one at a time with distance bounds
+        grp = int(os.environ.get("OTTOHIP_KM_GROUP", str(KM_GROUP)))
+        multi_ok = group is None and 32 < k <= 64 and dim <= 112 and dim % 4 == 0 and grp >= 2
+        pending = []  # later runs of a lockstep group, in run order
         for run in range(self.n_init):
-            if pending is not None:
-                inertia, Cp, labp, itp = pending
-                pending = None
-                if best is None or inertia < best[0]:
-                    best = (inertia, Cp, labp, itp)
+            if pending:
+                res = pending.pop(0)
+                if best is None or res[0] < best[0]:
+                    best = res
                 continue
-            if pair_ok and run + 1 < self.n_init:
-                res = self._fit_pair(Xc, [next(seed_stream), next(seed_stream)], grows, tol_abs, ctx, sh)
-                pending = res[1]
-                inertia, Cp, labp, itp = res[0]
-                if best is None or inertia < best[0]:
-                    best = (inertia, Cp, labp, itp)
+            if multi_ok and run + 1 < self.n_init:
+                g = min(grp, self.n_init - run, 4)
+                res = self._fit_multi(Xc, [next(seed_stream) for _ in range(g)], grows, tol_abs, ctx, sh)
+                pending = res[1:]
+                if best is None or res[0][0] < best[0]:
+                    best = res[0]
                 continue
             seeds = next(seed_stream)
             C = self._gather_rows(Xc, seeds, grows, group)
@@ -239,30 +238,32 @@ class KMeans:
         self.cluster_centers_ = C + mean_d
         return self
 
-    def _fit_pair(self, Xc, seeds2, grows, tol_abs, ctx, sh):
-        """Two runs of fit's single-GPU loop in lockstep: the same batches of device Lloyd steps, stop
-        checks and empty-cluster relocations per run, each run's E-step sharing one read of X with the
-        other's. Returns [(inertia, C, labels, n_iter)] for the two runs, in run order."""
+    def _fit_multi(self, Xc, seeds, grows, tol_abs, ctx, sh):
+        """G <= 4 runs of fit's single-GPU loop in lockstep: the same batches of device Lloyd steps, stop
+        checks and empty-cluster relocations per run, every run's E-step sharing one read of X with the
+        others'. Returns [(inertia, C, labels, n_iter)] for the runs, in run order."""
         import torch
         lib = _lib.load()
         n, dim = (int(v) for v in Xc.shape)
         k = self.n_clusters
         dev = Xc.device
-        C = [self._gather_rows(Xc, sd, grows, None) for sd in seeds2]
-        lab = [torch.full((max(n, 1),), -1, dtype=torch.int32, device=dev) for _ in range(2)]
-        sums = [torch.zeros(k * dim, dtype=torch.int64, device=dev) for _ in range(2)]
-        counts = [torch.zeros(k, dtype=torch.int64, device=dev) for _ in range(2)]
-        P = ctypes.c_void_p * 2
+        G = len(seeds)
+        C = [self._gather_rows(Xc, sd, grows, None) for sd in seeds]
+        lab = [torch.full((max(n, 1),), -1, dtype=torch.int32, device=dev) for _ in range(G)]
+        sums = [torch.zeros(k * dim, dtype=torch.int64, device=dev) for _ in range(G)]
+        counts = [torch.zeros(k, dtype=torch.int64, device=dev) for _ in range(G)]
+        P = ctypes.c_void_p * G
         pc, pl = P(*[_lib.ptr(x) for x in C]), P(*[_lib.ptr(x) for x in lab])
         ps, pn = P(*[_lib.ptr(x) for x in sums]), P(*[_lib.ptr(x) for x in counts])
-        it, done, strict = [0, 0], [False, False], [False, False]
-        st12 = (ctypes.c_double * 12)()
+        it, done, strict = [0] * G, [False] * G, [False] * G
+        st = (ctypes.c_double * (6 * G))()
         shift = ctypes.c_double()
         while not all(done):
-            steps = (ctypes.c_int * 2)(*[0 if done[g] else min(LLOYD_BATCH, self.max_iter - it[g]) for g in range(2)])
-            _lib.check(lib.ottohip_kmeans_lloyd_steps_pair(ctx.h, _lib.ptr(Xc), n, dim, pc, k, pl, ps, pn, steps,
-                                                           tol_abs, st12, sh))
-            for g in range(2):
+            steps = (ctypes.c_int * G)(*[0 if done[g] else min(LLOYD_BATCH, self.max_iter - it[g]) for g in range(G)])
+            _lib.check(lib.ottohip_kmeans_lloyd_steps_multi(ctx.h, _lib.ptr(Xc), n, dim, pc, k, pl, ps, pn, steps, G,
+                                                            tol_abs, st, sh))
+            st12 = st
+            for g in range(G):
                 if done[g]:
                     continue
                 it[g] += int(st12[6 * g + 4])
@@ -281,7 +282,7 @@ class KMeans:
                     done[g] = True
         out = []
         inr, chg = ctypes.c_double(), ctypes.c_int64()
-        for g in range(2):
+        for g in range(G):
             if not strict[g]:  # E-step with the final centres (labels match cluster_centers_)
                 _lib.check(lib.ottohip_kmeans_partial(ctx.h, _lib.ptr(Xc), n, dim, _lib.ptr(C[g]), k, _lib.ptr(lab[g]),
                                                       _lib.ptr(sums[g]), _lib.ptr(counts[g]), ctypes.byref(inr),

@@ -96,6 +96,7 @@ def test_kmeans_bounded_steps_equal_full_steps(gpu, monkeypatch, case):
         X = (centers[rng.integers(0, 40, 20000)] + rng.normal(size=(20000, 100))).astype(np.float32)
         k, n_init = 33, 3
     fits = []
+    monkeypatch.setenv("OTTOHIP_KM_GROUP", "1")  # the bounded single-run steps (lockstep groups carry no bounds)
     for bounds in ("0", "1"):
         monkeypatch.setenv("OTTOHIP_KM_BOUNDS", bounds)
         km = gp.KMeans(n_clusters=k, random_state=42, n_init=n_init).fit(X)
@@ -131,6 +132,7 @@ def test_kmeans_split_precision_steps_equal_exact_steps(gpu, monkeypatch, case):
         X = (centers[rng.integers(0, 40, 20000)] + rng.normal(size=(20000, 100))).astype(np.float32)
         n_init = 3
     fits = []
+    monkeypatch.setenv("OTTOHIP_KM_GROUP", "1")  # the single-run steps (lockstep groups always take the split pass)
     for split in ("0", "1"):  # the exact kernel on every row; the split pass + the exact kernel on near ties
         monkeypatch.setenv("OTTOHIP_KM_SPLIT", split)
         km = gp.KMeans(n_clusters=k, random_state=42, n_init=n_init).fit(X)
@@ -142,12 +144,12 @@ def test_kmeans_split_precision_steps_equal_exact_steps(gpu, monkeypatch, case):
 
 
 @pytest.mark.parametrize("case", ["sessions_k50", "relocation_k40", "blocks_k33"])
-def test_kmeans_pair_lockstep_equals_single_runs(gpu, monkeypatch, case):
-    """Two n_init runs in lockstep over one read of X per Lloyd step (ottohip_kmeans_lloyd_steps_pair)
-    give bit-identical labels, centres, inertia and iterations to the runs one at a time: k = 50 on
-    session embeddings (runs reach max_iter; n_init = 3, so a pair and a single run), duplicated rows
-    with empty clusters relocated in one run of a pair while the other keeps stepping (k = 40), and
-    k = 33 with runs that converge at different steps."""
+def test_kmeans_lockstep_equals_single_runs(gpu, monkeypatch, case):
+    """n_init runs in lockstep over one read of X per Lloyd step (ottohip_kmeans_lloyd_steps_multi, groups of
+    2, 3 and 4 runs) give bit-identical labels, centres, inertia and iterations to the runs one at a time
+    (with distance bounds): k = 50 on session embeddings (runs reach max_iter; n_init = 5: groups of 4 + 1,
+    3 + 2, 2 + 2 + 1), duplicated rows with empty clusters relocated in one run of a group while the others
+    keep stepping (k = 40), and k = 33 with runs that converge at different steps."""
     from otto_recommender_amd import popularity as gp
     rng = np.random.default_rng(19)
     if case == "sessions_k50":
@@ -155,7 +157,7 @@ def test_kmeans_pair_lockstep_equals_single_runs(gpu, monkeypatch, case):
         words = np.unique(ev.aid)
         emb = synth.embeddings(len(words), seed=1)
         X = gp.compute_sessions_embeddings(ev.session_offsets, ev.aid, ev.ts, ev.type, words, emb).cpu().numpy()
-        k, n_init = 50, 3
+        k, n_init = 50, 5
     elif case == "relocation_k40":
         centers = rng.normal(scale=2, size=(40, 100))
         X = (centers[rng.integers(0, 40, 30000)] + rng.normal(size=(30000, 100))).astype(np.float32)
@@ -166,13 +168,14 @@ def test_kmeans_pair_lockstep_equals_single_runs(gpu, monkeypatch, case):
         X = (centers[rng.integers(0, 40, 20000)] + rng.normal(size=(20000, 100))).astype(np.float32)
         k, n_init = 33, 4
     fits = []
-    for pair in ("0", "1"):
-        monkeypatch.setenv("OTTOHIP_KM_PAIR", pair)
+    for grp in ("1", "2", "3", "4"):
+        monkeypatch.setenv("OTTOHIP_KM_GROUP", grp)
         km = gp.KMeans(n_clusters=k, random_state=42, n_init=n_init).fit(X)
         fits.append((km.labels_.cpu().numpy(), km.cluster_centers_.cpu().numpy(), km.inertia_, km.n_iter_))
-    np.testing.assert_array_equal(fits[0][0], fits[1][0])
-    np.testing.assert_array_equal(fits[0][1], fits[1][1])
-    assert fits[0][2] == fits[1][2] and fits[0][3] == fits[1][3]
+    for f in fits[1:]:
+        np.testing.assert_array_equal(fits[0][0], f[0])
+        np.testing.assert_array_equal(fits[0][1], f[1])
+        assert fits[0][2] == f[2] and fits[0][3] == f[3]
 
 
 def test_kmeans_empty_cluster_relocation(gpu):

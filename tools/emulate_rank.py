@@ -53,6 +53,7 @@ def main():
         w, wpp, pc, ppp, names = gd.emit_for_owners(dev, G, mine, n_files, ctx=ctx)
         torch.cuda.synchronize()
         t_emit = time.perf_counter() - t0
+        own_wpp, own_ppp = list(wpp), list(ppp)  # this rank's send segments (words, pieces) per owner
         ph_emit = ctx.timings()
         ctx.set_timing(False)
         del w, pc
@@ -88,9 +89,9 @@ def main():
         rows = sum(shard.stats(n)["n_rows"] for n in names)
         shard.free()
     res = {"world": G, "rank": args.rank, "files": len(mine), "events": int(ev.n_events),
-           "send_words": int(sum(wpp)), "recv_words": int(ws.numel()), "recv_pieces": int(ps.numel()),
+           "send_words": int(sum(own_wpp)), "recv_words": int(ws.numel()), "recv_pieces": int(ps.numel()),
            "shard_rows": int(rows), "emit_s": t_emit, "reduce_received_s": t_red,
-           "send_bytes_remote": 4 * int(sum(wpp) - wpp[args.rank]) + 8 * int(sum(ppp) - ppp[args.rank]),
+           "send_bytes_remote": 4 * int(sum(own_wpp) - own_wpp[args.rank]) + 8 * int(sum(own_ppp) - own_ppp[args.rank]),
            "phases_ms": {n: round(ms, 3) for n, ms, _ in ph_emit + ph_red}}
     print(json.dumps(res))
 
