@@ -420,8 +420,12 @@ static int covis_emit_words(ottohip_ctx* ctx, const Front& F, const ottohip_even
   OH_HIP(hipMemsetAsync(eerr, 0, sizeof(int), s));
   // per-type task lists in pass 3 (OTTOHIP_EMIT_TASKS=0: every (rule, next type) of the wave in turn; read per call)
   const bool tasks = !(getenv("OTTOHIP_EMIT_TASKS") && !strcmp(getenv("OTTOHIP_EMIT_TASKS"), "0"));
+  // two pairs per lane per flush round (OTTOHIP_EMIT_FLUSH2=0: one; read per call)
+  const bool fl2 = !(getenv("OTTOHIP_EMIT_FLUSH2") && !strcmp(getenv("OTTOHIP_EMIT_FLUSH2"), "0"));
+  auto ek = guard ? (tasks ? k_emit<true, true, true> : k_emit<true, false, true>)
+                  : (tasks ? (fl2 ? k_emit<false, true, true> : k_emit<false, true, false>) : k_emit<false, false, true>);
   if (F.NB > 0)
-    (guard ? (tasks ? k_emit<true, true> : k_emit<true, false>) : (tasks ? k_emit<false, true> : k_emit<false, false>))<<<(unsigned)F.NB, 64, 0, s>>>(F.off, F.first, F.NB, F.evp, F.R, F.Lt, F.fb, ev->n_files, F.fid, F.cnt,
+    ek<<<(unsigned)F.NB, 64, 0, s>>>(F.off, F.first, F.NB, F.evp, F.R, F.Lt, F.fb, ev->n_files, F.fid, F.cnt,
                                          EvOff{F.poff, F.poff32}, w0, eerr, dbg);
   if (F.nl > 0)
     k_emit_long<<<F.nl, 64, 0, s>>>(F.off, F.long_list, F.d_loff, F.lscr, F.lpscr, F.evp, F.R, F.Lt, F.fb,

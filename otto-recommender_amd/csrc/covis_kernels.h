@@ -948,7 +948,7 @@ struct EmitLds {
   uint32_t sfile[64];
   uint16_t espos[EB_CAP];               // per batch event: position in tev (EB_NONE: invalid)
   uint8_t esid[EB_CAP];                 // per batch event: session index in the batch
-  uint32_t mark[64];                    // flush round id at the window positions where a record starts
+  uint32_t mark[128];                   // flush round id at the window positions where a record starts
 };
 
 // expand records [0, nrec) holding tot pairs: lane k of round c writes pair c + k. Record starts
@@ -1005,6 +1005,72 @@ __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, i
   }
 }
 
+// emit_flush with two pairs per lane per round (128 pairs: lane k writes pairs c + k and c + 64 + k): one mark
+// round (writes, barrier) and one loop trip per 128 pairs, and the two halves' record / list reads in flight
+// together. The halves run the same rank logic in order; the spanning record's carry passes from half to half.
+template <bool GUARD>
+__device__ __forceinline__ void emit_flush2(EmitLds& S, int nrec, uint32_t tot, int F, uint32_t* __restrict__ words,
+                                            int dbg, uint32_t& rid, int* __restrict__ err) {
+  if (dbg & 2) return;  // profiling ablation: records are built, never expanded
+  const uint32_t l = lane_id();
+  const uint32_t sa = (int)l < nrec ? S.u.r.rpre[l] : 0xFFFFFFFFu;
+  const uint32_t sb = (int)l + 64 < nrec ? S.u.r.rpre[l + 64] : 0xFFFFFFFFu;
+  const uint64_t below = (1ull << l) - 1ull, upto = below | (1ull << l);  // lanes < l, <= l
+  int ob = -1;        // last record starting before the current half's window
+  uint32_t cc = 0;    // words written in earlier halves by the record spanning into the current one
+  for (uint32_t c = 0; c < tot; c += 128) {
+    ++rid;
+    if (sa - c < 128u) S.mark[sa - c] = rid;
+    if (sb - c < 128u) S.mark[sb - c] = rid;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const uint64_t mA = __ballot(S.mark[l] == rid), mB = __ballot(S.mark[64 + l] == rid);
+    const uint64_t mleA = mA & upto, mleB = mB & upto;
+    const int oA = ob + (int)__popcll(mleA);
+    const int oB = ob + (int)__popcll(mA) + (int)__popcll(mleB);
+    ob += (int)__popcll(mA) + (int)__popcll(mB);
+    const uint32_t pA = c + l, pB = c + 64 + l;
+    bool qA = false, qB = false;
+    uint32_t wA = 0, wB = 0;
+    uint64_t dA = 0, dB = 0;
+    const bool badA = GUARD && pA < tot && (oA < 0 || oA >= nrec);
+    const bool badB = GUARD && pB < tot && (oB < 0 || oB >= nrec);
+    if (badA || badB) atomicOr(err, 8);
+    if (pA < tot && !badA) {
+      const uint4 rc = S.u.r.rec[oA];
+      uint32_t j = (rc.y & 1023u) + (pA - rc.x);
+      if (j >= ((rc.y >> 10) & 1023u)) j += rc.y >> 21;
+      const uint32_t a = (uint32_t)ev_aid(S.tev[j]);
+      qA = a >= rc.w;
+      wA = rc.z | (a << F);
+      dA = S.u.r.rout[oA];
+    }
+    if (pB < tot && !badB) {
+      const uint4 rc = S.u.r.rec[oB];
+      uint32_t j = (rc.y & 1023u) + (pB - rc.x);
+      if (j >= ((rc.y >> 10) & 1023u)) j += rc.y >> 21;
+      const uint32_t a = (uint32_t)ev_aid(S.tev[j]);
+      qB = a >= rc.w;
+      wB = rc.z | (a << F);
+      dB = S.u.r.rout[oB];
+    }
+    // half A: the record's lanes start at its mark, or at lane 0 for the record spanning into the half
+    const uint64_t QA = __ballot(qA);
+    const uint32_t firstA = mleA ? 63u - (uint32_t)__builtin_clzll(mleA) : 0u;
+    const uint64_t mineA = QA & ~((1ull << firstA) - 1ull);
+    const uint32_t carA = mleA ? 0u : cc;
+    if (qA && !(dbg & 1)) words[dA + carA + (uint32_t)__popcll(mineA & below)] = wA;
+    cc = (uint32_t)__builtin_amdgcn_readlane((int)(carA + (uint32_t)__popcll(mineA)), 63);
+    // half B
+    const uint64_t QB = __ballot(qB);
+    const uint32_t firstB = mleB ? 63u - (uint32_t)__builtin_clzll(mleB) : 0u;
+    const uint64_t mineB = QB & ~((1ull << firstB) - 1ull);
+    const uint32_t carB = mleB ? 0u : cc;
+    if (qB && !(dbg & 1)) words[dB + carB + (uint32_t)__popcll(mineB & below)] = wB;
+    cc = (uint32_t)__builtin_amdgcn_readlane((int)(carB + (uint32_t)__popcll(mineB)), 63);
+  }
+}
+
 // Per event type, the (rule, next type) windows an event of that type writes, as pass 3's task list: entry
 // q | tt << 4 | sym << 6, the non-symmetric rules first (a symmetric record's written length is only known to
 // S2's count, so it goes last in the event's run)
@@ -1030,7 +1096,7 @@ __device__ inline void emit_tasks_build(const RulesDev& R, EmitTasks& T) {
 // GUARD (OTTOHIP_DEBUG): bounds checks of the record arrays (err bit 8). TASKS: pass 3 iterates the per-type
 // task lists (lanes of different types search their own lists together); else (OTTOHIP_EMIT_TASKS=0) every
 // (rule, next type) of the wave's types in turn
-template <bool GUARD, bool TASKS>
+template <bool GUARD, bool TASKS, bool FL2 = true>
 __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restrict__ off, const int64_t* __restrict__ first,
                                              int64_t NB, const uint64_t* __restrict__ ev, RulesDev R, Layout L,
                                              const int64_t* __restrict__ fb, int nf, const uint32_t* __restrict__ fid,
@@ -1050,7 +1116,8 @@ __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restri
   int maxq = 0;
 #pragma unroll
   for (int t = 0; t < 3; ++t) maxq = max(maxq, R.n_of_type[t]);
-  S.mark[l] = 0u;
+  S.mark[l] = 0u;  // (both halves: a stale value equal to a later round id would be a false record start)
+  S.mark[64 + l] = 0u;
   uint32_t rid = 0;  // flush round id (marks of earlier rounds never match)
   int fcur = file_of(fb, nf, s0);
   int64_t next_b = fcur + 1 < nf ? fb[fcur + 1] : INT64_MAX;
@@ -1204,7 +1271,7 @@ __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restri
           if (nrec + nn > EB_RCAP) {
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            emit_flush<GUARD>(S, nrec, tot, L.F, words, dbg, rid, err);
+            (FL2 ? emit_flush2<GUARD> : emit_flush<GUARD>)(S, nrec, tot, L.F, words, dbg, rid, err);
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             nrec = 0; tot = 0;
@@ -1254,7 +1321,7 @@ __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restri
             if (nrec + nn > EB_RCAP) {
               __builtin_amdgcn_wave_barrier();
               __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-              emit_flush<GUARD>(S, nrec, tot, L.F, words, dbg, rid, err);
+              (FL2 ? emit_flush2<GUARD> : emit_flush<GUARD>)(S, nrec, tot, L.F, words, dbg, rid, err);
               __builtin_amdgcn_wave_barrier();
               __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
               nrec = 0; tot = 0;
@@ -1279,7 +1346,7 @@ __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restri
     if (nrec > 0) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      emit_flush<GUARD>(S, nrec, tot, L.F, words, dbg, rid, err);
+      (FL2 ? emit_flush2<GUARD> : emit_flush<GUARD>)(S, nrec, tot, L.F, words, dbg, rid, err);
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
