@@ -116,6 +116,21 @@ class DeviceEvents:
         return DeviceEvents((off - e0).contiguous(), self.aid[e0:e1], self.ts[e0:e1], self.type[e0:e1],
                             self.file_bounds[f0:f1 + 1] - self.file_bounds[f0], s1 - s0, e1 - e0)
 
+    def subset_file_list(self, files) -> "DeviceEvents":
+        """Files `files` (any order, no repeats) as one device event set, one file per entry (columns copied)."""
+        import torch
+        parts = [self.subset_files(int(f), int(f) + 1) for f in files]
+        base, offs, fb = 0, [], [0]
+        for v in parts:
+            offs.append(v.offsets[:-1] + base)
+            base += v.n_events
+            fb.append(fb[-1] + v.n_sessions)
+        dev = self.offsets.device
+        offs.append(torch.tensor([base], dtype=torch.int64, device=dev))
+        cat = lambda k: torch.cat([getattr(v, k) for v in parts]) if parts else getattr(self, k)[:0].clone()
+        return DeviceEvents(torch.cat(offs).contiguous(), cat("aid"), cat("ts"), cat("type"), np.asarray(fb, np.int64),
+                            fb[-1], base)
+
     def abi(self) -> _lib.Events:
         e = _lib.Events()
         e.session_offsets = _lib.ptr(self.offsets)
@@ -405,9 +420,11 @@ def table_keys_at(table: CovisTable, name, use_ge2: bool, idx, stream=None) -> n
 
 
 def boundary_keys(events: DeviceEvents, name: str, plan, file_rows, use_ge2: bool, n_items: int, ctx=None) -> dict:
-    """{(file, row): key} for every part boundary of `plan` that falls inside a file: the file is
-    counted alone (its per-file table, as count_co_events.py:94 writes it) and the key of that row
-    of its (aid, aid_next)-ordered (use_ge2: count >= 2) rows is read."""
+    """{(file, row): key} for every part boundary of `plan` that falls inside a file: the key of that row of
+    the file's own (aid, aid_next)-ordered (use_ge2: count >= 2) table, as count_co_events.py:94 writes it.
+    The boundary files are counted together, one part per file (ottohip_covis_count_parts: rows carry
+    their file's part), where the part machinery applies (n_items < 2^24, < 255 files); else each file
+    alone."""
     need = {}
     for fa, lo, fb, hi in plan:
         if lo > 0:
@@ -415,6 +432,20 @@ def boundary_keys(events: DeviceEvents, name: str, plan, file_rows, use_ge2: boo
         if hi < int(file_rows[fb]):
             need.setdefault(fb, set()).add(hi)
     out = {}
+    files = sorted(need)
+    if files and n_items <= (1 << 24) and len(files) <= 254:
+        sub = events.subset_file_list(files)
+        t = count_co_events_parts(sub, name, np.arange(len(files), dtype=np.int32), [], len(files), n_items, ctx=ctx)
+        lib = _lib.load()
+        for p, f in enumerate(files):
+            rows = np.ascontiguousarray(sorted(need[f]), np.int64)
+            keys = np.zeros(len(rows), np.uint64)
+            _lib.check(lib.ottohip_table_keys_at(t.ctx.h, t.h, p, 1 if use_ge2 else 0, rows.ctypes.data, len(rows),
+                                                 keys.ctypes.data, _lib.stream_handle(None)))
+            for r, k in zip(rows.tolist(), keys.tolist()):
+                out[(f, r)] = int(k)
+        t.free()
+        return out
     for f, rows in sorted(need.items()):
         rows = sorted(rows)
         t = count_co_events_fused(events.subset_files(f, f + 1), [name], n_items=n_items, ctx=ctx)

@@ -2745,8 +2745,10 @@ __global__ __launch_bounds__(256) void k_ph_hist(const uint8_t* __restrict__ rul
   }
 }
 // tie histograms of stage `st` (1: aid of the v == c* rows, 2: aid_next of the v == c*, aid == a* rows). Four
-// consecutive slots per thread (vector loads: one-byte loads per slot left the kernel address-bound); equal
-// (part, key) among a thread's slots (one row's slots are in aid order) take one atomic.
+// consecutive slots per thread (vector loads: one-byte loads per slot left the kernel address-bound). The slots
+// of one row sit together in aid order, so a stage-1 key repeats over thousands of slots: per slot column j the
+// wave's lanes (slots i0 + 4 l + j) are grouped by part, and per part one atomic per run of equal keys adds the
+// run's length (one atomic per slot serialised on the hot rows' counters).
 __global__ void k_ph_tie_hist(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a, const int32_t* __restrict__ b,
                               const uint32_t* __restrict__ c, const uint32_t* __restrict__ c2, int64_t n, int n_parts,
                               int use_ge2, PartCut pc_arg, int st, int64_t n_items, uint32_t* __restrict__ h) {
@@ -2754,38 +2756,59 @@ __global__ void k_ph_tie_hist(const uint8_t* __restrict__ rule, const int32_t* _
   __shared__ PartCut pc;
   if (threadIdx.x == 0) pc = pc_arg;
   __syncthreads();
-  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += (int64_t)gridDim.x * blockDim.x * 4) {
-    const uint32_t r4 = ld_rule4(rule, i, n);
-    if (r4 == 0xFFFFFFFFu) continue;
-    const uint4 v4 = ld_u4(use_ge2 ? c2 : c, i, n);
-    uint32_t tie = 0;
+  const int l = (int)lane_id();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  for (int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63)) * 4; i0 < n; i0 += stride) {  // wave-uniform
+    const int64_t i = i0 + 4 * l;
+    uint32_t r4 = 0xFFFFFFFFu, tie = 0;
+    uint4 v4 = make_uint4(0u, 0u, 0u, 0u), a4 = v4, b4 = v4;
+    if (i < n) {
+      r4 = ld_rule4(rule, i, n);
+      if (r4 != 0xFFFFFFFFu) {
+        v4 = ld_u4(use_ge2 ? c2 : c, i, n);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t p = (r4 >> (8 * j)) & 0xFFu;
-      tie |= (p < (uint32_t)n_parts && pc.stage[p] == (uint32_t)st && u4_at(v4, j) == pc.cstar[p] ? 1u : 0u) << j;
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t p = (r4 >> (8 * j)) & 0xFFu;
+          tie |= (p < (uint32_t)n_parts && pc.stage[p] == (uint32_t)st && u4_at(v4, j) == pc.cstar[p] ? 1u : 0u) << j;
+        }
+        if (tie) {
+          a4 = ld_u4(reinterpret_cast<const uint32_t*>(a), i, n);
+          if (st == 2) b4 = ld_u4(reinterpret_cast<const uint32_t*>(b), i, n);
+        }
+      }
     }
-    if (!tie) continue;
-    const uint4 a4 = ld_u4(reinterpret_cast<const uint32_t*>(a), i, n);
-    uint4 b4 = make_uint4(0u, 0u, 0u, 0u);
-    if (st == 2) b4 = ld_u4(reinterpret_cast<const uint32_t*>(b), i, n);
-    uint64_t cur = ~0ull;
-    uint32_t cnt = 0;
+    if (!__ballot(tie != 0u)) continue;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      uint64_t key = ~0ull;
+      uint32_t p = 0xFFFFFFFFu, key = 0;
+      bool tj = false;
       if ((tie >> j) & 1u) {
-        const uint32_t p = (r4 >> (8 * j)) & 0xFFu, ai = u4_at(a4, j);
-        if (st == 1) key = (uint64_t)p * n_items + ai;
-        else if (ai == pc.astar[p]) key = (uint64_t)p * n_items + u4_at(b4, j);
+        p = (r4 >> (8 * j)) & 0xFFu;
+        const uint32_t ai = u4_at(a4, j);
+        if (st == 1) { tj = true; key = ai; }
+        else if (ai == pc.astar[p]) { tj = true; key = u4_at(b4, j); }
       }
-      if (key == ~0ull) continue;
-      if (key != cur) {
-        if (cnt) atomicAdd(&h[cur], cnt);
-        cur = key; cnt = 0;
+      uint64_t pend = __ballot(tj);
+      while (pend) {
+        const int f = __ffsll((long long)pend) - 1;
+        const uint32_t pf = (uint32_t)__shfl((int)p, f);
+        const uint64_t mp = __ballot(tj && p == pf);
+        pend &= ~mp;
+        const bool in = (mp >> l) & 1ull;
+        const uint64_t below = mp & ((1ull << l) - 1ull);
+        const int prv = below ? 63 - __clzll((long long)below) : l;
+        const uint32_t kprev = (uint32_t)__shfl((int)key, prv);
+        const bool head = in && (!below || kprev != key);
+        const uint64_t hm = __ballot(head);
+        if (head) {
+          const uint64_t above = hm & ~((2ull << l) - 1ull);
+          const int nh = above ? __ffsll((long long)above) - 1 : 64;
+          const uint64_t upto = nh == 64 ? ~0ull : ((1ull << nh) - 1ull);
+          const uint32_t cnt = (uint32_t)__popcll(mp & upto & ~((1ull << l) - 1ull));
+          atomicAdd(&h[(uint64_t)pf * n_items + key], cnt);
+        }
       }
-      ++cnt;
     }
-    if (cnt) atomicAdd(&h[cur], cnt);
   }
 }
 // smallest index j with incl[j] >= need (incl = inclusive prefix of one part's histogram)
