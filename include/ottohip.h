@@ -338,11 +338,6 @@ int ottohip_kmeans_lloyd_iter(ottohip_ctx* ctx, const float* X, int64_t n, int d
 int ottohip_kmeans_lloyd_steps(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* centroids, int k,
                                int32_t* labels, int64_t* sums, int64_t* counts, int max_steps, double tol,
                                double* out, void* stream);
-/* Splits the rows of X once into the bf16 hi / lo pieces and squared norms the split-precision E-step of
- * lloyd_steps otherwise computes at every step (same values: labels, sums and stop checks unchanged); the
- * context keeps them for this X (pointer, n, dim) until the next prepare or ottohip_ctx_trim. The caller
- * re-prepares (or passes X = NULL to drop them) before X's contents change. */
-int ottohip_kmeans_prepare(ottohip_ctx* ctx, const float* X, int64_t n, int dim, void* stream);
 /* lloyd_steps for TWO independent runs (two n_init runs of :152-159) in lockstep: one read of X per step
  * scores both (the step is bound by the X stream). centroids / labels / sums / counts are HOST arrays
  * of the two runs' device pointers, max_steps (HOST int[2]) the step budget of each run (0: the run sits

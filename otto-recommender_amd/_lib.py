@@ -122,7 +122,6 @@ SIGNATURES = {
     "ottohip_kmeans_lloyd_steps_pair": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP, ctypes.c_int, _VP, _VP,
                                                        _VP, _VP, ctypes.c_double, ctypes.POINTER(ctypes.c_double),
                                                        _VP]),
-    "ottohip_kmeans_prepare": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP]),
     "ottohip_kmeans_lloyd_steps_multi": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP, ctypes.c_int, _VP, _VP,
                                                         _VP, _VP, ctypes.c_int, ctypes.c_double,
                                                         ctypes.POINTER(ctypes.c_double), _VP]),

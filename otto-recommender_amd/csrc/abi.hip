@@ -825,7 +825,6 @@ int ottohip_ctx_trim(ottohip_ctx* ctx) {
   ctx->spare.release();
   dev_trim();
   ctx->km_bvalid = false;  // the KMeans distance bounds lived in the released workspace
-  ctx->km_hlX = nullptr;   // so did the prepared KMeans rows
   return 0;
 }
 

@@ -124,11 +124,6 @@ struct Ctx {
   int64_t km_bn = -1;
   int km_bdim = 0, km_bk = 0;
   bool km_bvalid = false;
-  // KMeans rows split into bf16 hi / lo pieces + squared norms (ottohip_kmeans_prepare, workspace "km_xhl" /
-  // "km_xsq"), valid for the X of the last prepare call until the next prepare or trim
-  const void* km_hlX = nullptr;
-  int64_t km_hln = -1;
-  int km_hldim = 0;
 };
 
 inline int bits_for(uint64_t n_values) {  // bits needed to store values in [0, n_values)

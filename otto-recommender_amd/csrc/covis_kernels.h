@@ -2746,17 +2746,32 @@ __global__ __launch_bounds__(256) void k_ph_hist(const uint8_t* __restrict__ rul
 }
 // tie histograms of stage `st` (1: aid of the v == c* rows, 2: aid_next of the v == c*, aid == a* rows). Four
 // consecutive slots per thread (vector loads: one-byte loads per slot left the kernel address-bound). The slots
-// of one row sit together in aid order, so a stage-1 key repeats over thousands of slots: per slot column j the
-// wave's lanes (slots i0 + 4 l + j) are grouped by part, and per part one atomic per run of equal keys adds the
-// run's length (one atomic per slot serialised on the hot rows' counters).
-__global__ void k_ph_tie_hist(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a, const int32_t* __restrict__ b,
-                              const uint32_t* __restrict__ c, const uint32_t* __restrict__ c2, int64_t n, int n_parts,
-                              int use_ge2, PartCut pc_arg, int st, int64_t n_items, uint32_t* __restrict__ h) {
+// of one row sit together in aid order and the parts' rows interleave inside it, so a stage-1 key repeats over
+// thousands of slots: each wave keeps per-part counts of its current key in LDS and adds them to the histogram
+// once the key changes (one device atomic per (part, key) per wave instead of one per run of equal keys, which
+// serialised on the hot rows' counters); slot columns whose tie lanes hold other keys take the per-run atomics.
+__global__ __launch_bounds__(256) void k_ph_tie_hist(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
+                                                     const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
+                                                     const uint32_t* __restrict__ c2, int64_t n, int n_parts,
+                                                     int use_ge2, PartCut pc_arg, int st, int64_t n_items,
+                                                     uint32_t* __restrict__ h) {
   // the cut tables in LDS: indexing the kernel-argument copy by a lane's part went through scratch memory
   __shared__ PartCut pc;
+  __shared__ uint32_t wcnt[4][PH_MAXP];  // per wave: counts of its current key per part
+  const int l = (int)lane_id(), wv = threadIdx.x >> 6;
   if (threadIdx.x == 0) pc = pc_arg;
+  if (l < PH_MAXP) wcnt[wv][l] = 0;
   __syncthreads();
-  const int l = (int)lane_id();
+  uint32_t wkey = 0xFFFFFFFFu;  // wave-uniform
+  auto flush = [&]() {
+    if (wkey != 0xFFFFFFFFu && l < n_parts) {
+      const uint32_t x = wcnt[wv][l];
+      if (x) atomicAdd(&h[(uint64_t)l * n_items + wkey], x);
+      wcnt[wv][l] = 0;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  };
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
   for (int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63)) * 4; i0 < n; i0 += stride) {  // wave-uniform
     const int64_t i = i0 + 4 * l;
@@ -2788,7 +2803,23 @@ __global__ void k_ph_tie_hist(const uint8_t* __restrict__ rule, const int32_t* _
         if (st == 1) { tj = true; key = ai; }
         else if (ai == pc.astar[p]) { tj = true; key = u4_at(b4, j); }
       }
-      uint64_t pend = __ballot(tj);
+      const uint64_t tm = __ballot(tj);
+      if (!tm) continue;
+      const uint32_t k0 = (uint32_t)__shfl((int)key, __ffsll((long long)tm) - 1);
+      if (!__ballot(tj && key != k0)) {  // one key in this column: counted per part in LDS
+        if (k0 != wkey) { flush(); wkey = k0; }
+        uint64_t pend = tm;
+        while (pend) {
+          const uint32_t pf = (uint32_t)__shfl((int)p, __ffsll((long long)pend) - 1);
+          const uint64_t mp = __ballot(tj && p == pf);
+          pend &= ~mp;
+          if (l == 0) wcnt[wv][pf] += (uint32_t)__popcll(mp);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        continue;
+      }
+      uint64_t pend = tm;  // several keys: one atomic per run of equal keys per part
       while (pend) {
         const int f = __ffsll((long long)pend) - 1;
         const uint32_t pf = (uint32_t)__shfl((int)p, f);
@@ -2810,6 +2841,7 @@ __global__ void k_ph_tie_hist(const uint8_t* __restrict__ rule, const int32_t* _
       }
     }
   }
+  flush();
 }
 // smallest index j with incl[j] >= need (incl = inclusive prefix of one part's histogram)
 __global__ void k_ph_find(const uint64_t* __restrict__ excl, const uint32_t* __restrict__ h, int64_t n, uint64_t need,

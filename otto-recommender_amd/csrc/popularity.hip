@@ -591,10 +591,7 @@ __global__ __launch_bounds__(256) void k_km_filter(int64_t n, int k, const int32
 }
 
 // BL: score the rows erows[0, *n_eval) (k_km_filter's list) and rebuild their bounds
-// HL: the rows' bf16 hi / lo pieces and squared norms come precomputed (ottohip_kmeans_prepare: xhl[row][q][hi, lo]
-// for the 16-B pieces q = 2 s + h of dims 8 q .. 8 q + 7, xsq[row]) instead of being split from X at every step:
-// the same values, ~220 fewer VALU instructions per row tile (X itself is still read for the moved rows' sums)
-template <int NB, int KS, bool BL = false, bool HL = false>
+template <int NB, int KS, bool BL = false>
 __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __restrict__ X, int64_t n, int dim,
                                                              const float* __restrict__ C, const float* __restrict__ cn,
                                                              int k, int32_t* __restrict__ label,
@@ -607,9 +604,7 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
                                                              const uint32_t* __restrict__ erows = nullptr,
                                                              const unsigned long long* __restrict__ n_eval = nullptr,
                                                              float* __restrict__ ub = nullptr,
-                                                             float* __restrict__ lb = nullptr,
-                                                             const uint4* __restrict__ xhl = nullptr,
-                                                             const float* __restrict__ xsq = nullptr) {
+                                                             float* __restrict__ lb = nullptr) {
   if (gate && __builtin_amdgcn_readfirstlane(*gate)) return;
   extern __shared__ unsigned long long smem64[];
   uint4* Cf = reinterpret_cast<uint4*>(smem64);                               // [NB][KS][hi, lo][64]
@@ -646,33 +641,19 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
   const int64_t ntile = (nl + 31) >> 5;
   const int64_t nwv = (int64_t)gridDim.x * (KM_MT / 64);
   // the next tile's rows (and its rows' current labels) are loaded while this tile is scored
-  float4 raw[2 * KS];  // HL: the pieces' hi / lo bf16 words (as float4 bit patterns)
+  float4 raw[2 * KS];
   int32_t lab_n = -1;
-  float xs_n = 0.f;
   int64_t row_n = 0;
-  const int nqp = (dim + 7) >> 3;  // 16-B pieces per row in xhl
   auto load = [&](int64_t tt) __attribute__((always_inline)) {
     const int64_t ri = (tt << 5) + i32 < nl ? (tt << 5) + i32 : nl - 1;
     const int64_t rr = BL ? (int64_t)erows[ri] : ri;
     row_n = rr;
-    if constexpr (HL) {
-      const uint4* hp = xhl + rr * (int64_t)(2 * nqp);
+    const float* xp = X + rr * dim;
 #pragma unroll
-      for (int s_ = 0; s_ < KS; ++s_) {
-        const int q = 2 * s_ + h;
-        const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-        raw[2 * s_] = __builtin_bit_cast(float4, q < nqp ? hp[2 * q] : z);
-        raw[2 * s_ + 1] = __builtin_bit_cast(float4, q < nqp ? hp[2 * q + 1] : z);
-      }
-      xs_n = xsq[rr];
-    } else {
-      const float* xp = X + rr * dim;
-#pragma unroll
-      for (int s_ = 0; s_ < KS; ++s_) {
-        const int d0 = 16 * s_ + 8 * h;  // dim % 4 == 0: a 16-B piece is all in or all out
-        raw[2 * s_] = d0 < dim ? *reinterpret_cast<const float4*>(xp + d0) : make_float4(0.f, 0.f, 0.f, 0.f);
-        raw[2 * s_ + 1] = d0 + 4 < dim ? *reinterpret_cast<const float4*>(xp + d0 + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+    for (int s_ = 0; s_ < KS; ++s_) {
+      const int d0 = 16 * s_ + 8 * h;  // dim % 4 == 0: a 16-B piece is all in or all out
+      raw[2 * s_] = d0 < dim ? *reinterpret_cast<const float4*>(xp + d0) : make_float4(0.f, 0.f, 0.f, 0.f);
+      raw[2 * s_ + 1] = d0 + 4 < dim ? *reinterpret_cast<const float4*>(xp + d0 + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     lab_n = label[rr];
   };
@@ -684,29 +665,20 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
     const int64_t row = row_n;
     km_bf16x8 xh[KS], xl[KS];
     float xs = 0.f;
-    if constexpr (HL) {
 #pragma unroll
-      for (int s_ = 0; s_ < KS; ++s_) {
-        xh[s_] = __builtin_bit_cast(km_bf16x8, raw[2 * s_]);
-        xl[s_] = __builtin_bit_cast(km_bf16x8, raw[2 * s_ + 1]);
-      }
-      xs = xs_n;
-    } else {
+    for (int s_ = 0; s_ < KS; ++s_) {
+      const float4 p0 = raw[2 * s_], p1 = raw[2 * s_ + 1];
+      const float v[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
 #pragma unroll
-      for (int s_ = 0; s_ < KS; ++s_) {
-        const float4 p0 = raw[2 * s_], p1 = raw[2 * s_ + 1];
-        const float v[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
-#pragma unroll
-        for (int j = 0; j < 8; ++j) xs += v[j] * v[j];
-        uint4 hi, lo;
-        km_split8(v, hi, lo);
-        xh[s_] = __builtin_bit_cast(km_bf16x8, hi);
-        xl[s_] = __builtin_bit_cast(km_bf16x8, lo);
-      }
+      for (int j = 0; j < 8; ++j) xs += v[j] * v[j];
+      uint4 hi, lo;
+      km_split8(v, hi, lo);
+      xh[s_] = __builtin_bit_cast(km_bf16x8, hi);
+      xl[s_] = __builtin_bit_cast(km_bf16x8, lo);
     }
     const int32_t lab_cur = lab_n;
     if (t + nwv < ntile) load(t + nwv);
-    if (!HL) xs += __shfl_xor(xs, 32);
+    xs += __shfl_xor(xs, 32);
     km_f32x16 acc0 = {}, acc1 = {};
 #pragma unroll
     for (int s_ = 0; s_ < KS; ++s_) {
@@ -1051,48 +1023,6 @@ static bool km_mfma_ok(int k, int dim, const float* X, const float* C) {
          ((uintptr_t)C & 15) == 0;
 }
 
-// the rows of X split once per fit for k_km_assign_split<..., HL>: one thread per (row, half h) with the same
-// loads, split (km_split8) and norm accumulation order as the kernel's own per-step split, so the pieces and xsq
-// are bit-identical to what the kernel would compute (the halves' sums added lane h = 0 first, as its xor-shuffle)
-__global__ void k_km_split_rows(const float* __restrict__ X, int64_t n, int dim, int nqp, uint4* __restrict__ xhl,
-                                float* __restrict__ xsq) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t row = t >> 1;
-  const int h = (int)(t & 1);
-  const bool in = row < n;
-  const float* xp = X + (in ? row : 0) * dim;
-  float xs = 0.f;
-  for (int s_ = 0; 2 * s_ < nqp; ++s_) {
-    const int d0 = 16 * s_ + 8 * h;
-    const float4 p0 = in && d0 < dim ? *reinterpret_cast<const float4*>(xp + d0) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 p1 = in && d0 + 4 < dim ? *reinterpret_cast<const float4*>(xp + d0 + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float v[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
-#pragma unroll
-    for (int j = 0; j < 8; ++j) xs += v[j] * v[j];
-    uint4 hi, lo;
-    km_split8(v, hi, lo);
-    const int q = 2 * s_ + h;
-    if (in && q < nqp) {
-      xhl[row * (int64_t)(2 * nqp) + 2 * q] = hi;
-      xhl[row * (int64_t)(2 * nqp) + 2 * q + 1] = lo;
-    }
-  }
-  const float other = __shfl_xor(xs, 1);
-  if (in && h == 0) xsq[row] = xs + other;
-}
-
-// prepared rows of X (ctx cache) for the MFMA split E-step, or null
-static bool km_hl_for(Ctx* ctx, const float* X, int64_t n, int dim, const uint4** xhl, const float** xsq) {
-  const bool off = getenv("OTTOHIP_KM_PREP") && !strcmp(getenv("OTTOHIP_KM_PREP"), "0");  // A/B switch, read per call
-  if (off || ctx->km_hlX != X || ctx->km_hln != n || ctx->km_hldim != dim) return false;
-  uint4* a;
-  float* b;
-  if (ctx->ws.get("km_xhl", (size_t)n * 2 * ((dim + 7) / 8), &a) || ctx->ws.get("km_xsq", (size_t)n, &b)) return false;
-  *xhl = a;
-  *xsq = b;
-  return true;
-}
-
 // distance bounds in the batched Lloyd steps (OTTOHIP_KM_BOUNDS=0 / OTTOHIP_KM_SPLIT=0: A/B switches, read per call)
 static bool km_bounds_on(int64_t n) {
   const char* be = getenv("OTTOHIP_KM_BOUNDS");
@@ -1135,18 +1065,11 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
       // bounds >= 0 (batched steps): skip the rows whose distance bounds keep their label; 1 = the
       // bounds are not valid for these rows (every row scored, bounds rebuilt)
       const bool bl = bounds >= 0 && km_bounds_on(n);
-      // rows split once per fit (ottohip_kmeans_prepare) where prepared for this X
-      const uint4* xhl = nullptr;
-      const float* xsq = nullptr;
-      const bool hl = KS == 7 && km_hl_for(ctx, X, n, dim, &xhl, &xsq);
       auto sk = KS == 7 ? (NB == 1 ? k_km_assign_split<1, 7> : k_km_assign_split<2, 7>)
                         : (NB == 1 ? k_km_assign_split<1, 8> : k_km_assign_split<2, 8>);
       if (bl)
         sk = KS == 7 ? (NB == 1 ? k_km_assign_split<1, 7, true> : k_km_assign_split<2, 7, true>)
                      : (NB == 1 ? k_km_assign_split<1, 8, true> : k_km_assign_split<2, 8, true>);
-      if (hl)
-        sk = bl ? (NB == 1 ? k_km_assign_split<1, 7, true, true> : k_km_assign_split<2, 7, true, true>)
-                : (NB == 1 ? k_km_assign_split<1, 7, false, true> : k_km_assign_split<2, 7, false, true>);
       OH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(sk), hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)lds2));
       // one resident block per CU (the kernel's registers allow one 8-wave block): one round of blocks,
@@ -1178,10 +1101,10 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
                   ds[k / 10], dh[67]);
         }
         sk<<<(unsigned)ctx->n_cu, KM_MT, lds2, s>>>(X, n, dim, C, cn, k, labels, sums, cnt, changed, gate, amb, n_amb,
-                                                    erows, n_eval, ub, lb, xhl, xsq);
+                                                    erows, n_eval, ub, lb);
       } else {
         sk<<<sgrid, KM_MT, lds2, s>>>(X, n, dim, C, cn, k, labels, sums, cnt, changed, gate, amb, n_amb, nullptr, nullptr,
-                                     nullptr, nullptr, xhl, xsq);
+                                     nullptr, nullptr);
       }
       OH_HIP(hipGetLastError());
     }
@@ -1773,25 +1696,6 @@ int ottohip_kmeans_lloyd_iter(ottohip_ctx* ctx, const float* X, int64_t n, int d
 // split-precision pass plus the exact f32 kernel on its near ties (OTTOHIP_KM_SPLIT=0: the exact kernel on
 // every row; labels, sums and stop checks are identical): out[0] then holds the near ties' inertia only
 // (the run's inertia is ottohip_kmeans_inertia's).
-int ottohip_kmeans_prepare(ottohip_ctx* ctx, const float* X, int64_t n, int dim, void* stream) {
-  if (!ctx || n < 0 || (n > 0 && (!X || dim < 1 || dim > EMB_MAXD))) {
-    set_error("kmeans_prepare: bad arguments"); return OTTOHIP_EINVAL;
-  }
-  ctx->km_hlX = nullptr;  // X == NULL or n == 0: drop the prepared rows
-  if (!X || n == 0 || (dim & 3) || ((uintptr_t)X & 15)) return 0;  // shapes the split kernel's loads do not take
-  hipStream_t s = S(stream);
-  OH_HIP(hipSetDevice(ctx->device));
-  const int nqp = (dim + 7) / 8;
-  uint4* xhl;
-  float* xsq;
-  OH_TRY(ctx->ws.get("km_xhl", (size_t)n * 2 * nqp, &xhl));
-  OH_TRY(ctx->ws.get("km_xsq", (size_t)n, &xsq));
-  k_km_split_rows<<<grid_for(2 * n), 256, 0, s>>>(X, n, dim, nqp, xhl, xsq);
-  OH_HIP(hipGetLastError());
-  ctx->km_hlX = X; ctx->km_hln = n; ctx->km_hldim = dim;
-  return 0;
-}
-
 int ottohip_kmeans_lloyd_steps(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* centroids, int k,
                                int32_t* labels, int64_t* sums, int64_t* counts, int max_steps, double tol,
                                double* out, void* stream) {

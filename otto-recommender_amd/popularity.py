@@ -156,8 +156,6 @@ class KMeans:
         m1 = s1.cpu().numpy().astype(np.float64) / FX / n_all
         var = s2.cpu().numpy().astype(np.float64) / FX / n_all - m1 * m1
         tol_abs = float(np.mean(var)) * self.tol
-        if group is None:  # the rows split once into the E-step's bf16 pieces (dropped again below)
-            _lib.check(lib.ottohip_kmeans_prepare(ctx.h, _lib.ptr(Xc), n, dim, sh))
         seed_stream = _permutation_heads(self.random_state, n_all, k, self.n_init)
         sums = torch.empty(k * dim, dtype=torch.int64, device=dev)
         counts = torch.empty(k, dtype=torch.int64, device=dev)
@@ -236,8 +234,6 @@ class KMeans:
             if best is None or inertia < best[0]:
                 best = (inertia, C.clone(), labels[:n].clone(), it)
         seed_stream.close()
-        if group is None:
-            _lib.check(lib.ottohip_kmeans_prepare(ctx.h, None, 0, 0, sh))
         self.inertia_, C, self.labels_, self.n_iter_ = best
         self.cluster_centers_ = C + mean_d
         return self

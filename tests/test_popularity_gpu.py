@@ -143,28 +143,6 @@ def test_kmeans_split_precision_steps_equal_exact_steps(gpu, monkeypatch, case):
         assert fits[0][2] == f[2] and fits[0][3] == f[3]
 
 
-@pytest.mark.parametrize("bounds", ["1", "0"])
-def test_kmeans_prepared_rows_equal_per_step_split(gpu, monkeypatch, bounds):
-    """ottohip_kmeans_prepare (the rows split once into the E-step's bf16 hi / lo pieces and squared norms) gives
-    bit-identical labels, centres, inertia and iterations to the split computed at every step (OTTOHIP_KM_PREP=0):
-    k = 50 on session embeddings (the config-5 clustering), with and without distance bounds."""
-    from otto_recommender_amd import popularity as gp
-    ev = synth.generate(30_000, first_session=4242)
-    words = np.unique(ev.aid)
-    emb = synth.embeddings(len(words), seed=1)
-    X = gp.compute_sessions_embeddings(ev.session_offsets, ev.aid, ev.ts, ev.type, words, emb).cpu().numpy()
-    monkeypatch.setenv("OTTOHIP_KM_GROUP", "1")
-    monkeypatch.setenv("OTTOHIP_KM_BOUNDS", bounds)
-    fits = []
-    for prep in ("0", "1"):
-        monkeypatch.setenv("OTTOHIP_KM_PREP", prep)
-        km = gp.KMeans(n_clusters=50, random_state=42, n_init=2).fit(X)
-        fits.append((km.labels_.cpu().numpy(), km.cluster_centers_.cpu().numpy(), km.inertia_, km.n_iter_))
-    np.testing.assert_array_equal(fits[0][0], fits[1][0])
-    np.testing.assert_array_equal(fits[0][1], fits[1][1])
-    assert fits[0][2] == fits[1][2] and fits[0][3] == fits[1][3]
-
-
 @pytest.mark.parametrize("case", ["sessions_k50", "relocation_k40", "blocks_k33"])
 def test_kmeans_lockstep_equals_single_runs(gpu, monkeypatch, case):
     """n_init runs in lockstep over one read of X per Lloyd step (ottohip_kmeans_lloyd_steps_multi, groups of
