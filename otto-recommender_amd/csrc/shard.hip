@@ -103,6 +103,13 @@ __global__ void k_rec_row_key(const uint4* __restrict__ rec, const uint32_t* __r
 
 __device__ __forceinline__ uint64_t rec_key(const uint4& r) { return ((uint64_t)r.x << 32) | r.y; }
 
+// *unsorted = 1 when some record's (rule, aid) is below its predecessor's (records in (rule, aid) order, as the
+// part heads leave them in table slot order, need only the stable sort by aid_next: equal keys end up adjacent)
+__global__ void k_rec_order_check(const uint4* __restrict__ rec, int64_t n, int* __restrict__ unsorted) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
+  if (i < n && rec[i].x < rec[i - 1].x) *unsorted = 1;
+}
+
 // one random-read pass: records in key order (everything after it streams)
 __global__ void k_rec_gather(const uint4* __restrict__ rec, const uint32_t* __restrict__ perm, int64_t n,
                              uint4* __restrict__ out, uint32_t* __restrict__ head) {
@@ -254,12 +261,22 @@ int ottohip_table_from_records(ottohip_ctx* ctx, const void* records, int64_t n,
   int ph = ctx->begin("merge_sort", s, 16.0 * n);
   if (hipMemsetAsync(err, 0, sizeof(int), s) || hipMemsetAsync(stats, 0, MAX_RULES * 4 * 8, s)) return fail(OTTOHIP_EHIP);
   k_rec_next_key<<<grid_for(n), 256, 0, s>>>(rec, n, k0, v0, err, (uint32_t)n_items, n_rules);
+  // records already in (rule, aid) order skip the second sort (their slots end in (aid_next, rule, aid) order;
+  // the readers of a table do not depend on its slot order)
+  int* unsorted;
+  if ((rc = ws.get("mg_unsorted", 1, &unsorted))) return fail(rc);
+  if (hipMemsetAsync(unsorted, 0, sizeof(int), s)) return fail(OTTOHIP_EHIP);
+  k_rec_order_check<<<grid_for(n), 256, 0, s>>>(rec, n, unsorted);
+  int huns = 1;
+  if ((rc = d2h(&huns, unsorted, 1, s))) return fail(rc);
   uint32_t *k = k0, *v = v0;
   if ((rc = radix_sort_pairs(ctx, k, v, k1, v1, n, A, s))) return fail(rc);
-  uint32_t* kn = (k == k0) ? k1 : k0;
-  k_rec_row_key<<<grid_for(n), 256, 0, s>>>(rec, v, n, A, kn);
-  k = kn;
-  if ((rc = radix_sort_pairs(ctx, k, v, k == k0 ? k1 : k0, v == v0 ? v1 : v0, n, A + RB, s))) return fail(rc);
+  if (huns) {
+    uint32_t* kn = (k == k0) ? k1 : k0;
+    k_rec_row_key<<<grid_for(n), 256, 0, s>>>(rec, v, n, A, kn);
+    k = kn;
+    if ((rc = radix_sort_pairs(ctx, k, v, k == k0 ? k1 : k0, v == v0 ? v1 : v0, n, A + RB, s))) return fail(rc);
+  }
   ctx->end(ph, s);
   ph = ctx->begin("merge_reduce", s, 16.0 * n);
   uint4* srt;
