@@ -532,8 +532,11 @@ __global__ __launch_bounds__(64) void k_prep_count(const int64_t* __restrict__ o
         int run = -1;
         for (int q = 0; q < sR.n_of_type[t]; ++q) {
           const int r = sR.rule_of_type[t][q];
-          const int jb = lds_lower_ts(S.key, lo, hi, tsi + sR.lo[r]);
-          const int je = lds_upper_ts(S.key, jb, hi, tsi + sR.hi[r]);
+          // a window around dt = 0 ends at or after the event and starts at or before it (the session is in ts
+          // order): each search takes one side of the event
+          const bool around = sR.lo[r] <= 0 && sR.hi[r] >= 0;
+          const int jb = lds_lower_ts(S.key, lo, around ? idx : hi, tsi + sR.lo[r]);
+          const int je = lds_upper_ts(S.key, around ? idx + 1 : jb, hi, tsi + sR.hi[r]);
           if (je <= jb) continue;
           uint32_t m = 0;
           if (rule_sym(sR, r)) {
@@ -1260,10 +1263,13 @@ __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restri
           uint32_t len = 0, jb = 0, xlo = EB_NONE, xlen = 0;
           if (act) {
             const int a = S.sb[tt][k], e = S.sb[tt + 1][k];
-            jb = (uint32_t)lds_lower_ts(S.tev, a, e, tsi + lo);
-            const uint32_t je = (uint32_t)lds_upper_ts(S.tev, (int)jb, e, tsi + hi);
+            // own list with a window around dt = 0: the lower bound lies at or before the event's own run and the
+            // upper bound at or after it (the list is in ts order), so each search takes half of the list
+            const bool own = tt == t && lo <= 0 && hi >= 0;
+            jb = (uint32_t)lds_lower_ts(S.tev, a, own ? (int)rlo : e, tsi + lo);
+            const uint32_t je = (uint32_t)lds_upper_ts(S.tev, own ? (int)rhi : (int)jb, e, tsi + hi);
             len = je - jb;
-            if (tt == t && lo <= 0 && hi >= 0) { xlo = rlo; xlen = rhi - rlo; len -= xlen; }
+            if (own) { xlo = rlo; xlen = rhi - rlo; len -= xlen; }
           }
           const uint64_t m = __ballot(len > 0);
           const int nn = (int)__popcll(m);
