@@ -1000,7 +1000,7 @@ int ottohip_covis_count_parts(ottohip_ctx* ctx, const ottohip_events* ev, const 
   unsigned long long* ph;
   if ((rc = ctx->ws.get("part_hist", 512, &ph))) return fail(rc);
   OH_HIP(hipMemsetAsync(ph, 0, 512 * 8, s));
-  k_rule_hist<<<(unsigned)std::min<int64_t>(ceil_div((int64_t)T->n_slots, 256), (int64_t)ctx->n_cu * 8), 256, 0, s>>>(
+  k_rule_hist<<<(unsigned)std::min<int64_t>(ceil_div((int64_t)T->n_slots, 256 * SLOTS_T), (int64_t)ctx->n_cu * 8), 256, 0, s>>>(
       T->b.rule, T->b.count, T->n_slots, ph, ph + 256);
   OH_HIP(hipGetLastError());
   std::vector<unsigned long long> hh(512);
@@ -1301,7 +1301,7 @@ extern "C" int ottohip_table_part_heads(ottohip_ctx* ctx, const ottohip_table* t
   Workspace& ws = ctx->ws;
   const int64_t n = t->n_slots;
   const uint32_t thr = (uint32_t)std::max<int32_t>(min_count, 1);
-  const unsigned sgrid = (unsigned)std::min<int64_t>(ceil_div(n, 256), (int64_t)ctx->n_cu * 16);
+  const unsigned sgrid = (unsigned)std::min<int64_t>(ceil_div(n, 256 * SLOTS_T), (int64_t)ctx->n_cu * 16);
   // (1) v histogram per part
   unsigned long long* hist;
   OH_TRY(ws.get("ph_hist", (size_t)n_parts * PH_VBINS, &hist));
@@ -1330,26 +1330,58 @@ extern "C" int ottohip_table_part_heads(ottohip_ctx* ctx, const ottohip_table* t
   }
   const int64_t ni = t->n_items;
   if (n_tie) {
-    uint32_t *th, *found;
-    uint64_t* ex;
+    // stage 1 (a*): rank search over the parts' tie rows in slot order (= aid order)
+    const int64_t nb1 = ceil_div(n, FIN_B);
+    PhRank rk;
+    memset(&rk, 0, sizeof rk);
+    int nq = 0;
+    for (int p = 0; p < n_parts; ++p)
+      if (pc.stage[p] == 1u) { rk.need[nq] = need[p]; rk.part[nq] = (uint32_t)p; ++nq; }
+    uint32_t *rcnt, *found, *astar;
+    uint64_t* rex;
+    OH_TRY(ws.get("ph_rank_cnt", (size_t)nq * nb1, &rcnt));
+    OH_TRY(ws.get("ph_rank_ex", (size_t)nq * nb1, &rex));
+    OH_TRY(ws.get("ph_found", 2 * PH_MAXP, &found));
+    OH_TRY(ws.get("ph_astar", PH_MAXP, &astar));
+    k_ph_rank_count<<<(unsigned)nb1, FIN_T, 0, s>>>(t->b.rule, t->b.count, t->b.count_ge2, n, n_parts, use_ge2, pc, nb1,
+                                                     rcnt);
+    OH_TRY(exclusive_scan_u32(ctx, rcnt, rex, nq * nb1, nullptr, s));
+    OH_HIP(hipMemsetAsync(found, 0xFF, 2 * PH_MAXP * 4, s));
+    OH_HIP(hipMemsetAsync(astar, 0xFF, PH_MAXP * 4, s));
+    k_ph_find_multi<<<grid_for(nq * nb1), 256, 0, s>>>(rex, rcnt, nb1, nq, rk, found);
+    k_ph_tie_pick<<<(unsigned)nq, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.count, t->b.count_ge2, n, n_parts, use_ge2, pc,
+                                                  rk, found, astar);
+    uint32_t as[PH_MAXP];
+    OH_TRY(d2h(as, astar, (size_t)nq, s));
+    for (int q = 0; q < nq; ++q) {
+      const int p = (int)rk.part[q];
+      if (as[q] == 0xFFFFFFFFu) { set_error("table_part_heads: tie cut not found (part %d)", p); return OTTOHIP_EHIP; }
+      pc.astar[p] = as[q];
+      pc.stage[p] = 2;
+    }
+    // stage 2 (n*): aid_next histogram of the (c*, a*) tie rows; the rank left = need - ties with aid < a*
+    uint32_t* th;
+    uint64_t *ex, *lt;
     OH_TRY(ws.get("ph_tie", (size_t)n_parts * ni, &th));
     OH_TRY(ws.get("ph_tie_ex", (size_t)ni, &ex));
-    OH_TRY(ws.get("ph_found", 2, &found));
-    for (int st = 1; st <= 2; ++st) {
-      OH_HIP(hipMemsetAsync(th, 0, (size_t)n_parts * ni * 4, s));
-      k_ph_tie_hist<<<sgrid, 256, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n, n_parts,
-                                          use_ge2, pc, st, ni, th);
-      for (int p = 0; p < n_parts; ++p) {
-        if (pc.stage[p] != (uint32_t)st) continue;
-        OH_TRY(exclusive_scan_u32(ctx, th + (size_t)p * ni, ex, ni, nullptr, s));
-        OH_HIP(hipMemsetAsync(found, 0xFF, 8, s));
-        k_ph_find<<<grid_for(ni), 256, 0, s>>>(ex, th + (size_t)p * ni, ni, need[p], found);
-        uint32_t fr[2];
-        OH_TRY(d2h(fr, found, 2, s));
-        if (fr[0] == 0xFFFFFFFFu) { set_error("table_part_heads: tie cut not found (part %d)", p); return OTTOHIP_EHIP; }
-        if (st == 1) { pc.astar[p] = fr[0]; need[p] = fr[1]; pc.stage[p] = 2; }
-        else { pc.nstar[p] = fr[0]; pc.stage[p] = 3; }
-      }
+    OH_TRY(ws.get("ph_lt", PH_MAXP, &lt));
+    OH_HIP(hipMemsetAsync(th, 0, (size_t)n_parts * ni * 4, s));
+    OH_HIP(hipMemsetAsync(lt, 0, PH_MAXP * 8, s));
+    k_ph_tie_hist2<<<sgrid, 256, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n, n_parts,
+                                         use_ge2, pc, ni, th, reinterpret_cast<unsigned long long*>(lt));
+    uint64_t lth[PH_MAXP];
+    OH_TRY(d2h(lth, lt, PH_MAXP, s));
+    for (int p = 0; p < n_parts; ++p) {
+      if (pc.stage[p] != 2u) continue;
+      if (lth[p] >= need[p]) { set_error("table_part_heads: tie rank below the cut aid (part %d)", p); return OTTOHIP_EHIP; }
+      OH_TRY(exclusive_scan_u32(ctx, th + (size_t)p * ni, ex, ni, nullptr, s));
+      OH_HIP(hipMemsetAsync(found, 0xFF, 8, s));
+      k_ph_find<<<grid_for(ni), 256, 0, s>>>(ex, th + (size_t)p * ni, ni, need[p] - lth[p], found);
+      uint32_t fr[2];
+      OH_TRY(d2h(fr, found, 2, s));
+      if (fr[0] == 0xFFFFFFFFu) { set_error("table_part_heads: tie cut not found (part %d)", p); return OTTOHIP_EHIP; }
+      pc.nstar[p] = fr[0];
+      pc.stage[p] = 3;
     }
   }
   // (2) kept rows of every part -> records

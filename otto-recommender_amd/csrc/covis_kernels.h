@@ -2557,15 +2557,9 @@ __global__ __launch_bounds__(LDS_T) void k_agg_lds(const Task* __restrict__ task
 // once (aid <= aid_next); a kept row with aid != aid_next stands for itself and its mirror
 // (aid_next, aid), written right after it.
 constexpr int FIN_T = 256, FIN_PER = 16, FIN_B = FIN_T * FIN_PER;
-__device__ __forceinline__ bool blk_keep(const uint8_t* __restrict__ rule, const uint32_t* __restrict__ c,
-                                         const uint32_t* __restrict__ c2, int64_t i, int r, int use_ge2,
-                                         uint32_t thr) {
-  if (rule[i] != (uint8_t)r) return false;
-  return thr == 0 || (use_ge2 ? c2[i] : c[i]) >= thr;
-}
 // Slot scans read 4 consecutive slots per thread (slot arrays are 16-B aligned and i % 4 == 0): the rule
 // bytes as one u32, a u32 column as one uint4 (one-byte / one-word loads per slot ran at a third of HBM
-// bandwidth). Past n: rule 0xFF (no row). A block's FIN_B slots are FIN_PER / 4 rounds of 4 * FIN_T.
+// bandwidth). Past n: rule 0xFF (no row). A block's FIN_B slots are 16 consecutive slots per thread.
 __device__ __forceinline__ uint32_t ld_rule4(const uint8_t* __restrict__ rule, int64_t i, int64_t n) {
   if (i + 4 <= n) return *reinterpret_cast<const uint32_t*>(rule + i);
   uint32_t r = 0xFFFFFFFFu;
@@ -2589,27 +2583,62 @@ __device__ __forceinline__ uint32_t rule4_match(uint32_t r4, uint32_t r) {
   for (int j = 0; j < 4; ++j) m |= (((r4 >> (8 * j)) & 0xFFu) == r ? 1u : 0u) << j;
   return m;
 }
-// kept slots of the 4 at i (bit mask) and their mirrored rows (bit mask), per blk_keep
-__device__ __forceinline__ void blk_keep4(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
-                                          const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
-                                          const uint32_t* __restrict__ c2, int64_t i, int64_t n, int r, int use_ge2,
-                                          uint32_t thr, int sym, uint32_t& keep, uint32_t& mir, uint4& A, uint4& B,
-                                          uint4& V, uint4& G, bool want_g) {
-  keep = rule4_match(ld_rule4(rule, i, n), (uint32_t)r);
-  mir = 0;
+// 16 consecutive slots per thread (i % 16 == 0): the rule bytes as one uint4, then the u32 columns of the
+// 4-slot groups that hold a candidate as up to 4 independent uint4 loads. Four slots per thread left the
+// scans latency-bound (rule -> column -> aid chain per 4 slots: about a fifth of HBM bandwidth).
+constexpr int SLOTS_T = 16;
+static_assert(FIN_B == FIN_T * SLOTS_T, "a finalize block is one 16-slot run per thread");
+__device__ __forceinline__ uint4 ld_rule16(const uint8_t* __restrict__ rule, int64_t i, int64_t n) {
+  if (i + 16 <= n) return *reinterpret_cast<const uint4*>(rule + i);
+  return make_uint4(ld_rule4(rule, i, n), ld_rule4(rule, i + 4, n), ld_rule4(rule, i + 8, n), ld_rule4(rule, i + 12, n));
+}
+__device__ __forceinline__ uint32_t rule_at(const uint4& R, int s) { return (u4_at(R, s >> 2) >> (8 * (s & 3))) & 0xFFu; }
+struct Slots16 {
+  uint4 V[4], A[4], B[4], G[4];
+  __device__ __forceinline__ uint32_t v(int s) const { return u4_at(V[s >> 2], s & 3); }
+  __device__ __forceinline__ uint32_t a(int s) const { return u4_at(A[s >> 2], s & 3); }
+  __device__ __forceinline__ uint32_t b(int s) const { return u4_at(B[s >> 2], s & 3); }
+  __device__ __forceinline__ uint32_t g(int s) const { return u4_at(G[s >> 2], s & 3); }
+};
+// loads column `col` for the 4-slot groups with a bit in mask
+__device__ __forceinline__ void ld_groups(const uint32_t* __restrict__ col, int64_t i, int64_t n, uint32_t mask,
+                                          uint4 (&X)[4]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) X[g] = ((mask >> (4 * g)) & 15u) ? ld_u4(col, i + 4 * g, n) : make_uint4(0u, 0u, 0u, 0u);
+}
+// blk_keep over the 16 slots at i: keep / mir bit masks (bit s = slot i + s); V always loaded for kept
+// groups when `out`, A / B when `out` or sym (the mirror test), G when want_g
+__device__ __forceinline__ void blk_keep16(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
+                                           const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
+                                           const uint32_t* __restrict__ c2, int64_t i, int64_t n, int r, int use_ge2,
+                                           uint32_t thr, int sym, bool out, bool want_g, uint32_t& keep,
+                                           uint32_t& mir, Slots16& S) {
+  const uint4 R = ld_rule16(rule, i, n);
+  keep = 0; mir = 0;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) keep |= rule4_match(u4_at(R, g), (uint32_t)r) << (4 * g);
   if (!keep) return;
-  V = ld_u4(use_ge2 ? c2 : c, i, n);
-  if (want_g) G = use_ge2 ? V : ld_u4(c2, i, n);
+  if (thr || out) ld_groups(use_ge2 ? c2 : c, i, n, keep, S.V);
+  if (want_g) {
+    if (use_ge2) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) S.G[g] = S.V[g];
+    } else {
+      ld_groups(c2, i, n, keep, S.G);
+    }
+  }
   if (thr) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) keep &= ~((u4_at(V, j) < thr ? 1u : 0u) << j);
+    for (int s = 0; s < 16; ++s) keep &= ~((S.v(s) < thr ? 1u : 0u) << s);
+    if (!keep) return;
   }
-  if (!keep) return;
-  A = ld_u4(reinterpret_cast<const uint32_t*>(a), i, n);
-  B = ld_u4(reinterpret_cast<const uint32_t*>(b), i, n);
+  if (out || sym) {
+    ld_groups(reinterpret_cast<const uint32_t*>(a), i, n, keep, S.A);
+    ld_groups(reinterpret_cast<const uint32_t*>(b), i, n, keep, S.B);
+  }
   if (sym) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) mir |= (((keep >> j) & 1u) && u4_at(A, j) != u4_at(B, j) ? 1u : 0u) << j;
+    for (int s = 0; s < 16; ++s) mir |= (((keep >> s) & 1u) && S.a(s) != S.b(s) ? 1u : 0u) << s;
   }
 }
 __global__ __launch_bounds__(FIN_T) void k_blk_count(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
@@ -2617,16 +2646,13 @@ __global__ __launch_bounds__(FIN_T) void k_blk_count(const uint8_t* __restrict__
                                                      const uint32_t* __restrict__ c2, int64_t n, int r, int use_ge2,
                                                      uint32_t thr, int sym, uint32_t* __restrict__ bcnt) {
   __shared__ uint32_t wt[FIN_T / 64];
-  const int64_t base = (int64_t)blockIdx.x * FIN_B;
+  const int64_t i = (int64_t)blockIdx.x * FIN_B + (int64_t)threadIdx.x * SLOTS_T;
   uint32_t k = 0;
-#pragma unroll
-  for (int q = 0; q < FIN_PER / 4; ++q) {
-    const int64_t i = base + ((int64_t)q * FIN_T + threadIdx.x) * 4;
-    if (i >= n) break;
+  if (i < n) {
     uint32_t keep, mir;
-    uint4 A, B, V, G;
-    blk_keep4(rule, a, b, c, c2, i, n, r, use_ge2, thr, sym, keep, mir, A, B, V, G, false);
-    k += (uint32_t)__popc(keep) + (uint32_t)__popc(mir);
+    Slots16 S;
+    blk_keep16(rule, a, b, c, c2, i, n, r, use_ge2, thr, sym, false, false, keep, mir, S);
+    k = (uint32_t)__popc(keep) + (uint32_t)__popc(mir);
   }
   k = wave_sum(k);
   if ((threadIdx.x & 63) == 0) wt[threadIdx.x >> 6] = k;
@@ -2642,42 +2668,36 @@ __global__ __launch_bounds__(FIN_T) void k_blk_compact(const uint8_t* __restrict
                                                        uint32_t* __restrict__ o2, uint32_t* __restrict__ o3) {
   __shared__ uint32_t wt[FIN_T / 64];
   const int w = threadIdx.x >> 6;
-  const int64_t base = (int64_t)blockIdx.x * FIN_B;
-  uint64_t run = boff[blockIdx.x];
-  for (int q = 0; q < FIN_PER / 4; ++q) {
-    const int64_t i = base + ((int64_t)q * FIN_T + threadIdx.x) * 4;
-    uint32_t keep = 0, mir = 0;
-    uint4 A, B, V, G;
-    if (i < n) blk_keep4(rule, a, b, c, c2, i, n, r, use_ge2, thr, sym, keep, mir, A, B, V, G, o3 != nullptr);
-    const uint32_t kc = (uint32_t)__popc(keep) + (uint32_t)__popc(mir);
-    const uint32_t incl = wave_incl_scan(kc);
-    if ((threadIdx.x & 63) == 63) wt[w] = incl;
-    __syncthreads();
-    uint32_t pre = 0, tot = 0;
+  const int64_t i = (int64_t)blockIdx.x * FIN_B + (int64_t)threadIdx.x * SLOTS_T;
+  uint32_t keep = 0, mir = 0;
+  Slots16 S;
+  if (i < n) blk_keep16(rule, a, b, c, c2, i, n, r, use_ge2, thr, sym, true, o3 != nullptr, keep, mir, S);
+  // block prefix in thread order = slot order (thread t holds slots [16t, 16t + 16) of the block)
+  const uint32_t kc = (uint32_t)__popc(keep) + (uint32_t)__popc(mir);
+  const uint32_t incl = wave_incl_scan(kc);
+  if ((threadIdx.x & 63) == 63) wt[w] = incl;
+  __syncthreads();
+  uint32_t pre = 0;
 #pragma unroll
-    for (int k = 0; k < FIN_T / 64; ++k) { pre += k < w ? wt[k] : 0u; tot += wt[k]; }
-    if (keep) {
-      uint64_t p = run + pre + incl - kc;
+  for (int k = 0; k < FIN_T / 64; ++k) pre += k < w ? wt[k] : 0u;
+  if (!keep) return;
+  uint64_t p = boff[blockIdx.x] + pre + incl - kc;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (!((keep >> j) & 1u)) continue;
-        const uint32_t ai = u4_at(A, j), bi = u4_at(B, j), cv = u4_at(V, j), gv = o3 ? u4_at(G, j) : 0u;
-        if (o0) o0[p] = ai;
-        if (o1) o1[p] = bi;
-        if (o2) o2[p] = cv;
-        if (o3) o3[p] = gv;
-        ++p;
-        if ((mir >> j) & 1u) {
-          if (o0) o0[p] = bi;
-          if (o1) o1[p] = ai;
-          if (o2) o2[p] = cv;
-          if (o3) o3[p] = gv;
-          ++p;
-        }
-      }
+  for (int s = 0; s < SLOTS_T; ++s) {
+    if (!((keep >> s) & 1u)) continue;
+    const uint32_t ai = S.a(s), bi = S.b(s), cv = S.v(s), gv = o3 ? S.g(s) : 0u;
+    if (o0) o0[p] = ai;
+    if (o1) o1[p] = bi;
+    if (o2) o2[p] = cv;
+    if (o3) o3[p] = gv;
+    ++p;
+    if ((mir >> s) & 1u) {
+      if (o0) o0[p] = bi;
+      if (o1) o1[p] = ai;
+      if (o2) o2[p] = cv;
+      if (o3) o3[p] = gv;
+      ++p;
     }
-    run += tot;
-    __syncthreads();  // wt is rewritten by the next round
   }
 }
 
@@ -2688,22 +2708,29 @@ __global__ __launch_bounds__(256) void k_rule_hist(const uint8_t* __restrict__ r
   __shared__ unsigned long long hr[256], hp[256];
   hr[threadIdx.x] = 0; hp[threadIdx.x] = 0;
   __syncthreads();
-  // 4 consecutive slots per thread; equal rule bytes among them (the common case: one row's slots) take one
-  // pair of LDS atomics
-  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += (int64_t)gridDim.x * blockDim.x * 4) {
-    const uint32_t r4 = ld_rule4(rule, i, n);
-    if (r4 == 0xFFFFFFFFu) continue;
-    const uint4 c4 = ld_u4(count, i, n);
+  // 16 consecutive slots per thread; runs of equal rule bytes among them (the common case: one row's slots)
+  // take one pair of LDS atomics
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * SLOTS_T;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * SLOTS_T; i < n; i += stride) {
+    const uint4 R = ld_rule16(rule, i, n);
+    uint32_t live = 0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) live |= (u4_at(R, g) != 0xFFFFFFFFu ? 15u : 0u) << (4 * g);
+    if (!live) continue;
+    uint4 C[4];
+    ld_groups(count, i, n, live, C);
     uint32_t cur = 0xFFu, nr = 0;
     unsigned long long np = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t r = (r4 >> (8 * j)) & 0xFFu;
+    for (int s = 0; s < SLOTS_T; ++s) {
+      const uint32_t r = rule_at(R, s);
+      if (r == 0xFFu) continue;
       if (r != cur) {
         if (cur != 0xFFu) { atomicAdd(&hr[cur], (unsigned long long)nr); atomicAdd(&hp[cur], np); }
         cur = r; nr = 0; np = 0;
       }
-      if (r != 0xFFu) { ++nr; np += u4_at(c4, j); }
+      ++nr;
+      np += u4_at(C[s >> 2], s & 3);
     }
     if (cur != 0xFFu) { atomicAdd(&hr[cur], (unsigned long long)nr); atomicAdd(&hp[cur], np); }
   }
@@ -2723,25 +2750,65 @@ struct PartCut {
   uint32_t nstar[PH_MAXP];
   uint32_t stage[PH_MAXP];  // tie histograms: 1 = aids of the v == c* rows, 2 = aid_next of the (c*, a*) rows
 };
-__device__ __forceinline__ uint32_t ph_val(const uint32_t* c, const uint32_t* c2, int64_t i, int use_ge2) {
-  return use_ge2 ? c2[i] : c[i];
-}
 __global__ __launch_bounds__(256) void k_ph_hist(const uint8_t* __restrict__ rule, const uint32_t* __restrict__ c,
                                                  const uint32_t* __restrict__ c2, int64_t n, int n_parts, int use_ge2,
                                                  uint32_t thr, unsigned long long* __restrict__ hist) {
   __shared__ uint32_t hs[PH_MAXP][256];
   for (int i = threadIdx.x; i < PH_MAXP * 256; i += 256) (&hs[0][0])[i] = 0;
   __syncthreads();
-  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += (int64_t)gridDim.x * blockDim.x * 4) {
-    const uint32_t r4 = ld_rule4(rule, i, n);
-    if (r4 == 0xFFFFFFFFu) continue;
-    const uint4 v4 = ld_u4(use_ge2 ? c2 : c, i, n);
+  auto add = [&](uint32_t p, uint32_t v, uint32_t k) {
+    if (v < 256u) atomicAdd(&hs[p][v], k);
+    else atomicAdd(&hist[(uint64_t)p * PH_VBINS + (v < PH_VBINS ? v : PH_VBINS - 1)], (unsigned long long)k);
+  };
+  const int l = (int)lane_id();
+  // 16 slots per thread; the counts of v in [thr, thr + 8) of the thread's first part are kept in registers
+  // (four 16-bit fields per u64) and summed over the wave when its lanes share that part -- the common case:
+  // most rows have v near thr, so per-slot LDS atomics on a few bins serialised the wave
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * SLOTS_T;
+  for (int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63)) * SLOTS_T; i0 < n; i0 += stride) {  // wave-uniform
+    const int64_t i = i0 + (int64_t)l * SLOTS_T;
+    uint4 R = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    if (i < n) R = ld_rule16(rule, i, n);
+    uint32_t live = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t p = (r4 >> (8 * j)) & 0xFFu, v = u4_at(v4, j);
+    for (int g = 0; g < 4; ++g) live |= (u4_at(R, g) != 0xFFFFFFFFu ? 15u : 0u) << (4 * g);
+    uint4 V[4];
+    ld_groups(use_ge2 ? c2 : c, i, n, live, V);
+    uint32_t p0 = 0xFFu;
+    unsigned long long lo = 0, hi = 0;
+#pragma unroll
+    for (int s = 0; s < SLOTS_T; ++s) {
+      const uint32_t p = rule_at(R, s), v = u4_at(V[s >> 2], s & 3);
       if (p >= (uint32_t)n_parts || v < thr) continue;
-      if (v < 256u) atomicAdd(&hs[p][v], 1u);
-      else atomicAdd(&hist[(uint64_t)p * PH_VBINS + (v < PH_VBINS ? v : PH_VBINS - 1)], 1ull);
+      const uint32_t d = v - thr;
+      if (p0 == 0xFFu) p0 = p;
+      if (p == p0 && d < 8u) {
+        const unsigned long long inc = 1ull << (16 * (d & 3u));
+        if (d < 4u) lo += inc; else hi += inc;
+      } else {
+        add(p, v, 1u);
+      }
+    }
+    const bool has = (lo | hi) != 0ull;
+    const uint64_t act = __ballot(has);
+    if (!act) continue;
+    const uint32_t pf = (uint32_t)__shfl((int)p0, __ffsll((long long)act) - 1);
+    if (!__ballot(has && p0 != pf)) {  // one part: wave sums, lane 0 adds
+      lo = wave_sum64(lo);
+      hi = wave_sum64(hi);
+      if (l == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t x = (uint32_t)(((k < 4 ? lo : hi) >> (16 * (k & 3))) & 0xFFFFull);
+          if (x) add(pf, thr + (uint32_t)k, x);
+        }
+      }
+    } else if (has) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t x = (uint32_t)(((k < 4 ? lo : hi) >> (16 * (k & 3))) & 0xFFFFull);
+        if (x) add(p0, thr + (uint32_t)k, x);
+      }
     }
   }
   __syncthreads();
@@ -2750,104 +2817,151 @@ __global__ __launch_bounds__(256) void k_ph_hist(const uint8_t* __restrict__ rul
     if (x) atomicAdd(&hist[(uint64_t)(i >> 8) * PH_VBINS + (i & 255)], (unsigned long long)x);
   }
 }
-// tie histograms of stage `st` (1: aid of the v == c* rows, 2: aid_next of the v == c*, aid == a* rows). Four
-// consecutive slots per thread (vector loads: one-byte loads per slot left the kernel address-bound). The slots
-// of one row sit together in aid order and the parts' rows interleave inside it, so a stage-1 key repeats over
-// thousands of slots: each wave keeps per-part counts of its current key in LDS and adds them to the histogram
-// once the key changes (one device atomic per (part, key) per wave instead of one per run of equal keys, which
-// serialised on the hot rows' counters); slot columns whose tie lanes hold other keys take the per-run atomics.
-__global__ __launch_bounds__(256) void k_ph_tie_hist(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
-                                                     const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
-                                                     const uint32_t* __restrict__ c2, int64_t n, int n_parts,
-                                                     int use_ge2, PartCut pc_arg, int st, int64_t n_items,
-                                                     uint32_t* __restrict__ h) {
+// The tie cut. A part's slots sit in aid order (rows sorted by aid; the parts' rows interleave inside an aid's
+// range), so the aid of the part's need-th tie row (v == c*) in slot order is a*: stage 1 is a rank search --
+// per-block tie counts per part (k_ph_rank_count), one scan, the block holding the rank (k_ph_find_multi), the
+// slot inside it (k_ph_tie_pick). Stage 2 histograms the aid_next of the part's (c*, a*) tie rows and counts
+// its ties with aid < a* (the rank left for the aid_next cut).
+struct PhRank {
+  uint64_t need[PH_MAXP];  // per stage-1 part q: the rank (1-based) of the cut tie row
+  uint32_t part[PH_MAXP];
+};
+// stage-1 parts in q order: qx[p] = q, or -1
+__device__ __forceinline__ void ph_qindex(const PartCut& pc, int n_parts, int* qx) {
+  int q = 0;
+  for (int p = 0; p < PH_MAXP; ++p) qx[p] = p < n_parts && pc.stage[p] == 1u ? q++ : -1;
+}
+// tie rows (v == c*) of the stage-1 parts among the 16 slots at i: bit mask, and the slots' parts in R
+__device__ __forceinline__ uint32_t ph_ties16(const uint8_t* __restrict__ rule, const uint32_t* __restrict__ vcol,
+                                              int64_t i, int64_t n, int n_parts, const PartCut& pc, uint32_t stage,
+                                              uint4& R) {
+  R = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+  if (i < n) R = ld_rule16(rule, i, n);
+  uint32_t live = 0;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) live |= (u4_at(R, g) != 0xFFFFFFFFu ? 15u : 0u) << (4 * g);
+  uint4 V[4];
+  ld_groups(vcol, i, n, live, V);
+  uint32_t tie = 0;
+#pragma unroll
+  for (int s = 0; s < SLOTS_T; ++s) {
+    const uint32_t p = rule_at(R, s);
+    tie |= (p < (uint32_t)n_parts && pc.stage[p] == stage && u4_at(V[s >> 2], s & 3) == pc.cstar[p] ? 1u : 0u) << s;
+  }
+  return tie;
+}
+// per FIN_B block: tie rows per stage-1 part -> bcnt[q * nb + block]
+__global__ __launch_bounds__(FIN_T) void k_ph_rank_count(const uint8_t* __restrict__ rule, const uint32_t* __restrict__ c,
+                                                         const uint32_t* __restrict__ c2, int64_t n, int n_parts,
+                                                         int use_ge2, PartCut pc_arg, int64_t nb,
+                                                         uint32_t* __restrict__ bcnt) {
+  __shared__ PartCut pc;
+  __shared__ int qx[PH_MAXP];
+  __shared__ uint32_t bc[PH_MAXP];
+  if (threadIdx.x == 0) { pc = pc_arg; ph_qindex(pc, n_parts, qx); }
+  if (threadIdx.x < PH_MAXP) bc[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * FIN_B + (int64_t)threadIdx.x * SLOTS_T;
+  uint4 R;
+  const uint32_t tie = ph_ties16(rule, use_ge2 ? c2 : c, i, n, n_parts, pc, 1u, R);
+  uint32_t cp = 0xFFu, cc = 0;
+#pragma unroll
+  for (int s = 0; s < SLOTS_T; ++s) {  // runs of one part: one LDS atomic each
+    if (!((tie >> s) & 1u)) continue;
+    const uint32_t p = rule_at(R, s);
+    if (p != cp) {
+      if (cc) atomicAdd(&bc[qx[cp]], cc);
+      cp = p; cc = 0;
+    }
+    ++cc;
+  }
+  if (cc) atomicAdd(&bc[qx[cp]], cc);
+  __syncthreads();
+  if (threadIdx.x < PH_MAXP && qx[threadIdx.x] >= 0)
+    bcnt[(int64_t)qx[threadIdx.x] * nb + blockIdx.x] = bc[qx[threadIdx.x]];
+}
+// per stage-1 part q: the block j whose tie range holds rank need[q] (ex = one exclusive scan over all q's
+// blocks), found[2q] = j, found[2q + 1] = the rank inside block j
+__global__ void k_ph_find_multi(const uint64_t* __restrict__ ex, const uint32_t* __restrict__ bcnt, int64_t nb, int nq,
+                                PhRank rk, uint32_t* __restrict__ found) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nb * nq) return;
+  const int q = (int)(t / nb);
+  const uint64_t lo = ex[t] - ex[(int64_t)q * nb], hi = lo + bcnt[t], need = rk.need[q];
+  if (bcnt[t] && lo < need && need <= hi) { found[2 * q] = (uint32_t)(t - (int64_t)q * nb); found[2 * q + 1] = (uint32_t)(need - lo); }
+}
+// one block per stage-1 part q: the found[2q + 1]-th tie row of the part in block found[2q] -> its aid
+__global__ __launch_bounds__(FIN_T) void k_ph_tie_pick(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
+                                                       const uint32_t* __restrict__ c, const uint32_t* __restrict__ c2,
+                                                       int64_t n, int n_parts, int use_ge2, PartCut pc_arg, PhRank rk,
+                                                       const uint32_t* __restrict__ found, uint32_t* __restrict__ astar) {
+  __shared__ PartCut pc;
+  __shared__ uint32_t wt[FIN_T / 64];
+  if (threadIdx.x == 0) pc = pc_arg;
+  __syncthreads();
+  const int q = blockIdx.x;
+  const uint32_t j = found[2 * q], r = found[2 * q + 1], p = rk.part[q];
+  if (j == 0xFFFFFFFFu) return;  // block-uniform: the host reports the missing cut
+  const int64_t i = (int64_t)j * FIN_B + (int64_t)threadIdx.x * SLOTS_T;
+  uint4 R;
+  uint32_t tie = ph_ties16(rule, use_ge2 ? c2 : c, i, n, n_parts, pc, 1u, R);
+#pragma unroll
+  for (int s = 0; s < SLOTS_T; ++s) tie &= ~((rule_at(R, s) != p ? 1u : 0u) << s);
+  const uint32_t k = (uint32_t)__popc(tie), incl = wave_incl_scan(k);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) wt[w] = incl;
+  __syncthreads();
+  uint32_t pre = incl - k;
+  for (int x = 0; x < w; ++x) pre += wt[x];
+  if (pre < r && r <= pre + k) {
+    uint32_t m = tie;
+    for (uint32_t x = pre + 1; x < r; ++x) m &= m - 1;  // drop the lower set bits
+    astar[q] = (uint32_t)a[i + __ffs((int)m) - 1];
+  }
+}
+// stage 2: aid_next histogram of the (c*, a*) tie rows of the stage-2 parts, and per part the tie rows with
+// aid < a* (lt); 16 slots per thread, grid-stride
+__global__ __launch_bounds__(256) void k_ph_tie_hist2(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
+                                                      const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
+                                                      const uint32_t* __restrict__ c2, int64_t n, int n_parts,
+                                                      int use_ge2, PartCut pc_arg, int64_t n_items,
+                                                      uint32_t* __restrict__ h, unsigned long long* __restrict__ lt) {
   // the cut tables in LDS: indexing the kernel-argument copy by a lane's part went through scratch memory
   __shared__ PartCut pc;
-  __shared__ uint32_t wcnt[4][PH_MAXP];  // per wave: counts of its current key per part
-  const int l = (int)lane_id(), wv = threadIdx.x >> 6;
+  __shared__ uint32_t lts[PH_MAXP];
   if (threadIdx.x == 0) pc = pc_arg;
-  if (l < PH_MAXP) wcnt[wv][l] = 0;
+  if (threadIdx.x < PH_MAXP) lts[threadIdx.x] = 0;
   __syncthreads();
-  uint32_t wkey = 0xFFFFFFFFu;  // wave-uniform
-  auto flush = [&]() {
-    if (wkey != 0xFFFFFFFFu && l < n_parts) {
-      const uint32_t x = wcnt[wv][l];
-      if (x) atomicAdd(&h[(uint64_t)l * n_items + wkey], x);
-      wcnt[wv][l] = 0;
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  };
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
-  for (int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63)) * 4; i0 < n; i0 += stride) {  // wave-uniform
-    const int64_t i = i0 + 4 * l;
-    uint32_t r4 = 0xFFFFFFFFu, tie = 0;
-    uint4 v4 = make_uint4(0u, 0u, 0u, 0u), a4 = v4, b4 = v4;
-    if (i < n) {
-      r4 = ld_rule4(rule, i, n);
-      if (r4 != 0xFFFFFFFFu) {
-        v4 = ld_u4(use_ge2 ? c2 : c, i, n);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * SLOTS_T;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * SLOTS_T; i < n; i += stride) {
+    uint4 R;
+    const uint32_t tie = ph_ties16(rule, use_ge2 ? c2 : c, i, n, n_parts, pc, 2u, R);
+    if (!tie) continue;
+    uint4 A[4];
+    ld_groups(reinterpret_cast<const uint32_t*>(a), i, n, tie, A);
+    uint32_t cp = 0xFFu, cc = 0, at = 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t p = (r4 >> (8 * j)) & 0xFFu;
-          tie |= (p < (uint32_t)n_parts && pc.stage[p] == (uint32_t)st && u4_at(v4, j) == pc.cstar[p] ? 1u : 0u) << j;
+    for (int s = 0; s < SLOTS_T; ++s) {
+      if (!((tie >> s) & 1u)) continue;
+      const uint32_t p = rule_at(R, s), ai = u4_at(A[s >> 2], s & 3);
+      if (ai == pc.astar[p]) {
+        at |= 1u << s;
+      } else if (ai < pc.astar[p]) {
+        if (p != cp) {
+          if (cc) atomicAdd(&lts[cp], cc);
+          cp = p; cc = 0;
         }
-        if (tie) {
-          a4 = ld_u4(reinterpret_cast<const uint32_t*>(a), i, n);
-          if (st == 2) b4 = ld_u4(reinterpret_cast<const uint32_t*>(b), i, n);
-        }
+        ++cc;
       }
     }
-    if (!__ballot(tie != 0u)) continue;
+    if (cc) atomicAdd(&lts[cp], cc);
+    if (!at) continue;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      uint32_t p = 0xFFFFFFFFu, key = 0;
-      bool tj = false;
-      if ((tie >> j) & 1u) {
-        p = (r4 >> (8 * j)) & 0xFFu;
-        const uint32_t ai = u4_at(a4, j);
-        if (st == 1) { tj = true; key = ai; }
-        else if (ai == pc.astar[p]) { tj = true; key = u4_at(b4, j); }
-      }
-      const uint64_t tm = __ballot(tj);
-      if (!tm) continue;
-      const uint32_t k0 = (uint32_t)__shfl((int)key, __ffsll((long long)tm) - 1);
-      if (!__ballot(tj && key != k0)) {  // one key in this column: counted per part in LDS
-        if (k0 != wkey) { flush(); wkey = k0; }
-        uint64_t pend = tm;
-        while (pend) {
-          const uint32_t pf = (uint32_t)__shfl((int)p, __ffsll((long long)pend) - 1);
-          const uint64_t mp = __ballot(tj && p == pf);
-          pend &= ~mp;
-          if (l == 0) wcnt[wv][pf] += (uint32_t)__popcll(mp);
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        continue;
-      }
-      uint64_t pend = tm;  // several keys: one atomic per run of equal keys per part
-      while (pend) {
-        const int f = __ffsll((long long)pend) - 1;
-        const uint32_t pf = (uint32_t)__shfl((int)p, f);
-        const uint64_t mp = __ballot(tj && p == pf);
-        pend &= ~mp;
-        const bool in = (mp >> l) & 1ull;
-        const uint64_t below = mp & ((1ull << l) - 1ull);
-        const int prv = below ? 63 - __clzll((long long)below) : l;
-        const uint32_t kprev = (uint32_t)__shfl((int)key, prv);
-        const bool head = in && (!below || kprev != key);
-        const uint64_t hm = __ballot(head);
-        if (head) {
-          const uint64_t above = hm & ~((2ull << l) - 1ull);
-          const int nh = above ? __ffsll((long long)above) - 1 : 64;
-          const uint64_t upto = nh == 64 ? ~0ull : ((1ull << nh) - 1ull);
-          const uint32_t cnt = (uint32_t)__popcll(mp & upto & ~((1ull << l) - 1ull));
-          atomicAdd(&h[(uint64_t)pf * n_items + key], cnt);
-        }
-      }
-    }
+    for (int s = 0; s < SLOTS_T; ++s)  // the few rows of the cut aid
+      if ((at >> s) & 1u) atomicAdd(&h[(uint64_t)rule_at(R, s) * n_items + (uint32_t)b[i + s]], 1u);
   }
-  flush();
+  __syncthreads();
+  if (threadIdx.x < PH_MAXP && lts[threadIdx.x]) atomicAdd(&lt[threadIdx.x], (unsigned long long)lts[threadIdx.x]);
 }
 // smallest index j with incl[j] >= need (incl = inclusive prefix of one part's histogram)
 __global__ void k_ph_find(const uint64_t* __restrict__ excl, const uint32_t* __restrict__ h, int64_t n, uint64_t need,
@@ -2857,34 +2971,37 @@ __global__ void k_ph_find(const uint64_t* __restrict__ excl, const uint32_t* __r
   const uint64_t lo = excl[j], hi = lo + h[j];
   if (h[j] && lo < need && need <= hi) { out[0] = (uint32_t)j; out[1] = (uint32_t)(need - lo); }
 }
-// kept slots (bit mask) of the 4 at i; A / B / V loaded for the kept ones
-__device__ __forceinline__ uint32_t ph_keep4(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
-                                             const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
-                                             const uint32_t* __restrict__ c2, int64_t i, int64_t n, int n_parts,
-                                             int use_ge2, uint32_t thr, const PartCut& pc, bool want_ab, uint4& A,
-                                             uint4& B, uint4& V) {
-  const uint32_t r4 = ld_rule4(rule, i, n);
-  if (r4 == 0xFFFFFFFFu) return 0u;
-  V = ld_u4(use_ge2 ? c2 : c, i, n);
+// kept slots (bit mask) of the 16 at i; V loaded for the live groups, A / B for the groups with a tie row
+// (and with any kept row when want_ab)
+__device__ __forceinline__ uint32_t ph_keep16(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
+                                              const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
+                                              const uint32_t* __restrict__ c2, int64_t i, int64_t n, int n_parts,
+                                              int use_ge2, uint32_t thr, const PartCut& pc, bool want_ab, Slots16& S) {
+  const uint4 R = ld_rule16(rule, i, n);
+  uint32_t live = 0;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) live |= (u4_at(R, g) != 0xFFFFFFFFu ? 15u : 0u) << (4 * g);
+  if (!live) return 0u;
+  ld_groups(use_ge2 ? c2 : c, i, n, live, S.V);
   uint32_t keep = 0, tie = 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t p = (r4 >> (8 * j)) & 0xFFu, v = u4_at(V, j);
+  for (int s = 0; s < SLOTS_T; ++s) {
+    const uint32_t p = rule_at(R, s), v = S.v(s);
     if (p >= (uint32_t)n_parts || v < thr) continue;
     const uint32_t cs = pc.cstar[p];
-    if (v != cs) keep |= (v > cs ? 1u : 0u) << j;
-    else if (pc.astar[p] == 0xFFFFFFFFu) keep |= 1u << j;
-    else tie |= 1u << j;
+    if (v != cs) keep |= (v > cs ? 1u : 0u) << s;
+    else if (pc.astar[p] == 0xFFFFFFFFu) keep |= 1u << s;
+    else tie |= 1u << s;
   }
-  if (tie || (want_ab && keep)) {
-    A = ld_u4(reinterpret_cast<const uint32_t*>(a), i, n);
-    B = ld_u4(reinterpret_cast<const uint32_t*>(b), i, n);
-  }
+  const uint32_t need = tie | (want_ab ? keep : 0u);
+  if (!need) return keep;
+  ld_groups(reinterpret_cast<const uint32_t*>(a), i, n, need, S.A);
+  ld_groups(reinterpret_cast<const uint32_t*>(b), i, n, need, S.B);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (!((tie >> j) & 1u)) continue;
-    const uint32_t p = (r4 >> (8 * j)) & 0xFFu, ai = u4_at(A, j);
-    keep |= (ai < pc.astar[p] || (ai == pc.astar[p] && u4_at(B, j) <= pc.nstar[p]) ? 1u : 0u) << j;
+  for (int s = 0; s < SLOTS_T; ++s) {
+    if (!((tie >> s) & 1u)) continue;
+    const uint32_t p = rule_at(R, s), ai = S.a(s);
+    keep |= (ai < pc.astar[p] || (ai == pc.astar[p] && S.b(s) <= pc.nstar[p]) ? 1u : 0u) << s;
   }
   return keep;
 }
@@ -2896,14 +3013,11 @@ __global__ __launch_bounds__(FIN_T) void k_ph_count(const uint8_t* __restrict__ 
   __shared__ PartCut pc;  // LDS copy (lane-indexed)
   if (threadIdx.x == 0) pc = pc_arg;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * FIN_B;
+  const int64_t i = (int64_t)blockIdx.x * FIN_B + (int64_t)threadIdx.x * SLOTS_T;
   uint32_t k = 0;
-#pragma unroll
-  for (int q = 0; q < FIN_PER / 4; ++q) {
-    const int64_t i = base + ((int64_t)q * FIN_T + threadIdx.x) * 4;
-    if (i >= n) break;
-    uint4 A, B, V;
-    k += (uint32_t)__popc(ph_keep4(rule, a, b, c, c2, i, n, n_parts, use_ge2, thr, pc, false, A, B, V));
+  if (i < n) {
+    Slots16 S;
+    k = (uint32_t)__popc(ph_keep16(rule, a, b, c, c2, i, n, n_parts, use_ge2, thr, pc, false, S));
   }
   k = wave_sum(k);
   if ((threadIdx.x & 63) == 0) wt[threadIdx.x >> 6] = k;
@@ -2921,26 +3035,21 @@ __global__ __launch_bounds__(FIN_T) void k_ph_compact(const uint8_t* __restrict_
   if (threadIdx.x == 0) pc = pc_arg;
   __syncthreads();
   const int w = threadIdx.x >> 6;
-  const int64_t base = (int64_t)blockIdx.x * FIN_B;
-  uint64_t run = boff[blockIdx.x];
-  for (int q = 0; q < FIN_PER / 4; ++q) {
-    const int64_t i = base + ((int64_t)q * FIN_T + threadIdx.x) * 4;
-    uint4 A, B, V;
-    const uint32_t keep = i < n ? ph_keep4(rule, a, b, c, c2, i, n, n_parts, use_ge2, thr, pc, true, A, B, V) : 0u;
-    const uint32_t kc = (uint32_t)__popc(keep);
-    const uint32_t incl = wave_incl_scan(kc);
-    if ((threadIdx.x & 63) == 63) wt[w] = incl;
-    __syncthreads();
-    uint32_t pre = 0, tot = 0;
+  const int64_t i = (int64_t)blockIdx.x * FIN_B + (int64_t)threadIdx.x * SLOTS_T;
+  Slots16 S;
+  const uint32_t keep = i < n ? ph_keep16(rule, a, b, c, c2, i, n, n_parts, use_ge2, thr, pc, true, S) : 0u;
+  const uint32_t kc = (uint32_t)__popc(keep);
+  const uint32_t incl = wave_incl_scan(kc);
+  if ((threadIdx.x & 63) == 63) wt[w] = incl;
+  __syncthreads();
+  uint32_t pre = 0;
 #pragma unroll
-    for (int k = 0; k < FIN_T / 64; ++k) { pre += k < w ? wt[k] : 0u; tot += wt[k]; }
-    uint64_t p = run + pre + incl - kc;
+  for (int k = 0; k < FIN_T / 64; ++k) pre += k < w ? wt[k] : 0u;
+  if (!keep) return;
+  uint64_t p = boff[blockIdx.x] + pre + incl - kc;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if ((keep >> j) & 1u) out[p++] = make_uint4(u4_at(A, j), u4_at(B, j), u4_at(V, j), 0u);
-    run += tot;
-    __syncthreads();
-  }
+  for (int s = 0; s < SLOTS_T; ++s)
+    if ((keep >> s) & 1u) out[p++] = make_uint4(S.a(s), S.b(s), S.v(s), 0u);
 }
 
 // ------------------------------------------------------------------ finalize (merge A6)
