@@ -103,21 +103,23 @@ __global__ void k_rec_row_key(const uint4* __restrict__ rec, const uint32_t* __r
 
 __device__ __forceinline__ uint64_t rec_key(const uint4& r) { return ((uint64_t)r.x << 32) | r.y; }
 
-// *unsorted = 1 when some record's (rule, aid) is below its predecessor's (records in (rule, aid) order, as the
-// part heads leave them in table slot order, need only the stable sort by aid_next: equal keys end up adjacent)
-__global__ void k_rec_order_check(const uint4* __restrict__ rec, int64_t n, int* __restrict__ unsorted) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
-  if (i < n && rec[i].x < rec[i - 1].x) *unsorted = 1;
-}
-
-// one random-read pass: records in key order (everything after it streams)
-__global__ void k_rec_gather(const uint4* __restrict__ rec, const uint32_t* __restrict__ perm, int64_t n,
-                             uint4* __restrict__ out, uint32_t* __restrict__ head) {
+// one random-read pass: records in key order (everything after it streams); the head test reads the
+// predecessor from the block's LDS copy (a second random read only for each block's first record)
+__global__ __launch_bounds__(256) void k_rec_gather(const uint4* __restrict__ rec, const uint32_t* __restrict__ perm,
+                                                    int64_t n, uint4* __restrict__ out, uint32_t* __restrict__ head) {
+  __shared__ uint64_t kx[256];
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t k = 0;
+  if (i < n) {
+    const uint4 r = rec[perm[i]];
+    out[i] = r;
+    k = rec_key(r);
+  }
+  kx[threadIdx.x] = k;
+  __syncthreads();
   if (i >= n) return;
-  const uint32_t p = perm[i];
-  out[i] = rec[p];
-  head[i] = (i == 0 || rec_key(rec[p]) != rec_key(rec[perm[i - 1]])) ? 1u : 0u;
+  const uint64_t prev = i == 0 ? ~k : (threadIdx.x ? kx[threadIdx.x - 1] : rec_key(rec[perm[i - 1]]));
+  head[i] = prev != k ? 1u : 0u;
 }
 
 // one thread per run head (grid-stride): sum the run (<= one record per source rank) and write
@@ -166,6 +168,281 @@ __global__ __launch_bounds__(256) void k_rec_reduce(const uint4* __restrict__ sr
   __syncthreads();
   if (threadIdx.x < 2 * n_rules && part[threadIdx.x])
     atomicAdd(&stats[(threadIdx.x >> 1) * 4 + (threadIdx.x & 1)], part[threadIdx.x]);
+}
+
+// ---- merge of records already in (rule, aid) order (the part heads of A6): every (rule, aid) group is
+// merged on its own in an LDS hash (no global sort, no random gather); the merged rows stay in the group's
+// own slot range (the rest of the range holds no row, rule 0xFF). Groups too large for one workgroup's hash
+// take the sort path above on their records only, into slots [n, n + U_big).
+constexpr int GM_T = 256, GM_PER = 4, GM_B = GM_T * GM_PER;  // records per block of the group scans
+constexpr uint32_t GM_WAVE_MAX = 256;   // group size handled by one wave (hash of <= 512 entries)
+constexpr uint32_t GM_WAVE_CAP = 512;
+constexpr uint32_t GM_BLOCK_MAX = 2048; // group size handled by one workgroup (hash of <= 4096 entries)
+constexpr uint32_t GM_BLOCK_CAP = 4096;
+constexpr uint32_t GM_EMPTY = 0xFFFFFFFFu;
+
+// record i starts a (rule, aid) group; also the range checks of k_rec_next_key and the order check
+__device__ __forceinline__ bool grp_head(const uint4* __restrict__ rec, int64_t i, const uint4& r) {
+  return i == 0 || rec[i - 1].x != r.x;
+}
+__global__ __launch_bounds__(GM_T) void k_grp_count(const uint4* __restrict__ rec, int64_t n, uint32_t n_items,
+                                                    int n_rules, uint32_t* __restrict__ bcnt, int* __restrict__ err,
+                                                    int* __restrict__ unsorted) {
+  __shared__ uint32_t wt[GM_T / 64];
+  const int64_t base = (int64_t)blockIdx.x * GM_B;
+  uint32_t k = 0;
+  bool bad = false, uns = false;
+#pragma unroll
+  for (int q = 0; q < GM_PER; ++q) {
+    const int64_t i = base + q * GM_T + threadIdx.x;
+    if (i >= n) break;
+    const uint4 r = rec[i];
+    bad |= (r.x & REC_AID_MASK) >= n_items || r.y >= n_items || (int)(r.x >> 29) >= n_rules;
+    if (i > 0) {
+      const uint32_t px = rec[i - 1].x;
+      uns |= r.x < px;
+      k += px != r.x ? 1u : 0u;
+    } else {
+      k += 1u;
+    }
+  }
+  if (bad) atomicOr(err, 1);
+  if (uns) atomicOr(unsorted, 1);
+  k = wave_sum(k);
+  if ((threadIdx.x & 63) == 0) wt[threadIdx.x >> 6] = k;
+  __syncthreads();
+  if (threadIdx.x == 0) bcnt[blockIdx.x] = wt[0] + wt[1] + wt[2] + wt[3];
+}
+// group starts in record order: gs[g] = first record of group g (gs[G] = n is set by the host)
+__global__ __launch_bounds__(GM_T) void k_grp_starts(const uint4* __restrict__ rec, int64_t n,
+                                                     const uint64_t* __restrict__ boff, uint32_t* __restrict__ gs) {
+  __shared__ uint32_t wt[GM_T / 64];
+  const int w = threadIdx.x >> 6;
+  const int64_t base = (int64_t)blockIdx.x * GM_B;
+  uint64_t run = boff[blockIdx.x];
+  for (int q = 0; q < GM_PER; ++q) {
+    const int64_t i = base + q * GM_T + threadIdx.x;
+    uint32_t h = 0;
+    if (i < n) h = (i == 0 || rec[i - 1].x != rec[i].x) ? 1u : 0u;
+    const uint32_t incl = wave_incl_scan(h);
+    if ((threadIdx.x & 63) == 63) wt[w] = incl;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int x = 0; x < GM_T / 64; ++x) { pre += x < w ? wt[x] : 0u; tot += wt[x]; }
+    if (h) gs[run + pre + incl - 1] = (uint32_t)i;
+    run += tot;
+    __syncthreads();
+  }
+}
+// group classes: big[g] = length of a group above GM_BLOCK_MAX (else 0); the groups above GM_WAVE_MAX (the
+// workgroup merges and the big groups' 0xFF fills) are listed in mid (any order)
+__global__ void k_grp_classify(const uint32_t* __restrict__ gs, int64_t G, uint32_t* __restrict__ big,
+                               uint32_t* __restrict__ mid, unsigned long long* __restrict__ n_mid) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  const uint32_t L = gs[g + 1] - gs[g];
+  big[g] = L > GM_BLOCK_MAX ? L : 0u;
+  if (L > GM_WAVE_MAX) mid[atomicAdd(n_mid, 1ull)] = (uint32_t)g;
+}
+// (aid_next, record index) of the big groups' records, each group contiguous (the stable sort by aid_next then
+// leaves a group's equal keys adjacent). One thread per output position j; its group is the last g with
+// bbo[g] <= j (bbo = exclusive scan of the big lengths). A big group holds > GM_BLOCK_MAX >= 256 records, so a
+// block's 256 positions fall in at most two groups: two binary searches per block.
+__device__ __forceinline__ int64_t grp_of(const uint64_t* __restrict__ bbo, int64_t G, uint64_t j) {
+  int64_t lo = 0, hi = G;  // first g with bbo[g] > j
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (bbo[m] <= j) lo = m + 1; else hi = m;
+  }
+  return lo - 1;
+}
+__global__ __launch_bounds__(256) void k_grp_big_keys(const uint4* __restrict__ rec, const uint32_t* __restrict__ gs,
+                                                      int64_t G, const uint64_t* __restrict__ bbo, uint64_t n_big,
+                                                      uint32_t* __restrict__ key, uint32_t* __restrict__ val) {
+  static_assert(GM_BLOCK_MAX >= 256, "a block's positions span at most two big groups");
+  __shared__ int64_t sg[2];
+  const uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x;
+  if (threadIdx.x < 2) {
+    const uint64_t jl = std::min<uint64_t>(j0 + blockDim.x, n_big) - 1;
+    sg[threadIdx.x] = grp_of(bbo, G, threadIdx.x ? jl : j0);
+  }
+  __syncthreads();
+  const uint64_t j = j0 + threadIdx.x;
+  if (j >= n_big) return;
+  const int64_t g = j >= bbo[sg[1]] ? sg[1] : sg[0];
+  const uint32_t i = gs[g] + (uint32_t)(j - bbo[g]);
+  key[j] = rec[i].y;
+  val[j] = i;
+}
+__device__ __forceinline__ uint32_t gm_hash(uint32_t k, uint32_t cm) { return (k * 0x9E3779B1u) >> __clz((int)cm); }  // top bits
+// insert one record into an LDS hash (keys K, sums C / G2); a wrapped sum sets err bit 2
+__device__ __forceinline__ void gm_insert(uint32_t* K, uint32_t* C, uint32_t* G2, uint32_t cm, const uint4& r,
+                                          bool& wrap) {
+  uint32_t h = gm_hash(r.y, cm);
+  while (true) {
+    const uint32_t old = atomicCAS(&K[h], GM_EMPTY, r.y);
+    if (old == GM_EMPTY || old == r.y) break;
+    h = (h + 1) & cm;
+  }
+  const uint32_t oc = atomicAdd(&C[h], r.z);
+  wrap |= oc + r.z < oc;
+  atomicAdd(&G2[h], r.w);
+}
+struct GmOut {
+  uint8_t* rule;
+  int32_t* aid;
+  int32_t* next;
+  uint32_t* cnt;
+  uint32_t* ge2;
+};
+// per-rule rows / pairs of one block -> stats (rows, pairs at stats[rule * 4 + {0, 1}])
+__device__ __forceinline__ void gm_stats_flush(const uint64_t (&rows)[MAX_RULES], const uint64_t (&pairs)[MAX_RULES],
+                                               int n_rules, unsigned long long* part, unsigned long long* stats) {
+#pragma unroll
+  for (int q = 0; q < MAX_RULES; ++q) {
+    if (q >= n_rules) break;
+    const uint64_t rw = wave_sum64(rows[q]), pr = wave_sum64(pairs[q]);
+    if (lane_id() == 0 && rw) {
+      atomicAdd(&part[2 * q], (unsigned long long)rw);
+      atomicAdd(&part[2 * q + 1], (unsigned long long)pr);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * n_rules && part[threadIdx.x])
+    atomicAdd(&stats[(threadIdx.x >> 1) * 4 + (threadIdx.x & 1)], part[threadIdx.x]);
+}
+// one wave per group of <= GM_WAVE_MAX records
+__global__ __launch_bounds__(GM_T) void k_grp_merge_wave(const uint4* __restrict__ rec, const uint32_t* __restrict__ gs,
+                                                         int64_t G, int n_rules, GmOut O,
+                                                         unsigned long long* __restrict__ stats, int* __restrict__ err) {
+  __shared__ uint32_t sK[GM_T / 64][GM_WAVE_CAP], sC[GM_T / 64][GM_WAVE_CAP], sG[GM_T / 64][GM_WAVE_CAP];
+  __shared__ unsigned long long part[MAX_RULES * 2];
+  const int w = threadIdx.x >> 6;
+  const uint32_t l = lane_id();
+  uint32_t *K = sK[w], *C = sC[w], *G2 = sG[w];
+  for (uint32_t e = l; e < GM_WAVE_CAP; e += 64) { K[e] = GM_EMPTY; C[e] = 0; G2[e] = 0; }
+  if (threadIdx.x < MAX_RULES * 2) part[threadIdx.x] = 0;
+  __syncthreads();
+  uint64_t rows[MAX_RULES] = {}, pairs[MAX_RULES] = {};
+  bool wrap = false;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t g = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; g < G; g += nw) {  // wave-uniform
+    const uint32_t s0 = gs[g], L = gs[g + 1] - s0;
+    if (L > GM_WAVE_MAX) continue;
+    uint32_t cap = 64;
+    while (cap < 2 * L) cap <<= 1;
+    const uint32_t cm = cap - 1;
+    uint32_t x0 = 0;
+    for (uint32_t j = l; j < L; j += 64) {
+      const uint4 r = rec[s0 + j];
+      x0 = r.x;
+      gm_insert(K, C, G2, cm, r, wrap);
+    }
+    x0 = (uint32_t)__shfl((int)x0, 0);  // the group's (rule, aid)
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    uint32_t u = 0;
+    uint64_t ps = 0;
+    for (uint32_t e0 = 0; e0 < cap; e0 += 64) {
+      const uint32_t e = e0 + l, k = K[e];
+      const bool has = k != GM_EMPTY;
+      const uint64_t m = __ballot(has);
+      if (has) {
+        const uint32_t o = s0 + u + (uint32_t)__popcll(m & ((1ull << l) - 1ull));
+        const uint32_t c = C[e];
+        O.rule[o] = (uint8_t)(x0 >> 29);
+        O.aid[o] = (int32_t)(x0 & REC_AID_MASK);
+        O.next[o] = (int32_t)k;
+        O.cnt[o] = c;
+        O.ge2[o] = G2[e];
+        ps += c;
+        K[e] = GM_EMPTY; C[e] = 0; G2[e] = 0;
+      }
+      u += (uint32_t)__popcll(m);
+    }
+    for (uint32_t j = u + l; j < L; j += 64) O.rule[s0 + j] = 0xFF;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int r = (int)(x0 >> 29);
+    ps = wave_sum64(ps);
+#pragma unroll
+    for (int q = 0; q < MAX_RULES; ++q)
+      if (q == r && l == 0) { rows[q] += u; pairs[q] += ps; }
+  }
+  if (__ballot(wrap) && l == 0) atomicOr(err, 2);
+  gm_stats_flush(rows, pairs, n_rules, part, stats);
+}
+// one workgroup per listed group of (GM_WAVE_MAX, GM_BLOCK_MAX] records; the big groups' slot ranges get rule 0xFF
+__global__ __launch_bounds__(GM_T) void k_grp_merge_block(const uint4* __restrict__ rec, const uint32_t* __restrict__ gs,
+                                                          const uint32_t* __restrict__ mid,
+                                                          const unsigned long long* __restrict__ n_mid, int n_rules, GmOut O,
+                                                          unsigned long long* __restrict__ stats, int* __restrict__ err) {
+  __shared__ uint32_t K[GM_BLOCK_CAP], C[GM_BLOCK_CAP], G2[GM_BLOCK_CAP];
+  __shared__ unsigned long long part[MAX_RULES * 2];
+  __shared__ uint32_t wt[GM_T / 64];
+  __shared__ unsigned long long wps[GM_T / 64];
+  const int w = threadIdx.x >> 6;
+  const uint32_t l = lane_id();
+  for (uint32_t e = threadIdx.x; e < GM_BLOCK_CAP; e += GM_T) { K[e] = GM_EMPTY; C[e] = 0; G2[e] = 0; }
+  if (threadIdx.x < MAX_RULES * 2) part[threadIdx.x] = 0;
+  __syncthreads();
+  uint64_t rows[MAX_RULES] = {}, pairs[MAX_RULES] = {};
+  bool wrap = false;
+  const int64_t nm = (int64_t)*n_mid;
+  for (int64_t t = blockIdx.x; t < nm; t += gridDim.x) {  // block-uniform
+    const uint32_t g = mid[t], s0 = gs[g], L = gs[g + 1] - s0;
+    if (L > GM_BLOCK_MAX) {
+      for (uint32_t j = threadIdx.x; j < L; j += GM_T) O.rule[s0 + j] = 0xFF;
+      continue;
+    }
+    uint32_t cap = 64;
+    while (cap < 2 * L) cap <<= 1;
+    const uint32_t cm = cap - 1;
+    for (uint32_t j = threadIdx.x; j < L; j += GM_T) gm_insert(K, C, G2, cm, rec[s0 + j], wrap);
+    const uint32_t x0 = rec[s0].x;
+    __syncthreads();
+    uint32_t u = 0;
+    uint64_t ps = 0;
+    for (uint32_t e0 = 0; e0 < cap; e0 += GM_T) {  // block-ordered compaction, GM_T entries per round
+      const uint32_t e = e0 + threadIdx.x;
+      const uint32_t k = e < cap ? K[e] : GM_EMPTY;
+      const bool has = k != GM_EMPTY;
+      const uint32_t h = has ? 1u : 0u, incl = wave_incl_scan(h);
+      if (l == 63) wt[w] = incl;
+      __syncthreads();
+      uint32_t pre = 0, tot = 0;
+#pragma unroll
+      for (int x = 0; x < GM_T / 64; ++x) { pre += x < w ? wt[x] : 0u; tot += wt[x]; }
+      if (has) {
+        const uint32_t o = s0 + u + pre + incl - 1;
+        const uint32_t c = C[e];
+        O.rule[o] = (uint8_t)(x0 >> 29);
+        O.aid[o] = (int32_t)(x0 & REC_AID_MASK);
+        O.next[o] = (int32_t)k;
+        O.cnt[o] = c;
+        O.ge2[o] = G2[e];
+        ps += c;
+        K[e] = GM_EMPTY; C[e] = 0; G2[e] = 0;
+      }
+      u += tot;
+      __syncthreads();
+    }
+    for (uint32_t j = u + threadIdx.x; j < L; j += GM_T) O.rule[s0 + j] = 0xFF;
+    ps = wave_sum64(ps);
+    if (l == 0) wps[w] = ps;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int r = (int)(x0 >> 29);
+      const uint64_t pt = wps[0] + wps[1] + wps[2] + wps[3];
+#pragma unroll
+      for (int q = 0; q < MAX_RULES; ++q)
+        if (q == r) { rows[q] += u; pairs[q] += pt; }
+    }
+    __syncthreads();
+  }
+  if (__ballot(wrap) && l == 0) atomicOr(err, 2);
+  gm_stats_flush(rows, pairs, n_rules, part, stats);
 }
 
 }  // namespace ottohip
@@ -258,35 +535,72 @@ int ottohip_table_from_records(ottohip_ctx* ctx, const void* records, int64_t n,
       (rc = ws.get("mg_err", 1, &err)))
     return fail(rc);
   const int A = std::max(1, bits_for((uint64_t)n_items)), RB = bits_for((uint64_t)n_rules);
-  int ph = ctx->begin("merge_sort", s, 16.0 * n);
   if (hipMemsetAsync(err, 0, sizeof(int), s) || hipMemsetAsync(stats, 0, MAX_RULES * 4 * 8, s)) return fail(OTTOHIP_EHIP);
-  k_rec_next_key<<<grid_for(n), 256, 0, s>>>(rec, n, k0, v0, err, (uint32_t)n_items, n_rules);
-  // records already in (rule, aid) order skip the second sort (their slots end in (aid_next, rule, aid) order;
-  // the readers of a table do not depend on its slot order)
+  // (1) group scan: (rule, aid) groups per block, the range check and the order check in one pass
+  int ph = ctx->begin("merge_groups", s, 32.0 * n);
   int* unsorted;
-  if ((rc = ws.get("mg_unsorted", 1, &unsorted))) return fail(rc);
+  uint32_t* gbc;
+  uint64_t* gbo;
+  const int64_t nbg = ceil_div(n, GM_B);
+  if ((rc = ws.get("mg_unsorted", 1, &unsorted)) || (rc = ws.get("mg_gbc", (size_t)nbg, &gbc)) ||
+      (rc = ws.get("mg_gbo", (size_t)nbg, &gbo)))
+    return fail(rc);
   if (hipMemsetAsync(unsorted, 0, sizeof(int), s)) return fail(OTTOHIP_EHIP);
-  k_rec_order_check<<<grid_for(n), 256, 0, s>>>(rec, n, unsorted);
-  int huns = 1;
-  if ((rc = d2h(&huns, unsorted, 1, s))) return fail(rc);
-  uint32_t *k = k0, *v = v0;
-  if ((rc = radix_sort_pairs(ctx, k, v, k1, v1, n, A, s))) return fail(rc);
-  if (huns) {
-    uint32_t* kn = (k == k0) ? k1 : k0;
-    k_rec_row_key<<<grid_for(n), 256, 0, s>>>(rec, v, n, A, kn);
-    k = kn;
-    if ((rc = radix_sort_pairs(ctx, k, v, k == k0 ? k1 : k0, v == v0 ? v1 : v0, n, A + RB, s))) return fail(rc);
-  }
-  ctx->end(ph, s);
-  ph = ctx->begin("merge_reduce", s, 16.0 * n);
-  uint4* srt;
+  k_grp_count<<<(unsigned)nbg, GM_T, 0, s>>>(rec, n, (uint32_t)n_items, n_rules, gbc, err, unsorted);
+  if ((rc = exclusive_scan_u32(ctx, gbc, gbo, nbg, tot, s))) return fail(rc);
+  int hflags[2] = {0, 0};
+  uint64_t G = 0;
+  if ((rc = d2h(&hflags[0], err, 1, s)) || (rc = d2h(&hflags[1], unsorted, 1, s)) || (rc = d2h(&G, tot, 1, s))) return fail(rc);
+  if (hflags[0]) { set_error("table_from_records: record out of range (aid/aid_next >= n_items or rule >= n_rules)"); return fail(OTTOHIP_ERANGE); }
+  // OTTOHIP_MERGE_GROUPS=0 (read per call): the sort path for ordered records too (A/B, tests)
+  const char* genv = getenv("OTTOHIP_MERGE_GROUPS");
+  const bool grouped = !hflags[1] && !(genv && atoi(genv) == 0);
+  uint64_t U = 0, n_big = 0, U_big = 0;
+  uint32_t *gs = nullptr, *big = nullptr, *mid = nullptr;
+  unsigned long long* n_mid = nullptr;
+  uint4* srt = nullptr;
   if ((rc = ws.get("mg_srt", (size_t)n, &srt))) return fail(rc);
-  k_rec_gather<<<grid_for(n), 256, 0, s>>>(rec, v, n, srt, head);
-  if ((rc = exclusive_scan_u32(ctx, head, idx, n, tot, s))) return fail(rc);
-  uint64_t U = 0;
-  int herr = 0;
-  if ((rc = d2h(&U, tot, 1, s)) || (rc = d2h(&herr, err, 1, s))) return fail(rc);
-  if (herr) { set_error("table_from_records: record out of range (aid/aid_next >= n_items or rule >= n_rules)"); return fail(OTTOHIP_ERANGE); }
+  if (grouped) {
+    // records in (rule, aid) order (the part heads): per-group LDS merges; the big groups take the sort path
+    uint64_t* bbo;
+    if ((rc = ws.get("mg_gs", (size_t)G + 1, &gs)) || (rc = ws.get("mg_big", (size_t)G, &big)) ||
+        (rc = ws.get("mg_mid", (size_t)G, &mid)) || (rc = ws.get("mg_nmid", 1, &n_mid)) ||
+        (rc = ws.get("mg_bbo", (size_t)G, &bbo)))
+      return fail(rc);
+    k_grp_starts<<<(unsigned)nbg, GM_T, 0, s>>>(rec, n, gbo, gs);
+    const uint32_t nn = (uint32_t)n;
+    if (hipMemcpyAsync(gs + G, &nn, 4, hipMemcpyHostToDevice, s) || hipMemsetAsync(n_mid, 0, 8, s)) return fail(OTTOHIP_EHIP);
+    k_grp_classify<<<grid_for((int64_t)G), 256, 0, s>>>(gs, (int64_t)G, big, mid, n_mid);
+    if ((rc = exclusive_scan_u32(ctx, big, bbo, (int64_t)G, tot, s)) || (rc = d2h(&n_big, tot, 1, s))) return fail(rc);
+    ctx->end(ph, s);
+    if (n_big) {
+      ph = ctx->begin("merge_sort", s, 16.0 * n_big);
+      k_grp_big_keys<<<grid_for((int64_t)n_big), 256, 0, s>>>(rec, gs, (int64_t)G, bbo, n_big, k0, v0);
+      uint32_t *k = k0, *v = v0;
+      if ((rc = radix_sort_pairs(ctx, k, v, k1, v1, (int64_t)n_big, A, s))) return fail(rc);
+      k_rec_gather<<<grid_for((int64_t)n_big), 256, 0, s>>>(rec, v, (int64_t)n_big, srt, head);
+      if ((rc = exclusive_scan_u32(ctx, head, idx, (int64_t)n_big, tot, s)) || (rc = d2h(&U_big, tot, 1, s))) return fail(rc);
+      ctx->end(ph, s);
+    }
+    U = (uint64_t)n + U_big;  // slots: the groups' own ranges, then the big groups' rows
+  } else {
+    // any order (records received from several ranks): LSD sort by (rule, aid, aid_next) on a permutation
+    ctx->end(ph, s);
+    ph = ctx->begin("merge_sort", s, 16.0 * n);
+    k_rec_next_key<<<grid_for(n), 256, 0, s>>>(rec, n, k0, v0, err, (uint32_t)n_items, n_rules);
+    uint32_t *k = k0, *v = v0;
+    if ((rc = radix_sort_pairs(ctx, k, v, k1, v1, n, A, s))) return fail(rc);
+    if (hflags[1]) {
+      uint32_t* kn = (k == k0) ? k1 : k0;
+      k_rec_row_key<<<grid_for(n), 256, 0, s>>>(rec, v, n, A, kn);
+      k = kn;
+      if ((rc = radix_sort_pairs(ctx, k, v, k == k0 ? k1 : k0, v == v0 ? v1 : v0, n, A + RB, s))) return fail(rc);
+    }
+    ctx->end(ph, s);
+    k_rec_gather<<<grid_for(n), 256, 0, s>>>(rec, v, n, srt, head);
+    if ((rc = exclusive_scan_u32(ctx, head, idx, n, tot, s)) || (rc = d2h(&U, tot, 1, s))) return fail(rc);
+  }
+  ph = ctx->begin("merge_reduce", s, 16.0 * n);
   if (ctx->spare.cap >= U) {
     T->b = ctx->spare;
     ctx->spare = TableBufs();
@@ -295,19 +609,33 @@ int ottohip_table_from_records(ottohip_ctx* ctx, const void* records, int64_t n,
     ctx->spare.release();
     if ((rc = T->b.alloc(std::max<uint64_t>(U, 1)))) return fail(rc);
   }
-  k_rec_reduce<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), (int64_t)ctx->n_cu * 8), 256, 0, s>>>(srt, n, head, idx, n_rules, T->b.rule, T->b.aid, T->b.aid_next,
-                                           T->b.count, T->b.count_ge2, stats, err);
+  const unsigned rgrid_n = (unsigned)std::min<int64_t>(ceil_div(grouped ? (int64_t)n_big : n, 256), (int64_t)ctx->n_cu * 8);
+  if (grouped) {
+    const GmOut O{T->b.rule, T->b.aid, T->b.aid_next, T->b.count, T->b.count_ge2};
+    k_grp_merge_wave<<<(unsigned)std::min<int64_t>(ceil_div((int64_t)G, 4), (int64_t)ctx->n_cu * 8), GM_T, 0, s>>>(
+        rec, gs, (int64_t)G, n_rules, O, stats, err);
+    k_grp_merge_block<<<(unsigned)ctx->n_cu * 3, GM_T, 0, s>>>(rec, gs, mid, n_mid, n_rules, O, stats, err);
+    if (n_big)
+      k_rec_reduce<<<rgrid_n, 256, 0, s>>>(srt, (int64_t)n_big, head, idx, n_rules, T->b.rule + n, T->b.aid + n,
+                                           T->b.aid_next + n, T->b.count + n, T->b.count_ge2 + n, stats, err);
+  } else {
+    k_rec_reduce<<<rgrid_n, 256, 0, s>>>(srt, n, head, idx, n_rules, T->b.rule, T->b.aid, T->b.aid_next, T->b.count,
+                                         T->b.count_ge2, stats, err);
+  }
   if (hipGetLastError() != hipSuccess) { set_error("merge launch failed"); return fail(OTTOHIP_EHIP); }
   ctx->end(ph, s);
   unsigned long long st[MAX_RULES * 4];
+  int herr = 0;
   if ((rc = d2h(st, stats, MAX_RULES * 4, s)) || (rc = d2h(&herr, err, 1, s))) return fail(rc);
   if (herr) { set_error("table_from_records: merged count overflows u32"); return fail(OTTOHIP_ELIMIT); }
-  T->n_rows = (int64_t)U;
-  T->n_slots = (int64_t)U;
+  uint64_t rows = 0;
   for (int r = 0; r < n_rules; ++r) {
     T->stats[r].n_rows = (int64_t)st[r * 4 + 0];
     T->stats[r].n_pairs = (int64_t)st[r * 4 + 1];
+    rows += st[r * 4 + 0];
   }
+  T->n_rows = (int64_t)rows;
+  T->n_slots = (int64_t)U;
   *out = T;
   return 0;
 }

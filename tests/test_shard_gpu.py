@@ -222,3 +222,46 @@ def test_reduce_received_rejects_inconsistent_pieces(gpu):
     pieces = torch.tensor([(7 << 32) | 3], dtype=torch.int64, device="cuda")  # 3 words claimed, 5 sent
     with pytest.raises(L.OttoHipError):
         gd.reduce_received(words, pieces, NAMES, 1)
+
+
+@pytest.mark.parametrize("grouped", ["1", "0"])
+def test_from_records_ordered_groups(gpu, monkeypatch, grouped):
+    """Records in (rule, aid) order (as the A6 part heads leave them) merge per (rule, aid) group: groups of
+    one wave's size, of one workgroup's size and above it (the sort path into the slots after the groups'
+    ranges) all equal a numpy groupby-sum; OTTOHIP_MERGE_GROUPS=0 forces the sort path on the same input."""
+    import torch
+    from otto_recommender_amd import dist as gd
+    monkeypatch.setenv("OTTOHIP_MERGE_GROUPS", grouped)
+    rng = np.random.default_rng(7)
+    sizes = np.concatenate([rng.integers(1, 40, 3000), rng.integers(200, 2100, 60), [2049, 2048, 257, 256],
+                            rng.integers(2100, 30000, 6)])
+    rng.shuffle(sizes)
+    n_items = 50_000
+    rule = np.sort(rng.integers(0, len(NAMES), len(sizes)))
+    aid = np.zeros(len(sizes), np.int64)
+    for r in range(len(NAMES)):  # strictly increasing aids inside each rule
+        k = rule == r
+        aid[k] = np.sort(rng.choice(n_items, int(k.sum()), replace=False))
+    g_rule, g_aid = np.repeat(rule, sizes), np.repeat(aid, sizes)
+    # few distinct aid_next per group: long runs of duplicates, and hot groups with many distinct keys
+    span = np.repeat(np.where(sizes > 2000, n_items, np.maximum(2, sizes // 3)), sizes)
+    nxt = rng.integers(0, 1 << 30, len(g_aid)) % span
+    cnt = rng.integers(1, 1000, len(g_aid)).astype(np.uint32)
+    ge2 = np.where(cnt >= 2, cnt, 0).astype(np.uint32)
+    x = (g_rule.astype(np.uint32) << 29) | g_aid.astype(np.uint32)
+    rec = np.stack([x, nxt.astype(np.uint32), cnt, ge2], 1)
+    t = gd.table_from_records(torch.from_numpy(rec.view(np.int32)).cuda(), NAMES, n_items)
+    for r, n in enumerate(NAMES):
+        k = g_rule == r
+        key = g_aid[k] * n_items + nxt[k]
+        u, inv = np.unique(key, return_inverse=True)
+        ec = np.bincount(inv, weights=cnt[k].astype(np.float64)).astype(np.uint64)
+        eg = np.bincount(inv, weights=ge2[k].astype(np.float64)).astype(np.uint64)
+        a, b, c, c2 = t.to_numpy(n)
+        np.testing.assert_array_equal(a, (u // n_items).astype(np.int32), err_msg=n)
+        np.testing.assert_array_equal(b, (u % n_items).astype(np.int32), err_msg=n)
+        np.testing.assert_array_equal(c.astype(np.uint64), ec, err_msg=n)
+        np.testing.assert_array_equal(c2.astype(np.uint64), eg, err_msg=n)
+        st = t.stats(n)
+        assert st["n_rows"] == len(u) and st["n_pairs"] == int(ec.sum())
+    t.free()
