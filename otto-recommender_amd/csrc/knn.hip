@@ -95,8 +95,15 @@ constexpr int KN_GL = KN_IT * KN_CH / KN_T;  // glds per thread per tile (8)
 //   buffer cbuf[q * KN_BCAP ..] in insertion order and ncand[q] counts them. The final list is the
 //   first KN_C of the inserted candidates by (score desc, insertion order) -- exactly the candidates the
 //   index list would hold -- which k_knn_rerank_buf selects before the exact rerank.
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ s16x4 lo4(const bf16x8& v) {  // the low 4 bf16 of a fragment as the x8 MFMA's operand
+  const uint4 u = __builtin_bit_cast(uint4, v);
+  return __builtin_bit_cast(s16x4, make_uint2(u.x, u.y));
+}
+// HALF: the last k-step covers 8 columns with v_mfma_f32_32x32x8_bf16 (dim + 2 <= 16 (KS - 1) + 8: dim 100 -> 104
+//   columns instead of 112; the 14th chunk of a row is neither streamed nor multiplied).
 constexpr int KN_BCAP = 512;  // inserted candidates kept per query (overflow: the search reruns with index lists)
-template <int ABL, int KS, bool BUF = false>
+template <int ABL, int KS, bool BUF = false, bool HALF = false>
 __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ items, int64_t V,
                                                   const uint4* __restrict__ queries, int64_t nq,
                                                   uint32_t* __restrict__ cand, float* __restrict__ thr_io,
@@ -115,8 +122,13 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
   for (int s = 0; s < KS; ++s) {
     const int64_t qa = qbase + r, qb = qbase + 32 + r;
     uint4 ua = make_uint4(0, 0, 0, 0), ub = make_uint4(0, 0, 0, 0);
-    if (qa < nq) ua = queries[qa * KN_CH + 2 * s + h];
-    if (qb < nq) ub = queries[qb * KN_CH + 2 * s + h];
+    const bool tail = HALF && s == KS - 1;  // 8 columns: lane half h holds columns 16 s + 4 h .. + 3
+    if (qa < nq) ua = queries[qa * KN_CH + 2 * s + (tail ? 0 : h)];
+    if (qb < nq) ub = queries[qb * KN_CH + 2 * s + (tail ? 0 : h)];
+    if (tail) {
+      ua = h ? make_uint4(ua.z, ua.w, 0u, 0u) : make_uint4(ua.x, ua.y, 0u, 0u);
+      ub = h ? make_uint4(ub.z, ub.w, 0u, 0u) : make_uint4(ub.x, ub.y, 0u, 0u);
+    }
     bqa[s] = __builtin_bit_cast(bf16x8, ua);
     bqb[s] = __builtin_bit_cast(bf16x8, ub);
   }
@@ -146,7 +158,7 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
       const int p = u * KN_T + tid, row = p >> 4, c = p & 15;
       int64_t item = tt * KN_IT + row;
       if (item >= V) item = V - 1;
-      if (KS < KN_KD / 16 && (c ^ (row & 15)) >= 2 * KS) continue;
+      if (KS < KN_KD / 16 && (c ^ (row & 15)) >= 2 * KS - (HALF ? 1 : 0)) continue;
       __builtin_amdgcn_global_load_lds(items + item * KN_CH + (c ^ (row & 15)), dst + u * KN_T + w * 64, 16, 0, 0);
     }
   };
@@ -276,7 +288,12 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
     bf16x8 F[NSTEP];
     auto ld = [&](int g) __attribute__((always_inline)) {
       const int row = (g / KS) * 32 + r, s_ = g % KS;
-      F[g] = __builtin_bit_cast(bf16x8, T[row * KN_CH + ((2 * s_ + h) ^ (row & 15))]);
+      if (HALF && s_ == KS - 1) {  // the 8-column step: this lane half's 8 bytes of chunk 2 s_
+        const uint2 x = reinterpret_cast<const uint2*>(T)[(row * KN_CH + ((2 * s_) ^ (row & 15))) * 2 + h];
+        F[g] = __builtin_bit_cast(bf16x8, make_uint4(x.x, x.y, 0u, 0u));
+      } else {
+        F[g] = __builtin_bit_cast(bf16x8, T[row * KN_CH + ((2 * s_ + h) ^ (row & 15))]);
+      }
     };
 #pragma unroll
     for (int g = 0; g < AHEAD; ++g) ld(g);
@@ -285,8 +302,14 @@ __global__ __launch_bounds__(KN_T) void k_knn_main(const uint4* __restrict__ ite
       const int b = g / KS, s = g % KS, c = b & 1;
       if (g + AHEAD < NSTEP) ld(g + AHEAD);
       if (s == 0) { acc[c][0] = {}; acc[c][1] = {}; }
-      acc[c][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[g], bqa[s], acc[c][0], 0, 0, 0);
-      acc[c][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[g], bqb[s], acc[c][1], 0, 0, 0);
+      if (HALF && s == KS - 1) {  // v_mfma_f32_32x32x8_bf16 over the last 8 columns
+        const s16x4 fa = lo4(F[g]);
+        acc[c][0] = __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(fa, lo4(bqa[s]), acc[c][0], 0, 0, 0);
+        acc[c][1] = __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(fa, lo4(bqb[s]), acc[c][1], 0, 0, 0);
+      } else {
+        acc[c][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[g], bqa[s], acc[c][0], 0, 0, 0);
+        acc[c][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[g], bqb[s], acc[c][1], 0, 0, 0);
+      }
       if (s == KS - 1) drain(acc[c ^ 1][0], acc[c ^ 1][1], t * KN_IT + (int64_t)(b - 1) * 32);
     }
   }
@@ -465,11 +488,13 @@ int ottohip_knn_topk(ottohip_ctx* c, const ottohip_knn_index* ix, const int32_t*
   const int64_t nT = ceil_div(ix->n_items, KN_IT);
   float* thr = nullptr;
   const bool k8 = ix->dim + 2 > 7 * 16;
+  // the 8-column last k-step (OTTOHIP_KNN_HALF=0: seven 16-column steps; read per call)
+  const bool half = !k8 && ix->dim + 2 <= 6 * 16 + 8 && !(getenv("OTTOHIP_KNN_HALF") && !strcmp(getenv("OTTOHIP_KNN_HALF"), "0"));
   if (!abl && !nopre && (nT - 1) / pst >= KN_C) {  // enough sampled tiles for KN_C groups
     OH_TRY(ctx->ws.get("knn_thr", (size_t)n_q, &thr));
     const int64_t nS = (nT - 1 + pst - 1) / pst;
     ph = ctx->begin("knn_pre", s, 2.0 * (double)n_q * (double)(nS * KN_IT) * ix->dim);
-    (k8 ? k_knn_main<2, 8> : k_knn_main<2, 7>)<<<grid, KN_T, 0, s>>>(reinterpret_cast<const uint4*>(ix->packed), ix->n_items,
+    (k8 ? k_knn_main<2, 8> : (half ? k_knn_main<2, 7, false, true> : k_knn_main<2, 7>))<<<grid, KN_T, 0, s>>>(reinterpret_cast<const uint4*>(ix->packed), ix->n_items,
                                           reinterpret_cast<const uint4*>(qp), n_q, cand, thr, pst, nullptr, nullptr);
     ctx->end(ph, s);
   }
@@ -485,7 +510,7 @@ int ottohip_knn_topk(ottohip_ctx* c, const ottohip_knn_index* ix, const int32_t*
     OH_TRY(ctx->ws.get("knn_ncand", (size_t)n_q, &ncand));
     OH_TRY(ctx->ws.get("knn_ovf", 1, &ovf));
     OH_HIP(hipMemsetAsync(ovf, 0, sizeof(int), s));
-    (k8 ? k_knn_main<0, 8, true> : k_knn_main<0, 7, true>)<<<grid, KN_T, 0, s>>>(
+    (k8 ? k_knn_main<0, 8, true> : (half ? k_knn_main<0, 7, true, true> : k_knn_main<0, 7, true>))<<<grid, KN_T, 0, s>>>(
         reinterpret_cast<const uint4*>(ix->packed), ix->n_items, reinterpret_cast<const uint4*>(qp), n_q, cand, thr, pst,
         cbuf, ncand);
     ctx->end(ph, s);
@@ -500,7 +525,7 @@ int ottohip_knn_topk(ottohip_ctx* c, const ottohip_knn_index* ix, const int32_t*
   }
   if (!done) {
     auto kmain = k8 ? (abl == 3 ? k_knn_main<3, 8> : (abl ? k_knn_main<1, 8> : k_knn_main<0, 8>))
-                    : (abl == 3 ? k_knn_main<3, 7> : (abl ? k_knn_main<1, 7> : k_knn_main<0, 7>));
+                    : (abl == 3 ? k_knn_main<3, 7> : (abl ? k_knn_main<1, 7> : (half ? k_knn_main<0, 7, false, true> : k_knn_main<0, 7>)));
     kmain<<<grid, KN_T, 0, s>>>(reinterpret_cast<const uint4*>(ix->packed), ix->n_items,
                                 reinterpret_cast<const uint4*>(qp), n_q, cand, thr, pst, nullptr, nullptr);
     ctx->end(ph, s);
