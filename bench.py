@@ -202,7 +202,7 @@ def bench_knn(steps: int, warmup: int, n_items: int, n_q: int, with_cpu: bool, g
                         "frac": flops / (main_ms / 1e3) / 1e12 / MFMA_BF16_PEAK_TFLOPS,
                         "traffic": pmc_traffic("k_knn_main") if n_items == 1_855_603 and n_mine == 600_000 else None,
                         "traffic_note": "HBM/fabric bytes per launch (every 512-query workgroup streams the item matrix)",
-                        "flops_model": "2*Q*V*100 (K padding to 128 and the top-k epilogue not counted)",
+                        "flops_model": "2*Q*V*100 (the padded K (104 for dim 100: the +-norm columns and zeros) and the top-k epilogue not counted)",
                         # the whole search (pre-pass, main pass, candidate selection, rerank) on the same flops
                         "search_ms": sum(ph.values()),
                         "search_frac": flops / (sum(ph.values()) / 1e3) / 1e12 / MFMA_BF16_PEAK_TFLOPS if ph else None},
