@@ -539,7 +539,9 @@ def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTabl
         recs.append(torch.stack([a, b, c, torch.zeros_like(c)], 1))
         t.free()
         mark("part_finalize")
-    r = torch.cat(recs) if recs else torch.zeros((0, 4), dtype=torch.int32, device=events.aid.device)
+    # one part-heads tensor (the one-count path) is merged in place: torch.cat would copy its ~5 GB
+    r = (recs[0] if len(recs) == 1 else torch.cat(recs)) if recs else torch.zeros((0, 4), dtype=torch.int32,
+                                                                                 device=events.aid.device)
     merged = gd.table_from_records(r.contiguous(), [name], n_items, ctx=ctx)
     mark("merge_parts")
     out = merged.finalize(name, max_rows=max_pairs,

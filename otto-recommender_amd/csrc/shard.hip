@@ -277,17 +277,18 @@ __global__ __launch_bounds__(256) void k_grp_big_keys(const uint4* __restrict__ 
 }
 __device__ __forceinline__ uint32_t gm_hash(uint32_t k, uint32_t cm) { return (k * 0x9E3779B1u) >> __clz((int)cm); }  // top bits
 // insert one record into an LDS hash (keys K, sums C / G2); a wrapped sum sets err bit 2
-__device__ __forceinline__ void gm_insert(uint32_t* K, uint32_t* C, uint32_t* G2, uint32_t cm, const uint4& r,
+__device__ __forceinline__ bool gm_insert(uint32_t* K, uint32_t* C, uint32_t* G2, uint32_t cm, const uint4& r,
                                           bool& wrap) {
-  uint32_t h = gm_hash(r.y, cm);
+  uint32_t h = gm_hash(r.y, cm), old;
   while (true) {
-    const uint32_t old = atomicCAS(&K[h], GM_EMPTY, r.y);
+    old = atomicCAS(&K[h], GM_EMPTY, r.y);
     if (old == GM_EMPTY || old == r.y) break;
     h = (h + 1) & cm;
   }
   const uint32_t oc = atomicAdd(&C[h], r.z);
   wrap |= oc + r.z < oc;
   atomicAdd(&G2[h], r.w);
+  return old == GM_EMPTY;  // a new key
 }
 struct GmOut {
   uint8_t* rule;
@@ -373,15 +374,18 @@ __global__ __launch_bounds__(GM_T) void k_grp_merge_wave(const uint4* __restrict
   if (__ballot(wrap) && l == 0) atomicOr(err, 2);
   gm_stats_flush(rows, pairs, n_rules, part, stats);
 }
-// one workgroup per listed group of (GM_WAVE_MAX, GM_BLOCK_MAX] records; the big groups' slot ranges get rule 0xFF
+// one workgroup per listed group above GM_WAVE_MAX records; a group above GM_BLOCK_MAX whose distinct keys overflow
+// the hash gets rule 0xFF over its range and ovf[g] = its length (the sort path takes it)
 __global__ __launch_bounds__(GM_T) void k_grp_merge_block(const uint4* __restrict__ rec, const uint32_t* __restrict__ gs,
                                                           const uint32_t* __restrict__ mid,
                                                           const unsigned long long* __restrict__ n_mid, int n_rules, GmOut O,
+                                                          uint32_t* __restrict__ ovf, int opt,
                                                           unsigned long long* __restrict__ stats, int* __restrict__ err) {
   __shared__ uint32_t K[GM_BLOCK_CAP], C[GM_BLOCK_CAP], G2[GM_BLOCK_CAP];
   __shared__ unsigned long long part[MAX_RULES * 2];
   __shared__ uint32_t wt[GM_T / 64];
   __shared__ unsigned long long wps[GM_T / 64];
+  __shared__ uint32_t nocc;
   const int w = threadIdx.x >> 6;
   const uint32_t l = lane_id();
   for (uint32_t e = threadIdx.x; e < GM_BLOCK_CAP; e += GM_T) { K[e] = GM_EMPTY; C[e] = 0; G2[e] = 0; }
@@ -392,14 +396,32 @@ __global__ __launch_bounds__(GM_T) void k_grp_merge_block(const uint4* __restric
   const int64_t nm = (int64_t)*n_mid;
   for (int64_t t = blockIdx.x; t < nm; t += gridDim.x) {  // block-uniform
     const uint32_t g = mid[t], s0 = gs[g], L = gs[g + 1] - s0;
-    if (L > GM_BLOCK_MAX) {
-      for (uint32_t j = threadIdx.x; j < L; j += GM_T) O.rule[s0 + j] = 0xFF;
-      continue;
-    }
     uint32_t cap = 64;
-    while (cap < 2 * L) cap <<= 1;
+    while (cap < 2 * L && cap < GM_BLOCK_CAP) cap <<= 1;
     const uint32_t cm = cap - 1;
-    for (uint32_t j = threadIdx.x; j < L; j += GM_T) gm_insert(K, C, G2, cm, rec[s0 + j], wrap);
+    if (L <= GM_BLOCK_MAX) {
+      for (uint32_t j = threadIdx.x; j < L; j += GM_T) gm_insert(K, C, G2, cm, rec[s0 + j], wrap);
+    } else {
+      // optimistic: a big group whose distinct keys stay under 3/4 of the table merges here (at most GM_T new
+      // keys per batch after the check, so the probe always finds a slot); else it goes to the sort path
+      if (threadIdx.x == 0) nocc = 0;
+      __syncthreads();
+      bool full = false;
+      for (uint32_t j0 = 0; j0 < L; j0 += GM_T) {  // block-uniform
+        if (!opt || nocc > GM_BLOCK_CAP / 4 * 3) { full = true; break; }
+        const uint32_t j = j0 + threadIdx.x;
+        const uint32_t nw = wave_sum(j < L && gm_insert(K, C, G2, cm, rec[s0 + j], wrap) ? 1u : 0u);
+        if (l == 0 && nw) atomicAdd(&nocc, nw);
+        __syncthreads();
+      }
+      if (full) {
+        for (uint32_t e = threadIdx.x; e < cap; e += GM_T) { K[e] = GM_EMPTY; C[e] = 0; G2[e] = 0; }
+        for (uint32_t j = threadIdx.x; j < L; j += GM_T) O.rule[s0 + j] = 0xFF;
+        if (threadIdx.x == 0) ovf[g] = L;
+        __syncthreads();
+        continue;
+      }
+    }
     const uint32_t x0 = rec[s0].x;
     __syncthreads();
     uint32_t u = 0;
@@ -573,16 +595,7 @@ int ottohip_table_from_records(ottohip_ctx* ctx, const void* records, int64_t n,
     k_grp_classify<<<grid_for((int64_t)G), 256, 0, s>>>(gs, (int64_t)G, big, mid, n_mid);
     if ((rc = exclusive_scan_u32(ctx, big, bbo, (int64_t)G, tot, s)) || (rc = d2h(&n_big, tot, 1, s))) return fail(rc);
     ctx->end(ph, s);
-    if (n_big) {
-      ph = ctx->begin("merge_sort", s, 16.0 * n_big);
-      k_grp_big_keys<<<grid_for((int64_t)n_big), 256, 0, s>>>(rec, gs, (int64_t)G, bbo, n_big, k0, v0);
-      uint32_t *k = k0, *v = v0;
-      if ((rc = radix_sort_pairs(ctx, k, v, k1, v1, (int64_t)n_big, A, s))) return fail(rc);
-      k_rec_gather<<<grid_for((int64_t)n_big), 256, 0, s>>>(rec, v, (int64_t)n_big, srt, head);
-      if ((rc = exclusive_scan_u32(ctx, head, idx, (int64_t)n_big, tot, s)) || (rc = d2h(&U_big, tot, 1, s))) return fail(rc);
-      ctx->end(ph, s);
-    }
-    U = (uint64_t)n + U_big;  // slots: the groups' own ranges, then the big groups' rows
+    U = (uint64_t)n + n_big;  // slots: the groups' own ranges, then room for the overflowing big groups' rows
   } else {
     // any order (records received from several ranks): LSD sort by (rule, aid, aid_next) on a permutation
     ctx->end(ph, s);
@@ -609,15 +622,35 @@ int ottohip_table_from_records(ottohip_ctx* ctx, const void* records, int64_t n,
     ctx->spare.release();
     if ((rc = T->b.alloc(std::max<uint64_t>(U, 1)))) return fail(rc);
   }
-  const unsigned rgrid_n = (unsigned)std::min<int64_t>(ceil_div(grouped ? (int64_t)n_big : n, 256), (int64_t)ctx->n_cu * 8);
+  const unsigned rgrid_n = (unsigned)std::min<int64_t>(ceil_div(n, 256), (int64_t)ctx->n_cu * 8);
   if (grouped) {
     const GmOut O{T->b.rule, T->b.aid, T->b.aid_next, T->b.count, T->b.count_ge2};
     k_grp_merge_wave<<<(unsigned)std::min<int64_t>(ceil_div((int64_t)G, 4), (int64_t)ctx->n_cu * 8), GM_T, 0, s>>>(
         rec, gs, (int64_t)G, n_rules, O, stats, err);
-    k_grp_merge_block<<<(unsigned)ctx->n_cu * 3, GM_T, 0, s>>>(rec, gs, mid, n_mid, n_rules, O, stats, err);
-    if (n_big)
-      k_rec_reduce<<<rgrid_n, 256, 0, s>>>(srt, (int64_t)n_big, head, idx, n_rules, T->b.rule + n, T->b.aid + n,
-                                           T->b.aid_next + n, T->b.count + n, T->b.count_ge2 + n, stats, err);
+    // big groups whose keys overflow the workgroup hash: ovf[g] = length (the big-length array, scanned above)
+    // OTTOHIP_MERGE_OPT=0 (read per call): every big group takes the sort path
+    const char* oenv = getenv("OTTOHIP_MERGE_OPT");
+    const int opt = (oenv && atoi(oenv) == 0) ? 0 : 1;
+    uint32_t* ovf = big;
+    uint64_t* bbo;
+    if ((rc = ws.get("mg_bbo", (size_t)G, &bbo))) return fail(rc);
+    if (hipMemsetAsync(ovf, 0, (size_t)G * 4, s)) return fail(OTTOHIP_EHIP);
+    k_grp_merge_block<<<(unsigned)ctx->n_cu * 3, GM_T, 0, s>>>(rec, gs, mid, n_mid, n_rules, O, ovf, opt, stats, err);
+    uint64_t n_ovf = 0;
+    if ((rc = exclusive_scan_u32(ctx, ovf, bbo, (int64_t)G, tot, s)) || (rc = d2h(&n_ovf, tot, 1, s))) return fail(rc);
+    if (n_ovf) {
+      ctx->end(ph, s);
+      ph = ctx->begin("merge_sort", s, 16.0 * n_ovf);
+      k_grp_big_keys<<<grid_for((int64_t)n_ovf), 256, 0, s>>>(rec, gs, (int64_t)G, bbo, n_ovf, k0, v0);
+      uint32_t *k = k0, *v = v0;
+      if ((rc = radix_sort_pairs(ctx, k, v, k1, v1, (int64_t)n_ovf, A, s))) return fail(rc);
+      k_rec_gather<<<grid_for((int64_t)n_ovf), 256, 0, s>>>(rec, v, (int64_t)n_ovf, srt, head);
+      if ((rc = exclusive_scan_u32(ctx, head, idx, (int64_t)n_ovf, tot, s)) || (rc = d2h(&U_big, tot, 1, s))) return fail(rc);
+      k_rec_reduce<<<(unsigned)std::min<int64_t>(ceil_div((int64_t)n_ovf, 256), (int64_t)ctx->n_cu * 8), 256, 0, s>>>(
+          srt, (int64_t)n_ovf, head, idx, n_rules, T->b.rule + n, T->b.aid + n, T->b.aid_next + n, T->b.count + n,
+          T->b.count_ge2 + n, stats, err);
+    }
+    U = (uint64_t)n + U_big;
   } else {
     k_rec_reduce<<<rgrid_n, 256, 0, s>>>(srt, n, head, idx, n_rules, T->b.rule, T->b.aid, T->b.aid_next, T->b.count,
                                          T->b.count_ge2, stats, err);

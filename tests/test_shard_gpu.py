@@ -224,17 +224,19 @@ def test_reduce_received_rejects_inconsistent_pieces(gpu):
         gd.reduce_received(words, pieces, NAMES, 1)
 
 
-@pytest.mark.parametrize("grouped", ["1", "0"])
-def test_from_records_ordered_groups(gpu, monkeypatch, grouped):
+@pytest.mark.parametrize("grouped,opt", [("1", "1"), ("1", "0"), ("0", "1")])
+def test_from_records_ordered_groups(gpu, monkeypatch, grouped, opt):
     """Records in (rule, aid) order (as the A6 part heads leave them) merge per (rule, aid) group: groups of
-    one wave's size, of one workgroup's size and above it (the sort path into the slots after the groups'
-    ranges) all equal a numpy groupby-sum; OTTOHIP_MERGE_GROUPS=0 forces the sort path on the same input."""
+    one wave's size, of one workgroup's size and above it -- few distinct keys (the workgroup hash) or many
+    (the sort path into the slots after the groups' ranges) -- all equal a numpy groupby-sum;
+    OTTOHIP_MERGE_OPT=0 sends every big group to the sort path, OTTOHIP_MERGE_GROUPS=0 all records."""
     import torch
     from otto_recommender_amd import dist as gd
     monkeypatch.setenv("OTTOHIP_MERGE_GROUPS", grouped)
+    monkeypatch.setenv("OTTOHIP_MERGE_OPT", opt)
     rng = np.random.default_rng(7)
     sizes = np.concatenate([rng.integers(1, 40, 3000), rng.integers(200, 2100, 60), [2049, 2048, 257, 256],
-                            rng.integers(2100, 30000, 6)])
+                            rng.integers(2100, 30000, 10)])
     rng.shuffle(sizes)
     n_items = 50_000
     rule = np.sort(rng.integers(0, len(NAMES), len(sizes)))
@@ -244,7 +246,8 @@ def test_from_records_ordered_groups(gpu, monkeypatch, grouped):
         aid[k] = np.sort(rng.choice(n_items, int(k.sum()), replace=False))
     g_rule, g_aid = np.repeat(rule, sizes), np.repeat(aid, sizes)
     # few distinct aid_next per group: long runs of duplicates, and hot groups with many distinct keys
-    span = np.repeat(np.where(sizes > 2000, n_items, np.maximum(2, sizes // 3)), sizes)
+    big_span = np.where(np.arange(len(sizes)) % 2 == 0, n_items, 1500)  # big groups: many or few distinct keys
+    span = np.repeat(np.where(sizes > 2000, big_span, np.maximum(2, sizes // 3)), sizes)
     nxt = rng.integers(0, 1 << 30, len(g_aid)) % span
     cnt = rng.integers(1, 1000, len(g_aid)).astype(np.uint32)
     ge2 = np.where(cnt >= 2, cnt, 0).astype(np.uint32)
