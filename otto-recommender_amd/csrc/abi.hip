@@ -1214,6 +1214,57 @@ __global__ void k_keys_at(const uint32_t* __restrict__ perm, const uint32_t* __r
   keys[i] = ((uint64_t)sa[j] << 32) | sb[j];
 }
 
+// *uns = 1 where a compacted aid column descends (a rule's rows in slot order are in aid order when the
+// table came from one count and the rule keeps both directions, e.g. every part of a part-mode table)
+__global__ void k_sorted_check(const uint32_t* __restrict__ a, int64_t m, int* __restrict__ uns) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
+  if (i < m && a[i] < a[i - 1]) *uns = 1;
+}
+// one block per index of aid-ordered rows (sa ascending): the idx-th row in (aid, aid_next) order has aid
+// sa[idx], and its aid_next is the (idx - g0)-th smallest aid_next of that aid's rows [g0, g1): a radix select
+// (8 bits per pass over the group) instead of sorting every row of the rule
+__global__ __launch_bounds__(256) void k_keys_at_sel(const uint32_t* __restrict__ sa, const uint32_t* __restrict__ sb,
+                                                     int64_t m, const int64_t* __restrict__ idx,
+                                                     uint64_t* __restrict__ keys) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t s_prefix, s_k;
+  __shared__ int64_t s_g0, s_g1;
+  const int64_t r = idx[blockIdx.x];
+  const uint32_t a = sa[r];
+  if (threadIdx.x == 0) {
+    int64_t lo = 0, hi = r;  // first row of aid a
+    while (lo < hi) { const int64_t md = (lo + hi) >> 1; if (sa[md] < a) lo = md + 1; else hi = md; }
+    s_g0 = lo;
+    lo = r + 1; hi = m;  // first row past aid a
+    while (lo < hi) { const int64_t md = (lo + hi) >> 1; if (sa[md] <= a) lo = md + 1; else hi = md; }
+    s_g1 = lo;
+    s_k = (uint32_t)(r - s_g0);
+    s_prefix = 0;
+  }
+  __syncthreads();
+  const int64_t g0 = s_g0, g1 = s_g1;
+  uint32_t mask = 0;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    hist[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t prefix = s_prefix;
+    for (int64_t j = g0 + threadIdx.x; j < g1; j += blockDim.x) {
+      const uint32_t v = sb[j];
+      if ((v & mask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t k = s_k, d = 0;
+      while (hist[d] <= k) { k -= hist[d]; ++d; }
+      s_k = k;
+      s_prefix = prefix | (d << shift);
+    }
+    mask |= 255u << shift;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) keys[blockIdx.x] = ((uint64_t)a << 32) | s_prefix;
+}
+
 int ottohip_table_keys_at(ottohip_ctx* ctx, const ottohip_table* t, int rule, int use_ge2, const int64_t* idx,
                           int n_idx, uint64_t* keys, void* stream) {
   if (!ctx || !t || rule < 0 || rule >= t->n_rules || n_idx < 0 || (n_idx > 0 && (!idx || !keys))) {
@@ -1256,6 +1307,21 @@ int ottohip_table_keys_at(ottohip_ctx* ctx, const ottohip_table* t, int rule, in
   k_blk_compact<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n,
                                                rule, use_ge2 ? 1 : 0, use_ge2 ? 1u : 0u, t->sym(rule), boff, sa, sb,
                                                nullptr, nullptr);
+  OH_HIP(hipMemcpyAsync(didx, idx, (size_t)n_idx * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  if (!t->sym(rule)) {  // rows already in aid order (one count): a select per index, no sort
+    int* uns;
+    OH_TRY(ws.get("ka_uns", 1, &uns));
+    OH_HIP(hipMemsetAsync(uns, 0, sizeof(int), s));
+    k_sorted_check<<<grid_for((int64_t)m), 256, 0, s>>>(sa, (int64_t)m, uns);
+    int hu = 1;
+    OH_TRY(d2h(&hu, uns, 1, s));
+    if (!hu) {
+      k_keys_at_sel<<<(unsigned)n_idx, 256, 0, s>>>(sa, sb, (int64_t)m, didx, dkeys);
+      OH_HIP(hipGetLastError());
+      OH_TRY(d2h(keys, dkeys, (size_t)n_idx, s));
+      return 0;
+    }
+  }
   // LSD: aid_next, then aid (stable) -> (aid, aid_next) ascending
   const int abits = std::max(1, bits_for((uint64_t)t->n_items));
   uint32_t *k = k0, *v = v0;
@@ -1265,7 +1331,6 @@ int ottohip_table_keys_at(ottohip_ctx* ctx, const ottohip_table* t, int rule, in
   k_gather_key<<<grid_for((int64_t)m), 256, 0, s>>>(sa, v, (int64_t)m, 0, kn);
   k = kn;
   OH_TRY(radix_sort_pairs(ctx, k, v, k == k0 ? k1 : k0, v == v0 ? v1 : v0, (int64_t)m, abits, s));
-  OH_HIP(hipMemcpyAsync(didx, idx, (size_t)n_idx * sizeof(int64_t), hipMemcpyHostToDevice, s));
   k_keys_at<<<grid_for(n_idx), 256, 0, s>>>(v, sa, sb, didx, n_idx, dkeys);
   OH_HIP(hipGetLastError());
   OH_TRY(d2h(keys, dkeys, (size_t)n_idx, s));
