@@ -2996,12 +2996,22 @@ __device__ __forceinline__ uint32_t ph_keep16(const uint8_t* __restrict__ rule, 
   const uint32_t need = tie | (want_ab ? keep : 0u);
   if (!need) return keep;
   ld_groups(reinterpret_cast<const uint32_t*>(a), i, n, need, S.A);
-  ld_groups(reinterpret_cast<const uint32_t*>(b), i, n, need, S.B);
+  // aid_next decides only the tie rows of the cut aid (few): without the outputs, B is read for their groups only
+  uint32_t eq = 0;
 #pragma unroll
   for (int s = 0; s < SLOTS_T; ++s) {
     if (!((tie >> s) & 1u)) continue;
     const uint32_t p = rule_at(R, s), ai = S.a(s);
-    keep |= (ai < pc.astar[p] || (ai == pc.astar[p] && S.b(s) <= pc.nstar[p]) ? 1u : 0u) << s;
+    keep |= (ai < pc.astar[p] ? 1u : 0u) << s;
+    eq |= (ai == pc.astar[p] ? 1u : 0u) << s;
+  }
+  const uint32_t needb = want_ab ? need : eq;
+  if (!needb) return keep;
+  ld_groups(reinterpret_cast<const uint32_t*>(b), i, n, needb, S.B);
+#pragma unroll
+  for (int s = 0; s < SLOTS_T; ++s) {
+    if (!((eq >> s) & 1u)) continue;
+    keep |= (S.b(s) <= pc.nstar[rule_at(R, s)] ? 1u : 0u) << s;
   }
   return keep;
 }
