@@ -536,6 +536,12 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     OH_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_split_mean), &v, sizeof v, 0, hipMemcpyHostToDevice, s));
     OH_HIP(hipStreamSynchronize(s));
   }
+  static const char* runs_env = getenv("OTTOHIP_SPLIT_RUNS");  // A/B switch
+  if (runs_env && !strcmp(runs_env, "1")) {
+    const uint32_t v = 1;
+    OH_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_split_runs), &v, sizeof v, 0, hipMemcpyHostToDevice, s));
+    OH_HIP(hipStreamSynchronize(s));
+  }
   static const char* fuse_env = getenv("OTTOHIP_SPLIT_FUSE");  // A/B switch
   if (fuse_env && !strcmp(fuse_env, "0")) {
     const uint32_t v = 0;

@@ -197,6 +197,26 @@ __device__ __forceinline__ uint32_t lane_prev(uint32_t v) {
 __device__ __forceinline__ uint32_t lane_next(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);  // wave_shl:1
 }
+// LDS histogram add of digit d by a wave whose valid lanes form a prefix: runs of equal digits over consecutive
+// lanes (consecutive words; a hot key's words arrive in runs, so one digit can fill a wave) take one atomic of
+// the run length at the run's first lane; returns the lane's rank among the digit's words (same-address LDS
+// atomics of one wave instruction serialise). Wave-uniform call.
+__device__ __forceinline__ uint32_t lds_add_runs(uint32_t* h, uint32_t d, bool valid) {
+  const uint32_t l = lane_id();
+  const uint32_t pd = lane_prev(d);
+  const bool head = valid && (l == 0u || pd != d);
+  const uint64_t hm = __ballot(head);
+  const uint32_t nv = (uint32_t)__popcll(__ballot(valid));
+  const uint64_t le = l == 63u ? ~0ull : ((2ull << l) - 1ull);
+  const uint64_t after = hm & ~le;
+  const uint32_t nh = after ? (uint32_t)__ffsll((long long)after) - 1u : 64u;
+  const uint32_t end = nh < nv ? nh : nv;
+  uint32_t base = head ? atomicAdd(&h[d], end - l) : 0u;
+  const uint64_t upto = hm & le;
+  const int hl = upto ? 63 - __clzll((long long)upto) : 0;
+  base = (uint32_t)__shfl((int)base, hl);
+  return valid ? base + (l - (uint32_t)hl) : 0u;
+}
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) { return dpp_incl_scan<false>(v); }
 __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v) {

@@ -28,6 +28,8 @@ constexpr int LCAP = 512;         // sessions up to LCAP events run from LDS
 constexpr int SPLIT_MEAN = 420;   // hashed split buckets average at most this many words (register sorts only)
 constexpr int LDS_SPLIT_MEAN = 2560;  // the same with the LDS leaf (k_agg_lds takes buckets of <= 4096 words)
 __constant__ uint32_t c_split_mean = SPLIT_MEAN;  // OTTOHIP_SPLIT_MEAN overrides it (A/B switch, abi.hip)
+__constant__ uint32_t c_split_runs = 0;  // split histograms fold runs of equal digits over lanes (OTTOHIP_SPLIT_RUNS=1; measured
+                                          // +0.9 ms reduce: the extra VALU outweighs the few runs)
 __constant__ uint32_t c_split_fuse = 1;  // one-chunk split tasks counted inside k_split_scatter (OTTOHIP_SPLIT_FUSE=0: off)
 __constant__ uint32_t c_hash_prio = 0;  // OTTOHIP_HASH_PRIO: wave priority of the LDS-hash leaves (A/B switch)
 __constant__ uint32_t c_lds_leaf = 0;   // rows / split buckets of (SORT_MAX, LDS_CAP] words go to k_agg_lds (abi.hip)
@@ -2230,7 +2232,8 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_hist(const Task* __restrict__
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      if (i0 + threadIdx.x + j * SPLIT_T < c1) atomicAdd(&h[split_digit(wr[j], F, T.rem, nd)], 1u);
+      if (c_split_runs) lds_add_runs(h, split_digit(wr[j], F, T.rem, nd), i0 + threadIdx.x + j * SPLIT_T < c1);
+      else if (i0 + threadIdx.x + j * SPLIT_T < c1) atomicAdd(&h[split_digit(wr[j], F, T.rem, nd)], 1u);
   }
   __syncthreads();
   for (uint32_t d = threadIdx.x; d < nd; d += SPLIT_T) hmat[mat_base[t] + (uint64_t)d * nch + c] = h[d];
@@ -2276,7 +2279,8 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        if (i0 + tid + j * SPLIT_T < c1) atomicAdd(&h[split_digit(wr[j], F, T.rem, nd)], 1u);
+        if (c_split_runs) lds_add_runs(h, split_digit(wr[j], F, T.rem, nd), i0 + tid + j * SPLIT_T < c1);
+        else if (i0 + tid + j * SPLIT_T < c1) atomicAdd(&h[split_digit(wr[j], F, T.rem, nd)], 1u);
     }
     __syncthreads();
     uint32_t v[DPT], tsum = 0;
@@ -2318,7 +2322,8 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
 #pragma unroll
     for (int j = 0; j < SUB_PER_T; ++j) {
       dg[j] = split_digit(wr[j], F, T.rem, nd);
-      rk[j] = tid + j * SPLIT_T < m ? atomicAdd(&h[dg[j]], 1u) : 0u;
+      if (c_split_runs) rk[j] = lds_add_runs(h, dg[j], tid + j * SPLIT_T < m);
+      else rk[j] = tid + j * SPLIT_T < m ? atomicAdd(&h[dg[j]], 1u) : 0u;
     }
     __syncthreads();
     {  // exclusive scan of h over the digits -> st (thread t: digits DPT t .. DPT t + DPT - 1)

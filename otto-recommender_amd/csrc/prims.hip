@@ -113,7 +113,7 @@ __global__ __launch_bounds__(RS_T) void k_rs_hist(const uint32_t* __restrict__ k
 #pragma unroll 4
   for (int r = 0; r < RS_R * RS_SUB; ++r) {
     const int64_t idx = t0 + r * RS_T + threadIdx.x;
-    if (idx < n) atomicAdd(&h[w][(keys[idx] >> shift) & 255u], 1u);
+    lds_add_runs(h[w], idx < n ? (keys[idx] >> shift) & 255u : 0u, idx < n);  // runs of one digit: one atomic
   }
   __syncthreads();
   for (int d = threadIdx.x; d < 256; d += RS_T) {
