@@ -330,6 +330,14 @@ int ottohip_kmeans_update(ottohip_ctx* ctx, float* centroids, const int64_t* sum
  * counts, then update (sklearn relocates before the M-step). */
 int ottohip_kmeans_lloyd_iter(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* centroids, int k,
                               int32_t* labels, int64_t* sums, int64_t* counts, double* out, void* stream);
+/* Half-precision rows of a KMeans matrix (C2's E-step reads 208 B per row instead of 400 at dim 100): f16
+ * copies of X's rows and their exact f32 squared norms are kept in the context, and lloyd_steps on this same X
+ * (pointer, n, dim) scores with them; rows whose two best clusters are too close for the f16 scores go to the
+ * exact f32 kernel, so labels are those of the f32 E-step. X must not change until detach_half (or ctx_trim).
+ * Replaces nothing in the reference (sklearn's float64 Lloyd, model/kmeans_sessions.py:152-159): a device
+ * data-layout step of the same labels. OTTOHIP_KM_H16=0 ignores the attached rows. */
+int ottohip_kmeans_attach_half(ottohip_ctx* ctx, const float* X, int64_t n, int dim, void* stream);
+int ottohip_kmeans_detach_half(ottohip_ctx* ctx);
 /* Up to max_steps lloyd_iter steps with a single device->host copy: after each step the device
  * applies sklearn's stop checks (no label changed; shift^2 <= tol; an empty cluster, which leaves
  * the centroids untouched for the host's relocation) and the later steps do nothing. out (HOST

@@ -117,6 +117,8 @@ SIGNATURES = {
     "ottohip_rs_destroy": (None, [_VP]),
     "ottohip_kmeans_lloyd_iter": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP, ctypes.c_int, _VP, _VP, _VP,
                                                  ctypes.POINTER(ctypes.c_double), _VP]),
+    "ottohip_kmeans_attach_half": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP]),
+    "ottohip_kmeans_detach_half": (ctypes.c_int, [_VP]),
     "ottohip_kmeans_lloyd_steps": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP, ctypes.c_int, _VP, _VP, _VP,
                                                   ctypes.c_int, ctypes.c_double, ctypes.POINTER(ctypes.c_double), _VP]),
     "ottohip_kmeans_lloyd_steps_pair": (ctypes.c_int, [_VP, _VP, _I64, ctypes.c_int, _VP, ctypes.c_int, _VP, _VP,

@@ -831,6 +831,7 @@ int ottohip_ctx_trim(ottohip_ctx* ctx) {
   ctx->spare.release();
   dev_trim();
   ctx->km_bvalid = false;  // the KMeans distance bounds lived in the released workspace
+  ctx->km_hX = nullptr;     // and the attached half-precision rows
   return 0;
 }
 

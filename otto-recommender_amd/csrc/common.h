@@ -124,6 +124,13 @@ struct Ctx {
   int64_t km_bn = -1;
   int km_bdim = 0, km_bk = 0;
   bool km_bvalid = false;
+  // half-precision rows of an attached KMeans matrix (ottohip_kmeans_attach_half): the E-step of
+  // ottohip_kmeans_lloyd_steps on that X reads them (and the rows' exact squared norms) instead of the f32 rows
+  const void* km_hX = nullptr;
+  int64_t km_hn = -1;
+  int km_hdim = 0;
+  const void* km_x16 = nullptr;
+  const float* km_xn2 = nullptr;
 };
 
 inline int bits_for(uint64_t n_values) {  // bits needed to store values in [0, n_values)

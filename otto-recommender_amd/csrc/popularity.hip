@@ -487,6 +487,41 @@ __device__ __forceinline__ void km_split8(const float (&v)[8], uint4& hi, uint4&
 // get lb = 0 (scored again next step). Every bound is rounded outwards (relative 2^-20 / 1e-6).
 constexpr float KMB_SKIP = 2e-4f;
 constexpr float KMB_ERR = 2e-4f;
+// Half-precision E-step (H16: the rows as f16, xh = RN_f16(x), |x - xh| <= 2^-11 |x| + 2^-25 per element; c = ch + cl
+// in f16 within 2^-22 |c| + 2^-25): x.c ~ xh.ch + xh.cl on v_mfma_f32_32x32x16_f16 (products exact, f32 sums of 224
+// terms) is off by <= (2^-11 + 1.4e-5) |x| |c| + 3e-7 (|x| + |c|), a score by twice that: 1.01e-3 |x| |c| + 6e-7
+// (|x| + |c|). Decided when the two smallest scores differ by more than twice the sum with the exact kernel's
+// 1.5e-5 |x||c|, kept with a 2x margin: KMH_SEP = 4.1e-3 (|x| cmax) + KMH_ABS = 2.5e-6 (|x| + cmax). About 5 % of
+// the rows on session embeddings are then near ties (6e-4 for the bf16 split: ~1 %), scored by the exact kernel,
+// but every row reads 208 B instead of 400. The rows' squared norms are exact f32 sums (ottohip_kmeans_attach_half).
+constexpr float KMH_SEP = 4.1e-3f;
+constexpr float KMH_ABS = 2.5e-6f;
+constexpr float KMH_ERR = 1.2e-3f;  // score error bound for the rebuilt distance bounds (cmax (|x| + cmax) units)
+constexpr int KMH_AMB = 8192;       // near-tie rows staged per block (~5 % of a block's ~50 k rows)
+__global__ void k_km_half_rows(const float* __restrict__ X, int64_t n, int dim, int kc, uint4* __restrict__ X16,
+                               float* __restrict__ xn2) {
+  // one wave per row: lanes over the row's 16-B f16 chunks (kc per row, zero padded past dim), squared norm by
+  // a wave sum of the f32 elements
+  const int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int l = threadIdx.x & 63;
+  if (row >= n) return;
+  const float* xp = X + row * dim;
+  float ss = 0.f;
+  if (l < kc) {
+    _Float16 h[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d = 8 * l + j;
+      const float v = d < dim ? xp[d] : 0.f;
+      ss += v * v;
+      h[j] = (_Float16)v;
+    }
+    X16[row * kc + l] = __builtin_bit_cast(uint4, h);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
+  if (l == 0) xn2[row] = ss;
+}
 // dl: [0, 64) delta_j, [64] largest delta, [65] second largest, [66] its cluster (as float), [67] cmax
 __global__ void k_km_delta(const float* __restrict__ C, float* __restrict__ Cp, const float* __restrict__ cn,
                            int k, int dim, int force, float* __restrict__ dl, const int* __restrict__ gate,
@@ -591,7 +626,20 @@ __global__ __launch_bounds__(256) void k_km_filter(int64_t n, int k, const int32
 }
 
 // BL: score the rows erows[0, *n_eval) (k_km_filter's list) and rebuild their bounds
-template <int NB, int KS, bool BL = false>
+typedef _Float16 km_f16x8 __attribute__((ext_vector_type(8)));
+// v = hi + lo + r in f16 (round to nearest), |r| <= 2^-22 |v| + 2^-25
+__device__ __forceinline__ void km_split8_h(const float (&v)[8], uint4& hi, uint4& lo) {
+  _Float16 h[8], r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    h[j] = (_Float16)v[j];
+    r[j] = (_Float16)(v[j] - (float)h[j]);
+  }
+  hi = __builtin_bit_cast(uint4, h);
+  lo = __builtin_bit_cast(uint4, r);
+}
+// H16: the rows from X16 (f16, 2 KS chunks per row) and their squared norms xn2 (ottohip_kmeans_attach_half)
+template <int NB, int KS, bool BL = false, bool H16 = false>
 __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __restrict__ X, int64_t n, int dim,
                                                              const float* __restrict__ C, const float* __restrict__ cn,
                                                              int k, int32_t* __restrict__ label,
@@ -604,15 +652,18 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
                                                              const uint32_t* __restrict__ erows = nullptr,
                                                              const unsigned long long* __restrict__ n_eval = nullptr,
                                                              float* __restrict__ ub = nullptr,
-                                                             float* __restrict__ lb = nullptr) {
+                                                             float* __restrict__ lb = nullptr,
+                                                             const uint4* __restrict__ X16 = nullptr,
+                                                             const float* __restrict__ xn2 = nullptr) {
   if (gate && __builtin_amdgcn_readfirstlane(*gate)) return;
+  constexpr int AMB = H16 ? KMH_AMB : KMS_AMB;
   extern __shared__ unsigned long long smem64[];
   uint4* Cf = reinterpret_cast<uint4*>(smem64);                               // [NB][KS][hi, lo][64]
   unsigned long long* ls = reinterpret_cast<unsigned long long*>(Cf + NB * KS * 2 * 64);  // k * dim sums
   unsigned long long* lc = ls + k * dim;                                       // k counts
   int32_t* labl = reinterpret_cast<int32_t*>(lc + k);                         // [waves][3][32]
   float* cnl = reinterpret_cast<float*>(labl + (KM_MT / 64) * 96);             // [64]
-  uint32_t* amb = reinterpret_cast<uint32_t*>(cnl + 64);                       // [KMS_AMB]
+  uint32_t* amb = reinterpret_cast<uint32_t*>(cnl + 64);                       // [AMB]
   __shared__ uint32_t namb;
   __shared__ unsigned long long abase;
   const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6, h = l >> 5, i32 = l & 31;
@@ -624,7 +675,8 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = (c < k && d0 + j < dim) ? C[(int64_t)c * dim + d0 + j] : 0.f;
     uint4 hi, lo;
-    km_split8(v, hi, lo);
+    if constexpr (H16) km_split8_h(v, hi, lo);
+    else km_split8(v, hi, lo);
     Cf[(sb * 2 + 0) * 64 + ll] = hi;
     Cf[(sb * 2 + 1) * 64 + ll] = lo;
   }
@@ -641,19 +693,30 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
   const int64_t ntile = (nl + 31) >> 5;
   const int64_t nwv = (int64_t)gridDim.x * (KM_MT / 64);
   // the next tile's rows (and its rows' current labels) are loaded while this tile is scored
-  float4 raw[2 * KS];
+  float4 raw[H16 ? 1 : 2 * KS];
+  uint4 raw16[H16 ? KS : 1];
+  float xn_n = 0.f;
   int32_t lab_n = -1;
   int64_t row_n = 0;
   auto load = [&](int64_t tt) __attribute__((always_inline)) {
     const int64_t ri = (tt << 5) + i32 < nl ? (tt << 5) + i32 : nl - 1;
     const int64_t rr = BL ? (int64_t)erows[ri] : ri;
     row_n = rr;
-    const float* xp = X + rr * dim;
+    if constexpr (H16) {
 #pragma unroll
-    for (int s_ = 0; s_ < KS; ++s_) {
-      const int d0 = 16 * s_ + 8 * h;  // dim % 4 == 0: a 16-B piece is all in or all out
-      raw[2 * s_] = d0 < dim ? *reinterpret_cast<const float4*>(xp + d0) : make_float4(0.f, 0.f, 0.f, 0.f);
-      raw[2 * s_ + 1] = d0 + 4 < dim ? *reinterpret_cast<const float4*>(xp + d0 + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int s_ = 0; s_ < KS; ++s_) {
+        const int d0 = 16 * s_ + 8 * h;  // the chunk's zero padding past dim is stored: only wholly-past chunks skip
+        raw16[s_] = d0 < dim ? X16[rr * (2 * KS) + 2 * s_ + h] : make_uint4(0u, 0u, 0u, 0u);
+      }
+      xn_n = xn2[rr];
+    } else {
+      const float* xp = X + rr * dim;
+#pragma unroll
+      for (int s_ = 0; s_ < KS; ++s_) {
+        const int d0 = 16 * s_ + 8 * h;  // dim % 4 == 0: a 16-B piece is all in or all out
+        raw[2 * s_] = d0 < dim ? *reinterpret_cast<const float4*>(xp + d0) : make_float4(0.f, 0.f, 0.f, 0.f);
+        raw[2 * s_ + 1] = d0 + 4 < dim ? *reinterpret_cast<const float4*>(xp + d0 + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
     lab_n = label[rr];
   };
@@ -663,36 +726,56 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
     const int64_t r0 = t << 5;
     const bool in_r = r0 + i32 < nl;
     const int64_t row = row_n;
-    km_bf16x8 xh[KS], xl[KS];
+    km_bf16x8 xh[H16 ? 1 : KS], xl[H16 ? 1 : KS];
+    km_f16x8 xq[H16 ? KS : 1];
     float xs = 0.f;
+    if constexpr (H16) {
 #pragma unroll
-    for (int s_ = 0; s_ < KS; ++s_) {
-      const float4 p0 = raw[2 * s_], p1 = raw[2 * s_ + 1];
-      const float v[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+      for (int s_ = 0; s_ < KS; ++s_) xq[s_] = __builtin_bit_cast(km_f16x8, raw16[s_]);
+      xs = xn_n;
+    } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) xs += v[j] * v[j];
-      uint4 hi, lo;
-      km_split8(v, hi, lo);
-      xh[s_] = __builtin_bit_cast(km_bf16x8, hi);
-      xl[s_] = __builtin_bit_cast(km_bf16x8, lo);
+      for (int s_ = 0; s_ < KS; ++s_) {
+        const float4 p0 = raw[2 * s_], p1 = raw[2 * s_ + 1];
+        const float v[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xs += v[j] * v[j];
+        uint4 hi, lo;
+        km_split8(v, hi, lo);
+        xh[s_] = __builtin_bit_cast(km_bf16x8, hi);
+        xl[s_] = __builtin_bit_cast(km_bf16x8, lo);
+      }
     }
     const int32_t lab_cur = lab_n;
     if (t + nwv < ntile) load(t + nwv);
-    xs += __shfl_xor(xs, 32);
+    if constexpr (!H16) xs += __shfl_xor(xs, 32);
     km_f32x16 acc0 = {}, acc1 = {};
 #pragma unroll
     for (int s_ = 0; s_ < KS; ++s_) {
-      const km_bf16x8 ch0 = __builtin_bit_cast(km_bf16x8, Cf[((0 * KS + s_) * 2 + 0) * 64 + l]);
-      const km_bf16x8 cl0 = __builtin_bit_cast(km_bf16x8, Cf[((0 * KS + s_) * 2 + 1) * 64 + l]);
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, xh[s_], acc0, 0, 0, 0);
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, xl[s_], acc0, 0, 0, 0);
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl0, xh[s_], acc0, 0, 0, 0);
-      if (NB == 2) {
-        const km_bf16x8 ch1 = __builtin_bit_cast(km_bf16x8, Cf[((1 * KS + s_) * 2 + 0) * 64 + l]);
-        const km_bf16x8 cl1 = __builtin_bit_cast(km_bf16x8, Cf[((1 * KS + s_) * 2 + 1) * 64 + l]);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, xh[s_], acc1, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, xl[s_], acc1, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl1, xh[s_], acc1, 0, 0, 0);
+      if constexpr (H16) {  // xh.ch + xh.cl
+        const km_f16x8 ch0 = __builtin_bit_cast(km_f16x8, Cf[((0 * KS + s_) * 2 + 0) * 64 + l]);
+        const km_f16x8 cl0 = __builtin_bit_cast(km_f16x8, Cf[((0 * KS + s_) * 2 + 1) * 64 + l]);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ch0, xq[s_], acc0, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(cl0, xq[s_], acc0, 0, 0, 0);
+        if (NB == 2) {
+          const km_f16x8 ch1 = __builtin_bit_cast(km_f16x8, Cf[((1 * KS + s_) * 2 + 0) * 64 + l]);
+          const km_f16x8 cl1 = __builtin_bit_cast(km_f16x8, Cf[((1 * KS + s_) * 2 + 1) * 64 + l]);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ch1, xq[s_], acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(cl1, xq[s_], acc1, 0, 0, 0);
+        }
+      } else {
+        const km_bf16x8 ch0 = __builtin_bit_cast(km_bf16x8, Cf[((0 * KS + s_) * 2 + 0) * 64 + l]);
+        const km_bf16x8 cl0 = __builtin_bit_cast(km_bf16x8, Cf[((0 * KS + s_) * 2 + 1) * 64 + l]);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, xh[s_], acc0, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, xl[s_], acc0, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl0, xh[s_], acc0, 0, 0, 0);
+        if (NB == 2) {
+          const km_bf16x8 ch1 = __builtin_bit_cast(km_bf16x8, Cf[((1 * KS + s_) * 2 + 0) * 64 + l]);
+          const km_bf16x8 cl1 = __builtin_bit_cast(km_bf16x8, Cf[((1 * KS + s_) * 2 + 1) * 64 + l]);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, xh[s_], acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, xl[s_], acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl1, xh[s_], acc1, 0, 0, 0);
+        }
       }
     }
     // approximate scores |c|^2 - 2 x.c; the smallest, the lowest cluster holding it, the second smallest
@@ -737,10 +820,12 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
       if (NB == 2) m2 = fminf(m2, c0 + 32 == mc ? INFINITY : acc1[r]);
     }
     m2 = fminf(m2, __shfl_xor(m2, 32));
-    const bool decided = m2 - m > KMS_SEP * sqrtf(xs) * cmax;
+    const bool decided = H16 ? m2 - m > KMH_SEP * sqrtf(xs) * cmax + KMH_ABS * (sqrtf(xs) + cmax)
+                             : m2 - m > KMS_SEP * sqrtf(xs) * cmax;
     if (BL && h == 0 && in_r) {  // the row's bounds for these centres (near ties: none, lb = 0)
       const float cm = cmax * 1.000001f;
-      const float e = KMB_ERR * cm * (sqrtf(xs) * 1.0001f + cm);
+      const float e = H16 ? KMH_ERR * cm * (sqrtf(xs) * 1.0001f + cm) + KMH_ABS * (sqrtf(xs) + cm)
+                          : KMB_ERR * cm * (sqrtf(xs) * 1.0001f + cm);
       ub[row] = decided ? sqrtf(fmaxf(m + xs * 1.00001f + e, 0.f)) * 1.000001f : 0.f;
       lb[row] = decided ? sqrtf(fmaxf(m2 + xs * 0.99999f - e, 0.f)) * 0.999999f : 0.f;
     }
@@ -761,7 +846,7 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
       b = __shfl(b, 0);
       if (tie) {
         const uint32_t p = b + mbcnt(tm);
-        if (p < (uint32_t)KMS_AMB) amb[p] = (uint32_t)row;
+        if (p < (uint32_t)AMB) amb[p] = (uint32_t)row;
         else amb_rows[atomicAdd(n_amb, 1ull)] = (uint32_t)row;
       }
     }
@@ -772,7 +857,7 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
     if (ls[i]) atomicAdd(&sums[i], ls[i]);
   for (int i = tid; i < k; i += KM_MT)
     if (lc[i]) atomicAdd(&cnt[i], lc[i]);
-  const uint32_t na = namb < (uint32_t)KMS_AMB ? namb : (uint32_t)KMS_AMB;
+  const uint32_t na = namb < (uint32_t)AMB ? namb : (uint32_t)AMB;
   if (tid == 0) abase = na ? atomicAdd(n_amb, (unsigned long long)na) : 0ull;
   __syncthreads();
   for (uint32_t i = tid; i < na; i += KM_MT) amb_rows[abase + i] = amb[i];
@@ -1055,13 +1140,17 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
     split = split && inc && sums && changed && !dist && !(se && !strcmp(se, "0"));
     uint32_t* amb = nullptr;
     unsigned long long* n_amb = nullptr;
+    bool h16 = false;
     if (split) {
       OH_TRY(ctx->ws.get("km_amb", (size_t)std::max<int64_t>(n, 1), &amb));
       OH_TRY(ctx->ws.get("km_namb", 1, &n_amb));
       OH_HIP(hipMemsetAsync(n_amb, 0, 8, s));
       const int KS = dim <= 112 ? 7 : 8;
+      // the half-precision rows of an attached X (OTTOHIP_KM_H16=0: the bf16 split of the f32 rows; read per call)
+      const char* he = getenv("OTTOHIP_KM_H16");
+      h16 = ctx->km_hX == X && ctx->km_hn == n && ctx->km_hdim == dim && !(he && !strcmp(he, "0"));
       const size_t lds2 = (size_t)NB * KS * 2 * 64 * 16 + ((size_t)k * dim + k) * 8 + (KM_MT / 64) * 96 * 4 + 64 * 4 +
-                          (size_t)KMS_AMB * 4;
+                          (size_t)(h16 ? KMH_AMB : KMS_AMB) * 4;
       // bounds >= 0 (batched steps): skip the rows whose distance bounds keep their label; 1 = the
       // bounds are not valid for these rows (every row scored, bounds rebuilt)
       const bool bl = bounds >= 0 && km_bounds_on(n);
@@ -1070,6 +1159,13 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
       if (bl)
         sk = KS == 7 ? (NB == 1 ? k_km_assign_split<1, 7, true> : k_km_assign_split<2, 7, true>)
                      : (NB == 1 ? k_km_assign_split<1, 8, true> : k_km_assign_split<2, 8, true>);
+      if (h16)
+        sk = bl ? (KS == 7 ? (NB == 1 ? k_km_assign_split<1, 7, true, true> : k_km_assign_split<2, 7, true, true>)
+                           : (NB == 1 ? k_km_assign_split<1, 8, true, true> : k_km_assign_split<2, 8, true, true>))
+                : (KS == 7 ? (NB == 1 ? k_km_assign_split<1, 7, false, true> : k_km_assign_split<2, 7, false, true>)
+                           : (NB == 1 ? k_km_assign_split<1, 8, false, true> : k_km_assign_split<2, 8, false, true>));
+      const uint4* x16 = h16 ? reinterpret_cast<const uint4*>(ctx->km_x16) : nullptr;
+      const float* xn2 = h16 ? ctx->km_xn2 : nullptr;
       OH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(sk), hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)lds2));
       // one resident block per CU (the kernel's registers allow one 8-wave block): one round of blocks,
@@ -1101,10 +1197,10 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
                   ds[k / 10], dh[67]);
         }
         sk<<<(unsigned)ctx->n_cu, KM_MT, lds2, s>>>(X, n, dim, C, cn, k, labels, sums, cnt, changed, gate, amb, n_amb,
-                                                    erows, n_eval, ub, lb);
+                                                    erows, n_eval, ub, lb, x16, xn2);
       } else {
         sk<<<sgrid, KM_MT, lds2, s>>>(X, n, dim, C, cn, k, labels, sums, cnt, changed, gate, amb, n_amb, nullptr, nullptr,
-                                     nullptr, nullptr);
+                                     nullptr, nullptr, x16, xn2);
       }
       OH_HIP(hipGetLastError());
     }
@@ -1116,7 +1212,7 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
     OH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)lds));
     // near ties only (about 1-2 % of the rows): a quarter of the grid, fewer block set-ups and flushes
-    const unsigned egrid = split ? (unsigned)std::max(1, ctx->n_cu / 2) : grid;
+    const unsigned egrid = split ? (unsigned)std::max(1, h16 ? ctx->n_cu * 2 : ctx->n_cu / 2) : grid;  // ~5 % with H16
     kern<<<egrid, KM_MT, lds, s>>>(X, n, dim, nq, C, cn, k, labels, sums, cnt, inr, changed, dist, inc, gate,
                                    amb, n_amb);
     OH_HIP(hipGetLastError());
@@ -1696,6 +1792,29 @@ int ottohip_kmeans_lloyd_iter(ottohip_ctx* ctx, const float* X, int64_t n, int d
 // split-precision pass plus the exact f32 kernel on its near ties (OTTOHIP_KM_SPLIT=0: the exact kernel on
 // every row; labels, sums and stop checks are identical): out[0] then holds the near ties' inertia only
 // (the run's inertia is ottohip_kmeans_inertia's).
+int ottohip_kmeans_attach_half(ottohip_ctx* ctx, const float* X, int64_t n, int dim, void* stream) {
+  if (!ctx || !X || n < 1 || dim < 1 || dim > EMB_MAXD || (dim & 3)) {
+    set_error("kmeans_attach_half: bad arguments (dim <= %d, dim %% 4 == 0)", EMB_MAXD); return OTTOHIP_EINVAL;
+  }
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  const int kc = 2 * (dim <= 112 ? 7 : 8);  // 16-B chunks per row: the split kernel's 2 KS pieces
+  uint4* x16;
+  float* xn2;
+  OH_TRY(ctx->ws.get("km_x16", (size_t)n * kc, &x16));
+  OH_TRY(ctx->ws.get("km_xn2", (size_t)n, &xn2));
+  k_km_half_rows<<<(unsigned)ceil_div(n * 64, 256), 256, 0, s>>>(X, n, dim, kc, x16, xn2);
+  OH_HIP(hipGetLastError());
+  ctx->km_hX = X; ctx->km_hn = n; ctx->km_hdim = dim; ctx->km_x16 = x16; ctx->km_xn2 = xn2;
+  return 0;
+}
+
+int ottohip_kmeans_detach_half(ottohip_ctx* ctx) {
+  if (!ctx) return OTTOHIP_EINVAL;
+  ctx->km_hX = nullptr;
+  return 0;
+}
+
 int ottohip_kmeans_lloyd_steps(ottohip_ctx* ctx, const float* X, int64_t n, int dim, float* centroids, int k,
                                int32_t* labels, int64_t* sums, int64_t* counts, int max_steps, double tol,
                                double* out, void* stream) {

@@ -157,6 +157,11 @@ class KMeans:
         var = s2.cpu().numpy().astype(np.float64) / FX / n_all - m1 * m1
         tol_abs = float(np.mean(var)) * self.tol
         seed_stream = _permutation_heads(self.random_state, n_all, k, self.n_init)
+        # one GPU: the E-steps read f16 copies of the centred rows (exact f32 scoring of the near ties keeps the
+        # f32 labels); every fit attaches its own Xc, so a reused allocation never meets a stale copy
+        half = group is None and dim % 4 == 0 and os.environ.get("OTTOHIP_KM_H16", "1") != "0"
+        if half:
+            _lib.check(lib.ottohip_kmeans_attach_half(ctx.h, _lib.ptr(Xc), n, dim, sh))
         sums = torch.empty(k * dim, dtype=torch.int64, device=dev)
         counts = torch.empty(k, dtype=torch.int64, device=dev)
         labels = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
@@ -234,6 +239,8 @@ class KMeans:
             if best is None or inertia < best[0]:
                 best = (inertia, C.clone(), labels[:n].clone(), it)
         seed_stream.close()
+        if half:
+            lib.ottohip_kmeans_detach_half(ctx.h)
         self.inertia_, C, self.labels_, self.n_iter_ = best
         self.cluster_centers_ = C + mean_d
         return self
