@@ -498,6 +498,7 @@ constexpr float KMH_SEP = 4.1e-3f;
 constexpr float KMH_ABS = 2.5e-6f;
 constexpr float KMH_ERR = 1.2e-3f;  // score error bound for the rebuilt distance bounds (cmax (|x| + cmax) units)
 constexpr int KMH_AMB = 8192;       // near-tie rows staged per block (~5 % of a block's ~50 k rows)
+constexpr int KMH_MT = 768;         // H16 block: 12 waves (136-170 VGPRs: 3 waves per SIMD)
 __global__ void k_km_half_rows(const float* __restrict__ X, int64_t n, int dim, int kc, uint4* __restrict__ X16,
                                float* __restrict__ xn2) {
   // one wave per row: lanes over the row's 16-B f16 chunks (kc per row, zero padded past dim), squared norm by
@@ -640,7 +641,7 @@ __device__ __forceinline__ void km_split8_h(const float (&v)[8], uint4& hi, uint
 }
 // H16: the rows from X16 (f16, 2 KS chunks per row) and their squared norms xn2 (ottohip_kmeans_attach_half)
 template <int NB, int KS, bool BL = false, bool H16 = false>
-__global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __restrict__ X, int64_t n, int dim,
+__global__ __launch_bounds__(H16 ? KMH_MT : KM_MT, H16 ? 1 : 2) void k_km_assign_split(const float* __restrict__ X, int64_t n, int dim,
                                                              const float* __restrict__ C, const float* __restrict__ cn,
                                                              int k, int32_t* __restrict__ label,
                                                              unsigned long long* __restrict__ sums,
@@ -657,18 +658,19 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
                                                              const float* __restrict__ xn2 = nullptr) {
   if (gate && __builtin_amdgcn_readfirstlane(*gate)) return;
   constexpr int AMB = H16 ? KMH_AMB : KMS_AMB;
+  constexpr int MT = H16 ? KMH_MT : KM_MT;  // threads per block (H16: 12 waves, its registers allow 3 per SIMD)
   extern __shared__ unsigned long long smem64[];
   uint4* Cf = reinterpret_cast<uint4*>(smem64);                               // [NB][KS][hi, lo][64]
   unsigned long long* ls = reinterpret_cast<unsigned long long*>(Cf + NB * KS * 2 * 64);  // k * dim sums
   unsigned long long* lc = ls + k * dim;                                       // k counts
   int32_t* labl = reinterpret_cast<int32_t*>(lc + k);                         // [waves][3][32]
-  float* cnl = reinterpret_cast<float*>(labl + (KM_MT / 64) * 96);             // [64]
+  float* cnl = reinterpret_cast<float*>(labl + (MT / 64) * 96);             // [64]
   uint32_t* amb = reinterpret_cast<uint32_t*>(cnl + 64);                       // [AMB]
   __shared__ uint32_t namb;
   __shared__ unsigned long long abase;
   const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6, h = l >> 5, i32 = l & 31;
   // centroid fragments: lane (r, h) of block b, k-step s holds centroid 32 b + r, dims 16 s + 8 h .. + 7
-  for (int e = tid; e < NB * KS * 64; e += KM_MT) {
+  for (int e = tid; e < NB * KS * 64; e += MT) {
     const int ll = e & 63, sb = e >> 6, s_ = sb % KS, b = sb / KS;
     const int c = b * 32 + (ll & 31), d0 = 16 * s_ + 8 * (ll >> 5);
     float v[8];
@@ -681,7 +683,7 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
     Cf[(sb * 2 + 1) * 64 + ll] = lo;
   }
   if (tid < 64) cnl[tid] = cn[tid];
-  for (int i = tid; i < k * dim + k; i += KM_MT) ls[i] = 0ull;
+  for (int i = tid; i < k * dim + k; i += MT) ls[i] = 0ull;
   if (tid == 0) namb = 0;
   __syncthreads();
   float c2 = l < k ? cnl[l] : 0.f;
@@ -691,7 +693,7 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
   uint32_t nchg = 0;
   const int64_t nl = BL ? (int64_t)__builtin_amdgcn_readfirstlane((int)*n_eval) : n;  // rows to score
   const int64_t ntile = (nl + 31) >> 5;
-  const int64_t nwv = (int64_t)gridDim.x * (KM_MT / 64);
+  const int64_t nwv = (int64_t)gridDim.x * (MT / 64);
   // the next tile's rows (and its rows' current labels) are loaded while this tile is scored
   float4 raw[H16 ? 1 : 2 * KS];
   uint4 raw16[H16 ? KS : 1];
@@ -720,7 +722,7 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
     }
     lab_n = label[rr];
   };
-  const int64_t t_first = (int64_t)blockIdx.x * (KM_MT / 64) + wv;
+  const int64_t t_first = (int64_t)blockIdx.x * (MT / 64) + wv;
   if (t_first < ntile) load(t_first);
   for (int64_t t = t_first; t < ntile; t += nwv) {
     const int64_t r0 = t << 5;
@@ -853,14 +855,14 @@ __global__ __launch_bounds__(KM_MT, 2) void k_km_assign_split(const float* __res
     km_move_rows(X, dim, ls, lc, labl + wv * 96, mine && old != (int32_t)mi, row, mi, old);
   }
   __syncthreads();
-  for (int i = tid; i < k * dim; i += KM_MT)
+  for (int i = tid; i < k * dim; i += MT)
     if (ls[i]) atomicAdd(&sums[i], ls[i]);
-  for (int i = tid; i < k; i += KM_MT)
+  for (int i = tid; i < k; i += MT)
     if (lc[i]) atomicAdd(&cnt[i], lc[i]);
   const uint32_t na = namb < (uint32_t)AMB ? namb : (uint32_t)AMB;
   if (tid == 0) abase = na ? atomicAdd(n_amb, (unsigned long long)na) : 0ull;
   __syncthreads();
-  for (uint32_t i = tid; i < na; i += KM_MT) amb_rows[abase + i] = amb[i];
+  for (uint32_t i = tid; i < na; i += MT) amb_rows[abase + i] = amb[i];
   const uint32_t w = wave_sum(nchg);
   if (l == 0 && w) atomicAdd(changed, (unsigned long long)w);
 }
@@ -1149,7 +1151,8 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
       // the half-precision rows of an attached X (OTTOHIP_KM_H16=0: the bf16 split of the f32 rows; read per call)
       const char* he = getenv("OTTOHIP_KM_H16");
       h16 = ctx->km_hX == X && ctx->km_hn == n && ctx->km_hdim == dim && !(he && !strcmp(he, "0"));
-      const size_t lds2 = (size_t)NB * KS * 2 * 64 * 16 + ((size_t)k * dim + k) * 8 + (KM_MT / 64) * 96 * 4 + 64 * 4 +
+      const int smt = h16 ? KMH_MT : KM_MT;  // the split kernel's block size
+      const size_t lds2 = (size_t)NB * KS * 2 * 64 * 16 + ((size_t)k * dim + k) * 8 + (smt / 64) * 96 * 4 + 64 * 4 +
                           (size_t)(h16 ? KMH_AMB : KMS_AMB) * 4;
       // bounds >= 0 (batched steps): skip the rows whose distance bounds keep their label; 1 = the
       // bounds are not valid for these rows (every row scored, bounds rebuilt)
@@ -1170,7 +1173,7 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
                                  (int)lds2));
       // one resident block per CU (the kernel's registers allow one 8-wave block): one round of blocks,
       // so each block's LDS set-up and sum flush happen once
-      const unsigned sgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(ntile, KM_MT / 64), ctx->n_cu));
+      const unsigned sgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(ntile, smt / 64), ctx->n_cu));
       if (bl) {
         float *ub, *lb, *cp, *dl;
         uint32_t* erows;
@@ -1196,10 +1199,10 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
                   "median %.4g, p10 %.4g, cmax %.4g)\n", ne, (long long)n, bounds, dh[64], dh[65], ds[k / 2],
                   ds[k / 10], dh[67]);
         }
-        sk<<<(unsigned)ctx->n_cu, KM_MT, lds2, s>>>(X, n, dim, C, cn, k, labels, sums, cnt, changed, gate, amb, n_amb,
-                                                    erows, n_eval, ub, lb, x16, xn2);
+        sk<<<(unsigned)ctx->n_cu, smt, lds2, s>>>(X, n, dim, C, cn, k, labels, sums, cnt, changed, gate, amb, n_amb,
+                                                  erows, n_eval, ub, lb, x16, xn2);
       } else {
-        sk<<<sgrid, KM_MT, lds2, s>>>(X, n, dim, C, cn, k, labels, sums, cnt, changed, gate, amb, n_amb, nullptr, nullptr,
+        sk<<<sgrid, smt, lds2, s>>>(X, n, dim, C, cn, k, labels, sums, cnt, changed, gate, amb, n_amb, nullptr, nullptr,
                                      nullptr, nullptr, x16, xn2);
       }
       OH_HIP(hipGetLastError());
