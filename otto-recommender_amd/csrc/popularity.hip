@@ -1214,8 +1214,11 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
                       : (NB == 1 ? k_km_assign_mfma<1, KM_NQ, true> : k_km_assign_mfma<2, KM_NQ, true>);
     OH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)lds));
-    // near ties only (about 1-2 % of the rows): a quarter of the grid, fewer block set-ups and flushes
-    const unsigned egrid = split ? (unsigned)std::max(1, h16 ? ctx->n_cu * 2 : ctx->n_cu / 2) : grid;  // ~5 % with H16
+    // near ties only: about 1-2 % of the rows (bf16 split: half a block per CU) or ~5 % (H16: one block per CU,
+    // C2 1.143 s against 1.168 s at two and 1.245 s at half a block per CU); OTTOHIP_KM_EGRID = blocks (A/B)
+    const char* ege = getenv("OTTOHIP_KM_EGRID");
+    const int eg_env = ege ? atoi(ege) : 0;
+    const unsigned egrid = split ? (unsigned)std::max(1, eg_env > 0 ? eg_env : (h16 ? ctx->n_cu : ctx->n_cu / 2)) : grid;
     kern<<<egrid, KM_MT, lds, s>>>(X, n, dim, nq, C, cn, k, labels, sums, cnt, inr, changed, dist, inc, gate,
                                    amb, n_amb);
     OH_HIP(hipGetLastError());
