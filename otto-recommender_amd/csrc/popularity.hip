@@ -524,23 +524,31 @@ __global__ void k_km_half_rows(const float* __restrict__ X, int64_t n, int dim, 
   if (l == 0) xn2[row] = ss;
 }
 // dl: [0, 64) delta_j, [64] largest delta, [65] second largest, [66] its cluster (as float), [67] cmax
-__global__ void k_km_delta(const float* __restrict__ C, float* __restrict__ Cp, const float* __restrict__ cn,
-                           int k, int dim, int force, float* __restrict__ dl, const int* __restrict__ gate,
-                           unsigned long long* __restrict__ n_eval) {
+constexpr int KMD_T = 1024;  // k_km_delta: 16 waves, one centroid per wave at a time, lanes over the dims
+__global__ __launch_bounds__(KMD_T) void k_km_delta(const float* __restrict__ C, float* __restrict__ Cp,
+                                                     const float* __restrict__ cn, int k, int dim, int force,
+                                                     float* __restrict__ dl, const int* __restrict__ gate,
+                                                     unsigned long long* __restrict__ n_eval) {
   if (gate && __builtin_amdgcn_readfirstlane(*gate)) return;  // stopped: Cp stays the bounds' centres
-  const int j = threadIdx.x;  // one block of 64 threads
-  float d = 0.f;
-  if (j < k) {
+  __shared__ float sdl[64];
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (threadIdx.x < 64) sdl[threadIdx.x] = 0.f;
+  __syncthreads();
+  for (int j = wv; j < k; j += KMD_T / 64) {  // |C_j - Cp_j| in f64, rounded up
     double s = 0.0;
-    for (int i = 0; i < dim; ++i) {
+    for (int i = l; i < dim; i += 64) {
       const double t = (double)C[(int64_t)j * dim + i] - (double)Cp[(int64_t)j * dim + i];
       s += t * t;
     }
-    d = force ? INFINITY : (float)(sqrt(s) * (1.0 + 1e-6));
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+    if (l == 0) sdl[j] = force ? INFINITY : (float)(sqrt(s) * (1.0 + 1e-6));
   }
   __syncthreads();  // every read of Cp before it is overwritten
-  if (j < k)
-    for (int i = 0; i < dim; ++i) Cp[(int64_t)j * dim + i] = C[(int64_t)j * dim + i];
+  for (int i = threadIdx.x; i < k * dim; i += KMD_T) Cp[i] = C[i];
+  if (wv != 0) return;
+  const int j = l;
+  const float d = j < k ? sdl[j] : 0.f;
   // largest and second largest delta (ties: any cluster holding the largest, the second equals it)
   float m1 = d;
   int a1 = j;
@@ -1184,7 +1192,7 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
         OH_TRY(ctx->ws.get("km_dl", 68, &dl));
         OH_TRY(ctx->ws.get("km_erows", (size_t)n, &erows));
         OH_TRY(ctx->ws.get("km_neval", 1, &n_eval));
-        k_km_delta<<<1, 64, 0, s>>>(C, cp, cn, k, dim, bounds, dl, gate, n_eval);
+        k_km_delta<<<1, KMD_T, 0, s>>>(C, cp, cn, k, dim, bounds, dl, gate, n_eval);
         const unsigned fgrid = (unsigned)std::max<int64_t>(1, ceil_div(n, KMF_PER * 256));
         k_km_filter<<<fgrid, 256, 0, s>>>(n, k, labels, ub, lb, dl, erows, n_eval, gate);
         static const bool bdbg = getenv("OTTOHIP_KM_BDBG") != nullptr;  // rows scored per step (debugging aid)
