@@ -64,6 +64,8 @@ def cpu_baseline(seed: int = 0, pandas_files: int = 10) -> dict:
     out["host_cpus"] = res["host"]
     if "pandas" in res:
         out["reference_algorithm"] = res["pandas"]
+    if "merge" in res:  # count + merge on the CPU (beside a6.count_plus_merge_pairs_per_s)
+        out["count_plus_merge"] = res["merge"]
     return out
 
 

@@ -11,6 +11,8 @@ the same synthetic stream as the GPU line:
               dataframe pipeline (:17-94: unique, 10k-session parts, join on session, filters,
               groupby count), a process pool over files -- the reference's own algorithm.
 Both report qualifying pairs / s over the sample.
+  "merge"     count + merge (the reference's deliverable, :202 + :210): the C per-file tables, then the
+              numpy restatement of concat_files_w_stats (:103-181) over them.
 """
 from __future__ import annotations
 
@@ -105,6 +107,44 @@ def pandas_pool(n_files: int, workers: int, seed: int) -> dict:
             "seconds": wall, "pairs": pairs, "per_core_pairs_per_s": pairs / busy if busy else None}
 
 
+def count_plus_merge(n_files: int, threads: int, seed: int) -> dict:
+    """The reference's deliverable is count (ETA 20 min, model/count_co_events.py:202) PLUS merge (ETA 30 min,
+    :210): the per-file tables of the first n_files files (oracle/covis_oracle.c, files over a pool of
+    `threads` threads, the tables materialised as the reference writes them, :94-100), then
+    concat_files_w_stats (:103-181, the numpy restatement oracle/covis.py with the reference's thresholds:
+    per-file count >= 2 filter of click_to tables when N > 1e8, MIN_COUNT_TO_SAVE, count desc, head) of
+    every rule over those tables. value = qualifying pairs / (count + merge seconds)."""
+    from concurrent.futures import ThreadPoolExecutor
+    import covis as oracle
+    ev, fb = _files(n_files, seed)
+    off = np.asarray(ev.session_offsets, np.int64)
+
+    def one(f):
+        s0, s1 = int(fb[f]), int(fb[f + 1])
+        e0, e1 = int(off[s0]), int(off[s1])
+        return oracle.count_co_events_file(off[s0:s1 + 1], ev.aid[e0:e1], ev.ts[e0:e1], ev.type[e0:e1])
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as pool:  # ctypes releases the GIL inside the C count
+        tabs = list(pool.map(one, range(len(fb) - 1)))
+    count_s = time.perf_counter() - t0
+    pairs = sum(int(t[n][2].sum(dtype=np.int64)) for t in tabs for n in oracle.REFERENCE_RULES)
+    rows_in = sum(len(t[n][0]) for t in tabs for n in oracle.REFERENCE_RULES)
+    t0 = time.perf_counter()
+    rows_out = {}
+    for n in oracle.REFERENCE_RULES:
+        a, _, _ = oracle.concat_files_w_stats(n, [t[n] for t in tabs])
+        rows_out[n] = int(len(a))
+    merge_s = time.perf_counter() - t0
+    return {"value": pairs / (count_s + merge_s), "unit": "pairs/s", "cores": threads, "kind": "port",
+            "count_s": round(count_s, 2), "merge_s": round(merge_s, 2), "pairs": pairs, "file_rows": rows_in,
+            "merge_rows_per_s": rows_in / merge_s, "rows_out": rows_out, "files": len(fb) - 1,
+            "sample": f"count + merge of the first {len(fb) - 1} files ({ev.n_sessions} sessions, {pairs} pairs, "
+                      f"{rows_in} per-file rows): oracle/covis_oracle.c per-file tables over {threads} threads "
+                      f"({count_s:.1f} s), then oracle/covis.py concat_files_w_stats of the 5 rules with the "
+                      f"reference's thresholds (numpy, one core, {merge_s:.1f} s)"}
+
+
 def main():
     cfg = json.loads(sys.argv[1]) if len(sys.argv) > 1 else {}
     cores = host_cores()
@@ -116,6 +156,9 @@ def main():
     pdf = int(cfg.get("pandas_files", 10))
     if pdf > 0:
         out["pandas"] = pandas_pool(pdf, min(n, pdf), seed)
+    mf = int(cfg.get("merge_files", 16))
+    if mf > 0:
+        out["merge"] = count_plus_merge(mf, n, seed)
     print(json.dumps(out))
 
 

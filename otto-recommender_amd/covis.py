@@ -433,19 +433,27 @@ def boundary_keys(events: DeviceEvents, name: str, plan, file_rows, use_ge2: boo
             need.setdefault(fb, set()).add(hi)
     out = {}
     files = sorted(need)
-    if files and n_items <= (1 << 24) and len(files) <= 254:
+    # the part machinery: aid_next < 2^24, < 255 parts, and the call's files within a pair word's file bits
+    if files and n_items <= (1 << 24) and len(files) <= min(254, max_files_per_call([name], n_items)):
         sub = events.subset_file_list(files)
-        t = count_co_events_parts(sub, name, np.arange(len(files), dtype=np.int32), [], len(files), n_items, ctx=ctx)
-        lib = _lib.load()
-        for p, f in enumerate(files):
-            rows = np.ascontiguousarray(sorted(need[f]), np.int64)
-            keys = np.zeros(len(rows), np.uint64)
-            _lib.check(lib.ottohip_table_keys_at(t.ctx.h, t.h, p, 1 if use_ge2 else 0, rows.ctypes.data, len(rows),
-                                                 keys.ctypes.data, _lib.stream_handle(None)))
-            for r, k in zip(rows.tolist(), keys.tolist()):
-                out[(f, r)] = int(k)
-        t.free()
-        return out
+        try:
+            t = count_co_events_parts(sub, name, np.arange(len(files), dtype=np.int32), [], len(files), n_items,
+                                      ctx=ctx)
+        except _lib.OttoHipError as e:
+            if e.rc != _lib.OTTOHIP_ELIMIT:
+                raise
+            t = None  # a layout limit of the one-count form: each file alone below
+        if t is not None:
+            lib = _lib.load()
+            for p, f in enumerate(files):
+                rows = np.ascontiguousarray(sorted(need[f]), np.int64)
+                keys = np.zeros(len(rows), np.uint64)
+                _lib.check(lib.ottohip_table_keys_at(t.ctx.h, t.h, p, 1 if use_ge2 else 0, rows.ctypes.data,
+                                                     len(rows), keys.ctypes.data, _lib.stream_handle(None)))
+                for r, k in zip(rows.tolist(), keys.tolist()):
+                    out[(f, r)] = int(k)
+            t.free()
+            return out
     for f, rows in sorted(need.items()):
         rows = sorted(rows)
         t = count_co_events_fused(events.subset_files(f, f + 1), [name], n_items=n_items, ctx=ctx)

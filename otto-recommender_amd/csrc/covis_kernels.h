@@ -1033,6 +1033,14 @@ __device__ __forceinline__ void emit_flush2(EmitLds& S, int nrec, uint32_t tot, 
     const uint64_t mleA = mA & upto, mleB = mB & upto;
     const int oA = ob + (int)__popcll(mleA);
     const int oB = ob + (int)__popcll(mA) + (int)__popcll(mleB);
+    // always-on, wave-uniform: the marks seen so far must name records [0, nrec) and the first round must start
+    // at record 0. A stale or extra mark (round 4: uninitialised mark[64..127] equal to a later round id) would
+    // index past the records and write words at a wild address; instead the flush stops and the call fails
+    // (err bit 8, "record index outside the flush's records")
+    if (ob + (int)__popcll(mA) + (int)__popcll(mB) >= nrec || (c == 0 && !(mA & 1ull))) {
+      if (l == 0) atomicOr(err, 8);
+      break;
+    }
     ob += (int)__popcll(mA) + (int)__popcll(mB);
     const uint32_t pA = c + l, pB = c + 64 + l;
     bool qA = false, qB = false;
@@ -1074,6 +1082,8 @@ __device__ __forceinline__ void emit_flush2(EmitLds& S, int nrec, uint32_t tot, 
     if (qB && !(dbg & 1)) words[dB + carB + (uint32_t)__popcll(mineB & below)] = wB;
     cc = (uint32_t)__builtin_amdgcn_readlane((int)(carB + (uint32_t)__popcll(mineB)), 63);
   }
+  // every record start falls in exactly one round: the marks seen must number nrec (always on, wave-uniform)
+  if (tot > 0 && ob != nrec - 1 && l == 0) atomicOr(err, 8);
 }
 
 // Per event type, the (rule, next type) windows an event of that type writes, as pass 3's task list: entry

@@ -499,8 +499,12 @@ constexpr float KMH_ABS = 2.5e-6f;
 constexpr float KMH_ERR = 1.2e-3f;  // score error bound for the rebuilt distance bounds (cmax (|x| + cmax) units)
 constexpr int KMH_AMB = 8192;       // near-tie rows staged per block (~5 % of a block's ~50 k rows)
 constexpr int KMH_MT = 768;         // H16 block: 12 waves (136-170 VGPRs: 3 waves per SIMD)
+// KMH_MAXABS: the f16 copy is refused above this |x| (f16 overflows at 65504; centroids are row means, so their
+// f16 hi / lo split stays finite below it). The bits of max |x| (NaN included: its bits exceed inf's) reach
+// *amax by one atomicMax per wave.
+constexpr float KMH_MAXABS = 3.0e4f;
 __global__ void k_km_half_rows(const float* __restrict__ X, int64_t n, int dim, int kc, uint4* __restrict__ X16,
-                               float* __restrict__ xn2) {
+                               float* __restrict__ xn2, unsigned* __restrict__ amax) {
   // one wave per row: lanes over the row's 16-B f16 chunks (kc per row, zero padded past dim), squared norm by
   // a wave sum of the f32 elements
   const int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -508,6 +512,7 @@ __global__ void k_km_half_rows(const float* __restrict__ X, int64_t n, int dim, 
   if (row >= n) return;
   const float* xp = X + row * dim;
   float ss = 0.f;
+  unsigned mx = 0u;  // bits of max |x| over the lane's elements (non-negative floats order as unsigned ints)
   if (l < kc) {
     _Float16 h[8];
 #pragma unroll
@@ -516,12 +521,19 @@ __global__ void k_km_half_rows(const float* __restrict__ X, int64_t n, int dim, 
       const float v = d < dim ? xp[d] : 0.f;
       ss += v * v;
       h[j] = (_Float16)v;
+      mx = max(mx, __float_as_uint(v) & 0x7FFFFFFFu);
     }
     X16[row * kc + l] = __builtin_bit_cast(uint4, h);
   }
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
-  if (l == 0) xn2[row] = ss;
+  for (int o = 32; o >= 1; o >>= 1) {
+    ss += __shfl_xor(ss, o);
+    mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
+  }
+  if (l == 0) {
+    xn2[row] = ss;
+    if (mx > __float_as_uint(KMH_MAXABS)) atomicMax(amax, mx);
+  }
 }
 // dl: [0, 64) delta_j, [64] largest delta, [65] second largest, [66] its cluster (as float), [67] cmax
 constexpr int KMD_T = 1024;  // k_km_delta: 16 waves, one centroid per wave at a time, lanes over the dims
@@ -1817,8 +1829,19 @@ int ottohip_kmeans_attach_half(ottohip_ctx* ctx, const float* X, int64_t n, int 
   float* xn2;
   OH_TRY(ctx->ws.get("km_x16", (size_t)n * kc, &x16));
   OH_TRY(ctx->ws.get("km_xn2", (size_t)n, &xn2));
-  k_km_half_rows<<<(unsigned)ceil_div(n * 64, 256), 256, 0, s>>>(X, n, dim, kc, x16, xn2);
+  unsigned* amax;
+  OH_TRY(ctx->ws.get("km_amax", 1, &amax));
+  ctx->km_hX = nullptr;  // no half copy is attached unless this one is accepted
+  OH_HIP(hipMemsetAsync(amax, 0, sizeof(unsigned), s));
+  k_km_half_rows<<<(unsigned)ceil_div(n * 64, 256), 256, 0, s>>>(X, n, dim, kc, x16, xn2, amax);
   OH_HIP(hipGetLastError());
+  unsigned hmax = 0;
+  OH_TRY(d2h(&hmax, amax, 1, s));
+  if (hmax > __builtin_bit_cast(unsigned, KMH_MAXABS)) {
+    set_error("kmeans_attach_half: max |x| = %g exceeds the f16 range bound %g (or is not finite)",
+              (double)__builtin_bit_cast(float, hmax), (double)KMH_MAXABS);
+    return OTTOHIP_ELIMIT;
+  }
   ctx->km_hX = X; ctx->km_hn = n; ctx->km_hdim = dim; ctx->km_x16 = x16; ctx->km_xn2 = xn2;
   return 0;
 }

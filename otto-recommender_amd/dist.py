@@ -275,7 +275,7 @@ def _count_sharded_batches(events, file_ids, n_files_total: int, cap: int, group
     owner partition is the same in every batch, so no exchange)."""
     import torch
     fids = np.asarray(file_ids if file_ids is not None else range(len(events.file_bounds) - 1), np.int64)
-    recs, fs, out_names, pf, pf2 = [], None, None, [], []
+    recs, fs, out_names, pf, pf2, xs = [], None, None, [], [], {}
     for g0 in range(0, int(n_files_total), cap):
         g1 = min(int(n_files_total), g0 + cap)
         sel = np.nonzero((fids >= g0) & (fids < g1))[0]  # the rank's files are in ascending global order
@@ -288,6 +288,8 @@ def _count_sharded_batches(events, file_ids, n_files_total: int, cap: int, group
         fs = st if fs is None else [(a + c, b + d) for (a, b), (c, d) in zip(fs, st)]
         if cuts is not None and cuts.per_file:
             pf.append(t.file_rows_per_file); pf2.append(t.file_rows_ge2_per_file)
+        for k, v in t.exchange_stats.items():
+            xs[k] = max(xs.get(k, 0), v) if k.startswith("max") else xs.get(k, 0) + v
         r, _ = pack_by_owner(t, 1, stream)
         recs.append(r.clone())
         out_names = t.names
@@ -295,6 +297,7 @@ def _count_sharded_batches(events, file_ids, n_files_total: int, cap: int, group
     tab = table_from_records(torch.cat(recs).contiguous(), out_names, n_items, fs, ctx=ctx, stream=stream)
     if pf:
         tab.file_rows_per_file, tab.file_rows_ge2_per_file = np.concatenate(pf), np.concatenate(pf2)
+    tab.exchange_stats = xs
     return tab
 
 
@@ -342,6 +345,9 @@ def count_co_events_sharded(events, file_ids, n_files_total: int, group=None, na
     dev = torch.device("cuda", (ctx or _lib.context()).device)
     fids = list(range(nf)) if file_ids is None else [int(f) for f in file_ids]
     pending = []
+    # exchange sizes (entries; all_to_all_single takes them as int64 split sizes, RCCL as size_t counts)
+    xs = {"words_sent": 0, "max_words_to_peer": 0, "words_recv": 0, "max_words_from_peer": 0, "pieces_sent": 0,
+          "pieces_recv": 0}
     for c in range(len(bounds) - 1):
         f0, f1 = bounds[c], bounds[c + 1]
         em = None
@@ -359,6 +365,10 @@ def count_co_events_sharded(events, file_ids, n_files_total: int, group=None, na
         else:
             words, pieces = torch.empty(0, dtype=torch.int32, device=dev), torch.empty(0, dtype=torch.int64, device=dev)
         rc = finish_count_exchange(cnt)
+        xs["words_sent"] += sum(wpp); xs["pieces_sent"] += sum(ppp)
+        xs["max_words_to_peer"] = max([xs["max_words_to_peer"]] + list(wpp))
+        xs["words_recv"] += sum(r[0] for r in rc); xs["pieces_recv"] += sum(r[1] for r in rc)
+        xs["max_words_from_peer"] = max([xs["max_words_from_peer"]] + [r[0] for r in rc])
         if stream is not None and words.is_cuda:
             # RCCL orders its work after torch's current stream: make that stream wait for the
             # caller's stream (an event wait on the device, not a host synchronize)
@@ -384,6 +394,7 @@ def count_co_events_sharded(events, file_ids, n_files_total: int, group=None, na
         tab.file_rows_per_file, tab.file_rows_ge2_per_file = allreduce_per_file(tab.file_rows_per_file,
                                                                                 tab.file_rows_ge2_per_file, group)
     tab.rank, tab.world = rank, world
+    tab.exchange_stats = xs
     return tab
 
 

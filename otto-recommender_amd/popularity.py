@@ -161,7 +161,22 @@ class KMeans:
         # f32 labels); every fit attaches its own Xc, so a reused allocation never meets a stale copy
         half = group is None and dim % 4 == 0 and os.environ.get("OTTOHIP_KM_H16", "1") != "0"
         if half:
-            _lib.check(lib.ottohip_kmeans_attach_half(ctx.h, _lib.ptr(Xc), n, dim, sh))
+            # refused (ELIMIT) when some |x| is outside the f16 range bound: the E-steps then score the f32 rows
+            rc = lib.ottohip_kmeans_attach_half(ctx.h, _lib.ptr(Xc), n, dim, sh)
+            half = rc == 0
+            if rc not in (0, _lib.OTTOHIP_ELIMIT):
+                _lib.check(rc)
+        try:
+            return self._fit_runs(X, Xc, n, dim, k, group, grows, tol_abs, seed_stream, mean_d, ctx, sh, dev)
+        finally:
+            seed_stream.close()
+            if half:  # always paired with the attach: a later fit never meets this fit's f16 copy
+                lib.ottohip_kmeans_detach_half(ctx.h)
+
+    def _fit_runs(self, X, Xc, n, dim, k, group, grows, tol_abs, seed_stream, mean_d, ctx, sh, dev):
+        """fit's n_init runs (the Lloyd loops) over the centred rows Xc; keeps the best by inertia."""
+        import torch
+        lib = _lib.load()
         sums = torch.empty(k * dim, dtype=torch.int64, device=dev)
         counts = torch.empty(k, dtype=torch.int64, device=dev)
         labels = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
@@ -238,9 +253,6 @@ class KMeans:
             inertia = float(_allreduce(torch.tensor([inr.value], dtype=torch.float64), group).item())
             if best is None or inertia < best[0]:
                 best = (inertia, C.clone(), labels[:n].clone(), it)
-        seed_stream.close()
-        if half:
-            lib.ottohip_kmeans_detach_half(ctx.h)
         self.inertia_, C, self.labels_, self.n_iter_ = best
         self.cluster_centers_ = C + mean_d
         return self

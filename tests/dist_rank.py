@@ -71,6 +71,64 @@ def covis(out, cfg):
     np.savez(out, **res)
 
 
+def covis_full(out, cfg):
+    """BASELINE configs[3] at its real size: the 220 M-event stream's 100k-session files dealt to the ranks by
+    Σ n_s² (as bench.py), each rank generating only its own files; the sharded count of all five rules, then the
+    sharded A6 of every rule (branch (2) of click_to_click at N = 694 M included). Saves per rule the shard's
+    order-independent digests (they add over ranks to the single-table digests), the global statistics, the
+    exchange sizes, a sha256 of this rank's final table, and rank 0's final tables."""
+    import hashlib
+    import time
+    import torch
+    import torch.distributed as dist
+    import otto_recommender_amd.synth as synth
+    from otto_recommender_amd import covis as gc, dist as gd
+    rank, world = dist.get_rank(), dist.get_world_size()
+    seed, n_sess = int(cfg["seed"]), int(cfg["sessions"])
+    fb_all = synth.file_session_bounds(n_sess)
+    n_files = len(fb_all) - 1
+    lens = synth.session_lengths(n_sess, 0, seed).astype(np.float64)
+    weights = [float((lens[fb_all[f]:fb_all[f + 1]] ** 2).sum()) for f in range(n_files)]
+    mine = gd.deal_files(n_files, rank, world, weights)
+    parts = [synth.generate(int(fb_all[f + 1] - fb_all[f]), int(fb_all[f]), seed) for f in mine]
+    fb = np.concatenate([[0], np.cumsum([p.n_sessions for p in parts])]).astype(np.int64)
+    off = np.zeros(int(fb[-1]) + 1, np.int64)
+    base = 0
+    for i, p in enumerate(parts):
+        off[fb[i]:fb[i + 1] + 1] = p.session_offsets + base
+        base += p.n_events
+    ev = synth.Events(off, np.concatenate([p.session for p in parts]), np.concatenate([p.aid for p in parts]),
+                      np.concatenate([p.ts for p in parts]), np.concatenate([p.type for p in parts]))
+    del parts
+    dev = gc.DeviceEvents.from_host(ev, fb)
+    res = {"files": np.asarray(mine, np.int64), "events": np.array([ev.n_events], np.int64)}
+    del ev
+    t0 = time.perf_counter()
+    tab = gd.count_co_events_sharded(dev, mine, n_files)
+    torch.cuda.synchronize()
+    res["count_s"] = np.array([time.perf_counter() - t0])
+    xs = tab.exchange_stats
+    res["exchange"] = np.array([xs["words_sent"], xs["max_words_to_peer"], xs["words_recv"], xs["max_words_from_peer"],
+                                xs["pieces_sent"], xs["pieces_recv"]], np.int64)
+    for n in tab.names:
+        d, st = tab.digest(n), tab.stats(n)
+        res[f"digest/{n}"] = np.array([d["d_count"], d["d_count_ge2"], d["pairs"], d["pairs_ge2"], d["rows"]], np.uint64)
+        res[f"stats/{n}"] = np.array([st["file_rows"], st["file_rows_ge2"], st["n_rows"], st["n_pairs"]], np.int64)
+    for n in tab.names:
+        t0 = time.perf_counter()
+        a, b, c = gd.concat_files_w_stats_sharded(dev, mine, n_files, n, table=tab)
+        torch.cuda.synchronize()
+        res[f"a6_s/{n}"] = np.array([time.perf_counter() - t0])
+        x = torch.stack([a, b, c], 1).cpu().numpy().astype(np.int32)
+        res[f"final_sha/{n}"] = np.frombuffer(hashlib.sha256(x.tobytes()).digest(), np.uint8)
+        if rank == 0:
+            res[f"final/{n}"] = x
+        del a, b, c, x
+    tab.free()
+    torch.cuda.synchronize()
+    np.savez(out, **res)
+
+
 def pipeline(out, cfg):
     import torch.distributed as dist
     import otto_recommender_amd.synth as synth
@@ -107,7 +165,7 @@ def main():
     torch.cuda.set_device(0)
     dist.init_process_group("gloo")
     try:
-        {"covis": covis, "pipeline": pipeline}[mode](out, cfg)
+        {"covis": covis, "covis_full": covis_full, "pipeline": pipeline}[mode](out, cfg)
         dist.barrier()
     finally:
         dist.destroy_process_group()

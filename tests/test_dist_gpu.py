@@ -125,6 +125,45 @@ def test_covis_sharded_eight_ranks(gpu, tmp_path):
     assert len(set(_owner(full[0][full[2] == cstar], 8).tolist())) >= 5
 
 
+@pytest.mark.slow
+def test_covis_sharded_full_size_config4(gpu, tmp_path):
+    """BASELINE configs[3] at its real size: the 220 M-event stream (135 files of 100k sessions) session-sharded
+    over 8 fresh rank processes on cuda:0 (gloo), files dealt by Σ n_s², the sharded count of all five rules
+    (owner all-to-all-v of pair words in 2 event-balanced chunks) and the sharded A6 of every rule, including
+    branch (2) of click_to_click at N = 694 M split over the owners (model/count_co_events.py:80-181).
+    The shard digests are wrapping u64 sums over rows, so they add over the owners to the single-table digests
+    of tests/golden/digest_220m.json (C oracle, make_golden.py --full); every rank's A6 output equals the
+    golden rows / sum / sha256 and is identical on all ranks; the exchange's per-peer sizes stay below 2^31."""
+    import torch
+    g = json.load(open(os.path.join(HERE, "golden", "digest_220m.json")))
+    gpu.trim()  # this process's cached device buffers (earlier full-size tests) are not needed by the ranks
+    torch.cuda.empty_cache()
+    world = 8
+    res = _launch("covis_full", {"seed": g["seed"], "sessions": g["sessions"]}, tmp_path, world=world, timeout=800)
+    files = np.concatenate([r["files"] for r in res])
+    assert sorted(files.tolist()) == list(range(g["files"]))
+    assert sum(int(r["events"][0]) for r in res) == g["events"]
+    M = (1 << 64) - 1
+    for n in NAMES:
+        ref = g["rules"][n]
+        dig = [sum(int(r[f"digest/{n}"][i]) for r in res) & M for i in range(5)]
+        assert (dig[0], dig[1], dig[2], dig[3]) == (ref["d_count"], ref["d_count_ge2"], ref["pairs"], ref["pairs_ge2"]), n
+        for r in res:  # the global per-file statistics on every rank
+            st = r[f"stats/{n}"]
+            assert (int(st[0]), int(st[1])) == (ref["file_rows"], ref["file_rows_ge2"]), n
+        assert sum(int(r[f"stats/{n}"][3]) for r in res) == ref["pairs"], n
+        got = oracle.canonical_digest({n: tuple(res[0][f"final/{n}"][:, i] for i in range(3))})[n]
+        a6 = g["a6"][n]
+        assert (got["rows"], got["sum"], got["sha256"]) == (a6["rows"], a6["sum"], a6["sha256"]), n
+        assert len({bytes(r[f"final_sha/{n}"]) for r in res}) == 1, n  # identical on every rank
+    x = np.stack([r["exchange"] for r in res])
+    assert int(x[:, 1].max()) < 2 ** 31 and int(x[:, 3].max()) < 2 ** 31
+    assert int(x[:, 0].sum()) == int(x[:, 2].sum()) == sum(g["rules"][n]["pairs"] for n in NAMES)
+    print("config4 full: count_s", [round(float(r["count_s"][0]), 2) for r in res],
+          "a6_s", {n: round(max(float(r[f"a6_s/{n}"][0]) for r in res), 2) for n in NAMES},
+          "words recv per rank", x[:, 2].tolist())
+
+
 def _check_covis_sharded(cfg, tmp_path, world, timeout=240):
     import otto_recommender_amd.synth as synth
     res = _launch("covis", cfg, tmp_path, world=world, timeout=timeout)

@@ -143,6 +143,33 @@ def test_kmeans_split_precision_steps_equal_exact_steps(gpu, monkeypatch, case):
         assert fits[0][2] == f[2] and fits[0][3] == f[3]
 
 
+def test_kmeans_half_rows_refused_outside_f16_range(gpu, monkeypatch):
+    """A feature scaled to ~1e5 is outside f16's range (65504): ottohip_kmeans_attach_half refuses the f16 copy
+    (ELIMIT, not an inf score that fminf would drop), KMeans.fit then scores the f32 rows, and the result is
+    bit-identical to OTTOHIP_KM_H16=0."""
+    import torch
+    from otto_recommender_amd import popularity as gp, _lib
+    rng = np.random.default_rng(23)
+    centers = rng.normal(scale=3, size=(12, 100))
+    X = (centers[rng.integers(0, 12, 12000)] + rng.normal(size=(12000, 100))).astype(np.float32)
+    X[:, 7] *= 4e4  # |x| up to ~1e5 in one column
+    Xd = torch.from_numpy(X).cuda()
+    ctx = _lib.context()
+    rc = _lib.load().ottohip_kmeans_attach_half(ctx.h, _lib.ptr(Xd), X.shape[0], X.shape[1], None)
+    assert rc == _lib.OTTOHIP_ELIMIT, rc
+    assert b"f16" in _lib.load().ottohip_last_error()
+    fits = []
+    monkeypatch.setenv("OTTOHIP_KM_GROUP", "1")
+    for h16 in ("0", "1"):
+        monkeypatch.setenv("OTTOHIP_KM_H16", h16)
+        km = gp.KMeans(n_clusters=10, random_state=42, n_init=2).fit(X)
+        fits.append((km.labels_.cpu().numpy(), km.cluster_centers_.cpu().numpy(), km.inertia_, km.n_iter_))
+    np.testing.assert_array_equal(fits[0][0], fits[1][0])
+    np.testing.assert_array_equal(fits[0][1], fits[1][1])
+    assert fits[0][2] == fits[1][2] and fits[0][3] == fits[1][3]
+    assert len(np.unique(fits[1][0])) == 10
+
+
 @pytest.mark.parametrize("case", ["sessions_k50", "relocation_k40", "blocks_k33"])
 def test_kmeans_lockstep_equals_single_runs(gpu, monkeypatch, case):
     """n_init runs in lockstep over one read of X per Lloyd step (ottohip_kmeans_lloyd_steps_multi, groups of
