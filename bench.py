@@ -362,10 +362,15 @@ def main():
     ctx = _lib.context()
     torch.cuda.synchronize()
 
+    # the build histograms click_to_click's rows per file (A6 branch (2) plans its row slices from them,
+    # model/count_co_events.py:136-153, without a count of its own); OTTOHIP_BENCH_PER_FILE=none: plain build
+    pfr = os.environ.get("OTTOHIP_BENCH_PER_FILE", "click_to_click")
+    pfr = None if pfr in ("", "none", "0") else pfr
+
     def step():
         if world > 1:  # local count -> pack by owner -> all-to-all-v (RCCL) -> merge-sum
-            return gd.count_co_events_sharded(dev, my_files, n_files, ctx=ctx)
-        return gc.count_co_events_fused(dev, ctx=ctx)
+            return gd.count_co_events_sharded(dev, my_files, n_files, ctx=ctx, per_file_rule=pfr)
+        return gc.count_co_events_fused(dev, ctx=ctx, per_file_rule=pfr)
 
     for _ in range(args.warmup):
         step().free()

@@ -86,6 +86,11 @@ typedef struct {
   int32_t max_dt;   /* config.MAX_TIME_TO_NEXT (+86400) */
   int32_t n_items;  /* aid range [0, n_items); OTTO: 1855603 */
   int32_t dedup;    /* 1 = df.unique() first (count_co_events.py:92) */
+  int32_t sym;      /* ottohip_covis_emit / ottohip_covis_reduce_received only: 1 = a symmetric rule (click_to_click,
+                       cart_to_cart, buy_to_buy: count_co_events.py:64-71 with the window symmetric in dt) sends and
+                       stores each unordered pair once, its mirror produced by the table's readers; both sides of
+                       one exchange must agree, and key cuts (ottohip_file_opts lo / hi) need 0. The other count
+                       calls decide this themselves. */
 } ottohip_covis_params;
 
 /* per-rule statistics of a count table */

@@ -35,7 +35,7 @@ class Events(ctypes.Structure):
 
 class CovisParams(ctypes.Structure):
     _fields_ = [("min_dt", ctypes.c_int32), ("max_dt", ctypes.c_int32), ("n_items", ctypes.c_int32),
-                ("dedup", ctypes.c_int32)]
+                ("dedup", ctypes.c_int32), ("sym", ctypes.c_int32)]
 
 
 class RuleStats(ctypes.Structure):

@@ -271,14 +271,23 @@ class FileCuts:
 
 
 def count_co_events_fused(events: DeviceEvents, names=None, n_items: int = config.N_ITEMS_OTTO, dedup: bool = True,
-                          stream=None, ctx=None, max_files: int | None = None, cuts: FileCuts | None = None) -> CovisTable:
+                          stream=None, ctx=None, max_files: int | None = None, cuts: FileCuts | None = None,
+                          per_file_rule: str | None = None) -> CovisTable:
     """All rules over all files of `events` in one device pass (per-file counts folded into
     count / count_ge2): count_co_events_all_files + the groupby of concat_files_w_stats.
     More files than one pass can tell apart (max_files_per_call) are counted in batches of
     whole files and the batch tables merge-summed: count, count_ge2 and the per-file row
     statistics are sums over disjoint file sets. cuts: per-file options of one rule (FileCuts);
-    with per_file=True the table carries file_rows_per_file / file_rows_ge2_per_file (numpy)."""
+    with per_file=True the table carries file_rows_per_file / file_rows_ge2_per_file (numpy).
+    per_file_rule: the same per-file row statistics of one rule from this count (the reduce leaves
+    histogram every per-file row of the rule), so that concat_files_w_stats_fused's part-wise branch (2)
+    needs no count of its own to plan its row slices (model/count_co_events.py:136-153)."""
     ctx = ctx or _lib.context()
+    if per_file_rule is not None and cuts is None and per_file_rule in (names or config.CO_EVENTS_TO_COUNT):
+        tab = count_co_events_fused(events, names, n_items, dedup, stream, ctx, max_files,
+                                    FileCuts(per_file_rule, per_file=True))
+        tab.per_file_rule = per_file_rule
+        return tab
     cap = max_files or max_files_per_call(names, n_items)
     if cuts is not None and cuts.per_file:
         cap = min(cap, 1024)  # the per-file histogram's file range (ottohip_file_opts), as in dist.py
@@ -495,7 +504,8 @@ def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTabl
             timings[stage] = timings.get(stage, 0.0) + t - t_last[0]
             t_last[0] = t
     own = table is None
-    tab = table if table is not None else count_co_events_fused(events, [name], n_items=n_items, ctx=ctx)
+    tab = table if table is not None else count_co_events_fused(events, [name], n_items=n_items, ctx=ctx,
+                                                                per_file_rule=name)
     st = tab.stats(name)
     use_ge2 = "click_to" in name and st["file_rows"] > click_filter_rows
     N = st["file_rows_ge2"] if use_ge2 else st["file_rows"]
@@ -510,9 +520,12 @@ def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTabl
     n_parts = math.ceil(N / optim_rows)
     max_rows_part = int(max_rows_groupby / N * optim_rows)
     mark("prelude")
-    t = count_co_events_fused(events, [name], n_items=n_items, ctx=ctx, cuts=FileCuts(name, per_file=True))
-    R = t.file_rows_ge2_per_file if use_ge2 else t.file_rows_per_file
-    t.free()
+    if getattr(tab, "per_file_rule", None) == name:  # the table's own count histogrammed every file's rows
+        R = tab.file_rows_ge2_per_file if use_ge2 else tab.file_rows_per_file
+    else:
+        t = count_co_events_fused(events, [name], n_items=n_items, ctx=ctx, cuts=FileCuts(name, per_file=True))
+        R = t.file_rows_ge2_per_file if use_ge2 else t.file_rows_per_file
+        t.free()
     if int(R.sum()) != N:
         raise RuntimeError(f"{name}: per-file rows sum to {int(R.sum())}, the table's N is {N}")
     mark("file_rows")
@@ -753,7 +766,7 @@ def count_co_events_build(dir_sessions, dir_stats, names=None, **kw):
     files = sorted(glob.glob(f"{dir_sessions}/*.parquet"))
     dev = DeviceEvents.from_parquet(files)
     n_items = _n_items_for_device(dev.aid)
-    tab = count_co_events_fused(dev, names, n_items=n_items)
+    tab = count_co_events_fused(dev, names, n_items=n_items, per_file_rule="click_to_click")
     for n in tab.names:
         a, b, c = (x.cpu().numpy() for x in concat_files_w_stats_fused(dev, n, table=tab, n_items=n_items, **kw))
         _write_table(f"{dir_stats}/{n}.parquet", a, b, c, np.int32)

@@ -456,6 +456,7 @@ static int file_opts_setup(ottohip_ctx* ctx, const ottohip_file_opts* o, int n_r
   if (fo.sym && (o->lo_file >= 0 || o->hi_file >= 0)) { set_error("file_opts: key cuts on a symmetric table"); return OTTOHIP_EINVAL; }
   fo.lo_file = o->lo_file < 0 ? 0xFFFFFFFFu : (uint32_t)o->lo_file;
   fo.hi_file = o->hi_file < 0 ? 0xFFFFFFFFu : (uint32_t)o->hi_file;
+  fo.cuts = (o->lo_file >= 0 || o->hi_file >= 0) ? 1u : 0u;
   fo.lo_key = o->lo_key;
   fo.hi_key = o->hi_key;
   OH_TRY(ctx->ws.get("fo_dropped", 1, &fo.dropped));
@@ -1046,7 +1047,10 @@ int ottohip_covis_emit(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
   E->n_parts = n_parts;
   E->ev = *ev;
   int rc;
-  if ((rc = setup_rules(rules, n_rules, params, n_files_total, E->F.R, E->F.Lt))) { delete E; return rc; }
+  if ((rc = setup_rules(rules, n_rules, params, n_files_total, E->F.R, E->F.Lt, /*allow_sym=*/params->sym != 0))) {
+    delete E;
+    return rc;
+  }
   if ((rc = covis_front(ctx, ev, params, file_ids, n_parts, E->F, s))) { delete E; return rc; }
   E->gen = ctx->gen;
   E->ctx = ctx;
@@ -1112,7 +1116,11 @@ int ottohip_covis_reduce_received_opts(ottohip_ctx* ctx, const ottohip_rule* rul
   ctx->reset_timing();
   RulesDev R;
   Layout Lt;
-  OH_TRY(setup_rules(rules, n_rules, params, std::max(n_files_total, 1), R, Lt));
+  if (params->sym && opts && (opts->lo_file >= 0 || opts->hi_file >= 0)) {
+    set_error("reduce_received: key cuts on symmetric storage (params->sym must be 0)"); return OTTOHIP_EINVAL;
+  }
+  // the senders' storage (ottohip_covis_emit with the same params->sym): symmetric rules once per unordered pair
+  OH_TRY(setup_rules(rules, n_rules, params, std::max(n_files_total, 1), R, Lt, /*allow_sym=*/params->sym != 0));
   if (n_words >= ((int64_t)1 << 40) || n_pieces >= ((int64_t)1 << 32)) { set_error("received input too large"); return OTTOHIP_ELIMIT; }
   ottohip_table* T = new_table(ctx, n_rules, params->n_items);
   auto fail = [&](int rc) { ottohip_table_free(T); return rc; };

@@ -106,6 +106,7 @@ struct FileOpts {
   int type;              // row type of the rule
   uint32_t q;            // the rule's index among the rules of its type (word bits above aid_next)
   uint32_t lo_file, hi_file;  // 0xFFFFFFFF: no cut
+  uint32_t cuts;              // lo_file or hi_file set (else the leaves skip the per-word drop test)
   uint64_t lo_key, hi_key;    // key = aid << 32 | aid_next
   unsigned long long* hist;   // [nf] or null
   uint32_t nf;
@@ -1037,10 +1038,12 @@ __device__ __forceinline__ void emit_flush2(EmitLds& S, int nrec, uint32_t tot, 
     // at record 0. A stale or extra mark (round 4: uninitialised mark[64..127] equal to a later round id) would
     // index past the records and write words at a wild address; instead the flush stops and the call fails
     // (err bit 8, "record index outside the flush's records")
+#ifndef OH_EMIT_NOCHECK  // (a cost A/B build only: tools/build_ab.sh -DOH_EMIT_NOCHECK)
     if (ob + (int)__popcll(mA) + (int)__popcll(mB) >= nrec || (c == 0 && !(mA & 1ull))) {
       if (l == 0) atomicOr(err, 8);
       break;
     }
+#endif
     ob += (int)__popcll(mA) + (int)__popcll(mB);
     const uint32_t pA = c + l, pB = c + 64 + l;
     bool qA = false, qB = false;
@@ -1083,7 +1086,9 @@ __device__ __forceinline__ void emit_flush2(EmitLds& S, int nrec, uint32_t tot, 
     cc = (uint32_t)__builtin_amdgcn_readlane((int)(carB + (uint32_t)__popcll(mineB)), 63);
   }
   // every record start falls in exactly one round: the marks seen must number nrec (always on, wave-uniform)
+#ifndef OH_EMIT_NOCHECK
   if (tot > 0 && ob != nrec - 1 && l == 0) atomicOr(err, 8);
+#endif
 }
 
 // Per event type, the (rule, next type) windows an event of that type writes, as pass 3's task list: entry
@@ -1786,7 +1791,7 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
     rkk = row_key[TT.row];
     ndd = 0;
     if constexpr (FO) {  // the cut words become W_EMPTY (sorted past the task's new end)
-      if ((int)(rkk >> A) == fo.type) {
+      if (fo.cuts && (int)(rkk >> A) == fo.type) {
         const int32_t ad = (int32_t)(rkk & L.amask);
         uint32_t k = 0;
 #pragma unroll
@@ -1922,6 +1927,7 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
     const uint32_t* W = (T.buf ? w1 : w0) + T.begin;
     const RowInfo ri = row_info(row_key, T.row, L.A);
     const bool fo_row = FO && ri.type == fo.type;
+    const bool fo_cut = fo_row && fo.cuts;
     uint32_t ndrop = 0, dbg_loaded = 0, dbg_ins = 0;
     const uint32_t dbound = T.len;
     // optimistic: more keys possible than fit; give up at 3/4 fill and send the task to a split
@@ -1956,7 +1962,7 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
         if constexpr (FO) {  // branch-free: the cut word becomes W_EMPTY (the if-form lost ~15% of the
                              // W_EMPTY writes under hipcc 7.2 -O3: counted and cut at once, found by the
                              // reduce's conservation check, tests/test_covis_gpu.py::test_file_cuts_hot_rows)
-          const bool dr = fo_row && fo_drop(fo, wbuf[j], ri.aid, L);
+          const bool dr = fo_cut && fo_drop(fo, wbuf[j], ri.aid, L);
           ndrop += dr ? 1u : 0u;
           wbuf[j] = dr ? W_EMPTY : wbuf[j];
         }

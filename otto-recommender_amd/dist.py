@@ -170,13 +170,14 @@ class OwnerEmit:
     buffers (ottohip_emit_write) and returns (words int32 [P], pieces int64 [rows])."""
 
     def __init__(self, events, n_parts: int, file_ids=None, n_files_total: int | None = None, names=None,
-                 n_items: int = config.N_ITEMS_OTTO, dedup: bool = True, stream=None, ctx=None):
+                 n_items: int = config.N_ITEMS_OTTO, dedup: bool = True, stream=None, ctx=None, sym: bool = False):
         from .covis import reference_rules
         self.ctx = ctx or _lib.context()
         self.names, rules = reference_rules(names)
         p = _lib.CovisParams()
         p.min_dt, p.max_dt, p.n_items, p.dedup = (config.MIN_TIME_TO_NEXT, config.MAX_TIME_TO_NEXT, int(n_items),
                                                   int(dedup))
+        p.sym = 1 if sym else 0  # symmetric rules sent once per unordered pair (the owners must reduce with sym)
         ev = events.abi()
         nf = ev.n_files
         fids = (ctypes.c_int32 * nf)(*(range(nf) if file_ids is None else [int(f) for f in file_ids]))
@@ -207,24 +208,25 @@ class OwnerEmit:
 
 
 def emit_for_owners(events, n_parts: int, file_ids=None, n_files_total: int | None = None, names=None,
-                    n_items: int = config.N_ITEMS_OTTO, dedup: bool = True, stream=None, ctx=None):
+                    n_items: int = config.N_ITEMS_OTTO, dedup: bool = True, stream=None, ctx=None, sym: bool = False):
     """Pair words of this rank's files, laid out owner-major (ottohip_covis_emit + emit_write).
     Returns (words int32 [P], words_per_owner, pieces int64 [rows], pieces_per_owner, names)."""
-    em = OwnerEmit(events, n_parts, file_ids, n_files_total, names, n_items, dedup, stream, ctx)
+    em = OwnerEmit(events, n_parts, file_ids, n_files_total, names, n_items, dedup, stream, ctx, sym)
     words, pieces = em.write()
     return words, em.words_per_owner, pieces, em.pieces_per_owner, em.names
 
 
 def reduce_received(words, pieces, names, n_files_total: int, n_items: int = config.N_ITEMS_OTTO, dedup: bool = True,
-                    stream=None, ctx=None, cuts=None):
+                    stream=None, ctx=None, cuts=None, sym: bool = False):
     """Assemble the received segments (one word range per row) and reduce them to a table.
     cuts: covis.FileCuts in global file ids (per_file: this owner's rows per file, which the caller
-    all-reduces)."""
+    all-reduces). sym: the senders' storage (OwnerEmit sym): symmetric rules once per unordered pair."""
     from .covis import CovisTable, reference_rules
     ctx = ctx or _lib.context()
     names, rules = reference_rules(names)
     p = _lib.CovisParams()
     p.min_dt, p.max_dt, p.n_items, p.dedup = config.MIN_TIME_TO_NEXT, config.MAX_TIME_TO_NEXT, int(n_items), int(dedup)
+    p.sym = 1 if sym else 0
     h = ctypes.c_void_p()
     nw, npc = int(words.numel()), int(pieces.numel())
     args = (ctx.h, rules, len(names), ctypes.byref(p), int(n_files_total), _lib.ptr(words) if nw else None, nw,
@@ -313,17 +315,25 @@ def allreduce_per_file(rows, rows2, group=None):
 
 def count_co_events_sharded(events, file_ids, n_files_total: int, group=None, names=None,
                             n_items: int = config.N_ITEMS_OTTO, dedup: bool = True, stream=None, ctx=None,
-                            chunks: int | None = None, max_files: int | None = None, cuts=None):
+                            chunks: int | None = None, max_files: int | None = None, cuts=None,
+                            per_file_rule: str | None = None):
     """The N-GPU build: this rank's whole files (global ids file_ids) -> pair words laid out by
     owner -> all-to-all-v of words and row pieces (RCCL) -> assemble + reduce of the owner's
     rows. Returns this rank's shard (rows with owner(aid) == rank) of the single-GPU table;
     its file_rows / file_rows_ge2 are the GLOBAL per-file row counts (all-reduced), which is
     what concat_files_w_stats compares against its thresholds (:131, :135). cuts: covis.FileCuts
-    in global file ids, applied by the owners; per_file statistics are all-reduced (global)."""
+    in global file ids, applied by the owners; per_file statistics are all-reduced (global).
+    per_file_rule: every global file's rows of that rule from this count (covis.count_co_events_fused's
+    option), so that concat_files_w_stats_sharded plans branch (2) without a count of its own."""
     import torch.distributed as dist
     import torch
-    from .covis import reference_rules
+    from .covis import reference_rules, FileCuts
     from .covis import max_files_per_call
+    if per_file_rule is not None and cuts is None and per_file_rule in (names or config.CO_EVENTS_TO_COUNT):
+        tab = count_co_events_sharded(events, file_ids, n_files_total, group, names, n_items, dedup, stream, ctx,
+                                      chunks, max_files, FileCuts(per_file_rule, per_file=True))
+        tab.per_file_rule = per_file_rule
+        return tab
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     cap = max_files or max_files_per_call(names, n_items)
@@ -339,6 +349,10 @@ def count_co_events_sharded(events, file_ids, n_files_total: int, group=None, na
     # exchanges (empty chunks included); the receiver concatenates the chunks' words and pieces in
     # arrival order, which keeps each piece's words where reduce_received expects them.
     n_chunks = chunks if chunks is not None else int(os.environ.get("OTTOHIP_DIST_CHUNKS", "2"))
+    # symmetric rules (click_to_click, cart_to_cart, buy_to_buy; model/count_co_events.py:64-71) go to the owners
+    # once per unordered pair: the row (a, b), a <= b, at owner(a), which also stands for its mirror (b, a) (the
+    # shard's readers produce it). Key cuts (branch (2)'s parts) need both orders stored; OTTOHIP_DIST_SYM=0 = off
+    sym = (cuts is None or (cuts.lo is None and cuts.hi is None)) and os.environ.get("OTTOHIP_DIST_SYM", "1") != "0"
     nf = len(events.file_bounds) - 1
     bounds = _chunk_files(events, max(1, n_chunks))
     names = reference_rules(names)[0]
@@ -353,7 +367,7 @@ def count_co_events_sharded(events, file_ids, n_files_total: int, group=None, na
         em = None
         if f1 > f0:
             sub = events if (f0, f1) == (0, nf) else events.subset_files(f0, f1)
-            em = OwnerEmit(sub, world, fids[f0:f1], n_files_total, names, n_items, dedup, stream, ctx)
+            em = OwnerEmit(sub, world, fids[f0:f1], n_files_total, names, n_items, dedup, stream, ctx, sym)
             wpp, ppp = em.words_per_owner, em.pieces_per_owner
         else:  # no files in this chunk (e.g. a rank without files of one part): it still joins the exchange
             wpp, ppp = [0] * world, [0] * world
@@ -385,7 +399,7 @@ def count_co_events_sharded(events, file_ids, n_files_total: int, group=None, na
         # work.wait() (RCCL) orders only torch's current stream after the transfer (and the cat ran
         # there): the caller's stream, on which the reduce runs, waits for it
         stream.wait_stream(torch.cuda.current_stream())
-    tab = reduce_received(rw, rp, names, n_files_total, n_items, dedup, stream, ctx, cuts)
+    tab = reduce_received(rw, rp, names, n_files_total, n_items, dedup, stream, ctx, cuts, sym)
     del rw, rp
     fs = allreduce_file_stats([(tab.stats(r)["file_rows"], tab.stats(r)["file_rows_ge2"]) for r in range(len(names))],
                               group)
@@ -447,13 +461,15 @@ def run_hist(x, lo: int, hi: int, shift: int, mask: int, n_bins: int, ctx=None, 
     return h
 
 
-def head_cut(aid, count, max_rows: int, n_items: int, group=None, ctx=None, stream=None) -> int:
+def head_cut(aid, aid_next, count, max_rows: int, n_items: int, group=None, ctx=None, stream=None) -> int:
     """Length of this shard's share of the GLOBAL head(max_rows) of the (count desc, aid asc,
     aid_next asc) order, given the shard's rows already in that order (a finalize output).
     Exact and collective (every rank calls it): the cut count c* is found by a two-level 16-bit
     radix select over all-reduced count histograms, ties at c* by an all-reduced histogram over
-    aid (all rows of one aid live on its owner, so the owner of the cut aid keeps the first r
-    of them). A shard's kept rows are always a prefix of its order."""
+    aid (a*), then ties at (c*, a*) by an all-reduced histogram over aid_next (n*): the rows of one
+    aid may sit on several ranks (a symmetric rule's shard holds the mirrors (b, a) of its rows
+    (a, b) at owner(a)), but every key (aid, aid_next) is on exactly one rank. A shard's kept rows
+    are always a prefix of its order."""
     import torch
     import torch.distributed as dist
     m = int(count.numel())
@@ -486,7 +502,14 @@ def head_cut(aid, count, max_rows: int, n_items: int, group=None, ctx=None, stre
     before = int(cg[a_star].item()) - int(g3[a_star].item())
     mine = int(h3[:a_star].sum().item())
     own = int(h3[a_star].item())
-    return lo_c + mine + (need - before if own > 0 else 0)
+    need2 = need - before  # (c*, a*) rows still to keep, 1 <= need2 <= g3[a_star]
+    # ties at (c*, a*): aid_next histogram of those rows (a contiguous aid_next-ascending range on each rank)
+    lo_a = lo_c + mine
+    h4 = run_hist(aid_next, lo_a, lo_a + own, 0, 0xFFFFFFFF, n_items, ctx, stream)
+    g4 = _allreduce_sum(h4, group)
+    cg4 = torch.cumsum(g4, 0)
+    n_star = int(torch.searchsorted(cg4, torch.tensor([need2], dtype=cg4.dtype, device=cg4.device)).item())
+    return lo_a + int(h4[:n_star + 1].sum().item())
 
 
 def _records(a, b, c):
@@ -540,7 +563,7 @@ def finalize_sharded(table, name, max_rows=None, params: dict | None = None, gat
     p = dict(params or {})
     p["max_rows_groupby"] = _HUGE
     a, b, c = table.finalize(name, max_rows=_HUGE, params=p, stream=stream)
-    k = head_cut(a, c, mr, n_items, group, ctx, stream)
+    k = head_cut(a, b, c, mr, n_items, group, ctx, stream)
     a, b, c = a[:k], b[:k], c[:k]
     if not gather:
         return a, b, c
@@ -581,7 +604,7 @@ def concat_files_w_stats_sharded(events, file_ids, n_files_total: int, name: str
     file_ids = [int(f) for f in file_ids]
     own = table is None
     tab = table if table is not None else count_co_events_sharded(events, file_ids, n_files_total, group, [name],
-                                                                  n_items, stream=stream, ctx=ctx)
+                                                                  n_items, stream=stream, ctx=ctx, per_file_rule=name)
     st = tab.stats(name)
     use_ge2 = "click_to" in name and st["file_rows"] > click_filter_rows
     N = st["file_rows_ge2"] if use_ge2 else st["file_rows"]
@@ -598,10 +621,13 @@ def concat_files_w_stats_sharded(events, file_ids, n_files_total: int, name: str
     fid = np.asarray(file_ids, np.int64)
     if np.any(np.diff(fid) <= 0):
         raise ValueError("file_ids must be increasing (the rank's files in events order)")
-    t = count_co_events_sharded(events, file_ids, n_files_total, group, [name], n_items, stream=stream, ctx=ctx,
-                                cuts=FileCuts(name, per_file=True))
-    R = t.file_rows_ge2_per_file if use_ge2 else t.file_rows_per_file
-    t.free()
+    if getattr(tab, "per_file_rule", None) == name:  # from the table's own count
+        R = tab.file_rows_ge2_per_file if use_ge2 else tab.file_rows_per_file
+    else:
+        t = count_co_events_sharded(events, file_ids, n_files_total, group, [name], n_items, stream=stream, ctx=ctx,
+                                    cuts=FileCuts(name, per_file=True))
+        R = t.file_rows_ge2_per_file if use_ge2 else t.file_rows_per_file
+        t.free()
     if int(R.sum()) != N:
         raise RuntimeError(f"{name}: per-file rows sum to {int(R.sum())}, the global N is {N}")
     plan = part_plan(R, n_parts)

@@ -141,9 +141,10 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
     pairs = 0
     for folder, mine, n_files in folders:
         if group is None:
-            tab = gc.count_co_events_fused(folder, n_items=n_items, ctx=ctx)
+            tab = gc.count_co_events_fused(folder, n_items=n_items, ctx=ctx, per_file_rule="click_to_click")
         else:
-            tab = gd.count_co_events_sharded(folder, mine, n_files, group, n_items=n_items, ctx=ctx)
+            tab = gd.count_co_events_sharded(folder, mine, n_files, group, n_items=n_items, ctx=ctx,
+                                                 per_file_rule="click_to_click")
         pairs += sum(tab.stats(n)["n_pairs"] for n in tab.names)
         t = mark("covis_count", t)
         for n in tab.names:

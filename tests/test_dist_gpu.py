@@ -19,6 +19,7 @@ import covis as oracle
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 NAMES = list(oracle.REFERENCE_RULES)
+SYM_RULES = {"click_to_click", "cart_to_cart", "buy_to_buy"}  # stored once per unordered pair in the shards
 
 
 def _free_port():
@@ -158,7 +159,8 @@ def test_covis_sharded_full_size_config4(gpu, tmp_path):
         assert len({bytes(r[f"final_sha/{n}"]) for r in res}) == 1, n  # identical on every rank
     x = np.stack([r["exchange"] for r in res])
     assert int(x[:, 1].max()) < 2 ** 31 and int(x[:, 3].max()) < 2 ** 31
-    assert int(x[:, 0].sum()) == int(x[:, 2].sum()) == sum(g["rules"][n]["pairs"] for n in NAMES)
+    # every word sent is received; the symmetric rules' pairs travel once per unordered pair
+    assert int(x[:, 0].sum()) == int(x[:, 2].sum()) < sum(g["rules"][n]["pairs"] for n in NAMES)
     print("config4 full: count_s", [round(float(r["count_s"][0]), 2) for r in res],
           "a6_s", {n: round(max(float(r[f"a6_s/{n}"][0]) for r in res), 2) for n in NAMES},
           "words recv per rank", x[:, 2].tolist())
@@ -177,7 +179,8 @@ def _check_covis_sharded(cfg, tmp_path, world, timeout=240):
         c = np.concatenate([p[n][2] for p in per_file]).astype(np.int64)
         ra, rb, rc = oracle._groupby_sum(a, b, c)
         _, _, rg = oracle._groupby_sum(a, b, np.where(c >= 2, c, 0))
-        own = _owner(ra, world)
+        # a symmetric rule is exchanged once per unordered pair: owner(min(aid, aid_next)) holds both orders
+        own = _owner(np.minimum(ra, rb) if n in SYM_RULES else ra, world)
         for r, got in enumerate(res):
             m = own == r
             np.testing.assert_array_equal(got[f"shard/{n}"], np.stack([ra[m], rb[m], rc[m], rg[m]], 1).astype(np.int64),

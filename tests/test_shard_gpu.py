@@ -162,12 +162,15 @@ def test_from_records_edges(gpu):
     assert c.tolist() == [3] and c2.tolist() == [3]
 
 
+@pytest.mark.parametrize("sym", [False, True])
 @pytest.mark.parametrize("ranks", [[[0, 2], [1]], [[0], [1], [2]], [[2], [], [0, 1]]])
-def test_pair_exchange_equals_global_count(gpu, three_files, ranks):
+def test_pair_exchange_equals_global_count(gpu, three_files, ranks, sym):
     """The scalable N-GPU path (emit owner-major words with global file ids -> per-owner
     segments -> assemble + reduce), emulated on one GPU: each owner's table equals the
     single-GPU/oracle table restricted to its aids, including count_ge2 (per-file rule) and
-    the per-file row statistics of its rows."""
+    the per-file row statistics of its rows. sym: the symmetric rules are sent once per unordered
+    pair, so owner(a) holds the rows (a, b) with a <= b and (through the shard's readers) their
+    mirrors (b, a): its rows are those whose min(aid, aid_next) it owns."""
     import torch
     from otto_recommender_amd import covis as gc, dist as gd
     ev, fb, per_file, exp = three_files
@@ -176,35 +179,41 @@ def test_pair_exchange_equals_global_count(gpu, three_files, ranks):
     segs = []
     for files in ranks:
         sub, bounds = _subset_events(ev, fb, files)
-        w, wpp, pc, ppp, names = gd.emit_for_owners(gc.DeviceEvents.from_host(sub, bounds), G, files, 3)
+        w, wpp, pc, ppp, names = gd.emit_for_owners(gc.DeviceEvents.from_host(sub, bounds), G, files, 3, sym=sym)
         assert sum(wpp) == w.numel() and sum(ppp) == pc.numel()
         segs.append((w.clone(), wpp, pc.clone(), ppp))
+    sym_rules = {"click_to_click", "cart_to_cart", "buy_to_buy"} if sym else set()
+    if sym:  # each unordered pair of a symmetric rule is sent once
+        assert sum(int(w.numel()) for w, _, _, _ in segs) < sum(int(exp[n][2].sum()) for n in NAMES)
     for p in range(G):
         ws = torch.cat([w[sum(wpp[:p]):sum(wpp[:p + 1])] for w, wpp, _, _ in segs])
         ps = torch.cat([pc[sum(ppp[:p]):sum(ppp[:p + 1])] for _, _, pc, ppp in segs])
-        shard = gd.reduce_received(ws, ps, NAMES, 3)
+        shard = gd.reduce_received(ws, ps, NAMES, 3, sym=sym)
         for n in NAMES:
             a, b, c, c2 = shard.to_numpy(n)
             ra, rb, rc, rg = exp[n]
-            k = gd.owner_of(ra, G) == p
+            k = gd.owner_of(np.minimum(ra, rb) if n in sym_rules else ra, G) == p
             np.testing.assert_array_equal(a, ra[k], err_msg=n)
             np.testing.assert_array_equal(b, rb[k], err_msg=n)
             np.testing.assert_array_equal(c, rc[k], err_msg=n)
             np.testing.assert_array_equal(c2, rg[k], err_msg=n)
             st = shard.stats(n)
             assert st["n_rows"] == int(k.sum()) and st["n_pairs"] == int(rc[k].sum())
-            own = [gd.owner_of(pf[n][0], G) == p for pf in per_file]
+            own = [gd.owner_of(np.minimum(pf[n][0], pf[n][1]) if n in sym_rules else pf[n][0], G) == p
+                   for pf in per_file]
             assert st["file_rows"] == sum(int(o.sum()) for o in own)
             assert st["file_rows_ge2"] == sum(int((pf[n][2][o] >= 2).sum()) for pf, o in zip(per_file, own))
         shard.free()
 
 
-def test_pair_exchange_single_owner_matches_count(gpu, three_files):
-    """n_parts = 1 through emit/reduce_received reproduces ottohip_covis_count exactly."""
+@pytest.mark.parametrize("sym", [False, True])
+def test_pair_exchange_single_owner_matches_count(gpu, three_files, sym):
+    """n_parts = 1 through emit/reduce_received reproduces ottohip_covis_count exactly (with and without
+    symmetric storage)."""
     from otto_recommender_amd import covis as gc, dist as gd
     ev, fb, _, exp = three_files
-    w, wpp, pc, ppp, names = gd.emit_for_owners(gc.DeviceEvents.from_host(ev, fb), 1)
-    t = gd.reduce_received(w, pc, NAMES, 3)
+    w, wpp, pc, ppp, names = gd.emit_for_owners(gc.DeviceEvents.from_host(ev, fb), 1, sym=sym)
+    t = gd.reduce_received(w, pc, NAMES, 3, sym=sym)
     ref = gc.count_co_events_fused(gc.DeviceEvents.from_host(ev, fb))
     for n in NAMES:
         for x, y in zip(t.to_numpy(n), ref.to_numpy(n)):
