@@ -501,6 +501,8 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     OH_HIP(hipMemsetAsync(fo.dropped, 0, 8, s));
   }
   const bool FOon = fopts != nullptr || fo_parts != nullptr;
+  // per-file rows only (no key cuts, no parts): the register sorts keep their occupancy (k_agg_sort<M, 2>)
+  const bool FOhist = FOon && !fo.cuts && !fo.parts && fo.hist != nullptr;
   // symmetric rules store one row per unordered pair; the readers produce the mirrors (T->sym_mask)
   const uint64_t n_slots = P;
   if (ctx->spare.cap >= n_slots) {
@@ -658,9 +660,12 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
 #define OH_SORT(c, M)                                                                                        \
     if (nlist[c]) {                                                                                          \
       const unsigned g_ = (unsigned)std::min<uint64_t>(ceil_div((int64_t)nlist[c], 4), sgrid);              \
-      if (FOon)                                                                                              \
-        k_agg_sort<M, true><<<g_, 256, 0, ss>>>(TL.sort[c], (int64_t)nlist[c], w0, w1, row_key, R, Lt, n_rules, \
-                                                Osort, fo);                                                  \
+      if (FOhist)                                                                                            \
+        k_agg_sort<M, 2><<<g_, 256, (size_t)fo.nf * 8, ss>>>(TL.sort[c], (int64_t)nlist[c], w0, w1, row_key, R,  \
+                                                            Lt, n_rules, Osort, fo);                         \
+      else if (FOon)                                                                                         \
+        k_agg_sort<M, 1><<<g_, 256, 0, ss>>>(TL.sort[c], (int64_t)nlist[c], w0, w1, row_key, R, Lt, n_rules, \
+                                             Osort, fo);                                                     \
       else                                                                                                   \
         k_agg_sort<M><<<g_, 256, 0, ss>>>(TL.sort[c], (int64_t)nlist[c], w0, w1, row_key, R, Lt, n_rules, Osort, \
                                           fo);                                                               \

@@ -1574,7 +1574,8 @@ __device__ __forceinline__ uint32_t excl_at(const uint32_t (&x)[M], int m, uint3
 // end), unsorted; rows go to the slots [obegin, obegin + olen) of the table (the task's own word range),
 // the rest of that range is marked empty. stgk / stgb: this wave's staging rows (64*M + 64 each),
 // sacc: this wave's statistics accumulator, P / fh: the FO kernels' part tables and per-file rows.
-template <int M, bool FO>
+// FO: the FileOpts rule's per-file rows (fh); PM: part mode may be on (fo.parts), else compiled out
+template <int M, bool FO, bool PM = FO>
 __device__ __forceinline__ void agg_fold(uint32_t (&v)[M], uint64_t obegin, uint32_t olen, uint32_t rk,
                                          const RulesDev& sR, const Layout& L, const OutRows& O, const FileOpts& fo,
                                          const PartLds* P, unsigned long long* fh, uint32_t* stgk, uint32_t* stgb,
@@ -1590,10 +1591,10 @@ __device__ __forceinline__ void agg_fold(uint32_t (&v)[M], uint64_t obegin, uint
   const uint32_t pl = l == 0u ? ~v[0] : pl0, nl = l == 63u ? W_EMPTY : nl0;
   // part mode: parts of the elements and of the cross-lane neighbours (words of one key are in file
   // order, and the part is non-decreasing in the file for a fixed key, so a part's words stay adjacent)
-  uint32_t pt[FO ? M : 1];
+  uint32_t pt[PM ? M : 1];
   uint32_t ppl = 0, pnl = 0;
-  const bool pmode = FO && fo.parts;
-  if constexpr (FO) {
+  const bool pmode = PM && fo.parts;
+  if constexpr (PM) {
     if (pmode) {
 #pragma unroll
       for (int m = 0; m < M; ++m) pt[m] = v[m] != W_EMPTY ? word_part(*P, v[m], rk & L.amask, L) : 0xFFu;
@@ -1615,7 +1616,7 @@ __device__ __forceinline__ void agg_fold(uint32_t (&v)[M], uint64_t obegin, uint
     c[m] = we | ((ws & we) << 11);
     b[m] = c[m];
     uint32_t kbs = (prv >> F) != (v[m] >> F) ? 1u : 0u, kbe = (nxt >> F) != (v[m] >> F) ? 1u : 0u;
-    if constexpr (FO) {
+    if constexpr (PM) {
       if (pmode) {  // a k-run is one (key, part)
         const uint32_t pp = m > 0 ? pt[m - 1] : ppl, pn = m < M - 1 ? pt[m + 1] : pnl;
         kbs |= pp != pt[m] ? 1u : 0u;
@@ -1679,7 +1680,7 @@ __device__ __forceinline__ void agg_fold(uint32_t (&v)[M], uint64_t obegin, uint
       const uint32_t k2 = v[m] >> F, q = k2 >> A, cnt = b[m] & 0xFFFFu, cc = c[m];
       const uint32_t slot = ke ? idx : (uint32_t)(64 * M) + l;
       uint32_t k2s = k2;
-      if constexpr (FO) {
+      if constexpr (PM) {
         if (pmode) k2s = k2 | (pt[m] << 24);  // the part rides above aid_next (< 2^24 in part mode)
       }
       stgk[slot] = k2s;
@@ -1753,24 +1754,30 @@ __device__ __forceinline__ void agg_fold(uint32_t (&v)[M], uint64_t obegin, uint
 // The next task's words are loaded while the current one is folded. Per-rule statistics go
 // through a per-wave LDS accumulator (one lane, after wave sums of packed 16-bit fields: a
 // task holds <= 1024 words), so no per-thread accumulator arrays take registers.
-template <int M, bool FO = false>
+// FOM: 0 no FileOpts; 1 FileOpts with key cuts / part mode (static per-file table of FO_MAXF rows + the part
+// tables in LDS); 2 per-file rows only (the histogram of the call's fo.nf files in dynamic LDS, fo.nf * 8 bytes:
+// the main build's statistics cost no occupancy)
+extern __shared__ unsigned long long agg_sort_fh_dyn[];
+template <int M, int FOM = 0>
 __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task* __restrict__ tasks, int64_t n_tasks,
                                                   const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
                                                   const uint32_t* __restrict__ row_key, RulesDev R, Layout L,
                                                   int n_rules, OutRows O, FileOpts fo) {
+  constexpr bool FO = FOM != 0;
   __shared__ unsigned long long sacc[4][STAT_STRIDE];
   __shared__ RulesDev sR;
   __shared__ uint32_t stg[4][2][64 * M + 64];  // per wave: output rows of one task (key2, count | count_ge2 << 16),
                                               // + one dummy slot per lane
-  __shared__ unsigned long long fh[FO ? FO_MAXF : 1];  // per-file rows of the FileOpts rule
-  __shared__ std::conditional_t<FO, PartLds, char> sP[1];  // part-mode tables (FO kernels only)
+  __shared__ unsigned long long fh_s[FOM == 1 ? FO_MAXF : 1];  // per-file rows of the FileOpts rule
+  __shared__ std::conditional_t<FOM == 1, PartLds, char> sP[1];  // part-mode tables (FOM 1 only)
+  unsigned long long* fh = FOM == 2 ? agg_sort_fh_dyn : fh_s;
   const uint32_t l = lane_id();
   const int wv = threadIdx.x >> 6;
   if (threadIdx.x == 0) sR = R;
   for (int i = (int)l; i < STAT_STRIDE; i += 64) sacc[wv][i] = 0;
   if constexpr (FO) {
     for (uint32_t i = threadIdx.x; i < fo.nf; i += blockDim.x) fh[i] = 0;
-    part_lds_load(fo, sP[0]);
+    if constexpr (FOM == 1) part_lds_load(fo, sP[0]);
   }
   __syncthreads();
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -1790,7 +1797,7 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
     }
     rkk = row_key[TT.row];
     ndd = 0;
-    if constexpr (FO) {  // the cut words become W_EMPTY (sorted past the task's new end)
+    if constexpr (FOM == 1) {  // the cut words become W_EMPTY (sorted past the task's new end)
       if (fo.cuts && (int)(rkk >> A) == fo.type) {
         const int32_t ad = (int32_t)(rkk & L.amask);
         uint32_t k = 0;
@@ -1814,8 +1821,8 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
     const uint32_t len = T.len - nd;
     if (FO && nd && l == 0) atomicAdd(fo.dropped, (unsigned long long)nd);
     if (FO && fo.dbg && l == 0) { atomicAdd(fo.dbg + 2, (unsigned long long)nd); atomicAdd(fo.dbg + 3, (unsigned long long)len); }
-    agg_fold<M, FO>(v, T.begin, T.len, rk, sR, L, O, fo, reinterpret_cast<const PartLds*>(sP), fh, stg[wv][0], stg[wv][1],
-                    sacc[wv]);
+    agg_fold<M, FO, FOM == 1>(v, T.begin, T.len, rk, sR, L, O, fo, reinterpret_cast<const PartLds*>(sP), fh,
+                              stg[wv][0], stg[wv][1], sacc[wv]);
     T = Tn;
     rk = rkn;
     nd = ndn;
