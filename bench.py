@@ -367,10 +367,14 @@ def main():
     pfr = os.environ.get("OTTOHIP_BENCH_PER_FILE", "click_to_click")
     pfr = None if pfr in ("", "none", "0") else pfr
 
+    # the build also keeps its pair words, so A6's branch-(2) part table is re-folded from them, not counted again
+    # (OTTOHIP_BENCH_KEEP=0: not kept)
+    keep = os.environ.get("OTTOHIP_BENCH_KEEP", "1") != "0"
+
     def step():
         if world > 1:  # local count -> pack by owner -> all-to-all-v (RCCL) -> merge-sum
             return gd.count_co_events_sharded(dev, my_files, n_files, ctx=ctx, per_file_rule=pfr)
-        return gc.count_co_events_fused(dev, ctx=ctx, per_file_rule=pfr)
+        return gc.count_co_events_fused(dev, ctx=ctx, per_file_rule=pfr, keep_words=keep)
 
     for _ in range(args.warmup):
         step().free()

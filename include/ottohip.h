@@ -139,6 +139,8 @@ typedef struct {
   uint64_t hi_key;
   int64_t* file_rows;
   int64_t* file_rows_ge2;
+  int32_t keep_words; /* 1: the table keeps the count's emitted pair words and rows (device memory, ~4 B per stored
+                         pair; freed with the table) for ottohip_table_count_parts */
 } ottohip_file_opts;
 int ottohip_covis_count_opts(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip_rule* rules, int n_rules,
                              const ottohip_covis_params* params, const ottohip_file_opts* opts, ottohip_table** out,
@@ -163,6 +165,13 @@ typedef struct {
 int ottohip_covis_count_parts(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip_rule* rules, int n_rules,
                               const ottohip_covis_params* params, const ottohip_part_opts* parts, ottohip_table** out,
                               void* stream);
+/* ottohip_covis_count_parts without counting again: the part-tagged table of `rule` (an index of t's rules) re-folded
+ * from the words t kept (ottohip_file_opts.keep_words; the count's file ids, parts as above). A symmetric rule's
+ * stored row (a, b), a <= b, yields its mirror (b, a) as an explicit row with the mirror's own part (a cut file's
+ * key comparison differs between the two orders): the result is non-symmetric, its slots are not in aid order,
+ * and ottohip_table_part_heads takes it as such. Other rules' words in the rule's rows are skipped. */
+int ottohip_table_count_parts(ottohip_ctx* ctx, const ottohip_table* t, int rule, const ottohip_part_opts* parts,
+                              ottohip_table** out, void* stream);
 /* Heads of every part of a ottohip_covis_count_parts table (:155-162 for all parts at once): per part p,
  * among its rows with v >= min_count (v = count_ge2 if use_ge2 else count), the first max_rows_part in
  * (v desc, aid asc, aid_next asc) order, selected by histograms (no sort). Written to out_records

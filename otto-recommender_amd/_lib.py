@@ -46,7 +46,7 @@ class RuleStats(ctypes.Structure):
 class FileOpts(ctypes.Structure):
     _fields_ = [("rule", ctypes.c_int32), ("lo_file", ctypes.c_int32), ("hi_file", ctypes.c_int32),
                 ("n_files", ctypes.c_int32), ("lo_key", ctypes.c_uint64), ("hi_key", ctypes.c_uint64),
-                ("file_rows", ctypes.c_void_p), ("file_rows_ge2", ctypes.c_void_p)]
+                ("file_rows", ctypes.c_void_p), ("file_rows_ge2", ctypes.c_void_p), ("keep_words", ctypes.c_int32)]
 
 
 class PartOpts(ctypes.Structure):
@@ -76,6 +76,8 @@ SIGNATURES = {
                                                 ctypes.POINTER(_VP), _VP]),
     "ottohip_covis_count_parts": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int, ctypes.POINTER(CovisParams),
                                                  ctypes.POINTER(PartOpts), ctypes.POINTER(_VP), _VP]),
+    "ottohip_table_count_parts": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.POINTER(PartOpts), ctypes.POINTER(_VP),
+                                                  _VP]),
     "ottohip_table_part_heads": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_int, _I32, _I64, _VP, _I64,
                                                 ctypes.POINTER(_I64), _VP]),
     "ottohip_table_keys_at": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_int, _VP, ctypes.c_int, _VP, _VP]),

@@ -249,13 +249,13 @@ class FileCuts:
     aid << 32 | aid_next; file = index among the call's files, or global id in the sharded calls);
     per_file=True reports every file's rows of the rule (file_rows / file_rows_ge2 per file)."""
 
-    def __init__(self, rule: str, lo=None, hi=None, per_file: bool = False):
-        self.rule, self.lo, self.hi, self.per_file = rule, lo, hi, per_file
+    def __init__(self, rule: str, lo=None, hi=None, per_file: bool = False, keep_words: bool = False):
+        self.rule, self.lo, self.hi, self.per_file, self.keep_words = rule, lo, hi, per_file, keep_words
 
     def shifted(self, f0: int, f1: int) -> "FileCuts":
         """The options of the files [f0, f1) renumbered from 0 (a batch of whole files)."""
         mv = lambda c: (c[0] - f0, c[1]) if c is not None and f0 <= c[0] < f1 else None
-        return FileCuts(self.rule, mv(self.lo), mv(self.hi), self.per_file)
+        return FileCuts(self.rule, mv(self.lo), mv(self.hi), self.per_file, self.keep_words)
 
     def abi(self, names, n_files: int):
         o = _lib.FileOpts()
@@ -263,6 +263,7 @@ class FileCuts:
         o.lo_file, o.lo_key = (int(self.lo[0]), int(self.lo[1])) if self.lo is not None else (-1, 0)
         o.hi_file, o.hi_key = (int(self.hi[0]), int(self.hi[1])) if self.hi is not None else (-1, 0)
         o.n_files = int(n_files)
+        o.keep_words = 1 if self.keep_words else 0
         rows = rows2 = None
         if self.per_file:
             rows, rows2 = np.zeros(max(n_files, 1), np.int64), np.zeros(max(n_files, 1), np.int64)
@@ -272,7 +273,7 @@ class FileCuts:
 
 def count_co_events_fused(events: DeviceEvents, names=None, n_items: int = config.N_ITEMS_OTTO, dedup: bool = True,
                           stream=None, ctx=None, max_files: int | None = None, cuts: FileCuts | None = None,
-                          per_file_rule: str | None = None) -> CovisTable:
+                          per_file_rule: str | None = None, keep_words: bool = False) -> CovisTable:
     """All rules over all files of `events` in one device pass (per-file counts folded into
     count / count_ge2): count_co_events_all_files + the groupby of concat_files_w_stats.
     More files than one pass can tell apart (max_files_per_call) are counted in batches of
@@ -281,12 +282,20 @@ def count_co_events_fused(events: DeviceEvents, names=None, n_items: int = confi
     with per_file=True the table carries file_rows_per_file / file_rows_ge2_per_file (numpy).
     per_file_rule: the same per-file row statistics of one rule from this count (the reduce leaves
     histogram every per-file row of the rule), so that concat_files_w_stats_fused's part-wise branch (2)
-    needs no count of its own to plan its row slices (model/count_co_events.py:136-153)."""
+    needs no count of its own to plan its row slices (model/count_co_events.py:136-153).
+    keep_words: the table keeps the count's pair words (one pass of files only), so that branch (2)'s part-tagged
+    table is re-folded from them (ottohip_table_count_parts) instead of counted again."""
     ctx = ctx or _lib.context()
-    if per_file_rule is not None and cuts is None and per_file_rule in (names or config.CO_EVENTS_TO_COUNT):
+    nf = len(events.file_bounds) - 1
+    keep = keep_words and nf <= (max_files or max_files_per_call(names, n_items))
+    if cuts is None and (keep or (per_file_rule is not None and per_file_rule in (names or config.CO_EVENTS_TO_COUNT))):
+        pfr = per_file_rule if per_file_rule in (names or config.CO_EVENTS_TO_COUNT) else None
         tab = count_co_events_fused(events, names, n_items, dedup, stream, ctx, max_files,
-                                    FileCuts(per_file_rule, per_file=True))
-        tab.per_file_rule = per_file_rule
+                                    FileCuts(pfr or list(names or config.CO_EVENTS_TO_COUNT)[0], per_file=pfr is not None,
+                                             keep_words=keep))
+        if pfr is not None:
+            tab.per_file_rule = pfr
+        tab.kept_words = keep
         return tab
     cap = max_files or max_files_per_call(names, n_items)
     if cuts is not None and cuts.per_file:
@@ -328,6 +337,7 @@ def count_co_events_fused(events: DeviceEvents, names=None, n_items: int = confi
     tab = CovisTable(h, names, ctx)
     if cuts.per_file:
         tab.file_rows_per_file, tab.file_rows_ge2_per_file = rows[:nf], rows2[:nf]
+    tab.kept_words = bool(cuts.keep_words)
     return tab
 
 
@@ -398,6 +408,21 @@ def count_co_events_parts(events: DeviceEvents, name: str, first_part, cuts, n_p
     _lib.check(_lib.load().ottohip_covis_count_parts(ctx.h, ctypes.byref(ev), rules, 1, ctypes.byref(p), ctypes.byref(po),
                                                      ctypes.byref(h), _lib.stream_handle(stream)))
     return CovisTable(h, [name] * int(n_parts), ctx)
+
+
+def table_count_parts(table: CovisTable, name: str, first_part, cuts, n_parts: int, stream=None) -> CovisTable:
+    """ottohip_table_count_parts: count_co_events_parts re-folded from the words `table` kept (its count's files and
+    file ids): rows (part, aid, aid_next) of rule `name`, a symmetric rule's mirrors as explicit rows."""
+    fp = np.ascontiguousarray(first_part, np.int32)
+    cf = np.ascontiguousarray([f for f, _ in cuts] or [0], np.int32)
+    ck = np.ascontiguousarray([k for _, k in cuts] or [0], np.uint64)
+    po = _lib.PartOpts()
+    po.n_files, po.n_parts, po.first_part = len(fp), int(n_parts), fp.ctypes.data
+    po.n_cuts, po.cut_file, po.cut_key = len(cuts), cf.ctypes.data, ck.ctypes.data
+    h = ctypes.c_void_p()
+    _lib.check(_lib.load().ottohip_table_count_parts(table.ctx.h, table.h, table._rule(name), ctypes.byref(po),
+                                                     ctypes.byref(h), _lib.stream_handle(stream)))
+    return CovisTable(h, [name] * int(n_parts), table.ctx)
 
 
 def part_heads(table: CovisTable, n_parts: int, use_ge2: bool, min_count: int, max_rows_part: int, stream=None):
@@ -505,7 +530,7 @@ def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTabl
             t_last[0] = t
     own = table is None
     tab = table if table is not None else count_co_events_fused(events, [name], n_items=n_items, ctx=ctx,
-                                                                per_file_rule=name)
+                                                                per_file_rule=name, keep_words=True)
     st = tab.stats(name)
     use_ge2 = "click_to" in name and st["file_rows"] > click_filter_rows
     N = st["file_rows_ge2"] if use_ge2 else st["file_rows"]
@@ -515,7 +540,7 @@ def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTabl
         if own:
             tab.free()
         return out
-    if own:
+    if own and not getattr(tab, "kept_words", False):
         tab.free()
     n_parts = math.ceil(N / optim_rows)
     max_rows_part = int(max_rows_groupby / N * optim_rows)
@@ -539,7 +564,12 @@ def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTabl
     fits = one_count and n_items <= (1 << 24) and nf <= max_files_per_call([name], n_items)
     assign = part_assignment(plan, R, keys) if fits else None
     if assign is not None:  # every part from ONE count (its rows carry their part)
-        t = count_co_events_parts(events, name, assign[0], assign[1], len(plan), n_items, ctx=ctx)
+        if getattr(tab, "kept_words", False) and tab.h:  # re-folded from the words of the table's own count
+            t = table_count_parts(tab, name, assign[0], assign[1], len(plan))
+        else:
+            t = count_co_events_parts(events, name, assign[0], assign[1], len(plan), n_items, ctx=ctx)
+        if own:
+            tab.free()
         mark("part_count")
         heads = part_heads(t, len(plan), use_ge2, part["min_count"], max_rows_part) if len(plan) <= 32 else None
         if heads is not None:  # every part's head at once (histogram cuts, no per-part sort)
@@ -551,6 +581,8 @@ def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTabl
         t.free()
         mark("part_finalize")
         plan = []
+    if own:
+        tab.free()
     for fa, lo, fb, hi in plan:
         cuts = FileCuts(name, lo=(0, keys[(fa, lo)]) if lo > 0 else None,
                         hi=(fb - fa, keys[(fb, hi)]) if hi < int(R[fb]) else None)

@@ -130,6 +130,25 @@ struct Front {
   uint64_t* row_begin = nullptr;
 };
 
+// a count's emitted words and rows, kept by the table (ottohip_file_opts.keep_words) for ottohip_table_count_parts
+struct KeptEmission {
+  uint32_t* words = nullptr;      // [P] row-major pair words, as emitted
+  uint32_t* row_key = nullptr;    // [Rn] (type << A) | aid, ascending
+  uint64_t* row_begin = nullptr;  // [Rn] first word of each row
+  uint64_t P = 0;
+  int64_t Rn = 0;
+  RulesDev R;
+  Layout Lt;
+  int n_rules = 0, n_files = 0;
+};
+void kept_free(KeptEmission* k) {
+  if (!k) return;
+  dev_free(k->words);
+  dev_free(k->row_key);
+  dev_free(k->row_begin);
+  delete k;
+}
+
 struct ottohip_emit {
   Front F;
   ottohip_events ev;
@@ -487,7 +506,9 @@ static int file_opts_finish(const ottohip_file_opts* o, const FileOpts& fo, hipS
 static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P, const uint64_t* row_begin,
                         const uint32_t* row_key, int64_t Rn, const RulesDev& R, const Layout& Lt, int n_rules,
                         ottohip_table* T, hipStream_t s, const ottohip_file_opts* fopts = nullptr,
-                        const FileOpts* fo_parts = nullptr) {
+                        const FileOpts* fo_parts = nullptr, uint32_t* w2 = nullptr, uint64_t row_base = 0) {
+  // w2: a third word buffer for the split levels >= 1 (level 0 splits w0 -> w1, then w1 <-> w2), so w0 keeps the
+  // emitted words (ottohip_file_opts.keep_words); row_base: row_begin values are offsets + row_base (a row range)
   Workspace& ws = ctx->ws;
   int rc;
   int* err;
@@ -504,7 +525,8 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   // per-file rows only (no key cuts, no parts): the register sorts keep their occupancy (k_agg_sort<M, 2>)
   const bool FOhist = FOon && !fo.cuts && !fo.parts && fo.hist != nullptr;
   // symmetric rules store one row per unordered pair; the readers produce the mirrors (T->sym_mask)
-  const uint64_t n_slots = P;
+  // part mode with explicit mirror rows: slots [P, 2P) hold the mirror of the row at slot - P
+  const uint64_t n_slots = (fo_parts && fo_parts->mirror_off) ? 2 * P : P;
   if (ctx->spare.cap >= n_slots) {
     T->b = ctx->spare;
     ctx->spare = TableBufs();
@@ -525,7 +547,7 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   if (getenv("OTTOHIP_REDUCE_DBG")) hipMemsetAsync(T->b.rule, 0xFF, n_slots, s);
   OutRows O;
   O.rule = T->b.rule; O.aid = T->b.aid; O.aid_next = T->b.aid_next; O.count = T->b.count; O.count_ge2 = T->b.count_ge2;
-  O.cap = P; O.stats = stats;
+  O.cap = n_slots; O.stats = stats;
   T->sym_mask = R.sym_mask;
   // profiling ablation: OTTOHIP_REDUCE_DBG=1 drops the register-sort kernels' row stores
   static const int rdbg = getenv("OTTOHIP_REDUCE_DBG") ? atoi(getenv("OTTOHIP_REDUCE_DBG")) : 0;
@@ -597,7 +619,7 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   };
   if ((rc = get_lists(cap0, "t_splitA", 0))) return rc;
   hipMemsetAsync(lcount, 0, 8 * 8, s);
-  k_classify_rows<<<grid_for(Rn), 256, 0, s>>>(row_begin, Rn, P, Lt.WB, TL, err);
+  k_classify_rows<<<grid_for(Rn), 256, 0, s>>>(row_begin, Rn, P, Lt.WB, TL, err, row_base);
   const int agg_grid = ctx->n_cu * 8;
   static const bool overlap = !(getenv("OTTOHIP_REDUCE_OVERLAP") && !strcmp(getenv("OTTOHIP_REDUCE_OVERLAP"), "0"));
   hipStream_t s2 = nullptr;
@@ -609,7 +631,9 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   bool drained = false;
   const bool dbg = getenv("OTTOHIP_DEBUG") != nullptr;
   if (dbg) fprintf(stderr, "[ottohip] P=%llu rows=%lld\n", (unsigned long long)P, (long long)Rn);
+  uint32_t* wcur0 = w0;  // the word buffer of tasks with buf 0 at this level (w2 from level 1 on, if given)
   for (int level = 0; level < 40; ++level) {
+    wcur0 = (level == 0 || !w2) ? w0 : w2;
     unsigned long long nlist[N_LISTS];
     if ((rc = d2h(nlist, lcount, N_LISTS, s))) return rc;
     if ((rc = d2h(&herr, err, 1, s))) return rc;
@@ -650,10 +674,10 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     auto launch_hash = [&]() {
       const unsigned hg = (unsigned)std::min<uint64_t>(nlist[N_SORT], (uint64_t)agg_grid);
       if (FOon)
-        k_agg_hash<true><<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], w0, w1, row_key, R, Lt, n_rules, O,
+        k_agg_hash<true><<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], wcur0, w1, row_key, R, Lt, n_rules, O,
                                               TL.split, lcount + N_SORT + 1, fo);
       else
-        k_agg_hash<<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], w0, w1, row_key, R, Lt, n_rules, O, TL.split,
+        k_agg_hash<<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], wcur0, w1, row_key, R, Lt, n_rules, O, TL.split,
                                         lcount + N_SORT + 1, fo);
     };
     if (hf) launch_hash();
@@ -661,13 +685,13 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     if (nlist[c]) {                                                                                          \
       const unsigned g_ = (unsigned)std::min<uint64_t>(ceil_div((int64_t)nlist[c], 4), sgrid);              \
       if (FOhist)                                                                                            \
-        k_agg_sort<M, 2><<<g_, 256, (size_t)fo.nf * 8, ss>>>(TL.sort[c], (int64_t)nlist[c], w0, w1, row_key, R,  \
+        k_agg_sort<M, 2><<<g_, 256, (size_t)fo.nf * 8, ss>>>(TL.sort[c], (int64_t)nlist[c], wcur0, w1, row_key, R,  \
                                                             Lt, n_rules, Osort, fo);                         \
       else if (FOon)                                                                                         \
-        k_agg_sort<M, 1><<<g_, 256, 0, ss>>>(TL.sort[c], (int64_t)nlist[c], w0, w1, row_key, R, Lt, n_rules, \
+        k_agg_sort<M, 1><<<g_, 256, 0, ss>>>(TL.sort[c], (int64_t)nlist[c], wcur0, w1, row_key, R, Lt, n_rules, \
                                              Osort, fo);                                                     \
       else                                                                                                   \
-        k_agg_sort<M><<<g_, 256, 0, ss>>>(TL.sort[c], (int64_t)nlist[c], w0, w1, row_key, R, Lt, n_rules, Osort, \
+        k_agg_sort<M><<<g_, 256, 0, ss>>>(TL.sort[c], (int64_t)nlist[c], wcur0, w1, row_key, R, Lt, n_rules, Osort, \
                                           fo);                                                               \
     }
     OH_SORT(0, 1) OH_SORT(1, 2) OH_SORT(2, 4) OH_SORT(3, 8) OH_SORT(4, 16)
@@ -676,10 +700,10 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     if (nlist[N_SORT + 2]) {  // LDS leaves (hot segments are appended to the split list)
       const unsigned lg = (unsigned)std::min<uint64_t>(nlist[N_SORT + 2], (uint64_t)ctx->n_cu * 4);
       if (FOon)
-        k_agg_lds<true><<<lg, LDS_T, 0, s>>>(TL.lds, (int64_t)nlist[N_SORT + 2], w0, w1, row_key, R, Lt, O, TL.split,
+        k_agg_lds<true><<<lg, LDS_T, 0, s>>>(TL.lds, (int64_t)nlist[N_SORT + 2], wcur0, w1, row_key, R, Lt, O, TL.split,
                                              lcount + N_SORT + 1, TL.cap + split_extra, err, fo);
       else
-        k_agg_lds<<<lg, LDS_T, 0, s>>>(TL.lds, (int64_t)nlist[N_SORT + 2], w0, w1, row_key, R, Lt, O, TL.split,
+        k_agg_lds<<<lg, LDS_T, 0, s>>>(TL.lds, (int64_t)nlist[N_SORT + 2], wcur0, w1, row_key, R, Lt, O, TL.split,
                                        lcount + N_SORT + 1, TL.cap + split_extra, err, fo);
     }
     if (nlist[N_SORT]) {  // tasks that overflow the LDS table are appended to the split list
@@ -739,13 +763,13 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
         (rc = ws.get("sp_ctask", (size_t)nchunks, &ctask)))
       return rc;
     k_split_chunk_task<<<grid_for(ns), 256, 0, s>>>(chb, nch, ns, ctask);
-    k_split_hist<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, w0, w1, Lt.F, hmat);
+    k_split_hist<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, wcur0, w1, Lt.F, hmat);
     if ((rc = exclusive_scan_u32(ctx, hmat, hoff, nent, hoff + nent, s))) return rc;
     static const int sub = getenv("OTTOHIP_SPLIT_SUB") ? atoi(getenv("OTTOHIP_SPLIT_SUB")) : 4096;  // A/B switch
     if (sub == 8192)
-      k_split_scatter<8192><<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, hoff, w0, w1, Lt.F, hmat);
+      k_split_scatter<8192><<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, hoff, wcur0, w1, Lt.F, hmat);
     else
-      k_split_scatter<4096><<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, hoff, w0, w1, Lt.F, hmat);
+      k_split_scatter<4096><<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, hoff, wcur0, w1, Lt.F, hmat);
     // next lists (a sub-bucket is one task in exactly one list: ndig bounds every list): the other
     // parity's set, last read by the sorts of level - 1
     if (s2 && level >= 1) OH_HIP(hipStreamWaitEvent(s, ctx->ev_join[(level + 1) & 1], 0));
@@ -933,16 +957,138 @@ int ottohip_covis_count_opts(ottohip_ctx* ctx, const ottohip_events* ev, const o
     set_error("file_opts: n_files=%d < the call's %d files", opts->n_files, ev->n_files); return OTTOHIP_EINVAL;
   }
   file_opts_zero(opts);
+  // options that change the reduce (key cuts, per-file rows); keep_words alone only keeps the words
+  const ottohip_file_opts* fo_eff =
+      (opts && (opts->lo_file >= 0 || opts->hi_file >= 0 || opts->file_rows || opts->file_rows_ge2)) ? opts : nullptr;
+  const bool keep = opts && opts->keep_words;
   ottohip_table* T = new_table(ctx, n_rules, params->n_items);
   auto fail = [&](int rc) { ottohip_table_free(T); return rc; };
   int rc;
   if ((rc = covis_front(ctx, ev, params, nullptr, 1, F, s))) return fail(rc);
   if (F.P == 0) { *out = T; return 0; }
-  uint32_t *w0, *w1;
+  uint32_t *w0, *w1, *w2 = nullptr;
   if ((rc = ctx->ws.get("words0", (size_t)F.P, &w0)) || (rc = ctx->ws.get("words1", (size_t)F.P, &w1))) return fail(rc);
+  if (keep && (rc = ctx->ws.get("words2", (size_t)F.P, &w2))) return fail(rc);
   if ((rc = covis_emit_words(ctx, F, ev, w0, s))) return fail(rc);
-  if ((rc = covis_reduce(ctx, w0, w1, F.P, F.row_begin, F.row_key, F.Rn, F.R, F.Lt, n_rules, T, s, opts)))
+  if ((rc = covis_reduce(ctx, w0, w1, F.P, F.row_begin, F.row_key, F.Rn, F.R, F.Lt, n_rules, T, s, fo_eff, nullptr, w2)))
     return fail(rc);
+  if (keep) {  // the table takes the emitted words (w0, untouched by the three-buffer reduce) and the rows
+    KeptEmission* K = new KeptEmission();
+    K->words = static_cast<uint32_t*>(ctx->ws.take("words0"));
+    K->row_key = static_cast<uint32_t*>(ctx->ws.take("row_key"));
+    K->row_begin = static_cast<uint64_t*>(ctx->ws.take("row_begin"));
+    K->P = F.P; K->Rn = F.Rn; K->R = F.R; K->Lt = F.Lt; K->n_rules = n_rules; K->n_files = ev->n_files;
+    T->kept = K;
+  }
+  *out = T;
+  return 0;
+}
+
+// rows [r0, r1) of one row type in a row-key-ordered row list (keys (type << A) | aid), and their words
+__global__ void k_type_span(const uint32_t* __restrict__ rk, const uint64_t* __restrict__ rb, int64_t Rn, uint64_t P,
+                            int A, uint32_t type, uint64_t* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int64_t r[2];
+  for (int k = 0; k < 2; ++k) {
+    int64_t lo = 0, hi = Rn;
+    while (lo < hi) {
+      const int64_t m = (lo + hi) >> 1;
+      if ((rk[m] >> A) < type + (uint32_t)k) lo = m + 1; else hi = m;
+    }
+    r[k] = lo;
+  }
+  out[0] = (uint64_t)r[0]; out[1] = (uint64_t)r[1];
+  out[2] = r[0] < Rn ? rb[r[0]] : P; out[3] = r[1] < Rn ? rb[r[1]] : P;
+}
+
+int ottohip_table_count_parts(ottohip_ctx* ctx, const ottohip_table* t, int rule, const ottohip_part_opts* po,
+                                         ottohip_table** out, void* stream) {
+  if (!ctx || !t || !po || !out || !po->first_part || (po->n_cuts > 0 && (!po->cut_file || !po->cut_key))) {
+    set_error("table_count_parts: NULL argument"); return OTTOHIP_EINVAL;
+  }
+  *out = nullptr;
+  if (!t->kept) { set_error("table_count_parts: the table kept no words (ottohip_file_opts.keep_words)"); return OTTOHIP_EINVAL; }
+  const KeptEmission& K = *t->kept;
+  if (rule < 0 || rule >= K.n_rules) { set_error("table_count_parts: rule %d outside the count's rules", rule); return OTTOHIP_EINVAL; }
+  const int nf = K.n_files;
+  if (po->n_files != nf) { set_error("table_count_parts: n_files=%d, the count had %d files", po->n_files, nf); return OTTOHIP_EINVAL; }
+  if (nf > FO_MAXF) { set_error("table_count_parts: %d files > %d", nf, FO_MAXF); return OTTOHIP_ELIMIT; }
+  if (po->n_parts < 1 || po->n_parts > 254) { set_error("table_count_parts: n_parts=%d outside [1, 254]", po->n_parts); return OTTOHIP_ELIMIT; }
+  if (po->n_cuts < 0 || po->n_cuts > FO_MAXCUT) { set_error("table_count_parts: n_cuts=%d outside [0, %d]", po->n_cuts, FO_MAXCUT); return OTTOHIP_ELIMIT; }
+  if (K.Lt.A > 24) { set_error("table_count_parts: n_items > 2^24"); return OTTOHIP_ELIMIT; }
+  std::vector<uint8_t> part_of(nf), cut_of(nf, FO_NOCUT);
+  for (int f = 0; f < nf; ++f) {
+    if (po->first_part[f] < 0 || po->first_part[f] >= po->n_parts) { set_error("table_count_parts: first_part[%d] out of range", f); return OTTOHIP_EINVAL; }
+    part_of[f] = (uint8_t)po->first_part[f];
+  }
+  for (int c = 0; c < po->n_cuts; ++c) {
+    const int f = po->cut_file[c];
+    if (f < 0 || f >= nf || cut_of[f] != FO_NOCUT || part_of[f] + 1 >= po->n_parts) {
+      set_error("table_count_parts: cut %d (file %d) invalid: one cut per file, inside the parts", c, f); return OTTOHIP_EINVAL;
+    }
+    cut_of[f] = (uint8_t)c;
+  }
+  int type = -1, q = -1;
+  for (int tt = 0; tt < 3; ++tt)
+    for (int qq = 0; qq < K.R.n_of_type[tt]; ++qq)
+      if (K.R.rule_of_type[tt][qq] == rule) { type = tt; q = qq; }
+  if (type < 0) { set_error("table_count_parts: rule %d has no row type", rule); return OTTOHIP_EINVAL; }
+  hipStream_t s = S(stream);
+  OH_HIP(hipSetDevice(ctx->device));
+  ctx->reset_timing();
+  Workspace& ws = ctx->ws;
+  uint64_t* span;
+  OH_TRY(ws.get("tcp_span", 4, &span));
+  k_type_span<<<1, 64, 0, s>>>(K.row_key, K.row_begin, K.Rn, K.P, K.Lt.A, (uint32_t)type, span);
+  uint64_t sp[4];
+  OH_TRY(d2h(sp, span, 4, s));
+  const int64_t r0 = (int64_t)sp[0], r1 = (int64_t)sp[1];
+  const uint64_t wlo = sp[2], Psub = sp[3] - sp[2];
+  ottohip_table* T = new_table(ctx, 1, t->n_items);
+  auto fail = [&](int rc) { ottohip_table_free(T); return rc; };
+  T->n_rules = po->n_parts;
+  if (Psub == 0 || r1 <= r0) { *out = T; return 0; }
+  int rc;
+  uint32_t *w1, *w2;
+  if ((rc = ws.get("words1", (size_t)Psub, &w1)) || (rc = ws.get("words2", (size_t)Psub, &w2))) return fail(rc);
+  FileOpts fo;
+  memset(&fo, 0, sizeof fo);
+  fo.type = type;
+  fo.q = (uint32_t)q;
+  fo.lo_file = fo.hi_file = 0xFFFFFFFFu;
+  fo.nf = (uint32_t)nf;
+  fo.parts = 1;
+  fo.qonly = 1;  // the type's other rules' words are skipped (counted as dropped)
+  fo.mirror_off = ((K.R.sym_mask >> rule) & 1u) ? Psub : 0ull;
+  fo.ncut = (uint32_t)po->n_cuts;
+  for (int c = 0; c < po->n_cuts; ++c) fo.cut_key[c] = po->cut_key[c];
+  uint8_t *d_part, *d_cut;
+  if ((rc = ws.get("fo_part_of", (size_t)nf, &d_part)) || (rc = ws.get("fo_cut_of", (size_t)nf, &d_cut))) return fail(rc);
+  OH_HIP(hipMemcpyAsync(d_part, part_of.data(), nf, hipMemcpyHostToDevice, s));
+  OH_HIP(hipMemcpyAsync(d_cut, cut_of.data(), nf, hipMemcpyHostToDevice, s));
+  OH_HIP(hipStreamSynchronize(s));  // host vectors
+  fo.part_of = d_part;
+  fo.cut_of = d_cut;
+  // the kept words are only read: the level-0 split writes w1, the later levels w1 <-> w2
+  if ((rc = covis_reduce(ctx, K.words + wlo, w1, Psub, K.row_begin + r0, K.row_key + r0, r1 - r0, K.R, K.Lt, K.n_rules, T,
+                         s, nullptr, &fo, w2, wlo)))
+    return fail(rc);
+  T->sym_mask = 0;  // explicit rows (the mirrors written by the leaves)
+  T->aid_ordered = fo.mirror_off == 0;
+  T->n_rules = po->n_parts;
+  unsigned long long* ph;
+  if ((rc = ws.get("part_hist", 512, &ph))) return fail(rc);
+  OH_HIP(hipMemsetAsync(ph, 0, 512 * 8, s));
+  k_rule_hist<<<(unsigned)std::min<int64_t>(ceil_div((int64_t)T->n_slots, 256 * SLOTS_T), (int64_t)ctx->n_cu * 8), 256, 0, s>>>(
+      T->b.rule, T->b.count, T->n_slots, ph, ph + 256);
+  OH_HIP(hipGetLastError());
+  std::vector<unsigned long long> hh(512);
+  if ((rc = d2h(hh.data(), ph, hh.size(), s))) return fail(rc);
+  for (int p = 0; p < po->n_parts; ++p) {
+    T->stats[p] = ottohip_rule_stats{};
+    T->stats[p].n_rows = (int64_t)hh[p];
+    T->stats[p].n_pairs = (int64_t)hh[256 + p];
+  }
   *out = T;
   return 0;
 }
@@ -1367,6 +1513,7 @@ void ottohip_table_free(ottohip_table* t) {
   } else {
     t->b.release();
   }
+  kept_free(t->kept);
   delete t;
 }
 
@@ -1414,6 +1561,33 @@ extern "C" int ottohip_table_part_heads(ottohip_ctx* ctx, const ottohip_table* t
     if (need[p] < h[v]) { pc.stage[p] = 1; ++n_tie; }  // ties at c*: cut by (aid, aid_next)
   }
   const int64_t ni = t->n_items;
+  if (n_tie && !t->aid_ordered) {
+    // stage 1 (a*) on slots not in aid order: a histogram over the aids of each part's tie rows, then the aid
+    // where the tie rows' running count reaches the rank left
+    int nq = 0;
+    std::vector<int> qpart;
+    for (int p = 0; p < n_parts; ++p)
+      if (pc.stage[p] == 1u) { qpart.push_back(p); ++nq; }
+    uint32_t *ah, *found;
+    uint64_t* ex;
+    OH_TRY(ws.get("ph_aid_hist", (size_t)nq * ni, &ah));
+    OH_TRY(ws.get("ph_tie_ex", (size_t)ni, &ex));
+    OH_TRY(ws.get("ph_found", 2 * PH_MAXP, &found));
+    OH_HIP(hipMemsetAsync(ah, 0, (size_t)nq * ni * 4, s));
+    k_ph_tie_aid_hist<<<sgrid, 256, 0, s>>>(t->b.rule, t->b.aid, t->b.count, t->b.count_ge2, n, n_parts, use_ge2, pc, ni,
+                                            ah);
+    for (int q = 0; q < nq; ++q) {
+      const int p = qpart[q];
+      OH_TRY(exclusive_scan_u32(ctx, ah + (size_t)q * ni, ex, ni, nullptr, s));
+      OH_HIP(hipMemsetAsync(found, 0xFF, 8, s));
+      k_ph_find<<<grid_for(ni), 256, 0, s>>>(ex, ah + (size_t)q * ni, ni, need[p], found);
+      uint32_t fr[2];
+      OH_TRY(d2h(fr, found, 2, s));
+      if (fr[0] == 0xFFFFFFFFu) { set_error("table_part_heads: tie cut not found (part %d)", p); return OTTOHIP_EHIP; }
+      pc.astar[p] = fr[0];
+      pc.stage[p] = 2;
+    }
+  }
   if (n_tie) {
     // stage 1 (a*): rank search over the parts' tie rows in slot order (= aid order)
     const int64_t nb1 = ceil_div(n, FIN_B);
@@ -1422,11 +1596,13 @@ extern "C" int ottohip_table_part_heads(ottohip_ctx* ctx, const ottohip_table* t
     int nq = 0;
     for (int p = 0; p < n_parts; ++p)
       if (pc.stage[p] == 1u) { rk.need[nq] = need[p]; rk.part[nq] = (uint32_t)p; ++nq; }
-    uint32_t *rcnt, *found, *astar;
+    uint32_t* found;
+    OH_TRY(ws.get("ph_found", 2 * PH_MAXP, &found));
+    if (nq > 0) {  // (none left when the unordered table's stage 1 above took every tie part)
+    uint32_t *rcnt, *astar;
     uint64_t* rex;
     OH_TRY(ws.get("ph_rank_cnt", (size_t)nq * nb1, &rcnt));
     OH_TRY(ws.get("ph_rank_ex", (size_t)nq * nb1, &rex));
-    OH_TRY(ws.get("ph_found", 2 * PH_MAXP, &found));
     OH_TRY(ws.get("ph_astar", PH_MAXP, &astar));
     k_ph_rank_count<<<(unsigned)nb1, FIN_T, 0, s>>>(t->b.rule, t->b.count, t->b.count_ge2, n, n_parts, use_ge2, pc, nb1,
                                                      rcnt);
@@ -1443,6 +1619,7 @@ extern "C" int ottohip_table_part_heads(ottohip_ctx* ctx, const ottohip_table* t
       if (as[q] == 0xFFFFFFFFu) { set_error("table_part_heads: tie cut not found (part %d)", p); return OTTOHIP_EHIP; }
       pc.astar[p] = as[q];
       pc.stage[p] = 2;
+    }
     }
     // stage 2 (n*): aid_next histogram of the (c*, a*) tie rows; the rank left = need - ties with aid < a*
     uint32_t* th;

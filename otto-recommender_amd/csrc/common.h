@@ -74,6 +74,14 @@ struct Workspace {
     for (auto& kv : bufs) if (kv.second.p) dev_free(kv.second.p);
     bufs.clear();
   }
+  // hand a buffer over to the caller (who frees it with dev_free); the next get() allocates a new one
+  void* take(const char* name) {
+    auto it = bufs.find(name);
+    if (it == bufs.end()) return nullptr;
+    void* p = it->second.p;
+    bufs.erase(it);
+    return p;
+  }
 };
 
 struct Phase { std::string name; hipEvent_t a, b; double bytes; };
@@ -126,6 +134,9 @@ struct Ctx {
   bool km_bvalid = false;
   // half-precision rows of an attached KMeans matrix (ottohip_kmeans_attach_half): the E-step of
   // ottohip_kmeans_lloyd_steps on that X reads them (and the rows' exact squared norms) instead of the f32 rows
+  // the last ottohip_kmeans_attach_half found every |x| within the f16 range bound; beyond it the distance bounds
+  // are off too (two identical fits at |x| ~ 1e5 diverged with them on: tools/dbg/km_range2.py)
+  bool km_range_ok = true;
   const void* km_hX = nullptr;
   int64_t km_hn = -1;
   int km_hdim = 0;

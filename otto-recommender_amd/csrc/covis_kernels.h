@@ -119,6 +119,12 @@ struct FileOpts {
   const uint8_t* cut_of;      // device [nf]: index into cut_key, FO_NOCUT = none
   uint32_t ncut;
   uint64_t cut_key[FO_MAXCUT];
+  // part mode over the retained words of a multi-rule count (ottohip_table_count_parts): the words of the type's
+  // other rules are dropped (qonly), and a symmetric rule's stored row (a, b), a <= b, also yields its mirror
+  // (b, a) as an explicit row in the slot mirror_off + slot of the (non-symmetric) part table, with the mirror's
+  // own part (a cut file's key comparison differs between (a, b) and (b, a))
+  uint32_t qonly;
+  uint64_t mirror_off;        // 0: no mirror rows
   unsigned long long* dropped;  // words dropped by the cuts (the reduce's conservation check)
   unsigned long long* dbg;      // OTTOHIP_DEBUG: [hash dropped, hash kept, sort dropped, sort kept] or null
   unsigned long long* prof;     // OTTOHIP_HASH_PROF: per hash task {len | rows << 32, wall-clock ticks | full << 63} or null
@@ -141,8 +147,16 @@ __device__ __forceinline__ uint32_t word_part(const PartLds& P, uint32_t w, uint
   const uint64_t key = ((uint64_t)aid << 32) | ((w >> L.F) & L.amask);
   return (uint32_t)P.part_of[f] + ((ci != FO_NOCUT && key >= P.cut_key[ci & (FO_MAXCUT - 1)]) ? 1u : 0u);
 }
+// part of the mirror (aid_next, aid) of word w (valid) of row aid
+__device__ __forceinline__ uint32_t word_part_mirror(const PartLds& P, uint32_t w, uint32_t aid, const Layout& L) {
+  const uint32_t f = w & ((1u << L.F) - 1u);
+  const uint32_t ci = P.cut_of[f];
+  const uint64_t key = ((uint64_t)((w >> L.F) & L.amask) << 32) | aid;
+  return (uint32_t)P.part_of[f] + ((ci != FO_NOCUT && key >= P.cut_key[ci & (FO_MAXCUT - 1)]) ? 1u : 0u);
+}
 __device__ __forceinline__ bool fo_drop(const FileOpts& fo, uint32_t w, int32_t aid, const Layout& L) {
-  if (w == W_EMPTY || (w >> (L.A + L.F)) != fo.q) return false;
+  if (w == W_EMPTY) return false;
+  if ((w >> (L.A + L.F)) != fo.q) return fo.qonly != 0;
   const uint32_t f = w & ((1u << L.F) - 1u);
   const uint64_t key = ((uint64_t)(uint32_t)aid << 32) | ((w >> L.F) & L.amask);
   return (f == fo.lo_file && key < fo.lo_key) || (f == fo.hi_file && key >= fo.hi_key);
@@ -1032,17 +1046,15 @@ __device__ __forceinline__ void emit_flush2(EmitLds& S, int nrec, uint32_t tot, 
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     const uint64_t mA = __ballot(S.mark[l] == rid), mB = __ballot(S.mark[64 + l] == rid);
     const uint64_t mleA = mA & upto, mleB = mB & upto;
+#ifndef OH_EMIT_NOCHECK  // (a cost A/B build only: tools/build_ab.sh -DOH_EMIT_NOCHECK)
+    // always on: a lane's record index is clamped into [0, nrec), so a stale or extra mark (round 4: uninitialised
+    // mark[64..127] equal to a later round id) can no longer index past the records and write words at a wild
+    // address; the count of marks is checked after the loop (err bit 8) and the call fails
+    const int oA = min(max(ob + (int)__popcll(mleA), 0), nrec - 1);
+    const int oB = min(max(ob + (int)__popcll(mA) + (int)__popcll(mleB), 0), nrec - 1);
+#else
     const int oA = ob + (int)__popcll(mleA);
     const int oB = ob + (int)__popcll(mA) + (int)__popcll(mleB);
-    // always-on, wave-uniform: the marks seen so far must name records [0, nrec) and the first round must start
-    // at record 0. A stale or extra mark (round 4: uninitialised mark[64..127] equal to a later round id) would
-    // index past the records and write words at a wild address; instead the flush stops and the call fails
-    // (err bit 8, "record index outside the flush's records")
-#ifndef OH_EMIT_NOCHECK  // (a cost A/B build only: tools/build_ab.sh -DOH_EMIT_NOCHECK)
-    if (ob + (int)__popcll(mA) + (int)__popcll(mB) >= nrec || (c == 0 && !(mA & 1ull))) {
-      if (l == 0) atomicOr(err, 8);
-      break;
-    }
 #endif
     ob += (int)__popcll(mA) + (int)__popcll(mB);
     const uint32_t pA = c + l, pB = c + 64 + l;
@@ -1574,34 +1586,19 @@ __device__ __forceinline__ uint32_t excl_at(const uint32_t (&x)[M], int m, uint3
 // end), unsorted; rows go to the slots [obegin, obegin + olen) of the table (the task's own word range),
 // the rest of that range is marked empty. stgk / stgb: this wave's staging rows (64*M + 64 each),
 // sacc: this wave's statistics accumulator, P / fh: the FO kernels' part tables and per-file rows.
-// FO: the FileOpts rule's per-file rows (fh); PM: part mode may be on (fo.parts), else compiled out
-template <int M, bool FO, bool PM = FO>
-__device__ __forceinline__ void agg_fold(uint32_t (&v)[M], uint64_t obegin, uint32_t olen, uint32_t rk,
-                                         const RulesDev& sR, const Layout& L, const OutRows& O, const FileOpts& fo,
-                                         const PartLds* P, unsigned long long* fh, uint32_t* stgk, uint32_t* stgb,
-                                         unsigned long long* sacc) {
+// One run-fold pass over a sorted task (v, with the cross-lane neighbours pl / nl): rows (one per k-run end) are
+// staged in this wave's LDS and written to the slots [obegin, obegin + olen). PM: pt holds each element's part
+// (pmode), and a k-run is one (key, part). MIRROR: the pass writes the explicit mirror rows (part, aid_next, aid)
+// of a symmetric rule's stored rows (pt = the mirrors' parts; the diagonal aid_next == aid has no mirror) and
+// takes no statistics; else FO adds the FileOpts rule's per-file rows (fh) and the per-rule statistics go to sacc.
+template <int M, bool FO, bool PM, bool MIRROR>
+__device__ __forceinline__ uint32_t fold_pass(const uint32_t (&v)[M], uint32_t pl, uint32_t nl, const uint32_t* pt,
+                                          uint32_t ppl, uint32_t pnl, bool pmode, uint64_t obegin, uint32_t olen,
+                                          uint32_t rk, const RulesDev& sR, const Layout& L, const OutRows& O,
+                                          const FileOpts& fo, unsigned long long* fh, uint32_t* stgk, uint32_t* stgb,
+                                          unsigned long long* sacc) {
   const uint32_t l = lane_id();
   const int F = L.F, A = L.A;
-  wave_bitonic_sort<M>(v);
-  // neighbours across lanes; lane 0's predecessor and lane 63's successor are sentinels that differ
-  // from the element in every field (so no element needs an index test: words are < W_EMPTY, and the
-  // invalid tail is W_EMPTY, sorted last). All flags below are branch-free selects: the former
-  // short-circuit tests (e < len && (e == 0 || ...)) compiled to exec-mask branches per element.
-  const uint32_t pl0 = lane_prev(v[M - 1]), nl0 = lane_next(v[0]);
-  const uint32_t pl = l == 0u ? ~v[0] : pl0, nl = l == 63u ? W_EMPTY : nl0;
-  // part mode: parts of the elements and of the cross-lane neighbours (words of one key are in file
-  // order, and the part is non-decreasing in the file for a fixed key, so a part's words stay adjacent)
-  uint32_t pt[PM ? M : 1];
-  uint32_t ppl = 0, pnl = 0;
-  const bool pmode = PM && fo.parts;
-  if constexpr (PM) {
-    if (pmode) {
-#pragma unroll
-      for (int m = 0; m < M; ++m) pt[m] = v[m] != W_EMPTY ? word_part(*P, v[m], rk & L.amask, L) : 0xFFu;
-      ppl = lane_prev(pt[M - 1]);
-      pnl = lane_next(pt[0]);
-    }
-  }
   // (1) run flags from the neighbours (a w-run = one word = one (rule, aid_next, file)):
   //     X = [w-run end] | [singleton w-run] << 11, summed by one scan (fields <= 1024);
   //     k-run (rule, aid_next) starts and ends as bit masks over the lane's elements
@@ -1626,7 +1623,7 @@ __device__ __forceinline__ void agg_fold(uint32_t (&v)[M], uint64_t obegin, uint
     kst |= (valid & kbs) << m;
     kend |= (valid & kbe) << m;
   }
-  if constexpr (FO) {  // one per-file row per w-run end of the rule; a singleton w-run has count 1
+  if constexpr (FO && !MIRROR) {  // one per-file row per w-run end of the rule; a singleton w-run has count 1
     if (fo.hist && (int)(rk >> A) == fo.type) {
 #pragma unroll
       for (int m = 0; m < M; ++m)
@@ -1686,16 +1683,18 @@ __device__ __forceinline__ void agg_fold(uint32_t (&v)[M], uint64_t obegin, uint
       stgk[slot] = k2s;
       stgb[slot] = b[m];
       idx += ke;
-      const uint32_t offd = (k2 & L.amask) != (uint32_t)aid ? 1u : 0u;
-      const uint32_t mult = 1u + (offd & (q == 0 ? sym0 : (q == 1 ? sym1 : 0u)));
-      const uint32_t ra = (1u | ((cc & 0xFFFFu) << 16)) * mult, rb = (cnt | (cc & 0xFFFF0000u)) * mult;
-      sraw += ke ? (1u | (cnt << 16)) : 0u;
-      s0a += (ke && q == 0) ? ra : 0u; s0b += (ke && q == 0) ? rb : 0u;
-      s1a += (ke && q == 1) ? ra : 0u; s1b += (ke && q == 1) ? rb : 0u;
-      q2 |= (ke && q >= 2) ? 1u : 0u;
+      if constexpr (!MIRROR) {
+        const uint32_t offd = (k2 & L.amask) != (uint32_t)aid ? 1u : 0u;
+        const uint32_t mult = 1u + (offd & (q == 0 ? sym0 : (q == 1 ? sym1 : 0u)));
+        const uint32_t ra = (1u | ((cc & 0xFFFFu) << 16)) * mult, rb = (cnt | (cc & 0xFFFF0000u)) * mult;
+        sraw += ke ? (1u | (cnt << 16)) : 0u;
+        s0a += (ke && q == 0) ? ra : 0u; s0b += (ke && q == 0) ? rb : 0u;
+        s1a += (ke && q == 1) ? ra : 0u; s1b += (ke && q == 1) ? rb : 0u;
+        q2 |= (ke && q >= 2) ? 1u : 0u;
+      }
     }
   }
-  if (__ballot(q2 != 0u)) {  // more than 2 rules of one type (not in the reference's five)
+  if (!MIRROR && __ballot(q2 != 0u)) {  // more than 2 rules of one type (not in the reference's five)
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       const uint32_t k2 = v[m] >> F, q = k2 >> A;
@@ -1712,38 +1711,113 @@ __device__ __forceinline__ void agg_fold(uint32_t (&v)[M], uint64_t obegin, uint
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const bool store = O.cap != 0;
-  uint8_t* o_rule = O.rule + obegin;
-  int32_t* o_aid = O.aid + obegin;
-  int32_t* o_next = O.aid_next + obegin;
-  uint32_t* o_cnt = O.count + obegin;
-  uint32_t* o_c2 = O.count_ge2 + obegin;
+  const uint64_t ob = obegin + (MIRROR ? fo.mirror_off : 0ull);
+  uint8_t* o_rule = O.rule + ob;
+  int32_t* o_aid = O.aid + ob;
+  int32_t* o_next = O.aid_next + ob;
+  uint32_t* o_cnt = O.count + ob;
+  uint32_t* o_c2 = O.count_ge2 + ob;
   if (store)
     for (uint32_t i = l; i < nout; i += 64) {
       const uint32_t k2 = stgk[i], bb = stgb[i];
       const uint32_t q = k2 >> A;
       const int rule = pmode ? (int)(k2 >> 24) : (q == 0 ? r0 : (q == 1 ? r1 : sR.rule_of_type[type][q]));
       const int32_t next = (int32_t)(k2 & L.amask);
+      if (MIRROR && next == aid) { o_rule[i] = 0xFF; continue; }  // the diagonal row is its own mirror
       o_rule[i] = (uint8_t)rule;
-      o_aid[i] = aid;
-      o_next[i] = next;
+      o_aid[i] = MIRROR ? next : aid;
+      o_next[i] = MIRROR ? aid : next;
       o_cnt[i] = bb & 0xFFFFu;
       o_c2[i] = bb >> 16;
     }
   if (store)  // the rest of the task's word range holds no row (marked here, no table-wide fill)
     for (uint32_t i = nout + l; i < olen; i += 64) o_rule[i] = 0xFF;
-  for (int q = 0; q < (nq < 2 ? nq : 2); ++q) {
-    const uint32_t sa = wave_sum(q == 0 ? s0a : s1a), sb = wave_sum(q == 0 ? s0b : s1b);
-    if (l == 0 && sa) {
-      unsigned long long* acc = sacc + (q == 0 ? r0 : r1) * 4;
-      acc[0] += sa & 0xFFFFu; acc[1] += sb & 0xFFFFu; acc[2] += sa >> 16; acc[3] += sb >> 16;
+  if constexpr (!MIRROR) {
+    for (int q = 0; q < (nq < 2 ? nq : 2); ++q) {
+      const uint32_t sa = wave_sum(q == 0 ? s0a : s1a), sb = wave_sum(q == 0 ? s0b : s1b);
+      if (l == 0 && sa) {
+        unsigned long long* acc = sacc + (q == 0 ? r0 : r1) * 4;
+        acc[0] += sa & 0xFFFFu; acc[1] += sb & 0xFFFFu; acc[2] += sa >> 16; acc[3] += sb >> 16;
+      }
+    }
+    {
+      const uint32_t sr = wave_sum(sraw);
+      if (l == 0) { sacc[STAT_RAW] += sr & 0xFFFFu; sacc[STAT_RAW + 1] += sr >> 16; }
     }
   }
-  {
-    const uint32_t sr = wave_sum(sraw);
-    if (l == 0) { sacc[STAT_RAW] += sr & 0xFFFFu; sacc[STAT_RAW + 1] += sr >> 16; }
-  }
-  __builtin_amdgcn_wave_barrier();  // the staging rows are rewritten by the next task
+  __builtin_amdgcn_wave_barrier();  // the staging rows are rewritten by the next pass / task
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  return nout;
+}
+
+// The fold of one sorted task (k_agg_sort, k_agg_lds): v holds its <= 64*M words (W_EMPTY past the
+// end), unsorted; rows go to the slots [obegin, obegin + olen) of the table (the task's own word range),
+// the rest of that range is marked empty. stgk / stgb: this wave's staging rows (64*M + 64 each),
+// sacc: this wave's statistics accumulator, P / fh: the FO kernels' part tables and per-file rows.
+// FO: the FileOpts rule's per-file rows (fh); PM: part mode may be on (fo.parts), else compiled out. In part mode
+// with fo.mirror_off, a second pass writes the explicit mirror rows of the symmetric rule's stored rows.
+template <int M, bool FO, bool PM = FO>
+__device__ __forceinline__ void agg_fold(uint32_t (&v)[M], uint64_t obegin, uint32_t olen, uint32_t rk,
+                                         const RulesDev& sR, const Layout& L, const OutRows& O, const FileOpts& fo,
+                                         const PartLds* P, unsigned long long* fh, uint32_t* stgk, uint32_t* stgb,
+                                         unsigned long long* sacc) {
+  wave_bitonic_sort<M>(v);
+  // neighbours across lanes; lane 0's predecessor and lane 63's successor are sentinels that differ
+  // from the element in every field (so no element needs an index test: words are < W_EMPTY, and the
+  // invalid tail is W_EMPTY, sorted last). All flags below are branch-free selects: the former
+  // short-circuit tests (e < len && (e == 0 || ...)) compiled to exec-mask branches per element.
+  const uint32_t l = lane_id();
+  const uint32_t pl0 = lane_prev(v[M - 1]), nl0 = lane_next(v[0]);
+  const uint32_t pl = l == 0u ? ~v[0] : pl0, nl = l == 63u ? W_EMPTY : nl0;
+  // part mode: parts of the elements and of the cross-lane neighbours (words of one key are in file
+  // order, and the part is non-decreasing in the file for a fixed key, so a part's words stay adjacent)
+  uint32_t pt[PM ? M : 1];
+  uint32_t ppl = 0, pnl = 0;
+  const bool pmode = PM && fo.parts;
+  if constexpr (PM) {
+    if (pmode) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) pt[m] = v[m] != W_EMPTY ? word_part(*P, v[m], rk & L.amask, L) : 0xFFu;
+      ppl = lane_prev(pt[M - 1]);
+      pnl = lane_next(pt[0]);
+    }
+  }
+  const uint32_t nout =
+      fold_pass<M, FO, PM, false>(v, pl, nl, pt, ppl, pnl, pmode, obegin, olen, rk, sR, L, O, fo, fh, stgk, stgb, sacc);
+  if constexpr (PM) {
+    if (pmode && fo.mirror_off) {
+      // the mirrors' parts differ from the rows' only for words of a cut file between the two keys
+      bool differ = false;
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const uint32_t pm = v[m] != W_EMPTY ? word_part_mirror(*P, v[m], rk & L.amask, L) : 0xFFu;
+        differ |= pm != pt[m];
+        pt[m] = pm;
+      }
+      ppl = lane_prev(pt[M - 1]);
+      pnl = lane_next(pt[0]);
+      if (__ballot(differ)) {
+        fold_pass<M, FO, PM, true>(v, pl, nl, pt, ppl, pnl, pmode, obegin, olen, rk, sR, L, O, fo, fh, stgk, stgb,
+                                   sacc);
+      } else {  // the same runs: the staged rows with (aid, aid_next) swapped
+        const int32_t aid = (int32_t)(rk & L.amask);
+        const uint64_t ob = obegin + fo.mirror_off;
+        if (O.cap != 0)
+          for (uint32_t i = l; i < olen; i += 64) {
+            const uint32_t k2 = i < nout ? stgk[i] : 0u;
+            const int32_t next = (int32_t)(k2 & L.amask);
+            if (i >= nout || next == aid) { O.rule[ob + i] = 0xFF; continue; }
+            O.rule[ob + i] = (uint8_t)(k2 >> 24);
+            O.aid[ob + i] = next;
+            O.aid_next[ob + i] = aid;
+            O.count[ob + i] = stgb[i] & 0xFFFFu;
+            O.count_ge2[ob + i] = stgb[i] >> 16;
+          }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      }
+    }
+  }
 }
 
 // One wave per task of <= 64*M words (rows and split buckets): bitonic sort in registers, then
@@ -1798,7 +1872,7 @@ __global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task*
     rkk = row_key[TT.row];
     ndd = 0;
     if constexpr (FOM == 1) {  // the cut words become W_EMPTY (sorted past the task's new end)
-      if (fo.cuts && (int)(rkk >> A) == fo.type) {
+      if ((fo.cuts || fo.qonly) && (int)(rkk >> A) == fo.type) {
         const int32_t ad = (int32_t)(rkk & L.amask);
         uint32_t k = 0;
 #pragma unroll
@@ -1934,7 +2008,7 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
     const uint32_t* W = (T.buf ? w1 : w0) + T.begin;
     const RowInfo ri = row_info(row_key, T.row, L.A);
     const bool fo_row = FO && ri.type == fo.type;
-    const bool fo_cut = fo_row && fo.cuts;
+    const bool fo_cut = fo_row && (fo.cuts || fo.qonly);
     uint32_t ndrop = 0, dbg_loaded = 0, dbg_ins = 0;
     const uint32_t dbound = T.len;
     // optimistic: more keys possible than fit; give up at 3/4 fill and send the task to a split
@@ -2051,6 +2125,11 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
       }
     }
     __syncthreads();
+    // pass 0: the rows; pass 1 (part mode with mirror rows): the explicit mirrors (part_m, aid_next, aid) of a
+    // symmetric rule's stored rows at mirror_off + slot, no statistics (block-uniform)
+    const int npass = (FO && pmode && fo.mirror_off) ? 2 : 1;
+    uint32_t nout = 0;
+    for (int pass = 0; pass < npass; ++pass) {
     unsigned long long* B = lds;            // key2 << 32 | count
     unsigned long long* B2 = lds + cap;     // count_ge2 << 32 | nf2 << 16 | nf1
     for (uint32_t i = tid; i < cap; i += AGG_T) { B[i] = SLOT_EMPTY; B2[i] = 0; }
@@ -2063,7 +2142,9 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
       for (int j = 0; j < 8; ++j) {
         k2[j] = kw[s0 + j] == W_EMPTY ? W_EMPTY : kw[s0 + j] >> L.F;
         if constexpr (FO) {  // part mode: the folded key is (part, aid_next)
-          if (pmode && kw[s0 + j] != W_EMPTY) k2[j] |= word_part(sP[0], kw[s0 + j], (uint32_t)ri.aid, L) << 24;
+          if (pmode && kw[s0 + j] != W_EMPTY)
+            k2[j] |= (pass ? word_part_mirror(sP[0], kw[s0 + j], (uint32_t)ri.aid, L)
+                           : word_part(sP[0], kw[s0 + j], (uint32_t)ri.aid, L)) << 24;
         }
         c8[j] = kc[s0 + j];
       }
@@ -2076,15 +2157,19 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
       }
     }
     __syncthreads();
-    // compact into the task's own word range (outputs <= words)
+    // compact into the task's own word range (outputs <= words); the mirror pass skips the diagonal
     uint32_t mine = 0;
-    for (uint32_t i = tid; i < cap; i += AGG_T) mine += (uint32_t)(B[i] >> 32) != W_EMPTY;
+    for (uint32_t i = tid; i < cap; i += AGG_T) {
+      const uint32_t k2 = (uint32_t)(B[i] >> 32);
+      mine += k2 != W_EMPTY && !(pass && (int32_t)(k2 & L.amask) == ri.aid);
+    }
     const uint32_t incl = wave_incl_scan(mine);
     if ((tid & 63) == 63) wtot[tid >> 6] = incl;
     __syncthreads();
     uint32_t pre = 0;
     for (int k = 0; k < (tid >> 6); ++k) pre += wtot[k];
-    uint64_t p = T.begin + pre + incl - mine;
+    const uint64_t base = T.begin + (pass ? fo.mirror_off : 0ull);
+    uint64_t p = base + pre + incl - mine;
     for (uint32_t i = tid; i < cap; i += AGG_T) {
       const unsigned long long v = B[i];
       const uint32_t k2 = (uint32_t)(v >> 32);
@@ -2093,15 +2178,21 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
       const int rule = pmode ? 0 : R.rule_of_type[ri.type][k2 >> L.A];
       const uint32_t c = (uint32_t)v, c2 = (uint32_t)(v2 >> 32), nf = (uint32_t)v2;
       const int32_t next = (int32_t)(k2 & L.amask);
+      if (pass) {
+        if (next != ri.aid) put_row(O, p++, (int)(k2 >> 24), next, ri.aid, c, c2);
+        continue;
+      }
       const bool mr = rule_sym(R, rule) && next != ri.aid;
       put_row(O, p++, pmode ? (int)(k2 >> 24) : rule, ri.aid, next, c, c2);  // part mode: the part as "rule"
       acc.add(rule, c, nf, mr ? 2u : 1u);
     }
     // the rest of the task's word range holds no row (no table-wide fill: every word position
     // belongs to exactly one leaf task, sort or hash)
-    const uint32_t nout = wtot[0] + wtot[1] + wtot[2] + wtot[3];
-    for (uint32_t i = nout + tid; i < T.len; i += AGG_T) O.rule[T.begin + i] = 0xFF;
+    const uint32_t no = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+    for (uint32_t i = no + tid; i < T.len; i += AGG_T) O.rule[base + i] = 0xFF;
+    if (pass == 0) nout = no;
     __syncthreads();
+    }
     if (fo.prof && tid == 0) {
       fo.prof[2 * ti] = T.len | ((unsigned long long)nout << 32);
       fo.prof[2 * ti + 1] = wall_clock64() - t_start;
@@ -2166,11 +2257,11 @@ __device__ __forceinline__ void push_task_block(const TaskLists& TL, bool valid,
 }
 
 __global__ void k_classify_rows(const uint64_t* __restrict__ row_begin, int64_t R, uint64_t P, int WB,
-                                TaskLists TL, int* err) {
+                                TaskLists TL, int* err, uint64_t row_base) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = r < R;
   uint64_t b = 0, e = 0;
-  if (valid) { b = row_begin[r]; e = r + 1 < R ? row_begin[r + 1] : P; }
+  if (valid) { b = row_begin[r] - row_base; e = r + 1 < R ? row_begin[r + 1] - row_base : P; }
   push_task_block(TL, valid && e > b, b, e - b, (uint32_t)r, 0u, 0u, true, err);
 }
 
@@ -2945,6 +3036,49 @@ __global__ __launch_bounds__(FIN_T) void k_ph_tie_pick(const uint8_t* __restrict
     uint32_t m = tie;
     for (uint32_t x = pre + 1; x < r; ++x) m &= m - 1;  // drop the lower set bits
     astar[q] = (uint32_t)a[i + __ffs((int)m) - 1];
+  }
+}
+// stage 1 on a table whose slots are not in aid order (explicit mirror rows, ottohip_table_count_parts): per
+// stage-1 part q, a histogram over the aids of its tie rows, h[q * n_items + aid]; a thread's runs of one (part, aid)
+// take one atomic each, and a wave whose lanes' last runs share one (part, aid) (a hot aid's rows) takes one for all
+__global__ __launch_bounds__(256) void k_ph_tie_aid_hist(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
+                                                         const uint32_t* __restrict__ c, const uint32_t* __restrict__ c2,
+                                                         int64_t n, int n_parts, int use_ge2, PartCut pc_arg,
+                                                         int64_t n_items, uint32_t* __restrict__ h) {
+  __shared__ PartCut pc;
+  __shared__ int qx[PH_MAXP];
+  if (threadIdx.x == 0) { pc = pc_arg; ph_qindex(pc, n_parts, qx); }
+  __syncthreads();
+  const int l = (int)lane_id();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * SLOTS_T;
+  for (int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63)) * SLOTS_T; i0 < n; i0 += stride) {  // wave-uniform
+    const int64_t i = i0 + (int64_t)l * SLOTS_T;
+    uint4 R;
+    const uint32_t tie = ph_ties16(rule, use_ge2 ? c2 : c, i, n, n_parts, pc, 1u, R);
+    if (!__ballot(tie != 0u)) continue;
+    uint4 A[4];
+    ld_groups(reinterpret_cast<const uint32_t*>(a), i, n, tie, A);
+    uint32_t cp = 0xFFu, ca = 0, cc = 0;
+#pragma unroll
+    for (int s = 0; s < SLOTS_T; ++s) {
+      if (!((tie >> s) & 1u)) continue;
+      const uint32_t p = rule_at(R, s), ai = u4_at(A[s >> 2], s & 3);
+      if (p != cp || ai != ca) {
+        if (cc) atomicAdd(&h[(uint64_t)qx[cp] * n_items + ca], cc);
+        cp = p; ca = ai; cc = 0;
+      }
+      ++cc;
+    }
+    // the last run of every lane: one atomic for the wave when all of them name the same (part, aid)
+    const uint32_t key = cc ? ((cp << 24) | ca) : 0xFFFFFFFFu;
+    const uint64_t act = __ballot(cc != 0u);
+    const uint32_t k0 = (uint32_t)__shfl((int)key, __ffsll((long long)act) - 1);
+    if (!__ballot(cc != 0u && key != k0)) {
+      const uint32_t tot = wave_sum(cc);
+      if (l == __ffsll((long long)act) - 1) atomicAdd(&h[(uint64_t)qx[cp] * n_items + ca], tot);
+    } else if (cc) {
+      atomicAdd(&h[(uint64_t)qx[cp] * n_items + ca], cc);
+    }
   }
 }
 // stage 2: aid_next histogram of the (c*, a*) tie rows of the stage-2 parts, and per part the tie rows with

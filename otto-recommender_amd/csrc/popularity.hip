@@ -1176,7 +1176,7 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
                           (size_t)(h16 ? KMH_AMB : KMS_AMB) * 4;
       // bounds >= 0 (batched steps): skip the rows whose distance bounds keep their label; 1 = the
       // bounds are not valid for these rows (every row scored, bounds rebuilt)
-      const bool bl = bounds >= 0 && km_bounds_on(n);
+      const bool bl = bounds >= 0 && km_bounds_on(n) && ctx->km_range_ok;
       auto sk = KS == 7 ? (NB == 1 ? k_km_assign_split<1, 7> : k_km_assign_split<2, 7>)
                         : (NB == 1 ? k_km_assign_split<1, 8> : k_km_assign_split<2, 8>);
       if (bl)
@@ -1837,7 +1837,8 @@ int ottohip_kmeans_attach_half(ottohip_ctx* ctx, const float* X, int64_t n, int 
   OH_HIP(hipGetLastError());
   unsigned hmax = 0;
   OH_TRY(d2h(&hmax, amax, 1, s));
-  if (hmax > __builtin_bit_cast(unsigned, KMH_MAXABS)) {
+  ctx->km_range_ok = hmax <= __builtin_bit_cast(unsigned, KMH_MAXABS);
+  if (!ctx->km_range_ok) {
     set_error("kmeans_attach_half: max |x| = %g exceeds the f16 range bound %g (or is not finite)",
               (double)__builtin_bit_cast(float, hmax), (double)KMH_MAXABS);
     return OTTOHIP_ELIMIT;
@@ -1894,7 +1895,7 @@ int ottohip_kmeans_lloyd_steps(ottohip_ctx* ctx, const float* X, int64_t n, int 
   OH_TRY(d2h(h, st, 4, s));
   OH_TRY(d2h(c2, ctl, 2, s));
   ctx->km_bX = X; ctx->km_bL = labels; ctx->km_bn = n; ctx->km_bdim = dim; ctx->km_bk = k;
-  ctx->km_bvalid = km_bounds_on(n);
+  ctx->km_bvalid = km_bounds_on(n) && ctx->km_range_ok;
   unsigned long long c, e;
   memcpy(&c, &h[1], 8);
   memcpy(&e, &h[3], 8);

@@ -42,6 +42,8 @@ struct ottohip_ctx : public Ctx {
 };
 
 constexpr int TABLE_MAX_IDS = 256;  // rule ids of a table's rows (part ids: ottohip_covis_count_parts)
+struct KeptEmission;  // a count's emitted words and rows, kept for ottohip_table_count_parts (abi.hip)
+void kept_free(KeptEmission* k);
 struct ottohip_table {
   int device = 0;
   int n_rules = 0;
@@ -53,6 +55,8 @@ struct ottohip_table {
   int sym(int rule) const { return (int)((sym_mask >> rule) & 1u); }
   ottohip_rule_stats stats[TABLE_MAX_IDS];  // per rule (or per part of a ottohip_covis_count_parts table)
   ottohip_ctx* ctx = nullptr;
+  KeptEmission* kept = nullptr;  // ottohip_file_opts.keep_words: the count's words, for ottohip_table_count_parts
+  bool aid_ordered = true;       // a rule's (part's) slots are in aid order (false: explicit mirror rows)
 };
 
 static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }

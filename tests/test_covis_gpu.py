@@ -398,6 +398,51 @@ def test_concat_files_w_stats_part_branch(gpu, kw):
         np.testing.assert_array_equal(c, rc, err_msg=n)
 
 
+@pytest.mark.parametrize("kw", [
+    dict(max_rows_groupby=300_000, optim_rows=250_000, max_pairs=200_000, click_filter_rows=1_000_000),
+    dict(max_rows_groupby=50_000, optim_rows=20_000, max_pairs=10**9, click_filter_rows=10**9),
+])
+def test_part_branch_from_kept_words(gpu, kw):
+    """Branch (2) re-folded from the main build's own words (ottohip_file_opts.keep_words +
+    ottohip_table_count_parts): one 5-rule count that histograms click_to_click's rows per file and keeps its
+    words; each rule's part-tagged table comes from its row type's range of the kept words (the type's other rule
+    dropped; cart_to_cart's range starts inside the words), a symmetric rule's mirrors written as explicit rows
+    with their own parts. Per part equal to the part-tagged recount (ottohip_covis_count_parts), and A6 equal to
+    the restatement (model/count_co_events.py:135-166)."""
+    from otto_recommender_amd import covis as gc
+    ev = synth.generate(30_000, first_session=2024)
+    fb = synth.file_session_bounds(ev.n_sessions, per_file=3_000)
+    per_file = oracle.count_co_events_files(ev.session_offsets, ev.aid, ev.ts, ev.type, fb)
+    dev = gc.DeviceEvents.from_host(ev, fb)
+    tab = gc.count_co_events_fused(dev, per_file_rule="click_to_click", keep_words=True)
+    assert tab.kept_words and tab.per_file_rule == "click_to_click"
+    nf = len(fb) - 1
+    for n in ("click_to_click", "click_to_cart_or_buy", "cart_to_cart", "cart_to_buy", "buy_to_buy"):
+        ra, rb, rc = oracle.concat_files_w_stats(n, [p[n] for p in per_file], **kw)
+        a, b, c = (x.cpu().numpy() for x in gc.concat_files_w_stats_fused(dev, n, table=tab, **kw))
+        np.testing.assert_array_equal(a, ra, err_msg=n)
+        np.testing.assert_array_equal(b, rb, err_msg=n)
+        np.testing.assert_array_equal(c, rc, err_msg=n)
+        # the part tables themselves, against the recount, with a cut inside files 2 and 6
+        R = [len(p[n][0]) for p in per_file]
+        first = [0, 0, 0, 1, 1, 1, 1, 2, 2, 2][:nf]
+        keys = {}
+        for f, r in ((2, R[2] // 3), (6, R[6] // 2)):
+            if R[f] == 0:
+                continue
+            a_, b_, _ = per_file[f][n]
+            keys[f] = (int(a_[r]) << 32) | int(b_[r])
+        cuts = sorted(keys.items())
+        got = gc.table_count_parts(tab, n, first, cuts, 3)
+        ref = gc.count_co_events_parts(dev, n, first, cuts, 3)
+        for p_ in range(3):
+            for x, y in zip(got.to_numpy(p_), ref.to_numpy(p_)):
+                np.testing.assert_array_equal(x, y, err_msg=f"{n} part {p_}")
+            assert got.stats(p_) == ref.stats(p_), (n, p_)
+        got.free(); ref.free()
+    tab.free()
+
+
 def test_file_cuts_per_file_rows_and_key_slices(gpu):
     """ottohip_file_opts: per-file rows (and rows with count >= 2) of one rule equal every file's
     own table; a lo / hi key cut on a file keeps exactly the rows of its (aid, aid_next)-ordered
