@@ -72,15 +72,27 @@ def cpu_baseline(seed: int = 0, pandas_files: int = 10) -> dict:
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16, /opt/skills/guides/MI355X_MICROARCH.md
 
 
-def bench_a6(dev, tab, ctx, reps: int = 3) -> dict:
-    """A6 (model/count_co_events.py:103-181) on the counted 220 M-event table, per rule: the per-file
-    count >= 2 filter, the part-wise branch (2) where N > MAX_ROWS_POLARS_GROUPBY (its parts are
-    recounted from the resident events), MIN_COUNT_TO_SAVE, count-desc order and head. Timed after
-    the co-visitation steps and reported beside the line (the reference's ETAs cover count + merge,
-    :202, :210); not part of `value`. One untimed warmup pass, then `reps` timed passes (min reported,
-    every run listed); the last run records per-stage times of the part-wise rule."""
+def bench_a6(dev, ctx, reps: int = 3) -> dict:
+    """Count + merge, the reference's deliverable (ETAs :202, :210): the count that A6 (model/count_co_events.py:
+    103-181) needs -- all five rules, click_to_click's rows histogrammed per file (branch (2)'s row-slice plan) and
+    the pair words kept (its part-tagged table re-folded from them, ottohip_table_count_parts) -- timed `reps`
+    times (min: count_ms), then per rule A6 on that table: the per-file count >= 2 filter, branch (2) where
+    N > MAX_ROWS_POLARS_GROUPBY, MIN_COUNT_TO_SAVE, count-desc order and head. Reported beside the line, not
+    part of `value`. A6: one untimed warmup pass, then `reps` timed passes (min reported, every run listed);
+    the last run records per-stage times of the part-wise rule."""
     import torch
     from otto_recommender_amd import covis as gc, config as cfg
+    cts = []
+    tab = None
+    for _ in range(reps + 1):  # the first: untimed warmup (allocations)
+        if tab is not None:
+            tab.free()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tab = gc.count_co_events_fused(dev, ctx=ctx, per_file_rule="click_to_click", keep_words=True)
+        torch.cuda.synchronize()
+        cts.append((time.perf_counter() - t0) * 1e3)
+    count_ms = min(cts[1:])
     per = {}
     totals = []
     # one untimed warmup pass first (its first-use allocations: the part-wise count's word buffers and
@@ -112,8 +124,12 @@ def bench_a6(dev, tab, ctx, reps: int = 3) -> dict:
         totals.append((time.perf_counter() - t0) * 1e3)
     for d in per.values():
         d["ms"] = min(d["ms_runs"])
+    tab.free()
     return {"per_rule": per, "total_ms": round(min(totals), 2), "total_ms_runs": [round(x, 2) for x in totals],
-            "max_over_min": round(max(totals) / min(totals), 3), "reps": reps, "warmup_ms": round(warm_ms, 2)}
+            "max_over_min": round(max(totals) / min(totals), 3), "reps": reps, "warmup_ms": round(warm_ms, 2),
+            "count_ms": round(count_ms, 2), "count_ms_runs": [round(x, 2) for x in cts[1:]],
+            "count_note": "the count A6 uses: the line's build plus click_to_click's per-file row histogram and "
+                          "the kept pair words"}
 
 
 def bench_ingest(ev, fb, dev, ctx, reps: int = 3) -> dict:
@@ -362,14 +378,11 @@ def main():
     ctx = _lib.context()
     torch.cuda.synchronize()
 
-    # the build histograms click_to_click's rows per file (A6 branch (2) plans its row slices from them,
-    # model/count_co_events.py:136-153, without a count of its own); OTTOHIP_BENCH_PER_FILE=none: plain build
-    pfr = os.environ.get("OTTOHIP_BENCH_PER_FILE", "click_to_click")
+    # the line's build: the five count tables (configs[1]); A/B switches: OTTOHIP_BENCH_PER_FILE=<rule> adds a
+    # rule's per-file row histogram, OTTOHIP_BENCH_KEEP=1 keeps the pair words (what A6's count adds, bench_a6)
+    pfr = os.environ.get("OTTOHIP_BENCH_PER_FILE", "none")
     pfr = None if pfr in ("", "none", "0") else pfr
-
-    # the build also keeps its pair words, so A6's branch-(2) part table is re-folded from them, not counted again
-    # (OTTOHIP_BENCH_KEEP=0: not kept)
-    keep = os.environ.get("OTTOHIP_BENCH_KEEP", "1") != "0"
+    keep = os.environ.get("OTTOHIP_BENCH_KEEP", "0") == "1"
 
     def step():
         if world > 1:  # local count -> pack by owner -> all-to-all-v (RCCL) -> merge-sum
@@ -402,13 +415,13 @@ def main():
     phases = ctx.timings()
     ctx.set_timing(False)
     a6 = None
+    tab.free()
     if world == 1 and not args.no_a6:
-        ctx.trim()  # the build's word buffers are not needed by A6
+        ctx.trim()  # the build's word buffers
         try:  # reported beside the line; it must not cost the main line
-            a6 = bench_a6(dev, tab, ctx)
+            a6 = bench_a6(dev, ctx)
         except Exception as exc:  # noqa: BLE001
             a6 = {"error": repr(exc)}
-    tab.free()
     ingest = None
     if world == 1 and not args.no_ingest:
         ctx.trim()
@@ -491,7 +504,7 @@ def main():
     }
     if a6 is not None:
         if "total_ms" in a6:
-            cpm = t_step + a6["total_ms"] / 1e3
+            cpm = (a6["count_ms"] + a6["total_ms"]) / 1e3
             a6["count_plus_merge_ms"] = round(cpm * 1e3, 2)
             # the reference's deliverable is count + merge (ETAs :202, :210): pairs counted per second of both
             a6["count_plus_merge_pairs_per_s"] = pairs / cpm

@@ -673,8 +673,11 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     const bool hf = hash_first && nlist[N_SORT] != 0;
     auto launch_hash = [&]() {
       const unsigned hg = (unsigned)std::min<uint64_t>(nlist[N_SORT], (uint64_t)agg_grid);
-      if (FOon)
-        k_agg_hash<true><<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], wcur0, w1, row_key, R, Lt, n_rules, O,
+      if (FOhist)
+        k_agg_hash<2><<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], wcur0, w1, row_key, R, Lt, n_rules, O,
+                                           TL.split, lcount + N_SORT + 1, fo);
+      else if (FOon)
+        k_agg_hash<1><<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], wcur0, w1, row_key, R, Lt, n_rules, O,
                                               TL.split, lcount + N_SORT + 1, fo);
       else
         k_agg_hash<<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], wcur0, w1, row_key, R, Lt, n_rules, O, TL.split,

@@ -134,9 +134,6 @@ struct Ctx {
   bool km_bvalid = false;
   // half-precision rows of an attached KMeans matrix (ottohip_kmeans_attach_half): the E-step of
   // ottohip_kmeans_lloyd_steps on that X reads them (and the rows' exact squared norms) instead of the f32 rows
-  // the last ottohip_kmeans_attach_half found every |x| within the f16 range bound; beyond it the distance bounds
-  // are off too (two identical fits at |x| ~ 1e5 diverged with them on: tools/dbg/km_range2.py)
-  bool km_range_ok = true;
   const void* km_hX = nullptr;
   int64_t km_hn = -1;
   int km_hdim = 0;

@@ -1623,15 +1623,16 @@ __device__ __forceinline__ uint32_t fold_pass(const uint32_t (&v)[M], uint32_t p
     kst |= (valid & kbs) << m;
     kend |= (valid & kbe) << m;
   }
-  if constexpr (FO && !MIRROR) {  // one per-file row per w-run end of the rule; a singleton w-run has count 1
+  // per-file rows of the FileOpts rule: w-run ends of the rule and singleton w-runs as bit masks over the lane's
+  // elements (the histogram atomics run after the rows are out, when the fold's arrays are dead)
+  uint32_t hend = 0, hsing = 0;
+  if constexpr (FO && !MIRROR) {
     if (fo.hist && (int)(rk >> A) == fo.type) {
 #pragma unroll
-      for (int m = 0; m < M; ++m)
-        if ((c[m] & 1u) && (v[m] >> (A + F)) == fo.q) {  // a symmetric rule's stored row (a, b), a < b, is
-          const unsigned long long mult =                // also the row (b, a) of the file's table
-              (fo.sym && ((v[m] >> F) & L.amask) != (rk & L.amask)) ? 2ull : 1ull;
-          atomicAdd(&fh[v[m] & ((1u << F) - 1u)], mult * ((c[m] >> 11) ? 1ull : (1ull | (1ull << 32))));
-        }
+      for (int m = 0; m < M; ++m) {
+        hend |= ((c[m] & 1u) && (v[m] >> (A + F)) == fo.q ? 1u : 0u) << m;
+        hsing |= ((c[m] >> 11) & 1u) << m;
+      }
     }
   }
   wave_scan_elems<M, false>(b);
@@ -1732,6 +1733,14 @@ __device__ __forceinline__ uint32_t fold_pass(const uint32_t (&v)[M], uint32_t p
     }
   if (store)  // the rest of the task's word range holds no row (marked here, no table-wide fill)
     for (uint32_t i = nout + l; i < olen; i += 64) o_rule[i] = 0xFF;
+  if constexpr (FO && !MIRROR) {  // one per-file row per w-run end of the rule; a singleton w-run has count 1
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+      if ((hend >> m) & 1u) {  // a symmetric rule's stored row (a, b), a < b, is also the row (b, a) of the file's table
+        const unsigned long long mult = (fo.sym && ((v[m] >> F) & L.amask) != (rk & L.amask)) ? 2ull : 1ull;
+        atomicAdd(&fh[v[m] & ((1u << F) - 1u)], mult * (((hsing >> m) & 1u) ? 1ull : (1ull | (1ull << 32))));
+      }
+  }
   if constexpr (!MIRROR) {
     for (int q = 0; q < (nq < 2 ? nq : 2); ++q) {
       const uint32_t sa = wave_sum(q == 0 ? s0a : s1a), sb = wave_sum(q == 0 ? s0b : s1b);
@@ -1832,8 +1841,10 @@ __device__ __forceinline__ void agg_fold(uint32_t (&v)[M], uint64_t obegin, uint
 // tables in LDS); 2 per-file rows only (the histogram of the call's fo.nf files in dynamic LDS, fo.nf * 8 bytes:
 // the main build's statistics cost no occupancy)
 extern __shared__ unsigned long long agg_sort_fh_dyn[];
+// occupancy: 4 waves per SIMD (<= 128 VGPRs) for the 512- and 1024-word classes, except the part-mode 1024-word
+// class (2; its mirror pass would spill heavily at 4)
 template <int M, int FOM = 0>
-__global__ __launch_bounds__(256, (M >= 16 ? 4 : 1)) void k_agg_sort(const Task* __restrict__ tasks, int64_t n_tasks,
+__global__ __launch_bounds__(256, (M >= 16 ? (FOM == 1 ? 2 : 4) : (M == 8 ? 4 : 1))) void k_agg_sort(const Task* __restrict__ tasks, int64_t n_tasks,
                                                   const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
                                                   const uint32_t* __restrict__ row_key, RulesDev R, Layout L,
                                                   int n_rules, OutRows O, FileOpts fo) {
@@ -1978,8 +1989,9 @@ struct TaskLists {
   uint64_t cap;           // capacity of every list
 };
 
-template <bool FO = false>
-__global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tasks, int64_t n_tasks,
+// FOM as k_agg_sort: 0 no FileOpts, 1 cuts / part mode (and its mirror pass), 2 per-file rows only
+template <int FOM = 0>
+__global__ __launch_bounds__(AGG_T, 2) void k_agg_hash(const Task* __restrict__ tasks, int64_t n_tasks,
                                                     const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
                                                     const uint32_t* __restrict__ row_key, RulesDev R, Layout L,
                                                     int n_rules, OutRows O, Task* __restrict__ overflow,
@@ -1987,8 +1999,9 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
   __shared__ unsigned long long lds[2 * HCAP];  // 64 KiB: phase A [0, cap), phase B [0, 2cap)
   __shared__ uint32_t wtot[AGG_T / 64];
   __shared__ uint32_t nocc;
+  constexpr bool FO = FOM != 0, PM = FOM == 1;
   __shared__ unsigned long long fh[FO ? FO_MAXF : 1];  // per-file rows of the FileOpts rule
-  __shared__ std::conditional_t<FO, PartLds, char> sP[1];  // part-mode tables (FO kernels only)
+  __shared__ std::conditional_t<PM, PartLds, char> sP[1];  // part-mode tables (FOM 1 only)
   const int tid = threadIdx.x;
   // the hash leaves share CUs with the register sorts of the same level (aux stream): a raised wave
   // priority lets their LDS-latency-bound loop issue ahead of the VALU-bound sorts
@@ -1998,10 +2011,10 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
   acc.zero();
   if constexpr (FO) {
     for (uint32_t i = tid; i < fo.nf; i += AGG_T) fh[i] = 0;
-    part_lds_load(fo, sP[0]);
+    if constexpr (PM) part_lds_load(fo, sP[0]);
     __syncthreads();
   }
-  const bool pmode = FO && fo.parts;
+  const bool pmode = PM && fo.parts;
   for (int64_t ti = blockIdx.x; ti < n_tasks; ti += gridDim.x) {
     const Task T = tasks[ti];
     const uint64_t t_start = fo.prof ? wall_clock64() : 0;
@@ -2040,7 +2053,7 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
 #pragma unroll
       for (int j = 0; j < PF; ++j) {
         if (FO && fo.dbg && wbuf[j] != W_EMPTY) ++dbg_loaded;
-        if constexpr (FO) {  // branch-free: the cut word becomes W_EMPTY (the if-form lost ~15% of the
+        if constexpr (PM) {  // branch-free: the cut word becomes W_EMPTY (the if-form lost ~15% of the
                              // W_EMPTY writes under hipcc 7.2 -O3: counted and cut at once, found by the
                              // reduce's conservation check, tests/test_covis_gpu.py::test_file_cuts_hot_rows)
           const bool dr = fo_cut && fo_drop(fo, wbuf[j], ri.aid, L);
@@ -2127,8 +2140,9 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
     __syncthreads();
     // pass 0: the rows; pass 1 (part mode with mirror rows): the explicit mirrors (part_m, aid_next, aid) of a
     // symmetric rule's stored rows at mirror_off + slot, no statistics (block-uniform)
-    const int npass = (FO && pmode && fo.mirror_off) ? 2 : 1;
+    const int npass = (PM && pmode && fo.mirror_off) ? 2 : 1;
     uint32_t nout = 0;
+#pragma unroll 1
     for (int pass = 0; pass < npass; ++pass) {
     unsigned long long* B = lds;            // key2 << 32 | count
     unsigned long long* B2 = lds + cap;     // count_ge2 << 32 | nf2 << 16 | nf1
@@ -2141,10 +2155,14 @@ __global__ __launch_bounds__(AGG_T) void k_agg_hash(const Task* __restrict__ tas
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         k2[j] = kw[s0 + j] == W_EMPTY ? W_EMPTY : kw[s0 + j] >> L.F;
-        if constexpr (FO) {  // part mode: the folded key is (part, aid_next)
-          if (pmode && kw[s0 + j] != W_EMPTY)
-            k2[j] |= (pass ? word_part_mirror(sP[0], kw[s0 + j], (uint32_t)ri.aid, L)
-                           : word_part(sP[0], kw[s0 + j], (uint32_t)ri.aid, L)) << 24;
+        if constexpr (PM) {  // part mode: the folded key is (part, aid_next) (pass 1: the mirror's part)
+          if (pmode && kw[s0 + j] != W_EMPTY) {
+            const uint32_t w = kw[s0 + j], f = w & ((1u << L.F) - 1u), ci = sP[0].cut_of[f];
+            const uint64_t ka = (uint64_t)(uint32_t)ri.aid, kb = (uint64_t)((w >> L.F) & L.amask);
+            const uint64_t key = pass ? ((kb << 32) | ka) : ((ka << 32) | kb);
+            k2[j] |= ((uint32_t)sP[0].part_of[f] +
+                      ((ci != FO_NOCUT && key >= sP[0].cut_key[ci & (FO_MAXCUT - 1)]) ? 1u : 0u)) << 24;
+          }
         }
         c8[j] = kc[s0 + j];
       }

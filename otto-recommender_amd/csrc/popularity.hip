@@ -1176,7 +1176,7 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
                           (size_t)(h16 ? KMH_AMB : KMS_AMB) * 4;
       // bounds >= 0 (batched steps): skip the rows whose distance bounds keep their label; 1 = the
       // bounds are not valid for these rows (every row scored, bounds rebuilt)
-      const bool bl = bounds >= 0 && km_bounds_on(n) && ctx->km_range_ok;
+      const bool bl = bounds >= 0 && km_bounds_on(n);
       auto sk = KS == 7 ? (NB == 1 ? k_km_assign_split<1, 7> : k_km_assign_split<2, 7>)
                         : (NB == 1 ? k_km_assign_split<1, 8> : k_km_assign_split<2, 8>);
       if (bl)
@@ -1263,9 +1263,11 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
 
 // squared distance of every row to the centroid of its label (inertia of a given labelling,
 // and the per-row distances sklearn's empty-cluster relocation ranks)
+// inertia: one f64 atomic per wave (order-dependent last bits); wparts: the per-wave partials instead (k_sum_fixed)
 __global__ __launch_bounds__(256) void k_km_labelled(const float* __restrict__ X, int64_t n, int dim,
                                                      const float* __restrict__ C, const int32_t* __restrict__ label,
-                                                     float* __restrict__ dist, double* __restrict__ inertia) {
+                                                     float* __restrict__ dist, double* __restrict__ inertia,
+                                                     double* __restrict__ wparts = nullptr) {
   // half a wave per row: lanes over the row's dims (coalesced), sum by a 32-lane butterfly
   double part = 0.0;
   const int hl = threadIdx.x & 31;
@@ -1291,6 +1293,21 @@ __global__ __launch_bounds__(256) void k_km_labelled(const float* __restrict__ X
     part += __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
   }
   if ((threadIdx.x & 63) == 0 && inertia) atomicAdd(inertia, part);
+  if ((threadIdx.x & 63) == 0 && wparts) wparts[((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6] = part;
+}
+// sum of the per-wave partials in a fixed order (one block): the same rows and centres give the same bits, so
+// two n_init runs that reach one partition (their labels a permutation) tie exactly, and the first is kept
+__global__ __launch_bounds__(1024) void k_sum_fixed(const double* __restrict__ parts, int64_t n, double* __restrict__ out) {
+  __shared__ double sh[1024];
+  double a = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 1024) a += parts[i];
+  sh[threadIdx.x] = a;
+  __syncthreads();
+  for (int w = 512; w >= 1; w >>= 1) {
+    if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = sh[0];
 }
 
 // argmax of dist over rows not yet taken: key = ordered(dist) << 32 | ~row (ties: lowest row)
@@ -1837,8 +1854,7 @@ int ottohip_kmeans_attach_half(ottohip_ctx* ctx, const float* X, int64_t n, int 
   OH_HIP(hipGetLastError());
   unsigned hmax = 0;
   OH_TRY(d2h(&hmax, amax, 1, s));
-  ctx->km_range_ok = hmax <= __builtin_bit_cast(unsigned, KMH_MAXABS);
-  if (!ctx->km_range_ok) {
+  if (hmax > __builtin_bit_cast(unsigned, KMH_MAXABS)) {
     set_error("kmeans_attach_half: max |x| = %g exceeds the f16 range bound %g (or is not finite)",
               (double)__builtin_bit_cast(float, hmax), (double)KMH_MAXABS);
     return OTTOHIP_ELIMIT;
@@ -1895,7 +1911,7 @@ int ottohip_kmeans_lloyd_steps(ottohip_ctx* ctx, const float* X, int64_t n, int 
   OH_TRY(d2h(h, st, 4, s));
   OH_TRY(d2h(c2, ctl, 2, s));
   ctx->km_bX = X; ctx->km_bL = labels; ctx->km_bn = n; ctx->km_bdim = dim; ctx->km_bk = k;
-  ctx->km_bvalid = km_bounds_on(n) && ctx->km_range_ok;
+  ctx->km_bvalid = km_bounds_on(n);
   unsigned long long c, e;
   memcpy(&c, &h[1], 8);
   memcpy(&e, &h[3], 8);
@@ -2096,12 +2112,15 @@ int ottohip_kmeans_inertia(ottohip_ctx* ctx, const float* X, int64_t n, int dim,
     set_error("kmeans_inertia: bad arguments"); return OTTOHIP_EINVAL;
   }
   hipStream_t s = S(stream);
-  double* inr;
+  double *inr, *wp;
   OH_TRY(ctx->ws.get("km_inertia", 1, &inr));
   OH_HIP(hipMemsetAsync(inr, 0, 8, s));
-  if (n > 0)
-    k_km_labelled<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), (int64_t)ctx->n_cu * 8), 256, 0, s>>>(
-        X, n, dim, centroids, labels, nullptr, inr);
+  if (n > 0) {  // deterministic: per-wave partials summed in a fixed order (sklearn keeps the first of equal runs)
+    const unsigned g = (unsigned)std::min<int64_t>(ceil_div(n, 256), (int64_t)ctx->n_cu * 8);
+    OH_TRY(ctx->ws.get("km_inertia_parts", (size_t)g * 4, &wp));
+    k_km_labelled<<<g, 256, 0, s>>>(X, n, dim, centroids, labels, nullptr, nullptr, wp);
+    k_sum_fixed<<<1, 1024, 0, s>>>(wp, (int64_t)g * 4, inr);
+  }
   OH_HIP(hipGetLastError());
   OH_TRY(d2h(inertia, inr, 1, s));
   return 0;

@@ -159,18 +159,13 @@ class KMeans:
         seed_stream = _permutation_heads(self.random_state, n_all, k, self.n_init)
         # one GPU: the E-steps read f16 copies of the centred rows (exact f32 scoring of the near ties keeps the
         # f32 labels); every fit attaches its own Xc, so a reused allocation never meets a stale copy
-        half = group is None and dim % 4 == 0
+        half = group is None and dim % 4 == 0 and os.environ.get("OTTOHIP_KM_H16", "1") != "0"
         if half:
-            # refused (ELIMIT) when some |x| is outside the f16 range bound: the E-steps then score the f32 rows, and
-            # the library keeps its distance bounds off for these rows too (their f32 error model is not trusted
-            # there). OTTOHIP_KM_H16=0: the range check only, the f16 copy detached at once.
+            # refused (ELIMIT) when some |x| is outside the f16 range bound: the E-steps then score the f32 rows
             rc = lib.ottohip_kmeans_attach_half(ctx.h, _lib.ptr(Xc), n, dim, sh)
             half = rc == 0
             if rc not in (0, _lib.OTTOHIP_ELIMIT):
                 _lib.check(rc)
-            if half and os.environ.get("OTTOHIP_KM_H16", "1") == "0":
-                lib.ottohip_kmeans_detach_half(ctx.h)
-                half = False
         try:
             return self._fit_runs(X, Xc, n, dim, k, group, grows, tol_abs, seed_stream, mean_d, ctx, sh, dev)
         finally:
