@@ -74,9 +74,9 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16, /opt/skills/guides/MI355X_MICROARC
 
 def bench_a6(dev, ctx, reps: int = 3) -> dict:
     """Count + merge, the reference's deliverable (ETAs :202, :210): the count that A6 (model/count_co_events.py:
-    103-181) needs -- all five rules, click_to_click's rows histogrammed per file (branch (2)'s row-slice plan) and
-    the pair words kept (its part-tagged table re-folded from them, ottohip_table_count_parts) -- timed `reps`
-    times (min: count_ms), then per rule A6 on that table: the per-file count >= 2 filter, branch (2) where
+    103-181) needs -- all five rules with click_to_click's rows histogrammed per file (branch (2)'s row-slice plan;
+    OTTOHIP_A6_REFOLD=1 also keeps the pair words, covis.a6_refold) -- timed `reps` times (min: count_ms), then per
+    rule A6 on that table: the per-file count >= 2 filter, branch (2) where
     N > MAX_ROWS_POLARS_GROUPBY, MIN_COUNT_TO_SAVE, count-desc order and head. Reported beside the line, not
     part of `value`. A6: one untimed warmup pass, then `reps` timed passes (min reported, every run listed);
     the last run records per-stage times of the part-wise rule."""
@@ -89,7 +89,7 @@ def bench_a6(dev, ctx, reps: int = 3) -> dict:
             tab.free()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        tab = gc.count_co_events_fused(dev, ctx=ctx, per_file_rule="click_to_click", keep_words=True)
+        tab = gc.count_co_events_fused(dev, ctx=ctx, per_file_rule="click_to_click", keep_words=gc.a6_refold())
         torch.cuda.synchronize()
         cts.append((time.perf_counter() - t0) * 1e3)
     count_ms = min(cts[1:])
@@ -128,8 +128,7 @@ def bench_a6(dev, ctx, reps: int = 3) -> dict:
     return {"per_rule": per, "total_ms": round(min(totals), 2), "total_ms_runs": [round(x, 2) for x in totals],
             "max_over_min": round(max(totals) / min(totals), 3), "reps": reps, "warmup_ms": round(warm_ms, 2),
             "count_ms": round(count_ms, 2), "count_ms_runs": [round(x, 2) for x in cts[1:]],
-            "count_note": "the count A6 uses: the line's build plus click_to_click's per-file row histogram and "
-                          "the kept pair words"}
+            "count_note": "the count A6 uses: the line's build plus click_to_click's per-file row histogram"}
 
 
 def bench_ingest(ev, fb, dev, ctx, reps: int = 3) -> dict:

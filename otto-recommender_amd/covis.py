@@ -497,6 +497,14 @@ def boundary_keys(events: DeviceEvents, name: str, plan, file_rows, use_ge2: boo
     return out
 
 
+def a6_refold() -> bool:
+    """OTTOHIP_A6_REFOLD=1: branch (2)'s part table re-folded from the count's kept words (ottohip_table_count_parts)
+    instead of a part-tagged recount. Exact (tests/test_covis_gpu.py::test_part_branch_from_kept_words) but measured
+    slower at 220 M events (A6 193.6 vs 141.8 ms, gpurun_out/r5e): a symmetric rule's mirrors become explicit rows
+    outside aid order, so the part heads' tie cut and the merge of the heads lose their ordered fast paths."""
+    return os.environ.get("OTTOHIP_A6_REFOLD", "0") == "1"
+
+
 def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTable | None = None,
                                n_items: int = config.N_ITEMS_OTTO, max_rows_groupby: int = config.MAX_ROWS_POLARS_GROUPBY,
                                optim_rows: int = config.OPTIM_ROWS_POLARS_GROUPBY,
@@ -530,7 +538,7 @@ def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTabl
             t_last[0] = t
     own = table is None
     tab = table if table is not None else count_co_events_fused(events, [name], n_items=n_items, ctx=ctx,
-                                                                per_file_rule=name, keep_words=True)
+                                                                per_file_rule=name, keep_words=a6_refold())
     st = tab.stats(name)
     use_ge2 = "click_to" in name and st["file_rows"] > click_filter_rows
     N = st["file_rows_ge2"] if use_ge2 else st["file_rows"]
@@ -564,7 +572,8 @@ def concat_files_w_stats_fused(events: DeviceEvents, name: str, table: CovisTabl
     fits = one_count and n_items <= (1 << 24) and nf <= max_files_per_call([name], n_items)
     assign = part_assignment(plan, R, keys) if fits else None
     if assign is not None:  # every part from ONE count (its rows carry their part)
-        if getattr(tab, "kept_words", False) and tab.h:  # re-folded from the words of the table's own count
+        refold = a6_refold()
+        if refold and getattr(tab, "kept_words", False) and tab.h:  # re-folded from the words of the table's own count
             t = table_count_parts(tab, name, assign[0], assign[1], len(plan))
         else:
             t = count_co_events_parts(events, name, assign[0], assign[1], len(plan), n_items, ctx=ctx)

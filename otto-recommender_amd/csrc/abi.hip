@@ -524,6 +524,7 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   const bool FOon = fopts != nullptr || fo_parts != nullptr;
   // per-file rows only (no key cuts, no parts): the register sorts keep their occupancy (k_agg_sort<M, 2>)
   const bool FOhist = FOon && !fo.cuts && !fo.parts && fo.hist != nullptr;
+  const bool FOmir = FOon && fo.parts && fo.mirror_off != 0;  // part mode with explicit mirror rows
   // symmetric rules store one row per unordered pair; the readers produce the mirrors (T->sym_mask)
   // part mode with explicit mirror rows: slots [P, 2P) hold the mirror of the row at slot - P
   const uint64_t n_slots = (fo_parts && fo_parts->mirror_off) ? 2 * P : P;
@@ -676,6 +677,9 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
       if (FOhist)
         k_agg_hash<2><<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], wcur0, w1, row_key, R, Lt, n_rules, O,
                                            TL.split, lcount + N_SORT + 1, fo);
+      else if (FOmir)
+        k_agg_hash<3><<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], wcur0, w1, row_key, R, Lt, n_rules, O,
+                                           TL.split, lcount + N_SORT + 1, fo);
       else if (FOon)
         k_agg_hash<1><<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], wcur0, w1, row_key, R, Lt, n_rules, O,
                                               TL.split, lcount + N_SORT + 1, fo);
@@ -690,6 +694,9 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
       if (FOhist)                                                                                            \
         k_agg_sort<M, 2><<<g_, 256, (size_t)fo.nf * 8, ss>>>(TL.sort[c], (int64_t)nlist[c], wcur0, w1, row_key, R,  \
                                                             Lt, n_rules, Osort, fo);                         \
+      else if (FOmir)                                                                                        \
+        k_agg_sort<M, 3><<<g_, 256, 0, ss>>>(TL.sort[c], (int64_t)nlist[c], wcur0, w1, row_key, R, Lt, n_rules, \
+                                             Osort, fo);                                                     \
       else if (FOon)                                                                                         \
         k_agg_sort<M, 1><<<g_, 256, 0, ss>>>(TL.sort[c], (int64_t)nlist[c], wcur0, w1, row_key, R, Lt, n_rules, \
                                              Osort, fo);                                                     \

@@ -1623,16 +1623,15 @@ __device__ __forceinline__ uint32_t fold_pass(const uint32_t (&v)[M], uint32_t p
     kst |= (valid & kbs) << m;
     kend |= (valid & kbe) << m;
   }
-  // per-file rows of the FileOpts rule: w-run ends of the rule and singleton w-runs as bit masks over the lane's
-  // elements (the histogram atomics run after the rows are out, when the fold's arrays are dead)
-  uint32_t hend = 0, hsing = 0;
-  if constexpr (FO && !MIRROR) {
+  if constexpr (FO && !MIRROR) {  // one per-file row per w-run end of the rule; a singleton w-run has count 1
     if (fo.hist && (int)(rk >> A) == fo.type) {
 #pragma unroll
-      for (int m = 0; m < M; ++m) {
-        hend |= ((c[m] & 1u) && (v[m] >> (A + F)) == fo.q ? 1u : 0u) << m;
-        hsing |= ((c[m] >> 11) & 1u) << m;
-      }
+      for (int m = 0; m < M; ++m)
+        if ((c[m] & 1u) && (v[m] >> (A + F)) == fo.q) {  // a symmetric rule's stored row (a, b), a < b, is
+          const unsigned long long mult =                // also the row (b, a) of the file's table
+              (fo.sym && ((v[m] >> F) & L.amask) != (rk & L.amask)) ? 2ull : 1ull;
+          atomicAdd(&fh[v[m] & ((1u << F) - 1u)], mult * ((c[m] >> 11) ? 1ull : (1ull | (1ull << 32))));
+        }
     }
   }
   wave_scan_elems<M, false>(b);
@@ -1733,14 +1732,6 @@ __device__ __forceinline__ uint32_t fold_pass(const uint32_t (&v)[M], uint32_t p
     }
   if (store)  // the rest of the task's word range holds no row (marked here, no table-wide fill)
     for (uint32_t i = nout + l; i < olen; i += 64) o_rule[i] = 0xFF;
-  if constexpr (FO && !MIRROR) {  // one per-file row per w-run end of the rule; a singleton w-run has count 1
-#pragma unroll
-    for (int m = 0; m < M; ++m)
-      if ((hend >> m) & 1u) {  // a symmetric rule's stored row (a, b), a < b, is also the row (b, a) of the file's table
-        const unsigned long long mult = (fo.sym && ((v[m] >> F) & L.amask) != (rk & L.amask)) ? 2ull : 1ull;
-        atomicAdd(&fh[v[m] & ((1u << F) - 1u)], mult * (((hsing >> m) & 1u) ? 1ull : (1ull | (1ull << 32))));
-      }
-  }
   if constexpr (!MIRROR) {
     for (int q = 0; q < (nq < 2 ? nq : 2); ++q) {
       const uint32_t sa = wave_sum(q == 0 ? s0a : s1a), sb = wave_sum(q == 0 ? s0b : s1b);
@@ -1764,8 +1755,8 @@ __device__ __forceinline__ uint32_t fold_pass(const uint32_t (&v)[M], uint32_t p
 // the rest of that range is marked empty. stgk / stgb: this wave's staging rows (64*M + 64 each),
 // sacc: this wave's statistics accumulator, P / fh: the FO kernels' part tables and per-file rows.
 // FO: the FileOpts rule's per-file rows (fh); PM: part mode may be on (fo.parts), else compiled out. In part mode
-// with fo.mirror_off, a second pass writes the explicit mirror rows of the symmetric rule's stored rows.
-template <int M, bool FO, bool PM = FO>
+// with fo.mirror_off (MIR), a second pass writes the explicit mirror rows of the symmetric rule's stored rows.
+template <int M, bool FO, bool PM = FO, bool MIR = false>
 __device__ __forceinline__ void agg_fold(uint32_t (&v)[M], uint64_t obegin, uint32_t olen, uint32_t rk,
                                          const RulesDev& sR, const Layout& L, const OutRows& O, const FileOpts& fo,
                                          const PartLds* P, unsigned long long* fh, uint32_t* stgk, uint32_t* stgb,
@@ -1793,7 +1784,7 @@ __device__ __forceinline__ void agg_fold(uint32_t (&v)[M], uint64_t obegin, uint
   }
   const uint32_t nout =
       fold_pass<M, FO, PM, false>(v, pl, nl, pt, ppl, pnl, pmode, obegin, olen, rk, sR, L, O, fo, fh, stgk, stgb, sacc);
-  if constexpr (PM) {
+  if constexpr (PM && MIR) {
     if (pmode && fo.mirror_off) {
       // the mirrors' parts differ from the rows' only for words of a cut file between the two keys
       bool differ = false;
@@ -1838,13 +1829,13 @@ __device__ __forceinline__ void agg_fold(uint32_t (&v)[M], uint64_t obegin, uint
 // through a per-wave LDS accumulator (one lane, after wave sums of packed 16-bit fields: a
 // task holds <= 1024 words), so no per-thread accumulator arrays take registers.
 // FOM: 0 no FileOpts; 1 FileOpts with key cuts / part mode (static per-file table of FO_MAXF rows + the part
-// tables in LDS); 2 per-file rows only (the histogram of the call's fo.nf files in dynamic LDS, fo.nf * 8 bytes:
+// tables in LDS); 3 part mode with the explicit mirror rows (ottohip_table_count_parts); 2 per-file rows only (the histogram of the call's fo.nf files in dynamic LDS, fo.nf * 8 bytes:
 // the main build's statistics cost no occupancy)
 extern __shared__ unsigned long long agg_sort_fh_dyn[];
 // occupancy: 4 waves per SIMD (<= 128 VGPRs) for the 512- and 1024-word classes, except the part-mode 1024-word
 // class (2; its mirror pass would spill heavily at 4)
 template <int M, int FOM = 0>
-__global__ __launch_bounds__(256, (M >= 16 ? (FOM == 1 ? 2 : 4) : (M == 8 ? 4 : 1))) void k_agg_sort(const Task* __restrict__ tasks, int64_t n_tasks,
+__global__ __launch_bounds__(256, (M >= 16 ? (FOM == 1 ? 2 : (FOM == 3 ? 1 : 4)) : (M == 8 && FOM == 2 ? 4 : 1))) void k_agg_sort(const Task* __restrict__ tasks, int64_t n_tasks,
                                                   const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
                                                   const uint32_t* __restrict__ row_key, RulesDev R, Layout L,
                                                   int n_rules, OutRows O, FileOpts fo) {
@@ -1853,8 +1844,9 @@ __global__ __launch_bounds__(256, (M >= 16 ? (FOM == 1 ? 2 : 4) : (M == 8 ? 4 : 
   __shared__ RulesDev sR;
   __shared__ uint32_t stg[4][2][64 * M + 64];  // per wave: output rows of one task (key2, count | count_ge2 << 16),
                                               // + one dummy slot per lane
-  __shared__ unsigned long long fh_s[FOM == 1 ? FO_MAXF : 1];  // per-file rows of the FileOpts rule
-  __shared__ std::conditional_t<FOM == 1, PartLds, char> sP[1];  // part-mode tables (FOM 1 only)
+  constexpr bool PMODE = FOM == 1 || FOM == 3;
+  __shared__ unsigned long long fh_s[PMODE ? FO_MAXF : 1];  // per-file rows of the FileOpts rule
+  __shared__ std::conditional_t<PMODE, PartLds, char> sP[1];  // part-mode tables (FOM 1 / 3 only)
   unsigned long long* fh = FOM == 2 ? agg_sort_fh_dyn : fh_s;
   const uint32_t l = lane_id();
   const int wv = threadIdx.x >> 6;
@@ -1862,7 +1854,7 @@ __global__ __launch_bounds__(256, (M >= 16 ? (FOM == 1 ? 2 : 4) : (M == 8 ? 4 : 
   for (int i = (int)l; i < STAT_STRIDE; i += 64) sacc[wv][i] = 0;
   if constexpr (FO) {
     for (uint32_t i = threadIdx.x; i < fo.nf; i += blockDim.x) fh[i] = 0;
-    if constexpr (FOM == 1) part_lds_load(fo, sP[0]);
+    if constexpr (PMODE) part_lds_load(fo, sP[0]);
   }
   __syncthreads();
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -1882,7 +1874,7 @@ __global__ __launch_bounds__(256, (M >= 16 ? (FOM == 1 ? 2 : 4) : (M == 8 ? 4 : 
     }
     rkk = row_key[TT.row];
     ndd = 0;
-    if constexpr (FOM == 1) {  // the cut words become W_EMPTY (sorted past the task's new end)
+    if constexpr (PMODE) {  // the cut words become W_EMPTY (sorted past the task's new end)
       if ((fo.cuts || fo.qonly) && (int)(rkk >> A) == fo.type) {
         const int32_t ad = (int32_t)(rkk & L.amask);
         uint32_t k = 0;
@@ -1906,7 +1898,7 @@ __global__ __launch_bounds__(256, (M >= 16 ? (FOM == 1 ? 2 : 4) : (M == 8 ? 4 : 
     const uint32_t len = T.len - nd;
     if (FO && nd && l == 0) atomicAdd(fo.dropped, (unsigned long long)nd);
     if (FO && fo.dbg && l == 0) { atomicAdd(fo.dbg + 2, (unsigned long long)nd); atomicAdd(fo.dbg + 3, (unsigned long long)len); }
-    agg_fold<M, FO, FOM == 1>(v, T.begin, T.len, rk, sR, L, O, fo, reinterpret_cast<const PartLds*>(sP), fh,
+    agg_fold<M, FO, PMODE, FOM == 3>(v, T.begin, T.len, rk, sR, L, O, fo, reinterpret_cast<const PartLds*>(sP), fh,
                               stg[wv][0], stg[wv][1], sacc[wv]);
     T = Tn;
     rk = rkn;
@@ -1989,7 +1981,7 @@ struct TaskLists {
   uint64_t cap;           // capacity of every list
 };
 
-// FOM as k_agg_sort: 0 no FileOpts, 1 cuts / part mode (and its mirror pass), 2 per-file rows only
+// FOM as k_agg_sort: 0 no FileOpts, 1 cuts / part mode, 3 part mode with the mirror pass, 2 per-file rows only
 template <int FOM = 0>
 __global__ __launch_bounds__(AGG_T, 2) void k_agg_hash(const Task* __restrict__ tasks, int64_t n_tasks,
                                                     const uint32_t* __restrict__ w0, const uint32_t* __restrict__ w1,
@@ -1999,7 +1991,7 @@ __global__ __launch_bounds__(AGG_T, 2) void k_agg_hash(const Task* __restrict__ 
   __shared__ unsigned long long lds[2 * HCAP];  // 64 KiB: phase A [0, cap), phase B [0, 2cap)
   __shared__ uint32_t wtot[AGG_T / 64];
   __shared__ uint32_t nocc;
-  constexpr bool FO = FOM != 0, PM = FOM == 1;
+  constexpr bool FO = FOM != 0, PM = FOM == 1 || FOM == 3;
   __shared__ unsigned long long fh[FO ? FO_MAXF : 1];  // per-file rows of the FileOpts rule
   __shared__ std::conditional_t<PM, PartLds, char> sP[1];  // part-mode tables (FOM 1 only)
   const int tid = threadIdx.x;
@@ -2140,7 +2132,7 @@ __global__ __launch_bounds__(AGG_T, 2) void k_agg_hash(const Task* __restrict__ 
     __syncthreads();
     // pass 0: the rows; pass 1 (part mode with mirror rows): the explicit mirrors (part_m, aid_next, aid) of a
     // symmetric rule's stored rows at mirror_off + slot, no statistics (block-uniform)
-    const int npass = (PM && pmode && fo.mirror_off) ? 2 : 1;
+    const int npass = (FOM == 3 && pmode && fo.mirror_off) ? 2 : 1;
     uint32_t nout = 0;
 #pragma unroll 1
     for (int pass = 0; pass < npass; ++pass) {

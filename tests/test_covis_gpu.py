@@ -402,7 +402,7 @@ def test_concat_files_w_stats_part_branch(gpu, kw):
     dict(max_rows_groupby=300_000, optim_rows=250_000, max_pairs=200_000, click_filter_rows=1_000_000),
     dict(max_rows_groupby=50_000, optim_rows=20_000, max_pairs=10**9, click_filter_rows=10**9),
 ])
-def test_part_branch_from_kept_words(gpu, kw):
+def test_part_branch_from_kept_words(gpu, kw, monkeypatch):
     """Branch (2) re-folded from the main build's own words (ottohip_file_opts.keep_words +
     ottohip_table_count_parts): one 5-rule count that histograms click_to_click's rows per file and keeps its
     words; each rule's part-tagged table comes from its row type's range of the kept words (the type's other rule
@@ -410,6 +410,7 @@ def test_part_branch_from_kept_words(gpu, kw):
     with their own parts. Per part equal to the part-tagged recount (ottohip_covis_count_parts), and A6 equal to
     the restatement (model/count_co_events.py:135-166)."""
     from otto_recommender_amd import covis as gc
+    monkeypatch.setenv("OTTOHIP_A6_REFOLD", "1")  # A6 takes the re-fold (off by default: covis.a6_refold)
     ev = synth.generate(30_000, first_session=2024)
     fb = synth.file_session_bounds(ev.n_sessions, per_file=3_000)
     per_file = oracle.count_co_events_files(ev.session_offsets, ev.aid, ev.ts, ev.type, fb)
