@@ -487,16 +487,23 @@ __device__ __forceinline__ void km_split8(const float (&v)[8], uint4& hi, uint4&
 // get lb = 0 (scored again next step). Every bound is rounded outwards (relative 2^-20 / 1e-6).
 constexpr float KMB_SKIP = 2e-4f;
 constexpr float KMB_ERR = 2e-4f;
-// Half-precision E-step (H16: the rows as f16, xh = RN_f16(x), |x - xh| <= 2^-11 |x| + 2^-25 per element; c = ch + cl
-// in f16 within 2^-22 |c| + 2^-25): x.c ~ xh.ch + xh.cl on v_mfma_f32_32x32x16_f16 (products exact, f32 sums of 224
-// terms) is off by <= (2^-11 + 1.4e-5) |x| |c| + 3e-7 (|x| + |c|), a score by twice that: 1.01e-3 |x| |c| + 6e-7
-// (|x| + |c|). Decided when the two smallest scores differ by more than twice the sum with the exact kernel's
-// 1.5e-5 |x||c|, kept with a 2x margin: KMH_SEP = 4.1e-3 (|x| cmax) + KMH_ABS = 2.5e-6 (|x| + cmax). About 5 % of
-// the rows on session embeddings are then near ties (6e-4 for the bf16 split: ~1 %), scored by the exact kernel,
-// but every row reads 208 B instead of 400. The rows' squared norms are exact f32 sums (ottohip_kmeans_attach_half).
-constexpr float KMH_SEP = 4.1e-3f;
+// Half-precision E-step (H16: the rows as f16, xh = RN_f16(x) with the row's rounding residual e = x - xh, |e| <=
+// 2^-11 |x| + 2^-25 sqrt(dim); c = ch + cl in f16 within 2^-22 |c| + 2^-25 per element): x.c ~ xh.ch + xh.cl on
+// v_mfma_f32_32x32x16_f16 (products exact, f32 sums of 224 terms) is off by <= |e.c| + |xh.(c - ch - cl)| + the
+// sums' rounding <= |e| |c| + 1.45e-5 |x| |c| + 3e-7 (|x| + |c|) (Cauchy-Schwarz on the residual), a score by
+// twice that. Decided when the two smallest scores differ by more than twice the sum with the exact kernel's
+// 1.5e-5 |x||c| (4 |e| cmax + 8.8e-5 |x| cmax), kept with a 2x margin: KMH_SEP_E = 8 (|e| cmax) + KMH_SEP_X = 1.76e-4
+// (|x| cmax) + KMH_ABS = 2.5e-6 (|x| + cmax). |e| is the row's own residual norm (ottohip_kmeans_attach_half, rounded
+// up), ~0.3 of the worst case 2^-11 |x| the first version assumed for every row (KMH_SEP = 4.1e-3 |x| cmax, 8.6 %
+// of the scored rows near ties on session embeddings). Every row reads 208 B instead of 400.
+constexpr float KMH_SEP_E = 8.f;
+constexpr float KMH_SEP_X = 1.76e-4f;
 constexpr float KMH_ABS = 2.5e-6f;
-constexpr float KMH_ERR = 1.2e-3f;  // score error bound for the rebuilt distance bounds (cmax (|x| + cmax) units)
+// score error for the rebuilt distance bounds: 2 |e| cmax + 2.9e-5 |x| cmax with a 1.2x margin, plus |c|^2's f32
+// rounding (cmax^2 units)
+constexpr float KMH_ERR_E = 2.4f;
+constexpr float KMH_ERR_X = 3.5e-5f;
+constexpr float KMH_ERR_C = 1.2e-5f;
 constexpr int KMH_AMB = 8192;       // near-tie rows staged per block (~5 % of a block's ~50 k rows)
 constexpr int KMH_MT = 768;         // H16 block: 12 waves (136-170 VGPRs: 3 waves per SIMD)
 // KMH_MAXABS: the f16 copy is refused above this |x| (f16 overflows at 65504; centroids are row means, so their
@@ -511,7 +518,7 @@ __global__ void k_km_half_rows(const float* __restrict__ X, int64_t n, int dim, 
   const int l = threadIdx.x & 63;
   if (row >= n) return;
   const float* xp = X + row * dim;
-  float ss = 0.f;
+  float ss = 0.f, es = 0.f;
   unsigned mx = 0u;  // bits of max |x| over the lane's elements (non-negative floats order as unsigned ints)
   if (l < kc) {
     _Float16 h[8];
@@ -521,6 +528,8 @@ __global__ void k_km_half_rows(const float* __restrict__ X, int64_t n, int dim, 
       const float v = d < dim ? xp[d] : 0.f;
       ss += v * v;
       h[j] = (_Float16)v;
+      const float r = v - (float)h[j];  // exact in f32
+      es += r * r;
       mx = max(mx, __float_as_uint(v) & 0x7FFFFFFFu);
     }
     X16[row * kc + l] = __builtin_bit_cast(uint4, h);
@@ -528,10 +537,12 @@ __global__ void k_km_half_rows(const float* __restrict__ X, int64_t n, int dim, 
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
     ss += __shfl_xor(ss, o);
+    es += __shfl_xor(es, o);
     mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
   }
   if (l == 0) {
-    xn2[row] = ss;
+    // |x - xh| rounded up (f32 sum of <= 128 squares: relative error < 1e-5, sqrt half an ulp)
+    reinterpret_cast<float2*>(xn2)[row] = make_float2(ss, sqrtf(es * 1.00002f) * 1.000001f);
     if (mx > __float_as_uint(KMH_MAXABS)) atomicMax(amax, mx);
   }
 }
@@ -660,7 +671,10 @@ __device__ __forceinline__ void km_split8_h(const float (&v)[8], uint4& hi, uint
   lo = __builtin_bit_cast(uint4, r);
 }
 // H16: the rows from X16 (f16, 2 KS chunks per row) and their squared norms xn2 (ottohip_kmeans_attach_half)
-template <int NB, int KS, bool BL = false, bool H16 = false>
+// MV: a decided row whose label changes is listed {row, old | new << 16} in the block's own region of mv_list
+// (mv_cap entries per block, count in mv_cnt[block]); k_km_ties folds the regions into the sums (no LDS sums,
+// no per-row gather of the f32 row while the wave waits)
+template <int NB, int KS, bool BL = false, bool H16 = false, bool MV = false>
 __global__ __launch_bounds__(H16 ? KMH_MT : KM_MT, H16 ? 1 : 2) void k_km_assign_split(const float* __restrict__ X, int64_t n, int dim,
                                                              const float* __restrict__ C, const float* __restrict__ cn,
                                                              int k, int32_t* __restrict__ label,
@@ -675,18 +689,21 @@ __global__ __launch_bounds__(H16 ? KMH_MT : KM_MT, H16 ? 1 : 2) void k_km_assign
                                                              float* __restrict__ ub = nullptr,
                                                              float* __restrict__ lb = nullptr,
                                                              const uint4* __restrict__ X16 = nullptr,
-                                                             const float* __restrict__ xn2 = nullptr) {
+                                                             const float* __restrict__ xn2 = nullptr,  // {|x|^2, |x - xh|}
+                                                             uint2* __restrict__ mv_list = nullptr,
+                                                             uint32_t* __restrict__ mv_cnt = nullptr,
+                                                             uint32_t mv_cap = 0) {
   if (gate && __builtin_amdgcn_readfirstlane(*gate)) return;
   constexpr int AMB = H16 ? KMH_AMB : KMS_AMB;
   constexpr int MT = H16 ? KMH_MT : KM_MT;  // threads per block (H16: 12 waves, its registers allow 3 per SIMD)
   extern __shared__ unsigned long long smem64[];
   uint4* Cf = reinterpret_cast<uint4*>(smem64);                               // [NB][KS][hi, lo][64]
   unsigned long long* ls = reinterpret_cast<unsigned long long*>(Cf + NB * KS * 2 * 64);  // k * dim sums
-  unsigned long long* lc = ls + k * dim;                                       // k counts
-  int32_t* labl = reinterpret_cast<int32_t*>(lc + k);                         // [waves][3][32]
+  unsigned long long* lc = ls + (MV ? 0 : k * dim);                            // k counts
+  int32_t* labl = reinterpret_cast<int32_t*>(lc + (MV ? 0 : k));              // [waves][3][32]
   float* cnl = reinterpret_cast<float*>(labl + (MT / 64) * 96);             // [64]
   uint32_t* amb = reinterpret_cast<uint32_t*>(cnl + 64);                       // [AMB]
-  __shared__ uint32_t namb;
+  __shared__ uint32_t namb, nmv;
   __shared__ unsigned long long abase;
   const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6, h = l >> 5, i32 = l & 31;
   // centroid fragments: lane (r, h) of block b, k-step s holds centroid 32 b + r, dims 16 s + 8 h .. + 7
@@ -703,8 +720,9 @@ __global__ __launch_bounds__(H16 ? KMH_MT : KM_MT, H16 ? 1 : 2) void k_km_assign
     Cf[(sb * 2 + 1) * 64 + ll] = lo;
   }
   if (tid < 64) cnl[tid] = cn[tid];
-  for (int i = tid; i < k * dim + k; i += MT) ls[i] = 0ull;
-  if (tid == 0) namb = 0;
+  if constexpr (!MV)
+    for (int i = tid; i < k * dim + k; i += MT) ls[i] = 0ull;
+  if (tid == 0) { namb = 0; nmv = 0; }
   __syncthreads();
   float c2 = l < k ? cnl[l] : 0.f;
 #pragma unroll
@@ -717,7 +735,7 @@ __global__ __launch_bounds__(H16 ? KMH_MT : KM_MT, H16 ? 1 : 2) void k_km_assign
   // the next tile's rows (and its rows' current labels) are loaded while this tile is scored
   float4 raw[H16 ? 1 : 2 * KS];
   uint4 raw16[H16 ? KS : 1];
-  float xn_n = 0.f;
+  float xn_n = 0.f, en_n = 0.f;
   int32_t lab_n = -1;
   int64_t row_n = 0;
   auto load = [&](int64_t tt) __attribute__((always_inline)) {
@@ -728,9 +746,11 @@ __global__ __launch_bounds__(H16 ? KMH_MT : KM_MT, H16 ? 1 : 2) void k_km_assign
 #pragma unroll
       for (int s_ = 0; s_ < KS; ++s_) {
         const int d0 = 16 * s_ + 8 * h;  // the chunk's zero padding past dim is stored: only wholly-past chunks skip
-        raw16[s_] = d0 < dim ? X16[rr * (2 * KS) + 2 * s_ + h] : make_uint4(0u, 0u, 0u, 0u);
+        raw16[s_] = d0 < dim ? X16[rr * ((dim + 7) >> 3) + 2 * s_ + h] : make_uint4(0u, 0u, 0u, 0u);
       }
-      xn_n = xn2[rr];
+      const float2 ne = reinterpret_cast<const float2*>(xn2)[rr];
+      xn_n = ne.x;
+      en_n = ne.y;
     } else {
       const float* xp = X + rr * dim;
 #pragma unroll
@@ -750,11 +770,12 @@ __global__ __launch_bounds__(H16 ? KMH_MT : KM_MT, H16 ? 1 : 2) void k_km_assign
     const int64_t row = row_n;
     km_bf16x8 xh[H16 ? 1 : KS], xl[H16 ? 1 : KS];
     km_f16x8 xq[H16 ? KS : 1];
-    float xs = 0.f;
+    float xs = 0.f, ee = 0.f;
     if constexpr (H16) {
 #pragma unroll
       for (int s_ = 0; s_ < KS; ++s_) xq[s_] = __builtin_bit_cast(km_f16x8, raw16[s_]);
       xs = xn_n;
+      ee = en_n;
     } else {
 #pragma unroll
       for (int s_ = 0; s_ < KS; ++s_) {
@@ -842,11 +863,11 @@ __global__ __launch_bounds__(H16 ? KMH_MT : KM_MT, H16 ? 1 : 2) void k_km_assign
       if (NB == 2) m2 = fminf(m2, c0 + 32 == mc ? INFINITY : acc1[r]);
     }
     m2 = fminf(m2, __shfl_xor(m2, 32));
-    const bool decided = H16 ? m2 - m > KMH_SEP * sqrtf(xs) * cmax + KMH_ABS * (sqrtf(xs) + cmax)
+    const bool decided = H16 ? m2 - m > (KMH_SEP_E * ee + KMH_SEP_X * sqrtf(xs)) * cmax + KMH_ABS * (sqrtf(xs) + cmax)
                              : m2 - m > KMS_SEP * sqrtf(xs) * cmax;
     if (BL && h == 0 && in_r) {  // the row's bounds for these centres (near ties: none, lb = 0)
       const float cm = cmax * 1.000001f;
-      const float e = H16 ? KMH_ERR * cm * (sqrtf(xs) * 1.0001f + cm) + KMH_ABS * (sqrtf(xs) + cm)
+      const float e = H16 ? (KMH_ERR_E * ee + KMH_ERR_X * sqrtf(xs) * 1.0001f + KMH_ERR_C * cm) * cm + KMH_ABS * (sqrtf(xs) + cm)
                           : KMB_ERR * cm * (sqrtf(xs) * 1.0001f + cm);
       ub[row] = decided ? sqrtf(fmaxf(m + xs * 1.00001f + e, 0.f)) * 1.000001f : 0.f;
       lb[row] = decided ? sqrtf(fmaxf(m2 + xs * 0.99999f - e, 0.f)) * 0.999999f : 0.f;
@@ -872,14 +893,228 @@ __global__ __launch_bounds__(H16 ? KMH_MT : KM_MT, H16 ? 1 : 2) void k_km_assign
         else amb_rows[atomicAdd(n_amb, 1ull)] = (uint32_t)row;
       }
     }
-    km_move_rows(X, dim, ls, lc, labl + wv * 96, mine && old != (int32_t)mi, row, mi, old);
+    if constexpr (MV) {
+      const bool mvf = mine && old != (int32_t)mi;
+      const uint64_t mm = __ballot(mvf);
+      if (mm) {
+        uint32_t b = 0;
+        if (l == 0) b = atomicAdd(&nmv, (uint32_t)__popcll(mm));
+        b = __shfl(b, 0);
+        if (mvf)
+          mv_list[(size_t)blockIdx.x * mv_cap + b + mbcnt(mm)] =
+              make_uint2((uint32_t)row, (old < 0 ? 0xFFFFu : (uint32_t)old) | (mi << 16));
+      }
+    } else {
+      km_move_rows(X, dim, ls, lc, labl + wv * 96, mine && old != (int32_t)mi, row, mi, old);
+    }
   }
   __syncthreads();
-  for (int i = tid; i < k * dim; i += MT)
-    if (ls[i]) atomicAdd(&sums[i], ls[i]);
-  for (int i = tid; i < k; i += MT)
-    if (lc[i]) atomicAdd(&cnt[i], lc[i]);
+  if constexpr (MV) {
+    if (tid == 0) mv_cnt[blockIdx.x] = nmv;
+  } else {
+    for (int i = tid; i < k * dim; i += MT)
+      if (ls[i]) atomicAdd(&sums[i], ls[i]);
+    for (int i = tid; i < k; i += MT)
+      if (lc[i]) atomicAdd(&cnt[i], lc[i]);
+  }
   const uint32_t na = namb < (uint32_t)AMB ? namb : (uint32_t)AMB;
+  if (tid == 0) abase = na ? atomicAdd(n_amb, (unsigned long long)na) : 0ull;
+  __syncthreads();
+  for (uint32_t i = tid; i < na; i += MT) amb_rows[abase + i] = amb[i];
+  const uint32_t w = wave_sum(nchg);
+  if (l == 0 && w) atomicAdd(changed, (unsigned long long)w);
+}
+
+// The H16 pass of the bounded batched steps with move lists (the production E-step of C2), rebuilt for issue
+// cost (k_km_assign_split<NB, KS, true, true, true> spent ~445 VALU instructions per 32-row tile):
+// - two register sets in ping-pong (no copy of the prefetched row into the working registers) and the row
+//   indices of erows two tiles ahead, so a row gather never waits on its index load;
+// - rows of ceil(dim / 8) chunks read unconditionally (the chunk past a row is the next row's first, masked);
+// - accumulators start at -|c|^2 / 2, so acc = x.c - |c|^2 / 2 = -score / 2 comes out of the MFMA chain (no
+//   per-score fma; the chain's f32 rounding now also covers |c|^2 / 2: + 1.45e-5 cmax^2 per score, in the
+//   decision threshold (KMH_SEP_C) and the rebuilt bounds (KMH_ERR_C16));
+// - largest and second largest acc by a max / med3 chain (2 ops per score), then the lowest cluster holding
+//   the largest (the approximate argmin only labels rows whose gap is above the threshold, where it is unique).
+constexpr float KMH_SEP_C = 5.8e-5f;    // cmax^2 units (2x margin)
+constexpr float KMH_ERR_C16 = 2.5e-5f;  // cmax^2 units: chain rounding of |c|^2 / 2 and |c|^2's own (1.2x margin)
+template <int NB, int KS>
+__global__ __launch_bounds__(KMH_MT, 1) void k_km_split16(int64_t n, int dim, const float* __restrict__ C,
+                                                          const float* __restrict__ cn, int k,
+                                                          int32_t* __restrict__ label,
+                                                          unsigned long long* __restrict__ changed,
+                                                          const int* __restrict__ gate,
+                                                          uint32_t* __restrict__ amb_rows,
+                                                          unsigned long long* __restrict__ n_amb,
+                                                          const uint32_t* __restrict__ erows,
+                                                          const unsigned long long* __restrict__ n_eval,
+                                                          float* __restrict__ ub, float* __restrict__ lb,
+                                                          const uint4* __restrict__ X16, const float2* __restrict__ xne,
+                                                          uint2* __restrict__ mv_list, uint32_t* __restrict__ mv_cnt,
+                                                          uint32_t mv_cap) {
+  if (gate && __builtin_amdgcn_readfirstlane(*gate)) return;
+  constexpr int MT = KMH_MT, W = MT / 64;
+  extern __shared__ unsigned long long smem64[];
+  uint4* Cf = reinterpret_cast<uint4*>(smem64);                  // [NB][KS][hi, lo][64]
+  float* cnl = reinterpret_cast<float*>(Cf + NB * KS * 2 * 64);  // [64]: -|c|^2 / 2
+  uint32_t* amb = reinterpret_cast<uint32_t*>(cnl + 64);          // [KMH_AMB]
+  __shared__ uint32_t namb, nmv;
+  __shared__ unsigned long long abase;
+  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6, h = l >> 5, i32 = l & 31;
+  for (int e = tid; e < NB * KS * 64; e += MT) {
+    const int ll = e & 63, sb = e >> 6, s_ = sb % KS, b = sb / KS;
+    const int c = b * 32 + (ll & 31), d0 = 16 * s_ + 8 * (ll >> 5);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (c < k && d0 + j < dim) ? C[(int64_t)c * dim + d0 + j] : 0.f;
+    uint4 hi, lo;
+    km_split8_h(v, hi, lo);
+    Cf[(sb * 2 + 0) * 64 + ll] = hi;
+    Cf[(sb * 2 + 1) * 64 + ll] = lo;
+  }
+  if (tid < 64) cnl[tid] = -0.5f * cn[tid];  // padding clusters: cn = inf, so acc = -inf
+  if (tid == 0) { namb = 0; nmv = 0; }
+  __syncthreads();
+  float c2 = l < k ? cn[l] : 0.f;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) c2 = fmaxf(c2, __shfl_xor(c2, o));
+  const float cmax = sqrtf(c2);
+  const int kch = (dim + 7) >> 3;
+  const uint32_t lastmask = 2 * (KS - 1) + h < kch ? ~0u : 0u;  // the lane's last chunk lies inside the row
+  uint32_t nchg = 0;
+  const int64_t nl = (int64_t)__builtin_amdgcn_readfirstlane((int)*n_eval);
+  const int64_t ntile = (nl + 31) >> 5;
+  const int64_t nwv = (int64_t)gridDim.x * W;
+  auto ridx = [&](int64_t tt) __attribute__((always_inline)) -> uint32_t {
+    const int64_t ri = (tt << 5) + i32 < nl ? (tt << 5) + i32 : nl - 1;
+    return erows[ri];
+  };
+  auto load = [&](uint4 (&x)[KS], float2& ne, int32_t& lab, uint32_t rr) __attribute__((always_inline)) {
+    const uint4* p = X16 + (size_t)rr * kch + h;
+#pragma unroll
+    for (int s_ = 0; s_ < KS; ++s_) x[s_] = p[2 * s_];
+    ne = xne[rr];
+    lab = label[rr];
+  };
+  auto score = [&](const uint4 (&x)[KS], float2 ne, int32_t lab_cur, uint32_t row, int64_t t)
+                   __attribute__((always_inline)) {
+    const bool in_r = (t << 5) + i32 < nl;
+    km_f32x16 acc0, acc1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 n0 = *reinterpret_cast<const float4*>(cnl + 8 * j + 4 * h);
+      acc0[4 * j + 0] = n0.x; acc0[4 * j + 1] = n0.y; acc0[4 * j + 2] = n0.z; acc0[4 * j + 3] = n0.w;
+      if (NB == 2) {
+        const float4 n1 = *reinterpret_cast<const float4*>(cnl + 32 + 8 * j + 4 * h);
+        acc1[4 * j + 0] = n1.x; acc1[4 * j + 1] = n1.y; acc1[4 * j + 2] = n1.z; acc1[4 * j + 3] = n1.w;
+      }
+    }
+#pragma unroll
+    for (int s_ = 0; s_ < KS; ++s_) {
+      uint4 xv = x[s_];
+      if (s_ == KS - 1) {  // masked here, not at the load (a mask there waits for the load)
+        xv.x &= lastmask;
+        xv.y &= lastmask;
+        xv.z &= lastmask;
+        xv.w &= lastmask;
+      }
+      const km_f16x8 xq = __builtin_bit_cast(km_f16x8, xv);
+      const km_f16x8 ch0 = __builtin_bit_cast(km_f16x8, Cf[((0 * KS + s_) * 2 + 0) * 64 + l]);
+      const km_f16x8 cl0 = __builtin_bit_cast(km_f16x8, Cf[((0 * KS + s_) * 2 + 1) * 64 + l]);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ch0, xq, acc0, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(cl0, xq, acc0, 0, 0, 0);
+      if (NB == 2) {
+        const km_f16x8 ch1 = __builtin_bit_cast(km_f16x8, Cf[((1 * KS + s_) * 2 + 0) * 64 + l]);
+        const km_f16x8 cl1 = __builtin_bit_cast(km_f16x8, Cf[((1 * KS + s_) * 2 + 1) * 64 + l]);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ch1, xq, acc1, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(cl1, xq, acc1, 0, 0, 0);
+      }
+    }
+    // +inf the compiler cannot see as a constant: med3(a, b, +inf) would fold to a max that canonicalizes its
+    // operands (one more instruction per score)
+    const float pinf = __uint_as_float(0x7F800000u | ((uint32_t)k >> 31));
+    float a1 = -INFINITY, a2 = -INFINITY;  // largest, second largest (a tie at the top: a2 == a1)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      a2 = __builtin_amdgcn_fmed3f(a1, a2, acc0[r]);
+      a1 = __builtin_amdgcn_fmed3f(a1, acc0[r], pinf);
+      if (NB == 2) {
+        a2 = __builtin_amdgcn_fmed3f(a1, a2, acc1[r]);
+        a1 = __builtin_amdgcn_fmed3f(a1, acc1[r], pinf);
+      }
+    }
+    {
+      const float p1 = __shfl_xor(a1, 32), p2 = __shfl_xor(a2, 32);
+      a2 = fmaxf(fminf(a1, p1), fmaxf(a2, p2));
+      a1 = fmaxf(a1, p1);
+    }
+    int mc = 64;
+#pragma unroll
+    for (int r = 15; r >= 0; --r)
+      if (NB == 2) mc = acc1[r] == a1 ? 32 + (r & 3) + 8 * (r >> 2) + 4 * h : mc;
+#pragma unroll
+    for (int r = 15; r >= 0; --r) mc = acc0[r] == a1 ? (r & 3) + 8 * (r >> 2) + 4 * h : mc;
+    mc = min(mc, __shfl_xor(mc, 32));
+    const float xs = ne.x, ee = ne.y, xn = sqrtf(xs);
+    const float m = -2.f * a1, m2 = -2.f * a2;  // the two smallest approximate scores |c|^2 - 2 x.c
+    const bool decided = m2 - m > (KMH_SEP_E * ee + KMH_SEP_X * xn + KMH_SEP_C * cmax) * cmax + KMH_ABS * (xn + cmax);
+    if (h == 0 && in_r) {  // the row's bounds for these centres (near ties: none, lb = 0)
+      const float cm = cmax * 1.000001f;
+      const float e = (KMH_ERR_E * ee + KMH_ERR_X * xn * 1.0001f + KMH_ERR_C16 * cm) * cm + KMH_ABS * (xn + cm);
+      ub[row] = decided ? sqrtf(fmaxf(m + xs * 1.00001f + e, 0.f)) * 1.000001f : 0.f;
+      lb[row] = decided ? sqrtf(fmaxf(m2 + xs * 0.99999f - e, 0.f)) * 0.999999f : 0.f;
+    }
+    const int32_t mi = mc;
+    const bool mvf = h == 0 && in_r && decided && lab_cur != mi;
+    if (mvf) label[row] = mi;
+    nchg += mvf;
+    const uint64_t mm = __ballot(mvf);
+    if (mm) {
+      uint32_t b = 0;
+      if (l == 0) b = atomicAdd(&nmv, (uint32_t)__popcll(mm));
+      b = __shfl(b, 0);
+      if (mvf)
+        mv_list[(size_t)blockIdx.x * mv_cap + b + mbcnt(mm)] =
+            make_uint2(row, (lab_cur < 0 ? 0xFFFFu : (uint32_t)lab_cur) | ((uint32_t)mi << 16));
+    }
+    const bool tie = h == 0 && in_r && !decided;
+    const uint64_t tm = __ballot(tie);
+    if (tm) {
+      uint32_t b = 0;
+      if (l == 0) b = atomicAdd(&namb, (uint32_t)__popcll(tm));
+      b = __shfl(b, 0);
+      if (tie) {
+        const uint32_t p = b + mbcnt(tm);
+        if (p < (uint32_t)KMH_AMB) amb[p] = row;
+        else amb_rows[atomicAdd(n_amb, 1ull)] = row;
+      }
+    }
+  };
+  // tiles t0, t0 + nwv, ... of this wave: set A scores tile t while set B's rows are in flight, and back. The
+  // loads are unconditional (no register merges that wait on them): past the last tile ridx gives row
+  // erows[nl - 1] to every lane, one line.
+  const int64_t t0 = (int64_t)blockIdx.x * W + wv;
+  if (t0 < ntile) {
+    uint4 xa[KS], xb[KS];
+    float2 nea, neb;
+    int32_t laba, labb;
+    uint32_t rA = ridx(t0), rB = ridx(t0 + nwv);
+    load(xa, nea, laba, rA);
+    for (int64_t t = t0; t < ntile; t += 2 * nwv) {
+      // each index load is issued before the row loads it must not wait behind (vmcnt counts in issue order)
+      const int64_t t1 = t + nwv;
+      const uint32_t rC = ridx(t + 2 * nwv);
+      load(xb, neb, labb, rB);
+      score(xa, nea, laba, rA, t);
+      const uint32_t rD = ridx(t + 3 * nwv);
+      load(xa, nea, laba, rC);
+      if (t1 < ntile) score(xb, neb, labb, rB, t1);
+      rA = rC;
+      rB = rD;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) mv_cnt[blockIdx.x] = nmv;
+  const uint32_t na = namb < (uint32_t)KMH_AMB ? namb : (uint32_t)KMH_AMB;
   if (tid == 0) abase = na ? atomicAdd(n_amb, (unsigned long long)na) : 0ull;
   __syncthreads();
   for (uint32_t i = tid; i < na; i += MT) amb_rows[abase + i] = amb[i];
@@ -1120,6 +1355,198 @@ __global__ __launch_bounds__(KM_MT) void k_km_apply_moves(const float* __restric
     if (lc[i]) atomicAdd(&cnt[i], lc[i]);
 }
 
+// The near ties of a split pass with its move list (MV): one block per CU. Phase A folds the split pass's
+// move regions (the f32 rows of the decided label changes, gathered 8 rows per lane group at a time)
+// into the block's LDS sums; phase B scores the listed near-tie rows exactly as k_km_assign_mfma<LIST>
+// (same f32 MFMA chain, same argmin and ties) with the next tile's row index, row pieces and label
+// loaded while the current one is scored, and a changed row's vector added from the registers that
+// hold it (lanes i and i + 32: dims 8q + 4h .. + 3) instead of a second read of the row. One flush of
+// the block's sums; changed-row count and the near ties' inertia part once per block.
+template <int NB, int NQ>
+__global__ __launch_bounds__(KM_MT, 2) void k_km_ties(const float* __restrict__ X, int dim, int nq,
+                                                      const float* __restrict__ C, const float* __restrict__ cn,
+                                                      int k, int32_t* __restrict__ label,
+                                                      unsigned long long* __restrict__ sums,
+                                                      unsigned long long* __restrict__ cnt,
+                                                      double* __restrict__ inertia,
+                                                      unsigned long long* __restrict__ changed,
+                                                      const int* __restrict__ gate,
+                                                      const uint32_t* __restrict__ lrows,
+                                                      const unsigned long long* __restrict__ lnrows,
+                                                      const uint2* __restrict__ mv_list,
+                                                      const uint32_t* __restrict__ mv_cnt, uint32_t mv_cap,
+                                                      int n_regions) {
+  if (gate && __builtin_amdgcn_readfirstlane(*gate)) return;
+  extern __shared__ unsigned long long smem64[];
+  float4* Bl = reinterpret_cast<float4*>(smem64);                              // [NB][nq][64]
+  int32_t* labl = reinterpret_cast<int32_t*>(Bl + NB * nq * 64);                // [waves][3][32]
+  float* cnl = reinterpret_cast<float*>(labl + (KM_MT / 64) * 96);             // [64]
+  unsigned long long* ls = reinterpret_cast<unsigned long long*>(cnl + 64);    // k * dim sums, k counts
+  unsigned long long* lc = ls + k * dim;
+  __shared__ uint32_t s_chg;
+  __shared__ double s_part;
+  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6, h = l >> 5, i32 = l & 31;
+  for (int e = tid; e < NB * nq * 64; e += KM_MT) {
+    const int ll = e & 63, q = (e >> 6) % nq, b = (e >> 6) / nq;
+    const int c = b * 32 + (ll & 31), d0 = 8 * q + 4 * (ll >> 5);
+    float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < k && d0 < dim) f = *reinterpret_cast<const float4*>(C + (int64_t)c * dim + d0);
+    Bl[e] = f;
+  }
+  if (tid < 64) cnl[tid] = cn[tid];
+  for (int i = tid; i < k * dim + k; i += KM_MT) ls[i] = 0ull;
+  if (tid == 0) { s_chg = 0; s_part = 0.0; }
+  __syncthreads();
+  // phase A: the split pass's label changes (their rows leave the old cluster, enter the new one)
+  for (int r = blockIdx.x; r < n_regions; r += gridDim.x) {
+    const int64_t nm = mv_cnt[r];
+    const uint2* ml = mv_list + (size_t)r * mv_cap;
+    for (int64_t b = (int64_t)wv * 32; b < nm; b += (KM_MT / 64) * 32) {
+      const bool f = l < 32 && b + l < nm;
+      uint2 m = make_uint2(0u, 0u);
+      if (f) m = ml[b + l];
+      const uint32_t from = m.y & 0xFFFFu;
+      km_move_rows(X, dim, ls, lc, labl + wv * 96, f, (int64_t)m.x, m.y >> 16, from == 0xFFFFu ? -1 : (int32_t)from);
+    }
+  }
+  // phase B: the near ties
+  double part = 0.0;
+  uint32_t nchg = 0;
+  const int64_t nl = (int64_t)__builtin_amdgcn_readfirstlane((int)*lnrows);
+  const int64_t ntile = (nl + 31) >> 5;
+  const int64_t nwv = (int64_t)gridDim.x * (KM_MT / 64);
+  float4 an[NQ];
+  int64_t row_n = 0;
+  int32_t lab_n = -1;
+  auto load = [&](int64_t tt) __attribute__((always_inline)) {
+    const int64_t ri = (tt << 5) + i32 < nl ? (tt << 5) + i32 : nl - 1;
+    const int64_t rr = (int64_t)lrows[ri];
+    const float* x = X + rr * dim;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int d0 = 8 * q + 4 * h;
+      an[q] = (q < nq && d0 < dim) ? *reinterpret_cast<const float4*>(x + d0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    row_n = rr;
+    lab_n = label[rr];
+  };
+  const int64_t t_first = (int64_t)blockIdx.x * (KM_MT / 64) + wv;
+  if (t_first < ntile) load(t_first);
+  for (int64_t t = t_first; t < ntile; t += nwv) {
+    const bool in_l = (t << 5) + i32 < nl;
+    const int64_t row = row_n;
+    const int32_t lab_cur = lab_n;
+    float4 a[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) a[q] = an[q];
+    if (t + nwv < ntile) load(t + nwv);
+    float xs = 0.f;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) xs += a[q].x * a[q].x + a[q].y * a[q].y + a[q].z * a[q].z + a[q].w * a[q].w;
+    xs += __shfl_xor(xs, 32);
+    km_f32x16 acc0 = {}, acc1 = {};
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      if (q < nq) {
+        const float4 b0 = Bl[q * 64 + l];
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(b0.x, a[q].x, acc0, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(b0.y, a[q].y, acc0, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(b0.z, a[q].z, acc0, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(b0.w, a[q].w, acc0, 0, 0, 0);
+        if (NB == 2) {
+          const float4 b1 = Bl[(nq + q) * 64 + l];
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b1.x, a[q].x, acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b1.y, a[q].y, acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b1.z, a[q].z, acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b1.w, a[q].w, acc1, 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 n0 = *reinterpret_cast<const float4*>(cnl + 8 * j + 4 * h);
+      acc0[4 * j + 0] = n0.x - 2.f * acc0[4 * j + 0];
+      acc0[4 * j + 1] = n0.y - 2.f * acc0[4 * j + 1];
+      acc0[4 * j + 2] = n0.z - 2.f * acc0[4 * j + 2];
+      acc0[4 * j + 3] = n0.w - 2.f * acc0[4 * j + 3];
+      if (NB == 2) {
+        const float4 n1 = *reinterpret_cast<const float4*>(cnl + 32 + 8 * j + 4 * h);
+        acc1[4 * j + 0] = n1.x - 2.f * acc1[4 * j + 0];
+        acc1[4 * j + 1] = n1.y - 2.f * acc1[4 * j + 1];
+        acc1[4 * j + 2] = n1.z - 2.f * acc1[4 * j + 2];
+        acc1[4 * j + 3] = n1.w - 2.f * acc1[4 * j + 3];
+      }
+    }
+    float m = INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      m = fminf(m, acc0[r]);
+      if (NB == 2) m = fminf(m, acc1[r]);
+    }
+    int mc = 64;
+#pragma unroll
+    for (int r = 15; r >= 0; --r) {
+      if (NB == 2) mc = acc1[r] == m ? 32 + (r & 3) + 8 * (r >> 2) + 4 * h : mc;
+    }
+#pragma unroll
+    for (int r = 15; r >= 0; --r) mc = acc0[r] == m ? (r & 3) + 8 * (r >> 2) + 4 * h : mc;
+    {
+      const float pm = __shfl_xor(m, 32);
+      const int pc = __shfl_xor(mc, 32);
+      if (pm < m || (pm == m && pc < mc)) { m = pm; mc = pc; }
+    }
+    const int32_t mi = mc;
+    const bool chg = in_l && lab_cur != mi;  // both lanes of the row agree (same row, label and argmin)
+    if (h == 0 && in_l) {
+      nchg += chg;
+      if (chg) label[row] = mi;
+      part += (double)fmaxf(xs + m, 0.f);
+    }
+    if (__ballot(chg)) {
+      if (chg) {  // the row's dims held by this lane into the new cluster's sums, out of the old one's
+        unsigned long long* rw = ls + mi * dim;
+        unsigned long long* ow = ls + (lab_cur >= 0 ? lab_cur : 0) * dim;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const float v4[4] = {a[q].x, a[q].y, a[q].z, a[q].w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int d = 8 * q + 4 * h + u;
+            if (q < nq && d < dim) {
+              const long long v = km_fx(v4[u]);
+              atomicAdd(&rw[d], (unsigned long long)v);
+              if (lab_cur >= 0) atomicAdd(&ow[d], (unsigned long long)(-v));
+            }
+          }
+        }
+        if (h == 0) {
+          atomicAdd(&lc[mi], 1ull);
+          if (lab_cur >= 0) atomicAdd(&lc[lab_cur], ~0ull);
+        }
+      }
+    }
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint64_t b = __double_as_longlong(part);
+    const uint32_t lo = __shfl_xor((uint32_t)b, o), hi = __shfl_xor((uint32_t)(b >> 32), o);
+    part += __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+  }
+  const uint32_t w = wave_sum(nchg);
+  if (l == 0) {
+    if (w) atomicAdd(&s_chg, w);
+    atomicAdd(&s_part, part);
+  }
+  __syncthreads();
+  for (int i = tid; i < k * dim; i += KM_MT)
+    if (ls[i]) atomicAdd(&sums[i], ls[i]);
+  for (int i = tid; i < k; i += KM_MT)
+    if (lc[i]) atomicAdd(&cnt[i], lc[i]);
+  if (tid == 0) {
+    if (s_chg) atomicAdd(changed, (unsigned long long)s_chg);
+    atomicAdd(inertia, s_part);
+  }
+}
+
 // inc: sums / cnt hold the exact sums / counts of the rows under `labels` (the previous labels) and
 // are updated by the rows whose label changes (MFMA kernel); otherwise they are accumulated from
 // scratch by every row (the caller zeroes them)
@@ -1162,7 +1589,10 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
     split = split && inc && sums && changed && !dist && !(se && !strcmp(se, "0"));
     uint32_t* amb = nullptr;
     unsigned long long* n_amb = nullptr;
-    bool h16 = false;
+    bool h16 = false, mv = false;
+    uint2* mv_list = nullptr;
+    uint32_t* mv_cnt = nullptr;
+    uint32_t mv_cap = 0;
     if (split) {
       OH_TRY(ctx->ws.get("km_amb", (size_t)std::max<int64_t>(n, 1), &amb));
       OH_TRY(ctx->ws.get("km_namb", 1, &n_amb));
@@ -1177,12 +1607,20 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
       // bounds >= 0 (batched steps): skip the rows whose distance bounds keep their label; 1 = the
       // bounds are not valid for these rows (every row scored, bounds rebuilt)
       const bool bl = bounds >= 0 && km_bounds_on(n);
+      // MV (H16 with bounds): label changes to per-block move lists, folded by k_km_ties (OTTOHIP_KM_MV=0: the
+      // split pass's own LDS sums; A/B switch, read per call)
+      const char* mve = getenv("OTTOHIP_KM_MV");
+      mv = h16 && bl && !(mve && !strcmp(mve, "0"));
+      const size_t lds2m = lds2 - (mv ? ((size_t)k * dim + k) * 8 : 0);
       auto sk = KS == 7 ? (NB == 1 ? k_km_assign_split<1, 7> : k_km_assign_split<2, 7>)
                         : (NB == 1 ? k_km_assign_split<1, 8> : k_km_assign_split<2, 8>);
       if (bl)
         sk = KS == 7 ? (NB == 1 ? k_km_assign_split<1, 7, true> : k_km_assign_split<2, 7, true>)
                      : (NB == 1 ? k_km_assign_split<1, 8, true> : k_km_assign_split<2, 8, true>);
-      if (h16)
+      if (h16 && mv)
+        sk = KS == 7 ? (NB == 1 ? k_km_assign_split<1, 7, true, true, true> : k_km_assign_split<2, 7, true, true, true>)
+                     : (NB == 1 ? k_km_assign_split<1, 8, true, true, true> : k_km_assign_split<2, 8, true, true, true>);
+      else if (h16)
         sk = bl ? (KS == 7 ? (NB == 1 ? k_km_assign_split<1, 7, true, true> : k_km_assign_split<2, 7, true, true>)
                            : (NB == 1 ? k_km_assign_split<1, 8, true, true> : k_km_assign_split<2, 8, true, true>))
                 : (KS == 7 ? (NB == 1 ? k_km_assign_split<1, 7, false, true> : k_km_assign_split<2, 7, false, true>)
@@ -1190,7 +1628,7 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
       const uint4* x16 = h16 ? reinterpret_cast<const uint4*>(ctx->km_x16) : nullptr;
       const float* xn2 = h16 ? ctx->km_xn2 : nullptr;
       OH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(sk), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)lds2));
+                                 (int)lds2m));
       // one resident block per CU (the kernel's registers allow one 8-wave block): one round of blocks,
       // so each block's LDS set-up and sum flush happen once
       const unsigned sgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(ntile, smt / 64), ctx->n_cu));
@@ -1219,11 +1657,29 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
                   "median %.4g, p10 %.4g, cmax %.4g)\n", ne, (long long)n, bounds, dh[64], dh[65], ds[k / 2],
                   ds[k / 10], dh[67]);
         }
-        sk<<<(unsigned)ctx->n_cu, smt, lds2, s>>>(X, n, dim, C, cn, k, labels, sums, cnt, changed, gate, amb, n_amb,
-                                                  erows, n_eval, ub, lb, x16, xn2);
+        if (mv) {  // a block's region holds every row it can score: its tiles' share of ceil(n / 32)
+          const int64_t wpb = smt / 64, nwv = (int64_t)ctx->n_cu * wpb;
+          mv_cap = (uint32_t)(ceil_div(ceil_div(n, 32), nwv) * wpb * 32);
+          OH_TRY(ctx->ws.get("km_mv", (size_t)ctx->n_cu * mv_cap, &mv_list));
+          OH_TRY(ctx->ws.get("km_mvc", (size_t)ctx->n_cu, &mv_cnt));
+        }
+        const char* s16e = getenv("OTTOHIP_KM_S16");  // A/B switch, read per call
+        if (mv && !(s16e && !strcmp(s16e, "0"))) {
+          auto s16 = KS == 7 ? (NB == 1 ? k_km_split16<1, 7> : k_km_split16<2, 7>)
+                             : (NB == 1 ? k_km_split16<1, 8> : k_km_split16<2, 8>);
+          const size_t lds16 = (size_t)NB * KS * 2 * 64 * 16 + 64 * 4 + (size_t)KMH_AMB * 4;
+          OH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(s16), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds16));
+          s16<<<(unsigned)ctx->n_cu, KMH_MT, lds16, s>>>(n, dim, C, cn, k, labels, changed, gate, amb, n_amb, erows,
+                                                         n_eval, ub, lb, x16, reinterpret_cast<const float2*>(xn2),
+                                                         mv_list, mv_cnt, mv_cap);
+        } else {
+          sk<<<(unsigned)ctx->n_cu, smt, lds2m, s>>>(X, n, dim, C, cn, k, labels, sums, cnt, changed, gate, amb, n_amb,
+                                                     erows, n_eval, ub, lb, x16, xn2, mv_list, mv_cnt, mv_cap);
+        }
       } else {
         sk<<<sgrid, smt, lds2, s>>>(X, n, dim, C, cn, k, labels, sums, cnt, changed, gate, amb, n_amb, nullptr, nullptr,
-                                     nullptr, nullptr, x16, xn2);
+                                     nullptr, nullptr, x16, xn2, nullptr, nullptr, 0);
       }
       OH_HIP(hipGetLastError());
     }
@@ -1239,6 +1695,26 @@ static int launch_km_assign(Ctx* ctx, int k, hipStream_t s, const float* X, int6
     const char* ege = getenv("OTTOHIP_KM_EGRID");
     const int eg_env = ege ? atoi(ege) : 0;
     const unsigned egrid = split ? (unsigned)std::max(1, eg_env > 0 ? eg_env : (h16 ? ctx->n_cu : ctx->n_cu / 2)) : grid;
+    if (mv) {
+      auto tk = nq == 13 ? (NB == 1 ? k_km_ties<1, 13> : k_km_ties<2, 13>)
+                         : (NB == 1 ? k_km_ties<1, KM_NQ> : k_km_ties<2, KM_NQ>);
+      OH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(tk), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      tk<<<egrid, KM_MT, lds, s>>>(X, dim, nq, C, cn, k, labels, sums, cnt, inr, changed, gate, amb, n_amb, mv_list,
+                                   mv_cnt, mv_cap, ctx->n_cu);
+      OH_HIP(hipGetLastError());
+      static const bool bdbg = getenv("OTTOHIP_KM_BDBG") != nullptr;  // near ties and split-pass moves per step
+      if (bdbg) {
+        unsigned long long na = 0;
+        std::vector<uint32_t> mc(ctx->n_cu);
+        OH_TRY(d2h(&na, n_amb, 1, s));
+        OH_TRY(d2h(mc.data(), mv_cnt, (size_t)ctx->n_cu, s));
+        uint64_t nm = 0, mx = 0;
+        for (uint32_t v : mc) { nm += v; mx = std::max<uint64_t>(mx, v); }
+        fprintf(stderr, "[ottohip] kmeans step: %llu near ties, %llu split-pass moves (max %llu per block)\n", na,
+                (unsigned long long)nm, (unsigned long long)mx);
+      }
+      return 0;
+    }
     kern<<<egrid, KM_MT, lds, s>>>(X, n, dim, nq, C, cn, k, labels, sums, cnt, inr, changed, dist, inc, gate,
                                    amb, n_amb);
     OH_HIP(hipGetLastError());
@@ -1841,11 +2317,14 @@ int ottohip_kmeans_attach_half(ottohip_ctx* ctx, const float* X, int64_t n, int 
   }
   hipStream_t s = S(stream);
   OH_HIP(hipSetDevice(ctx->device));
-  const int kc = 2 * (dim <= 112 ? 7 : 8);  // 16-B chunks per row: the split kernel's 2 KS pieces
+  // 16-B chunks per row (8 dims each; the last one zero padded past dim), one pad chunk after the last row:
+  // k_km_split16 reads a row's KS chunk pairs unconditionally and masks the one past the row
+  const int kc = (dim + 7) / 8;
   uint4* x16;
   float* xn2;
-  OH_TRY(ctx->ws.get("km_x16", (size_t)n * kc, &x16));
-  OH_TRY(ctx->ws.get("km_xn2", (size_t)n, &xn2));
+  OH_TRY(ctx->ws.get("km_x16", (size_t)n * kc + 1, &x16));
+  OH_HIP(hipMemsetAsync(x16 + (size_t)n * kc, 0, sizeof(uint4), s));
+  OH_TRY(ctx->ws.get("km_xn2", (size_t)n * 2, &xn2));  // {|x|^2, |x - xh|} per row
   unsigned* amax;
   OH_TRY(ctx->ws.get("km_amax", 1, &amax));
   ctx->km_hX = nullptr;  // no half copy is attached unless this one is accepted

@@ -133,8 +133,11 @@ def test_kmeans_split_precision_steps_equal_exact_steps(gpu, monkeypatch, case):
         n_init = 3
     fits = []
     monkeypatch.setenv("OTTOHIP_KM_GROUP", "1")  # the single-run steps (lockstep groups always take the split pass)
-    for split in ("0", "1"):  # the exact kernel on every row; the split pass + the exact kernel on near ties
+    # the exact kernel on every row; the split pass + the exact kernel on near ties, the label changes through
+    # the move lists (k_km_ties) and through the split pass's own LDS sums (OTTOHIP_KM_MV=0)
+    for split, mv in (("0", "1"), ("1", "1"), ("1", "0")):
         monkeypatch.setenv("OTTOHIP_KM_SPLIT", split)
+        monkeypatch.setenv("OTTOHIP_KM_MV", mv)
         km = gp.KMeans(n_clusters=k, random_state=42, n_init=n_init).fit(X)
         fits.append((km.labels_.cpu().numpy(), km.cluster_centers_.cpu().numpy(), km.inertia_, km.n_iter_))
     for f in fits[1:]:
