@@ -135,6 +135,10 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
     n_tr_sessions = ev_tr.n_sessions
     del ev_tr, ev_te, allev
     t = mark("upload", t)
+    # C2's n_init seed draws (numpy's permutation heads over all sessions) start now, on a host thread, and are
+    # ready when the clustering begins
+    km_model = gp.KMeans(n_clusters=n_clusters, max_iter=kmeans_iter, n_init=n_init)
+    km_seeds = gp.SeedHeads(km_model.random_state, train.n_sessions + test.n_sessions, n_clusters, km_model.n_init)
     folders = [(dev_all.subset_files(0, n_tr_files), my_tr, len(fb_tr) - 1),
                (dev_all.subset_files(n_tr_files, len(fb) - 1), my_te, len(fb_te) - 1)]
     merged = {n: [] for n in config.CO_EVENTS_TO_COUNT}
@@ -177,8 +181,7 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
     grows = np.concatenate([np.concatenate([np.arange(fb_tr[f], fb_tr[f + 1]) for f in my_tr] or [np.zeros(0)]),
                             train.n_sessions + np.concatenate([np.arange(fb_te[f], fb_te[f + 1]) for f in my_te]
                                                               or [np.zeros(0)])]).astype(np.int64)
-    km = gp.KMeans(n_clusters=n_clusters, max_iter=kmeans_iter, n_init=n_init).fit(se, ctx, group=group,
-                                                                                  global_rows=grows)
+    km = km_model.fit(se, ctx, group=group, global_rows=grows, seed_heads=km_seeds)
     labels_all = km.labels_
     t = mark("C2_kmeans", t)
     pop50 = gp.count_popularity(dev_all.offsets, dev_all.aid, dev_all.ts, dev_all.type, labels_all, n_clusters,

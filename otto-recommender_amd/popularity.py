@@ -69,32 +69,53 @@ def _allreduce(t, group):
     return _allreduce_sum(t, group)
 
 
-def _permutation_heads(seed: int, n: int, k: int, runs: int):
+class SeedHeads:
     """numpy RandomState(seed).permutation(n)[:k] for `runs` successive calls (sklearn 1.2's
     KMeans(init='random') seeds of its n_init runs), by the library's MT19937 replica
-    (ottohip_rs_permutation_head). The next run's draw is computed in a worker thread (ctypes
-    releases the GIL) while the current run iterates on the GPU."""
-    from concurrent.futures import ThreadPoolExecutor
-    lib = _lib.load()
-    h = ctypes.c_void_p()
-    _lib.check(lib.ottohip_rs_create(int(seed) & 0xFFFFFFFF, ctypes.byref(h)))
+    (ottohip_rs_permutation_head). All `runs` heads are drawn in order by a background thread from
+    construction on (ctypes releases the GIL): built before the stages that precede C2 (pipeline.run),
+    the ~0.1-0.3 s of draws for n ~ 13 M no longer sit in front of the first Lloyd step. Iterating
+    yields the heads in run order (blocking until each is drawn)."""
 
-    def draw():
-        out = np.empty(k, np.int64)
-        _lib.check(lib.ottohip_rs_permutation_head(h, int(n), int(k), out.ctypes.data))
-        return out
+    def __init__(self, seed: int, n: int, k: int, runs: int):
+        import queue
+        import threading
+        self.key = (int(seed), int(n), int(k), int(runs))
+        self._q = queue.Queue()
+        self._t = threading.Thread(target=self._work, daemon=True)
+        self._t.start()
 
-    ex = ThreadPoolExecutor(1)
-    try:
-        fut = ex.submit(draw)
-        for r in range(runs):
-            cur = fut.result()
-            if r + 1 < runs:
-                fut = ex.submit(draw)
-            yield cur
-    finally:
-        ex.shutdown(wait=True)
-        lib.ottohip_rs_destroy(h)
+    def _work(self):
+        seed, n, k, runs = self.key
+        lib = _lib.load()
+        h = ctypes.c_void_p()
+        try:
+            _lib.check(lib.ottohip_rs_create(seed & 0xFFFFFFFF, ctypes.byref(h)))
+            for _ in range(runs):
+                out = np.empty(k, np.int64)
+                _lib.check(lib.ottohip_rs_permutation_head(h, n, k, out.ctypes.data))
+                self._q.put(out)
+        except BaseException as e:  # re-raised in the consumer
+            self._q.put(e)
+        finally:
+            if h:
+                lib.ottohip_rs_destroy(h)
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        item = self._q.get()
+        if isinstance(item, BaseException):
+            raise item
+        return item
+
+    def close(self):
+        self._t.join()
+
+
+def _permutation_heads(seed: int, n: int, k: int, runs: int) -> SeedHeads:
+    return SeedHeads(seed, n, k, runs)
 
 
 class KMeans:
@@ -123,7 +144,9 @@ class KMeans:
         self.init = init
         self.n_init = 10 if n_init == "auto" else int(n_init)
 
-    def fit(self, X, ctx=None, stream=None, group=None, global_rows=None):
+    def fit(self, X, ctx=None, stream=None, group=None, global_rows=None, seed_heads=None):
+        """seed_heads: a SeedHeads(random_state, n_samples, n_clusters, n_init) started earlier (the same draws,
+        computed ahead); one with another key is not used."""
         import torch
         ctx = ctx or _lib.context()
         dev = torch.device("cuda", ctx.device)
@@ -156,7 +179,9 @@ class KMeans:
         m1 = s1.cpu().numpy().astype(np.float64) / FX / n_all
         var = s2.cpu().numpy().astype(np.float64) / FX / n_all - m1 * m1
         tol_abs = float(np.mean(var)) * self.tol
-        seed_stream = _permutation_heads(self.random_state, n_all, k, self.n_init)
+        key = (int(self.random_state), int(n_all), int(k), int(self.n_init))
+        seed_stream = seed_heads if seed_heads is not None and seed_heads.key == key else \
+            _permutation_heads(self.random_state, n_all, k, self.n_init)
         # one GPU: the E-steps read f16 copies of the centred rows (exact f32 scoring of the near ties keeps the
         # f32 labels); every fit attaches its own Xc, so a reused allocation never meets a stale copy
         half = group is None and dim % 4 == 0 and os.environ.get("OTTOHIP_KM_H16", "1") != "0"
