@@ -221,6 +221,55 @@ struct MergedLists {
 
 __device__ __forceinline__ uint32_t cs_hash(uint32_t x, uint32_t mask) { return (x * 0x9E3779B1u >> 9) & mask; }
 
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+  return ((uint64_t)hi << 32) | lo;
+}
+// Ascending bitonic sort of a wave's 64 R keys in registers: lane l holds positions l R .. l R + R - 1 (keys
+// past n read as ~0). Stages whose partner lies in another lane exchange through __shfl_xor; the last log2 R
+// stages of every merge are in-register compare-exchanges. Then the first n sorted keys go to out(p, key).
+template <int R, class OUT>
+__device__ __forceinline__ void wave_sort_u64(const uint64_t* __restrict__ SK, int n, OUT out) {
+  const int l = (int)lane_id();
+  uint64_t v[R];
+#pragma unroll
+  for (int q = 0; q < R; ++q) v[q] = l * R + q < n ? SK[l * R + q] : ~0ull;
+#pragma unroll 1
+  for (int k = 2; k <= 64 * R; k <<= 1) {
+#pragma unroll 1
+    for (int j = k >> 1; j >= R; j >>= 1) {  // partner lane l ^ (j / R), same slot
+      const int lj = j / R;
+      const bool lower = (l & lj) == 0;
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        const uint64_t w = shfl_xor_u64(v[q], lj);
+        const bool up = ((l * R + q) & k) == 0;
+        const bool mn = lower == up;  // this position keeps the smaller key
+        const bool lt = w < v[q];
+        v[q] = (lt == mn) ? w : v[q];
+      }
+    }
+#pragma unroll
+    for (int j = R / 2; j >= 1; j >>= 1) {  // partner slot q ^ j in this lane
+      if (j <= (k >> 1)) {
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+          if ((q & j) == 0) {
+            const bool up = ((l * R + q) & k) == 0;
+            const uint64_t a = v[q], b = v[q | j];
+            const bool sw = (a > b) == up;
+            v[q] = sw ? b : a;
+            v[q | j] = sw ? a : b;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < R; ++q)
+    if (l * R + q < n) out(l * R + q, v[q]);
+}
+
 // one wave per session (WAVES sessions per block); pass 0 counts, pass 1 writes at cand_off
 template <int HC, int WAVES>
 __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __restrict__ off,
@@ -240,7 +289,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
   __shared__ uint64_t hkm64[WAVES][HC];  // keys [0, HC) and masks [HC, 2 HC) as u32; sort keys (OVL)
   __shared__ uint32_t ho[WAVES][HC];
   __shared__ uint64_t sk[OVL ? 1 : WAVES][OVL ? 1 : HC];
-  __shared__ uint32_t pre[WAVES][65], ka[WAVES][64], ki[WAVES][64], kl[WAVES][64];
+  __shared__ uint32_t flg[WAVES][64];  // chunk tags of the kept aids' first elements
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int64_t gi = (int64_t)blockIdx.x * WAVES + w;
   if (gi >= n_sess) return;
@@ -248,8 +297,9 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
   uint32_t* K = reinterpret_cast<uint32_t*>(hkm64[w]);
   uint32_t* Mk = K + HC;
   uint32_t* Ord = ho[w];
-  uint32_t* PRE = pre[w];
   for (int i = l; i < HC; i += 64) { K[i] = CS_EMPTY; Mk[i] = 0; Ord[i] = 0xFFFFFFFFu; }
+  flg[w][l] = 0u;
+  uint32_t tag = 0;
   __builtin_amdgcn_wave_barrier();
   bool full = false;
   auto insert = [&](uint32_t x, uint32_t bits, uint32_t ord) {
@@ -276,44 +326,45 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
       cnt += 1;  // the self pair (aid, aid)
     }
     const uint32_t incl = wave_incl_scan(cnt);
-    PRE[l + 1] = incl;
-    if (l == 0) PRE[0] = 0;
-    ka[w][l] = (uint32_t)r.aid;  // read back by the lanes that expand this aid's entries
-    ki[w][l] = r.info;
-    kl[w][l] = lo;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const uint32_t start = incl - cnt;  // the lane's first element
+    const uint32_t aid_l = (uint32_t)r.aid, info_l = r.info;
     const uint32_t T = (dbg & 4) ? 0u : __shfl(incl, 63);
-    // element e -> (owner kept aid, its info, list entry); the next element's global loads are
-    // issued before the current one is inserted (the loop is latency-bound)
-    auto fetch = [&](uint32_t e, uint32_t& a, uint32_t& info, uint32_t& j, uint32_t& x, uint32_t& br) {
-      uint32_t lo_k = 0, hi_k = kb;  // owner: largest k with PRE[k] <= e
-      while (hi_k - lo_k > 1) {
-        const uint32_t m = (lo_k + hi_k) >> 1;
-        if (PRE[m] <= e) lo_k = m; else hi_k = m;
-      }
-      const int kk = (int)lo_k;
-      a = ka[w][kk];
-      info = ki[w][kk];
-      j = e - PRE[kk];
+    // the elements of chunk [c0, c0 + 64), one per lane: the owner of element c0 + l is the kept aid of the
+    // last start at or before it: the chunk's first owner (starts <= c0) plus the starts in (c0, c0 + l],
+    // found by a ballot over the chunk's start flags (a fresh tag per chunk: no clearing). The next chunk's
+    // global loads are issued before the current one is inserted (the loop is latency-bound).
+    auto fetch = [&](uint32_t c0, uint32_t& a, uint32_t& info, uint32_t& j, uint32_t& x, uint32_t& br) {
+      ++tag;
+      if ((uint32_t)l < kb && start > c0 && start < c0 + 64) flg[w][start - c0] = tag;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      const uint64_t M = __ballot(flg[w][l] == tag);
+      const uint32_t kb0 = (uint32_t)__popcll(__ballot((uint32_t)l < kb && start <= c0)) - 1u;
+      const uint32_t own = kb0 + (uint32_t)mbcnt(M) + (uint32_t)((M >> l) & 1ull);
+      a = (uint32_t)__shfl((int)aid_l, (int)own);
+      info = (uint32_t)__shfl((int)info_l, (int)own);
+      const uint32_t st = (uint32_t)__shfl((int)start, (int)own), lo_o = (uint32_t)__shfl((int)lo, (int)own);
+      const uint32_t e = c0 + (uint32_t)l;
+      j = e - st;
       x = a; br = 0;
-      if (j > 0) {
-        const uint32_t base = kl[w][kk];
-        x = (uint32_t)L.mx[base + j - 1];
-        br = L.mbr[base + j - 1];
+      if (e < T && j > 0) {
+        x = (uint32_t)L.mx[lo_o + j - 1];
+        br = L.mbr[lo_o + j - 1];
       }
     };
     uint32_t a0 = 0, i0 = 0, j0 = 0, x0 = 0, b0 = 0;
-    if ((uint32_t)l < T) fetch(l, a0, i0, j0, x0, b0);
-    for (uint32_t e = l; e < T; e += 64) {
+    if (T > 0) fetch(0u, a0, i0, j0, x0, b0);
+    for (uint32_t c0 = 0; c0 < T; c0 += 64) {
       uint32_t a1 = 0, i1 = 0, j1 = 0, x1 = 0, b1 = 0;
-      if (e + 64 < T) fetch(e + 64, a1, i1, j1, x1, b1);
-      const uint32_t ord = i0 & 0xFFFFu, tm = (i0 >> 16) & 7u, th = i0 >> 19;
-      if (j0 == 0) {
-        insert(a0, 1u | (tm << 8), ord);
-      } else if (x0 == a0 || (b0 & 0xFFu) <= th) {
-        // R5 (:512-516) pair kept iff aid_next == aid or its best co-count / w2v rank <= th
-        insert(x0, (b0 >> 8) | (x0 == a0 ? 1u : 0u) | (tm << 8), ord);
+      if (c0 + 64 < T) fetch(c0 + 64, a1, i1, j1, x1, b1);
+      if (c0 + (uint32_t)l < T) {
+        const uint32_t ord = i0 & 0xFFFFu, tm = (i0 >> 16) & 7u, th = i0 >> 19;
+        if (j0 == 0) {
+          insert(a0, 1u | (tm << 8), ord);
+        } else if (x0 == a0 || (b0 & 0xFFu) <= th) {
+          // R5 (:512-516) pair kept iff aid_next == aid or its best co-count / w2v rank <= th
+          insert(x0, (b0 >> 8) | (x0 == a0 ? 1u : 0u) | (tm << 8), ord);
+        }
       }
       a0 = a1; i0 = i1; j0 = j1; x0 = x1; b0 = b1;
     }
@@ -387,6 +438,23 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
     if (l == 0) n_cand[s] = (uint32_t)cnt;
     return;
   }
+  const uint64_t o = cand_off[s] & ~CS_OVF_BIT;
+  if (l == 0) n_cand[s] = (uint32_t)cnt;
+  auto emit = [&](int i, uint64_t v) __attribute__((always_inline)) {
+    o_next[o + i] = (int32_t)(uint32_t)(v >> 16);
+    o_ord[o + i] = (int16_t)(v >> 48);
+    o_flags[o + i] = (uint16_t)(v & 0x1FFu);
+  };
+  if (!(dbg & 1) && cnt <= 64 * 16) {  // in registers: 64 R >= cnt keys
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (cnt <= 64) wave_sort_u64<1>(SK, cnt, emit);
+    else if (cnt <= 128) wave_sort_u64<2>(SK, cnt, emit);
+    else if (cnt <= 256) wave_sort_u64<4>(SK, cnt, emit);
+    else if (cnt <= 512) wave_sort_u64<8>(SK, cnt, emit);
+    else wave_sort_u64<16>(SK, cnt, emit);
+    return;
+  }
   int P2 = 1;
   while (P2 < cnt) P2 <<= 1;
   if (dbg & 1) P2 = 1;  // (profiling) skip the sort
@@ -407,14 +475,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
   }
-  const uint64_t o = cand_off[s] & ~CS_OVF_BIT;
-  if (l == 0) n_cand[s] = (uint32_t)cnt;
-  for (int i = l; i < cnt; i += 64) {
-    const uint64_t v = SK[i];
-    o_next[o + i] = (int32_t)(uint32_t)(v >> 16);
-    o_ord[o + i] = (int16_t)(v >> 48);
-    o_flags[o + i] = (uint16_t)(v & 0x1FFu);
-  }
+  for (int i = l; i < cnt; i += 64) emit(i, SK[i]);
 }
 
 // Single-pass layout: an upper bound of every session's candidates (its kept aids' merged-list

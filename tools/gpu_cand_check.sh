@@ -3,7 +3,7 @@
 set -o pipefail
 O=gpurun_out/${1:-candcheck}; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread tests/test_popularity_gpu.py > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread ${TESTS:-tests/test_popularity_gpu.py} > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 for run in 1 2; do
   timeout -k 10 400 python3 -u bench.py --no-cpu --no-a6 --no-ingest --steps 1 --warmup 0 --knn-steps 0 > "$O/c_$run.log" 2>&1 || { tail -20 "$O/c_$run.log"; exit 1; }
