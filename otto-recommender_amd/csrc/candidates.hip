@@ -136,14 +136,21 @@ __global__ __launch_bounds__(64) void k_cand_aids(const int64_t* __restrict__ of
 
 // Per-aid union of the 7 source lists (SURVEY.md §8(a) R4-R5 are pair-level: a pair (aid, aid_next)
 // carries every source that lists it and is kept if its best rank passes). One wave per aid:
-// elements (x, source bit, rank) of all lists in LDS, duplicates of x folded (OR of bits, min rank),
-// unique entries written at the aid's element offset; ucnt[a] = number of unique entries.
+// elements (x, source bit, rank) of all lists in LDS, duplicates of x folded (OR of bits, min rank).
+// A kept aid's trim threshold th is at most 31 (5 bits) and R5 keeps an entry iff x == aid or its rank
+// <= th, so the unique entries are written ordered by that test: the self entry (x == aid) first, then by
+// rank 0..31 (entries ranked above 31 can never be kept and are dropped); ucnt[a] = entries written and
+// pc[a][th] = the entries a kept aid with threshold th takes (a prefix of the list): k_cand_build scans
+// only those instead of every entry (the long sessions' lists were mostly entries above their th).
 constexpr int ML_MAX = 256;  // elements per aid across the 7 lists
+constexpr int ML_TH = 32;    // trim thresholds 0..31
 __global__ __launch_bounds__(256) void k_ml_build(CandLists L, const uint32_t* __restrict__ eoff,
                                                   int32_t* __restrict__ mx, uint16_t* __restrict__ mbr,
-                                                  uint32_t* __restrict__ ucnt, int* __restrict__ err) {
+                                                  uint32_t* __restrict__ ucnt, uint16_t* __restrict__ pc,
+                                                  int* __restrict__ err) {
   __shared__ uint32_t ex[4][ML_MAX];
-  __shared__ uint16_t eb[4][ML_MAX];
+  __shared__ uint16_t eb[4][ML_MAX], uk[4][ML_MAX];
+  __shared__ uint32_t hs[4][ML_TH + 1];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int64_t a = (int64_t)blockIdx.x * 4 + w;
   if (a >= L.n_items) return;
@@ -153,7 +160,12 @@ __global__ __launch_bounds__(256) void k_ml_build(CandLists L, const uint32_t* _
     if (L.off[q]) { beg[q] = L.off[q][a]; len[q] = L.off[q][a + 1] - beg[q]; } else { beg[q] = 0; len[q] = 0; }
     tot += len[q];
   }
-  if (tot > ML_MAX) { if (l == 0) { atomicOr(err, 4); ucnt[a] = 0; } return; }
+  if (tot > ML_MAX) {
+    if (l == 0) { atomicOr(err, 4); ucnt[a] = 0; }
+    if (l < ML_TH) pc[a * ML_TH + l] = 0;
+    return;
+  }
+  if (l <= ML_TH) hs[w][l] = 0;
   for (uint32_t e = l; e < tot; e += 64) {
     uint32_t j = e;
     int q = 0;
@@ -173,29 +185,47 @@ __global__ __launch_bounds__(256) void k_ml_build(CandLists L, const uint32_t* _
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const uint32_t o = eoff[a];
-  uint32_t base = 0;
+  // unique entries (the first occurrence of each x) with their folded bits and rank, counted per bucket
+  // (0: x == aid, 1 + r: rank r <= 31); the others marked 0xFFFF
   for (uint32_t e0 = 0; e0 < tot; e0 += 64) {
     const uint32_t e = e0 + l;
-    bool first = e < tot;
-    uint32_t bits = 0, rk = 255;
-    if (first) {
+    if (e < tot) {
       const uint32_t x = ex[w][e];
+      bool first = true;
+      uint32_t bits = 0, rk = 255;
       for (uint32_t f = 0; f < tot; ++f) {
         if (ex[w][f] != x) continue;
         if (f < e) { first = false; break; }
         bits |= eb[w][f] >> 8;
         rk = min(rk, (uint32_t)(eb[w][f] & 0xFFu));
       }
+      const int key = x == (uint32_t)a ? 0 : (rk < (uint32_t)ML_TH ? 1 + (int)rk : -1);
+      uk[w][e] = first && key >= 0 ? (uint16_t)(bits << 8 | rk) : (uint16_t)0xFFFFu;
+      if (first && key >= 0) atomicAdd(&hs[w][key], 1u);
     }
-    const uint64_t b = __ballot(first);
-    if (first) {
-      const uint32_t k = base + (uint32_t)mbcnt(b);
-      mx[o + k] = (int32_t)ex[w][e];
-      mbr[o + k] = (uint16_t)(bits << 8 | rk);
-    }
-    base += (uint32_t)__popcll(b);
   }
-  if (l == 0) ucnt[a] = base;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const uint32_t c = l <= ML_TH ? hs[w][l] : 0u;
+  const uint32_t incl = wave_incl_scan(c);
+  if (l >= 1 && l <= ML_TH) pc[a * ML_TH + l - 1] = (uint16_t)incl;  // entries of the self bucket and ranks <= l - 1
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  if (l <= ML_TH) hs[w][l] = incl - c;  // bucket starts
+  if (l == ML_TH) ucnt[a] = incl;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  for (uint32_t e0 = 0; e0 < tot; e0 += 64) {
+    const uint32_t e = e0 + l;
+    const uint16_t v = e < tot ? uk[w][e] : (uint16_t)0xFFFFu;
+    if (v != 0xFFFFu) {
+      const uint32_t x = ex[w][e];
+      const int key = x == (uint32_t)a ? 0 : 1 + (int)(v & 0xFFu);
+      const uint32_t p = atomicAdd(&hs[w][key], 1u);  // order within a bucket: any (the folds commute)
+      mx[o + p] = (int32_t)x;
+      mbr[o + p] = v;
+    }
+  }
 }
 
 __global__ void k_ml_total(CandLists L, uint32_t* __restrict__ tot) {
@@ -210,7 +240,8 @@ __global__ void k_ml_total(CandLists L, uint32_t* __restrict__ tot) {
 
 struct MergedLists {
   const uint32_t* eoff;   // [n_items] element offset of the aid
-  const uint32_t* ucnt;   // [n_items] unique entries
+  const uint32_t* ucnt;   // [n_items] entries kept in the list (self entry, ranks <= 31)
+  const uint16_t* pc;     // [n_items][32] entries a kept aid with trim threshold th takes
   const int32_t* mx;
   const uint16_t* mbr;    // source bits << 8 | min rank
   int32_t n_items;
@@ -322,7 +353,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
     r.aid = 0; r.info = 0;
     if ((uint32_t)l < kb) {
       r = kept[e0 + k0 + l];
-      if (r.aid < L.n_items) { lo = L.eoff[r.aid]; cnt = L.ucnt[r.aid]; }
+      if (r.aid < L.n_items) { lo = L.eoff[r.aid]; cnt = L.pc[(int64_t)r.aid * ML_TH + (r.info >> 19)]; }
       cnt += 1;  // the self pair (aid, aid)
     }
     const uint32_t incl = wave_incl_scan(cnt);
@@ -448,11 +479,14 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
   if (!(dbg & 1) && cnt <= 64 * 16) {  // in registers: 64 R >= cnt keys
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // (cnt <= HC: a table's tier bounds the register count)
     if (cnt <= 64) wave_sort_u64<1>(SK, cnt, emit);
     else if (cnt <= 128) wave_sort_u64<2>(SK, cnt, emit);
-    else if (cnt <= 256) wave_sort_u64<4>(SK, cnt, emit);
-    else if (cnt <= 512) wave_sort_u64<8>(SK, cnt, emit);
-    else wave_sort_u64<16>(SK, cnt, emit);
+    else if (HC <= 256 || cnt <= 256) wave_sort_u64<4>(SK, cnt, emit);
+    else if constexpr (HC >= 512) {
+      if (HC <= 512 || cnt <= 512) wave_sort_u64<8>(SK, cnt, emit);
+      else if constexpr (HC >= 1024) wave_sort_u64<16>(SK, cnt, emit);
+    }
     return;
   }
   int P2 = 1;
@@ -491,8 +525,8 @@ __global__ void k_cand_bound(const int64_t* __restrict__ off, int64_t S, const K
   const uint32_t nk = n_kept[s];
   uint64_t t = 0;
   for (uint32_t k = 0; k < nk && t < cap; ++k) {
-    const int32_t a = kept[e0 + k].aid;
-    t += 1u + (a < L.n_items ? L.ucnt[a] : 0u);
+    const KeptAid r = kept[e0 + k];
+    t += 1u + (r.aid < L.n_items ? L.pc[(int64_t)r.aid * ML_TH + (r.info >> 19)] : 0u);
   }
   const int32_t c = session_cl ? session_cl[s] : -1;
   if (c >= 0 && c < L.n_clusters) t += L.pop_off[c + 1] - L.pop_off[c];
@@ -522,6 +556,27 @@ __global__ __launch_bounds__(256) void k_cand_compact(const uint64_t* __restrict
     o_ord[d0 + i] = xo[b + i];
     o_flags[d0 + i] = xf[b + i];
   }
+}
+
+// sessions by their candidate bound (tables at a load <= 3/4): tier 0 (ub <= 192: 256-slot tables), tier 1
+// (<= 384: 512 slots), tier 2 (the rest: 1024 slots, then the overflow tier); lists[t * S ..] and cnt3[t]
+__global__ __launch_bounds__(256) void k_cand_tier(const uint32_t* __restrict__ ub, int64_t S, int64_t* __restrict__ lists,
+                                                   uint32_t* __restrict__ cnt3) {
+  __shared__ uint32_t c[3], b[3];
+  if (threadIdx.x < 3) c[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  int t = -1;
+  uint32_t p = 0;
+  if (s < S) {
+    const uint32_t u = ub[s];
+    t = u <= 192 ? 0 : (u <= 384 ? 1 : 2);
+    p = atomicAdd(&c[t], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) b[threadIdx.x] = c[threadIdx.x] ? atomicAdd(&cnt3[threadIdx.x], c[threadIdx.x]) : 0u;
+  __syncthreads();
+  if (t >= 0) lists[t * S + b[t] + p] = s;
 }
 
 __global__ void k_cand_ovf_src(const int32_t* __restrict__ ovf_sess, int64_t n, uint32_t cap,
@@ -827,13 +882,14 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
   M.pop_off = L.pop_off; M.pop_aid = L.pop_aid; M.n_clusters = L.n_clusters;
   {
     uint32_t *tot_e, *ucnt, *eoff32;
+    uint16_t* pc;
     uint64_t *eoff, *etot;
     int32_t* mx;
     uint16_t* mbr;
     const int64_t NI = std::max<int32_t>(L.n_items, 1);
     if ((rc = ws.get("ml_tot", (size_t)NI + 1, &tot_e)) || (rc = ws.get("ml_eoff", (size_t)NI + 1, &eoff)) ||
         (rc = ws.get("ml_eoff32", (size_t)NI + 1, &eoff32)) || (rc = ws.get("ml_ucnt", (size_t)NI, &ucnt)) ||
-        (rc = ws.get("ml_etot", 1, &etot)))
+        (rc = ws.get("ml_etot", 1, &etot)) || (rc = ws.get("ml_pc", (size_t)NI * ML_TH, &pc)))
       return fail(rc);
     int ph0 = ctx->begin("cand_merge_lists", s, 0);
     hipMemsetAsync(tot_e + NI, 0, 4, s);
@@ -846,9 +902,9 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
         (rc = ws.get("ml_br", (size_t)std::max<uint64_t>(ne, 1), &mbr)))
       return fail(rc);
     k_u64_to_u32<<<grid_for(NI + 1), 256, 0, s>>>(eoff, NI + 1, eoff32);
-    k_ml_build<<<(unsigned)ceil_div(NI, 4), 256, 0, s>>>(L, eoff32, mx, mbr, ucnt, err);
+    k_ml_build<<<(unsigned)ceil_div(NI, 4), 256, 0, s>>>(L, eoff32, mx, mbr, ucnt, pc, err);
     ctx->end(ph0, s);
-    M.eoff = eoff32; M.ucnt = ucnt; M.mx = mx; M.mbr = mbr;
+    M.eoff = eoff32; M.ucnt = ucnt; M.pc = pc; M.mx = mx; M.mbr = mbr;
   }
   int ph = ctx->begin("cand_aids", s, 9.0 * E);
   hipMemsetAsync(n_ovf, 0, sizeof(uint32_t), s);
@@ -874,9 +930,34 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
   if ((rc = ws.get("cs_pool_next", pcap, &p_next)) || (rc = ws.get("cs_pool_ord", pcap, &p_ord)) ||
       (rc = ws.get("cs_pool_flags", pcap, &p_flags)))
     return fail(rc);
-  k_cand_build<HC1, W><<<(unsigned)ceil_div(Sn, W), 64 * W, 0, s>>>(session_offsets, nullptr, Sn, kept, n_kept,
-                                                                     session_cl, M, 1, n_cand, pool_off, p_next, p_ord,
-                                                                     p_flags, ovf, n_ovf, dbg);
+  // tables sized by the session's bound (OTTOHIP_CAND_TIER=0: every session in a 1024-slot table first): the
+  // smaller tables hold more waves per CU (69 % of the config-5 sessions have a bound <= 256, 8 % above 1024)
+  static const bool tiers = !(getenv("OTTOHIP_CAND_TIER") && !strcmp(getenv("OTTOHIP_CAND_TIER"), "0"));
+  if (tiers) {
+    int64_t* tl;
+    uint32_t* tc;
+    if ((rc = ws.get("cs_tier", (size_t)Sn * 3, &tl)) || (rc = ws.get("cs_tierc", 3, &tc))) return fail(rc);
+    OH_HIP(hipMemsetAsync(tc, 0, 3 * sizeof(uint32_t), s));
+    k_cand_tier<<<(unsigned)ceil_div(Sn, 256), 256, 0, s>>>(ub, Sn, tl, tc);
+    uint32_t h3[3];
+    if ((rc = d2h(h3, tc, 3, s))) return fail(rc);
+    if (h3[0])
+      k_cand_build<256, 4><<<(unsigned)ceil_div((int64_t)h3[0], 4), 256, 0, s>>>(
+          session_offsets, tl, h3[0], kept, n_kept, session_cl, M, 1, n_cand, pool_off, p_next, p_ord, p_flags, ovf,
+          n_ovf, dbg);
+    if (h3[1])
+      k_cand_build<512, 2><<<(unsigned)ceil_div((int64_t)h3[1], 2), 128, 0, s>>>(
+          session_offsets, tl + Sn, h3[1], kept, n_kept, session_cl, M, 1, n_cand, pool_off, p_next, p_ord, p_flags,
+          ovf, n_ovf, dbg);
+    if (h3[2])
+      k_cand_build<HC1, W><<<(unsigned)ceil_div((int64_t)h3[2], W), 64 * W, 0, s>>>(
+          session_offsets, tl + 2 * Sn, h3[2], kept, n_kept, session_cl, M, 1, n_cand, pool_off, p_next, p_ord,
+          p_flags, ovf, n_ovf, dbg);
+  } else {
+    k_cand_build<HC1, W><<<(unsigned)ceil_div(Sn, W), 64 * W, 0, s>>>(session_offsets, nullptr, Sn, kept, n_kept,
+                                                                       session_cl, M, 1, n_cand, pool_off, p_next, p_ord,
+                                                                       p_flags, ovf, n_ovf, dbg);
+  }
   uint32_t novf = 0;
   int herr = 0;
   if ((rc = d2h(&novf, n_ovf, 1, s)) || (rc = d2h(&herr, err, 1, s))) return fail(rc);
@@ -906,6 +987,31 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
     uint32_t novf2 = 0;
     if ((rc = d2h(&novf2, n_ovf2, 1, s))) return fail(rc);
     if (novf2) { set_error("candidates_generate: %u sessions exceed 4096 candidates", novf2); return fail(OTTOHIP_ELIMIT); }
+  }
+  if (dbg & 8) {  // (profiling) per-session candidate count distribution, then the uncapped bound's, then both
+    std::vector<uint32_t> hc(Sn), hb(Sn);
+    if ((rc = d2h(hc.data(), n_cand, (size_t)Sn, s))) return fail(rc);
+    k_cand_bound<<<grid_for(Sn), 256, 0, s>>>(session_offsets, Sn, kept, n_kept, session_cl, M, 1u << 30, ub);
+    if ((rc = d2h(hb.data(), ub, (size_t)Sn, s))) return fail(rc);
+    int64_t jb[4][4] = {};
+    auto bin4 = [](uint32_t v) { return v <= 256 ? 0 : v <= 512 ? 1 : v <= 1024 ? 2 : 3; };
+    int64_t sb[6] = {0, 0, 0, 0, 0, 0};
+    for (int64_t i = 0; i < Sn; ++i) {
+      const uint32_t v = hb[i];
+      sb[v <= 128 ? 0 : v <= 256 ? 1 : v <= 384 ? 2 : v <= 512 ? 3 : v <= 1024 ? 4 : 5]++;
+      jb[bin4(v)][bin4(hc[i])]++;
+    }
+    fprintf(stderr, "[ottohip] candidate bound per session: <=128 %lld, <=256 %lld, <=384 %lld, <=512 %lld, <=1024 %lld, "
+            "more %lld\n", (long long)sb[0], (long long)sb[1], (long long)sb[2], (long long)sb[3], (long long)sb[4],
+            (long long)sb[5]);
+    for (int a = 0; a < 4; ++a)
+      fprintf(stderr, "[ottohip] bound bin %d -> count bins %lld %lld %lld %lld\n", a, (long long)jb[a][0],
+              (long long)jb[a][1], (long long)jb[a][2], (long long)jb[a][3]);
+    int64_t nb[6] = {0, 0, 0, 0, 0, 0};
+    for (uint32_t v : hc) nb[v <= 128 ? 0 : v <= 256 ? 1 : v <= 384 ? 2 : v <= 512 ? 3 : v <= 1024 ? 4 : 5]++;
+    fprintf(stderr, "[ottohip] candidates per session: <=128 %lld, <=256 %lld, <=384 %lld, <=512 %lld, <=1024 %lld, "
+            "more %lld\n", (long long)nb[0], (long long)nb[1], (long long)nb[2], (long long)nb[3], (long long)nb[4],
+            (long long)nb[5]);
   }
   if ((rc = exclusive_scan_u32(ctx, n_cand, C->off, Sn + 1, tot, s))) return fail(rc);
   uint64_t nc = 0;

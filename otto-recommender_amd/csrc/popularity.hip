@@ -934,8 +934,12 @@ __global__ __launch_bounds__(H16 ? KMH_MT : KM_MT, H16 ? 1 : 2) void k_km_assign
 //   decision threshold (KMH_SEP_C) and the rebuilt bounds (KMH_ERR_C16));
 // - largest and second largest acc by a max / med3 chain (2 ops per score), then the lowest cluster holding
 //   the largest (the approximate argmin only labels rows whose gap is above the threshold, where it is unique).
-constexpr float KMH_SEP_C = 5.8e-5f;    // cmax^2 units (2x margin)
-constexpr float KMH_ERR_C16 = 2.5e-5f;  // cmax^2 units: chain rounding of |c|^2 / 2 and |c|^2's own (1.2x margin)
+// the cluster bits in the 6 low mantissa bits (k_km_split16) move a value by < 64 ulp = 7.63e-6 |acc|, |acc| <=
+// |x| cmax + cmax^2 / 2: a score gap by <= 3.05e-5 |x| cmax + 1.53e-5 cmax^2 (2x margin below), a score by half
+constexpr float KMH_SEP_X16 = 1.76e-4f + 6.1e-5f;  // |x| cmax units (2x margin)
+constexpr float KMH_SEP_C = 5.8e-5f + 3.1e-5f;     // cmax^2 units (2x margin)
+constexpr float KMH_ERR_X16 = 3.5e-5f + 1.9e-5f;   // |x| cmax units (1.2x margin)
+constexpr float KMH_ERR_C16 = 2.5e-5f + 9.2e-6f;   // cmax^2 units: chain rounding of |c|^2 / 2, |c|^2's own, cluster bits
 template <int NB, int KS>
 __global__ __launch_bounds__(KMH_MT, 1) void k_km_split16(int64_t n, int dim, const float* __restrict__ C,
                                                           const float* __restrict__ cn, int k,
@@ -970,7 +974,8 @@ __global__ __launch_bounds__(KMH_MT, 1) void k_km_split16(int64_t n, int dim, co
     Cf[(sb * 2 + 0) * 64 + ll] = hi;
     Cf[(sb * 2 + 1) * 64 + ll] = lo;
   }
-  if (tid < 64) cnl[tid] = -0.5f * cn[tid];  // padding clusters: cn = inf, so acc = -inf
+  // padding clusters: -FLT_MAX (finite, so the cluster bits below keep it a number, and never the largest)
+  if (tid < 64) cnl[tid] = tid < k ? -0.5f * cn[tid] : -3.402823466e38f;
   if (tid == 0) { namb = 0; nmv = 0; }
   __syncthreads();
   float c2 = l < k ? cn[l] : 0.f;
@@ -1030,6 +1035,16 @@ __global__ __launch_bounds__(KMH_MT, 1) void k_km_split16(int64_t n, int dim, co
     }
     // +inf the compiler cannot see as a constant: med3(a, b, +inf) would fold to a max that canonicalizes its
     // operands (one more instruction per score)
+    // each value carries its cluster in the 6 low mantissa bits (within 63 ulp: 7.6e-6 |acc|, in the
+    // thresholds), so the largest value names its cluster: no compare / select scan for the argmax
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const uint32_t c0 = (uint32_t)((r & 3) + 8 * (r >> 2) + 4 * h);
+      acc0[r] = __uint_as_float((__float_as_uint(acc0[r]) & ~63u) | c0);
+      if (NB == 2) acc1[r] = __uint_as_float((__float_as_uint(acc1[r]) & ~63u) | (c0 + 32u));
+    }
+    // +inf the compiler cannot see as a constant: med3(a, b, +inf) would fold to a max that canonicalizes its
+    // operands (one more instruction per score)
     const float pinf = __uint_as_float(0x7F800000u | ((uint32_t)k >> 31));
     float a1 = -INFINITY, a2 = -INFINITY;  // largest, second largest (a tie at the top: a2 == a1)
 #pragma unroll
@@ -1046,19 +1061,13 @@ __global__ __launch_bounds__(KMH_MT, 1) void k_km_split16(int64_t n, int dim, co
       a2 = fmaxf(fminf(a1, p1), fmaxf(a2, p2));
       a1 = fmaxf(a1, p1);
     }
-    int mc = 64;
-#pragma unroll
-    for (int r = 15; r >= 0; --r)
-      if (NB == 2) mc = acc1[r] == a1 ? 32 + (r & 3) + 8 * (r >> 2) + 4 * h : mc;
-#pragma unroll
-    for (int r = 15; r >= 0; --r) mc = acc0[r] == a1 ? (r & 3) + 8 * (r >> 2) + 4 * h : mc;
-    mc = min(mc, __shfl_xor(mc, 32));
+    const int mc = (int)(__float_as_uint(a1) & 63u);
     const float xs = ne.x, ee = ne.y, xn = sqrtf(xs);
     const float m = -2.f * a1, m2 = -2.f * a2;  // the two smallest approximate scores |c|^2 - 2 x.c
-    const bool decided = m2 - m > (KMH_SEP_E * ee + KMH_SEP_X * xn + KMH_SEP_C * cmax) * cmax + KMH_ABS * (xn + cmax);
+    const bool decided = m2 - m > (KMH_SEP_E * ee + KMH_SEP_X16 * xn + KMH_SEP_C * cmax) * cmax + KMH_ABS * (xn + cmax);
     if (h == 0 && in_r) {  // the row's bounds for these centres (near ties: none, lb = 0)
       const float cm = cmax * 1.000001f;
-      const float e = (KMH_ERR_E * ee + KMH_ERR_X * xn * 1.0001f + KMH_ERR_C16 * cm) * cm + KMH_ABS * (xn + cm);
+      const float e = (KMH_ERR_E * ee + KMH_ERR_X16 * xn * 1.0001f + KMH_ERR_C16 * cm) * cm + KMH_ABS * (xn + cm);
       ub[row] = decided ? sqrtf(fmaxf(m + xs * 1.00001f + e, 0.f)) * 1.000001f : 0.f;
       lb[row] = decided ? sqrtf(fmaxf(m2 + xs * 0.99999f - e, 0.f)) * 0.999999f : 0.f;
     }
