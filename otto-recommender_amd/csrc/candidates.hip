@@ -476,16 +476,22 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
     o_ord[o + i] = (int16_t)(v >> 48);
     o_flags[o + i] = (uint16_t)(v & 0x1FFu);
   };
-  if (!(dbg & 1) && cnt <= 64 * 16) {  // in registers: 64 R >= cnt keys
+  constexpr int RMAX = HC / 64 < 64 ? HC / 64 : 64;
+  if (!(dbg & 1) && cnt <= 64 * RMAX) {  // in registers: 64 R >= cnt keys (cnt <= HC bounds R by the tier)
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    // (cnt <= HC: a table's tier bounds the register count)
     if (cnt <= 64) wave_sort_u64<1>(SK, cnt, emit);
     else if (cnt <= 128) wave_sort_u64<2>(SK, cnt, emit);
     else if (HC <= 256 || cnt <= 256) wave_sort_u64<4>(SK, cnt, emit);
     else if constexpr (HC >= 512) {
       if (HC <= 512 || cnt <= 512) wave_sort_u64<8>(SK, cnt, emit);
-      else if constexpr (HC >= 1024) wave_sort_u64<16>(SK, cnt, emit);
+      else if constexpr (HC >= 1024) {
+        if (HC <= 1024 || cnt <= 1024) wave_sort_u64<16>(SK, cnt, emit);
+        else if constexpr (HC >= 2048) {
+          if (HC <= 2048 || cnt <= 2048) wave_sort_u64<32>(SK, cnt, emit);
+          else if constexpr (HC >= 4096) wave_sort_u64<64>(SK, cnt, emit);
+        }
+      }
     }
     return;
   }
@@ -518,19 +524,22 @@ __global__ __launch_bounds__(64 * WAVES) void k_cand_build(const int64_t* __rest
 // count, and a compaction copies the regions into the session-ordered CSR (no count pass).
 __global__ void k_cand_bound(const int64_t* __restrict__ off, int64_t S, const KeptAid* __restrict__ kept,
                              const uint32_t* __restrict__ n_kept, const int32_t* __restrict__ session_cl,
-                             MergedLists L, uint32_t cap, uint32_t* __restrict__ ub) {
+                             MergedLists L, uint32_t cap, uint32_t* __restrict__ ub,
+                             uint32_t* __restrict__ ubx = nullptr, uint32_t capx = 0) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= S) return;
   const int64_t e0 = off[s];
   const uint32_t nk = n_kept[s];
   uint64_t t = 0;
-  for (uint32_t k = 0; k < nk && t < cap; ++k) {
+  const uint32_t cm = ubx ? capx : cap;  // ubx: the bound capped at capx (tier routing), ub at cap (pool regions)
+  for (uint32_t k = 0; k < nk && t < cm; ++k) {
     const KeptAid r = kept[e0 + k];
     t += 1u + (r.aid < L.n_items ? L.pc[(int64_t)r.aid * ML_TH + (r.info >> 19)] : 0u);
   }
   const int32_t c = session_cl ? session_cl[s] : -1;
   if (c >= 0 && c < L.n_clusters) t += L.pop_off[c + 1] - L.pop_off[c];
   ub[s] = (uint32_t)(t < cap ? t : cap);
+  if (ubx) ubx[s] = (uint32_t)(t < capx ? t : capx);
 }
 
 // one wave per session: pool region [src_off, + n) -> CSR [dst_off, + n)
@@ -559,9 +568,11 @@ __global__ __launch_bounds__(256) void k_cand_compact(const uint64_t* __restrict
 }
 
 // sessions by their candidate bound (tables at a load <= 3/4): tier 0 (ub <= 192: 256-slot tables), tier 1
-// (<= 384: 512 slots), tier 2 (the rest: 1024 slots, then the overflow tier); lists[t * S ..] and cnt3[t]
+// (<= 384: 512 slots), tier 2 (<= 1536: 1024 slots, then the overflow tier); lists[t * S ..] and cnt3[t]. A
+// bound above 1536 goes straight to the overflow list (on config 5 every such session holds > 1024 candidates)
 __global__ __launch_bounds__(256) void k_cand_tier(const uint32_t* __restrict__ ub, int64_t S, int64_t* __restrict__ lists,
-                                                   uint32_t* __restrict__ cnt3) {
+                                                   uint32_t* __restrict__ cnt3, int32_t* __restrict__ ovf,
+                                                   uint32_t* __restrict__ n_ovf) {
   __shared__ uint32_t c[3], b[3];
   if (threadIdx.x < 3) c[threadIdx.x] = 0;
   __syncthreads();
@@ -571,7 +582,9 @@ __global__ __launch_bounds__(256) void k_cand_tier(const uint32_t* __restrict__ 
   if (s < S) {
     const uint32_t u = ub[s];
     t = u <= 192 ? 0 : (u <= 384 ? 1 : 2);
-    p = atomicAdd(&c[t], 1u);
+    if (u > 1536) ovf[atomicAdd(n_ovf, 1u)] = (int32_t)s;
+    else p = atomicAdd(&c[t], 1u);
+    if (u > 1536) t = -1;
   }
   __syncthreads();
   if (threadIdx.x < 3) b[threadIdx.x] = c[threadIdx.x] ? atomicAdd(&cnt3[threadIdx.x], c[threadIdx.x]) : 0u;
@@ -919,7 +932,10 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
   if ((rc = ws.get("cs_ub", (size_t)Sn, &ub)) || (rc = ws.get("cs_pool_off", (size_t)Sn + 1, &pool_off)) ||
       (rc = ws.get("cs_ptot", 1, &ptot)))
     return fail(rc);
-  k_cand_bound<<<grid_for(Sn), 256, 0, s>>>(session_offsets, Sn, kept, n_kept, session_cl, M, (uint32_t)HC1, ub);
+  uint32_t* ubx;
+  if ((rc = ws.get("cs_ubx", (size_t)Sn, &ubx))) return fail(rc);
+  k_cand_bound<<<grid_for(Sn), 256, 0, s>>>(session_offsets, Sn, kept, n_kept, session_cl, M, (uint32_t)HC1, ub, ubx,
+                                             (uint32_t)HC2);
   if ((rc = exclusive_scan_u32(ctx, ub, pool_off, Sn, ptot, s))) return fail(rc);
   uint64_t npool = 0;
   if ((rc = d2h(&npool, ptot, 1, s))) return fail(rc);
@@ -938,7 +954,7 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
     uint32_t* tc;
     if ((rc = ws.get("cs_tier", (size_t)Sn * 3, &tl)) || (rc = ws.get("cs_tierc", 3, &tc))) return fail(rc);
     OH_HIP(hipMemsetAsync(tc, 0, 3 * sizeof(uint32_t), s));
-    k_cand_tier<<<(unsigned)ceil_div(Sn, 256), 256, 0, s>>>(ub, Sn, tl, tc);
+    k_cand_tier<<<(unsigned)ceil_div(Sn, 256), 256, 0, s>>>(ubx, Sn, tl, tc, ovf, n_ovf);
     uint32_t h3[3];
     if ((rc = d2h(h3, tc, 3, s))) return fail(rc);
     if (h3[0])
@@ -993,18 +1009,19 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
     if ((rc = d2h(hc.data(), n_cand, (size_t)Sn, s))) return fail(rc);
     k_cand_bound<<<grid_for(Sn), 256, 0, s>>>(session_offsets, Sn, kept, n_kept, session_cl, M, 1u << 30, ub);
     if ((rc = d2h(hb.data(), ub, (size_t)Sn, s))) return fail(rc);
-    int64_t jb[4][4] = {};
+    int64_t jb[6][4] = {};
     auto bin4 = [](uint32_t v) { return v <= 256 ? 0 : v <= 512 ? 1 : v <= 1024 ? 2 : 3; };
+    auto bin6 = [](uint32_t v) { return v <= 256 ? 0 : v <= 512 ? 1 : v <= 1024 ? 2 : v <= 1536 ? 3 : v <= 2048 ? 4 : 5; };
     int64_t sb[6] = {0, 0, 0, 0, 0, 0};
     for (int64_t i = 0; i < Sn; ++i) {
       const uint32_t v = hb[i];
       sb[v <= 128 ? 0 : v <= 256 ? 1 : v <= 384 ? 2 : v <= 512 ? 3 : v <= 1024 ? 4 : 5]++;
-      jb[bin4(v)][bin4(hc[i])]++;
+      jb[bin6(v)][bin4(hc[i])]++;
     }
     fprintf(stderr, "[ottohip] candidate bound per session: <=128 %lld, <=256 %lld, <=384 %lld, <=512 %lld, <=1024 %lld, "
             "more %lld\n", (long long)sb[0], (long long)sb[1], (long long)sb[2], (long long)sb[3], (long long)sb[4],
             (long long)sb[5]);
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < 6; ++a)
       fprintf(stderr, "[ottohip] bound bin %d -> count bins %lld %lld %lld %lld\n", a, (long long)jb[a][0],
               (long long)jb[a][1], (long long)jb[a][2], (long long)jb[a][3]);
     int64_t nb[6] = {0, 0, 0, 0, 0, 0};
