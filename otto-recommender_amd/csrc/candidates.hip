@@ -626,16 +626,23 @@ __global__ __launch_bounds__(64) void k_cand_recall(const uint64_t* __restrict__
   __syncthreads();
   for (int t = 0; t < 3; ++t) {
     const int64_t lb = lab_off[t * (S + 1) + s], le = lab_off[t * (S + 1) + s + 1];
+    // one label at a time, the wave's lanes over the candidates (a label is at most once in the session's
+    // deduplicated list; one lane per label scanning the list serially was latency-bound: 42 ms per step)
     uint32_t h20 = 0, h100 = 0, h200 = 0, hall = 0, tru = 0;
-    for (int64_t j = lb + l; j < le; j += 64) {
+    for (int64_t j = lb; j < le; ++j) {
       const int32_t y = lab_aid[j];
       int r = 0;
-      for (int i = 0; i < n; ++i)
-        if (cnext[c0 + i] == y) { r = frank[i]; break; }
+      for (int i0 = 0; i0 < n; i0 += 64) {
+        const int i = i0 + l;
+        const uint64_t b = __ballot(i < n && cnext[c0 + i] == y);
+        if (b) {
+          r = frank[i0 + __builtin_ctzll(b)];
+          break;
+        }
+      }
       tru += 1;
       if (r > 0) { hall += 1; h20 += r <= 20; h100 += r <= 100; h200 += r <= 200; }
     }
-    h20 = wave_sum(h20); h100 = wave_sum(h100); h200 = wave_sum(h200); hall = wave_sum(hall); tru = wave_sum(tru);
     if (l == 0 && tru) {
       const uint32_t K = (uint32_t)max_k;
       unsigned long long* o = sums + (size_t)(s & 255) * 16 + t * 5;  // striped: 256 copies of [3][5]
