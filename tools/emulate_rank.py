@@ -4,7 +4,9 @@ Rank `--rank` of `--world` gets its balanced whole files of the 220M-event strea
 them, packs rows by owner and merge-sums ALL of its packed records as if they were the
 records it receives (same volume in expectation: owner(aid) is a uniform hash). Prints per
 phase device times (HIP events): the per-rank compute of the N-GPU step, without the
-all-to-all itself."""
+all-to-all itself. --sym 1 (default): the symmetric rules travel once per unordered pair, as
+dist.count_co_events_sharded sends them; the exchange is modelled as max(sent, received remote bytes)
+over 7 xGMI links at 153 GB/s each (and at half that rate)."""
 import argparse
 import json
 import os
@@ -22,6 +24,7 @@ def main():
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--events", type=int, default=220_000_000)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--sym", type=int, default=1)
     args = ap.parse_args()
     import torch
     import otto_recommender_amd.synth as synth
@@ -50,7 +53,7 @@ def main():
         ctx.set_timing(True)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        w, wpp, pc, ppp, names = gd.emit_for_owners(dev, G, mine, n_files, ctx=ctx)
+        w, wpp, pc, ppp, names = gd.emit_for_owners(dev, G, mine, n_files, ctx=ctx, sym=bool(args.sym))
         torch.cuda.synchronize()
         t_emit = time.perf_counter() - t0
         own_wpp, own_ppp = list(wpp), list(ppp)  # this rank's send segments (words, pieces) per owner
@@ -70,7 +73,7 @@ def main():
     del full
     devf = gc.DeviceEvents.from_host(evf, fb_all)
     del evf
-    w, wpp, pc, ppp, names = gd.emit_for_owners(devf, G, None, n_files, ctx=ctx)
+    w, wpp, pc, ppp, names = gd.emit_for_owners(devf, G, None, n_files, ctx=ctx, sym=bool(args.sym))
     del devf
     o = args.rank
     ws = w[sum(wpp[:o]):sum(wpp[:o + 1])].clone()
@@ -81,17 +84,24 @@ def main():
         ctx.set_timing(True)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        shard = gd.reduce_received(ws, ps, names, n_files, ctx=ctx)
+        shard = gd.reduce_received(ws, ps, names, n_files, ctx=ctx, sym=bool(args.sym))
         torch.cuda.synchronize()
         t_red = time.perf_counter() - t0
         ph_red = ctx.timings()
         ctx.set_timing(False)
         rows = sum(shard.stats(n)["n_rows"] for n in names)
         shard.free()
-    res = {"world": G, "rank": args.rank, "files": len(mine), "events": int(ev.n_events),
+    # received from the other ranks: owner o's segment of every file minus its own files' (uniform hash: the
+    # own files' share of the segment is their share of the sent words)
+    send_remote = 4 * int(sum(own_wpp) - own_wpp[args.rank]) + 8 * int(sum(own_ppp) - own_ppp[args.rank])
+    recv_remote = 4 * int(ws.numel() - own_wpp[args.rank]) + 8 * int(ps.numel() - own_ppp[args.rank])
+    link = 7 * 153e9
+    res = {"world": G, "rank": args.rank, "sym": args.sym, "files": len(mine), "events": int(ev.n_events),
            "send_words": int(sum(own_wpp)), "recv_words": int(ws.numel()), "recv_pieces": int(ps.numel()),
            "shard_rows": int(rows), "emit_s": t_emit, "reduce_received_s": t_red,
-           "send_bytes_remote": 4 * int(sum(own_wpp) - own_wpp[args.rank]) + 8 * int(sum(own_ppp) - own_ppp[args.rank]),
+           "send_bytes_remote": send_remote, "recv_bytes_remote": recv_remote,
+           "xgmi_ms_peak": round(max(send_remote, recv_remote) / link * 1e3, 3),
+           "xgmi_ms_half": round(2 * max(send_remote, recv_remote) / link * 1e3, 3),
            "phases_ms": {n: round(ms, 3) for n, ms, _ in ph_emit + ph_red}}
     print(json.dumps(res))
 
