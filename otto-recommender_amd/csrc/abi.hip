@@ -389,8 +389,15 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
         uint32_t* posA = poss == pos ? pos2 : pos;
         k_rows_tile<<<(unsigned)nb, RT_T, 0, s>>>(rks, poss, F.cnt, E, kmask, INV, cshift, boff, nullptr, F.poff32, 0u,
                                                   0xFFFFFFFFu, 1, F.row_key, F.row_begin, rkA);
-        OH_TRY(radix_pass(ctx, poss, rkA, posA, rks, E, std::max(0, bits_for((uint64_t)E) - 8), s));
-        k_poff_scatter<<<grid_for(E), 256, 0, s>>>(posA, rks, E, F.poff32);
+        const uint64_t* dstart = nullptr;
+        int ntl = 0;
+        OH_TRY(radix_pass(ctx, poss, rkA, posA, rks, E, std::max(0, bits_for((uint64_t)E) - 8), s, &dstart, &ntl));
+        // OTTOHIP_POFF_XCD=1: the XCD-aware scatter (A/B switch, off: 6.47 vs 6.85 GB written per build, slower)
+        static const bool pxcd = getenv("OTTOHIP_POFF_XCD") && !strcmp(getenv("OTTOHIP_POFF_XCD"), "1");
+        if (pxcd)
+          k_poff_scatter_xcd<<<(unsigned)(8 * std::max(1, ctx->n_cu)), 256, 0, s>>>(posA, rks, E, dstart, ntl, F.poff32);
+        else
+          k_poff_scatter<<<grid_for(E), 256, 0, s>>>(posA, rks, E, F.poff32);
       } else {
         k_rows_tile<<<(unsigned)nb, RT_T, 0, s>>>(rks, poss, F.cnt, E, kmask, INV, cshift, boff, nullptr, F.poff32, 0u,
                                                   0xFFFFFFFFu, 1, F.row_key, F.row_begin);

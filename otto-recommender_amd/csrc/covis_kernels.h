@@ -718,6 +718,24 @@ __global__ void k_poff_scatter(const uint32_t* __restrict__ pos, const uint32_t*
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k < n) poff32[pos[k]] = woff[k];
 }
+// XCD-aware form: block b runs on XCD b % 8 (workgroups are dealt round robin) and XCD x writes only the
+// slices (position high-bit digits) d = x (mod 8), one after the other, its blocks splitting each slice: a
+// destination line is written through ONE L2, where its 4-B writes merge before the line goes to HBM (from
+// eight XCDs a line went out in parts: 6.85 GB written per build for 0.88 GB of offsets). dstart[d * ntiles]
+// = the first element of slice d (radix_pass' offsets); gridDim.x % 8 == 0.
+__global__ __launch_bounds__(256) void k_poff_scatter_xcd(const uint32_t* __restrict__ pos,
+                                                          const uint32_t* __restrict__ woff, int64_t n,
+                                                          const uint64_t* __restrict__ dstart, int ntiles,
+                                                          uint32_t* __restrict__ poff32) {
+  const int x = blockIdx.x & 7, j = blockIdx.x >> 3, nj = gridDim.x >> 3;
+  for (int d = x; d < 256; d += 8) {
+    const int64_t a = (int64_t)dstart[(int64_t)d * ntiles];
+    const int64_t b = d + 1 < 256 ? (int64_t)dstart[(int64_t)(d + 1) * ntiles] : n;
+    const int64_t per = (b - a + nj - 1) / nj;
+    const int64_t s0 = a + (int64_t)j * per, s1 = s0 + per < b ? s0 + per : b;
+    for (int64_t k = s0 + threadIdx.x; k < s1; k += 256) poff32[pos[k]] = woff[k];
+  }
+}
 
 // ---- rows without a sort (OTTOHIP_ROWS=atomic, one GPU): the row of key k is the dense index k of
 // (type << A | aid); its words are cut into RA_SUB sub-ranges, one per counter, so the atomics of a hot

@@ -15,5 +15,5 @@ int radix_sort_pairs(Ctx* ctx, uint32_t*& keys, uint32_t*& vals, uint32_t* keys_
                      int64_t n, int bits, hipStream_t s, bool iota_vals = false);
 // one stable 8-bit pass on digit (key >> shift) & 255
 int radix_pass(Ctx* ctx, const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout, int64_t n,
-               int shift, hipStream_t s);
+               int shift, hipStream_t s, const uint64_t** digit_start = nullptr, int* n_tiles = nullptr);
 }  // namespace ottohip
