@@ -2857,47 +2857,29 @@ __global__ __launch_bounds__(256) void k_rule_hist(const uint8_t* __restrict__ r
   __syncthreads();
   // 16 consecutive slots per thread; runs of equal rule bytes among them (the common case: one row's slots)
   // take one pair of LDS atomics
-  // (the lanes' last runs are summed per wave, one distinct rule byte at a time, before the LDS atomics: a
-  // part-mode table's neighbouring slots mostly hold one part, and 64 lanes adding to one LDS counter
-  // serialised: 83 % of the kernel's LDS cycles were same-address conflicts)
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * SLOTS_T;
-  const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * SLOTS_T;
-  const int l = (int)(threadIdx.x & 63);
-  for (int64_t ib = i0 - l * SLOTS_T; ib < n; ib += stride) {  // wave-uniform trip count
-    const int64_t i = ib + l * SLOTS_T;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * SLOTS_T; i < n; i += stride) {
+    const uint4 R = ld_rule16(rule, i, n);
+    uint32_t live = 0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) live |= (u4_at(R, g) != 0xFFFFFFFFu ? 15u : 0u) << (4 * g);
+    if (!live) continue;
+    uint4 C[4];
+    ld_groups(count, i, n, live, C);
     uint32_t cur = 0xFFu, nr = 0;
     unsigned long long np = 0;
-    if (i < n) {
-      const uint4 R = ld_rule16(rule, i, n);
-      uint32_t live = 0;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) live |= (u4_at(R, g) != 0xFFFFFFFFu ? 15u : 0u) << (4 * g);
-      if (live) {
-        uint4 C[4];
-        ld_groups(count, i, n, live, C);
-#pragma unroll
-        for (int s = 0; s < SLOTS_T; ++s) {
-          const uint32_t r = rule_at(R, s);
-          if (r == 0xFFu) continue;
-          if (r != cur) {
-            if (cur != 0xFFu) { atomicAdd(&hr[cur], (unsigned long long)nr); atomicAdd(&hp[cur], np); }
-            cur = r; nr = 0; np = 0;
-          }
-          ++nr;
-          np += u4_at(C[s >> 2], s & 3);
-        }
+    for (int s = 0; s < SLOTS_T; ++s) {
+      const uint32_t r = rule_at(R, s);
+      if (r == 0xFFu) continue;
+      if (r != cur) {
+        if (cur != 0xFFu) { atomicAdd(&hr[cur], (unsigned long long)nr); atomicAdd(&hp[cur], np); }
+        cur = r; nr = 0; np = 0;
       }
+      ++nr;
+      np += u4_at(C[s >> 2], s & 3);
     }
-    uint64_t pend = __ballot(cur != 0xFFu);
-    while (pend) {
-      const int lead = __builtin_ctzll(pend);
-      const uint32_t p = (uint32_t)__shfl((int)cur, lead);
-      const bool mine = cur == p && ((pend >> l) & 1ull);
-      const uint32_t sr = wave_sum(mine ? nr : 0u);
-      const unsigned long long sp = wave_sum64(mine ? np : 0ull);
-      if (l == lead) { atomicAdd(&hr[p], (unsigned long long)sr); atomicAdd(&hp[p], sp); }
-      pend &= ~__ballot(mine);
-    }
+    if (cur != 0xFFu) { atomicAdd(&hr[cur], (unsigned long long)nr); atomicAdd(&hp[cur], np); }
   }
   __syncthreads();
   if (hr[threadIdx.x]) { atomicAdd(&rows[threadIdx.x], hr[threadIdx.x]); atomicAdd(&pairs[threadIdx.x], hp[threadIdx.x]); }
