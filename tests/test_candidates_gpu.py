@@ -120,6 +120,44 @@ def test_candidates_edge_sessions(gpu):
         np.testing.assert_array_equal(got[col].to_numpy().astype(np.int64), ref[col].to_numpy().astype(np.int64))
 
 
+def _tier_fixture(seed=5):
+    """sessions of 30, 12, 9, 7, 4, 2 and 1 distinct aids, every aid with 20-entry lists in all seven sources:
+    3205, 1559, 1212, 931, 564, 282 and 141 candidates (oracle), so the build's table tiers are all taken --
+    bound <= 192 (256 slots), <= 384 (512), <= 1536 (1024 slots; a session above 1024 candidates overflows to
+    the 4096-slot tier) and > 1536 (straight to the 4096-slot tier), register sorts of 1 to 64 keys per lane"""
+    rng = np.random.default_rng(seed)
+    rows = []
+    for s, na in ((10, 30), (11, 12), (12, 9), (13, 7), (14, 4), (15, 2), (16, 1)):
+        aids = rng.choice(100000, na, replace=False) + 1000
+        for i, a in enumerate(aids):
+            rows.append((s, int(a), 1000 + 60 * i, int(rng.integers(0, 3))))
+    df = pd.DataFrame(rows, columns=["session", "aid", "ts", "type"])
+    uni = np.unique(df.aid)
+
+    def lists(col, dt):
+        a = np.repeat(uni, 20)
+        b = rng.integers(0, 1855603, len(a))
+        rk = np.tile(np.arange(1, 21), len(uni))
+        return pd.DataFrame({"aid": a.astype(np.int32), "aid_next": b.astype(np.int32),
+                             col: rk.astype(dt)}).drop_duplicates(["aid", "aid_next"])
+    r1 = {n: lists(f"{n}_rank", np.int16) for n in RULES}
+    return df, r1, lists("rank_w2vec_all", np.int8), lists("rank_w2vec_1_2", np.int8)
+
+
+def test_candidates_table_tiers(gpu):
+    from otto_recommender_amd import candidates as gcand
+    df, r1, ka, k12 = _tier_fixture()
+    ref = oracle_retrieve.candidates(df, r1, ka.rename(columns={"rank_w2vec_all": "rank"}),
+                                     k12.rename(columns={"rank_w2vec_1_2": "rank"}))
+    sizes = ref.groupby("session").size().to_numpy()
+    assert sizes.max() > 3000 and ((sizes > 1024) & (sizes < 1536)).any() and (sizes < 192).any()
+    got = gcand.retrieve_candidates(df, r1, ka, k12)
+    assert len(got) == len(ref)
+    for col in ["session", "aid_next", "ts_order_aid"] + gcand.SRC_NAMES:
+        np.testing.assert_array_equal(got[col].to_numpy().astype(np.int64), ref[col].to_numpy().astype(np.int64),
+                                      err_msg=col)
+
+
 def test_candidates_written_in_retrieved_schema(gpu, tmp_path):
     """retrieve_candidates(..., file_out) writes the retrieved file of model/retrieve.py:651-655: rows
     sorted by (session, ts_order_aid), columns session:int32, aid_next:int32, ts_order_aid:int16,
