@@ -23,6 +23,29 @@ void set_error(const char* fmt, ...) {
 namespace ottohip {
 Ctx* ctx_base(ottohip_ctx* c) { return c; }
 
+int ensure_part_stats(const ottohip_table* tc) {
+  if (!tc || !tc->part_stats_pending) return 0;
+  ottohip_table* T = const_cast<ottohip_table*>(tc);
+  Ctx* ctx = T->ctx;
+  const hipStream_t s = nullptr;  // the null stream: ordered after the table's producer on any stream
+  OH_HIP(hipSetDevice(T->device));
+  unsigned long long* ph;
+  OH_TRY(ctx->ws.get("part_hist", 512, &ph));
+  OH_HIP(hipMemsetAsync(ph, 0, 512 * 8, s));
+  k_rule_hist<<<(unsigned)std::min<int64_t>(ceil_div((int64_t)T->n_slots, 256 * SLOTS_T), (int64_t)ctx->n_cu * 8), 256,
+                0, s>>>(T->b.rule, T->b.count, T->n_slots, ph, ph + 256);
+  OH_HIP(hipGetLastError());
+  std::vector<unsigned long long> hh(512);
+  OH_TRY(d2h(hh.data(), ph, hh.size(), s));
+  for (int p = 0; p < T->part_stats_pending; ++p) {
+    T->stats[p].n_rows = (int64_t)hh[p];
+    T->stats[p].n_pairs = (int64_t)hh[256 + p];
+  }
+  T->part_stats_pending = 0;
+  return 0;
+}
+
+
 static bool alloc_log_on() {
   static const bool on = getenv("OTTOHIP_ALLOC_LOG") != nullptr;
   return on;
@@ -1093,19 +1116,10 @@ int ottohip_table_count_parts(ottohip_ctx* ctx, const ottohip_table* t, int rule
   T->sym_mask = 0;  // explicit rows (the mirrors written by the leaves)
   T->aid_ordered = fo.mirror_off == 0;
   T->n_rules = po->n_parts;
-  unsigned long long* ph;
-  if ((rc = ws.get("part_hist", 512, &ph))) return fail(rc);
-  OH_HIP(hipMemsetAsync(ph, 0, 512 * 8, s));
-  k_rule_hist<<<(unsigned)std::min<int64_t>(ceil_div((int64_t)T->n_slots, 256 * SLOTS_T), (int64_t)ctx->n_cu * 8), 256, 0, s>>>(
-      T->b.rule, T->b.count, T->n_slots, ph, ph + 256);
-  OH_HIP(hipGetLastError());
-  std::vector<unsigned long long> hh(512);
-  if ((rc = d2h(hh.data(), ph, hh.size(), s))) return fail(rc);
-  for (int p = 0; p < po->n_parts; ++p) {
-    T->stats[p] = ottohip_rule_stats{};
-    T->stats[p].n_rows = (int64_t)hh[p];
-    T->stats[p].n_pairs = (int64_t)hh[256 + p];
-  }
+  // per part: rows and pairs, counted when first read (ottohip_table_stats / _copy / _finalize): the part heads
+  // (ottohip_table_part_heads) do not need them, and the table scan took 4.3 ms per A6 of click_to_click
+  for (int p = 0; p < po->n_parts; ++p) T->stats[p] = ottohip_rule_stats{};
+  T->part_stats_pending = po->n_parts;
   *out = T;
   return 0;
 }
@@ -1173,19 +1187,10 @@ int ottohip_covis_count_parts(ottohip_ctx* ctx, const ottohip_events* ev, const 
     return fail(rc);
   // per part: rows and pairs (file statistics stay 0: the part-wise finalize is told which column to use)
   T->n_rules = po->n_parts;
-  unsigned long long* ph;
-  if ((rc = ctx->ws.get("part_hist", 512, &ph))) return fail(rc);
-  OH_HIP(hipMemsetAsync(ph, 0, 512 * 8, s));
-  k_rule_hist<<<(unsigned)std::min<int64_t>(ceil_div((int64_t)T->n_slots, 256 * SLOTS_T), (int64_t)ctx->n_cu * 8), 256, 0, s>>>(
-      T->b.rule, T->b.count, T->n_slots, ph, ph + 256);
-  OH_HIP(hipGetLastError());
-  std::vector<unsigned long long> hh(512);
-  if ((rc = d2h(hh.data(), ph, hh.size(), s))) return fail(rc);
-  for (int p = 0; p < po->n_parts; ++p) {
-    T->stats[p] = ottohip_rule_stats{};
-    T->stats[p].n_rows = (int64_t)hh[p];
-    T->stats[p].n_pairs = (int64_t)hh[256 + p];
-  }
+  // per part: rows and pairs, counted when first read (ottohip_table_stats / _copy / _finalize): the part heads
+  // (ottohip_table_part_heads) do not need them, and the table scan took 4.3 ms per A6 of click_to_click
+  for (int p = 0; p < po->n_parts; ++p) T->stats[p] = ottohip_rule_stats{};
+  T->part_stats_pending = po->n_parts;
   *out = T;
   return 0;
 }
@@ -1362,6 +1367,7 @@ int ottohip_table_set_file_stats(ottohip_table* t, int rule, int64_t file_rows, 
 
 int ottohip_table_stats(const ottohip_table* t, int rule, ottohip_rule_stats* st) {
   if (!t || !st || rule < 0 || rule >= t->n_rules) { set_error("table_stats: bad args"); return OTTOHIP_EINVAL; }
+  OH_TRY(ensure_part_stats(t));
   *st = t->stats[rule];
   return 0;
 }
@@ -1369,6 +1375,7 @@ int ottohip_table_stats(const ottohip_table* t, int rule, ottohip_rule_stats* st
 int ottohip_table_copy(const ottohip_table* t, int rule, int32_t* aid, int32_t* aid_next, uint32_t* count,
                        uint32_t* count_ge2, void* stream) {
   if (!t || rule < 0 || rule >= t->n_rules) { set_error("table_copy: bad args"); return OTTOHIP_EINVAL; }
+  OH_TRY(ensure_part_stats(t));
   if (t->n_rows == 0 || t->stats[rule].n_rows == 0) return 0;
   hipStream_t s = S(stream);
   Ctx* ctx = t->ctx;
@@ -1663,7 +1670,8 @@ extern "C" int ottohip_table_part_heads(ottohip_ctx* ctx, const ottohip_table* t
       pc.stage[p] = 3;
     }
   }
-  // (2) kept rows of every part -> records
+  // (2) kept rows of every part -> records (a single pass with a decoupled look-back over the tiles measured 98 ms
+  // against 3.9 + 8 ms for count, scan, compact: agent-scope status reads cross the XCDs at ~0.2 us a tile)
   const int64_t nb = ceil_div(n, FIN_B);
   uint32_t* bcnt;
   uint64_t *boff, *tot;
@@ -1689,6 +1697,7 @@ extern "C" int ottohip_table_finalize(ottohip_ctx* ctx, const ottohip_table* t, 
   if (!ctx || !t || !mp || !n_out || rule < 0 || rule >= t->n_rules) { set_error("finalize: bad args"); return OTTOHIP_EINVAL; }
   *n_out = 0;
   hipStream_t s = S(stream);
+  OH_TRY(ensure_part_stats(t));
   const ottohip_rule_stats& st = t->stats[rule];
   const bool use_ge2 = mp->click_rule && st.file_rows > mp->filter_rows;
   const int64_t n_after = use_ge2 ? st.file_rows_ge2 : st.file_rows;

@@ -57,7 +57,12 @@ struct ottohip_table {
   ottohip_ctx* ctx = nullptr;
   KeptEmission* kept = nullptr;  // ottohip_file_opts.keep_words: the count's words, for ottohip_table_count_parts
   bool aid_ordered = true;       // a rule's (part's) slots are in aid order (false: explicit mirror rows)
+  int part_stats_pending = 0;    // part-mode tables: the per-part rows / pairs are counted when first read
 };
+// a part-mode table's per-part statistics (rows, pairs per rule byte), counted on first use (abi.hip)
+namespace ottohip {
+int ensure_part_stats(const ottohip_table* t);
+}
 
 static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
