@@ -12,7 +12,7 @@ EXTRA="$*"
 OBJ=$(mktemp -d)
 for f in abi prims knn shard merge ingest retrieve candidates popularity; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$SRC/../../include" -Wno-unused-function \
-    -Wno-unused-value -Wno-unused-result -munsafe-fp-atomics $EXTRA -c -o "$OBJ/$f.o" "$SRC/$f.hip" &
+    -Wno-unused-value -Wno-unused-result -munsafe-fp-atomics $([ $f = knn ] && echo -fno-honor-nans) $EXTRA -c -o "$OBJ/$f.o" "$SRC/$f.hip" &
 done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/otto-recommender_amd/libottohip_ab.so" "$OBJ"/*.o
