@@ -288,6 +288,10 @@ int ottohip_candidates_generate(ottohip_ctx* ctx, const int64_t* session_offsets
 int ottohip_candidates_info(const ottohip_candidates* c, int64_t* n_sessions, int64_t* n_cand);
 int ottohip_candidates_copy(const ottohip_candidates* c, uint64_t* off, int32_t* aid_next, int16_t* ts_order,
                             uint16_t* flags, void* stream);
+/* the candidates' own device arrays (valid until ottohip_candidates_free; read-only): a zero-copy view for
+ * consumers on the device (R7 reads off / aid_next in place of a ottohip_candidates_copy of 8 B per candidate) */
+int ottohip_candidates_view(const ottohip_candidates* c, const uint64_t** off, const int32_t** aid_next,
+                            const int16_t** ts_order, const uint16_t** flags);
 void ottohip_candidates_free(ottohip_candidates* c);
 /* R9 (model/eval_retrieved.py:45-118) for the candidates whose flags intersect src_mask (0 = all):
  * labels per type t as CSR lab_off[t * (n_sessions + 1) + s] into lab_aid (unique per session/type).

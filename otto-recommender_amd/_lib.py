@@ -100,6 +100,8 @@ SIGNATURES = {
     "ottohip_lists_build": (ctypes.c_int, [_VP, _VP, _VP, _VP, _I64, _I32, _VP, _VP, _VP, _VP]),
     "ottohip_candidates_generate": (ctypes.c_int, [_VP, _VP, _I64, _VP, _VP, _VP, _VP, _VP, ctypes.POINTER(_VP), _VP]),
     "ottohip_candidates_info": (ctypes.c_int, [_VP, ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
+    "ottohip_candidates_view": (ctypes.c_int, [_VP, ctypes.POINTER(_VP), ctypes.POINTER(_VP), ctypes.POINTER(_VP),
+                                               ctypes.POINTER(_VP)]),
     "ottohip_candidates_copy": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
     "ottohip_candidates_free": (None, [_VP]),
     "ottohip_labels_csr": (ctypes.c_int, [_VP, _VP, _I64, _VP, _VP, _VP, _I64, _VP, _VP, ctypes.POINTER(_I64), _VP]),

@@ -123,6 +123,13 @@ class Candidates:
         k = self.n_cand
         return {"off": off, "aid_next": nxt[:k], "ts_order_aid": ordr[:k], "flags": flags[:k]}
 
+    def view(self) -> dict:
+        """The device arrays' addresses (ottohip_candidates_view, no copy; valid while this object lives):
+        {"off", "aid_next", "ts_order_aid", "flags"} -> int."""
+        p = [ctypes.c_void_p() for _ in range(4)]
+        _lib.check(_lib.load().ottohip_candidates_view(self.h, *(ctypes.byref(x) for x in p)))
+        return {k: int(x.value or 0) for k, x in zip(("off", "aid_next", "ts_order_aid", "flags"), p)}
+
     def to_pandas(self, session_ids=None):
         """DataFrame[session, aid_next:int32, ts_order_aid:int16, src_*:int8] in output order."""
         import pandas as pd

@@ -1074,6 +1074,16 @@ int ottohip_candidates_copy(const ottohip_candidates* c, uint64_t* off, int32_t*
   return 0;
 }
 
+int ottohip_candidates_view(const ottohip_candidates* c, const uint64_t** off, const int32_t** aid_next,
+                            const int16_t** ts_order, const uint16_t** flags) {
+  if (!c) { set_error("candidates_view: NULL"); return OTTOHIP_EINVAL; }
+  if (off) *off = c->off;
+  if (aid_next) *aid_next = c->next;
+  if (ts_order) *ts_order = c->ord;
+  if (flags) *flags = c->flags;
+  return 0;
+}
+
 void ottohip_candidates_free(ottohip_candidates* c) {
   if (!c) return;
   (void)hipDeviceSynchronize();

@@ -130,6 +130,20 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
     lab_cols = [torch.from_numpy(np.ascontiguousarray(labels[k].to_numpy(), dt)).to(dev)
                 for k, dt in (("session", np.int32), ("aid", np.int32), ("type", np.int8))]
     sess_dev = torch.from_numpy(np.ascontiguousarray(sess, np.int32)).to(dev)
+    # the two Word2Vec embedding tables (inputs like the events): resident once for the kNN indexes (B3), the
+    # session embeddings (C1) and R7, instead of one host->device copy of 0.74 GB per consumer
+    emb_dev = {}
+
+    def resident(e):
+        if isinstance(e, torch.Tensor) and e.device == dev and e.dtype == torch.float32:
+            return e.contiguous()
+        if id(e) not in emb_dev:
+            x = e if isinstance(e, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(e, np.float32))
+            emb_dev[id(e)] = x.to(dev, torch.float32).contiguous()
+        return emb_dev[id(e)]
+
+    emb_all, emb_12 = resident(emb_all), resident(emb_12)
+    del emb_dev
     # the host copies made for the upload are input preparation: released here, not at the step's end
     # (freeing ~2 GB of host arrays took ~0.25 s after the last stage)
     n_tr_sessions = ev_tr.n_sessions
@@ -199,9 +213,8 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
     t = mark("candidates", t)
     # ---- R7: cosine similarity / Euclidean distance between each candidate and its session's C1
     # embedding (model/retrieve.py:604-625; candidates without an aid embedding: 0 / -1)
-    csr = cands.to_torch()
-    se_test = se[n_tr_sessions:]
-    sim = gp.session_item_similarity(csr["off"], csr["aid_next"], se_test, words_all, emb_all, None, n_items, ctx)
+    se_test = se[n_tr_sessions:]  # the candidates' arrays read in place (no copy of 8 B per candidate)
+    sim = gp.session_item_similarity(cands, None, se_test, words_all, emb_all, None, n_items, ctx)
     t = mark("R7_similarity", t)
     lo, la = gcand.labels_csr_device(*lab_cols, sess_dev, ctx=ctx)
     t = mark("labels_csr", t)
@@ -234,6 +247,6 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
         else:
             out["intermediates"]["candidates_csr"] = cands.to_torch()
     cands.free()
-    del csr, sim, se_test
+    del sim, se_test
     mark("finish", t)
     return out

@@ -429,22 +429,26 @@ def count_popularity(offsets, aid, ts, type_, session_cl, n_clusters: int, n_ite
 
 def session_item_similarity(cand_off, aid_next, sess_emb, words, embeddings, sess_has=None,
                             n_items: int = config.N_ITEMS_OTTO, ctx=None, stream=None):
-    """R7 for candidates in CSR (cand_off [S+1]): torch (cos_sim_ses_aid, eucl_dist_ses_aid) f32."""
+    """R7 for candidates in CSR (cand_off [S+1]): torch (cos_sim_ses_aid, eucl_dist_ses_aid) f32.
+    cand_off may be a candidates.Candidates (aid_next None): its device arrays are read in place."""
     import torch
     ctx = ctx or _lib.context()
     dev = torch.device("cuda", ctx.device)
-    off = _t(cand_off, dev, torch.int64)
-    nxt = _t(aid_next, dev, torch.int32)
+    if hasattr(cand_off, "view") and hasattr(cand_off, "n_cand"):
+        v = cand_off.view()
+        S, n, p_off, p_nxt = cand_off.n_sessions, cand_off.n_cand, v["off"], v["aid_next"]
+    else:
+        off = _t(cand_off, dev, torch.int64)
+        nxt = _t(aid_next, dev, torch.int32)
+        S, n, p_off, p_nxt = int(off.numel()) - 1, int(nxt.numel()), _lib.ptr(off), _lib.ptr(nxt)
     se = _t(sess_emb, dev, torch.float32)
     emb = _t(embeddings, dev, torch.float32)
     has = None if sess_has is None else _t(sess_has, dev, torch.uint8)
     rmap = row_of_aid_map(words, n_items, dev)
-    S = int(off.numel()) - 1
-    n = int(nxt.numel())
     cos = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
     eu = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
     _lib.check(_lib.load().ottohip_session_item_similarity(
-        ctx.h, _lib.ptr(off), S, _lib.ptr(nxt) if n else None, _lib.ptr(se), _lib.ptr(has) if has is not None else None,
+        ctx.h, p_off, S, p_nxt if n else None, _lib.ptr(se), _lib.ptr(has) if has is not None else None,
         _lib.ptr(rmap), int(rmap.numel()), _lib.ptr(emb), int(emb.shape[1]), _lib.ptr(cos), _lib.ptr(eu),
         _lib.stream_handle(stream)))
     return cos[:n], eu[:n]

@@ -210,3 +210,31 @@ def test_labels_csr_device_matches_host(gpu):
     np.testing.assert_array_equal(la_d.cpu().numpy(), la_h)
     lo_e, la_e = gcand.labels_csr_device(np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0, np.int8), sess_ids)
     assert int(lo_e.abs().sum().item()) == 0 and la_e.numel() == 0
+
+
+
+def test_candidates_view_feeds_similarity(gpu):
+    """ottohip_candidates_view: the candidates' own arrays read in place (the pipeline's R7 input); R7 over the
+    view equals R7 over the ottohip_candidates_copy arrays, element for element."""
+    from otto_recommender_amd import candidates as gcand, popularity as gp
+    ev, df, r1, ka, k12, cl, pop = _fixture(1500, seed=21, first=7)
+    r1t = {n: (f["aid"].to_numpy(), f["aid_next"].to_numpy(), f[f"{n}_rank"].to_numpy()) for n, f in r1.items()}
+
+    def kn(f):
+        return f["aid"].to_numpy(), f["aid_next"].to_numpy(), f[[c for c in f.columns if c.startswith("rank_")][0]].to_numpy()
+
+    src = gcand.CandidateSources(r1t, kn(ka), kn(k12))
+    c = gcand.generate(ev.session_offsets, ev.aid, ev.ts, ev.type, src, None)
+    assert c.n_cand > 1000
+    t = c.to_torch()
+    v = c.view()
+    assert v["off"] and v["aid_next"] and v["off"] != t["off"].data_ptr() and v["aid_next"] != t["aid_next"].data_ptr()
+    words = np.unique(ev.aid).astype(np.int32)
+    emb = synth.embeddings(len(words), seed=2)
+    se = np.random.default_rng(4).normal(size=(c.n_sessions, emb.shape[1])).astype(np.float32)
+    a = [x.cpu().numpy() for x in gp.session_item_similarity(t["off"], t["aid_next"], se, words, emb)]
+    b = [x.cpu().numpy() for x in gp.session_item_similarity(c, None, se, words, emb)]
+    assert len(b[0]) == c.n_cand
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    c.free()
