@@ -189,12 +189,15 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
     knn = [_knn_lists(w, e, knn_queries, ctx, dev, group) for w, e in ((words_all, emb_all), (words_12, emb_12))]
     t = mark("knn", t)
     # ---- pop-cluster source: C1 embeddings of all sessions, C2 KMeans, C3 ranks (cl50)
+    rmap_all = gp.row_of_aid_map(words_all, n_items, dev)  # aid -> row of emb_all, for C1 and R7
     se = gp.compute_sessions_embeddings(dev_all.offsets, dev_all.aid, dev_all.ts, dev_all.type, words_all, emb_all,
-                                        n_items, ctx)
+                                        n_items, ctx, rmap=rmap_all)
     t = mark("C1_embeddings", t)
-    grows = np.concatenate([np.concatenate([np.arange(fb_tr[f], fb_tr[f + 1]) for f in my_tr] or [np.zeros(0)]),
-                            train.n_sessions + np.concatenate([np.arange(fb_te[f], fb_te[f + 1]) for f in my_te]
-                                                              or [np.zeros(0)])]).astype(np.int64)
+    grows = None  # one GPU: every session, in order (KMeans.fit takes local rows as the global ones)
+    if group is not None:
+        grows = np.concatenate([np.concatenate([np.arange(fb_tr[f], fb_tr[f + 1]) for f in my_tr] or [np.zeros(0)]),
+                                train.n_sessions + np.concatenate([np.arange(fb_te[f], fb_te[f + 1]) for f in my_te]
+                                                                  or [np.zeros(0)])]).astype(np.int64)
     km = km_model.fit(se, ctx, group=group, global_rows=grows, seed_heads=km_seeds)
     labels_all = km.labels_
     t = mark("C2_kmeans", t)
@@ -214,7 +217,7 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
     # ---- R7: cosine similarity / Euclidean distance between each candidate and its session's C1
     # embedding (model/retrieve.py:604-625; candidates without an aid embedding: 0 / -1)
     se_test = se[n_tr_sessions:]  # the candidates' arrays read in place (no copy of 8 B per candidate)
-    sim = gp.session_item_similarity(cands, None, se_test, words_all, emb_all, None, n_items, ctx)
+    sim = gp.session_item_similarity(cands, None, se_test, words_all, emb_all, None, n_items, ctx, rmap=rmap_all)
     t = mark("R7_similarity", t)
     lo, la = gcand.labels_csr_device(*lab_cols, sess_dev, ctx=ctx)
     t = mark("labels_csr", t)
@@ -235,7 +238,7 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
             "tables": {n: tuple(h(x) for x in v) for n, v in tables.items()},
             "r1": {n: tuple(h(x) for x in v) for n, v in r1.items()},
             "knn": [tuple(h(x) for x in v) for v in knn],
-            "cluster_labels": h(labels_all), "cluster_rows": grows, "pop": p[["cl50", "aid"]].reset_index(drop=True),
+            "cluster_labels": h(labels_all), "cluster_rows": grows if grows is not None else np.arange(int(labels_all.numel()), dtype=np.int64), "pop": p[["cl50", "aid"]].reset_index(drop=True),
             "n_clusters": n_clusters, "test_session_ids": sess}
         if keep_candidates:  # R7 of every candidate and the test sessions' C1 embeddings (small runs)
             out["intermediates"]["similarity"] = tuple(h(x) for x in sim)

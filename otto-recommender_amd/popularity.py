@@ -38,8 +38,9 @@ def row_of_aid_map(words, n_items: int, dev):
 
 
 def compute_sessions_embeddings(offsets, aid, ts, type_, words, embeddings, n_items: int = config.N_ITEMS_OTTO,
-                                ctx=None, stream=None):
-    """C1 for a session-sorted event table: torch f32 [n_sessions, dim] on the device."""
+                                ctx=None, stream=None, rmap=None):
+    """C1 for a session-sorted event table: torch f32 [n_sessions, dim] on the device.
+    rmap: row_of_aid_map(words, n_items, device), if the caller holds it already."""
     import torch
     ctx = ctx or _lib.context()
     dev = torch.device("cuda", ctx.device)
@@ -47,7 +48,7 @@ def compute_sessions_embeddings(offsets, aid, ts, type_, words, embeddings, n_it
     off = off - off[0]
     a, s_, y = _t(aid, dev, torch.int32), _t(ts, dev, torch.int32), _t(type_, dev, torch.int8)
     emb = _t(embeddings, dev, torch.float32)
-    rmap = row_of_aid_map(words, n_items, dev)
+    rmap = row_of_aid_map(words, n_items, dev) if rmap is None else rmap
     S = int(off.numel()) - 1
     dim = int(emb.shape[1])
     out = torch.empty((max(S, 1), dim), dtype=torch.float32, device=dev)
@@ -162,7 +163,7 @@ class KMeans:
             if len(grows) != n or np.any(np.diff(grows) <= 0):
                 raise ValueError("global_rows: one increasing global row id per local row")
         else:
-            n_all, grows = n, np.arange(n, dtype=np.int64)
+            n_all, grows = n, None  # one GPU: local row = global row (no 8 B per row of host ids)
         if n_all < k:
             raise ValueError(f"n_samples={n_all} should be >= n_clusters={k}")
         # column means (exact fixed-point sums), centring, tol = mean variance * tol
@@ -338,12 +339,17 @@ class KMeans:
 
     @staticmethod
     def _gather_rows(Xc, rows, grows, group):
-        """global rows of the (row-sharded) matrix, replicated: each rank fills the ones it owns."""
+        """global rows of the (row-sharded) matrix, replicated: each rank fills the ones it owns
+        (grows None: the rows are the global rows 0..n-1)."""
         import torch
         rows = np.asarray(rows, np.int64)
         C = torch.zeros((len(rows), Xc.shape[1]), dtype=torch.float32, device=Xc.device)
-        loc = np.searchsorted(grows, rows)
-        mine = np.flatnonzero((loc < len(grows)) & (grows[np.minimum(loc, len(grows) - 1)] == rows)) if len(grows) else []
+        if grows is None:
+            loc = rows
+            mine = np.flatnonzero((rows >= 0) & (rows < Xc.shape[0]))
+        else:
+            loc = np.searchsorted(grows, rows)
+            mine = np.flatnonzero((loc < len(grows)) & (grows[np.minimum(loc, len(grows) - 1)] == rows)) if len(grows) else []
         if len(mine):
             C[torch.from_numpy(mine).to(Xc.device)] = Xc[torch.from_numpy(loc[mine]).to(Xc.device)]
         return _allreduce(C, group).contiguous()
@@ -358,7 +364,8 @@ class KMeans:
         d2 = (ctypes.c_float * m)()
         _lib.check(_lib.load().ottohip_kmeans_farthest(ctx.h, _lib.ptr(Xc), n, Xc.shape[1], _lib.ptr(C),
                                                        _lib.ptr(labels), m, rows, d2, sh))
-        cand = [(float(d2[j]), int(grows[rows[j]]), int(labels[rows[j]].item())) for j in range(m) if rows[j] >= 0]
+        gid = (lambda r: int(r)) if grows is None else (lambda r: int(grows[r]))
+        cand = [(float(d2[j]), gid(rows[j]), int(labels[rows[j]].item())) for j in range(m) if rows[j] >= 0]
         if group is not None:
             import torch.distributed as dist
             allc = [None] * dist.get_world_size(group)
@@ -428,7 +435,7 @@ def count_popularity(offsets, aid, ts, type_, session_cl, n_clusters: int, n_ite
 
 
 def session_item_similarity(cand_off, aid_next, sess_emb, words, embeddings, sess_has=None,
-                            n_items: int = config.N_ITEMS_OTTO, ctx=None, stream=None):
+                            n_items: int = config.N_ITEMS_OTTO, ctx=None, stream=None, rmap=None):
     """R7 for candidates in CSR (cand_off [S+1]): torch (cos_sim_ses_aid, eucl_dist_ses_aid) f32.
     cand_off may be a candidates.Candidates (aid_next None): its device arrays are read in place."""
     import torch
@@ -444,7 +451,7 @@ def session_item_similarity(cand_off, aid_next, sess_emb, words, embeddings, ses
     se = _t(sess_emb, dev, torch.float32)
     emb = _t(embeddings, dev, torch.float32)
     has = None if sess_has is None else _t(sess_has, dev, torch.uint8)
-    rmap = row_of_aid_map(words, n_items, dev)
+    rmap = row_of_aid_map(words, n_items, dev) if rmap is None else rmap
     cos = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
     eu = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
     _lib.check(_lib.load().ottohip_session_item_similarity(
