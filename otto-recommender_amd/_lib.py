@@ -252,6 +252,18 @@ class Context:
 _CTX = {}
 
 
+_LANE_CTX: dict = {}
+
+
+def lane_context(device: int, lane: int) -> Context:
+    """A further context of `device` for work issued from another host thread on its own stream (KMeans run
+    lanes): its own workspace and per-call state; cached per (device, lane)."""
+    key = (int(device), int(lane))
+    if key not in _LANE_CTX:
+        _LANE_CTX[key] = Context(int(device))
+    return _LANE_CTX[key]
+
+
 def context(device: int | None = None) -> Context:
     import torch
     d = torch.cuda.current_device() if device is None else device

@@ -61,6 +61,7 @@ def compute_sessions_embeddings(offsets, aid, ts, type_, words, embeddings, n_it
 FX = float(1 << 24)  # fixed-point scale of the device sums (csrc/popularity.hip KM_FX)
 LLOYD_BATCH = 10  # Lloyd steps per ottohip_kmeans_lloyd_steps call (the stop checks run on the device)
 KM_GROUP = 1  # n_init runs in lockstep per read of X (ottohip_kmeans_lloyd_steps_multi); 1: one bounded run at a time
+KM_LANES = 1  # one GPU: runs on this many host threads, each with its own context and stream (OTTOHIP_KM_LANES)
 
 
 def _allreduce(t, group):
@@ -193,13 +194,13 @@ class KMeans:
             if rc not in (0, _lib.OTTOHIP_ELIMIT):
                 _lib.check(rc)
         try:
-            return self._fit_runs(X, Xc, n, dim, k, group, grows, tol_abs, seed_stream, mean_d, ctx, sh, dev)
+            return self._fit_runs(X, Xc, n, dim, k, group, grows, tol_abs, seed_stream, mean_d, ctx, sh, dev, half)
         finally:
             seed_stream.close()
             if half:  # always paired with the attach: a later fit never meets this fit's f16 copy
                 lib.ottohip_kmeans_detach_half(ctx.h)
 
-    def _fit_runs(self, X, Xc, n, dim, k, group, grows, tol_abs, seed_stream, mean_d, ctx, sh, dev):
+    def _fit_runs(self, X, Xc, n, dim, k, group, grows, tol_abs, seed_stream, mean_d, ctx, sh, dev, half=False):
         """fit's n_init runs (the Lloyd loops) over the centred rows Xc; keeps the best by inertia."""
         import torch
         lib = _lib.load()
@@ -214,6 +215,12 @@ class KMeans:
         grp = int(os.environ.get("OTTOHIP_KM_GROUP", str(KM_GROUP)))
         multi_ok = group is None and 32 < k <= 64 and dim <= 112 and dim % 4 == 0 and grp >= 2
         pending = []  # later runs of a lockstep group, in run order
+        lanes = int(os.environ.get("OTTOHIP_KM_LANES", str(KM_LANES)))
+        if group is None and not multi_ok and lanes >= 2 and self.n_init >= 2:
+            best = self._fit_lanes(Xc, n, dim, k, seed_stream, tol_abs, ctx, min(lanes, self.n_init), half)
+            self.inertia_, C, self.labels_, self.n_iter_ = best
+            self.cluster_centers_ = C + mean_d
+            return self
         for run in range(self.n_init):
             if pending:
                 res = pending.pop(0)
@@ -282,6 +289,101 @@ class KMeans:
         self.inertia_, C, self.labels_, self.n_iter_ = best
         self.cluster_centers_ = C + mean_d
         return self
+
+    def _run_one(self, Xc, n, dim, k, seeds, tol_abs, ctx, sh, labels, sums, counts):
+        """One single-GPU run (batched device Lloyd steps, empty-cluster relocation, final E-step and inertia)
+        on ctx / stream sh and torch's current stream: (inertia, C, labels, n_iter)."""
+        import torch
+        lib = _lib.load()
+        st6 = (ctypes.c_double * 6)()
+        inr, chg, shift = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+        C = self._gather_rows(Xc, seeds, None, None)
+        labels.fill_(-1)
+        sums.zero_()
+        counts.zero_()
+        strict, it = False, 0
+        while it < self.max_iter:
+            _lib.check(lib.ottohip_kmeans_lloyd_steps(ctx.h, _lib.ptr(Xc), n, dim, _lib.ptr(C), k, _lib.ptr(labels),
+                                                      _lib.ptr(sums), _lib.ptr(counts),
+                                                      min(LLOYD_BATCH, self.max_iter - it), tol_abs, st6, sh))
+            it += int(st6[4])
+            n_changed, reason = int(st6[1]), int(st6[5])
+            shift.value = st6[2]
+            if reason == 3:  # empty clusters: relocate on a copy (sums / counts follow the labels), M-step
+                rs_, rc_ = sums.clone(), counts.clone()
+                empty = np.flatnonzero(rc_.cpu().numpy() == 0)
+                self._relocate(Xc, C, labels, rs_, rc_, empty, None, None, ctx, sh)
+                _lib.check(lib.ottohip_kmeans_update(ctx.h, _lib.ptr(C), _lib.ptr(rs_), _lib.ptr(rc_), k, dim,
+                                                     ctypes.byref(shift), sh))
+                reason = 1 if n_changed == 0 else (2 if shift.value <= tol_abs else 0)
+            if reason == 1:
+                strict = True
+            if reason in (1, 2):
+                break
+        if not strict:  # E-step with the final centres (labels match cluster_centers_)
+            _lib.check(lib.ottohip_kmeans_partial(ctx.h, _lib.ptr(Xc), n, dim, _lib.ptr(C), k, _lib.ptr(labels),
+                                                  _lib.ptr(sums), _lib.ptr(counts), ctypes.byref(inr),
+                                                  ctypes.byref(chg), sh))
+        _lib.check(lib.ottohip_kmeans_inertia(ctx.h, _lib.ptr(Xc), n, dim, _lib.ptr(C), _lib.ptr(labels),
+                                              ctypes.byref(inr), sh))
+        return float(inr.value), C, labels[:n].clone(), it
+
+    def _fit_lanes(self, Xc, n, dim, k, seed_stream, tol_abs, ctx, lanes, half):
+        """One GPU, n_init runs on `lanes` host threads, each with its own library context (workspace, distance
+        bounds, f16 rows) and HIP stream: run r on lane r % lanes, so one run's small per-step kernels (filter,
+        near ties, centre update) overlap another run's E-step. Every run is computed as alone (bit-identical
+        to the sequential loop); the best is the lowest inertia, the earlier run on ties."""
+        import threading
+        import torch
+        lib = _lib.load()
+        dev = Xc.device
+        seeds = [next(seed_stream) for _ in range(self.n_init)]
+        caller = torch.cuda.current_stream(dev)
+        ctxs = [ctx] + [_lib.lane_context(ctx.device, i) for i in range(1, lanes)]
+        streams = [torch.cuda.Stream(dev) for _ in range(lanes)]
+        for st in streams:
+            st.wait_stream(caller)  # Xc, its f16 copy on ctx and the seeds' inputs are ready
+        attached = []
+        results = [None] * self.n_init
+        errors = []
+
+        def lane(li):
+            try:
+                with torch.cuda.stream(streams[li]):
+                    lsh = _lib.stream_handle(streams[li])
+                    if li > 0 and half:
+                        rc = lib.ottohip_kmeans_attach_half(ctxs[li].h, _lib.ptr(Xc), n, dim, lsh)
+                        if rc == 0:
+                            attached.append(li)
+                        elif rc != _lib.OTTOHIP_ELIMIT:
+                            _lib.check(rc)
+                    sums = torch.empty(k * dim, dtype=torch.int64, device=dev)
+                    counts = torch.empty(k, dtype=torch.int64, device=dev)
+                    labels = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+                    for run in range(li, self.n_init, lanes):
+                        results[run] = self._run_one(Xc, n, dim, k, seeds[run], tol_abs, ctxs[li],
+                                                     _lib.stream_handle(streams[li]), labels, sums, counts)
+            except BaseException as e:  # noqa: BLE001 -- re-raised on the caller's thread
+                errors.append(e)
+
+        threads = [threading.Thread(target=lane, args=(li,), daemon=True) for li in range(lanes)]
+        try:
+            for t in threads:
+                t.start()
+        finally:
+            for t in threads:
+                t.join()
+            for li in attached:
+                lib.ottohip_kmeans_detach_half(ctxs[li].h)
+            for st in streams:
+                caller.wait_stream(st)
+        if errors:
+            raise errors[0]
+        best = None
+        for res in results:  # run order: an equal inertia keeps the earlier run
+            if best is None or res[0] < best[0]:
+                best = res
+        return best
 
     def _fit_multi(self, Xc, seeds, grows, tol_abs, ctx, sh):
         """G <= 4 runs of fit's single-GPU loop in lockstep: the same batches of device Lloyd steps, stop

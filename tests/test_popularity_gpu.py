@@ -71,6 +71,36 @@ def test_kmeans_lloyd_step_batches_equal_single_steps(gpu, monkeypatch):
     assert fits[0][2] == fits[1][2] and fits[0][3] == fits[1][3]
 
 
+@pytest.mark.parametrize("case", ["sessions_k50", "relocation_k9"])
+def test_kmeans_run_lanes_equal_sequential_runs(gpu, monkeypatch, case):
+    """KMeans.fit's n_init runs on 2 or 3 host threads (OTTOHIP_KM_LANES: a context and a HIP stream per lane, run
+    r on lane r % lanes) give the sequential loop's labels, centres, inertia and iterations bit for bit, incl. the
+    empty-cluster relocations (relocation_k9) and the earlier-run rule for the best inertia."""
+    from otto_recommender_amd import popularity as gp
+    rng = np.random.default_rng(12)
+    if case == "sessions_k50":
+        ev = synth.generate(30_000, first_session=99)
+        words = np.unique(ev.aid)
+        emb = synth.embeddings(len(words), seed=1)
+        X = gp.compute_sessions_embeddings(ev.session_offsets, ev.aid, ev.ts, ev.type, words, emb).cpu().numpy()
+        k, n_init = 50, 5
+    else:
+        centers = rng.normal(scale=2, size=(9, 100))
+        X = (centers[rng.integers(0, 9, 30000)] + rng.normal(size=(30000, 100))).astype(np.float32)
+        X[:4000] = X[0]
+        k, n_init = 9, 10
+    monkeypatch.setenv("OTTOHIP_KM_GROUP", "1")
+    fits = []
+    for lanes in ("1", "2", "3"):
+        monkeypatch.setenv("OTTOHIP_KM_LANES", lanes)
+        km = gp.KMeans(n_clusters=k, random_state=7, n_init=n_init).fit(X)
+        fits.append((km.labels_.cpu().numpy(), km.cluster_centers_.cpu().numpy(), km.inertia_, km.n_iter_))
+    for f in fits[1:]:
+        np.testing.assert_array_equal(fits[0][0], f[0])
+        np.testing.assert_array_equal(fits[0][1], f[1])
+        assert fits[0][2] == f[2] and fits[0][3] == f[3]
+
+
 @pytest.mark.parametrize("case", ["sessions_k50", "relocation_k9", "blocks_k33"])
 def test_kmeans_bounded_steps_equal_full_steps(gpu, monkeypatch, case):
     """The bounded Lloyd steps (rows whose distance bounds separate keep their label unscored,
