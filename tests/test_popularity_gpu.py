@@ -5,6 +5,8 @@ tolerance 3e-6 absolute after round6 (one unit in the 6th decimal plus fp32 outp
 the reference's own polars f32 summation order is unspecified). C2 KMeans: sklearn 1.2's
 algorithm as restated in the oracle (itself pinned against scikit-learn); labels agree on >= 99.9 %
 of rows (fp32 vs f64 near-ties), centroids within 1e-3, inertia rel 1e-5. R7: rtol 1e-5 vs f64."""
+import os
+
 import numpy as np
 import pandas as pd
 import pytest
@@ -71,6 +73,8 @@ def test_kmeans_lloyd_step_batches_equal_single_steps(gpu, monkeypatch):
     assert fits[0][2] == fits[1][2] and fits[0][3] == fits[1][3]
 
 
+@pytest.mark.skipif(os.environ.get("OTTOHIP_TEST_KM_LANES") != "1",
+                    reason="run lanes are off by default (KM_LANES = 1) and not yet run on the box: OTTOHIP_TEST_KM_LANES=1")
 @pytest.mark.parametrize("case", ["sessions_k50", "relocation_k9"])
 def test_kmeans_run_lanes_equal_sequential_runs(gpu, monkeypatch, case):
     """KMeans.fit's n_init runs on 2 or 3 host threads (OTTOHIP_KM_LANES: a context and a HIP stream per lane, run
