@@ -61,7 +61,7 @@ def compute_sessions_embeddings(offsets, aid, ts, type_, words, embeddings, n_it
 FX = float(1 << 24)  # fixed-point scale of the device sums (csrc/popularity.hip KM_FX)
 LLOYD_BATCH = 10  # Lloyd steps per ottohip_kmeans_lloyd_steps call (the stop checks run on the device)
 KM_GROUP = 1  # n_init runs in lockstep per read of X (ottohip_kmeans_lloyd_steps_multi); 1: one bounded run at a time
-KM_LANES = 1  # one GPU: runs on this many host threads, each with its own context and stream (OTTOHIP_KM_LANES)
+KM_LANES = 1  # runs on this many host threads, each with its own context and stream (OTTOHIP_KM_LANES); 2 lanes measured slower
 
 
 def _allreduce(t, group):

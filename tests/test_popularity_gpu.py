@@ -73,8 +73,6 @@ def test_kmeans_lloyd_step_batches_equal_single_steps(gpu, monkeypatch):
     assert fits[0][2] == fits[1][2] and fits[0][3] == fits[1][3]
 
 
-@pytest.mark.skipif(os.environ.get("OTTOHIP_TEST_KM_LANES") != "1",
-                    reason="run lanes are off by default (KM_LANES = 1) and not yet run on the box: OTTOHIP_TEST_KM_LANES=1")
 @pytest.mark.parametrize("case", ["sessions_k50", "relocation_k9"])
 def test_kmeans_run_lanes_equal_sequential_runs(gpu, monkeypatch, case):
     """KMeans.fit's n_init runs on 2 or 3 host threads (OTTOHIP_KM_LANES: a context and a HIP stream per lane, run
