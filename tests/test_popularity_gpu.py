@@ -5,7 +5,6 @@ tolerance 3e-6 absolute after round6 (one unit in the 6th decimal plus fp32 outp
 the reference's own polars f32 summation order is unspecified). C2 KMeans: sklearn 1.2's
 algorithm as restated in the oracle (itself pinned against scikit-learn); labels agree on >= 99.9 %
 of rows (fp32 vs f64 near-ties), centroids within 1e-3, inertia rel 1e-5. R7: rtol 1e-5 vs f64."""
-import os
 
 import numpy as np
 import pandas as pd
