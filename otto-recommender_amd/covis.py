@@ -287,15 +287,16 @@ def count_co_events_fused(events: DeviceEvents, names=None, n_items: int = confi
     table is re-folded from them (ottohip_table_count_parts) instead of counted again."""
     ctx = ctx or _lib.context()
     nf = len(events.file_bounds) - 1
-    keep = keep_words and nf <= (max_files or max_files_per_call(names, n_items))
-    if cuts is None and (keep or (per_file_rule is not None and per_file_rule in (names or config.CO_EVENTS_TO_COUNT))):
-        pfr = per_file_rule if per_file_rule in (names or config.CO_EVENTS_TO_COUNT) else None
+    pfr = per_file_rule if per_file_rule in (names or config.CO_EVENTS_TO_COUNT) else None
+    # words are kept only by a count of one pass: per-file statistics cap a pass at 1024 files (below)
+    keep = keep_words and nf <= min(max_files or max_files_per_call(names, n_items), 1024 if pfr else 1 << 62)
+    if cuts is None and (keep or pfr is not None):
         tab = count_co_events_fused(events, names, n_items, dedup, stream, ctx, max_files,
                                     FileCuts(pfr or list(names or config.CO_EVENTS_TO_COUNT)[0], per_file=pfr is not None,
                                              keep_words=keep))
         if pfr is not None:
             tab.per_file_rule = pfr
-        tab.kept_words = keep
+        tab.kept_words = keep and getattr(tab, "kept_words", False)  # a batched merge keeps none
         return tab
     cap = max_files or max_files_per_call(names, n_items)
     if cuts is not None and cuts.per_file:

@@ -27,8 +27,11 @@ int ensure_part_stats(const ottohip_table* tc) {
   if (!tc || !tc->part_stats_pending) return 0;
   ottohip_table* T = const_cast<ottohip_table*>(tc);
   Ctx* ctx = T->ctx;
-  const hipStream_t s = nullptr;  // the null stream: ordered after the table's producer on any stream
+  // the null stream, ordered after the producer's stream by the event recorded there (a torch pool stream is
+  // created non-blocking, so the null stream alone would not wait for the reduce that wrote the slots)
+  const hipStream_t s = nullptr;
   OH_HIP(hipSetDevice(T->device));
+  if (T->produced) OH_HIP(hipStreamWaitEvent(s, T->produced, 0));
   unsigned long long* ph;
   OH_TRY(ctx->ws.get("part_hist", 512, &ph));
   OH_HIP(hipMemsetAsync(ph, 0, 512 * 8, s));
@@ -42,6 +45,10 @@ int ensure_part_stats(const ottohip_table* tc) {
     T->stats[p].n_pairs = (int64_t)hh[256 + p];
   }
   T->part_stats_pending = 0;
+  if (T->produced) {
+    (void)hipEventDestroy(T->produced);
+    T->produced = nullptr;
+  }
   return 0;
 }
 
@@ -1120,6 +1127,8 @@ int ottohip_table_count_parts(ottohip_ctx* ctx, const ottohip_table* t, int rule
   // (ottohip_table_part_heads) do not need them, and the table scan took 4.3 ms per A6 of click_to_click
   for (int p = 0; p < po->n_parts; ++p) T->stats[p] = ottohip_rule_stats{};
   T->part_stats_pending = po->n_parts;
+  OH_HIP(hipEventCreateWithFlags(&T->produced, hipEventDisableTiming));
+  OH_HIP(hipEventRecord(T->produced, s));
   *out = T;
   return 0;
 }
@@ -1191,6 +1200,8 @@ int ottohip_covis_count_parts(ottohip_ctx* ctx, const ottohip_events* ev, const 
   // (ottohip_table_part_heads) do not need them, and the table scan took 4.3 ms per A6 of click_to_click
   for (int p = 0; p < po->n_parts; ++p) T->stats[p] = ottohip_rule_stats{};
   T->part_stats_pending = po->n_parts;
+  OH_HIP(hipEventCreateWithFlags(&T->produced, hipEventDisableTiming));
+  OH_HIP(hipEventRecord(T->produced, s));
   *out = T;
   return 0;
 }
@@ -1538,6 +1549,7 @@ void ottohip_table_free(ottohip_table* t) {
     t->b.release();
   }
   kept_free(t->kept);
+  if (t->produced) (void)hipEventDestroy(t->produced);
   delete t;
 }
 

@@ -1018,7 +1018,11 @@ __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, i
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     const uint64_t mm = __ballot(S.mark[l] == rid);
     const uint64_t mle = mm & upto;
+#ifndef OH_EMIT_NOCHECK  // always on, as in emit_flush2: the record index clamped into [0, nrec), marks counted below
+    const int o = min(max(ob + (int)__popcll(mle), 0), nrec - 1);
+#else
     const int o = ob + (int)__popcll(mle);
+#endif
     ob += (int)__popcll(mm);
     const uint32_t p = c + l;
     bool qual = false;
@@ -1041,6 +1045,10 @@ __device__ __forceinline__ void emit_flush(EmitLds& S, int nrec, uint32_t tot, i
     if (qual && !(dbg & 1) && !bad) words[S.u.r.rout[o] + car + (uint32_t)__popcll(mine & below)] = word;
     cc = (uint32_t)__builtin_amdgcn_readlane((int)(car + (uint32_t)__popcll(mine)), 63);
   }
+  // every record start falls in exactly one round: the marks seen must number nrec (err bit 8 -> the call fails)
+#ifndef OH_EMIT_NOCHECK
+  if (tot > 0 && ob != nrec - 1 && l == 0) atomicOr(err, 8);
+#endif
 }
 
 // emit_flush with two pairs per lane per round (128 pairs: lane k writes pairs c + k and c + 64 + k): one mark

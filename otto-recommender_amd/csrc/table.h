@@ -58,6 +58,8 @@ struct ottohip_table {
   KeptEmission* kept = nullptr;  // ottohip_file_opts.keep_words: the count's words, for ottohip_table_count_parts
   bool aid_ordered = true;       // a rule's (part's) slots are in aid order (false: explicit mirror rows)
   int part_stats_pending = 0;    // part-mode tables: the per-part rows / pairs are counted when first read
+  hipEvent_t produced = nullptr; // part-mode tables: recorded on the producer's stream after the reduce; the
+                                 // deferred statistics wait on it (the producer may be a non-blocking stream)
 };
 // a part-mode table's per-part statistics (rows, pairs per rule byte), counted on first use (abi.hip)
 namespace ottohip {

@@ -271,7 +271,7 @@ def _chunk_files(events, n_chunks: int) -> list:
 
 
 def _count_sharded_batches(events, file_ids, n_files_total: int, cap: int, group, names, n_items, dedup, stream, ctx,
-                           chunks, cuts=None):
+                           chunks, cuts=None, sym=None):
     """More global files than a pair word can tell apart: batches of cap global file ids, each
     counted sharded (batch-local file ids), and every rank merge-sums its own shard tables (the
     owner partition is the same in every batch, so no exchange)."""
@@ -285,7 +285,7 @@ def _count_sharded_batches(events, file_ids, n_files_total: int, cap: int, group
         sub = events.subset_files(lo, hi)
         t = count_co_events_sharded(sub, (fids[lo:hi] - g0).tolist(), g1 - g0, group, names, n_items, dedup, stream,
                                     ctx, chunks, max_files=cap,
-                                    cuts=cuts.shifted(g0, g1) if cuts is not None else None)
+                                    cuts=cuts.shifted(g0, g1) if cuts is not None else None, sym=sym)
         st = [(t.stats(r)["file_rows"], t.stats(r)["file_rows_ge2"]) for r in range(len(t.names))]
         fs = st if fs is None else [(a + c, b + d) for (a, b), (c, d) in zip(fs, st)]
         if cuts is not None and cuts.per_file:
@@ -316,7 +316,7 @@ def allreduce_per_file(rows, rows2, group=None):
 def count_co_events_sharded(events, file_ids, n_files_total: int, group=None, names=None,
                             n_items: int = config.N_ITEMS_OTTO, dedup: bool = True, stream=None, ctx=None,
                             chunks: int | None = None, max_files: int | None = None, cuts=None,
-                            per_file_rule: str | None = None):
+                            per_file_rule: str | None = None, sym: bool | None = None):
     """The N-GPU build: this rank's whole files (global ids file_ids) -> pair words laid out by
     owner -> all-to-all-v of words and row pieces (RCCL) -> assemble + reduce of the owner's
     rows. Returns this rank's shard (rows with owner(aid) == rank) of the single-GPU table;
@@ -324,24 +324,35 @@ def count_co_events_sharded(events, file_ids, n_files_total: int, group=None, na
     what concat_files_w_stats compares against its thresholds (:131, :135). cuts: covis.FileCuts
     in global file ids, applied by the owners; per_file statistics are all-reduced (global).
     per_file_rule: every global file's rows of that rule from this count (covis.count_co_events_fused's
-    option), so that concat_files_w_stats_sharded plans branch (2) without a count of its own."""
+    option), so that concat_files_w_stats_sharded plans branch (2) without a count of its own.
+    sym: None = symmetric rules stored once per unordered pair unless key cuts are given; False = every ordered
+    pair at owner(aid) (the storage every part of one branch-(2) plan must share, so that a key lives on one
+    rank in all parts). The mode is decided once here and holds for every file batch of the call."""
     import torch.distributed as dist
     import torch
     from .covis import reference_rules, FileCuts
     from .covis import max_files_per_call
     if per_file_rule is not None and cuts is None and per_file_rule in (names or config.CO_EVENTS_TO_COUNT):
         tab = count_co_events_sharded(events, file_ids, n_files_total, group, names, n_items, dedup, stream, ctx,
-                                      chunks, max_files, FileCuts(per_file_rule, per_file=True))
+                                      chunks, max_files, FileCuts(per_file_rule, per_file=True), sym=sym)
         tab.per_file_rule = per_file_rule
         return tab
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    # symmetric rules (click_to_click, cart_to_cart, buy_to_buy; model/count_co_events.py:64-71) go to the owners
+    # once per unordered pair: the row (a, b), a <= b, at owner(a), which also stands for its mirror (b, a) (the
+    # shard's readers produce it). Key cuts (branch (2)'s parts) need both orders stored; OTTOHIP_DIST_SYM=0 = off
+    key_cut = cuts is not None and (cuts.lo is not None or cuts.hi is not None)
+    if sym and key_cut:
+        raise ValueError("symmetric storage cannot take key cuts (both orders of a pair are needed)")
+    if sym is None:
+        sym = not key_cut and os.environ.get("OTTOHIP_DIST_SYM", "1") != "0"
     cap = max_files or max_files_per_call(names, n_items)
     if cuts is not None and cuts.per_file:
         cap = min(cap, 1024)  # the per-file histogram's file range (ottohip_file_opts)
     if int(n_files_total) > cap:
         tab = _count_sharded_batches(events, file_ids, n_files_total, cap, group, names, n_items, dedup, stream,
-                                     ctx or _lib.context(), chunks, cuts)
+                                     ctx or _lib.context(), chunks, cuts, sym)
         tab.rank, tab.world = rank, world
         return tab
     # the rank's files in n_chunks contiguous groups (balanced by events): chunk c's all-to-all
@@ -349,10 +360,6 @@ def count_co_events_sharded(events, file_ids, n_files_total: int, group=None, na
     # exchanges (empty chunks included); the receiver concatenates the chunks' words and pieces in
     # arrival order, which keeps each piece's words where reduce_received expects them.
     n_chunks = chunks if chunks is not None else int(os.environ.get("OTTOHIP_DIST_CHUNKS", "2"))
-    # symmetric rules (click_to_click, cart_to_cart, buy_to_buy; model/count_co_events.py:64-71) go to the owners
-    # once per unordered pair: the row (a, b), a <= b, at owner(a), which also stands for its mirror (b, a) (the
-    # shard's readers produce it). Key cuts (branch (2)'s parts) need both orders stored; OTTOHIP_DIST_SYM=0 = off
-    sym = (cuts is None or (cuts.lo is None and cuts.hi is None)) and os.environ.get("OTTOHIP_DIST_SYM", "1") != "0"
     nf = len(events.file_bounds) - 1
     bounds = _chunk_files(events, max(1, n_chunks))
     names = reference_rules(names)[0]
@@ -654,8 +661,11 @@ def concat_files_w_stats_sharded(events, file_ids, n_files_total: int, name: str
         l0, l1 = int(np.searchsorted(fid, fa)), int(np.searchsorted(fid, fb + 1))
         cuts = FileCuts(name, lo=(fa, keys[(fa, lo)]) if lo > 0 else None,
                         hi=(fb, keys[(fb, hi)]) if hi < int(R[fb]) else None)
+        # one storage mode for every part (sym=False): a part whose boundaries both fall on file ends would
+        # otherwise store its mirrors at owner(min(a, b)) while the key-cut parts hold (b, a) at owner(b), and the
+        # owner-local merge below could not sum them
         t = count_co_events_sharded(events.subset_files(l0, l1), file_ids[l0:l1], n_files_total, group, [name],
-                                    n_items, stream=stream, ctx=ctx, cuts=cuts)
+                                    n_items, stream=stream, ctx=ctx, cuts=cuts, sym=False)
         pieces.append(finalize_sharded(t, name, max_rows_part, part, False, n_items, group, stream))
         t.free()
     dev = torch.device("cuda", ctx.device)

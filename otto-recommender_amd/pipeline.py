@@ -231,6 +231,7 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
     out = {"pairs": int(pairs), "candidates": int(n_cand), "local_candidates": cands.n_cand,
            "local_test_files": len(my_te),
            "test_sessions": int(test.n_sessions), "kmeans_iter": km.n_iter_, "kmeans_inertia": km.inertia_,
+           "kmeans_runs": list(km.run_stats_), "kmeans_best_run": km.best_run_,
            "recall": rec, "timings_s": T}
     if keep_tables:  # host copies of every stage's output, for the parity tests
         h = lambda x: x.cpu().numpy()
@@ -243,6 +244,7 @@ def run(train, test, labels, words_all, emb_all, words_12, emb_12, n_items: int 
         if keep_candidates:  # R7 of every candidate and the test sessions' C1 embeddings (small runs)
             out["intermediates"]["similarity"] = tuple(h(x) for x in sim)
             out["intermediates"]["test_session_embeddings"] = h(se_test)
+            out["intermediates"]["session_embeddings"] = h(se)  # C1 of every session: C2's input rows
         else:
             out["intermediates"]["similarity"] = sim
         if keep_candidates:

@@ -218,21 +218,25 @@ class KMeans:
         lanes = int(os.environ.get("OTTOHIP_KM_LANES", str(KM_LANES)))
         if group is None and not multi_ok and lanes >= 2 and self.n_init >= 2:
             best = self._fit_lanes(Xc, n, dim, k, seed_stream, tol_abs, ctx, min(lanes, self.n_init), half)
-            self.inertia_, C, self.labels_, self.n_iter_ = best
+            self.inertia_, C, self.labels_, self.n_iter_ = best[:4]
+            self.best_run_ = best[4]
             self.cluster_centers_ = C + mean_d
             return self
+        self.run_stats_ = []  # (inertia, n_iter) of every run, in run order
         for run in range(self.n_init):
             if pending:
                 res = pending.pop(0)
+                self.run_stats_.append((res[0], res[3]))
                 if best is None or res[0] < best[0]:
-                    best = res
+                    best = res + (run,)
                 continue
             if multi_ok and run + 1 < self.n_init:
                 g = min(grp, self.n_init - run, 4)
                 res = self._fit_multi(Xc, [next(seed_stream) for _ in range(g)], grows, tol_abs, ctx, sh)
                 pending = res[1:]
+                self.run_stats_.append((res[0][0], res[0][3]))
                 if best is None or res[0][0] < best[0]:
-                    best = res[0]
+                    best = res[0] + (run,)
                 continue
             seeds = next(seed_stream)
             C = self._gather_rows(Xc, seeds, grows, group)
@@ -284,9 +288,10 @@ class KMeans:
             _lib.check(lib.ottohip_kmeans_inertia(ctx.h, _lib.ptr(Xc), n, dim, _lib.ptr(C), _lib.ptr(labels),
                                                   ctypes.byref(inr), sh))
             inertia = float(_allreduce(torch.tensor([inr.value], dtype=torch.float64), group).item())
+            self.run_stats_.append((inertia, it))
             if best is None or inertia < best[0]:
-                best = (inertia, C.clone(), labels[:n].clone(), it)
-        self.inertia_, C, self.labels_, self.n_iter_ = best
+                best = (inertia, C.clone(), labels[:n].clone(), it, run)
+        self.inertia_, C, self.labels_, self.n_iter_, self.best_run_ = best
         self.cluster_centers_ = C + mean_d
         return self
 
@@ -380,9 +385,14 @@ class KMeans:
         if errors:
             raise errors[0]
         best = None
-        for res in results:  # run order: an equal inertia keeps the earlier run
+        self.run_stats_ = [(r[0], r[3]) for r in results]
+        for run, res in enumerate(results):  # run order: an equal inertia keeps the earlier run
             if best is None or res[0] < best[0]:
-                best = res
+                best = res + (run,)
+        # the kept run's tensors were allocated on its lane's stream and are used (and later freed) on the
+        # caller's: tell the caching allocator, so a reused pool stream cannot take their blocks early
+        best[1].record_stream(caller)
+        best[2].record_stream(caller)
         return best
 
     def _fit_multi(self, Xc, seeds, grows, tol_abs, ctx, sh):

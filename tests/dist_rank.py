@@ -30,14 +30,35 @@ def _my_events(ev, fb, files):
                         cat("type", np.int8)), bounds
 
 
+def structured_events(cfg):
+    """Events whose per-file click_to_click tables have exactly 2 * m_f rows (cfg["structured"] = [m_f per file]):
+    session j of every file clicks aids j and j + 5000 three times each, alternating, a minute apart, so its
+    table holds (j, j + 5000) and (j + 5000, j) with count 9, and the same keys recur in every file. The row
+    counts are chosen by the caller to put a branch-(2) part boundary exactly on a file end."""
+    import otto_recommender_amd.synth as synth
+    rows, fb, s = [], [0], 0
+    for m in cfg["structured"]:
+        for j in range(m):
+            for e in range(6):
+                rows.append((s, j if e % 2 == 0 else j + 5000, 1_000_000 + 60 * e, 0))
+            s += 1
+        fb.append(s)
+    a = np.array(rows, np.int64)
+    ev = synth.events_from_columns(a[:, 0], a[:, 1], a[:, 2], a[:, 3])
+    return ev, np.array(fb, np.int64)
+
+
 def covis(out, cfg):
     import torch
     import torch.distributed as dist
     import otto_recommender_amd.synth as synth
     from otto_recommender_amd import covis as gc, dist as gd, config
     rank, world = dist.get_rank(), dist.get_world_size()
-    ev = synth.generate(cfg["sessions"], first_session=cfg.get("first_session", 0))
-    fb = synth.file_session_bounds(ev.n_sessions, per_file=cfg["per_file"])
+    if "structured" in cfg:
+        ev, fb = structured_events(cfg)
+    else:
+        ev = synth.generate(cfg["sessions"], first_session=cfg.get("first_session", 0))
+        fb = synth.file_session_bounds(ev.n_sessions, per_file=cfg["per_file"])
     n_files = len(fb) - 1
     lens = np.diff(ev.session_offsets).astype(np.float64)
     w = [float((lens[fb[f]:fb[f + 1]] ** 2).sum()) for f in range(n_files)]

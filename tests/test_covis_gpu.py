@@ -315,6 +315,25 @@ def test_emit_record_guard_dense_sessions(gpu, monkeypatch):
     _assert_single_file(ev)
 
 
+@pytest.mark.parametrize("flush2,tasks", [("0", "1"), ("1", "0"), ("0", "0")])
+def test_emit_variants_single_pair_flush_and_type_loop(gpu, monkeypatch, flush2, tasks):
+    """The release (not OTTOHIP_DEBUG) emit in its non-default forms: the single-pair flush (OTTOHIP_EMIT_FLUSH2=0,
+    emit_flush: record index clamped, marks counted, err bit 8 on a mismatch) and the per-(rule, next type) loop
+    of pass 3 (OTTOHIP_EMIT_TASKS=0), on dense sessions (every flush full) and on a random slice: tables equal
+    the oracle's."""
+    monkeypatch.setenv("OTTOHIP_EMIT_FLUSH2", flush2)
+    monkeypatch.setenv("OTTOHIP_EMIT_TASKS", tasks)
+    rng = np.random.default_rng(31)
+    rows = []
+    for s_ in range(300):
+        ty = np.zeros(64, np.int64); ty[rng.choice(64, 2, replace=False)] = [1, 2]
+        rows.append(np.stack([np.full(64, s_), rng.choice(50_000, 64, replace=False),
+                              np.sort(rng.integers(0, 3600, 64)), ty], 1))
+    a = np.concatenate(rows)
+    _assert_single_file(synth.events_from_columns(a[:, 0], a[:, 1], a[:, 2], a[:, 3]))
+    _assert_single_file(synth.generate(3000, first_session=123_456))
+
+
 def test_per_file_rows_beyond_1024_files(gpu):
     """count_co_events_fused with per-file statistics over more files than the per-file histogram
     holds (1024), on a small item vocabulary (a pair word could tell 2^21 files apart): the call runs

@@ -166,11 +166,35 @@ def test_covis_sharded_full_size_config4(gpu, tmp_path):
           "words recv per rank", x[:, 2].tolist())
 
 
+def test_covis_sharded_part_boundary_on_file_end(gpu, tmp_path):
+    """Branch (2) with a part boundary exactly on a file end next to one that cuts a file: files of
+    400, 400, 600, 600, 400 click_to_click rows (tests/dist_rank.structured_events) in 3 parts of 800 rows, so
+    part 0 is files 0-1 whole (no key cut) and parts 1-2 meet inside file 3. Every part must use one storage
+    mode (dist.concat_files_w_stats_sharded counts all parts with sym=False): a symmetric part 0 would keep the
+    mirror (j + 5000, j) at owner(j) while parts 1-2 hold it at owner(j + 5000), and the owner-local merge of
+    the parts would leave the key split over two ranks (count 18 on one, 27 on the other, instead of 45)."""
+    from otto_recommender_amd.covis import part_plan
+    cfg = {"structured": [100, 100, 150, 150, 100], "rules": ["click_to_click"],
+           "merges": {"boundary": {"click_filter_rows": 10**9, "max_rows_groupby": 2_000, "optim_rows": 800,
+                                   "max_pairs": 10**6}}}
+    plan = part_plan([400, 400, 600, 600, 400], 3)
+    assert plan[:2] == [(0, 0, 1, 400), (2, 0, 3, 200)], plan  # part 0: whole files; part 1 ends inside file 3
+    res, per_file = _check_covis_sharded(cfg, tmp_path, world=2)
+    assert [len(p["click_to_click"][0]) for p in per_file] == [400, 400, 600, 600, 400]
+    f = res[0]["final/boundary/click_to_click"]
+    m = (f[:, 0] >= 5000) & (f[:, 1] < 100)
+    assert m.sum() == 100 and set(f[m, 2].tolist()) == {45}  # (j + 5000, j) summed over all three parts
+
+
 def _check_covis_sharded(cfg, tmp_path, world, timeout=240):
     import otto_recommender_amd.synth as synth
     res = _launch("covis", cfg, tmp_path, world=world, timeout=timeout)
-    ev = synth.generate(cfg["sessions"], first_session=cfg["first_session"])
-    fb = synth.file_session_bounds(ev.n_sessions, per_file=cfg["per_file"])
+    if "structured" in cfg:
+        from dist_rank import structured_events
+        ev, fb = structured_events(cfg)
+    else:
+        ev = synth.generate(cfg["sessions"], first_session=cfg["first_session"])
+        fb = synth.file_session_bounds(ev.n_sessions, per_file=cfg["per_file"])
     per_file = oracle.count_co_events_files(ev.session_offsets, ev.aid, ev.ts, ev.type, fb)
     files = np.concatenate([r["files"] for r in res])
     assert sorted(files.tolist()) == list(range(len(fb) - 1)) and all(len(r["files"]) for r in res)
@@ -187,6 +211,8 @@ def _check_covis_sharded(cfg, tmp_path, world, timeout=240):
                                           err_msg=f"shard {r} {n}")
             np.testing.assert_array_equal(got[f"stats/{n}"], [len(a), int((c >= 2).sum())])
         for tag, kw in cfg["merges"].items():
+            if n not in cfg.get("rules", NAMES):
+                continue
             ref = np.stack([np.asarray(x, np.int64) for x in
                             oracle.concat_files_w_stats(n, [p[n] for p in per_file], **kw)], 1)
             for r, got in enumerate(res):
