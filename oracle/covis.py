@@ -24,7 +24,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_SO = os.path.join(_HERE, "_build", "libcovis_oracle.so")
+# OTTO_ORACLE_SO: another build of the same source (the sanitized one, tests/test_sanitize.py)
+_SO = os.environ.get("OTTO_ORACLE_SO") or os.path.join(_HERE, "_build", "libcovis_oracle.so")
 
 # config.py:41-42
 MIN_TIME_TO_NEXT = -24 * 60 * 60

@@ -73,36 +73,49 @@ void alloc_log_end(double t0, const char* what, const char* name, size_t bytes) 
           1e3 * (t.tv_sec + 1e-9 * t.tv_nsec - t0), fr / 1e9);
 }
 
-// ---- device block cache (common.h)
+// ---- device block cache (common.h), one per device: a block is handed out again only on the device it was
+// allocated on, and a trim (ottohip_ctx_trim) returns only the calling device's free blocks, so one context's
+// trim never frees what another device's contexts cache
 static std::mutex g_cache_mu;
-static std::multimap<size_t, void*> g_cache_free;  // size -> block
-static std::map<void*, size_t> g_cache_live;       // block -> size
+struct DevCache {
+  std::multimap<size_t, void*> free_;  // size -> block
+};
+static std::map<int, DevCache> g_cache;                       // device -> its free blocks
+static std::map<void*, std::pair<int, size_t>> g_cache_live;  // block -> (device, size)
+
+static int cur_device() {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  return d;
+}
 
 hipError_t dev_alloc(void** p, size_t bytes, const char* what) {
   std::lock_guard<std::mutex> lk(g_cache_mu);
-  auto it = g_cache_free.lower_bound(bytes);
-  if (it != g_cache_free.end() && it->first <= 2 * bytes) {
+  const int dev = cur_device();
+  auto& fr = g_cache[dev].free_;
+  auto it = fr.lower_bound(bytes);
+  if (it != fr.end() && it->first <= 2 * bytes) {
     *p = it->second;
-    g_cache_live[it->second] = it->first;
-    g_cache_free.erase(it);
+    g_cache_live[it->second] = {dev, it->first};
+    fr.erase(it);
     return hipSuccess;
   }
   const double t0 = alloc_log_begin();
   hipError_t e = hipMalloc(p, bytes);
-  if (e != hipSuccess && !g_cache_free.empty()) {  // give the cached blocks back and retry once
+  if (e != hipSuccess && !fr.empty()) {  // give this device's cached blocks back and retry once
     (void)hipGetLastError();
     (void)hipDeviceSynchronize();
-    for (auto& kv : g_cache_free) (void)hipFree(kv.second);
-    g_cache_free.clear();
+    for (auto& kv : fr) (void)hipFree(kv.second);
+    fr.clear();
     e = hipMalloc(p, bytes);
   }
   alloc_log_end(t0, "hipMalloc", what, bytes);
   if (e != hipSuccess) { (void)hipGetLastError(); *p = nullptr; return e; }
-  g_cache_live[*p] = bytes;
+  g_cache_live[*p] = {dev, bytes};
   return hipSuccess;
 }
 
-// cached bytes are capped (OTTOHIP_CACHE_GB, default 128) so memory the library no longer uses
+// cached bytes are capped per device (OTTOHIP_CACHE_GB, default 128) so memory the library no longer uses
 // stays available to other allocators in the process (torch)
 static size_t cache_cap() {
   static const size_t cap = (size_t)((getenv("OTTOHIP_CACHE_GB") ? atof(getenv("OTTOHIP_CACHE_GB")) : 128.0) * 1e9);
@@ -114,25 +127,33 @@ void dev_free(void* p) {
   std::lock_guard<std::mutex> lk(g_cache_mu);
   auto it = g_cache_live.find(p);
   if (it == g_cache_live.end()) { (void)hipFree(p); return; }
-  g_cache_free.emplace(it->second, p);
+  const int dev = it->second.first;
+  auto& fr = g_cache[dev].free_;
+  fr.emplace(it->second.second, p);
   g_cache_live.erase(it);
   size_t tot = 0;
-  for (auto& kv : g_cache_free) tot += kv.first;
-  while (tot > cache_cap() && !g_cache_free.empty()) {  // largest blocks go back first
-    auto last = std::prev(g_cache_free.end());
+  for (auto& kv : fr) tot += kv.first;
+  if (tot <= cache_cap()) return;
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  if (prev != dev) (void)hipSetDevice(dev);
+  while (tot > cache_cap() && !fr.empty()) {  // largest blocks go back first
+    auto last = std::prev(fr.end());
     tot -= last->first;
     (void)hipDeviceSynchronize();
     (void)hipFree(last->second);
-    g_cache_free.erase(last);
+    fr.erase(last);
   }
+  if (prev != dev) (void)hipSetDevice(prev);
 }
 
 void dev_trim() {
   std::lock_guard<std::mutex> lk(g_cache_mu);
-  if (g_cache_free.empty()) return;
+  auto it = g_cache.find(cur_device());
+  if (it == g_cache.end() || it->second.free_.empty()) return;
   (void)hipDeviceSynchronize();
-  for (auto& kv : g_cache_free) (void)hipFree(kv.second);
-  g_cache_free.clear();
+  for (auto& kv : it->second.free_) (void)hipFree(kv.second);
+  it->second.free_.clear();
 }
 }
 

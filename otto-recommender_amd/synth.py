@@ -39,7 +39,8 @@ class _Params(ctypes.Structure):
 def _lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(_HERE, "libottosynth.so")
+        # OTTOSYNTH_SO: another build of synth.cpp (the sanitized one, tests/test_sanitize.py)
+        path = os.environ.get("OTTOSYNTH_SO") or os.path.join(_HERE, "libottosynth.so")
         if not os.path.exists(path):
             raise RuntimeError(f"{path} missing: run __graft_entry__.build() (make -C csrc)")
         lib = ctypes.CDLL(path)
