@@ -281,6 +281,33 @@ static ottohip_table* new_table(ottohip_ctx* ctx, int n_rules, int32_t n_items) 
   return T;
 }
 
+// The multi-GPU row keys' owner map for (n_items, G), in the context workspace: a2l[aid] = the aid's index among
+// the aids of its owner (aid order), l2a[obase[o] + i] = the inverse; *LB = bits of the largest owner's count.
+static int owner_map(ottohip_ctx* ctx, int32_t n_items, int G, hipStream_t s, const uint32_t** a2l,
+                     const uint32_t** l2a, const uint32_t** obase, int* LB) {
+  uint32_t *da2l, *dl2a, *dob;
+  OH_TRY(ctx->ws.get("om_a2l", (size_t)std::max(n_items, 1), &da2l));
+  OH_TRY(ctx->ws.get("om_l2a", (size_t)std::max(n_items, 1), &dl2a));
+  OH_TRY(ctx->ws.get("om_obase", (size_t)G + 1, &dob));
+  if (ctx->om_items != n_items || ctx->om_parts != G) {
+    std::vector<uint32_t> cnt(G + 1, 0), a2l_h(std::max(n_items, 1)), l2a_h(std::max(n_items, 1));
+    for (int32_t a = 0; a < n_items; ++a) a2l_h[a] = cnt[owner_dev((uint32_t)a, (uint32_t)G)]++;
+    uint32_t mx = 0;
+    std::vector<uint32_t> ob(G + 1, 0);
+    for (int o = 0; o < G; ++o) { mx = std::max(mx, cnt[o]); ob[o + 1] = ob[o] + cnt[o]; }
+    for (int32_t a = 0; a < n_items; ++a) l2a_h[ob[owner_dev((uint32_t)a, (uint32_t)G)] + a2l_h[a]] = (uint32_t)a;
+    OH_HIP(hipMemcpyAsync(da2l, a2l_h.data(), (size_t)n_items * 4, hipMemcpyHostToDevice, s));
+    OH_HIP(hipMemcpyAsync(dl2a, l2a_h.data(), (size_t)n_items * 4, hipMemcpyHostToDevice, s));
+    OH_HIP(hipMemcpyAsync(dob, ob.data(), (size_t)(G + 1) * 4, hipMemcpyHostToDevice, s));
+    OH_HIP(hipStreamSynchronize(s));  // the host vectors go out of scope
+    ctx->om_items = n_items;
+    ctx->om_parts = G;
+    ctx->om_lb = std::max(1, bits_for((uint64_t)mx));
+  }
+  *a2l = da2l; *l2a = dl2a; *obase = dob; *LB = ctx->om_lb;
+  return 0;
+}
+
 // S1 prep, S2 count, S3 rows. n_parts > 1: owner-major rows, and (emit handle) owner bounds.
 static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip_covis_params* params,
                        const int32_t* file_ids, int n_parts, Front& F, hipStream_t s, ottohip_emit* EM = nullptr) {
@@ -325,7 +352,17 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
   // the byte above the sorted key bits, and the sort generates the event positions itself
   static const bool rows_legacy = getenv("OTTOHIP_ROWS") && !strcmp(getenv("OTTOHIP_ROWS"), "legacy");
   const int cshift = (Lt.A + 2 + 7) / 8 * 8;  // first byte above the sorted key bits
-  const bool fused = !rows_legacy && n_parts == 1 && cshift + 8 <= 32 &&
+  // n_parts > 1: the fused layout with owner-local aid indices when (owner, type, local index) and the invalid
+  // key G << (LB + 2) fit below the count byte (OTTOHIP_OWNER_LOCAL=0: the 4-pass owner-key sort)
+  const bool ol_env = !(getenv("OTTOHIP_OWNER_LOCAL") && !strcmp(getenv("OTTOHIP_OWNER_LOCAL"), "0"));  // per call
+  const uint32_t *om_a2l = nullptr, *om_l2a = nullptr, *om_obase = nullptr;
+  int om_lb = 0;
+  bool owner_local = false;
+  if (!rows_legacy && n_parts > 1 && ol_env && cshift + 8 <= 32 && 3ull * (uint64_t)params->n_items < (1ull << 24)) {
+    OH_TRY(owner_map(ctx, params->n_items, n_parts, s, &om_a2l, &om_l2a, &om_obase, &om_lb));
+    owner_local = ((uint64_t)n_parts << (om_lb + 2)) < (1ull << cshift);
+  }
+  const bool fused = !rows_legacy && (n_parts == 1 || owner_local) && cshift + 8 <= 32 &&
                      3ull * (uint64_t)params->n_items < (1ull << 24);
   uint32_t* pos_w = fused ? nullptr : pos;
   int ph = ctx->begin("prep_count", s, 9.0 * E + 8.0 * (Sn + 1) + 8.0 * E + 12.0 * E);
@@ -395,14 +432,21 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
   }
   uint32_t INV = 3u << Lt.A;
   int kbits = Lt.A + 2;
-  if (n_parts > 1) {
+  uint32_t kmask = Lt.A + 2 >= 32 ? ~0u : (1u << (Lt.A + 2)) - 1u;
+  if (owner_local) {
+    const uint32_t INV2 = (uint32_t)n_parts << (om_lb + 2);
+    k_owner_key_local<<<grid_for(E), 256, 0, s>>>(rk, E, INV, Lt.A, (uint32_t)n_parts, om_lb, INV2,
+                                                 (1u << cshift) - 1u, om_a2l);
+    INV = INV2;
+    kbits = bits_for((uint64_t)INV2 + 1);
+    kmask = (1u << cshift) - 1u;
+  } else if (n_parts > 1) {
     const uint32_t INV2 = (uint32_t)n_parts << (Lt.A + 2);
     k_owner_key<<<grid_for(E), 256, 0, s>>>(rk, E, INV, Lt.A, (uint32_t)n_parts, INV2);
     INV = INV2;
     kbits = Lt.A + 2 + bits_for((uint64_t)n_parts + 1);
     if (kbits > 32) { set_error("row key with owner bits > 32 bits"); return OTTOHIP_ELIMIT; }
   }
-  const uint32_t kmask = Lt.A + 2 >= 32 ? ~0u : (1u << (Lt.A + 2)) - 1u;
   // fused layout: counts ride in the keys' spare bits (written by S2), one u64 scan carries word
   // offset and row index; the sort's first pass takes the event positions from its own indices
   uint32_t *rks = rk, *poss = pos;
@@ -458,6 +502,9 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
       k_rows_tile<<<(unsigned)nb, RT_T, 0, s>>>(rks, poss, F.cnt, E, kmask, INV, cshift, boff, F.poff, nullptr, 0u, 0u,
                                                 1, F.row_key, F.row_begin);
     }
+    // owner-local keys back to (type, aid): the rows downstream (owner bounds, pieces, reduce) read those
+    if (owner_local && F.Rn > 0)
+      k_rows_decode<<<grid_for(F.Rn), 256, 0, s>>>(F.row_key, F.Rn, Lt.A, om_lb, om_obase, om_l2a);
     OH_HIP(hipGetLastError());
     ctx->end(ph, s);
     return 0;
@@ -930,6 +977,7 @@ int ottohip_ctx_trim(ottohip_ctx* ctx) {
   dev_trim();
   ctx->km_bvalid = false;  // the KMeans distance bounds lived in the released workspace
   ctx->km_hX = nullptr;     // and the attached half-precision rows
+  ctx->om_items = -1;       // and the owner map
   return 0;
 }
 

@@ -139,6 +139,10 @@ struct Ctx {
   int km_hdim = 0;
   const void* km_x16 = nullptr;
   const float* km_xn2 = nullptr;
+  // multi-GPU row keys (abi.hip owner_map): per aid its index among its owner's aids (aid order) and the inverse,
+  // for (n_items, G) = (om_items, om_parts); om_lb = bits of the largest owner's aid count
+  int64_t om_items = -1;
+  int om_parts = 0, om_lb = 0;
 };
 
 inline int bits_for(uint64_t n_values) {  // bits needed to store values in [0, n_values)

@@ -802,6 +802,26 @@ __global__ void k_owner_key(uint32_t* __restrict__ rk, int64_t n, uint32_t INV, 
   rk[k] = key == INV ? INV2 : ((owner_dev(key & ((1u << A) - 1u), G) << (A + 2)) | key);
 }
 
+// the same owner-major order in fewer key bits (the fused row layout): (owner, type, the aid's index among its
+// owner's aids), the count byte at cshift kept. Local indices follow aid order, so the sort order is the one of
+// (owner, type, aid); k_rows_decode turns the rows' keys back into (type, aid)
+__global__ void k_owner_key_local(uint32_t* __restrict__ rk, int64_t n, uint32_t INV, int A, uint32_t G, int LB,
+                                  uint32_t INV2, uint32_t kmask, const uint32_t* __restrict__ a2l) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t x = rk[k], key = x & kmask, hi = x & ~kmask;
+  if (key == INV) { rk[k] = hi | INV2; return; }
+  const uint32_t aid = key & ((1u << A) - 1u), t = key >> A;
+  rk[k] = hi | (owner_dev(aid, G) << (LB + 2)) | (t << LB) | a2l[aid];
+}
+__global__ void k_rows_decode(uint32_t* __restrict__ row_key, int64_t R, int A, int LB,
+                              const uint32_t* __restrict__ obase, const uint32_t* __restrict__ l2a) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const uint32_t k = row_key[r], o = k >> (LB + 2), t = (k >> LB) & 3u, loc = k & ((1u << LB) - 1u);
+  row_key[r] = (t << A) | l2a[obase[o] + loc];
+}
+
 // first row of every owner (rows are owner-major); first_row[G] = R
 __global__ void k_part_bounds(const uint32_t* __restrict__ row_key, int64_t R, int A, uint32_t G,
                               uint64_t* __restrict__ first_row) {

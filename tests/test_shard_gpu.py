@@ -206,6 +206,24 @@ def test_pair_exchange_equals_global_count(gpu, three_files, ranks, sym):
         shard.free()
 
 
+@pytest.mark.parametrize("G", [2, 3, 8, 16])
+def test_owner_local_keys_equal_owner_key_sort(gpu, three_files, monkeypatch, G):
+    """The multi-GPU rows phase on owner-local aid indices (the fused layout: (owner, type, the aid's index among its
+    owner's aids) in 24 key bits, 3 radix passes, rows decoded back to (type, aid)) writes the same send segments as
+    the 4-pass sort of (owner, type, aid) keys (OTTOHIP_OWNER_LOCAL=0): words, word and piece counts per owner, and
+    the pieces, bit for bit (local indices follow aid order, so both sorts give one order)."""
+    from otto_recommender_amd import covis as gc, dist as gd
+    ev, fb, _, _ = three_files
+    outs = []
+    for ol in ("0", "1"):
+        monkeypatch.setenv("OTTOHIP_OWNER_LOCAL", ol)
+        w, wpp, pc, ppp, names = gd.emit_for_owners(gc.DeviceEvents.from_host(ev, fb), G, None, 3, sym=True)
+        outs.append((w.cpu().numpy(), list(wpp), pc.cpu().numpy(), list(ppp)))
+    assert outs[0][1] == outs[1][1] and outs[0][3] == outs[1][3]
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][2], outs[1][2])
+
+
 @pytest.mark.parametrize("sym", [False, True])
 def test_pair_exchange_single_owner_matches_count(gpu, three_files, sym):
     """n_parts = 1 through emit/reduce_received reproduces ottohip_covis_count exactly (with and without
