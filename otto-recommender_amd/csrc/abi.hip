@@ -173,6 +173,7 @@ struct Front {
   uint64_t* lscr = nullptr;
   uint32_t* lpscr = nullptr;
   uint32_t* cnt = nullptr;
+  uint32_t* link = nullptr;    // grouped row entries (one-GPU / owner-local fused layout), else null
   uint64_t* poff = nullptr;
   uint32_t* poff32 = nullptr;  // instead of poff when every word offset < 2^32 (one-GPU fused layout)
   uint64_t P = 0;
@@ -365,10 +366,16 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
   const bool fused = !rows_legacy && (n_parts == 1 || owner_local) && cshift + 8 <= 32 &&
                      3ull * (uint64_t)params->n_items < (1ull << 24);
   uint32_t* pos_w = fused ? nullptr : pos;
+  static const bool rows_atomic = getenv("OTTOHIP_ROWS") && !strcmp(getenv("OTTOHIP_ROWS"), "atomic");
+  // grouped row entries (fused layout): one S3 sort entry per (session, type, aid) with pairs; OTTOHIP_GROUP=0: one per
+  // event (read per call, A/B switch)
+  const bool group = fused && !rows_atomic && !(getenv("OTTOHIP_GROUP") && !strcmp(getenv("OTTOHIP_GROUP"), "0"));
+  F.link = nullptr;
+  if (group) OH_TRY(ws.get("link", (size_t)E, &F.link));
   int ph = ctx->begin("prep_count", s, 9.0 * E + 8.0 * (Sn + 1) + 8.0 * E + 12.0 * E);
   k_block_first<<<grid_for(Sn + 1), 256, 0, s>>>(off, Sn, NB, F.first, F.long_list, n_long);
   k_prep_count<<<(unsigned)NB, 64, 0, s>>>(off, F.first, NB, ev->aid, ev->ts, ev->type, F.evp, params->n_items,
-                                           params->dedup, err, R, Lt.A, F.cnt, rk, pos_w, fused ? cshift : 0);
+                                           params->dedup, err, R, Lt.A, F.cnt, rk, pos_w, fused ? cshift : 0, F.link);
   if (hipGetLastError() != hipSuccess) { set_error("k_prep_count launch failed"); return OTTOHIP_EHIP; }
   int32_t nl = 0;
   OH_TRY(d2h(&nl, n_long, 1, s));
@@ -392,14 +399,13 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
     k_prep_long<<<nl, 64, 0, s>>>(off, F.long_list, F.d_loff, F.lscr, ev->aid, ev->ts, ev->type, F.evp,
                                   params->n_items, params->dedup, err);
     k_count_long<<<nl, 64, 0, s>>>(off, F.long_list, F.d_loff, F.lscr, F.lpscr, F.evp, R, Lt.A, F.cnt, rk, pos_w,
-                                   fused ? cshift : 0);
+                                   fused ? cshift : 0, F.link);
     if (hipGetLastError() != hipSuccess) { set_error("long-session launch failed"); return OTTOHIP_EHIP; }
   }
   ctx->end(ph, s);
 
   // ---- S3 rows (aid-major transpose; owner-major first when n_parts > 1)
   ph = ctx->begin("rows", s, 0);
-  static const bool rows_atomic = getenv("OTTOHIP_ROWS") && !strcmp(getenv("OTTOHIP_ROWS"), "atomic");
   if (rows_atomic && fused) {  // no sort: dense rows, per-event ranks by returning atomics (k_rows_atomic)
     const uint32_t INVa = 3u << Lt.A;
     const uint32_t kmask_a = Lt.A + 2 >= 32 ? ~0u : (1u << (Lt.A + 2)) - 1u;
@@ -450,15 +456,21 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
   // fused layout: counts ride in the keys' spare bits (written by S2), one u64 scan carries word
   // offset and row index; the sort's first pass takes the event positions from its own indices
   uint32_t *rks = rk, *poss = pos;
-  OH_TRY(radix_sort_pairs(ctx, rks, poss, rk2, pos2, E, kbits, s, fused));
+  // fused layout: the sort's first pass drops the keys without a row entry (events without pairs; grouped: members),
+  // the later passes and the row passes below run over the En kept entries
+  int64_t En = E;
+  const SortSkip skip{fused ? (1u << cshift) - 1u : 0u, INV, &En};
+  OH_TRY(radix_sort_pairs(ctx, rks, poss, rk2, pos2, E, kbits, s, fused, fused ? &skip : nullptr));
   uint64_t* tot;
   OH_TRY(ws.get("tot", 4, &tot));
   if (fused) {
-    const int64_t nb = ceil_div(E, RT_TILE);
+    // saturated count bytes are read back from the link array (grouped: the group's total) or the counts
+    const uint32_t* csrc = F.link ? F.link : F.cnt;
+    const int64_t nb = ceil_div(En, RT_TILE);
     uint64_t *bsum, *boff;
-    OH_TRY(ws.get("rt_sums", (size_t)nb, &bsum));
-    OH_TRY(ws.get("rt_offs", (size_t)nb, &boff));
-    k_rows_sums<<<(unsigned)nb, RT_T, 0, s>>>(rks, poss, F.cnt, E, kmask, INV, cshift, bsum);
+    OH_TRY(ws.get("rt_sums", (size_t)std::max<int64_t>(nb, 1), &bsum));
+    OH_TRY(ws.get("rt_offs", (size_t)std::max<int64_t>(nb, 1), &boff));
+    if (nb > 0) k_rows_sums<<<(unsigned)nb, RT_T, 0, s>>>(rks, poss, csrc, En, kmask, INV, cshift, bsum);
     OH_TRY(exclusive_scan_u64(ctx, bsum, boff, nb, tot, s));
     uint64_t X = 0;
     OH_TRY(d2h(&X, tot, 1, s));
@@ -479,29 +491,32 @@ static int covis_front(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip
       // (position, offset) pairs by the positions' top 8 bits, and the final scatter writes one
       // 1/256 slice of poff32 at a time (OTTOHIP_POFF_PART=0: the tile pass scatters directly)
       static const char* ppenv = getenv("OTTOHIP_POFF_PART");  // A/B switch
-      if (!(ppenv && !strcmp(ppenv, "0")) && E > 4096) {
+      if (!(ppenv && !strcmp(ppenv, "0")) && En > 4096) {
         uint32_t* rkA = rks == rk ? rk2 : rk;  // the sort's idle pair
         uint32_t* posA = poss == pos ? pos2 : pos;
-        k_rows_tile<<<(unsigned)nb, RT_T, 0, s>>>(rks, poss, F.cnt, E, kmask, INV, cshift, boff, nullptr, F.poff32, 0u,
+        k_rows_tile<<<(unsigned)nb, RT_T, 0, s>>>(rks, poss, csrc, En, kmask, INV, cshift, boff, nullptr, F.poff32, 0u,
                                                   0xFFFFFFFFu, 1, F.row_key, F.row_begin, rkA);
         const uint64_t* dstart = nullptr;
         int ntl = 0;
-        OH_TRY(radix_pass(ctx, poss, rkA, posA, rks, E, std::max(0, bits_for((uint64_t)E) - 8), s, &dstart, &ntl));
+        OH_TRY(radix_pass(ctx, poss, rkA, posA, rks, En, std::max(0, bits_for((uint64_t)E) - 8), s, &dstart, &ntl));
         // OTTOHIP_POFF_XCD=1: the XCD-aware scatter (A/B switch, off: 6.47 vs 6.85 GB written per build, slower)
         static const bool pxcd = getenv("OTTOHIP_POFF_XCD") && !strcmp(getenv("OTTOHIP_POFF_XCD"), "1");
         if (pxcd)
-          k_poff_scatter_xcd<<<(unsigned)(8 * std::max(1, ctx->n_cu)), 256, 0, s>>>(posA, rks, E, dstart, ntl, F.poff32);
+          k_poff_scatter_xcd<<<(unsigned)(8 * std::max(1, ctx->n_cu)), 256, 0, s>>>(posA, rks, En, dstart, ntl, F.poff32);
         else
-          k_poff_scatter<<<grid_for(E), 256, 0, s>>>(posA, rks, E, F.poff32);
-      } else {
-        k_rows_tile<<<(unsigned)nb, RT_T, 0, s>>>(rks, poss, F.cnt, E, kmask, INV, cshift, boff, nullptr, F.poff32, 0u,
+          k_poff_scatter<<<grid_for(En), 256, 0, s>>>(posA, rks, En, F.poff32);
+      } else if (nb > 0) {
+        k_rows_tile<<<(unsigned)nb, RT_T, 0, s>>>(rks, poss, csrc, En, kmask, INV, cshift, boff, nullptr, F.poff32, 0u,
                                                   0xFFFFFFFFu, 1, F.row_key, F.row_begin);
       }
     } else {
       OH_TRY(ws.get("poff", (size_t)E, &F.poff));
-      k_rows_tile<<<(unsigned)nb, RT_T, 0, s>>>(rks, poss, F.cnt, E, kmask, INV, cshift, boff, F.poff, nullptr, 0u, 0u,
-                                                1, F.row_key, F.row_begin);
+      if (nb > 0)
+        k_rows_tile<<<(unsigned)nb, RT_T, 0, s>>>(rks, poss, csrc, En, kmask, INV, cshift, boff, F.poff, nullptr, 0u, 0u,
+                                                  1, F.row_key, F.row_begin);
     }
+    // grouped row entries: every member's word offset from its rep's (the emit reads one offset per event)
+    if (F.link) k_link_fix<<<grid_for(E, 256 * LF_PER), 256, 0, s>>>(F.link, E, F.poff32, F.poff);
     // owner-local keys back to (type, aid): the rows downstream (owner bounds, pieces, reduce) read those
     if (owner_local && F.Rn > 0)
       k_rows_decode<<<grid_for(F.Rn), 256, 0, s>>>(F.row_key, F.Rn, Lt.A, om_lb, om_obase, om_l2a);
@@ -550,10 +565,10 @@ static int covis_emit_words(ottohip_ctx* ctx, const Front& F, const ottohip_even
                   : (tasks ? (fl2 ? k_emit<false, true, true> : k_emit<false, true, false>) : k_emit<false, false, true>);
   if (F.NB > 0)
     ek<<<(unsigned)F.NB, 64, 0, s>>>(F.off, F.first, F.NB, F.evp, F.R, F.Lt, F.fb, ev->n_files, F.fid, F.cnt,
-                                         EvOff{F.poff, F.poff32}, w0, eerr, dbg);
+                                         EvOff{F.poff, F.poff32, nullptr}, w0, eerr, dbg);
   if (F.nl > 0)
     k_emit_long<<<F.nl, 64, 0, s>>>(F.off, F.long_list, F.d_loff, F.lscr, F.lpscr, F.evp, F.R, F.Lt, F.fb,
-                                     ev->n_files, F.fid, F.cnt, EvOff{F.poff, F.poff32}, w0);
+                                     ev->n_files, F.fid, F.cnt, EvOff{F.poff, F.poff32, nullptr}, w0);
   if (hipGetLastError() != hipSuccess) { set_error("k_emit launch failed"); return OTTOHIP_EHIP; }
   ctx->end(ph, s);
   int herr = 0;

@@ -329,13 +329,25 @@ __device__ __forceinline__ uint32_t count_event(const SessView& S, int i, const 
 // the row key of an event, with (cshift > 0: the fused row layout of S3) its pair count saturated
 // at RK_CSAT in the byte above the sorted key bits
 constexpr uint32_t RK_CSAT = 255u;
+
+// Grouped row entries (the fused row layout, S2 -> S3 -> S4). The events of one session with the same (type, aid) and
+// a nonzero pair count form one group; only one of them (the group's rep) enters the S3 sort, with the group's total
+// count, and the group's words are one run of its row: a member's run starts at the rep's word offset plus its
+// prefix gpre inside the group (the order of words inside a row is free: the reduce sorts them). Per event, link[e]:
+//   LK_REP | count   the event is its own row entry (a rep: count = the group's total; a long session's event; an event
+//                    without pairs, count 0)
+//   (delta + 512) << 21 | gpre   a member: its rep is event e + delta (|delta| < 512, same batch), gpre < 2^21
+// (gpre < 512 members x MAX_RULES x 511 partners < 2^21)
+constexpr uint32_t LK_REP = 0x80000000u;
+constexpr int LK_DSHIFT = 21;
+constexpr uint32_t LK_GMASK = (1u << LK_DSHIFT) - 1u;
 __device__ __forceinline__ uint32_t rk_with_count(uint32_t key, uint32_t c, int cshift) {
   return cshift ? key | ((c < RK_CSAT ? c : RK_CSAT) << cshift) : key;
 }
 
 __device__ __forceinline__ void count_session(const SessView& S, int64_t e0, int n, const RulesDev& R, int A,
                                               uint32_t* __restrict__ cnt, uint32_t* __restrict__ rk,
-                                              uint32_t* __restrict__ pos, int cshift) {
+                                              uint32_t* __restrict__ pos, int cshift, uint32_t* __restrict__ link) {
   const uint32_t INV = 3u << A;
   for (int k = lane_id(); k < n; k += 64) {
     uint32_t c = 0, key = INV;
@@ -346,6 +358,7 @@ __device__ __forceinline__ void count_session(const SessView& S, int64_t e0, int
     cnt[e0 + k] = c;
     rk[e0 + k] = rk_with_count(key, c, cshift);
     if (pos) pos[e0 + k] = (uint32_t)(e0 + k);
+    if (link) link[e0 + k] = LK_REP | c;  // a long session's events are not grouped: every event is its own row entry
   }
 }
 
@@ -354,7 +367,7 @@ __global__ __launch_bounds__(64) void k_count_long(const int64_t* __restrict__ o
                                                    uint64_t* __restrict__ scratch, uint32_t* __restrict__ pscratch,
                                                    const uint64_t* __restrict__ ev, RulesDev R, int A,
                                                    uint32_t* __restrict__ cnt, uint32_t* __restrict__ rk,
-                                                   uint32_t* __restrict__ pos, int cshift) {
+                                                   uint32_t* __restrict__ pos, int cshift, uint32_t* __restrict__ link) {
   const int64_t s = list[blockIdx.x];
   const int64_t e0 = off[s];
   const int n = (int)(off[s + 1] - e0);
@@ -364,7 +377,7 @@ __global__ __launch_bounds__(64) void k_count_long(const int64_t* __restrict__ o
   uint32_t* pref = pscratch + 3 * (so + blockIdx.x);
   S.ev = evs; S.pref = pref; S.pstride = n + 1;
   S.nv = load_session(ev + e0, n, evs, pref, n + 1);
-  count_session(S, e0, n, R, A, cnt, rk, pos, cshift);
+  count_session(S, e0, n, R, A, cnt, rk, pos, cshift, link);
 }
 
 // ------------------------------------------------------------------ S1+S2 fused
@@ -402,13 +415,15 @@ struct PrepLds {
   uint8_t esid[PB_CAP];
   uint8_t uns[64];        // session has a ts decrease: full ranking
 };
+static_assert((uint64_t)PB_CAP * MAX_RULES * (LCAP - 1) < (1ull << LK_DSHIFT), "group prefixes in link bits");
 
 __global__ __launch_bounds__(64) void k_prep_count(const int64_t* __restrict__ off, const int64_t* __restrict__ first,
                                                    int64_t NB, const int32_t* __restrict__ aid,
                                                    const int32_t* __restrict__ ts, const int8_t* __restrict__ ty,
                                                    uint64_t* __restrict__ ev, int n_items, int dedup, int* err,
                                                    RulesDev R, int A, uint32_t* __restrict__ cnt,
-                                                   uint32_t* __restrict__ rk, uint32_t* __restrict__ pos, int cshift) {
+                                                   uint32_t* __restrict__ rk, uint32_t* __restrict__ pos, int cshift,
+                                                   uint32_t* __restrict__ link) {
   __shared__ PrepLds S;
   __shared__ RulesDev sR;
   const int l = threadIdx.x;
@@ -535,6 +550,10 @@ __global__ __launch_bounds__(64) void k_prep_count(const int64_t* __restrict__ o
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     // ---- partner counts and row keys
+    constexpr int NCH = PB_CAP / 64;
+    uint32_t cv[NCH];  // grouped rows: the counts of the lane's events (c is wave-uniform: a select per chunk)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) cv[c] = 0u;
 #pragma unroll 1
     for (int c = 0; c < nch; ++c) {
       const int idx = c * 64 + l;
@@ -577,11 +596,93 @@ __global__ __launch_bounds__(64) void k_prep_count(const int64_t* __restrict__ o
         if (cn) key = ((uint32_t)t << A) | (uint32_t)ev_aid(e);
       }
       cnt[E0 + idx] = cn;
-      rk[E0 + idx] = rk_with_count(key, cn, cshift);
-      if (pos) pos[E0 + idx] = (uint32_t)(E0 + idx);
+      if (link) {
+#pragma unroll
+        for (int j = 0; j < NCH; ++j)
+          if (j == c) cv[j] = cn;
+      } else {
+        rk[E0 + idx] = rk_with_count(key, cn, cshift);
+        if (pos) pos[E0 + idx] = (uint32_t)(E0 + idx);
+      }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (link) {
+      // ---- grouped row entries (LK_REP): events of one session with equal (type, aid) and pairs, found by an LDS
+      // hash over (aid, session, type); each member takes its prefix in the group by one LDS atomic add, the
+      // member that gets 0 is the rep and publishes its position. The hash overlays the dead prefix counts (keys)
+      // and the batch's events (sums: the group keys are read into registers first; the events are stored).
+      uint32_t gk[NCH], sg[NCH];  // sg: the pair count, then slot << 22 | prefix
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int idx = c * 64 + l;
+        gk[c] = 0u;
+        sg[c] = 0u;
+        if (c < nch && idx < nb_ev) {
+          const uint64_t e = S.key[idx];
+          sg[c] = cv[c];
+          if (e != EV_INVALID && sg[c] != 0)  // aid < 2^23 (the fused layout's bound): the key fits 31 bits
+            gk[c] = (((uint32_t)ev_aid(e) << 8) | ((uint32_t)S.esid[idx] << 2) | (uint32_t)ev_type(e)) + 1u;
+        }
+      }
+      int tb = 6;
+      while ((1 << tb) < 2 * nb_ev && tb < 10) ++tb;
+      const uint32_t TS = 1u << tb;
+      uint32_t* hkey = reinterpret_cast<uint32_t*>(&S.srt[0]);
+      uint32_t* hval = reinterpret_cast<uint32_t*>(&S.key[0]);
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      for (uint32_t i = l; i < TS; i += 64) { hkey[i] = 0u; hval[i] = 0u; }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      // the first probes of all chunks go out back to back (a wave's LDS operations complete in order, so a later
+      // chunk's probe sees an earlier chunk's insert); the few collisions then walk on, lane by lane. The event whose
+      // probe inserted the key is the group's rep: it sets the group's sum to its own count (prefix 0) and replaces the
+      // key by its position (the probing is over); the other members add their counts, the returned sum is their prefix
+      uint32_t hs[NCH], pv[NCH];
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        hs[c] = (gk[c] * 0x9E3779B1u) >> (32 - tb);
+        pv[c] = gk[c] ? atomicCAS(&hkey[hs[c]], 0u, gk[c]) : 1u;
+      }
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+        while (pv[c] != 0u && pv[c] != gk[c] && gk[c]) {
+          hs[c] = (hs[c] + 1u) & (TS - 1u);
+          pv[c] = atomicCAS(&hkey[hs[c]], 0u, gk[c]);
+        }
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+        if (gk[c] && pv[c] == 0u) { hval[hs[c]] = sg[c]; hkey[hs[c]] = (uint32_t)(c * 64 + l); }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+        if (gk[c] && pv[c] != 0u) sg[c] = atomicAdd(&hval[hs[c]], sg[c]);
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      // row keys and links: a rep's key carries the group's total (LK_REP | total), a member's link its rep and prefix
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int idx = c * 64 + l;
+        if (c < nch && idx < nb_ev) {
+          uint32_t key = INV, lk = LK_REP, tot = 0u;
+          if (gk[c] && pv[c] == 0u) {
+            tot = hval[hs[c]];
+            const uint32_t g = gk[c] - 1u;
+            key = ((g & 3u) << A) | (g >> 8);
+            lk = LK_REP | tot;
+          } else if (gk[c]) {
+            const int delta = (int)hkey[hs[c]] - idx;
+            lk = ((uint32_t)(delta + 512) << LK_DSHIFT) | sg[c];
+          }
+          rk[E0 + idx] = rk_with_count(key, tot, cshift);
+          link[E0 + idx] = lk;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
     b += nsess;
   }
 }
@@ -592,7 +693,15 @@ __global__ __launch_bounds__(64) void k_prep_count(const int64_t* __restrict__ o
 struct EvOff {
   const uint64_t* p64;
   const uint32_t* p32;
+  const uint32_t* link;  // grouped row entries (LK_REP): a member's run follows from its rep's offset; null: none
   __device__ __forceinline__ uint64_t at(int64_t e) const { return p32 ? (uint64_t)p32[e] : p64[e]; }
+  // the first word of event e's run (e has pairs)
+  __device__ __forceinline__ uint64_t run(int64_t e) const {
+    if (!link) return at(e);
+    const uint32_t lk = link[e];
+    if (lk & LK_REP) return at(e);
+    return at(e + (int64_t)(lk >> LK_DSHIFT) - 512) + (lk & LK_GMASK);
+  }
 };
 
 __global__ void k_gather_counts(const uint32_t* __restrict__ rk, const uint32_t* __restrict__ pos,
@@ -630,6 +739,7 @@ __global__ void k_rows(const uint32_t* __restrict__ rk, const uint32_t* __restri
 // (RK_CSAT: the key byte above the sorted digits, LSD passes sort whole bytes; written by S1+S2)
 constexpr int RT_T = 256, RT_I = 8, RT_TILE = RT_T * RT_I;
 
+// cnt: per event pair counts, or (grouped rows) the link array, whose rep entries hold LK_REP | the group's total
 __device__ __forceinline__ uint64_t rows_x(const uint32_t* __restrict__ rks, const uint32_t* __restrict__ poss,
                                            const uint32_t* __restrict__ cnt, int64_t k, uint32_t kmask, uint32_t INV,
                                            int shift, uint32_t& key, bool& start) {
@@ -638,7 +748,7 @@ __device__ __forceinline__ uint64_t rows_x(const uint32_t* __restrict__ rks, con
   if (key == INV) { start = false; return 0; }
   start = k == 0 || (rks[k - 1] & kmask) != key;
   uint32_t c = kk >> shift;
-  if (c == RK_CSAT) c = cnt[poss[k]];
+  if (c == RK_CSAT) c = cnt[poss[k]] & ~LK_REP;
   return ((uint64_t)c << 24) | (start ? 1u : 0u);
 }
 
@@ -717,6 +827,33 @@ __global__ void k_poff_scatter(const uint32_t* __restrict__ pos, const uint32_t*
                                uint32_t* __restrict__ poff32) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k < n) poff32[pos[k]] = woff[k];
+}
+// grouped row entries: a member's run starts at its rep's word offset plus its prefix in the group (LK_REP); the
+// reps' offsets are final, so members read them while other members are written
+// LF_PER events per thread (stride blockDim): their link and rep-offset loads are in flight together
+constexpr int LF_PER = 8;
+__global__ __launch_bounds__(256) void k_link_fix(const uint32_t* __restrict__ link, int64_t n,
+                                                  uint32_t* __restrict__ poff32, uint64_t* __restrict__ poff) {
+  const int64_t e0 = (int64_t)blockIdx.x * (256 * LF_PER) + threadIdx.x;
+  uint32_t lk[LF_PER];
+#pragma unroll
+  for (int j = 0; j < LF_PER; ++j) lk[j] = e0 + j * 256 < n ? link[e0 + j * 256] : LK_REP;
+  uint64_t o[LF_PER];
+#pragma unroll
+  for (int j = 0; j < LF_PER; ++j) {
+    o[j] = 0;
+    if (!(lk[j] & LK_REP)) {
+      const int64_t r = e0 + j * 256 + (int64_t)(lk[j] >> LK_DSHIFT) - 512;
+      o[j] = poff32 ? (uint64_t)poff32[r] : poff[r];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < LF_PER; ++j)
+    if (!(lk[j] & LK_REP)) {
+      const int64_t e = e0 + j * 256;
+      if (poff32) poff32[e] = (uint32_t)(o[j] + (lk[j] & LK_GMASK));
+      else poff[e] = o[j] + (lk[j] & LK_GMASK);
+    }
 }
 // XCD-aware form: block b runs on XCD b % 8 (workgroups are dealt round robin) and XCD x writes only the
 // slices (position high-bit digits) d = x (mod 8), one after the other, its blocks splitting each slice: a
@@ -931,7 +1068,7 @@ __device__ __forceinline__ void emit_session(const SessView& S, int64_t e0, cons
   for (int i0 = 0; i0 < S.nv; i0 += 4) {
     const int i = i0 + sg;
     bool active = i < S.nv && cnt[e0 + i] != 0u;
-    uint64_t out = active ? poff.at(e0 + i) : 0;
+    uint64_t out = active ? poff.run(e0 + i) : 0;
     const uint64_t e = active ? S.ev[i] : 0;
     const int t = ev_type(e);
     const int64_t tsi = ev_ts(e);
@@ -1308,7 +1445,7 @@ __global__ __launch_bounds__(64) OH_EMIT_WPE void k_emit(const int64_t* __restri
       const uint64_t v = valid ? S.tev[sp] : EV_INVALID;
       const int t = ev_type(v);
       const uint32_t k = in ? S.esid[idx] : 0u;
-      const uint64_t eout = valid ? poff.at(E0 + idx) : 0;
+      const uint64_t eout = valid && cnt[E0 + idx] ? poff.run(E0 + idx) : 0;
       const uint32_t ecnt = valid ? cnt[E0 + idx] : 0;
       const int64_t tsi = ev_ts(v);
       const uint32_t file = S.sfile[k];

@@ -113,8 +113,11 @@ __device__ __forceinline__ int xcd_tile(int b, int nb, int xcd) {
   return x * q + min(x, r) + (b >> 3);
 }
 
+// SKIP (the compacting first pass of radix_sort_pairs): keys with (key & smask) == sinv are not counted
+template <bool SKIP = false>
 __global__ __launch_bounds__(RS_T) void k_rs_hist(const uint32_t* __restrict__ keys, int64_t n, int shift,
-                                                  uint32_t* __restrict__ hist, int nb, int xcd) {
+                                                  uint32_t* __restrict__ hist, int nb, int xcd, uint32_t smask = 0u,
+                                                  uint32_t sinv = 0u) {
   const int tile = xcd_tile(blockIdx.x, nb, xcd);
   __shared__ uint32_t h[RS_WAVES][256];
   for (int i = threadIdx.x; i < RS_WAVES * 256; i += RS_T) (&h[0][0])[i] = 0;
@@ -124,7 +127,12 @@ __global__ __launch_bounds__(RS_T) void k_rs_hist(const uint32_t* __restrict__ k
 #pragma unroll 4
   for (int r = 0; r < RS_R * RS_SUB; ++r) {
     const int64_t idx = t0 + r * RS_T + threadIdx.x;
-    lds_add_runs(h[w], idx < n ? (keys[idx] >> shift) & 255u : 0u, idx < n);  // runs of one digit: one atomic
+    if constexpr (SKIP) {  // first pass over event-order keys: few runs of one digit, and skipped keys break runs
+      const uint32_t k = idx < n ? keys[idx] : sinv;
+      if ((k & smask) != sinv) atomicAdd(&h[w][(k >> shift) & 255u], 1u);
+    } else {
+      lds_add_runs(h[w], idx < n ? (keys[idx] >> shift) & 255u : 0u, idx < n);  // runs of one digit: one atomic
+    }
   }
   __syncthreads();
   for (int d = threadIdx.x; d < 256; d += RS_T) {
@@ -134,17 +142,21 @@ __global__ __launch_bounds__(RS_T) void k_rs_hist(const uint32_t* __restrict__ k
   }
 }
 
+// SKIP: keys with (key & smask) == sinv are dropped (the output holds the others, densely)
+template <bool SKIP = false>
 __global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict__ kin,
                                                      const uint32_t* __restrict__ vin,
                                                      uint32_t* __restrict__ kout,
                                                      uint32_t* __restrict__ vout, int64_t n, int shift,
-                                                     const uint64_t* __restrict__ gofs, int nb, int iota, int xcd) {
+                                                     const uint64_t* __restrict__ gofs, int nb, int iota, int xcd,
+                                                     uint32_t smask = 0u, uint32_t sinv = 0u) {
   const int tile = xcd_tile(blockIdx.x, nb, xcd);
   __shared__ uint32_t wcnt[RS_WAVES][256];
   __shared__ uint32_t bstart[256];
   __shared__ uint32_t tcnt[256];  // the sub-tile's count per digit
   __shared__ uint32_t run[256];   // keys of each digit written by the block's earlier sub-tiles
   __shared__ uint32_t wsum[RS_WAVES];
+  __shared__ uint32_t tvalid;     // SKIP: the sub-tile's kept keys
   __shared__ uint32_t stage_k[RS_TILE];
   __shared__ uint32_t stage_v[RS_TILE];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
@@ -155,12 +167,15 @@ __global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict_
     for (int i = tid; i < RS_WAVES * 256; i += RS_T) (&wcnt[0][0])[i] = 0;
     __syncthreads();
     uint32_t key[RS_R], val[RS_R], rnk[RS_R];
+    uint32_t vmask = 0;  // SKIP: kept keys of this thread (bit r)
     // wave w owns the contiguous quarter [t0 + w*1024, t0 + (w+1)*1024): stable order
 #pragma unroll
     for (int r = 0; r < RS_R; ++r) {
       const int64_t idx = t0 + w * (RS_R * 64) + r * 64 + l;
-      const bool valid = idx < n;
+      bool valid = idx < n;
       key[r] = valid ? kin[idx] : 0u;
+      if constexpr (SKIP) valid = valid && (key[r] & smask) != sinv;
+      vmask |= valid ? (1u << r) : 0u;
       val[r] = valid ? (iota ? (uint32_t)idx : vin[idx]) : 0u;
       const uint32_t d = (key[r] >> shift) & 255u;
       uint64_t m = __ballot(valid);
@@ -191,12 +206,12 @@ __global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict_
       uint32_t pre = 0;
       for (int k = 0; k < w; ++k) pre += wsum[k];
       bstart[d] = pre + incl - tot;
+      if (d == 255) tvalid = pre + incl;
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < RS_R; ++r) {
-      const int64_t idx = t0 + w * (RS_R * 64) + r * 64 + l;
-      if (idx < n) {
+      if ((vmask >> r) & 1u) {
         const uint32_t d = (key[r] >> shift) & 255u;
         const uint32_t p = bstart[d] + wcnt[w][d] + rnk[r];
         stage_k[p] = key[r];
@@ -204,7 +219,7 @@ __global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict_
       }
     }
     __syncthreads();
-    const int64_t tn = n - t0 < RS_TILE ? n - t0 : RS_TILE;
+    const int64_t tn = SKIP ? (int64_t)tvalid : (n - t0 < RS_TILE ? n - t0 : RS_TILE);
     for (int p = tid; p < tn; p += RS_T) {
       const uint32_t k = stage_k[p];
       const uint32_t d = (k >> shift) & 255u;
@@ -246,19 +261,41 @@ int radix_pass(Ctx* ctx, const uint32_t* kin, const uint32_t* vin, uint32_t* kou
 }
 
 int radix_sort_pairs(Ctx* ctx, uint32_t*& keys, uint32_t*& vals, uint32_t* keys_alt, uint32_t* vals_alt,
-                     int64_t n, int bits, hipStream_t s, bool iota_vals) {
-  if (n <= 1 || bits <= 0) {  // nothing to sort; generated values still have to be written
+                     int64_t n, int bits, hipStream_t s, bool iota_vals, const SortSkip* skip) {
+  if (skip) {  // the compacting first pass generates the values and drops the skipped keys
+    if (!iota_vals || bits <= 0) { set_error("radix_sort_pairs: skipping needs iota values and bits > 0"); return OTTOHIP_EINVAL; }
+    *skip->n_out = 0;
+    if (n <= 0) return 0;
+  } else if (n <= 1 || bits <= 0) {  // nothing to sort; generated values still have to be written
     if (iota_vals && n > 1) { set_error("radix_sort_pairs: iota values need bits > 0"); return OTTOHIP_EINVAL; }
     if (iota_vals && n == 1) OH_HIP(hipMemsetAsync(vals, 0, sizeof(uint32_t), s));
     return 0;
   }
   if (n >= ((int64_t)1 << 32)) { set_error("radix_sort_pairs: n=%lld too large", (long long)n); return OTTOHIP_ELIMIT; }
-  const int nb = (int)ceil_div(n, RS_BLOCK);
+  int nb = (int)ceil_div(n, RS_BLOCK);
   uint32_t* hist; uint64_t* gofs;
   OH_TRY(ctx->ws.get("rs_hist", (size_t)nb * 256, &hist));
   OH_TRY(ctx->ws.get("rs_gofs", (size_t)nb * 256, &gofs));
   uint32_t *ka = keys, *va = vals, *kb = keys_alt, *vb = vals_alt;
   for (int shift = 0; shift < bits; shift += 8) {
+    if (skip && shift == 0) {
+      uint64_t* tot;
+      OH_TRY(ctx->ws.get("rs_total", 1, &tot));
+      k_rs_hist<true><<<nb, RS_T, 0, s>>>(ka, n, 0, hist, nb, rs_xcd(), skip->mask, skip->inv);
+      OH_HIP(hipGetLastError());
+      OH_TRY(exclusive_scan_u32(ctx, hist, gofs, (int64_t)nb * 256, tot, s));
+      k_rs_scatter<true><<<nb, RS_T, 0, s>>>(ka, va, kb, vb, n, 0, gofs, nb, 1, rs_xcd(), skip->mask, skip->inv);
+      OH_HIP(hipGetLastError());
+      uint64_t kept = 0;
+      OH_HIP(hipMemcpyAsync(&kept, tot, sizeof kept, hipMemcpyDeviceToHost, s));
+      OH_HIP(hipStreamSynchronize(s));
+      n = (int64_t)kept;
+      *skip->n_out = n;
+      nb = (int)ceil_div(n, RS_BLOCK);
+      std::swap(ka, kb); std::swap(va, vb);
+      if (n <= 1) break;  // nothing left to order: (ka, va) hold the kept key, if any
+      continue;
+    }
     k_rs_hist<<<nb, RS_T, 0, s>>>(ka, n, shift, hist, nb, rs_xcd());
     OH_HIP(hipGetLastError());
     OH_TRY(exclusive_scan_u32(ctx, hist, gofs, (int64_t)nb * 256, nullptr, s));
