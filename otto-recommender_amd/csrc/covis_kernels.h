@@ -57,14 +57,26 @@ struct RulesDev {
 
 __device__ __forceinline__ bool rule_sym(const RulesDev& R, int r) { return (R.sym_mask >> r) & 1u; }
 
-// partners j in [jb, je) of the same type t with aid_j >= aid (packed low word aid << 2 | type)
-__device__ __forceinline__ uint32_t count_sym_partners(const uint64_t* ev, int jb, int je, uint32_t aid, int t) {
+// partners j in [jb, je) of the same type t with aid_j >= aid (packed low word aid << 2 | type). With x = w - lo,
+// the partner qualifies iff x is a non-negative multiple of 4 below 2^(A+2): rotating x right by 2 moves a type
+// mismatch (x & 3 != 0) into bits 30-31 and a negative difference (aid_j < aid) to >= 2^30 - 2^A, so one compare
+// against 2^29 decides when aid < 2^29 (A <= 29); wider aids take the plain test. Four partners per step (two
+// ds_read2 of the keys' low words).
+__device__ __forceinline__ uint32_t count_sym_partners(const uint64_t* ev, int jb, int je, uint32_t aid, int t, int A) {
   const uint32_t lo = (aid << 2) | (uint32_t)t;
   uint32_t m = 0;
-  for (int j = jb; j < je; ++j) {
-    const uint32_t w = (uint32_t)ev[j];
-    m += ((w & 3u) == (uint32_t)t && w >= lo) ? 1u : 0u;
+  if (A > 29) {
+    for (int j = jb; j < je; ++j) {
+      const uint32_t w = (uint32_t)ev[j];
+      m += ((w & 3u) == (uint32_t)t && w >= lo) ? 1u : 0u;
+    }
+    return m;
   }
+  constexpr uint32_t LIM = 1u << 29;
+  auto ok = [&](uint32_t w) { return __builtin_amdgcn_alignbit(w - lo, w - lo, 2) < LIM ? 1u : 0u; };
+  int j = jb;
+  for (; j + 4 <= je; j += 4) m += ok((uint32_t)ev[j]) + ok((uint32_t)ev[j + 1]) + ok((uint32_t)ev[j + 2]) + ok((uint32_t)ev[j + 3]);
+  for (; j < je; ++j) m += ok((uint32_t)ev[j]);
   return m;
 }
 
@@ -299,7 +311,7 @@ __device__ __forceinline__ int equal_run(const uint64_t* evs, int nv, int i) {
   return b - a;
 }
 
-__device__ __forceinline__ uint32_t count_event(const SessView& S, int i, const RulesDev& R) {
+__device__ __forceinline__ uint32_t count_event(const SessView& S, int i, const RulesDev& R, int A) {
   const uint64_t e = S.ev[i];
   const int t = ev_type(e);
   const int64_t tsi = ev_ts(e);
@@ -312,7 +324,7 @@ __device__ __forceinline__ uint32_t count_event(const SessView& S, int i, const 
     if (je <= jb) continue;
     uint32_t m = 0;
     if (rule_sym(R, r)) {
-      m = count_sym_partners(S.ev, jb, je, (uint32_t)ev_aid(e), t);
+      m = count_sym_partners(S.ev, jb, je, (uint32_t)ev_aid(e), t, A);
     } else {
       for (int tt = 0; tt < 3; ++tt)
         if ((R.mask[r] >> tt) & 1u) m += S.pref[tt * S.pstride + je] - S.pref[tt * S.pstride + jb];
@@ -352,7 +364,7 @@ __device__ __forceinline__ void count_session(const SessView& S, int64_t e0, int
   for (int k = lane_id(); k < n; k += 64) {
     uint32_t c = 0, key = INV;
     if (k < S.nv) {
-      c = count_event(S, k, R);
+      c = count_event(S, k, R, A);
       if (c) { const uint64_t e = S.ev[k]; key = ((uint32_t)ev_type(e) << A) | (uint32_t)ev_aid(e); }
     }
     cnt[e0 + k] = c;
@@ -566,17 +578,30 @@ __global__ __launch_bounds__(64) void k_prep_count(const int64_t* __restrict__ o
         const int t = ev_type(e);
         const int64_t tsi = ev_ts(e);
         int run = -1;
+#if defined(OH_PREP_ABL) && OH_PREP_ABL == 3  // timing ablation: no window counts at all, wrong counts
+        cn = 1;
+        if (false)
+#endif
+        int32_t plo = 1, phi = -1;  // the previous rule's window: rules of one type sharing a window share its searches
+        int jb = 0, je = 0;
         for (int q = 0; q < sR.n_of_type[t]; ++q) {
           const int r = sR.rule_of_type[t][q];
           // a window around dt = 0 ends at or after the event and starts at or before it (the session is in ts
           // order): each search takes one side of the event
-          const bool around = sR.lo[r] <= 0 && sR.hi[r] >= 0;
-          const int jb = lds_lower_ts(S.key, lo, around ? idx : hi, tsi + sR.lo[r]);
-          const int je = lds_upper_ts(S.key, around ? idx + 1 : jb, hi, tsi + sR.hi[r]);
+          if (sR.lo[r] != plo || sR.hi[r] != phi) {
+            plo = sR.lo[r]; phi = sR.hi[r];
+            const bool around = plo <= 0 && phi >= 0;
+            jb = lds_lower_ts(S.key, lo, around ? idx : hi, tsi + plo);
+            je = lds_upper_ts(S.key, around ? idx + 1 : jb, hi, tsi + phi);
+          }
           if (je <= jb) continue;
           uint32_t m = 0;
           if (rule_sym(sR, r)) {
-            m = count_sym_partners(S.key, jb, je, (uint32_t)ev_aid(e), t);
+#if defined(OH_PREP_ABL) && OH_PREP_ABL == 1  // timing ablation (tools/prep_probe.py): no window scan, wrong counts
+            m = (uint32_t)(je - jb);
+#else
+            m = count_sym_partners(S.key, jb, je, (uint32_t)ev_aid(e), t, A);
+#endif
           } else {
 #pragma unroll
             for (int tt = 0; tt < 3; ++tt)
