@@ -1718,14 +1718,20 @@ extern "C" int ottohip_table_part_heads(ottohip_ctx* ctx, const ottohip_table* t
       if (pc.stage[p] == 1u) { rk.need[nq] = need[p]; rk.part[nq] = (uint32_t)p; ++nq; }
     uint32_t* found;
     OH_TRY(ws.get("ph_found", 2 * PH_MAXP, &found));
+    // stage 2 on an aid-ordered table scans only the blocks that can hold the cut aid (per-block first / last aids from
+    // the rank pass); OTTOHIP_PH_FULL=1: the full-table stage-2 pass (A/B switch, read per call)
+    const bool ranged = t->aid_ordered && !(getenv("OTTOHIP_PH_FULL") && !strcmp(getenv("OTTOHIP_PH_FULL"), "1"));
+    std::vector<int64_t> rlo(PH_MAXP, -1), rhi(PH_MAXP, -1);
+    std::vector<uint64_t> lbase(PH_MAXP, 0);
     if (nq > 0) {  // (none left when the unordered table's stage 1 above took every tie part)
-    uint32_t *rcnt, *astar;
+    uint32_t *rcnt, *astar, *baid = nullptr;
     uint64_t* rex;
     OH_TRY(ws.get("ph_rank_cnt", (size_t)nq * nb1, &rcnt));
     OH_TRY(ws.get("ph_rank_ex", (size_t)nq * nb1, &rex));
     OH_TRY(ws.get("ph_astar", PH_MAXP, &astar));
+    if (ranged) OH_TRY(ws.get("ph_baid", (size_t)2 * nb1, &baid));
     k_ph_rank_count<<<(unsigned)nb1, FIN_T, 0, s>>>(t->b.rule, t->b.count, t->b.count_ge2, n, n_parts, use_ge2, pc, nb1,
-                                                     rcnt);
+                                                     rcnt, t->b.aid, baid);
     OH_TRY(exclusive_scan_u32(ctx, rcnt, rex, nq * nb1, nullptr, s));
     OH_HIP(hipMemsetAsync(found, 0xFF, 2 * PH_MAXP * 4, s));
     OH_HIP(hipMemsetAsync(astar, 0xFF, PH_MAXP * 4, s));
@@ -1740,6 +1746,28 @@ extern "C" int ottohip_table_part_heads(ottohip_ctx* ctx, const ottohip_table* t
       pc.astar[p] = as[q];
       pc.stage[p] = 2;
     }
+    if (ranged) {
+      // the block range of each cut aid; the tie rows before it (all with aid < a*) from the rank scan
+      uint32_t* rng;
+      OH_TRY(ws.get("ph_range", (size_t)2 * PH_MAXP, &rng));
+      std::vector<uint32_t> rinit(2 * PH_MAXP);
+      for (int q = 0; q < PH_MAXP; ++q) { rinit[2 * q] = 0xFFFFFFFFu; rinit[2 * q + 1] = 0u; }
+      OH_HIP(hipMemcpyAsync(rng, rinit.data(), rinit.size() * 4, hipMemcpyHostToDevice, s));
+      k_ph_aid_range<<<grid_for(nb1 * nq), 256, 0, s>>>(baid, nb1, nq, astar, rng);
+      std::vector<uint32_t> rh(2 * nq);
+      OH_TRY(d2h(rh.data(), rng, rh.size(), s));  // (synchronizes: rinit stays valid until here)
+      for (int q = 0; q < nq; ++q) {
+        const int p = (int)rk.part[q];
+        if (rh[2 * q] == 0xFFFFFFFFu || rh[2 * q + 1] < rh[2 * q]) {
+          set_error("table_part_heads: cut aid range not found (part %d)", p); return OTTOHIP_EHIP;
+        }
+        rlo[p] = rh[2 * q]; rhi[p] = rh[2 * q + 1];
+        uint64_t e2[2];
+        OH_TRY(d2h(&e2[0], rex + (size_t)q * nb1 + rlo[p], 1, s));
+        OH_TRY(d2h(&e2[1], rex + (size_t)q * nb1, 1, s));
+        lbase[p] = e2[0] - e2[1];
+      }
+    }
     }
     // stage 2 (n*): aid_next histogram of the (c*, a*) tie rows; the rank left = need - ties with aid < a*
     uint32_t* th;
@@ -1749,10 +1777,26 @@ extern "C" int ottohip_table_part_heads(ottohip_ctx* ctx, const ottohip_table* t
     OH_TRY(ws.get("ph_lt", PH_MAXP, &lt));
     OH_HIP(hipMemsetAsync(th, 0, (size_t)n_parts * ni * 4, s));
     OH_HIP(hipMemsetAsync(lt, 0, PH_MAXP * 8, s));
-    k_ph_tie_hist2<<<sgrid, 256, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n, n_parts,
-                                         use_ge2, pc, ni, th, reinterpret_cast<unsigned long long*>(lt));
+    bool all_ranged = ranged;
+    for (int p = 0; p < n_parts; ++p)
+      if (pc.stage[p] == 2u && rlo[p] < 0) all_ranged = false;
+    if (all_ranged) {
+      for (int p = 0; p < n_parts; ++p) {
+        if (pc.stage[p] != 2u) continue;
+        const int64_t a0 = rlo[p] * FIN_B, a1 = std::min<int64_t>(n, (rhi[p] + 1) * FIN_B);
+        const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(a1 - a0, 256 * SLOTS_T), sgrid));
+        k_ph_tie_hist2<<<g, 256, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, a1, n_parts,
+                                         use_ge2, pc, ni, th, reinterpret_cast<unsigned long long*>(lt), a0, p);
+      }
+    } else {
+      k_ph_tie_hist2<<<sgrid, 256, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n, n_parts,
+                                           use_ge2, pc, ni, th, reinterpret_cast<unsigned long long*>(lt));
+    }
     uint64_t lth[PH_MAXP];
     OH_TRY(d2h(lth, lt, PH_MAXP, s));
+    if (all_ranged)
+      for (int p = 0; p < n_parts; ++p)
+        if (pc.stage[p] == 2u) lth[p] += lbase[p];
     for (int p = 0; p < n_parts; ++p) {
       if (pc.stage[p] != 2u) continue;
       if (lth[p] >= need[p]) { set_error("table_part_heads: tie rank below the cut aid (part %d)", p); return OTTOHIP_EHIP; }

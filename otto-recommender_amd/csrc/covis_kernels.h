@@ -3187,20 +3187,40 @@ __device__ __forceinline__ uint32_t ph_ties16(const uint8_t* __restrict__ rule, 
   }
   return tie;
 }
-// per FIN_B block: tie rows per stage-1 part -> bcnt[q * nb + block]
+// per FIN_B block: tie rows per stage-1 part -> bcnt[q * nb + block]; with baid, the aids of the block's first and last
+// part rows -> baid[2 block], baid[2 block + 1] (an empty block: 0xFFFFFFFF, 0): the slots are in aid order, so the
+// blocks that can hold a cut aid's rows form one range (k_ph_aid_range)
 __global__ __launch_bounds__(FIN_T) void k_ph_rank_count(const uint8_t* __restrict__ rule, const uint32_t* __restrict__ c,
                                                          const uint32_t* __restrict__ c2, int64_t n, int n_parts,
                                                          int use_ge2, PartCut pc_arg, int64_t nb,
-                                                         uint32_t* __restrict__ bcnt) {
+                                                         uint32_t* __restrict__ bcnt, const int32_t* __restrict__ a = nullptr,
+                                                         uint32_t* __restrict__ baid = nullptr) {
   __shared__ PartCut pc;
   __shared__ int qx[PH_MAXP];
   __shared__ uint32_t bc[PH_MAXP];
-  if (threadIdx.x == 0) { pc = pc_arg; ph_qindex(pc, n_parts, qx); }
+  __shared__ uint32_t sfirst, slast;
+  if (threadIdx.x == 0) { pc = pc_arg; ph_qindex(pc, n_parts, qx); sfirst = 0xFFFFFFFFu; slast = 0u; }
   if (threadIdx.x < PH_MAXP) bc[threadIdx.x] = 0;
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * FIN_B + (int64_t)threadIdx.x * SLOTS_T;
   uint4 R;
   const uint32_t tie = ph_ties16(rule, use_ge2 ? c2 : c, i, n, n_parts, pc, 1u, R);
+  if (baid) {  // the block's first and last slot holding a part row (slot offsets inside the block, + 1 for the last)
+    uint32_t live = 0;
+#pragma unroll
+    for (int s = 0; s < SLOTS_T; ++s) live |= (rule_at(R, s) < (uint32_t)n_parts ? 1u : 0u) << s;
+    // threads hold consecutive slots: the wave's first / last thread with a part row holds its first / last one (one
+    // LDS atomic per wave; one per thread serialised 256 atomics on two words per block)
+    const uint32_t o = (uint32_t)threadIdx.x * SLOTS_T;
+    const uint32_t fs = live ? o + (uint32_t)(__ffs((int)live) - 1) : 0xFFFFFFFFu;
+    const uint32_t ls = live ? o + (uint32_t)(32 - __clz((int)live)) : 0u;
+    const uint64_t m = __ballot(live != 0u);
+    if (m) {
+      const int lf = __ffsll((long long)m) - 1, ll = 63 - __clzll((long long)m);
+      const uint32_t wf = (uint32_t)__shfl((int)fs, lf), wl = (uint32_t)__shfl((int)ls, ll);
+      if (lane_id() == 0) { atomicMin(&sfirst, wf); atomicMax(&slast, wl); }
+    }
+  }
   uint32_t cp = 0xFFu, cc = 0;
 #pragma unroll
   for (int s = 0; s < SLOTS_T; ++s) {  // runs of one part: one LDS atomic each
@@ -3216,6 +3236,30 @@ __global__ __launch_bounds__(FIN_T) void k_ph_rank_count(const uint8_t* __restri
   __syncthreads();
   if (threadIdx.x < PH_MAXP && qx[threadIdx.x] >= 0)
     bcnt[(int64_t)qx[threadIdx.x] * nb + blockIdx.x] = bc[qx[threadIdx.x]];
+  if (baid && threadIdx.x == 0) {
+    const int64_t b0 = (int64_t)blockIdx.x * FIN_B;
+    const bool any = sfirst != 0xFFFFFFFFu;
+    baid[2 * blockIdx.x] = any ? (uint32_t)a[b0 + sfirst] : 0xFFFFFFFFu;
+    baid[2 * blockIdx.x + 1] = any ? (uint32_t)a[b0 + slast - 1] : 0u;
+  }
+}
+// per stage-2 part q (its cut aid astar[q]): the first block whose last aid is >= a* and the last block whose first
+// aid is <= a* (empty blocks skipped) -> range[2q] (atomicMin), range[2q + 1] (atomicMax); every slot of aid a* lies in
+// between, and no slot before the range holds an aid >= a*
+__global__ void k_ph_aid_range(const uint32_t* __restrict__ baid, int64_t nb, int nq, const uint32_t* __restrict__ astar,
+                               uint32_t* __restrict__ range) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nb * nq) return;
+  const int q = (int)(t / nb);
+  const int64_t j = t - (int64_t)q * nb;
+  const uint32_t f = baid[2 * j], l = baid[2 * j + 1], as = astar[q];
+  if (f == 0xFFFFFFFFu || as == 0xFFFFFFFFu) return;
+  // only the blocks at an edge take an atomic (its neighbour on the outside ends below / starts above a*, or is empty);
+  // every block past the cut taking one serialised millions of atomics on one word
+  const uint32_t lprev = j > 0 ? baid[2 * j - 1] : 0u;               // empty: 0
+  const uint32_t fnext = j + 1 < nb ? baid[2 * j + 2] : 0xFFFFFFFFu;  // empty: 0xFFFFFFFF
+  if (l >= as && lprev < as) atomicMin(&range[2 * q], (uint32_t)j);
+  if (f <= as && fnext > as) atomicMax(&range[2 * q + 1], (uint32_t)j);
 }
 // per stage-1 part q: the block j whose tie range holds rank need[q] (ex = one exclusive scan over all q's
 // blocks), found[2q] = j, found[2q + 1] = the rank inside block j
@@ -3301,19 +3345,27 @@ __global__ __launch_bounds__(256) void k_ph_tie_aid_hist(const uint8_t* __restri
 }
 // stage 2: aid_next histogram of the (c*, a*) tie rows of the stage-2 parts, and per part the tie rows with
 // aid < a* (lt); 16 slots per thread, grid-stride
+// slot range [s0, n) (s0 a multiple of SLOTS_T); only_part >= 0: that part's rows only (the others' stage stays 2
+// for their own launches)
 __global__ __launch_bounds__(256) void k_ph_tie_hist2(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
                                                       const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
                                                       const uint32_t* __restrict__ c2, int64_t n, int n_parts,
                                                       int use_ge2, PartCut pc_arg, int64_t n_items,
-                                                      uint32_t* __restrict__ h, unsigned long long* __restrict__ lt) {
+                                                      uint32_t* __restrict__ h, unsigned long long* __restrict__ lt,
+                                                      int64_t s0 = 0, int only_part = -1) {
   // the cut tables in LDS: indexing the kernel-argument copy by a lane's part went through scratch memory
   __shared__ PartCut pc;
   __shared__ uint32_t lts[PH_MAXP];
-  if (threadIdx.x == 0) pc = pc_arg;
+  if (threadIdx.x == 0) {
+    pc = pc_arg;
+    if (only_part >= 0)
+      for (int p = 0; p < PH_MAXP; ++p)
+        if (p != only_part && pc.stage[p] == 2u) pc.stage[p] = 4u;  // not this launch's part
+  }
   if (threadIdx.x < PH_MAXP) lts[threadIdx.x] = 0;
   __syncthreads();
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * SLOTS_T;
-  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * SLOTS_T; i < n; i += stride) {
+  for (int64_t i = s0 + ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * SLOTS_T; i < n; i += stride) {
     uint4 R;
     const uint32_t tie = ph_ties16(rule, use_ge2 ? c2 : c, i, n, n_parts, pc, 2u, R);
     if (!tie) continue;
