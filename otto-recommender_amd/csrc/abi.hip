@@ -1708,6 +1708,11 @@ extern "C" int ottohip_table_part_heads(ottohip_ctx* ctx, const ottohip_table* t
       pc.stage[p] = 2;
     }
   }
+  // the rank pass' per-block counts (aid-ordered tables with tie cuts): k_ph_count then reads only the blocks of the
+  // cut aids' ranges
+  uint32_t *rk_cnt = nullptr, *rk_sure = nullptr, *rk_rng = nullptr;
+  int rk_nq = 0;
+  int64_t rk_lo = -1, rk_hi = -1;
   if (n_tie) {
     // stage 1 (a*): rank search over the parts' tie rows in slot order (= aid order)
     const int64_t nb1 = ceil_div(n, FIN_B);
@@ -1724,14 +1729,18 @@ extern "C" int ottohip_table_part_heads(ottohip_ctx* ctx, const ottohip_table* t
     std::vector<int64_t> rlo(PH_MAXP, -1), rhi(PH_MAXP, -1);
     std::vector<uint64_t> lbase(PH_MAXP, 0);
     if (nq > 0) {  // (none left when the unordered table's stage 1 above took every tie part)
-    uint32_t *rcnt, *astar, *baid = nullptr;
+    uint32_t *rcnt, *astar, *baid = nullptr, *sure = nullptr;
     uint64_t* rex;
     OH_TRY(ws.get("ph_rank_cnt", (size_t)nq * nb1, &rcnt));
     OH_TRY(ws.get("ph_rank_ex", (size_t)nq * nb1, &rex));
     OH_TRY(ws.get("ph_astar", PH_MAXP, &astar));
-    if (ranged) OH_TRY(ws.get("ph_baid", (size_t)2 * nb1, &baid));
+    if (ranged) {
+      OH_TRY(ws.get("ph_baid", (size_t)2 * nb1, &baid));
+      OH_TRY(ws.get("ph_sure", (size_t)nb1, &sure));
+    }
     k_ph_rank_count<<<(unsigned)nb1, FIN_T, 0, s>>>(t->b.rule, t->b.count, t->b.count_ge2, n, n_parts, use_ge2, pc, nb1,
-                                                     rcnt, t->b.aid, baid);
+                                                     rcnt, t->b.aid, baid, thr, sure);
+    if (ranged) { rk_cnt = rcnt; rk_sure = sure; rk_nq = nq; }
     OH_TRY(exclusive_scan_u32(ctx, rcnt, rex, nq * nb1, nullptr, s));
     OH_HIP(hipMemsetAsync(found, 0xFF, 2 * PH_MAXP * 4, s));
     OH_HIP(hipMemsetAsync(astar, 0xFF, PH_MAXP * 4, s));
@@ -1754,6 +1763,7 @@ extern "C" int ottohip_table_part_heads(ottohip_ctx* ctx, const ottohip_table* t
       for (int q = 0; q < PH_MAXP; ++q) { rinit[2 * q] = 0xFFFFFFFFu; rinit[2 * q + 1] = 0u; }
       OH_HIP(hipMemcpyAsync(rng, rinit.data(), rinit.size() * 4, hipMemcpyHostToDevice, s));
       k_ph_aid_range<<<grid_for(nb1 * nq), 256, 0, s>>>(baid, nb1, nq, astar, rng);
+      rk_rng = rng;
       std::vector<uint32_t> rh(2 * nq);
       OH_TRY(d2h(rh.data(), rng, rh.size(), s));  // (synchronizes: rinit stays valid until here)
       for (int q = 0; q < nq; ++q) {
@@ -1762,6 +1772,8 @@ extern "C" int ottohip_table_part_heads(ottohip_ctx* ctx, const ottohip_table* t
           set_error("table_part_heads: cut aid range not found (part %d)", p); return OTTOHIP_EHIP;
         }
         rlo[p] = rh[2 * q]; rhi[p] = rh[2 * q + 1];
+        rk_lo = rk_lo < 0 ? rlo[p] : std::min<int64_t>(rk_lo, rlo[p]);
+        rk_hi = std::max<int64_t>(rk_hi, rhi[p]);
         uint64_t e2[2];
         OH_TRY(d2h(&e2[0], rex + (size_t)q * nb1 + rlo[p], 1, s));
         OH_TRY(d2h(&e2[1], rex + (size_t)q * nb1, 1, s));
@@ -1818,8 +1830,17 @@ extern "C" int ottohip_table_part_heads(ottohip_ctx* ctx, const ottohip_table* t
   OH_TRY(ws.get("blk_cnt", (size_t)nb, &bcnt));
   OH_TRY(ws.get("blk_off", (size_t)nb, &boff));
   OH_TRY(ws.get("fin_tot", 1, &tot));
-  k_ph_count<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n, n_parts,
-                                            use_ge2, thr, pc, bcnt);
+  if (rk_sure && rk_rng && rk_lo >= 0 && rk_nq > 0) {
+    // the rank pass' counts outside the cut aids' ranges, the exact count inside them
+    uint32_t* inr;
+    OH_TRY(ws.get("ph_inrange", (size_t)nb, &inr));
+    k_ph_combine<<<grid_for(nb), 256, 0, s>>>(rk_sure, rk_cnt, nb, rk_nq, rk_rng, bcnt, inr);
+    k_ph_count<<<(unsigned)(rk_hi - rk_lo + 1), FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count,
+                                                               t->b.count_ge2, n, n_parts, use_ge2, thr, pc, bcnt, rk_lo, inr);
+  } else {
+    k_ph_count<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n, n_parts,
+                                              use_ge2, thr, pc, bcnt);
+  }
   OH_TRY(exclusive_scan_u32(ctx, bcnt, boff, nb, tot, s));
   uint64_t m = 0;
   OH_TRY(d2h(&m, tot, 1, s));

@@ -3194,17 +3194,34 @@ __global__ __launch_bounds__(FIN_T) void k_ph_rank_count(const uint8_t* __restri
                                                          const uint32_t* __restrict__ c2, int64_t n, int n_parts,
                                                          int use_ge2, PartCut pc_arg, int64_t nb,
                                                          uint32_t* __restrict__ bcnt, const int32_t* __restrict__ a = nullptr,
-                                                         uint32_t* __restrict__ baid = nullptr) {
+                                                         uint32_t* __restrict__ baid = nullptr, uint32_t thr = 1u,
+                                                         uint32_t* __restrict__ sure = nullptr) {
   __shared__ PartCut pc;
   __shared__ int qx[PH_MAXP];
   __shared__ uint32_t bc[PH_MAXP];
-  __shared__ uint32_t sfirst, slast;
-  if (threadIdx.x == 0) { pc = pc_arg; ph_qindex(pc, n_parts, qx); sfirst = 0xFFFFFFFFu; slast = 0u; }
+  __shared__ uint32_t sfirst, slast, ssure;
+  if (threadIdx.x == 0) { pc = pc_arg; ph_qindex(pc, n_parts, qx); sfirst = 0xFFFFFFFFu; slast = 0u; ssure = 0u; }
   if (threadIdx.x < PH_MAXP) bc[threadIdx.x] = 0;
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * FIN_B + (int64_t)threadIdx.x * SLOTS_T;
   uint4 R;
   const uint32_t tie = ph_ties16(rule, use_ge2 ? c2 : c, i, n, n_parts, pc, 1u, R);
+  if (sure) {  // rows kept whatever the tie cut: v > c*, or v == c* of a part without a tie cut (k_ph_count's test)
+    uint4 V[4];
+    uint32_t live = 0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) live |= (u4_at(R, g) != 0xFFFFFFFFu ? 15u : 0u) << (4 * g);
+    ld_groups(use_ge2 ? c2 : c, i, n, live, V);
+    uint32_t k = 0;
+#pragma unroll
+    for (int s = 0; s < SLOTS_T; ++s) {
+      const uint32_t p = rule_at(R, s), v = u4_at(V[s >> 2], s & 3);
+      if (p >= (uint32_t)n_parts || v < thr) continue;
+      k += (v > pc.cstar[p] || (v == pc.cstar[p] && pc.stage[p] != 1u)) ? 1u : 0u;
+    }
+    k = wave_sum(k);
+    if (lane_id() == 0 && k) atomicAdd(&ssure, k);
+  }
   if (baid) {  // the block's first and last slot holding a part row (slot offsets inside the block, + 1 for the last)
     uint32_t live = 0;
 #pragma unroll
@@ -3236,6 +3253,7 @@ __global__ __launch_bounds__(FIN_T) void k_ph_rank_count(const uint8_t* __restri
   __syncthreads();
   if (threadIdx.x < PH_MAXP && qx[threadIdx.x] >= 0)
     bcnt[(int64_t)qx[threadIdx.x] * nb + blockIdx.x] = bc[qx[threadIdx.x]];
+  if (sure && threadIdx.x == 0) sure[blockIdx.x] = ssure;
   if (baid && threadIdx.x == 0) {
     const int64_t b0 = (int64_t)blockIdx.x * FIN_B;
     const bool any = sfirst != 0xFFFFFFFFu;
@@ -3345,6 +3363,22 @@ __global__ __launch_bounds__(256) void k_ph_tie_aid_hist(const uint8_t* __restri
 }
 // stage 2: aid_next histogram of the (c*, a*) tie rows of the stage-2 parts, and per part the tie rows with
 // aid < a* (lt); 16 slots per thread, grid-stride
+// kept rows per block from the rank pass (k_ph_count's result without re-reading the table): the sure rows plus, per
+// stage-2 part q, all of its tie rows in blocks before its cut aid's range and none after it; blocks inside some
+// range [rng[2q], rng[2q + 1]] are left to k_ph_count (flag 1 in inr)
+__global__ void k_ph_combine(const uint32_t* __restrict__ sure, const uint32_t* __restrict__ tcnt, int64_t nb, int nq,
+                             const uint32_t* __restrict__ rng, uint32_t* __restrict__ bcnt, uint32_t* __restrict__ inr) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nb) return;
+  uint32_t k = sure[j], in = 0;
+  for (int q = 0; q < nq; ++q) {
+    const uint32_t lo = rng[2 * q], hi = rng[2 * q + 1];
+    if ((uint64_t)j < lo) k += tcnt[(int64_t)q * nb + j];
+    else if ((uint64_t)j <= hi) in = 1;
+  }
+  bcnt[j] = k;
+  inr[j] = in;
+}
 // slot range [s0, n) (s0 a multiple of SLOTS_T); only_part >= 0: that part's rows only (the others' stage stays 2
 // for their own launches)
 __global__ __launch_bounds__(256) void k_ph_tie_hist2(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
@@ -3450,12 +3484,15 @@ __device__ __forceinline__ uint32_t ph_keep16(const uint8_t* __restrict__ rule, 
 __global__ __launch_bounds__(FIN_T) void k_ph_count(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
                                                     const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
                                                     const uint32_t* __restrict__ c2, int64_t n, int n_parts, int use_ge2,
-                                                    uint32_t thr, PartCut pc_arg, uint32_t* __restrict__ bcnt) {
+                                                    uint32_t thr, PartCut pc_arg, uint32_t* __restrict__ bcnt,
+                                                    int64_t blk0 = 0, const uint32_t* __restrict__ only = nullptr) {
   __shared__ uint32_t wt[FIN_T / 64];
   __shared__ PartCut pc;  // LDS copy (lane-indexed)
+  const int64_t blk = blk0 + blockIdx.x;
+  if (only && !only[blk]) return;  // block-uniform: counted by k_ph_combine
   if (threadIdx.x == 0) pc = pc_arg;
   __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * FIN_B + (int64_t)threadIdx.x * SLOTS_T;
+  const int64_t i = blk * FIN_B + (int64_t)threadIdx.x * SLOTS_T;
   uint32_t k = 0;
   if (i < n) {
     Slots16 S;
@@ -3464,7 +3501,7 @@ __global__ __launch_bounds__(FIN_T) void k_ph_count(const uint8_t* __restrict__ 
   k = wave_sum(k);
   if ((threadIdx.x & 63) == 0) wt[threadIdx.x >> 6] = k;
   __syncthreads();
-  if (threadIdx.x == 0) bcnt[blockIdx.x] = wt[0] + wt[1] + wt[2] + wt[3];
+  if (threadIdx.x == 0) bcnt[blk] = wt[0] + wt[1] + wt[2] + wt[3];
 }
 // kept rows -> records {aid, aid_next, v, 0} (rule 0) at block offsets boff, in slot order
 __global__ __launch_bounds__(FIN_T) void k_ph_compact(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
