@@ -1071,6 +1071,51 @@ static void file_opts_zero(const ottohip_file_opts* o) {
   }
 }
 
+// the first word of each row type's rows in a row-key-ordered row list (keys (type << A) | aid) for types 0..2, and
+// P: out[t] .. out[t + 1] is type t's word (= table slot) range
+__global__ void k_type_slots(const uint32_t* __restrict__ rk, const uint64_t* __restrict__ rb, int64_t Rn, uint64_t P,
+                             int A, uint64_t* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  for (uint32_t t = 0; t < 3; ++t) {
+    int64_t lo = 0, hi = Rn;
+    while (lo < hi) {
+      const int64_t m = (lo + hi) >> 1;
+      if ((rk[m] >> A) < t) lo = m + 1; else hi = m;
+    }
+    out[t] = lo < Rn ? rb[lo] : P;
+  }
+  out[3] = P;
+}
+// a rule's slot range in table t: [*s0, *s1) (every slot when the table has no type ranges)
+static int rule_slot_range(ottohip_table* t, int rule, hipStream_t s, int64_t* s0, int64_t* s1) {
+  *s0 = 0; *s1 = t->n_slots;
+  if (!t->type_slots_dev || rule < 0 || rule >= TABLE_MAX_IDS) return 0;
+  const int ty = t->rule_type[rule];
+  if (ty < 0 || ty > 2) return 0;
+  if (!t->type_slots_known) {
+    uint64_t h[4];
+    OH_TRY(d2h(h, t->type_slots_dev, 4, s));
+    for (int k = 0; k < 4; ++k) t->type_slots[k] = (int64_t)h[k];
+    t->type_slots_known = true;
+  }
+  *s0 = std::min<int64_t>(t->type_slots[ty], t->n_slots);
+  *s1 = std::min<int64_t>(t->type_slots[ty + 1], t->n_slots);
+  if (*s1 < *s0) { *s0 = 0; *s1 = t->n_slots; }
+  return 0;
+}
+// the finalize-scan blocks over a rule's slot range: first slot i0 (block-aligned: slots before the range hold other
+// types' rows), end n, nb blocks of FIN_B slots (OTTOHIP_FIN_ALL=1: every slot; A/B switch, read per call)
+static int rule_scan_blocks(const ottohip_table* t, int rule, hipStream_t s, int64_t* i0, int64_t* n, int64_t* nb) {
+  int64_t s0 = 0, s1 = t->n_slots;
+  if (!(getenv("OTTOHIP_FIN_ALL") && !strcmp(getenv("OTTOHIP_FIN_ALL"), "1")))
+    OH_TRY(rule_slot_range(const_cast<ottohip_table*>(t), rule, s, &s0, &s1));
+  *i0 = s0 / FIN_B * FIN_B;
+  *n = s1;
+  *nb = std::max<int64_t>(1, ceil_div(s1 - *i0, FIN_B));
+  return 0;
+}
+
+
 int ottohip_covis_count_opts(ottohip_ctx* ctx, const ottohip_events* ev, const ottohip_rule* rules, int n_rules,
                              const ottohip_covis_params* params, const ottohip_file_opts* opts, ottohip_table** out,
                              void* stream) {
@@ -1101,6 +1146,12 @@ int ottohip_covis_count_opts(ottohip_ctx* ctx, const ottohip_events* ev, const o
   if ((rc = ctx->ws.get("words0", (size_t)F.P, &w0)) || (rc = ctx->ws.get("words1", (size_t)F.P, &w1))) return fail(rc);
   if (keep && (rc = ctx->ws.get("words2", (size_t)F.P, &w2))) return fail(rc);
   if ((rc = covis_emit_words(ctx, F, ev, w0, s))) return fail(rc);
+  // the slot range of every row type (rows are type-major), for the per-rule readers; read back on first use
+  // (queued before the reduce, whose closing statistics read synchronises the stream)
+  if (dev_alloc(reinterpret_cast<void**>(&T->type_slots_dev), 4 * sizeof(uint64_t), "type_slots") == hipSuccess) {
+    k_type_slots<<<1, 64, 0, s>>>(F.row_key, F.row_begin, F.Rn, F.P, F.Lt.A, T->type_slots_dev);
+    for (int r = 0; r < n_rules; ++r) T->rule_type[r] = (int8_t)rules[r].this_type;
+  }
   if ((rc = covis_reduce(ctx, w0, w1, F.P, F.row_begin, F.row_key, F.Rn, F.R, F.Lt, n_rules, T, s, fo_eff, nullptr, w2)))
     return fail(rc);
   if (keep) {  // the table takes the emitted words (w0, untouched by the three-buffer reduce) and the rows
@@ -1474,18 +1525,18 @@ int ottohip_table_copy(const ottohip_table* t, int rule, int32_t* aid, int32_t* 
   if (t->n_rows == 0 || t->stats[rule].n_rows == 0) return 0;
   hipStream_t s = S(stream);
   Ctx* ctx = t->ctx;
-  const int64_t n = t->n_slots;
-  const int64_t nb = ceil_div(n, FIN_B);
+  int64_t i0, n, nb;
+  OH_TRY(rule_scan_blocks(t, rule, s, &i0, &n, &nb));
   uint32_t* bcnt;
   uint64_t* boff;
   OH_TRY(ctx->ws.get("blk_cnt", (size_t)nb, &bcnt));
   OH_TRY(ctx->ws.get("blk_off", (size_t)nb, &boff));
   k_blk_count<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n, rule, 0, 0u,
-                                             t->sym(rule), bcnt);
+                                             t->sym(rule), bcnt, i0);
   OH_TRY(exclusive_scan_u32(ctx, bcnt, boff, nb, nullptr, s));
   k_blk_compact<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n,
                                                rule, 0, 0u, t->sym(rule), boff, reinterpret_cast<uint32_t*>(aid),
-                                               reinterpret_cast<uint32_t*>(aid_next), count, count_ge2);
+                                               reinterpret_cast<uint32_t*>(aid_next), count, count_ge2, i0);
   OH_HIP(hipGetLastError());
   return 0;
 }
@@ -1558,8 +1609,8 @@ int ottohip_table_keys_at(ottohip_ctx* ctx, const ottohip_table* t, int rule, in
   if (n_idx == 0) return 0;
   hipStream_t s = S(stream);
   Workspace& ws = ctx->ws;
-  const int64_t n = t->n_slots;
-  const int64_t nb = ceil_div(std::max<int64_t>(n, 1), FIN_B);
+  int64_t i0, n, nb;
+  OH_TRY(rule_scan_blocks(t, rule, s, &i0, &n, &nb));
   uint32_t* bcnt;
   uint64_t *boff, *tot;
   OH_TRY(ws.get("blk_cnt", (size_t)nb, &bcnt));
@@ -1569,7 +1620,7 @@ int ottohip_table_keys_at(ottohip_ctx* ctx, const ottohip_table* t, int rule, in
   if (t->n_rows > 0 && n > 0) {
     // rows of the rule (use_ge2: per-file count >= 2, i.e. count_ge2 >= 1)
     k_blk_count<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n, rule,
-                                               use_ge2 ? 1 : 0, use_ge2 ? 1u : 0u, t->sym(rule), bcnt);
+                                               use_ge2 ? 1 : 0, use_ge2 ? 1u : 0u, t->sym(rule), bcnt, i0);
     OH_TRY(exclusive_scan_u32(ctx, bcnt, boff, nb, tot, s));
     OH_TRY(d2h(&m, tot, 1, s));
   }
@@ -1591,7 +1642,7 @@ int ottohip_table_keys_at(ottohip_ctx* ctx, const ottohip_table* t, int rule, in
   OH_TRY(ws.get("ka_keys", (size_t)n_idx, &dkeys));
   k_blk_compact<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n,
                                                rule, use_ge2 ? 1 : 0, use_ge2 ? 1u : 0u, t->sym(rule), boff, sa, sb,
-                                               nullptr, nullptr);
+                                               nullptr, nullptr, i0);
   OH_HIP(hipMemcpyAsync(didx, idx, (size_t)n_idx * sizeof(int64_t), hipMemcpyHostToDevice, s));
   if (!t->sym(rule)) {  // rows already in aid order (one count): a select per index, no sort
     int* uns;
@@ -1633,6 +1684,7 @@ void ottohip_table_free(ottohip_table* t) {
     t->b.release();
   }
   kept_free(t->kept);
+  dev_free(t->type_slots_dev);
   if (t->produced) (void)hipEventDestroy(t->produced);
   delete t;
 }
@@ -1875,15 +1927,15 @@ extern "C" int ottohip_table_finalize(ottohip_ctx* ctx, const ottohip_table* t, 
   if (t->n_rows == 0) return 0;
   const uint32_t thr = (uint32_t)std::max<int32_t>(mp->min_count, 1);
   Workspace& ws = ctx->ws;
-  const int64_t n = t->n_slots;
-  const int64_t nb = ceil_div(n, FIN_B);
+  int64_t i0, n, nb;  // only the rule's row type's slots
+  OH_TRY(rule_scan_blocks(t, rule, s, &i0, &n, &nb));
   uint32_t* bcnt;
   uint64_t *boff, *tot;
   OH_TRY(ws.get("blk_cnt", (size_t)nb, &bcnt));
   OH_TRY(ws.get("blk_off", (size_t)nb, &boff));
   OH_TRY(ws.get("fin_tot", 1, &tot));
   k_blk_count<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n, rule,
-                                             use_ge2 ? 1 : 0, thr, t->sym(rule), bcnt);
+                                             use_ge2 ? 1 : 0, thr, t->sym(rule), bcnt, i0);
   OH_TRY(exclusive_scan_u32(ctx, bcnt, boff, nb, tot, s));
   uint64_t m = 0;
   OH_TRY(d2h(&m, tot, 1, s));
@@ -1897,7 +1949,7 @@ extern "C" int ottohip_table_finalize(ottohip_ctx* ctx, const ottohip_table* t, 
   OH_TRY(ws.get("fin_k1", (size_t)m, &k1));
   OH_TRY(ws.get("fin_v1", (size_t)m, &v1));
   k_blk_compact<<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n,
-                                               rule, use_ge2 ? 1 : 0, thr, t->sym(rule), boff, sa, sb, sc, nullptr);
+                                               rule, use_ge2 ? 1 : 0, thr, t->sym(rule), boff, sa, sb, sc, nullptr, i0);
   // LSD: aid_next asc, then aid asc, then count desc (stable) -> (count desc, aid, aid_next);
   // aids are < n_items, so their passes cover bits_for(n_items) bits (3 x 8 at 1.86 M items)
   const int abits = std::max(1, bits_for((uint64_t)t->n_items));

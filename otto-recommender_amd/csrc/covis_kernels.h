@@ -2981,9 +2981,9 @@ __device__ __forceinline__ void blk_keep16(const uint8_t* __restrict__ rule, con
 __global__ __launch_bounds__(FIN_T) void k_blk_count(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
                                                      const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
                                                      const uint32_t* __restrict__ c2, int64_t n, int r, int use_ge2,
-                                                     uint32_t thr, int sym, uint32_t* __restrict__ bcnt) {
+                                                     uint32_t thr, int sym, uint32_t* __restrict__ bcnt, int64_t i0 = 0) {
   __shared__ uint32_t wt[FIN_T / 64];
-  const int64_t i = (int64_t)blockIdx.x * FIN_B + (int64_t)threadIdx.x * SLOTS_T;
+  const int64_t i = i0 + (int64_t)blockIdx.x * FIN_B + (int64_t)threadIdx.x * SLOTS_T;
   uint32_t k = 0;
   if (i < n) {
     uint32_t keep, mir;
@@ -3002,10 +3002,10 @@ __global__ __launch_bounds__(FIN_T) void k_blk_compact(const uint8_t* __restrict
                                                        const uint32_t* __restrict__ c2, int64_t n, int r, int use_ge2,
                                                        uint32_t thr, int sym, const uint64_t* __restrict__ boff,
                                                        uint32_t* __restrict__ o0, uint32_t* __restrict__ o1,
-                                                       uint32_t* __restrict__ o2, uint32_t* __restrict__ o3) {
+                                                       uint32_t* __restrict__ o2, uint32_t* __restrict__ o3, int64_t i0 = 0) {
   __shared__ uint32_t wt[FIN_T / 64];
   const int w = threadIdx.x >> 6;
-  const int64_t i = (int64_t)blockIdx.x * FIN_B + (int64_t)threadIdx.x * SLOTS_T;
+  const int64_t i = i0 + (int64_t)blockIdx.x * FIN_B + (int64_t)threadIdx.x * SLOTS_T;
   uint32_t keep = 0, mir = 0;
   Slots16 S;
   if (i < n) blk_keep16(rule, a, b, c, c2, i, n, r, use_ge2, thr, sym, true, o3 != nullptr, keep, mir, S);

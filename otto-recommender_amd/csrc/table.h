@@ -57,6 +57,12 @@ struct ottohip_table {
   ottohip_ctx* ctx = nullptr;
   KeptEmission* kept = nullptr;  // ottohip_file_opts.keep_words: the count's words, for ottohip_table_count_parts
   bool aid_ordered = true;       // a rule's (part's) slots are in aid order (false: explicit mirror rows)
+  // rows are type-major in a count's table: the first slot of each row type (types 0..2) and the end, written on the
+  // device by the count (type_slots_dev, read back on first use); a rule's rows lie in its type's slot range
+  uint64_t* type_slots_dev = nullptr;
+  int64_t type_slots[4] = {0, 0, 0, 0};
+  bool type_slots_known = false;
+  int8_t rule_type[TABLE_MAX_IDS] = {};  // -1: unknown (scan every slot)
   int part_stats_pending = 0;    // part-mode tables: the per-part rows / pairs are counted when first read
   hipEvent_t produced = nullptr; // part-mode tables: recorded on the producer's stream after the reduce; the
                                  // deferred statistics wait on it (the producer may be a non-blocking stream)
