@@ -467,6 +467,170 @@ __global__ __launch_bounds__(GM_T) void k_grp_merge_block(const uint4* __restric
   gm_stats_flush(rows, pairs, n_rules, part, stats);
 }
 
+// ---- big groups whose keys overflow the workgroup hash (ovf[g] > 0): a segmented one-pass partition of each
+// group by a hash digit of aid_next into buckets of about GB_AVG records (the digit's bits chosen per group), then
+// one workgroup hash per bucket. Replaces the sort path (a 3-pass LSD sort of every big-group record by aid_next,
+// a random gather and a reduce). A bucket's rows land in its own record range of the slots [n, n + n_ovf) (rule
+// 0xFF over the rest). A bucket whose distinct keys overflow the hash sets *bovf: the host then runs the sort path
+// for all big groups instead (the buckets' statistics are kept apart until then).
+constexpr int GB_T = 256, GB_PER = 64, GB_CH = GB_T * GB_PER;  // records per partition chunk
+constexpr int GB_MAXBITS = 13;                                  // <= 8192 buckets per group (LDS histogram)
+__device__ __forceinline__ uint32_t gb_digit(uint32_t k, int bits) { return (k * 0x85EBCA77u) >> (32 - bits); }
+// the big groups, listed (any order), with their partition plan: og[k] = group, L, bits, chunks, matrix entries
+__global__ void k_gb_list(const uint32_t* __restrict__ ovf, int64_t G, uint32_t avg, uint32_t* __restrict__ og,
+                          uint32_t* __restrict__ gbits, uint32_t* __restrict__ gnch, uint32_t* __restrict__ gent,
+                          uint32_t* __restrict__ gnbk, unsigned long long* __restrict__ nog) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  const uint32_t L = ovf[g];
+  if (!L) return;
+  int bits = 1;
+  while (bits < GB_MAXBITS && ((uint64_t)avg << bits) < L) ++bits;
+  const uint32_t nch = (L + GB_CH - 1) / GB_CH;
+  const uint32_t k = (uint32_t)atomicAdd(nog, 1ull);
+  og[k] = (uint32_t)g;
+  gbits[k] = (uint32_t)bits;
+  gnch[k] = nch;
+  gent[k] = nch << bits;
+  gnbk[k] = 1u << bits;
+}
+// k of chunk / bucket index c: the last k with base[k] <= c (base: exclusive scan over the listed groups)
+__device__ __forceinline__ uint32_t gb_owner(const uint64_t* __restrict__ base, uint32_t nk, uint64_t c) {
+  uint32_t lo = 0, hi = nk;
+  while (lo < hi) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (base[m] <= c) lo = m + 1; else hi = m;
+  }
+  return lo - 1;
+}
+// one block per chunk of GB_CH records of one big group: the chunk's bucket histogram into the group's matrix
+// (bucket-major: entry b * nch + chunk), so one exclusive scan of all matrices gives every (bucket, chunk) its
+// destination in the partitioned order
+template <bool SCATTER>
+__global__ __launch_bounds__(GB_T) void k_gb_part(const uint4* __restrict__ rec, const uint32_t* __restrict__ gs,
+                                                  const uint32_t* __restrict__ og, const uint32_t* __restrict__ gbits,
+                                                  const uint32_t* __restrict__ gnch, const uint64_t* __restrict__ gchb,
+                                                  const uint64_t* __restrict__ gmtb, uint32_t nog,
+                                                  uint32_t* __restrict__ mat, const uint64_t* __restrict__ moff,
+                                                  uint4* __restrict__ out) {
+  __shared__ uint32_t h[1 << GB_MAXBITS];
+  __shared__ uint32_t sk;
+  if (threadIdx.x == 0) sk = gb_owner(gchb, nog, blockIdx.x);
+  __syncthreads();
+  const uint32_t k = sk, g = og[k], bits = gbits[k], nch = gnch[k], nbk = 1u << bits;
+  const uint32_t ci = blockIdx.x - (uint32_t)gchb[k];
+  const uint32_t s0 = gs[g], L = gs[g + 1] - s0;
+  const uint32_t j0 = ci * GB_CH, j1 = min(L, j0 + GB_CH);
+  const uint64_t mb = gmtb[k];
+  for (uint32_t b = threadIdx.x; b < nbk; b += GB_T) h[b] = SCATTER ? (uint32_t)moff[mb + (uint64_t)b * nch + ci] : 0u;
+  __syncthreads();
+  for (uint32_t j = j0 + threadIdx.x; j < j1; j += GB_T) {
+    const uint4 r = rec[s0 + j];
+    const uint32_t d = gb_digit(r.y, (int)bits);
+    if (SCATTER) {
+      // destination offsets below 2^32: n_ovf < n < 2^32 (checked by the caller)
+      out[atomicAdd(&h[d], 1u)] = r;
+    } else {
+      atomicAdd(&h[d], 1u);
+    }
+  }
+  if (!SCATTER) {
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nbk; b += GB_T) mat[mb + (uint64_t)b * nch + ci] = h[b];
+  }
+}
+// one workgroup per bucket (grid-stride): the bucket's records [moff(b, chunk 0), moff(b + 1, chunk 0)) of the
+// partitioned records merged in an LDS hash, rows written to slots n + that range
+__global__ __launch_bounds__(GM_T) void k_gb_merge(const uint4* __restrict__ prt, const uint32_t* __restrict__ og,
+                                                   const uint32_t* __restrict__ gs, const uint4* __restrict__ rec,
+                                                   const uint32_t* __restrict__ gnch, const uint64_t* __restrict__ gmtb,
+                                                   const uint64_t* __restrict__ gbkb, uint32_t nog, uint64_t nbk_tot,
+                                                   const uint64_t* __restrict__ moff, uint64_t n_ovf, int64_t n,
+                                                   int n_rules, GmOut O, unsigned long long* __restrict__ stats,
+                                                   int* __restrict__ err, int* __restrict__ bovf) {
+  __shared__ uint32_t K[GM_BLOCK_CAP], C[GM_BLOCK_CAP], G2[GM_BLOCK_CAP];
+  __shared__ unsigned long long part[MAX_RULES * 2];
+  __shared__ uint32_t wt[GM_T / 64];
+  __shared__ unsigned long long wps[GM_T / 64];
+  __shared__ uint32_t nocc;
+  const int w = threadIdx.x >> 6;
+  const uint32_t l = lane_id();
+  for (uint32_t e = threadIdx.x; e < GM_BLOCK_CAP; e += GM_T) { K[e] = GM_EMPTY; C[e] = 0; G2[e] = 0; }
+  if (threadIdx.x < MAX_RULES * 2) part[threadIdx.x] = 0;
+  __syncthreads();
+  uint64_t rows[MAX_RULES] = {}, pairs[MAX_RULES] = {};
+  bool wrap = false;
+  for (uint64_t t = blockIdx.x; t < nbk_tot; t += gridDim.x) {  // block-uniform
+    const uint32_t k = gb_owner(gbkb, nog, t);
+    const uint32_t b = (uint32_t)(t - gbkb[k]), nch = gnch[k];
+    const uint64_t r0 = moff[gmtb[k] + (uint64_t)b * nch];
+    const uint64_t r1 = t + 1 < nbk_tot ? moff[gmtb[k] + (uint64_t)(b + 1) * nch] : n_ovf;  // next bucket's start
+    const uint32_t L = (uint32_t)(r1 - r0);
+    if (L == 0) continue;
+    uint32_t cap = 64;
+    while (cap < 2 * L && cap < GM_BLOCK_CAP) cap <<= 1;
+    const uint32_t cm = cap - 1;
+    if (threadIdx.x == 0) nocc = 0;
+    __syncthreads();
+    bool full = false;
+    for (uint32_t j0 = 0; j0 < L; j0 += GM_T) {  // block-uniform; <= GM_T new keys per batch after the check
+      if (nocc > cap / 4 * 3) { full = true; break; }
+      const uint32_t j = j0 + threadIdx.x;
+      const uint32_t nw = wave_sum(j < L && gm_insert(K, C, G2, cm, prt[r0 + j], wrap) ? 1u : 0u);
+      if (l == 0 && nw) atomicAdd(&nocc, nw);
+      __syncthreads();
+    }
+    if (full) {  // the sort path takes every big group (the host sees *bovf)
+      if (threadIdx.x == 0) atomicOr(bovf, 1);
+      for (uint32_t e = threadIdx.x; e < cap; e += GM_T) { K[e] = GM_EMPTY; C[e] = 0; G2[e] = 0; }
+      __syncthreads();
+      continue;
+    }
+    const uint32_t x0 = rec[gs[og[k]]].x;  // the group's (rule, aid)
+    const uint64_t o0 = (uint64_t)n + r0;
+    uint32_t u = 0;
+    uint64_t ps = 0;
+    for (uint32_t e0 = 0; e0 < cap; e0 += GM_T) {
+      const uint32_t e = e0 + threadIdx.x;
+      const uint32_t kk = e < cap ? K[e] : GM_EMPTY;
+      const bool has = kk != GM_EMPTY;
+      const uint32_t incl = wave_incl_scan(has ? 1u : 0u);
+      if (l == 63) wt[w] = incl;
+      __syncthreads();
+      uint32_t pre = 0, tot = 0;
+#pragma unroll
+      for (int x = 0; x < GM_T / 64; ++x) { pre += x < w ? wt[x] : 0u; tot += wt[x]; }
+      if (has) {
+        const uint64_t o = o0 + u + pre + incl - 1;
+        const uint32_t c = C[e];
+        O.rule[o] = (uint8_t)(x0 >> 29);
+        O.aid[o] = (int32_t)(x0 & REC_AID_MASK);
+        O.next[o] = (int32_t)kk;
+        O.cnt[o] = c;
+        O.ge2[o] = G2[e];
+        ps += c;
+        K[e] = GM_EMPTY; C[e] = 0; G2[e] = 0;
+      }
+      u += tot;
+      __syncthreads();
+    }
+    for (uint32_t j = u + threadIdx.x; j < L; j += GM_T) O.rule[o0 + j] = 0xFF;
+    ps = wave_sum64(ps);
+    if (l == 0) wps[w] = ps;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int r = (int)(x0 >> 29);
+      const uint64_t pt = wps[0] + wps[1] + wps[2] + wps[3];
+#pragma unroll
+      for (int q = 0; q < MAX_RULES; ++q)
+        if (q == r) { rows[q] += u; pairs[q] += pt; }
+    }
+    __syncthreads();
+  }
+  if (__ballot(wrap) && l == 0) atomicOr(err, 2);
+  gm_stats_flush(rows, pairs, n_rules, part, stats);
+}
+
 }  // namespace ottohip
 
 using namespace ottohip;
@@ -578,6 +742,7 @@ int ottohip_table_from_records(ottohip_ctx* ctx, const void* records, int64_t n,
   const char* genv = getenv("OTTOHIP_MERGE_GROUPS");
   const bool grouped = !hflags[1] && !(genv && atoi(genv) == 0);
   uint64_t U = 0, n_big = 0, U_big = 0;
+  std::vector<unsigned long long> bst_add;  // the bucket merge's statistics (added once it succeeded)
   uint32_t *gs = nullptr, *big = nullptr, *mid = nullptr;
   unsigned long long* n_mid = nullptr;
   uint4* srt = nullptr;
@@ -638,7 +803,59 @@ int ottohip_table_from_records(ottohip_ctx* ctx, const void* records, int64_t n,
     k_grp_merge_block<<<(unsigned)ctx->n_cu * 3, GM_T, 0, s>>>(rec, gs, mid, n_mid, n_rules, O, ovf, opt, stats, err);
     uint64_t n_ovf = 0;
     if ((rc = exclusive_scan_u32(ctx, ovf, bbo, (int64_t)G, tot, s)) || (rc = d2h(&n_ovf, tot, 1, s))) return fail(rc);
-    if (n_ovf) {
+    // the big groups' bucket merge (OTTOHIP_MERGE_BUCKETS=0, read per call: the sort path; OTTOHIP_MERGE_BUCKET_AVG:
+    // records per bucket, default 1024)
+    const char* benv = getenv("OTTOHIP_MERGE_BUCKETS");
+    const bool buckets = !(benv && atoi(benv) == 0);
+    bool bucketed = false;
+    if (n_ovf && buckets) {
+      ctx->end(ph, s);
+      ph = ctx->begin("merge_buckets", s, 48.0 * n_ovf);
+      const char* aenv = getenv("OTTOHIP_MERGE_BUCKET_AVG");
+      const uint32_t avg = (uint32_t)std::max(64, aenv ? atoi(aenv) : 1024);
+      uint32_t *og, *gbits, *gnch, *gent, *gnbk, *mat;
+      uint64_t *gchb, *gmtb, *gbkb, *moff, *t3;
+      unsigned long long *nog_d, *gst;
+      int* bovf;
+      if ((rc = ws.get("gb_og", (size_t)G, &og)) || (rc = ws.get("gb_bits", (size_t)G, &gbits)) ||
+          (rc = ws.get("gb_nch", (size_t)G, &gnch)) || (rc = ws.get("gb_ent", (size_t)G, &gent)) ||
+          (rc = ws.get("gb_nbk", (size_t)G, &gnbk)) || (rc = ws.get("gb_chb", (size_t)G + 1, &gchb)) ||
+          (rc = ws.get("gb_mtb", (size_t)G + 1, &gmtb)) || (rc = ws.get("gb_bkb", (size_t)G + 1, &gbkb)) ||
+          (rc = ws.get("gb_t3", 3, &t3)) || (rc = ws.get("gb_nog", 1, &nog_d)) ||
+          (rc = ws.get("gb_stats", MAX_RULES * 4, &gst)) || (rc = ws.get("gb_ovf", 1, &bovf)))
+        return fail(rc);
+      if (hipMemsetAsync(nog_d, 0, 8, s) || hipMemsetAsync(gst, 0, MAX_RULES * 4 * 8, s) || hipMemsetAsync(bovf, 0, 4, s))
+        return fail(OTTOHIP_EHIP);
+      k_gb_list<<<grid_for((int64_t)G), 256, 0, s>>>(ovf, (int64_t)G, avg, og, gbits, gnch, gent, gnbk, nog_d);
+      unsigned long long nog = 0;
+      if ((rc = d2h(&nog, nog_d, 1, s))) return fail(rc);
+      if ((rc = exclusive_scan_u32(ctx, gnch, gchb, (int64_t)nog, t3, s)) ||
+          (rc = exclusive_scan_u32(ctx, gent, gmtb, (int64_t)nog, t3 + 1, s)) ||
+          (rc = exclusive_scan_u32(ctx, gnbk, gbkb, (int64_t)nog, t3 + 2, s)))
+        return fail(rc);
+      uint64_t tt[3];
+      if ((rc = d2h(tt, t3, 3, s))) return fail(rc);
+      const uint64_t nchunks = tt[0], nent = tt[1], nbk_tot = tt[2];
+      if ((rc = ws.get("gb_mat", (size_t)nent, &mat)) || (rc = ws.get("gb_moff", (size_t)nent + 1, &moff))) return fail(rc);
+      k_gb_part<false><<<(unsigned)nchunks, GB_T, 0, s>>>(rec, gs, og, gbits, gnch, gchb, gmtb, (uint32_t)nog, mat,
+                                                         nullptr, nullptr);
+      if ((rc = exclusive_scan_u32(ctx, mat, moff, (int64_t)nent, moff + nent, s))) return fail(rc);
+      k_gb_part<true><<<(unsigned)nchunks, GB_T, 0, s>>>(rec, gs, og, gbits, gnch, gchb, gmtb, (uint32_t)nog, nullptr,
+                                                        moff, srt);
+      const GmOut O{T->b.rule, T->b.aid, T->b.aid_next, T->b.count, T->b.count_ge2};
+      k_gb_merge<<<(unsigned)std::min<uint64_t>(nbk_tot, (uint64_t)ctx->n_cu * 3), GM_T, 0, s>>>(
+          srt, og, gs, rec, gnch, gmtb, gbkb, (uint32_t)nog, nbk_tot, moff, n_ovf, n, n_rules, O, gst, err, bovf);
+      int hb = 0;
+      if ((rc = d2h(&hb, bovf, 1, s))) return fail(rc);
+      if (!hb) {
+        unsigned long long bs[MAX_RULES * 4];
+        if ((rc = d2h(bs, gst, MAX_RULES * 4, s))) return fail(rc);
+        bst_add = std::vector<unsigned long long>(bs, bs + MAX_RULES * 4);
+        U_big = n_ovf;  // slots: each bucket's record range
+        bucketed = true;
+      }
+    }
+    if (n_ovf && !bucketed) {
       ctx->end(ph, s);
       ph = ctx->begin("merge_sort", s, 16.0 * n_ovf);
       k_grp_big_keys<<<grid_for((int64_t)n_ovf), 256, 0, s>>>(rec, gs, (int64_t)G, bbo, n_ovf, k0, v0);
@@ -661,6 +878,7 @@ int ottohip_table_from_records(ottohip_ctx* ctx, const void* records, int64_t n,
   int herr = 0;
   if ((rc = d2h(st, stats, MAX_RULES * 4, s)) || (rc = d2h(&herr, err, 1, s))) return fail(rc);
   if (herr) { set_error("table_from_records: merged count overflows u32"); return fail(OTTOHIP_ELIMIT); }
+  for (size_t q = 0; q < bst_add.size(); ++q) st[q] += bst_add[q];
   uint64_t rows = 0;
   for (int r = 0; r < n_rules; ++r) {
     T->stats[r].n_rows = (int64_t)st[r * 4 + 0];

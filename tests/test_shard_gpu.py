@@ -251,19 +251,25 @@ def test_reduce_received_rejects_inconsistent_pieces(gpu):
         gd.reduce_received(words, pieces, NAMES, 1)
 
 
-@pytest.mark.parametrize("grouped,opt", [("1", "1"), ("1", "0"), ("0", "1")])
-def test_from_records_ordered_groups(gpu, monkeypatch, grouped, opt):
+@pytest.mark.parametrize("grouped,opt,buckets,avg", [("1", "1", "1", "1024"), ("1", "0", "1", "1024"),
+                                                     ("1", "1", "1", "200"), ("1", "1", "0", "1024"),
+                                                     ("1", "1", "1", "100000"), ("0", "1", "1", "1024")])
+def test_from_records_ordered_groups(gpu, monkeypatch, grouped, opt, buckets, avg):
     """Records in (rule, aid) order (as the A6 part heads leave them) merge per (rule, aid) group: groups of
     one wave's size, of one workgroup's size and above it -- few distinct keys (the workgroup hash) or many
-    (the sort path into the slots after the groups' ranges) -- all equal a numpy groupby-sum;
-    OTTOHIP_MERGE_OPT=0 sends every big group to the sort path, OTTOHIP_MERGE_GROUPS=0 all records."""
+    (the bucket merge, or the sort path, into the slots after the groups' ranges) -- all equal a numpy
+    groupby-sum; OTTOHIP_MERGE_OPT=0 sends every big group to the bucket merge, OTTOHIP_MERGE_BUCKETS=0 to the
+    sort path, OTTOHIP_MERGE_GROUPS=0 all records to the sort path; OTTOHIP_MERGE_BUCKET_AVG=100000 (one bucket
+    per group: the hash overflows) exercises the bucket merge's fall back to the sort path."""
     import torch
     from otto_recommender_amd import dist as gd
     monkeypatch.setenv("OTTOHIP_MERGE_GROUPS", grouped)
     monkeypatch.setenv("OTTOHIP_MERGE_OPT", opt)
+    monkeypatch.setenv("OTTOHIP_MERGE_BUCKETS", buckets)
+    monkeypatch.setenv("OTTOHIP_MERGE_BUCKET_AVG", avg)
     rng = np.random.default_rng(7)
     sizes = np.concatenate([rng.integers(1, 40, 3000), rng.integers(200, 2100, 60), [2049, 2048, 257, 256],
-                            rng.integers(2100, 30000, 10)])
+                            rng.integers(2100, 30000, 10), [200_000]])
     rng.shuffle(sizes)
     n_items = 50_000
     rule = np.sort(rng.integers(0, len(NAMES), len(sizes)))
