@@ -185,6 +185,13 @@ int ottohip_table_part_heads(ottohip_ctx* ctx, const ottohip_table* t, int n_par
  * table these are the boundary keys of a row slice (ottohip_file_opts). OTTOHIP_ERANGE: idx >= rows. */
 int ottohip_table_keys_at(ottohip_ctx* ctx, const ottohip_table* t, int rule, int use_ge2, const int64_t* idx,
                           int n_idx, uint64_t* keys, void* stream);
+/* ottohip_table_keys_at for rules (parts) 0 .. n_parts - 1 of a part-mode table in one pass over its slots (the
+ * boundary keys of every boundary file from one ottohip_covis_count_parts table with one part per file,
+ * model/count_co_events.py:136-139 / :94): idx (HOST) holds n_idx[0] indices of part 0, then n_idx[1] of part 1,
+ * ...; keys (HOST out) likewise. Tables whose parts are symmetric or not in aid order, or n_parts > 16, take
+ * ottohip_table_keys_at per part. OTTOHIP_ERANGE: an index >= its part's rows. */
+int ottohip_table_keys_at_parts(ottohip_ctx* ctx, const ottohip_table* t, int n_parts, int use_ge2,
+                                const int64_t* idx, const int32_t* n_idx, uint64_t* keys, void* stream);
 int ottohip_table_stats(const ottohip_table* t, int rule, ottohip_rule_stats* st);
 /* copy one rule's rows (unordered) into caller device buffers of n_rows entries;
  * any output pointer may be NULL */

@@ -81,6 +81,7 @@ SIGNATURES = {
     "ottohip_table_part_heads": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_int, _I32, _I64, _VP, _I64,
                                                 ctypes.POINTER(_I64), _VP]),
     "ottohip_table_keys_at": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_int, _VP, ctypes.c_int, _VP, _VP]),
+    "ottohip_table_keys_at_parts": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_int, _VP, _VP, _VP, _VP]),
     "ottohip_table_stats": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.POINTER(RuleStats)]),
     "ottohip_table_copy": (ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, _VP, _VP, _VP]),
     "ottohip_table_free": (None, [_VP]),

@@ -454,6 +454,19 @@ def table_keys_at(table: CovisTable, name, use_ge2: bool, idx, stream=None) -> n
     return keys[:len(idx)]
 
 
+def table_keys_at_parts(table: CovisTable, use_ge2: bool, idx_per_part, stream=None) -> list:
+    """ottohip_table_keys_at_parts: for parts 0 .. len(idx_per_part) - 1 of a part-mode table, the keys (aid << 32 |
+    aid_next) of rows idx_per_part[p] of part p's rows in (aid, aid_next) order, all parts in one pass."""
+    n_idx = np.ascontiguousarray([len(r) for r in idx_per_part], np.int32)
+    idx = np.ascontiguousarray(np.concatenate([np.asarray(r, np.int64).reshape(-1) for r in idx_per_part] +
+                                              [np.zeros(0, np.int64)]), np.int64)
+    keys = np.zeros(max(len(idx), 1), np.uint64)
+    _lib.check(_lib.load().ottohip_table_keys_at_parts(table.ctx.h, table.h, len(idx_per_part), 1 if use_ge2 else 0,
+                                                       idx.ctypes.data, n_idx.ctypes.data, keys.ctypes.data,
+                                                       _lib.stream_handle(stream)))
+    return np.split(keys[:len(idx)], np.cumsum(n_idx)[:-1])
+
+
 def boundary_keys(events: DeviceEvents, name: str, plan, file_rows, use_ge2: bool, n_items: int, ctx=None) -> dict:
     """{(file, row): key} for every part boundary of `plan` that falls inside a file: the key of that row of
     the file's own (aid, aid_next)-ordered (use_ge2: count >= 2) table, as count_co_events.py:94 writes it.
@@ -479,13 +492,10 @@ def boundary_keys(events: DeviceEvents, name: str, plan, file_rows, use_ge2: boo
                 raise
             t = None  # a layout limit of the one-count form: each file alone below
         if t is not None:
-            lib = _lib.load()
-            for p, f in enumerate(files):
-                rows = np.ascontiguousarray(sorted(need[f]), np.int64)
-                keys = np.zeros(len(rows), np.uint64)
-                _lib.check(lib.ottohip_table_keys_at(t.ctx.h, t.h, p, 1 if use_ge2 else 0, rows.ctypes.data,
-                                                     len(rows), keys.ctypes.data, _lib.stream_handle(None)))
-                for r, k in zip(rows.tolist(), keys.tolist()):
+            # every boundary file's keys from one pass over the table (ottohip_table_keys_at_parts)
+            rows_of = [sorted(need[f]) for f in files]
+            for f, rows, keys in zip(files, rows_of, table_keys_at_parts(t, use_ge2, rows_of)):
+                for r, k in zip(rows, keys.tolist()):
                     out[(f, r)] = int(k)
             t.free()
             return out

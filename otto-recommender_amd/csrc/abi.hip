@@ -1673,6 +1673,94 @@ int ottohip_table_keys_at(ottohip_ctx* ctx, const ottohip_table* t, int rule, in
   return 0;
 }
 
+int ottohip_table_keys_at_parts(ottohip_ctx* ctx, const ottohip_table* t, int n_parts, int use_ge2,
+                                const int64_t* idx, const int32_t* n_idx, uint64_t* keys, void* stream) {
+  if (!ctx || !t || !n_idx || n_parts < 1 || n_parts > t->n_rules) {
+    set_error("table_keys_at_parts: bad args"); return OTTOHIP_EINVAL;
+  }
+  int64_t total = 0;
+  for (int p = 0; p < n_parts; ++p) {
+    if (n_idx[p] < 0) { set_error("table_keys_at_parts: n_idx[%d] < 0", p); return OTTOHIP_EINVAL; }
+    total += n_idx[p];
+  }
+  if (total == 0) return 0;
+  if (!idx || !keys) { set_error("table_keys_at_parts: NULL idx / keys"); return OTTOHIP_EINVAL; }
+  bool one_pass = n_parts <= KP_MAXP && t->aid_ordered;
+  for (int p = 0; p < n_parts; ++p) one_pass = one_pass && !t->sym(p);
+  auto per_part = [&]() -> int {  // each part on its own (ottohip_table_keys_at)
+    int64_t o = 0;
+    for (int p = 0; p < n_parts; ++p) {
+      if (n_idx[p]) OH_TRY(ottohip_table_keys_at(ctx, t, p, use_ge2, idx + o, n_idx[p], keys + o, stream));
+      o += n_idx[p];
+    }
+    return 0;
+  };
+  if (!one_pass) return per_part();
+  hipStream_t s = S(stream);
+  Workspace& ws = ctx->ws;
+  const int64_t n = t->n_slots;
+  const int64_t nb = ceil_div(std::max<int64_t>(n, 1), FIN_B);
+  uint32_t* bcnt;
+  uint64_t *boff, *seg;
+  OH_TRY(ws.get("kp_cnt", (size_t)(n_parts * nb), &bcnt));
+  OH_TRY(ws.get("kp_off", (size_t)(n_parts * nb + 1), &boff));
+  OH_TRY(ws.get("kp_seg", (size_t)n_parts + 1, &seg));
+  std::vector<uint64_t> sg(n_parts + 1, 0);
+  if (t->n_rows > 0 && n > 0) {
+    const uint32_t thr = use_ge2 ? 1u : 0u;
+    k_blk_parts<false><<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n,
+                                                      n_parts, use_ge2 ? 1 : 0, thr, nb, bcnt, nullptr, nullptr, nullptr);
+    OH_TRY(exclusive_scan_u32(ctx, bcnt, boff, n_parts * nb, boff + n_parts * nb, s));
+    k_part_seg<<<1, 64, 0, s>>>(boff, nb, n_parts, seg);
+    OH_TRY(d2h(sg.data(), seg, (size_t)n_parts + 1, s));
+  }
+  {
+    int64_t o = 0;
+    for (int p = 0; p < n_parts; ++p) {
+      const uint64_t m = sg[p + 1] - sg[p];
+      for (int64_t j = o; j < o + n_idx[p]; ++j)
+        if (idx[j] < 0 || (uint64_t)idx[j] >= m) {
+          set_error("table_keys_at_parts: index %lld outside part %d's %llu rows", (long long)idx[j], p,
+                    (unsigned long long)m);
+          return OTTOHIP_ERANGE;
+        }
+      o += n_idx[p];
+    }
+  }
+  const uint64_t mt = sg[n_parts];
+  uint32_t *sa, *sb;
+  int64_t* didx;
+  uint64_t* dkeys;
+  int* uns;
+  OH_TRY(ws.get("fin_sa", (size_t)mt, &sa));
+  OH_TRY(ws.get("fin_sb", (size_t)mt, &sb));
+  OH_TRY(ws.get("ka_idx", (size_t)total, &didx));
+  OH_TRY(ws.get("ka_keys", (size_t)total, &dkeys));
+  OH_TRY(ws.get("ka_uns", 1, &uns));
+  const uint32_t thr = use_ge2 ? 1u : 0u;
+  k_blk_parts<true><<<(unsigned)nb, FIN_T, 0, s>>>(t->b.rule, t->b.aid, t->b.aid_next, t->b.count, t->b.count_ge2, n,
+                                                   n_parts, use_ge2 ? 1 : 0, thr, nb, nullptr, boff, sa, sb);
+  OH_HIP(hipMemcpyAsync(didx, idx, (size_t)total * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  OH_HIP(hipMemsetAsync(uns, 0, sizeof(int), s));
+  for (int p = 0; p < n_parts; ++p) {
+    const int64_t m = (int64_t)(sg[p + 1] - sg[p]);
+    if (m > 1) k_sorted_check<<<grid_for(m), 256, 0, s>>>(sa + sg[p], m, uns);
+  }
+  int hu = 1;
+  OH_TRY(d2h(&hu, uns, 1, s));
+  if (hu) return per_part();  // a part's rows not in aid order: the sort path per part
+  int64_t o = 0;
+  for (int p = 0; p < n_parts; ++p) {
+    if (n_idx[p])
+      k_keys_at_sel<<<(unsigned)n_idx[p], 256, 0, s>>>(sa + sg[p], sb + sg[p], (int64_t)(sg[p + 1] - sg[p]), didx + o,
+                                                      dkeys + o);
+    o += n_idx[p];
+  }
+  OH_HIP(hipGetLastError());
+  OH_TRY(d2h(keys, dkeys, (size_t)total, s));
+  return 0;
+}
+
 void ottohip_table_free(ottohip_table* t) {
   if (!t) return;
   (void)hipSetDevice(t->device);

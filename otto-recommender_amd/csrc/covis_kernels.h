@@ -3037,6 +3037,88 @@ __global__ __launch_bounds__(FIN_T) void k_blk_compact(const uint8_t* __restrict
     }
   }
 }
+// the rows of every part p < np of a part-mode table (rule byte = part, no mirrors) in one pass: !OUT counts each
+// block's rows per part (bcnt[p * nb + block]); OUT writes their (aid, aid_next) to sa / sb at boff[p * nb + block]
+// in slot order (use_ge2: rows with count_ge2 >= thr; else count >= thr)
+constexpr int KP_MAXP = 16;
+template <bool OUT>
+__global__ __launch_bounds__(FIN_T) void k_blk_parts(const uint8_t* __restrict__ rule, const int32_t* __restrict__ a,
+                                                     const int32_t* __restrict__ b, const uint32_t* __restrict__ c,
+                                                     const uint32_t* __restrict__ c2, int64_t n, int np, int use_ge2,
+                                                     uint32_t thr, int64_t nb, uint32_t* __restrict__ bcnt,
+                                                     const uint64_t* __restrict__ boff, uint32_t* __restrict__ sa,
+                                                     uint32_t* __restrict__ sb) {
+  __shared__ uint32_t wt[KP_MAXP][FIN_T / 64];
+  const int w = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * FIN_B + (int64_t)threadIdx.x * SLOTS_T;
+  uint4 R = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+  uint32_t kept = 0;
+  Slots16 S;
+  if (i < n) {
+    R = ld_rule16(rule, i, n);
+    uint32_t live = 0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) live |= (u4_at(R, g) != 0xFFFFFFFFu ? 15u : 0u) << (4 * g);
+    if (live) {
+      if (thr) ld_groups(use_ge2 ? c2 : c, i, n, live, S.V);
+#pragma unroll
+      for (int s = 0; s < SLOTS_T; ++s)
+        kept |= (rule_at(R, s) < (uint32_t)np && (!thr || S.v(s) >= thr) ? 1u : 0u) << s;
+      if (OUT && kept) {
+        ld_groups(reinterpret_cast<const uint32_t*>(a), i, n, kept, S.A);
+        ld_groups(reinterpret_cast<const uint32_t*>(b), i, n, kept, S.B);
+      }
+    }
+  }
+  uint32_t incl[KP_MAXP];
+#pragma unroll
+  for (int p = 0; p < KP_MAXP; ++p) {
+    if (p >= np) break;  // block-uniform
+    uint32_t kc = 0;
+#pragma unroll
+    for (int s = 0; s < SLOTS_T; ++s) kc += ((kept >> s) & 1u) && rule_at(R, s) == (uint32_t)p ? 1u : 0u;
+    incl[p] = wave_incl_scan(kc);
+    if ((threadIdx.x & 63) == 63) wt[p][w] = incl[p];
+  }
+  __syncthreads();
+  if (!OUT) {
+    if ((int)threadIdx.x < np) {
+      uint32_t t = 0;
+#pragma unroll
+      for (int x = 0; x < FIN_T / 64; ++x) t += wt[threadIdx.x][x];
+      bcnt[(int64_t)threadIdx.x * nb + blockIdx.x] = t;
+    }
+    return;
+  }
+  if (!kept) return;
+  uint64_t cur[KP_MAXP];
+#pragma unroll
+  for (int p = 0; p < KP_MAXP; ++p) {
+    if (p >= np) break;
+    uint32_t pre = 0, kc = 0;
+#pragma unroll
+    for (int x = 0; x < FIN_T / 64; ++x) pre += x < w ? wt[p][x] : 0u;
+#pragma unroll
+    for (int s = 0; s < SLOTS_T; ++s) kc += ((kept >> s) & 1u) && rule_at(R, s) == (uint32_t)p ? 1u : 0u;
+    cur[p] = boff[(int64_t)p * nb + blockIdx.x] + pre + incl[p] - kc;
+  }
+#pragma unroll
+  for (int s = 0; s < SLOTS_T; ++s) {
+    if (!((kept >> s) & 1u)) continue;
+    const uint32_t p = rule_at(R, s);
+    uint64_t o = 0;
+#pragma unroll
+    for (int q = 0; q < KP_MAXP; ++q)
+      if ((uint32_t)q == p) o = cur[q]++;
+    sa[o] = S.a(s);
+    sb[o] = S.b(s);
+  }
+}
+// out[p] = boff[p * nb] (p < np), out[np] = the total
+__global__ void k_part_seg(const uint64_t* __restrict__ boff, int64_t nb, int np, uint64_t* __restrict__ out) {
+  const int p = threadIdx.x;
+  if (p <= np) out[p] = boff[(int64_t)p * nb];
+}
 
 // rows and pairs per rule byte (part-mode tables: per part), block histograms in LDS
 __global__ __launch_bounds__(256) void k_rule_hist(const uint8_t* __restrict__ rule, const uint32_t* __restrict__ count,

@@ -487,6 +487,26 @@ def test_file_cuts_per_file_rows_and_key_slices(gpu):
         idx = [0, 5, int(sel.sum()) // 2, int(sel.sum()) - 1]
         np.testing.assert_array_equal(gc.table_keys_at(t1, n, ge2, idx), key[sel][idx])
         t1.free()
+    # every file's keys from one part-mode table (one part per file) in one pass (ottohip_table_keys_at_parts),
+    # as boundary_keys reads them; an index past a part's rows is ERANGE
+    import otto_recommender_amd._lib as L
+    tp = gc.count_co_events_parts(dev, n, [0, 1, 2, 3], [], 4)
+    for ge2 in (False, True):
+        want, idx_pp = [], []
+        for f in range(4):
+            af, bf, cf = per_file[f][n]
+            kf = ((af.astype(np.uint64) << np.uint64(32)) | bf.astype(np.uint64))[cf >= 2 if ge2 else slice(None)]
+            ix = np.unique([0, 3, len(kf) // 2, len(kf) - 1]) if f != 2 else np.zeros(0, np.int64)  # part 2: none
+            idx_pp.append(ix)
+            want.append(kf[ix])
+        got = gc.table_keys_at_parts(tp, ge2, idx_pp)
+        for f in range(4):
+            np.testing.assert_array_equal(got[f], want[f], err_msg=f"file {f} ge2={ge2}")
+            if len(idx_pp[f]):
+                np.testing.assert_array_equal(gc.table_keys_at(tp, f, ge2, idx_pp[f]), want[f])
+    with pytest.raises(L.OttoHipError):
+        gc.table_keys_at_parts(tp, False, [[0], [len(per_file[1][n][0])], [], []])
+    tp.free()
     lo, hi = int(key[len(key) // 3]), int(key[2 * len(key) // 3])
     t = gc.count_co_events_fused(dev, [n], cuts=gc.FileCuts(n, lo=(1, lo), hi=(2, hi), per_file=True))
     keep1, a2, b2, c2 = key >= lo, *per_file[2][n]
