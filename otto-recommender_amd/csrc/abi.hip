@@ -1301,7 +1301,10 @@ int ottohip_covis_count_parts(ottohip_ctx* ctx, const ottohip_events* ev, const 
   OH_HIP(hipSetDevice(ctx->device));
   ctx->reset_timing();
   Front F;
-  OH_TRY(setup_rules(rules, n_rules, params, nf, F.R, F.Lt, /*allow_sym=*/false));
+  // OTTOHIP_A6_SYMPART=1 (read per call; experiment): a symmetric rule stores each unordered pair once and the
+  // leaves write the mirrors as explicit rows with their own parts at slot + P (the table is then not in aid order)
+  const bool sympart = getenv("OTTOHIP_A6_SYMPART") && !strcmp(getenv("OTTOHIP_A6_SYMPART"), "1");
+  OH_TRY(setup_rules(rules, n_rules, params, nf, F.R, F.Lt, /*allow_sym=*/sympart));
   ottohip_table* T = new_table(ctx, n_rules, params->n_items);
   auto fail = [&](int rc) { ottohip_table_free(T); return rc; };
   int rc;
@@ -1327,8 +1330,13 @@ int ottohip_covis_count_parts(ottohip_ctx* ctx, const ottohip_events* ev, const 
   OH_HIP(hipStreamSynchronize(s));  // host vectors
   fo.part_of = d_part;
   fo.cut_of = d_cut;
+  fo.mirror_off = (F.R.sym_mask & 1u) ? F.P : 0ull;
   if ((rc = covis_reduce(ctx, w0, w1, F.P, F.row_begin, F.row_key, F.Rn, F.R, F.Lt, n_rules, T, s, nullptr, &fo)))
     return fail(rc);
+  if (fo.mirror_off) {
+    T->sym_mask = 0;  // explicit rows (the mirrors written by the leaves)
+    T->aid_ordered = false;
+  }
   // per part: rows and pairs (file statistics stay 0: the part-wise finalize is told which column to use)
   T->n_rules = po->n_parts;
   // per part: rows and pairs, counted when first read (ottohip_table_stats / _copy / _finalize): the part heads
