@@ -753,6 +753,53 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   const bool dbg = getenv("OTTOHIP_DEBUG") != nullptr;
   if (dbg) fprintf(stderr, "[ottohip] P=%llu rows=%lld\n", (unsigned long long)P, (long long)Rn);
   uint32_t* wcur0 = w0;  // the word buffer of tasks with buf 0 at this level (w2 from level 1 on, if given)
+  // Split pipelining (OTTOHIP_SPLIT_PIPE=1, read per call; off by default: step 57.0-57.3 vs 57.0-57.1 ms same box,
+  // the early leaves and the second half's scatter contend for the same CUs): a large split scatters and classifies its tasks in
+  // two halves; the next level's leaves of the first half's sub-buckets (hash, then register sorts, on the aux
+  // stream) start while the second half is scattered on the main stream. done[c]: tasks of list c of the level
+  // whose leaves were launched that way; hash_early: its hash leaves run on the aux stream (ev_hash).
+  const char* pipe_env = getenv("OTTOHIP_SPLIT_PIPE");
+  const bool pipe = s2 != nullptr && !lds_leaf && !dbg && getenv("OTTOHIP_HASH_PROF") == nullptr &&
+                    (pipe_env && atoi(pipe_env) == 1);
+  // splits of >= 2048 chunks (32 M words) are pipelined (OTTOHIP_SPLIT_PIPE_MIN: another bound, for tests)
+  const uint64_t PIPE_MIN_CHUNKS = getenv("OTTOHIP_SPLIT_PIPE_MIN") ? (uint64_t)atoll(getenv("OTTOHIP_SPLIT_PIPE_MIN")) : 2048;
+  unsigned long long done[N_LISTS] = {};
+  bool hash_early = false;
+  // leaves of tasks [lo[c], hi[c]) of the sort classes / [lo[N_SORT], hi[N_SORT]) of the hash list, buffer wb0 for
+  // buf 0
+  auto launch_hash_range = [&](uint64_t lo, uint64_t hi, uint32_t* wb0, hipStream_t st) {
+    if (hi <= lo) return;
+    const int64_t nh = (int64_t)(hi - lo);
+    const Task* th = TL.hash + lo;
+    const unsigned hg = (unsigned)std::min<int64_t>(nh, (int64_t)agg_grid);
+    if (FOhist)
+      k_agg_hash<2><<<hg, AGG_T, 0, st>>>(th, nh, wb0, w1, row_key, R, Lt, n_rules, O, TL.split, lcount + N_SORT + 1, fo);
+    else if (FOmir)
+      k_agg_hash<3><<<hg, AGG_T, 0, st>>>(th, nh, wb0, w1, row_key, R, Lt, n_rules, O, TL.split, lcount + N_SORT + 1, fo);
+    else if (FOon)
+      k_agg_hash<1><<<hg, AGG_T, 0, st>>>(th, nh, wb0, w1, row_key, R, Lt, n_rules, O, TL.split, lcount + N_SORT + 1, fo);
+    else
+      k_agg_hash<<<hg, AGG_T, 0, st>>>(th, nh, wb0, w1, row_key, R, Lt, n_rules, O, TL.split, lcount + N_SORT + 1, fo);
+  };
+  auto launch_sorts = [&](const unsigned long long* lo, const unsigned long long* hi, uint32_t* wb0, hipStream_t st) {
+    const unsigned sgrid = (unsigned)ctx->n_cu * 32;
+#define OH_SORT(c, M)                                                                                          \
+    if (hi[c] > lo[c]) {                                                                                       \
+      const int64_t n_ = (int64_t)(hi[c] - lo[c]);                                                             \
+      const Task* t_ = TL.sort[c] + lo[c];                                                                     \
+      const unsigned g_ = (unsigned)std::min<uint64_t>(ceil_div(n_, 4), sgrid);                                \
+      if (FOhist)                                                                                              \
+        k_agg_sort<M, 2><<<g_, 256, (size_t)fo.nf * 8, st>>>(t_, n_, wb0, w1, row_key, R, Lt, n_rules, Osort, fo); \
+      else if (FOmir)                                                                                          \
+        k_agg_sort<M, 3><<<g_, 256, 0, st>>>(t_, n_, wb0, w1, row_key, R, Lt, n_rules, Osort, fo);             \
+      else if (FOon)                                                                                           \
+        k_agg_sort<M, 1><<<g_, 256, 0, st>>>(t_, n_, wb0, w1, row_key, R, Lt, n_rules, Osort, fo);             \
+      else                                                                                                     \
+        k_agg_sort<M><<<g_, 256, 0, st>>>(t_, n_, wb0, w1, row_key, R, Lt, n_rules, Osort, fo);                \
+    }
+    OH_SORT(0, 1) OH_SORT(1, 2) OH_SORT(2, 4) OH_SORT(3, 8) OH_SORT(4, 16)
+#undef OH_SORT
+  };
   for (int level = 0; level < 40; ++level) {
     wcur0 = (level == 0 || !w2) ? w0 : w2;
     unsigned long long nlist[N_LISTS];
@@ -781,7 +828,6 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
       }
       fprintf(stderr, "\n");
     }
-    const unsigned sgrid = (unsigned)ctx->n_cu * 32;
     // the register-sort tasks of this level run on the aux stream, beside this level's hash and
     // split on s (VALU-bound sorts next to the LDS/HBM-bound split); their task lists are only
     // rewritten by the next level's classify, which waits for them (ev_join)
@@ -791,41 +837,10 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     // blocks take CU slots before the sorts' many short ones (step -0.5 ms same box; OTTOHIP_HASH_FIRST=0:
     // sorts first)
     static const bool hash_first = !(getenv("OTTOHIP_HASH_FIRST") && !strcmp(getenv("OTTOHIP_HASH_FIRST"), "0"));
-    const bool hf = hash_first && nlist[N_SORT] != 0;
-    auto launch_hash = [&]() {
-      const unsigned hg = (unsigned)std::min<uint64_t>(nlist[N_SORT], (uint64_t)agg_grid);
-      if (FOhist)
-        k_agg_hash<2><<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], wcur0, w1, row_key, R, Lt, n_rules, O,
-                                           TL.split, lcount + N_SORT + 1, fo);
-      else if (FOmir)
-        k_agg_hash<3><<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], wcur0, w1, row_key, R, Lt, n_rules, O,
-                                           TL.split, lcount + N_SORT + 1, fo);
-      else if (FOon)
-        k_agg_hash<1><<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], wcur0, w1, row_key, R, Lt, n_rules, O,
-                                              TL.split, lcount + N_SORT + 1, fo);
-      else
-        k_agg_hash<<<hg, AGG_T, 0, s>>>(TL.hash, (int64_t)nlist[N_SORT], wcur0, w1, row_key, R, Lt, n_rules, O, TL.split,
-                                        lcount + N_SORT + 1, fo);
-    };
+    const bool hf = hash_first && nlist[N_SORT] > done[N_SORT];
+    auto launch_hash = [&]() { launch_hash_range(done[N_SORT], nlist[N_SORT], wcur0, s); };
     if (hf) launch_hash();
-#define OH_SORT(c, M)                                                                                        \
-    if (nlist[c]) {                                                                                          \
-      const unsigned g_ = (unsigned)std::min<uint64_t>(ceil_div((int64_t)nlist[c], 4), sgrid);              \
-      if (FOhist)                                                                                            \
-        k_agg_sort<M, 2><<<g_, 256, (size_t)fo.nf * 8, ss>>>(TL.sort[c], (int64_t)nlist[c], wcur0, w1, row_key, R,  \
-                                                            Lt, n_rules, Osort, fo);                         \
-      else if (FOmir)                                                                                        \
-        k_agg_sort<M, 3><<<g_, 256, 0, ss>>>(TL.sort[c], (int64_t)nlist[c], wcur0, w1, row_key, R, Lt, n_rules, \
-                                             Osort, fo);                                                     \
-      else if (FOon)                                                                                         \
-        k_agg_sort<M, 1><<<g_, 256, 0, ss>>>(TL.sort[c], (int64_t)nlist[c], wcur0, w1, row_key, R, Lt, n_rules, \
-                                             Osort, fo);                                                     \
-      else                                                                                                   \
-        k_agg_sort<M><<<g_, 256, 0, ss>>>(TL.sort[c], (int64_t)nlist[c], wcur0, w1, row_key, R, Lt, n_rules, Osort, \
-                                          fo);                                                               \
-    }
-    OH_SORT(0, 1) OH_SORT(1, 2) OH_SORT(2, 4) OH_SORT(3, 8) OH_SORT(4, 16)
-#undef OH_SORT
+    launch_sorts(done, nlist, wcur0, ss);
     if (s2) OH_HIP(hipEventRecord(ctx->ev_join[level & 1], s2));
     if (nlist[N_SORT + 2]) {  // LDS leaves (hot segments are appended to the split list)
       const unsigned lg = (unsigned)std::min<uint64_t>(nlist[N_SORT + 2], (uint64_t)ctx->n_cu * 4);
@@ -836,7 +851,7 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
         k_agg_lds<<<lg, LDS_T, 0, s>>>(TL.lds, (int64_t)nlist[N_SORT + 2], wcur0, w1, row_key, R, Lt, O, TL.split,
                                        lcount + N_SORT + 1, TL.cap + split_extra, err, fo);
     }
-    if (nlist[N_SORT]) {  // tasks that overflow the LDS table are appended to the split list
+    if (nlist[N_SORT] > done[N_SORT]) {  // tasks that overflow the LDS table are appended to the split list
       static const bool hprof = getenv("OTTOHIP_HASH_PROF") != nullptr && !hash_first;  // per-task profile (debugging aid)
       if (hprof) {
         if ((rc = ws.get("hash_prof", (size_t)(2 * nlist[N_SORT]), &fo.prof))) return rc;
@@ -861,8 +876,11 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
         fo.prof = nullptr;
       }
     }
+    if (hash_early) OH_HIP(hipStreamWaitEvent(s, ctx->ev_hash, 0));  // the early hash leaves' overflow tasks
     if (nlist[N_SORT] || nlist[N_SORT + 2])
       if ((rc = d2h(nlist, lcount, N_LISTS, s))) return rc;
+    hash_early = false;
+    for (int c = 0; c < N_LISTS; ++c) done[c] = 0;
     const int64_t ns = (int64_t)nlist[N_SORT + 1];
     if (dbg) fprintf(stderr, "[ottohip] level %d: split after hash overflow %lld\n", level, (long long)ns);
     if (ns == 0) {
@@ -878,15 +896,21 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     if ((rc = ws.get("sp_nch", (size_t)ns, &nch)) || (rc = ws.get("sp_ndg", (size_t)ns, &ndg)) ||
         (rc = ws.get("sp_nen", (size_t)ns, &nen)) || (rc = ws.get("sp_chb", (size_t)ns + 1, &chb)) ||
         (rc = ws.get("sp_dgb", (size_t)ns + 1, &dgb)) || (rc = ws.get("sp_mtb", (size_t)ns + 1, &mtb)) ||
-        (rc = ws.get("sp_tot", 3, &tot2)))
+        (rc = ws.get("sp_tot", 6, &tot2)))
       return rc;
     k_split_prepare<<<grid_for(ns), 256, 0, s>>>(cur_split, ns, nch, ndg, nen);
     if ((rc = exclusive_scan_u32(ctx, nch, chb, ns, tot2, s)) || (rc = exclusive_scan_u32(ctx, ndg, dgb, ns, tot2 + 1, s)) ||
         (rc = exclusive_scan_u32(ctx, nen, mtb, ns, tot2 + 2, s)))
       return rc;
-    uint64_t tt[3];
-    if ((rc = d2h(tt, tot2, 3, s))) return rc;
+    if (pipe) k_split_half<<<1, 64, 0, s>>>(chb, dgb, ns, tot2, tot2 + 3);  // (task, chunk, digit) of the halves' border
+    uint64_t tt[6] = {0, 0, 0, 0, 0, 0};
+    if ((rc = d2h(tt, tot2, pipe ? 6 : 3, s))) return rc;
     const int64_t nchunks = (int64_t)tt[0], ndig = (int64_t)tt[1], nent = (int64_t)tt[2];
+    // pipelined when the split is large and the border falls strictly inside it
+    const bool piped = pipe && (uint64_t)nchunks >= PIPE_MIN_CHUNKS && tt[3] > 0 && (int64_t)tt[3] < ns &&
+                       tt[4] > 0 && (int64_t)tt[4] < nchunks && tt[5] > 0 && (int64_t)tt[5] < ndig;
+    const uint32_t cA = piped ? (uint32_t)tt[4] : (uint32_t)nchunks;
+    const int64_t dA = piped ? (int64_t)tt[5] : ndig;
     uint32_t *hmat, *ctask;
     uint64_t* hoff;
     if ((rc = ws.get("sp_hmat", (size_t)nent, &hmat)) || (rc = ws.get("sp_hoff", (size_t)nent + 1, &hoff)) ||
@@ -896,17 +920,43 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
     k_split_hist<<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, wcur0, w1, Lt.F, hmat);
     if ((rc = exclusive_scan_u32(ctx, hmat, hoff, nent, hoff + nent, s))) return rc;
     static const int sub = getenv("OTTOHIP_SPLIT_SUB") ? atoi(getenv("OTTOHIP_SPLIT_SUB")) : 4096;  // A/B switch
-    if (sub == 8192)
-      k_split_scatter<8192><<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, hoff, wcur0, w1, Lt.F, hmat);
-    else
-      k_split_scatter<4096><<<(unsigned)nchunks, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, hoff, wcur0, w1, Lt.F, hmat);
+    auto scatter = [&](uint32_t c0, uint32_t c1) {
+      if (c1 <= c0) return;
+      if (sub == 8192)
+        k_split_scatter<8192><<<c1 - c0, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, hoff, wcur0, w1, Lt.F, hmat, c0);
+      else
+        k_split_scatter<4096><<<c1 - c0, SPLIT_T, 0, s>>>(cur_split, ns, chb, ctask, mtb, hoff, wcur0, w1, Lt.F, hmat, c0);
+    };
+    scatter(0, cA);
     // next lists (a sub-bucket is one task in exactly one list: ndig bounds every list): the other
     // parity's set, last read by the sorts of level - 1
     if (s2 && level >= 1) OH_HIP(hipStreamWaitEvent(s, ctx->ev_join[(level + 1) & 1], 0));
     const uint64_t capn = (uint64_t)ndig;
     if ((rc = get_lists(std::max(cap0, capn), srcA ? "t_splitB" : "t_splitA", (level + 1) & 1))) return rc;
     hipMemsetAsync(lcount, 0, 8 * 8, s);
-    k_split_classify<<<grid_for(ndig), 256, 0, s>>>(cur_split, ns, dgb, mtb, hoff, ndig, TL, err, hmat);
+    k_split_classify<<<grid_for(dA), 256, 0, s>>>(cur_split, ns, dgb, mtb, hoff, dA, TL, err, hmat, 0);
+    if (piped) {
+      if (getenv("OTTOHIP_SPLIT_PIPE_LOG")) fprintf(stderr, "[ottohip] level %d split pipelined at chunk %u of %lld\n", level, cA, (long long)nchunks);
+      // the first half's sub-buckets are classified: its next-level leaves start on the aux stream (hash first,
+      // then the register sorts) while the second half is scattered and classified here
+      OH_HIP(hipEventRecord(ctx->ev_half, s));
+      scatter(cA, (uint32_t)nchunks);
+      if (ndig > dA)
+        k_split_classify<<<grid_for(ndig - dA), 256, 0, s>>>(cur_split, ns, dgb, mtb, hoff, ndig, TL, err, hmat, dA);
+      OH_HIP(hipStreamWaitEvent(ctx->aux2, ctx->ev_half, 0));
+      unsigned long long nA[N_LISTS];
+      if ((rc = d2h(nA, lcount, N_LISTS, ctx->aux2))) return rc;
+      OH_HIP(hipStreamWaitEvent(s2, ctx->ev_half, 0));
+      uint32_t* wb0 = w2 ? w2 : w0;  // the next level's buffer of buf-0 tasks
+      if (nA[N_SORT]) {
+        launch_hash_range(0, nA[N_SORT], wb0, s2);
+        OH_HIP(hipEventRecord(ctx->ev_hash, s2));
+        hash_early = true;
+      }
+      const unsigned long long zero[N_LISTS] = {};
+      launch_sorts(zero, nA, wb0, s2);
+      for (int c = 0; c <= N_SORT; ++c) done[c] = nA[c];
+    }
     srcA = !srcA;
     if (hipGetLastError() != hipSuccess) { set_error("split launch failed"); return OTTOHIP_EHIP; }
   }
@@ -974,6 +1024,9 @@ void ottohip_ctx_destroy(ottohip_ctx* ctx) {
   dev_trim();
   if (ctx->aux) {
     hipStreamDestroy(ctx->aux);
+    if (ctx->aux2) hipStreamDestroy(ctx->aux2);
+    if (ctx->ev_half) hipEventDestroy(ctx->ev_half);
+    if (ctx->ev_hash) hipEventDestroy(ctx->ev_hash);
     hipEventDestroy(ctx->ev_fork);
     hipEventDestroy(ctx->ev_join[0]);
     hipEventDestroy(ctx->ev_join[1]);

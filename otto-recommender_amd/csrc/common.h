@@ -98,9 +98,16 @@ struct Ctx {
   // second stream of the reduce (register-sort tasks overlap the split of the same level)
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};  // join: by reduce level parity
+  // split pipelining: a third stream for the host's read of the first half's task counts; ev_half: the first
+  // half classified, ev_hash: the next level's first-half hash leaves done
+  hipStream_t aux2 = nullptr;
+  hipEvent_t ev_half = nullptr, ev_hash = nullptr;
   int aux_stream() {
     if (aux) return 0;
     if (hipStreamCreateWithFlags(&aux, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&aux2, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&ev_half, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ev_hash, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ev_join[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ev_join[1], hipEventDisableTiming) != hipSuccess) {

@@ -2485,6 +2485,21 @@ __global__ void k_classify_rows(const uint64_t* __restrict__ row_begin, int64_t 
 
 // split: per task k digit bits, chunks of SPLIT_CH words
 constexpr int SPLIT_CH = 16384;
+// the split's halves: the first task t with chunk_base[t] >= nchunks / 2 (a task boundary near the middle) ->
+// out[0] = t, out[1] = chunk_base[t], out[2] = digit_base[t]
+__global__ void k_split_half(const uint64_t* __restrict__ chunk_base, const uint64_t* __restrict__ digit_base, int64_t n,
+                             const uint64_t* __restrict__ nchunks_total, uint64_t* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint64_t half = *nchunks_total / 2;
+  int64_t lo = 0, hi = n;  // first t with chunk_base[t] >= half
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (chunk_base[m] < half) lo = m + 1; else hi = m;
+  }
+  out[0] = (uint64_t)lo;
+  out[1] = lo < n ? chunk_base[lo] : *nchunks_total;
+  out[2] = lo < n ? digit_base[lo] : 0ull;
+}
 constexpr int SPLIT_T = 256;
 
 // Digits of one split: ceil(len / SPLIT_MEAN), 2..SPLIT_DMAX (any count, not only powers of two), so
@@ -2579,16 +2594,18 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
                                                            const uint64_t* __restrict__ mat_base,
                                                            const uint64_t* __restrict__ hoff,
                                                            uint32_t* __restrict__ w0, uint32_t* __restrict__ w1, int F,
-                                                           uint32_t* __restrict__ hmat) {
+                                                           uint32_t* __restrict__ hmat, uint32_t chunk0 = 0) {
+  // chunk0: the first chunk of this launch (a split may run as two launches over chunk ranges)
   constexpr int DPT = SPLIT_DMAX / SPLIT_T;  // digits per thread in the scans
   __shared__ uint32_t h[SPLIT_DMAX], st[SPLIT_DMAX];
   __shared__ uint64_t gb[SPLIT_DMAX];
   __shared__ uint32_t stage[SUB];
   __shared__ uint32_t wsum[SPLIT_T / 64];
-  const int64_t t = chunk_task[blockIdx.x];
+  const uint32_t cid = chunk0 + blockIdx.x;
+  const int64_t t = chunk_task[cid];
   const Task T = tasks[t];
   const uint32_t nd = split_ndig(T), nch = (uint32_t)ceil_div((int64_t)T.len, SPLIT_CH);
-  const uint32_t c = (uint32_t)(blockIdx.x - chunk_base[t]);
+  const uint32_t c = (uint32_t)(cid - chunk_base[t]);
   const uint64_t c0 = (uint64_t)c * SPLIT_CH;
   const uint64_t c1 = c0 + SPLIT_CH < T.len ? c0 + SPLIT_CH : T.len;
   const uint32_t* Win = (T.buf ? w1 : w0) + T.begin;
@@ -2696,8 +2713,10 @@ __global__ __launch_bounds__(SPLIT_T) void k_split_scatter(const Task* __restric
 // one thread per (split task, digit): push the non-empty sub-buckets as next-level tasks
 __global__ void k_split_classify(const Task* __restrict__ tasks, int64_t n, const uint64_t* __restrict__ digit_base,
                                  const uint64_t* __restrict__ mat_base, const uint64_t* __restrict__ hoff,
-                                 int64_t n_digits_total, TaskLists TL, int* err, const uint32_t* __restrict__ hmat) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                 int64_t n_digits_total, TaskLists TL, int* err, const uint32_t* __restrict__ hmat,
+                                 int64_t d0 = 0) {
+  // digits [d0, n_digits_total) (a split may classify its digits in two launches)
+  const int64_t i = d0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   Task T;
   T.begin = 0; T.rem = 0; T.row = 0; T.buf = 0; T.len = 0;
   uint64_t b = 0, c = 0;

@@ -202,8 +202,13 @@ def test_long_sessions(gpu):
     _assert_single_file(ev, n_items=64)
 
 
-def test_heavy_rows_split_and_hash_paths(gpu):
-    # one hot aid paired with many distinct aids (split path) and with itself (heavy buckets)
+@pytest.mark.parametrize("pipe", ["0", "1"])
+def test_heavy_rows_split_and_hash_paths(gpu, monkeypatch, capfd, pipe):
+    # one hot aid paired with many distinct aids (split path) and with itself (heavy buckets); pipe=1: every split
+    # runs in two halves with the next level's first-half leaves started early (OTTOHIP_SPLIT_PIPE, off by default)
+    monkeypatch.setenv("OTTOHIP_SPLIT_PIPE", pipe)
+    monkeypatch.setenv("OTTOHIP_SPLIT_PIPE_MIN", "2")
+    monkeypatch.setenv("OTTOHIP_SPLIT_PIPE_LOG", "1")
     rng = np.random.default_rng(5)
     rows = []
     for s in range(4000):
@@ -214,10 +219,15 @@ def test_heavy_rows_split_and_hash_paths(gpu):
     a = np.array(rows)
     ev = synth.events_from_columns(a[:, 0], a[:, 1], a[:, 2], a[:, 3])
     _assert_single_file(ev, n_items=200_000)
+    assert ("split pipelined" in capfd.readouterr().err) == (pipe == "1")
 
 
-def test_hot_row_overflow_resplit(gpu):
+@pytest.mark.parametrize("pipe", ["0", "1"])
+def test_hot_row_overflow_resplit(gpu, monkeypatch, capfd, pipe):
     # a hot aid next to ~1M distinct partners: split buckets overflow the LDS table and are re-split
+    monkeypatch.setenv("OTTOHIP_SPLIT_PIPE", pipe)
+    monkeypatch.setenv("OTTOHIP_SPLIT_PIPE_MIN", "2")
+    monkeypatch.setenv("OTTOHIP_SPLIT_PIPE_LOG", "1")
     rng = np.random.default_rng(9)
     n_s, n = 3000, 40
     rows = []
@@ -228,6 +238,7 @@ def test_hot_row_overflow_resplit(gpu):
     a = np.concatenate(rows)
     ev = synth.events_from_columns(a[:, 0], a[:, 1], a[:, 2], a[:, 3])
     _assert_single_file(ev, names=["click_to_click"])
+    assert ("split pipelined" in capfd.readouterr().err) == (pipe == "1")
 
 
 def test_dedup_off_matches_pandas_without_unique(gpu):
