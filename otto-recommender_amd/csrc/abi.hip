@@ -660,12 +660,9 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   }
   unsigned long long *stats, *lcount;
   OH_TRY(ws.get("stats", (size_t)STAT_STRIPES * STAT_STRIDE, &stats));
-  OH_TRY(ws.get("lcount", 9, &lcount));
-  // the reduce's error word sits after the list counters, so each level reads both in one copy (the per-level
-  // memset clears the 8 counters only)
-  err = reinterpret_cast<int*>(lcount + 8);
+  OH_TRY(ws.get("lcount", 8, &lcount));
   hipMemsetAsync(stats, 0, (size_t)STAT_STRIPES * STAT_STRIDE * 8, s);
-  hipMemsetAsync(err, 0, 8, s);
+  hipMemsetAsync(err, 0, sizeof(int), s);
   // rows are written at their task's word offsets; each leaf task marks the rest of its range
   // (rule 0xFF), so the slots need no fill (a debug ablation drops the sort kernels' stores)
   if (getenv("OTTOHIP_REDUCE_DBG")) hipMemsetAsync(T->b.rule, 0xFF, n_slots, s);
@@ -805,10 +802,9 @@ static int covis_reduce(ottohip_ctx* ctx, uint32_t* w0, uint32_t* w1, uint64_t P
   };
   for (int level = 0; level < 40; ++level) {
     wcur0 = (level == 0 || !w2) ? w0 : w2;
-    unsigned long long nlist[N_LISTS + 1];
-    static_assert(N_LISTS == 8, "the error word follows 8 list counters");
-    if ((rc = d2h(nlist, lcount, N_LISTS + 1, s))) return rc;
-    herr = (int)(uint32_t)nlist[N_LISTS];
+    unsigned long long nlist[N_LISTS];
+    if ((rc = d2h(nlist, lcount, N_LISTS, s))) return rc;
+    if ((rc = d2h(&herr, err, 1, s))) return rc;
     if (herr) { set_error("task list overflow / row too large (err=%d)", herr); return OTTOHIP_ELIMIT; }
     if (dbg) {
       fprintf(stderr, "[ottohip] level %d: sort %llu/%llu/%llu/%llu/%llu hash %llu split %llu lds %llu\n", level, nlist[0],
