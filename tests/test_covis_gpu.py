@@ -202,13 +202,8 @@ def test_long_sessions(gpu):
     _assert_single_file(ev, n_items=64)
 
 
-@pytest.mark.parametrize("pipe", ["0", "1"])
-def test_heavy_rows_split_and_hash_paths(gpu, monkeypatch, capfd, pipe):
-    # one hot aid paired with many distinct aids (split path) and with itself (heavy buckets); pipe=1: every split
-    # runs in two halves with the next level's first-half leaves started early (OTTOHIP_SPLIT_PIPE, off by default)
-    monkeypatch.setenv("OTTOHIP_SPLIT_PIPE", pipe)
-    monkeypatch.setenv("OTTOHIP_SPLIT_PIPE_MIN", "2")
-    monkeypatch.setenv("OTTOHIP_SPLIT_PIPE_LOG", "1")
+def test_heavy_rows_split_and_hash_paths(gpu):
+    # one hot aid paired with many distinct aids (split path) and with itself (heavy buckets)
     rng = np.random.default_rng(5)
     rows = []
     for s in range(4000):
@@ -219,16 +214,10 @@ def test_heavy_rows_split_and_hash_paths(gpu, monkeypatch, capfd, pipe):
     a = np.array(rows)
     ev = synth.events_from_columns(a[:, 0], a[:, 1], a[:, 2], a[:, 3])
     _assert_single_file(ev, n_items=200_000)
-    if pipe == "0":
-        assert "split pipelined" not in capfd.readouterr().err
 
 
-@pytest.mark.parametrize("pipe", ["0", "1"])
-def test_hot_row_overflow_resplit(gpu, monkeypatch, capfd, pipe):
+def test_hot_row_overflow_resplit(gpu):
     # a hot aid next to ~1M distinct partners: split buckets overflow the LDS table and are re-split
-    monkeypatch.setenv("OTTOHIP_SPLIT_PIPE", pipe)
-    monkeypatch.setenv("OTTOHIP_SPLIT_PIPE_MIN", "2")
-    monkeypatch.setenv("OTTOHIP_SPLIT_PIPE_LOG", "1")
     rng = np.random.default_rng(9)
     n_s, n = 3000, 40
     rows = []
@@ -239,8 +228,15 @@ def test_hot_row_overflow_resplit(gpu, monkeypatch, capfd, pipe):
     a = np.concatenate(rows)
     ev = synth.events_from_columns(a[:, 0], a[:, 1], a[:, 2], a[:, 3])
     _assert_single_file(ev, names=["click_to_click"])
-    if pipe == "0":
-        assert "split pipelined" not in capfd.readouterr().err
+
+
+def test_split_pipelined_paths(gpu, monkeypatch):
+    # OTTOHIP_SPLIT_PIPE=1 (off by default): every split of >= 2 chunks runs in two halves with the next level's
+    # first-half leaves started early; the split-path cases above still equal the oracle
+    monkeypatch.setenv("OTTOHIP_SPLIT_PIPE", "1")
+    monkeypatch.setenv("OTTOHIP_SPLIT_PIPE_MIN", "2")
+    test_heavy_rows_split_and_hash_paths(gpu)
+    test_hot_row_overflow_resplit(gpu)
 
 
 def test_dedup_off_matches_pandas_without_unique(gpu):
